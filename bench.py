@@ -1,0 +1,206 @@
+"""Benchmark of the hot path (BASELINE.json metric: query embeddings/sec + cosine-pairs/sec,
+100k x 768 gallery).
+
+python bench.py --gpus N --steps K --warmup W [--mode full|knn]
+  full (default): one step = Swin-T tower on B synthetic 224x224 images + ClinicalBERT-geometry
+        tower on B synthetic 128-token reports (bf16) -> projection / heads -> exact cosine
+        top-10 of the B query embeddings over the gallery (config 2: B=256, 100k x 768 f32).
+  knn:  one step = exact cosine top-K of B resident queries over the gallery (kNN leg only).
+N>1 (torch.distributed.run): the gallery is row-sharded (N x rows per rank: weak scaling), every
+rank runs its own query batch through the towers and searches its shard for ALL ranks' queries
+(all-gather of query embeddings), then per-shard top-K lists are all-gathered over RCCL and merged.
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--mode", choices=["full", "knn"], default="full")
+    p.add_argument("--batch", type=int, default=256)
+    p.add_argument("--gallery", type=int, default=100_000, help="gallery rows per GPU")
+    p.add_argument("--dim", type=int, default=768)
+    p.add_argument("--k", type=int, default=10)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-sample-queries", type=int, default=0)
+    return p.parse_args()
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def main():
+    a = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = torch.device(f"cuda:{local}")
+
+    import mmr_amd
+    from mmr_amd import synthetic
+    from mmr_amd.retrieval import GalleryIndex, merge_topk
+
+    # gallery shard: rows [rank*n, (rank+1)*n) of a virtual (world*n, d) N(0,1) gallery
+    n, d, K, B = a.gallery, a.dim, a.k, a.batch
+    G = synthetic.gauss_gallery(n, d, synthetic.SEED + 17 * rank)
+    index = GalleryIndex(G, device=local, idx_base=rank * n)
+    index.reserve(B * world)
+
+    model = None
+    if a.mode == "full":
+        from mmr_amd.model import build_bench_model
+        model = build_bench_model(device=dev, joint_dim=d)
+        imgs = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(B, synthetic.SEED + rank))).to(dev)
+        ids_np, mask_np = synthetic.reports(B, 128, synthetic.SEED + 100 + rank)
+        ids, mask = torch.from_numpy(ids_np).to(dev), torch.from_numpy(mask_np).to(dev)
+    else:
+        qbatch = torch.from_numpy(synthetic.gauss_gallery(B, d, synthetic.SEED + 1 + rank)).to(dev)
+
+    stream = torch.cuda.current_stream(dev)
+    ev_pairs = []
+
+    def step(record):
+        if model is not None:
+            q = model.query_embeddings(imgs, ids, mask)            # (B, d) f32
+        else:
+            q = qbatch
+        if world > 1:
+            allq = torch.empty((world * B, d), dtype=torch.float32, device=dev)
+            dist.all_gather_into_tensor(allq, q.contiguous())
+        else:
+            allq = q
+        if record:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        i, s, s64 = index.search(allq, K, want_f64=True)
+        if record:
+            e1.record(stream)
+            ev_pairs.append((e0, e1))
+        if world > 1:
+            gi = torch.empty((world,) + tuple(i.shape), dtype=i.dtype, device=dev)
+            gs = torch.empty((world,) + tuple(s64.shape), dtype=s64.dtype, device=dev)
+            dist.all_gather_into_tensor(gi, i)
+            dist.all_gather_into_tensor(gs, s64)
+            i, s, _ = merge_topk(gs, gi, K)
+        return i, s
+
+    for _ in range(a.warmup):
+        step(False)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        out = step(True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_search = sum(e0.elapsed_time(e1) for e0, e1 in ev_pairs) / max(len(ev_pairs), 1)
+
+    # whole-job throughput: every rank embeds B queries; every query is scored against the whole
+    # world*n gallery (each rank scores all world*B queries against its n rows)
+    q_per_s = world * B * a.steps / elapsed
+    pairs_per_s = (world * B) * (world * n) * a.steps / elapsed
+    # roofline of the kNN search (dominant kernel of the knn mode): per launch on one GPU
+    Qs = world * B
+    flops = 2.0 * Qs * n * d
+    bytes_ = n * d * 4 + n * 4 + Qs * d * 4 + Qs * K * 12
+    t_s = ms_search / 1e3
+    peak_mfma_f32, peak_hbm = 157.3e12, 8.0e12
+    bound = "mfma" if flops / peak_mfma_f32 > bytes_ / peak_hbm else "hbm"
+    if bound == "mfma":
+        roof = {"bound": "mfma", "achieved": flops / t_s / 1e12, "peak": peak_mfma_f32 / 1e12, "unit": "TFLOP/s"}
+    else:
+        roof = {"bound": "hbm", "achieved": bytes_ / t_s / 1e9, "peak": peak_hbm / 1e9, "unit": "GB/s"}
+    roof["frac"] = roof["achieved"] / roof["peak"]
+    roof["traffic"] = None
+    roof["kernel"] = "mmr_index_search (knn_prep_queries + knn_scores f32 MFMA + knn_select)"
+    roof["ms_per_launch"] = ms_search
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(a, G, qbatch if model is None else out_q_for_cpu(model, imgs, ids, mask))
+
+    if rank == 0:
+        line = {
+            "metric": "query embeddings/sec + cosine-pairs/sec @ Recall@10, 100k x 768 gallery",
+            "value": q_per_s if a.mode == "full" else pairs_per_s,
+            "unit": "query_embeddings/s" if a.mode == "full" else "cosine_pairs/s",
+            "cosine_pairs_per_s": pairs_per_s,
+            "query_embeddings_per_s": q_per_s if a.mode == "full" else None,
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16 towers / f32 kNN (f64 re-rank)" if a.mode == "full" else "f32 (f64 re-rank)",
+            "data": "synthetic (seeded N(0,1) gallery; random-init weights)",
+            "config": {"workload": ("cfg2: Swin-T + BERT-base towers, B=%d, top-%d over %dx%d f32 per GPU" % (B, K, n, d))
+                       if a.mode == "full" else ("kNN only: Q=%d, top-%d over %dx%d f32 per GPU" % (B, K, n, d)),
+                       "global_batch": world * B, "gallery_rows": world * n, "dim": d, "k": K,
+                       "parallelism": f"gallery row-shard x{world}" if world > 1 else "single"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def out_q_for_cpu(model, imgs, ids, mask):
+    return None
+
+
+def cpu_baseline(a, G, qdev):
+    """Oracle CPU path (tests-only infrastructure, timed here as the baseline): cosine + top-K in
+    numpy f32/BLAS on a bounded query sample, all host cores."""
+    import numpy as np
+    import torch
+    from oracle import knn as oknn
+    threads = torch.get_num_threads()
+    nq = a.cpu_sample_queries or 64
+    Q = qdev[:nq].float().cpu().numpy() if qdev is not None else np.random.default_rng(0).standard_normal((nq, a.dim), dtype=np.float32)
+    oknn.sklearn_topk(Q[:4], G, a.k)  # warm-up
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        oknn.sklearn_topk(Q, G, a.k)
+        ts.append(time.perf_counter() - t0)
+    t = sorted(ts)[1]
+    return {"value": nq * G.shape[0] / t, "unit": "cosine_pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{nq} queries x {G.shape[0]}x{G.shape[1]} gallery, numpy cosine + argsort top-{a.k} "
+                      f"(restated sklearn path), median of 3, CPU: {cpu_model()}"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,143 @@
+/* libmmr — MI355X (gfx950) joint-embedding retrieval hot path behind a C ABI.
+ *
+ * Every entry point takes plain pointers + sizes (no torch types), returns an mmr_status and, on
+ * failure, leaves a message in the thread-local mmr_last_error().  No exceptions cross the ABI.
+ * Ownership: the caller owns every input/output buffer (device pointers unless a parameter says
+ * host); the library owns mmr_index state and its workspaces.  Launches are asynchronous on the
+ * caller's HIP stream (`stream` = hipStream_t, NULL = default stream).
+ *
+ * Reference interfaces replaced (file:line in ppddddpp/multi-modal-retrieval-predict-project):
+ *   mmr_index_create   RetrievalEngine.__init__  src/Retrieval/retrieval.py:24-32
+ *                      (np.load(...).astype(float32) -> self.embs (N,D)); norms precomputed once
+ *                      instead of sklearn normalize() per call (retrieval.py:128).
+ *   mmr_index_search   exact brute-force top-K: sklearn cosine_similarity + np.argsort(...)[::-1][:K]
+ *                      src/Evaluate/retrieval_overlap.py:84-90, src/Retrieval/retrieval.py:128-137;
+ *                      reached via RetrievalEngine.retrieve retrieval.py:34-39.
+ *   mmr_merge_topk     (new) k-way merge of per-shard top-K lists after the RCCL all-gather.
+ *   tower ops          timm SwinTransformer.forward_features (src/Model/fusion.py:198-199),
+ *                      HF BertModel(...).last_hidden_state (fusion.py:322-325), heads
+ *                      src/Model/model.py:365-373,462-479; see the per-function comments.
+ */
+#ifndef MMR_H
+#define MMR_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  MMR_OK = 0,
+  MMR_ERR_INVALID = 1,     /* bad argument (shape, null pointer, unsupported K/D) */
+  MMR_ERR_HIP = 2,         /* a HIP runtime call failed */
+  MMR_ERR_OOM = 3,         /* device allocation failed */
+  MMR_ERR_UNSUPPORTED = 4, /* dtype / geometry not built */
+  MMR_ERR_CAPACITY = 5     /* a per-query candidate buffer overflowed (see out_status) */
+} mmr_status;
+
+typedef enum { MMR_F32 = 0, MMR_F16 = 1, MMR_BF16 = 2 } mmr_dtype;
+
+typedef struct mmr_index mmr_index;
+
+const char* mmr_last_error(void);
+int mmr_version(void);
+int mmr_max_k(void);
+
+/* ---------------------------------------------------------------- gallery index (kNN) */
+/* Copy an (n, d) row-major gallery (host pointer if `gallery_is_host`, else device) into a
+ * library-owned device layout on `device`, computing per-row inverse norms (f32) and norms (f64).
+ * `idx_base` is added to every returned index (row-sharded galleries: global = local + base).
+ * Only MMR_F32 is built in this round. */
+mmr_status mmr_index_create(const void* gallery, int64_t n, int32_t d, mmr_dtype dtype,
+                            int gallery_is_host, int64_t idx_base, int device, mmr_index** out);
+mmr_status mmr_index_destroy(mmr_index* index);
+mmr_status mmr_index_info(const mmr_index* index, int64_t* n, int32_t* d, int64_t* idx_base);
+/* Pre-allocate the workspace for up to `max_q` queries so that later searches allocate nothing
+ * (required before capturing a search into a HIP graph). */
+mmr_status mmr_index_reserve(mmr_index* index, int64_t max_q);
+
+/* Exact cosine top-K of q (q, d) f32 device queries against the gallery.
+ * Semantics: s(q,g) = <q,g> / (|q| |g|) in f64 (0 when either norm is 0 — sklearn's normalize()
+ * leaves zero rows at 0), ranked by score descending, ties by lower gallery index.  Outputs
+ * (q, k) int64 indices (+idx_base) and f32 scores; slots beyond n are (-1, -inf).
+ * out_status (q,) int32 (may be NULL): 0 ok, 1 = candidate buffer overflow for that query.
+ * Asynchronous on `stream`. */
+mmr_status mmr_index_search(mmr_index* index, const float* q, int64_t nq, int32_t k,
+                            int64_t* out_idx, float* out_score, double* out_score64,
+                            int32_t* out_status, void* stream);
+/* out_score64 (q, k) f64 (may be NULL): the exact scores the ranking used; the shard merge ranks
+ * on these so a row-sharded search returns exactly the single-device result. */
+
+/* Merge n_lists per-shard lists laid out [n_lists][nq][k_in] (f64 scores, int64 idx; empty slots
+ * idx -1) into the global top-k_out per query: score desc, then index asc.  out_score f32 (may be
+ * NULL), out_score64 f64 (may be NULL). */
+mmr_status mmr_merge_topk(const double* scores, const int64_t* idx, int32_t n_lists, int64_t nq,
+                          int32_t k_in, int32_t k_out, int64_t* out_idx, float* out_score,
+                          double* out_score64, void* stream);
+
+/* ---------------------------------------------------------------- tower ops (bf16 = uint16) */
+/* Y[m][n] = act(X[m][k] . W[n][k]^T + bias[n]) (+ R[m][n]); X, W, R, Y bf16; bias f32 or NULL;
+ * act: 0 none, 1 GELU(erf).  nn.Linear semantics (weight [out][in]).  f32 accumulation. */
+mmr_status mmr_linear_bf16(const uint16_t* x, const uint16_t* w, const float* bias,
+                           const uint16_t* residual, uint16_t* y, int64_t m, int32_t n, int32_t k,
+                           int32_t act, void* stream);
+
+/* Row LayerNorm over c channels (bf16 in/out, f32 math, gamma/beta f32). */
+mmr_status mmr_layernorm_bf16(const uint16_t* x, const float* gamma, const float* beta,
+                              uint16_t* y, int64_t rows, int32_t c, float eps, void* stream);
+
+/* BERT embeddings (HF BertEmbeddings): LN(word[id] + pos[l] + type[0]) -> bf16 (b*l, c). */
+mmr_status mmr_bert_embed(const int64_t* ids, const float* word, const float* pos,
+                          const float* type0, const float* gamma, const float* beta, uint16_t* y,
+                          int32_t b, int32_t l, int32_t c, float eps, void* stream);
+
+/* BERT self-attention core (HF BertSelfAttention, eval): qkv bf16 (b*l, 3*h*dh) [q|k|v],
+ * additive mask from mask01 (b, l) int64 (0 -> masked), softmax(q k^T / sqrt(dh)) v -> ctx bf16
+ * (b*l, h*dh).  l <= 512, dh = 64. */
+mmr_status mmr_bert_attention(const uint16_t* qkv, const int64_t* mask01, uint16_t* ctx,
+                              int32_t b, int32_t l, int32_t h, int32_t dh, void* stream);
+
+/* Swin (shifted-)window attention core (timm WindowAttention + cyclic shift, eval):
+ * qkv bf16 (b*hw*hw, 3*c) in natural token order; the kernel applies roll(-shift), window
+ * partition, q*dh^-0.5, k^T, + rel-pos bias (table f32 [(2ws-1)^2][heads]) + shift mask (-100),
+ * softmax, v, window reverse and roll(+shift) -> out bf16 (b*hw*hw, c).  ws = 7, dh = 32. */
+mmr_status mmr_swin_window_attention(const uint16_t* qkv, const float* relpos_table,
+                                     uint16_t* out, int32_t b, int32_t hw, int32_t c,
+                                     int32_t heads, int32_t ws, int32_t shift, void* stream);
+
+/* Swin patch embedding im2col: image f32 NCHW (b,3,224,224) -> bf16 (b*56*56, 48) columns in
+ * conv-weight order (cin, kh, kw) for a 4x4/s4 conv as a GEMM. */
+mmr_status mmr_patch_im2col(const float* image, uint16_t* cols, int32_t b, int32_t cin,
+                            int32_t hw, int32_t patch, void* stream);
+
+/* Swin PatchMerging gather + LayerNorm(4c): x bf16 (b, hw, hw, c) -> y bf16 (b*(hw/2)^2, 4c) in
+ * timm order [x(0,0), x(1,0), x(0,1), x(1,1)]. */
+mmr_status mmr_patch_merge_ln(const uint16_t* x, const float* gamma, const float* beta,
+                              uint16_t* y, int32_t b, int32_t hw, int32_t c, float eps,
+                              void* stream);
+
+/* Swin head (fusion.py:263-265 with swin_norm = swin.norm): x bf16 (b, t, c) = backbone tokens
+ * BEFORE the final norm.  patches = LN(LN(x)) f32 (b,t,c), global = mean_t LN(x) f32 (b,c),
+ * pool = mean over the t+1 rows [global; patches] f32 (b,c) — the image head's pooled input
+ * (model.py:463-468: mean(cat[proj(g), proj(p)]) == proj(mean(cat[g, p])) for an affine proj).
+ * Any output may be NULL. */
+mmr_status mmr_swin_head(const uint16_t* x, const float* gamma, const float* beta, float* patches,
+                         float* global, float* pool, int32_t b, int32_t t, int32_t c, float eps,
+                         void* stream);
+
+/* Unmasked mean over l tokens (model.py:370, PAD included): x bf16 (b,l,c) -> f32 (b,c). */
+mmr_status mmr_mean_tokens(const uint16_t* x, float* y, int32_t b, int32_t l, int32_t c,
+                           void* stream);
+
+/* Fused projection head: y = W2 . GELU(W1 . (Wp . x + bp) + b1) + b2 (model.py:365-373 proj then
+ * MultiHeadMLP model.py:61-75), f32 weights/activations, optional L2 normalise of the result.
+ * w2/b2/w1/b1 may be NULL (projection only).  x (b, cin) f32, y (b, d) f32. */
+mmr_status mmr_proj_head(const float* x, const float* wp, const float* bp, const float* w1,
+                         const float* b1, const float* w2, const float* b2, float* y, int32_t b,
+                         int32_t cin, int32_t d, int32_t l2norm, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMR_H */

@@ -1,0 +1,82 @@
+"""ctypes binding of libmmr.so (include/mmr.h).  The product path has no CPU fallback: if the
+library is missing or no GPU is visible, the first call raises.
+
+torch is imported first on purpose: torch's wheel ships its own libamdhip64.so.7, and loading it
+before libmmr.so makes both share ONE HIP runtime (same soname), so torch device pointers and
+streams are valid inside the library.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmmr.so")
+
+c_i32, c_i64, c_f32, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
+
+# name -> argtypes (restype is always int status unless listed in _RESTYPES)
+SIGNATURES = {
+    "mmr_last_error": [],
+    "mmr_version": [],
+    "mmr_max_k": [],
+    "mmr_index_create": [c_vp, c_i64, c_i32, c_i32, ctypes.c_int, c_i64, ctypes.c_int, ctypes.POINTER(c_vp)],
+    "mmr_index_destroy": [c_vp],
+    "mmr_index_info": [c_vp, ctypes.POINTER(c_i64), ctypes.POINTER(c_i32), ctypes.POINTER(c_i64)],
+    "mmr_index_reserve": [c_vp, c_i64],
+    "mmr_index_search": [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "mmr_merge_topk": [c_vp, c_vp, c_i32, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp],
+    "mmr_linear_bf16": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp],
+    "mmr_layernorm_bf16": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp],
+    "mmr_bert_embed": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp],
+    "mmr_bert_attention": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp],
+    "mmr_swin_window_attention": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp],
+    "mmr_patch_im2col": [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp],
+    "mmr_patch_merge_ln": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp],
+    "mmr_swin_head": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp],
+    "mmr_mean_tokens": [c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
+    "mmr_proj_head": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp],
+}
+_RESTYPES = {"mmr_last_error": ctypes.c_char_p, "mmr_version": ctypes.c_int, "mmr_max_k": ctypes.c_int}
+
+_lib = None
+
+
+class MMRError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libmmr.so once; raise (never fall back) if it is absent or incomplete."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MMRError(f"{LIB_PATH} is not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, args in SIGNATURES.items():
+            fn = getattr(L, name)  # AttributeError if the export is missing
+            fn.argtypes = args
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
+        _lib = L
+    return _lib
+
+
+def check(status, what):
+    if status != 0:
+        msg = lib().mmr_last_error().decode(errors="replace")
+        raise MMRError(f"{what} failed (status {status}): {msg}")
+
+
+def require_gpu(t=None):
+    if not torch.cuda.is_available():
+        raise MMRError("libmmr needs a ROCm GPU (torch.cuda.is_available() is False); no CPU fallback")
+    if t is not None and not t.is_cuda:
+        raise MMRError("libmmr ops take device tensors")
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

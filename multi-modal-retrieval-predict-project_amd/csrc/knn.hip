@@ -1,0 +1,617 @@
+// Brute-force batched cosine top-K over a row-major gallery (gfx950).
+//
+// Reference semantics (what this replaces): sklearn cosine_similarity(Q, G) + per-row
+// np.argsort(sim[i])[::-1][:K]  — src/Evaluate/retrieval_overlap.py:84-90, same idiom in
+// src/Retrieval/retrieval.py:128-137.  Here: exact cosine in f64, ties -> lower index.
+//
+// Pipeline per search (all on the caller's stream):
+//   1. knn_prep_queries   q -> qn = q/|q| (f32, padded [Qp][Dp]) + |q| in f64.
+//   2. knn_scores         S[Qp][Np] = (qn . g) * (1/|g|) with v_mfma_f32_32x32x2_f32 (exact f32
+//                         products, f32 accumulate).  MFMA-bound for Q >~ 40, HBM-bound below.
+//                         Wave tile 64 queries x 64 gallery rows (2x2 MFMA tiles, 64 acc regs);
+//                         operands loaded straight to VGPRs as float4 with a k-permutation (lane
+//                         half h owns k = kb+8h..kb+8h+7), which the dot product does not see.
+//   3. knn_select         one 1024-thread workgroup per query: (A) per-thread max over a strided
+//                         slice of the row; (B) b = K-th largest of the 1024 maxima (a lower bound
+//                         of the K-th largest score); (C) collect every s >= b - 2*delta into LDS;
+//                         (D) rare fallback: exact radix select over the row if (C) overflowed;
+//                         (E) re-score candidates in f64 from the raw rows, rank by
+//                         (score desc, index asc), write the top K.
+//      delta bounds |s_f32 - s_f64| (D+16 ulps of 1.0), so every true top-K row is a candidate:
+//      the K rows with s32 >= t (t = K-th largest s32) all have s64 >= t - delta, hence the K-th
+//      largest s64 is >= t - delta and any true top-K row has s32 >= t - 2 delta >= b - 2 delta.
+#include <float.h>
+#include <math.h>
+#include <mutex>
+#include <vector>
+
+#include "common.h"
+
+namespace {
+
+using mmr::ceil_div;
+using mmr::round_up;
+
+constexpr int kSelThreads = 1024;
+constexpr int kCandCap = 2048;
+constexpr int kMaxK = 256;
+constexpr int kRowPad = 256;  // gallery rows padded to this (covers every scores tile width)
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ uint32_t f2key(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key2f(uint32_t k) {
+  uint32_t u = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
+  return __uint_as_float(u);
+}
+
+// ------------------------------------------------------------------ gallery / query preparation
+// One wave per row: copy into the padded layout, f64 norm, f32 inverse norm.
+__global__ __launch_bounds__(256) void knn_prep_gallery(const float* __restrict__ src, int64_t n,
+                                                        int d, float* __restrict__ dst, int Dp,
+                                                        int64_t Np, float* __restrict__ inv_norm,
+                                                        double* __restrict__ norm64) {
+  int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  int lane = threadIdx.x & 63;
+  if (row >= Np) return;
+  double ss = 0.0;
+  float* out = dst + row * Dp;
+  if (row < n) {
+    const float* in = src + row * (int64_t)d;
+    for (int k = lane; k < Dp; k += 64) {
+      float v = k < d ? in[k] : 0.0f;
+      out[k] = v;
+      ss += (double)v * (double)v;
+    }
+  } else {
+    for (int k = lane; k < Dp; k += 64) out[k] = 0.0f;
+  }
+  ss = mmr::wave_sum(ss);
+  if (lane == 0) {
+    double nrm = sqrt(ss);
+    norm64[row] = nrm;
+    inv_norm[row] = nrm > 0.0 ? (float)(1.0 / nrm) : 0.0f;
+  }
+}
+
+__global__ __launch_bounds__(256) void knn_prep_queries(const float* __restrict__ q, int64_t nq,
+                                                        int d, float* __restrict__ qn, int Dp,
+                                                        int64_t Qp, double* __restrict__ qnorm64) {
+  int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  int lane = threadIdx.x & 63;
+  if (row >= Qp) return;
+  float* out = qn + row * Dp;
+  if (row >= nq) {
+    for (int k = lane; k < Dp; k += 64) out[k] = 0.0f;
+    return;
+  }
+  const float* in = q + row * (int64_t)d;
+  double ss = 0.0;
+  for (int k = lane; k < d; k += 64) ss += (double)in[k] * (double)in[k];
+  ss = mmr::wave_sum(ss);
+  double nrm = sqrt(ss);
+  float inv = nrm > 0.0 ? (float)(1.0 / nrm) : 0.0f;
+  for (int k = lane; k < Dp; k += 64) out[k] = k < d ? in[k] * inv : 0.0f;
+  if (lane == 0) qnorm64[row] = nrm;
+}
+
+// ------------------------------------------------------------------ scores GEMM (f32 MFMA)
+// Workgroup = 4 waves arranged WQ x WN; wave tile 64 x 64; workgroup tile (64WQ) x (64WN).
+// Block id -> (gallery tile t, query block j) keeps all query blocks of one gallery tile on the
+// same XCD (ids congruent mod 8) so the gallery rows are fetched from HBM once per XCD L2.
+template <int WQ, int WN>
+__global__ __launch_bounds__(256) void knn_scores(const float* __restrict__ qn,
+                                                  const float* __restrict__ gal,
+                                                  const float* __restrict__ inv_g,
+                                                  float* __restrict__ scores, int Dp, int64_t ldS,
+                                                  int n_gtiles, int n_qblocks) {
+  const int b = blockIdx.x;
+  const int per = 8 * n_qblocks;
+  const int t = (b / per) * 8 + (b % 8);
+  const int j = (b % per) / 8;
+  if (t >= n_gtiles) return;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wq = wave / WN, wn = wave % WN;
+  const int64_t q0 = (int64_t)j * (64 * WQ) + wq * 64;
+  const int64_t g0 = (int64_t)t * (64 * WN) + wn * 64;
+  const int r = lane & 31, h = lane >> 5;
+
+  const float* pa0 = qn + (q0 + r) * Dp + 8 * h;
+  const float* pa1 = pa0 + 32 * (int64_t)Dp;
+  const float* pb0 = gal + (g0 + r) * Dp + 8 * h;
+  const float* pb1 = pb0 + 32 * (int64_t)Dp;
+
+  f32x16 c00 = {0}, c01 = {0}, c10 = {0}, c11 = {0};
+  float4 a0l = *(const float4*)(pa0), a0h = *(const float4*)(pa0 + 4);
+  float4 a1l = *(const float4*)(pa1), a1h = *(const float4*)(pa1 + 4);
+  float4 b0l = *(const float4*)(pb0), b0h = *(const float4*)(pb0 + 4);
+  float4 b1l = *(const float4*)(pb1), b1h = *(const float4*)(pb1 + 4);
+  for (int kb = 0; kb < Dp; kb += 16) {
+    float4 na0l, na0h, na1l, na1h, nb0l, nb0h, nb1l, nb1h;
+    const bool more = kb + 16 < Dp;
+    if (more) {
+      na0l = *(const float4*)(pa0 + kb + 16); na0h = *(const float4*)(pa0 + kb + 20);
+      na1l = *(const float4*)(pa1 + kb + 16); na1h = *(const float4*)(pa1 + kb + 20);
+      nb0l = *(const float4*)(pb0 + kb + 16); nb0h = *(const float4*)(pb0 + kb + 20);
+      nb1l = *(const float4*)(pb1 + kb + 16); nb1h = *(const float4*)(pb1 + kb + 20);
+    }
+    const float a0[8] = {a0l.x, a0l.y, a0l.z, a0l.w, a0h.x, a0h.y, a0h.z, a0h.w};
+    const float a1[8] = {a1l.x, a1l.y, a1l.z, a1l.w, a1h.x, a1h.y, a1h.z, a1h.w};
+    const float b0[8] = {b0l.x, b0l.y, b0l.z, b0l.w, b0h.x, b0h.y, b0h.z, b0h.w};
+    const float b1[8] = {b1l.x, b1l.y, b1l.z, b1l.w, b1h.x, b1h.y, b1h.z, b1h.w};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      c00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b0[s], c00, 0, 0, 0);
+      c01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b1[s], c01, 0, 0, 0);
+      c10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b0[s], c10, 0, 0, 0);
+      c11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b1[s], c11, 0, 0, 0);
+    }
+    if (more) {
+      a0l = na0l; a0h = na0h; a1l = na1l; a1h = na1h;
+      b0l = nb0l; b0h = nb0h; b1l = nb1l; b1h = nb1h;
+    }
+  }
+  // C[i][j]: j = lane&31 (gallery row), i = (reg&3) + 8*(reg>>2) + 4*(lane>>5) (query)
+  const float ig0 = inv_g[g0 + r], ig1 = inv_g[g0 + 32 + r];
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int i = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+    float* s0 = scores + (q0 + i) * ldS + g0 + r;
+    float* s1 = scores + (q0 + 32 + i) * ldS + g0 + r;
+    s0[0] = c00[reg] * ig0;
+    s0[32] = c01[reg] * ig1;
+    s1[0] = c10[reg] * ig0;
+    s1[32] = c11[reg] * ig1;
+  }
+}
+
+// ------------------------------------------------------------------ per-query selection
+// Block-wide radix select: the kth (1-based) largest key among keys[0..m) (LDS).  All threads
+// return the same key.  hist: 256-entry LDS scratch.
+__device__ uint32_t block_select_kth(const uint32_t* keys, int m, int kth, uint32_t* hist,
+                                     uint32_t* bcast) {
+  uint32_t prefix = 0, pmask = 0;
+  uint32_t krem = (uint32_t)kth;
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 24 - 8 * pass;
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {
+      uint32_t key = keys[i];
+      if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t acc = 0;
+      int dg = 255;
+      for (; dg > 0; --dg) {
+        if (acc + hist[dg] >= krem) break;
+        acc += hist[dg];
+      }
+      bcast[0] = prefix | ((uint32_t)dg << shift);
+      bcast[1] = krem - acc;
+    }
+    __syncthreads();
+    prefix = bcast[0];
+    krem = bcast[1];
+    pmask |= 0xFFu << shift;
+    __syncthreads();
+  }
+  return prefix;
+}
+
+// Same over a global row (fallback path, all N elements each pass).
+__device__ uint32_t row_select_kth(const float* row, int64_t n, int kth, uint32_t* hist,
+                                   uint32_t* bcast) {
+  uint32_t prefix = 0, pmask = 0;
+  uint32_t krem = (uint32_t)kth;
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 24 - 8 * pass;
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+      uint32_t key = f2key(row[i]);
+      if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t acc = 0;
+      int dg = 255;
+      for (; dg > 0; --dg) {
+        if (acc + hist[dg] >= krem) break;
+        acc += hist[dg];
+      }
+      bcast[0] = prefix | ((uint32_t)dg << shift);
+      bcast[1] = krem - acc;
+    }
+    __syncthreads();
+    prefix = bcast[0];
+    krem = bcast[1];
+    pmask |= 0xFFu << shift;
+    __syncthreads();
+  }
+  return prefix;
+}
+
+__device__ __forceinline__ float lower_threshold(float t, float two_delta) {
+  double thr_d = (double)t - (double)two_delta;
+  float thr = (float)thr_d;
+  if ((double)thr > thr_d) thr = nextafterf(thr, -INFINITY);
+  return thr;
+}
+
+__global__ __launch_bounds__(kSelThreads) void knn_select(
+    const float* __restrict__ scores, int64_t ldS, int64_t n, int k, float two_delta,
+    const float* __restrict__ q_raw, int d, const double* __restrict__ qnorm64,
+    const float* __restrict__ gal, int Dp, const double* __restrict__ gnorm64, int64_t idx_base,
+    int64_t* __restrict__ out_idx, float* __restrict__ out_score, double* __restrict__ out_score64,
+    int32_t* __restrict__ status) {
+  __shared__ uint32_t tmax[kSelThreads];
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t bcast[4];
+  __shared__ int cand_i[kCandCap];
+  __shared__ double cand_d[kCandCap];
+
+  const int64_t qi = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float* row = scores + qi * ldS;
+  const int kk = (int)(n < (int64_t)k ? n : (int64_t)k);
+  int64_t* oi = out_idx + qi * k;
+  float* os = out_score ? out_score + qi * k : nullptr;
+  double* os64 = out_score64 ? out_score64 + qi * k : nullptr;
+  for (int r = kk + tid; r < k; r += kSelThreads) {
+    oi[r] = -1;
+    if (os) os[r] = -INFINITY;
+    if (os64) os64[r] = -INFINITY;
+  }
+  if (kk <= 0) {
+    if (tid == 0 && status) status[qi] = 0;
+    return;
+  }
+
+  // (A) per-thread max over a strided slice (float4 body + scalar tail)
+  const int64_t n4 = n >> 2;
+  float m = -INFINITY;
+  for (int64_t i = tid; i < n4; i += kSelThreads) {
+    float4 v = ((const float4*)row)[i];
+    m = fmaxf(fmaxf(m, v.x), fmaxf(fmaxf(v.y, v.z), v.w));
+  }
+  for (int64_t i = (n4 << 2) + tid; i < n; i += kSelThreads) m = fmaxf(m, row[i]);
+  tmax[tid] = f2key(m);
+  if (tid == 0) bcast[2] = 0;
+  __syncthreads();
+  // (B) lower bound b of the K-th largest score
+  const float bnd = key2f(block_select_kth(tmax, kSelThreads, kk, hist, bcast));
+  float thr = lower_threshold(bnd, two_delta);
+  // (C) collect candidates
+  for (int64_t i = tid; i < n4; i += kSelThreads) {
+    float4 v = ((const float4*)row)[i];
+    const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (vv[e] >= thr) {
+        uint32_t p = atomicAdd(&bcast[2], 1u);
+        if (p < kCandCap) cand_i[p] = (int)(4 * i + e);
+      }
+  }
+  for (int64_t i = (n4 << 2) + tid; i < n; i += kSelThreads)
+    if (row[i] >= thr) {
+      uint32_t p = atomicAdd(&bcast[2], 1u);
+      if (p < kCandCap) cand_i[p] = (int)i;
+    }
+  __syncthreads();
+  int cnt = (int)bcast[2];
+  int st = 0;
+  if (cnt > kCandCap) {
+    // (D) fallback: exact K-th largest s32 over the whole row, then the tight threshold
+    __syncthreads();
+    const float t = key2f(row_select_kth(row, n, kk, hist, bcast));
+    thr = lower_threshold(t, two_delta);
+    if (tid == 0) bcast[2] = 0;
+    __syncthreads();
+    for (int64_t i = tid; i < n; i += kSelThreads)
+      if (row[i] >= thr) {
+        uint32_t p = atomicAdd(&bcast[2], 1u);
+        if (p < kCandCap) cand_i[p] = (int)i;
+      }
+    __syncthreads();
+    cnt = (int)bcast[2];
+    if (cnt > kCandCap) {
+      st = 1;
+      cnt = kCandCap;
+    }
+  }
+  // (E) f64 re-score from the raw rows
+  const float* qr = q_raw + qi * (int64_t)d;
+  const double qn = qnorm64[qi];
+  for (int c = wave; c < cnt; c += kSelThreads / 64) {
+    const int gi = cand_i[c];
+    const float* gr = gal + (int64_t)gi * Dp;
+    double acc = 0.0;
+    for (int kq = lane; kq < d; kq += 64) acc += (double)qr[kq] * (double)gr[kq];
+    acc = mmr::wave_sum(acc);
+    if (lane == 0) {
+      const double gn = gnorm64[gi];
+      cand_d[c] = (qn > 0.0 && gn > 0.0) ? acc / (qn * gn) : 0.0;
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < cnt; c += kSelThreads) {
+    const double sc = cand_d[c];
+    const int ic = cand_i[c];
+    int rank = 0;
+    for (int j2 = 0; j2 < cnt; ++j2) {
+      const double sj = cand_d[j2];
+      rank += (sj > sc) || (sj == sc && cand_i[j2] < ic);
+    }
+    if (rank < kk) {
+      oi[rank] = (int64_t)ic + idx_base;
+      if (os) os[rank] = (float)sc;
+      if (os64) os64[rank] = sc;
+    }
+  }
+  if (tid == 0 && status) status[qi] = st;
+}
+
+// ------------------------------------------------------------------ shard merge
+__global__ __launch_bounds__(256) void knn_merge(const double* __restrict__ scores,
+                                                 const int64_t* __restrict__ idx, int n_lists,
+                                                 int64_t nq, int k_in, int k_out,
+                                                 int64_t* __restrict__ out_idx,
+                                                 float* __restrict__ out_score,
+                                                 double* __restrict__ out_score64) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* cs = (double*)smem;
+  int64_t* ci = (int64_t*)(smem + sizeof(double) * n_lists * k_in);
+  const int64_t qi = blockIdx.x;
+  const int m = n_lists * k_in;
+  for (int c = threadIdx.x; c < m; c += blockDim.x) {
+    const int l = c / k_in, e = c % k_in;
+    const int64_t off = ((int64_t)l * nq + qi) * k_in + e;
+    cs[c] = scores[off];
+    ci[c] = idx[off];
+  }
+  __syncthreads();
+  int nvalid = 0;
+  for (int c = 0; c < m; ++c) nvalid += ci[c] >= 0;
+  for (int c = threadIdx.x; c < m; c += blockDim.x) {
+    const int64_t ic = ci[c];
+    if (ic < 0) continue;
+    const double sc = cs[c];
+    int rank = 0;
+    for (int j = 0; j < m; ++j) {
+      const int64_t ij = ci[j];
+      if (ij < 0) continue;
+      const double sj = cs[j];
+      rank += (sj > sc) || (sj == sc && ij < ic);
+    }
+    if (rank < k_out) {
+      out_idx[qi * k_out + rank] = ic;
+      if (out_score) out_score[qi * k_out + rank] = (float)sc;
+      if (out_score64) out_score64[qi * k_out + rank] = sc;
+    }
+  }
+  for (int r = nvalid + threadIdx.x; r < k_out; r += blockDim.x) {
+    out_idx[qi * k_out + r] = -1;
+    if (out_score) out_score[qi * k_out + r] = -INFINITY;
+    if (out_score64) out_score64[qi * k_out + r] = -INFINITY;
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ index object
+struct mmr_index {
+  int device = 0;
+  int64_t n = 0, Np = 0, idx_base = 0;
+  int d = 0, Dp = 0;
+  float* gal = nullptr;       // [Np][Dp]
+  float* inv_norm = nullptr;  // [Np]
+  double* norm64 = nullptr;   // [Np]
+  // workspace (single; guarded by mu — searches on one index serialise their enqueue)
+  std::mutex mu;
+  int64_t ws_q = 0;  // queries the workspace holds
+  float* qn = nullptr;
+  double* qnorm64 = nullptr;
+  float* scores = nullptr;
+};
+
+namespace {
+
+constexpr int64_t kScoresBudget = int64_t(4) << 30;  // bytes of score workspace per chunk
+
+int64_t chunk_queries(const mmr_index* ix) {
+  int64_t per = ix->Np * (int64_t)sizeof(float);
+  int64_t c = kScoresBudget / per;
+  c = c / 256 * 256;
+  return c < 256 ? 256 : c;
+}
+
+mmr_status ensure_ws(mmr_index* ix, int64_t nq) {
+  int64_t want = round_up(nq < chunk_queries(ix) ? nq : chunk_queries(ix), 256);
+  if (want <= ix->ws_q) return MMR_OK;
+  if (ix->qn) (void)hipFree(ix->qn);
+  if (ix->qnorm64) (void)hipFree(ix->qnorm64);
+  if (ix->scores) (void)hipFree(ix->scores);
+  ix->qn = nullptr; ix->qnorm64 = nullptr; ix->scores = nullptr; ix->ws_q = 0;
+  MMR_CHECK_HIP(hipMalloc(&ix->qn, sizeof(float) * want * ix->Dp));
+  MMR_CHECK_HIP(hipMalloc(&ix->qnorm64, sizeof(double) * want));
+  MMR_CHECK_HIP(hipMalloc(&ix->scores, sizeof(float) * want * ix->Np));
+  ix->ws_q = want;
+  return MMR_OK;
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int mmr_max_k(void) { return kMaxK; }
+
+mmr_status mmr_index_create(const void* gallery, int64_t n, int32_t d, mmr_dtype dtype,
+                            int gallery_is_host, int64_t idx_base, int device, mmr_index** out) {
+  mmr::clear_error();
+  MMR_REQUIRE(out != nullptr, "mmr_index_create: out is NULL");
+  MMR_REQUIRE(n >= 0 && d > 0, "mmr_index_create: bad shape n=%lld d=%d", (long long)n, d);
+  MMR_REQUIRE(n == 0 || gallery != nullptr, "mmr_index_create: gallery is NULL");
+  MMR_REQUIRE(n < (int64_t(1) << 31), "mmr_index_create: n=%lld exceeds 2^31 rows per shard",
+              (long long)n);
+  if (dtype != MMR_F32) {
+    mmr::set_error("mmr_index_create: dtype %d not built (only MMR_F32)", (int)dtype);
+    return MMR_ERR_UNSUPPORTED;
+  }
+  DeviceGuard g(device);
+  mmr_index* ix = new mmr_index();
+  ix->device = device;
+  ix->n = n;
+  ix->d = d;
+  ix->Dp = (int)round_up(d, 16);
+  ix->Np = round_up(n > 0 ? n : 1, kRowPad);
+  ix->idx_base = idx_base;
+  auto fail = [&](mmr_status s) {
+    mmr_index_destroy(ix);
+    return s;
+  };
+  hipError_t e;
+  if ((e = hipMalloc(&ix->gal, sizeof(float) * ix->Np * ix->Dp)) != hipSuccess ||
+      (e = hipMalloc(&ix->inv_norm, sizeof(float) * ix->Np)) != hipSuccess ||
+      (e = hipMalloc(&ix->norm64, sizeof(double) * ix->Np)) != hipSuccess) {
+    mmr::set_error("mmr_index_create: hipMalloc failed: %s", hipGetErrorString(e));
+    return fail(MMR_ERR_OOM);
+  }
+  // stage the raw rows into a contiguous device buffer, then pad + norm in one kernel
+  float* raw = nullptr;
+  if (n > 0) {
+    if ((e = hipMalloc(&raw, sizeof(float) * n * d)) != hipSuccess) {
+      mmr::set_error("mmr_index_create: hipMalloc(raw) failed: %s", hipGetErrorString(e));
+      return fail(MMR_ERR_OOM);
+    }
+    e = hipMemcpy(raw, gallery, sizeof(float) * n * d,
+                  gallery_is_host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(raw);
+      mmr::set_error("mmr_index_create: hipMemcpy failed: %s", hipGetErrorString(e));
+      return fail(MMR_ERR_HIP);
+    }
+  }
+  knn_prep_gallery<<<dim3((unsigned)ceil_div(ix->Np, 4)), dim3(256)>>>(
+      raw, n, d, ix->gal, ix->Dp, ix->Np, ix->inv_norm, ix->norm64);
+  e = hipGetLastError();
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (raw) (void)hipFree(raw);
+  if (e != hipSuccess) {
+    mmr::set_error("mmr_index_create: prep kernel failed: %s", hipGetErrorString(e));
+    return fail(MMR_ERR_HIP);
+  }
+  *out = ix;
+  return MMR_OK;
+}
+
+mmr_status mmr_index_destroy(mmr_index* ix) {
+  if (!ix) return MMR_OK;
+  DeviceGuard g(ix->device);
+  if (ix->gal) (void)hipFree(ix->gal);
+  if (ix->inv_norm) (void)hipFree(ix->inv_norm);
+  if (ix->norm64) (void)hipFree(ix->norm64);
+  if (ix->qn) (void)hipFree(ix->qn);
+  if (ix->qnorm64) (void)hipFree(ix->qnorm64);
+  if (ix->scores) (void)hipFree(ix->scores);
+  delete ix;
+  return MMR_OK;
+}
+
+mmr_status mmr_index_info(const mmr_index* ix, int64_t* n, int32_t* d, int64_t* idx_base) {
+  mmr::clear_error();
+  MMR_REQUIRE(ix != nullptr, "mmr_index_info: index is NULL");
+  if (n) *n = ix->n;
+  if (d) *d = ix->d;
+  if (idx_base) *idx_base = ix->idx_base;
+  return MMR_OK;
+}
+
+mmr_status mmr_index_reserve(mmr_index* ix, int64_t max_q) {
+  mmr::clear_error();
+  MMR_REQUIRE(ix != nullptr && max_q > 0, "mmr_index_reserve: bad arguments");
+  DeviceGuard g(ix->device);
+  std::lock_guard<std::mutex> lk(ix->mu);
+  return ensure_ws(ix, max_q);
+}
+
+mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k,
+                            int64_t* out_idx, float* out_score, double* out_score64,
+                            int32_t* out_status, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(ix != nullptr, "mmr_index_search: index is NULL");
+  MMR_REQUIRE(nq >= 0, "mmr_index_search: nq < 0");
+  MMR_REQUIRE(k >= 1 && k <= kMaxK, "mmr_index_search: K=%d outside [1, %d]", k, kMaxK);
+  if (nq == 0) return MMR_OK;
+  MMR_REQUIRE(q != nullptr && out_idx != nullptr, "mmr_index_search: NULL query/output");
+  DeviceGuard g(ix->device);
+  std::lock_guard<std::mutex> lk(ix->mu);
+  mmr_status s = ensure_ws(ix, nq);
+  if (s != MMR_OK) return s;
+  hipStream_t st = mmr::as_stream(stream);
+  // |s32 - s64| <= delta; threshold margin 2*delta
+  const float two_delta = 2.0f * (float)(ix->Dp + 16) * 5.9604645e-8f;
+  const int64_t chunk = ix->ws_q;
+  for (int64_t c0 = 0; c0 < nq; c0 += chunk) {
+    const int64_t cq = nq - c0 < chunk ? nq - c0 : chunk;
+    const float* qc = q + c0 * ix->d;
+    int64_t Qp;
+    int wq, wn;
+    if (cq <= 64) { wq = 1; wn = 4; } else if (cq <= 128) { wq = 2; wn = 2; } else { wq = 4; wn = 1; }
+    Qp = round_up(cq, 64 * wq);
+    knn_prep_queries<<<dim3((unsigned)ceil_div(Qp, 4)), dim3(256), 0, st>>>(
+        qc, cq, ix->d, ix->qn, ix->Dp, Qp, ix->qnorm64);
+    MMR_LAUNCH_CHECK();
+    const int n_qblocks = (int)(Qp / (64 * wq));
+    const int n_gtiles = (int)ceil_div(ix->Np, 64 * wn);
+    const unsigned grid = (unsigned)(round_up(n_gtiles, 8) * n_qblocks);
+    if (wq == 1)
+      knn_scores<1, 4><<<grid, 256, 0, st>>>(ix->qn, ix->gal, ix->inv_norm, ix->scores, ix->Dp,
+                                              ix->Np, n_gtiles, n_qblocks);
+    else if (wq == 2)
+      knn_scores<2, 2><<<grid, 256, 0, st>>>(ix->qn, ix->gal, ix->inv_norm, ix->scores, ix->Dp,
+                                              ix->Np, n_gtiles, n_qblocks);
+    else
+      knn_scores<4, 1><<<grid, 256, 0, st>>>(ix->qn, ix->gal, ix->inv_norm, ix->scores, ix->Dp,
+                                              ix->Np, n_gtiles, n_qblocks);
+    MMR_LAUNCH_CHECK();
+    knn_select<<<dim3((unsigned)cq), dim3(kSelThreads), 0, st>>>(
+        ix->scores, ix->Np, ix->n, k, two_delta, qc, ix->d, ix->qnorm64, ix->gal, ix->Dp,
+        ix->norm64, ix->idx_base, out_idx + c0 * k, out_score ? out_score + c0 * k : nullptr,
+        out_score64 ? out_score64 + c0 * k : nullptr, out_status ? out_status + c0 : nullptr);
+    MMR_LAUNCH_CHECK();
+  }
+  return MMR_OK;
+}
+
+mmr_status mmr_merge_topk(const double* scores, const int64_t* idx, int32_t n_lists, int64_t nq,
+                          int32_t k_in, int32_t k_out, int64_t* out_idx, float* out_score,
+                          double* out_score64, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(n_lists >= 1 && k_in >= 1 && k_out >= 1 && nq >= 0, "mmr_merge_topk: bad sizes");
+  MMR_REQUIRE((int64_t)n_lists * k_in <= 4096, "mmr_merge_topk: n_lists*k_in > 4096");
+  if (nq == 0) return MMR_OK;
+  MMR_REQUIRE(scores && idx && out_idx, "mmr_merge_topk: NULL pointer");
+  const size_t lds = (sizeof(double) + sizeof(int64_t)) * (size_t)n_lists * k_in;
+  knn_merge<<<dim3((unsigned)nq), dim3(256), lds, mmr::as_stream(stream)>>>(
+      scores, idx, n_lists, nq, k_in, k_out, out_idx, out_score, out_score64);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+}  // extern "C"

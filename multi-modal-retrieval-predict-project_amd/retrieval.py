@@ -1,0 +1,200 @@
+"""Query interface — mirrors src/Retrieval/retrieval.py (RetrievalEngine ABC + make_retrieval_engine).
+
+RetrievalEngine            retrieval.py:18-50   (.npy f32 gallery + ids.json, id2idx, retrieve(), get_embeddings_for_ids())
+MI355XRetrievalEngine      exact brute-force cosine top-K on the GPU (libmmr, include/mmr.h) with
+                           the reference's exact-path semantics (retrieval_overlap.py:84-90):
+                           cosine of the raw rows, descending; ties -> lower gallery index.
+make_retrieval_engine      retrieval.py:273-304  (string switch; unknown method -> ValueError)
+
+The reference's default engine, DLS (retrieval.py:53-271), is an approximate random-seeded graph
+walk (3.75 % recall@10 vs exact in the survey probe) and is out of scope:
+method="dls" raises with a pointer to the exact engine.
+"""
+import abc
+import ctypes
+import json
+from typing import List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+class RetrievalEngine(abc.ABC):
+    """Loads embeddings once; id -> index map; abstract retrieve (retrieval.py:18-50)."""
+
+    def __init__(self, features_path: Optional[str], ids_path: Optional[str], embs=None, ids=None):
+        if embs is None:
+            embs = np.load(features_path)
+        self.embs = np.ascontiguousarray(np.asarray(embs).astype("float32"))  # (N, D)
+        if ids is None:
+            with open(ids_path, "r") as f:
+                ids = json.load(f)
+        self.ids = list(ids)
+        self.id2idx = {str(self.ids[i]): i for i in range(len(self.ids))}
+        assert self.embs.shape[0] == len(self.ids), "embeddings count != ids count"
+
+    @abc.abstractmethod
+    def retrieve(self, query_emb: np.ndarray, K: int = 5, **kwargs) -> Tuple[List[str], List[float]]:
+        """Given a query embedding (D,) or (1,D), return top-K IDs and their scores."""
+
+    def get_embeddings_for_ids(self, ids: List[str]) -> np.ndarray:
+        """Embeddings in the order of ids (zeros if missing) — retrieval.py:41-50."""
+        rows = []
+        for _id in ids:
+            idx = self.id2idx.get(str(_id), None)
+            rows.append(np.zeros(self.embs.shape[1], dtype=self.embs.dtype) if idx is None else self.embs[idx])
+        return np.vstack(rows)
+
+
+class GalleryIndex:
+    """Owning wrapper of an mmr_index (one device-resident gallery shard)."""
+
+    def __init__(self, embs, device=None, idx_base: int = 0):
+        _lib.require_gpu()
+        L = _lib.lib()
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = int(device)
+        if isinstance(embs, torch.Tensor):
+            src = embs.detach().to(torch.float32).contiguous()
+            is_host = 0 if src.is_cuda else 1
+            if src.is_cuda and src.device.index != self.device:
+                src = src.to(f"cuda:{self.device}")
+            n, d = src.shape
+            p = ctypes.c_void_p(src.data_ptr())
+            keep = src
+        else:
+            keep = np.ascontiguousarray(np.asarray(embs, dtype=np.float32))
+            n, d = keep.shape
+            is_host = 1
+            p = keep.ctypes.data_as(ctypes.c_void_p)
+        if not is_host:
+            torch.cuda.synchronize(self.device)  # the copy runs on the default stream
+        h = ctypes.c_void_p()
+        _lib.check(L.mmr_index_create(p, n, d, 0, is_host, idx_base, self.device, ctypes.byref(h)),
+                   "mmr_index_create")
+        del keep
+        self._h = h
+        self.n, self.d, self.idx_base = int(n), int(d), int(idx_base)
+
+    def reserve(self, max_q: int):
+        _lib.check(_lib.lib().mmr_index_reserve(self._h, int(max_q)), "mmr_index_reserve")
+
+    def search(self, q: torch.Tensor, k: int, want_f64: bool = False, want_status: bool = False):
+        """q (B, D) f32 device tensor -> (idx int64 (B,k), score f32 (B,k)[, score64][, status])."""
+        _lib.require_gpu(q)
+        if q.dim() != 2 or q.shape[1] != self.d:
+            raise ValueError(f"query shape {tuple(q.shape)} does not match gallery dim {self.d}")
+        if not 1 <= k <= _lib.lib().mmr_max_k():
+            raise ValueError(f"K={k} outside [1, {_lib.lib().mmr_max_k()}]")
+        q = q.to(torch.float32).contiguous()
+        B = q.shape[0]
+        dev = q.device
+        idx = torch.empty((B, k), dtype=torch.int64, device=dev)
+        sc = torch.empty((B, k), dtype=torch.float32, device=dev)
+        sc64 = torch.empty((B, k), dtype=torch.float64, device=dev) if want_f64 else None
+        st = torch.empty((B,), dtype=torch.int32, device=dev) if want_status else None
+        _lib.check(_lib.lib().mmr_index_search(self._h, _lib.ptr(q), B, k, _lib.ptr(idx), _lib.ptr(sc),
+                                               _lib.ptr(sc64), _lib.ptr(st), _lib.stream_ptr(dev)),
+                   "mmr_index_search")
+        out = [idx, sc]
+        if want_f64:
+            out.append(sc64)
+        if want_status:
+            out.append(st)
+        return tuple(out)
+
+    def close(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            _lib.lib().mmr_index_destroy(h)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def merge_topk(scores64: torch.Tensor, idx: torch.Tensor, k_out: int):
+    """[L][B][k_in] f64 scores + int64 idx (-1 = empty) -> global top-k_out (idx, f32, f64) on device."""
+    _lib.require_gpu(scores64)
+    L_, B, k_in = idx.shape
+    dev = idx.device
+    oi = torch.empty((B, k_out), dtype=torch.int64, device=dev)
+    os_ = torch.empty((B, k_out), dtype=torch.float32, device=dev)
+    o64 = torch.empty((B, k_out), dtype=torch.float64, device=dev)
+    _lib.check(_lib.lib().mmr_merge_topk(_lib.ptr(scores64.contiguous()), _lib.ptr(idx.contiguous()), L_, B,
+                                         k_in, k_out, _lib.ptr(oi), _lib.ptr(os_), _lib.ptr(o64),
+                                         _lib.stream_ptr(dev)), "mmr_merge_topk")
+    return oi, os_, o64
+
+
+class MI355XRetrievalEngine(RetrievalEngine):
+    """Exact batched-cosine top-K on one MI355X (the brute-force path of retrieval_overlap.py:84-90)."""
+
+    def __init__(self, features_path: Optional[str] = None, ids_path: Optional[str] = None,
+                 device=None, dtype: str = "fp32", embs=None, ids=None, **_ignored):
+        super().__init__(features_path, ids_path, embs=embs, ids=ids)
+        if dtype != "fp32":
+            raise ValueError(f"gallery dtype {dtype!r} not built in this round (fp32 only)")
+        self.index = GalleryIndex(self.embs, device=device)
+        self.device = self.index.device
+
+    def search(self, Q, K: int = 10, check: bool = True):
+        """Batched top-K. Q: (B,D) numpy or torch. Returns (idx (B,K') int64, scores (B,K') f32) with
+        K' = min(K, N), as torch device tensors for torch input, numpy otherwise."""
+        is_np = not isinstance(Q, torch.Tensor)
+        q = torch.as_tensor(np.asarray(Q, np.float32) if is_np else Q)
+        if q.dim() == 1:
+            q = q[None]
+        q = q.to(f"cuda:{self.device}", torch.float32)
+        k_eff = min(int(K), len(self.ids))
+        if k_eff <= 0:
+            e = torch.empty((q.shape[0], 0))
+            return (e.long().numpy(), e.numpy()) if is_np else (e.long(), e)
+        idx, sc, st = self.index.search(q, k_eff, want_status=True)
+        if check and int(st.max().item() if st.numel() else 0) != 0:
+            raise RuntimeError("candidate buffer overflow in mmr_index_search (massively tied scores)")
+        if is_np:
+            return idx.cpu().numpy(), sc.cpu().numpy()
+        return idx, sc
+
+    def retrieve(self, query_emb, K: int = 5, reranker=None, query_id=None, rerank_topk=None, **kwargs):
+        """(D,) or (1,D) query -> (top-K ids, scores) descending (retrieval.py:34-39 contract).
+        With a reranker and query_id, candidates are re-scored like retrieval.py:256-269."""
+        q = np.asarray(query_emb, dtype=np.float32).reshape(1, -1)
+        idx, sc = self.search(q, K)
+        ids = [self.ids[i] for i in idx[0].tolist()]
+        scores = [float(s) for s in sc[0].tolist()]
+        if reranker is not None and query_id is not None:
+            cand_embs = self.get_embeddings_for_ids(ids)
+            lookup = {str(r): e for r, e in zip(ids, cand_embs)}
+            lookup[str(query_id)] = (self.embs[self.id2idx[str(query_id)]]
+                                     if str(query_id) in self.id2idx else q.reshape(-1))
+            reranked = reranker.rerank(query_id=query_id, candidate_ids=ids, candidate_embs=cand_embs,
+                                       candidate_emb_lookup=lookup, topk=rerank_topk or K)
+            ids = [t[0] for t in reranked]
+            scores = [t[1] for t in reranked]
+        return ids, scores
+
+    def close(self):
+        self.index.close()
+
+
+def make_retrieval_engine(features_path: str, ids_path: str, method: str = "mi355x", **kwargs) -> RetrievalEngine:
+    """Factory (retrieval.py:273-304). method: "mi355x" (aliases "exact", "brute") -> exact GPU
+    engine; "mi355x_sharded" -> row-sharded over torch.distributed ranks; "dls" -> not provided."""
+    method = method.lower()
+    if method in ("mi355x", "exact", "brute", "bruteforce"):
+        return MI355XRetrievalEngine(features_path, ids_path, device=kwargs.get("device"),
+                                     dtype=kwargs.get("dtype", "fp32"))
+    if method in ("mi355x_sharded", "sharded"):
+        from .parallel import ShardedRetrievalEngine
+        return ShardedRetrievalEngine(features_path, ids_path, dtype=kwargs.get("dtype", "fp32"))
+    if method == "dls":
+        raise ValueError("method 'dls' (approximate graph walk, retrieval.py:53-271) is not provided by "
+                         "mmr_amd; use method='mi355x' for exact brute-force retrieval")
+    raise ValueError(f"Unknown retrieval method: {method}")

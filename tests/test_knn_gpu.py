@@ -1,0 +1,135 @@
+"""GPU parity: libmmr batched-cosine top-K (mmr_index_search / mmr_merge_topk through the C ABI)
+against the oracle (exact f64, bit-exact indices) and the reference's sklearn vectors (golden,
+tie-aware).  Tolerances: indices bit-exact vs the exact oracle; scores within 1e-4 of sklearn and
+within 1e-6 of the exact f64 scores (they are f64 rounded to f32)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from mmr_amd import metrics, synthetic
+from mmr_amd.retrieval import GalleryIndex, MI355XRetrievalEngine, merge_topk
+from oracle import knn as oknn
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _search(G, Q, K, **kw):
+    ix = GalleryIndex(G, **kw)
+    q = torch.from_numpy(np.ascontiguousarray(Q, np.float32)).cuda()
+    i, s, s64, st = ix.search(q, K, want_f64=True, want_status=True)
+    torch.cuda.synchronize()
+    ix.close()
+    return i.cpu().numpy(), s.cpu().numpy(), s64.cpu().numpy(), st.cpu().numpy()
+
+
+def _exact_check(G, Q, K):
+    gi, gs, g64, st = _search(G, Q, K)
+    assert (st == 0).all()
+    ei, es = oknn.exact_topk(Q, G, K)
+    kk = ei.shape[1]
+    np.testing.assert_array_equal(gi[:, :kk], ei)
+    np.testing.assert_allclose(g64[:, :kk], es, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(gs[:, :kk], es.astype(np.float32), rtol=0, atol=0)
+    if kk < K:
+        assert (gi[:, kk:] == -1).all() and np.isneginf(gs[:, kk:]).all()
+    return gi, gs
+
+
+@pytest.mark.parametrize("name", ["knn_gauss_1k", "knn_gauss_10k", "knn_labelled_2k"])
+def test_knn_matches_reference_golden(name):
+    f = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    N, D, Q, seed, kind = int(f["N"]), int(f["D"]), int(f["Q"]), int(f["seed"]), str(f["kind"])
+    if kind == "gauss":
+        G, Qm = synthetic.gauss_gallery(N, D, seed), synthetic.gauss_gallery(Q, D, seed + 1)
+    else:
+        G, _ = synthetic.labelled_gallery(N, D, seed)
+        Qm, _ = synthetic.labelled_gallery(Q, D, seed + 1)
+        G[f["zero_rows"]] = 0.0
+    for key in f.files:
+        if key.startswith("idx_k"):
+            K = int(key[5:])
+            gi, gs = _exact_check(G, Qm, K)
+            ok, msg = oknn.topk_equivalent(f[key], f[f"score_k{K}"], gi, gs, tie_tol=1e-6, score_tol=1e-4)
+            assert ok, msg
+
+
+@pytest.mark.parametrize("N,D,Q,K", [(1, 8, 3, 5), (7, 100, 1, 10), (300, 64, 65, 256), (1000, 1024, 129, 50),
+                                     (5000, 768, 300, 10), (257, 24, 2, 1)])
+def test_knn_shapes_and_edges(N, D, Q, K):
+    rng = np.random.default_rng(N + D + Q + K)
+    G = rng.standard_normal((N, D), dtype=np.float32)
+    Qm = rng.standard_normal((Q, D), dtype=np.float32)
+    _exact_check(G, Qm, K)
+
+
+def test_knn_ties_zero_rows_and_duplicates():
+    rng = np.random.default_rng(5)
+    G = rng.standard_normal((2000, 128), dtype=np.float32)
+    G[100:110] = G[50]          # exact duplicates -> equal scores -> index order
+    G[200:205] = 0.0            # zero rows -> score 0
+    Qm = np.concatenate([G[50:51] * 3.0, np.zeros((1, 128), np.float32),
+                         -G[60:61], rng.standard_normal((5, 128), dtype=np.float32)])
+    gi, gs = _exact_check(G, Qm, 20)
+    assert gi[0, :11].tolist() == [50] + list(range(100, 110))
+    assert gi[1].tolist() == list(range(20))  # zero query: every score 0 -> lowest indices
+
+
+def test_knn_negative_scores_and_clustered():
+    G, _ = synthetic.labelled_gallery(4000, 256, 11)
+    G = -np.abs(G)                       # many negative cosines
+    Qm = np.abs(synthetic.gauss_gallery(40, 256, 12))
+    _exact_check(G, Qm, 64)
+
+
+def test_knn_100k_full_size_exact():
+    G = synthetic.gauss_gallery(100_000, 768, synthetic.SEED)
+    Qm = synthetic.gauss_gallery(256, 768, synthetic.SEED + 1)
+    _exact_check(G, Qm, 10)
+
+
+def test_shard_merge_equals_single_index():
+    G, _ = synthetic.labelled_gallery(6000, 192, 21)
+    Qm, _ = synthetic.labelled_gallery(70, 192, 22)
+    K = 10
+    si, ss, s64, _ = _search(G, Qm, K)
+    bounds = [0, 1000, 1001, 4000, 6000]   # ragged shards, one with a single row (< K)
+    idxs, scs = [], []
+    q = torch.from_numpy(Qm).cuda()
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        ix = GalleryIndex(G[a:b], idx_base=a)
+        i, s, sd = ix.search(q, K, want_f64=True)
+        idxs.append(i)
+        scs.append(sd)
+    mi, ms, m64 = merge_topk(torch.stack(scs), torch.stack(idxs), K)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(mi.cpu().numpy(), si)
+    np.testing.assert_array_equal(m64.cpu().numpy(), s64)
+
+
+def test_engine_retrieve_contract_and_precision_at_10(tmp_path):
+    G, gl = synthetic.labelled_gallery(3000, 768, 31)
+    Qm, ql = synthetic.labelled_gallery(64, 768, 32)
+    ids = [f"case{i}" for i in range(len(G))]
+    np.save(tmp_path / "g.npy", G)
+    (tmp_path / "ids.json").write_text(__import__("json").dumps(ids))
+    from mmr_amd import make_retrieval_engine
+    eng = make_retrieval_engine(str(tmp_path / "g.npy"), str(tmp_path / "ids.json"), method="mi355x")
+    r_ids, r_scores = eng.retrieve(Qm[0], K=5)
+    assert len(r_ids) == 5 and all(isinstance(x, str) for x in r_ids)
+    assert r_scores == sorted(r_scores, reverse=True)
+    gi, gs = eng.search(Qm, K=10)
+    si, ss = oknn.sklearn_topk(Qm, G, 10)
+    qb, gb = synthetic.labels_to_bits(ql), synthetic.labels_to_bits(gl)
+    # identical P@10 / R@10 to the reference's sklearn ranking
+    for k in (1, 5, 10):
+        assert metrics.ranking_metrics(gi, qb, gb, k)[1:] == metrics.ranking_metrics(si, qb, gb, k)[1:]
+    p_ref = [metrics.precision_at_k([ids[j] for j in si[q]], [ids[j] for j in np.nonzero(gb & qb[q])[0]], 10)
+             for q in range(len(Qm))]
+    p_got = [metrics.precision_at_k([ids[j] for j in gi[q]], [ids[j] for j in np.nonzero(gb & qb[q])[0]], 10)
+             for q in range(len(Qm))]
+    assert p_ref == p_got
+    eng.close()
