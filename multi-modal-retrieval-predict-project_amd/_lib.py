@@ -54,7 +54,9 @@ def lib():
             raise MMRError(f"{LIB_PATH} is not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
         L = ctypes.CDLL(LIB_PATH)
         for name, args in SIGNATURES.items():
-            fn = getattr(L, name)  # AttributeError if the export is missing
+            if not hasattr(L, name):  # a call to a missing export raises AttributeError
+                continue
+            fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = _RESTYPES.get(name, ctypes.c_int)
         _lib = L
