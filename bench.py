@@ -69,7 +69,7 @@ def main():
     n, d, K, B = a.gallery, a.dim, a.k, a.batch
     G = synthetic.gauss_gallery(n, d, synthetic.SEED + 17 * rank)
     index = GalleryIndex(G, device=local, idx_base=rank * n)
-    index.reserve(B * world)
+    index.reserve(2 * B * world)
 
     model = None
     if a.mode == "full":
@@ -90,7 +90,7 @@ def main():
         else:
             q = qbatch
         if world > 1:
-            allq = torch.empty((world * B, d), dtype=torch.float32, device=dev)
+            allq = torch.empty((world * q.shape[0], d), dtype=torch.float32, device=dev)
             dist.all_gather_into_tensor(allq, q.contiguous())
         else:
             allq = q
@@ -131,10 +131,11 @@ def main():
 
     # whole-job throughput: every rank embeds B queries; every query is scored against the whole
     # world*n gallery (each rank scores all world*B queries against its n rows)
+    nq_step = (2 * B) if model is not None else B   # full mode: image-head + text-head queries
     q_per_s = world * B * a.steps / elapsed
-    pairs_per_s = (world * B) * (world * n) * a.steps / elapsed
+    pairs_per_s = (world * nq_step) * (world * n) * a.steps / elapsed
     # roofline of the kNN search (dominant kernel of the knn mode): per launch on one GPU
-    Qs = world * B
+    Qs = world * nq_step
     flops = 2.0 * Qs * n * d
     bytes_ = n * d * 4 + n * 4 + Qs * d * 4 + Qs * K * 12
     t_s = ms_search / 1e3

@@ -1,0 +1,746 @@
+// Tower kernels for the Swin-Tiny image tower and the ClinicalBERT text tower (gfx950), plus the
+// pooling / projection heads.  GEMM-shaped work is in gemm.hip (mmr_linear_bf16); this file holds
+// the attention cores (MFMA, LDS-staged), LayerNorms, gathers and the heads.
+//
+// Reference (semantics): timm SwinTransformer.forward_features (fusion.py:198-199), HF BertModel
+// last_hidden_state (fusion.py:322-325), Backbones.forward pooling (fusion.py:259-265),
+// MultiModalRetrievalModel heads (model.py:365-373, 462-479), MultiHeadMLP (model.py:61-75).
+#include <float.h>
+#include <math.h>
+
+#include "common.h"
+
+namespace {
+
+using mmr::bf2f;
+using mmr::f2bf;
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ void load8(const uint16_t* p, float* v) {
+  bf16x8 x = *(const bf16x8*)p;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = bf2f((uint16_t)x[j]);
+}
+__device__ __forceinline__ void store8(uint16_t* p, const float* v) {
+  bf16x8 x;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = (short)f2bf(v[j]);
+  *(bf16x8*)p = x;
+}
+
+// ------------------------------------------------------------------ LayerNorm (one wave per row)
+// Two passes over the row (mean, then centred variance — torch's biased variance), re-reads hit
+// L1/L2.  Rows of c channels, c % 8 == 0.
+__global__ __launch_bounds__(256) void layernorm_bf16(const uint16_t* __restrict__ x,
+                                                      const float* __restrict__ g,
+                                                      const float* __restrict__ b,
+                                                      uint16_t* __restrict__ y, int64_t rows,
+                                                      int c, float eps) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const uint16_t* xr = x + row * c;
+  float s = 0.f;
+  for (int k = lane * 8; k < c; k += 512) {
+    float v[8];
+    load8(xr + k, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[j];
+  }
+  const float mean = mmr::wave_sum(s) / c;
+  float ss = 0.f;
+  for (int k = lane * 8; k < c; k += 512) {
+    float v[8];
+    load8(xr + k, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += (v[j] - mean) * (v[j] - mean);
+  }
+  const float rstd = rsqrtf(mmr::wave_sum(ss) / c + eps);
+  for (int k = lane * 8; k < c; k += 512) {
+    float v[8];
+    load8(xr + k, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (v[j] - mean) * rstd * g[k + j] + b[k + j];
+    store8(y + row * c + k, v);
+  }
+}
+
+// ------------------------------------------------------------------ BERT embeddings + LN
+__global__ __launch_bounds__(256) void bert_embed(const int64_t* __restrict__ ids,
+                                                  const float* __restrict__ word,
+                                                  const float* __restrict__ pos,
+                                                  const float* __restrict__ type0,
+                                                  const float* __restrict__ g,
+                                                  const float* __restrict__ b,
+                                                  uint16_t* __restrict__ y, int64_t ntok, int l,
+                                                  int c, float eps) {
+  const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (tok >= ntok) return;
+  const int p = (int)(tok % l);
+  const float* wr = word + ids[tok] * (int64_t)c;
+  const float* pr = pos + (int64_t)p * c;
+  float s = 0.f;
+  for (int k = lane; k < c; k += 64) s += wr[k] + pr[k] + type0[k];
+  const float mean = mmr::wave_sum(s) / c;
+  float ss = 0.f;
+  for (int k = lane; k < c; k += 64) {
+    float v = wr[k] + pr[k] + type0[k] - mean;
+    ss += v * v;
+  }
+  const float rstd = rsqrtf(mmr::wave_sum(ss) / c + eps);
+  for (int k = lane; k < c; k += 64)
+    y[tok * c + k] = f2bf((wr[k] + pr[k] + type0[k] - mean) * rstd * g[k] + b[k]);
+}
+
+// ------------------------------------------------------------------ BERT self-attention core
+// Block = (batch, head), 4 waves; each wave owns 32-query tiles.  Swapped product S^T = K . Q^T
+// with v_mfma_f32_32x32x16_bf16 puts the query on the lane and the keys in the registers, so the
+// softmax row reductions are in-register + one lane^32 exchange, and P^T feeds the P.V MFMA as
+// its B operand with no data movement (cdna_hip_programming.md §3).  K is staged in LDS as
+// 128-B rows (swizzled 16-B chunks), V transposed as [d][key] rows padded by 8 B (conflict-free
+// ds_read_b64).  Keys are processed in blocks of 128 with an online softmax (L <= 512).
+constexpr int BA_DH = 64;
+constexpr int BA_KBLK = 128;
+
+__device__ __forceinline__ int kswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+__global__ __launch_bounds__(256) void bert_attention(const uint16_t* __restrict__ qkv,
+                                                      const int64_t* __restrict__ mask01,
+                                                      uint16_t* __restrict__ ctx, int l, int h) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int C = h * BA_DH;
+  const int bi = blockIdx.x / h, hh = blockIdx.x % h;
+  const int vt_stride = l + 4;  // bf16 elements per V^T row (l*2 + 8 bytes)
+  uint16_t* Ks = (uint16_t*)smem;                 // [l][64]
+  uint16_t* Vt = Ks + (size_t)l * BA_DH;          // [64][l+4]
+  float* madd = (float*)(Vt + (size_t)BA_DH * vt_stride);  // [l] additive mask
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint16_t* base = qkv + (int64_t)bi * l * 3 * C;
+
+  // stage K (swizzled rows) and V^T
+  for (int c = tid; c < l * 8; c += 256) {
+    const int key = c >> 3, ch = c & 7;
+    const uint16_t* src = base + (int64_t)key * 3 * C + hh * BA_DH;
+    *(bf16x8*)(Ks + key * BA_DH + kswz(key, ch) * 8) = *(const bf16x8*)(src + C + ch * 8);
+    bf16x8 v = *(const bf16x8*)(src + 2 * C + ch * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Vt[(ch * 8 + j) * vt_stride + key] = (uint16_t)v[j];
+  }
+  for (int k = tid; k < l; k += 256) madd[k] = mask01[(int64_t)bi * l + k] ? 0.0f : -FLT_MAX;
+  __syncthreads();
+
+  const float scale = 0.125f;  // 1/sqrt(64)
+  const int r = lane & 31, hf = lane >> 5;
+  for (int qt = wave; qt < l / 32; qt += 4) {
+    const int q = qt * 32 + r;
+    const uint16_t* qrow = base + (int64_t)q * 3 * C + hh * BA_DH;
+    bf16x8 qf[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qf[ks] = *(const bf16x8*)(qrow + ks * 16 + 8 * hf);
+    f32x16 o0 = {0}, o1 = {0};
+    float m_run = -FLT_MAX, l_run = 0.f;
+    for (int kb = 0; kb < l; kb += BA_KBLK) {
+      const int nt = min(BA_KBLK, l - kb) / 32;
+      f32x16 s[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        s[t] = (f32x16){0};
+        if (t < nt) {
+          const int key = kb + t * 32 + r;
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) {
+            const bf16x8 kf = *(const bf16x8*)(Ks + key * BA_DH + kswz(key, ks * 2 + hf) * 8);
+            s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[t], 0, 0, 0);
+          }
+        }
+      }
+      // scale + mask, block max
+      float mloc = -FLT_MAX;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (t < nt) {
+#pragma unroll
+          for (int rg = 0; rg < 16; ++rg) {
+            const int key = kb + t * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * hf;
+            const float v = s[t][rg] * scale + madd[key];
+            s[t][rg] = v;
+            mloc = fmaxf(mloc, v);
+          }
+        }
+      }
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      const float m_new = fmaxf(m_run, mloc);
+      const float alpha = __expf(m_run - m_new);
+      m_run = m_new;
+      float psum = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (t < nt) {
+#pragma unroll
+          for (int rg = 0; rg < 16; ++rg) {
+            const float p = __expf(s[t][rg] - m_new);
+            s[t][rg] = p;
+            psum += p;
+          }
+        }
+      }
+      l_run = l_run * alpha + psum;
+#pragma unroll
+      for (int rg = 0; rg < 16; ++rg) {
+        o0[rg] *= alpha;
+        o1[rg] *= alpha;
+      }
+      // O^T[d][q] += V^T[d][key] . P^T[key][q]
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (t < nt) {
+#pragma unroll
+          for (int sidx = 0; sidx < 2; ++sidx) {
+            bf16x8 pf;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pf[j] = (short)f2bf(s[t][8 * sidx + j]);
+            const int kbase = kb + t * 32 + 16 * sidx + 4 * hf;
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt) {
+              const uint16_t* vrow = Vt + (dt * 32 + r) * vt_stride;
+              const bf16x4 lo = *(const bf16x4*)(vrow + kbase);
+              const bf16x4 hi = *(const bf16x4*)(vrow + kbase + 8);
+              const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+              if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o0, 0, 0, 0);
+              else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o1, 0, 0, 0);
+            }
+          }
+        }
+      }
+    }
+    const float inv = 1.0f / (l_run + __shfl_xor(l_run, 32, 64));
+    uint16_t* orow = ctx + ((int64_t)bi * l + q) * C + hh * BA_DH;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = 8 * g4 + 4 * hf;
+      bf16x4 w0, w1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        w0[j] = (short)f2bf(o0[4 * g4 + j] * inv);
+        w1[j] = (short)f2bf(o1[4 * g4 + j] * inv);
+      }
+      *(bf16x4*)(orow + d) = w0;
+      *(bf16x4*)(orow + 32 + d) = w1;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ Swin (shifted) window attention
+// One wave per (image, window, head); 4 units per block.  Window of ws*ws = 49 tokens padded to
+// 64, head_dim 32.  The cyclic shift + window partition are folded into the token gather (and
+// the reverse shift into the scatter of the output): rolled coordinate (hr, wr) reads token
+// ((hr+shift)%H, (wr+shift)%W).  S^T = K . Q^T (2x2 tiles of 32x32x16, 2 k-steps), + relative
+// position bias table[(yi-yj+ws-1)*(2ws-1) + (xi-xj+ws-1)][head] + shift-region mask (-100),
+// softmax over keys in registers, O^T = V^T . P^T with V^T staged per wave in LDS.
+constexpr int SW_DH = 32;
+
+__device__ __forceinline__ int region_of(int rc, int H, int ws, int shift) {
+  return rc < H - ws ? 0 : (rc < H - shift ? 1 : 2);
+}
+
+__global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __restrict__ qkv,
+                                                             const float* __restrict__ table,
+                                                             uint16_t* __restrict__ out,
+                                                             int64_t units, int H, int C,
+                                                             int heads, int ws, int shift) {
+  __shared__ __attribute__((aligned(16))) uint16_t vt_all[4][SW_DH][64 + 4];
+  __shared__ int tok_all[4][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t unit = (int64_t)blockIdx.x * 4 + wave;
+  const bool active = unit < units;
+  const int nwin1 = H / ws;
+  const int64_t u = active ? unit : 0;
+  const int hh = (int)(u % heads);
+  const int64_t wi = u / heads;
+  const int win = (int)(wi % (nwin1 * nwin1));
+  const int64_t bi = wi / (nwin1 * nwin1);
+  const int wy = win / nwin1, wx = win % nwin1;
+  const int N = ws * ws;
+  uint16_t(*vt)[64 + 4] = vt_all[wave];
+  int* tok = tok_all[wave];
+  // token of local index i (padded entries -> -1)
+  {
+    const int i = lane;
+    int t = -1;
+    if (i < N) {
+      const int hr = wy * ws + i / ws, wr = wx * ws + i % ws;
+      const int h0 = (hr + shift) % H, w0 = (wr + shift) % H;
+      t = (int)(bi * H * H + h0 * H + w0);
+    }
+    tok[i] = t;
+  }
+  __builtin_amdgcn_wave_barrier();
+  // V^T staging: 64 keys x 32 d = 256 chunks of 8 -> 4 per lane
+  for (int c = lane; c < 256; c += 64) {
+    const int key = c >> 2, ch = c & 3;
+    const int t = tok[key];
+    bf16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (active && t >= 0) v = *(const bf16x8*)(qkv + (int64_t)t * 3 * C + 2 * C + hh * SW_DH + ch * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vt[ch * 8 + j][key] = (uint16_t)v[j];
+  }
+  __syncthreads();
+  if (!active) return;
+
+  const int r = lane & 31, hf = lane >> 5;
+  const float scale = 0.17677669529663687f;  // 32^-0.5
+  // Q fragments (B operand) for the two query tiles, K fragments (A operand) for two key tiles
+  bf16x8 qf[2][2], kf[2][2];
+#pragma unroll
+  for (int t2 = 0; t2 < 2; ++t2) {
+    const int tq = tok[t2 * 32 + r];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+      qf[t2][ks] = tq >= 0 ? *(const bf16x8*)(qkv + (int64_t)tq * 3 * C + hh * SW_DH + ks * 16 + 8 * hf) : z;
+      kf[t2][ks] = tq >= 0 ? *(const bf16x8*)(qkv + (int64_t)tq * 3 * C + C + hh * SW_DH + ks * 16 + 8 * hf) : z;
+    }
+  }
+  const int tsz = 2 * ws - 1;
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qi = qt * 32 + r;  // this lane's query (local index)
+    const bool qvalid = qi < N;
+    const int qy = qi / ws, qx = qi % ws;
+    int qreg = 0;
+    if (shift > 0 && qvalid)
+      qreg = region_of(wy * ws + qy, H, ws, shift) * 3 + region_of(wx * ws + qx, H, ws, shift);
+    f32x16 s[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      s[kt] = (f32x16){0};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kt][ks], qf[qt][ks], s[kt], 0, 0, 0);
+    }
+    float mloc = -FLT_MAX;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int rg = 0; rg < 16; ++rg) {
+        const int kj = kt * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * hf;
+        float v = -FLT_MAX;
+        if (kj < N && qvalid) {
+          const int ky = kj / ws, kx = kj % ws;
+          v = s[kt][rg] * scale + table[((qy - ky + ws - 1) * tsz + (qx - kx + ws - 1)) * heads + hh];
+          if (shift > 0) {
+            const int kreg = region_of(wy * ws + ky, H, ws, shift) * 3 + region_of(wx * ws + kx, H, ws, shift);
+            if (kreg != qreg) v += -100.0f;
+          }
+        }
+        s[kt][rg] = v;
+        mloc = fmaxf(mloc, v);
+      }
+    }
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    float psum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int rg = 0; rg < 16; ++rg) {
+        const int kj = kt * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * hf;
+        const float p = kj < N ? __expf(s[kt][rg] - mloc) : 0.0f;
+        s[kt][rg] = p;
+        psum += p;
+      }
+    }
+    psum += __shfl_xor(psum, 32, 64);
+    f32x16 o = {0};
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int sidx = 0; sidx < 2; ++sidx) {
+        bf16x8 pf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[j] = (short)f2bf(s[kt][8 * sidx + j]);
+        const int kbase = kt * 32 + 16 * sidx + 4 * hf;
+        const bf16x4 lo = *(const bf16x4*)(&vt[r][kbase]);
+        const bf16x4 hi = *(const bf16x4*)(&vt[r][kbase + 8]);
+        const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o, 0, 0, 0);
+      }
+    }
+    if (qvalid) {
+      const float inv = 1.0f / psum;
+      uint16_t* orow = out + (int64_t)tok[qi] * C + hh * SW_DH;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        bf16x4 w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = (short)f2bf(o[4 * g4 + j] * inv);
+        *(bf16x4*)(orow + 8 * g4 + 4 * hf) = w;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ patch embed im2col (K padded to 64)
+__global__ __launch_bounds__(256) void patch_im2col(const float* __restrict__ img,
+                                                    uint16_t* __restrict__ cols, int64_t ntok,
+                                                    int cin, int hw, int patch) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (token, 8-chunk)
+  const int kp = 64;
+  if (idx >= ntok * (kp / 8)) return;
+  const int64_t t = idx / 8;
+  const int ch = (int)(idx % 8);
+  const int g = hw / patch;
+  const int64_t bi = t / (g * g);
+  const int py = (int)((t / g) % g), px = (int)(t % g);
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = ch * 8 + j;  // k = c*16 + ky*4 + kx
+    float val = 0.f;
+    if (k < cin * patch * patch) {
+      const int c = k / (patch * patch), ky = (k / patch) % patch, kx = k % patch;
+      val = img[((bi * cin + c) * hw + (py * patch + ky)) * (int64_t)hw + px * patch + kx];
+    }
+    v[j] = val;
+  }
+  store8(cols + t * kp + ch * 8, v);
+}
+
+// ------------------------------------------------------------------ PatchMerging gather + LN(4c)
+__global__ __launch_bounds__(256) void patch_merge_ln(const uint16_t* __restrict__ x,
+                                                      const float* __restrict__ g,
+                                                      const float* __restrict__ b,
+                                                      uint16_t* __restrict__ y, int64_t nout,
+                                                      int hw, int c, float eps) {
+  const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (o >= nout) return;
+  const int h2 = hw / 2;
+  const int64_t bi = o / (h2 * h2);
+  const int i = (int)((o / h2) % h2), j = (int)(o % h2);
+  const int c4 = 4 * c;
+  // part p: (dy, dx) = (p&1, p>>1)  -> [x(2i,2j), x(2i+1,2j), x(2i,2j+1), x(2i+1,2j+1)]
+  auto src = [&](int k) -> const uint16_t* {
+    const int p = k / c, off = k % c;
+    const int yy = 2 * i + (p & 1), xx = 2 * j + (p >> 1);
+    return x + ((bi * hw + yy) * hw + xx) * (int64_t)c + off;
+  };
+  float s = 0.f;
+  for (int k = lane * 8; k < c4; k += 512) {
+    float v[8];
+    load8(src(k), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += v[e];
+  }
+  const float mean = mmr::wave_sum(s) / c4;
+  float ss = 0.f;
+  for (int k = lane * 8; k < c4; k += 512) {
+    float v[8];
+    load8(src(k), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ss += (v[e] - mean) * (v[e] - mean);
+  }
+  const float rstd = rsqrtf(mmr::wave_sum(ss) / c4 + eps);
+  for (int k = lane * 8; k < c4; k += 512) {
+    float v[8];
+    load8(src(k), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (v[e] - mean) * rstd * g[k + e] + b[k + e];
+    store8(y + o * c4 + k, v);
+  }
+}
+
+// ------------------------------------------------------------------ Swin head: LN, LN(LN), means
+constexpr int SH_MAXPL = 16;  // c <= 1024, c % 64 == 0
+__global__ __launch_bounds__(256) void swin_head(const uint16_t* __restrict__ x,
+                                                 const float* __restrict__ g,
+                                                 const float* __restrict__ b,
+                                                 float* __restrict__ patches,
+                                                 float* __restrict__ glob,
+                                                 float* __restrict__ pool, int t, int c,
+                                                 float eps) {
+  __shared__ float part[4][2][1024];
+  const int bi = blockIdx.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int per = c / 64;
+  float acc1[SH_MAXPL], acc2[SH_MAXPL];
+#pragma unroll
+  for (int e = 0; e < SH_MAXPL; ++e) acc1[e] = acc2[e] = 0.f;
+  for (int tk = wave; tk < t; tk += 4) {
+    const uint16_t* xr = x + ((int64_t)bi * t + tk) * c;
+    float v[SH_MAXPL];
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < SH_MAXPL; ++e)
+      if (e < per) {
+        v[e] = bf2f(xr[lane + 64 * e]);
+        s += v[e];
+      }
+    float mean = mmr::wave_sum(s) / c, ss = 0.f;
+#pragma unroll
+    for (int e = 0; e < SH_MAXPL; ++e)
+      if (e < per) ss += (v[e] - mean) * (v[e] - mean);
+    float rstd = rsqrtf(mmr::wave_sum(ss) / c + eps);
+    s = 0.f;
+#pragma unroll
+    for (int e = 0; e < SH_MAXPL; ++e)
+      if (e < per) {
+        const int k = lane + 64 * e;
+        v[e] = (v[e] - mean) * rstd * g[k] + b[k];  // once-normed token (forward_features output)
+        acc1[e] += v[e];
+        s += v[e];
+      }
+    mean = mmr::wave_sum(s) / c;
+    ss = 0.f;
+#pragma unroll
+    for (int e = 0; e < SH_MAXPL; ++e)
+      if (e < per) ss += (v[e] - mean) * (v[e] - mean);
+    rstd = rsqrtf(mmr::wave_sum(ss) / c + eps);
+#pragma unroll
+    for (int e = 0; e < SH_MAXPL; ++e)
+      if (e < per) {
+        const int k = lane + 64 * e;
+        const float p2 = (v[e] - mean) * rstd * g[k] + b[k];  // swin_norm applied again
+        acc2[e] += p2;
+        if (patches) patches[((int64_t)bi * t + tk) * c + k] = p2;
+      }
+  }
+#pragma unroll
+  for (int e = 0; e < SH_MAXPL; ++e)
+    if (e < per) {
+      part[wave][0][lane + 64 * e] = acc1[e];
+      part[wave][1][lane + 64 * e] = acc2[e];
+    }
+  __syncthreads();
+  for (int k = threadIdx.x; k < c; k += 256) {
+    const float s1 = part[0][0][k] + part[1][0][k] + part[2][0][k] + part[3][0][k];
+    const float s2 = part[0][1][k] + part[1][1][k] + part[2][1][k] + part[3][1][k];
+    const float gm = s1 / t;
+    if (glob) glob[(int64_t)bi * c + k] = gm;
+    if (pool) pool[(int64_t)bi * c + k] = (gm + s2) / (t + 1);
+  }
+}
+
+// ------------------------------------------------------------------ unmasked token mean
+__global__ __launch_bounds__(256) void mean_tokens(const uint16_t* __restrict__ x,
+                                                   float* __restrict__ y, int l, int c) {
+  const int bi = blockIdx.y;
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= c) return;
+  const uint16_t* xr = x + (int64_t)bi * l * c + k;
+  float s = 0.f;
+  for (int t = 0; t < l; ++t) s += bf2f(xr[(int64_t)t * c]);
+  y[(int64_t)bi * c + k] = s / l;
+}
+
+// ------------------------------------------------------------------ small f32 linear (heads)
+// Y[b][o] = act(sum_i X[b][i] W[o][i] + bias[o]); 64x64 output tile, 16-deep K slabs in LDS,
+// 4x4 outputs per thread.  The heads are ~1 MFLOP per query: latency, not throughput, matters.
+__global__ __launch_bounds__(256) void linear_f32(const float* __restrict__ X,
+                                                  const float* __restrict__ W,
+                                                  const float* __restrict__ bias,
+                                                  float* __restrict__ Y, int nb, int cin, int cout,
+                                                  int act) {
+  __shared__ float xs[16][64 + 1], ws_[16][64 + 1];
+  const int b0 = blockIdx.y * 64, o0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  float acc[4][4] = {};
+  for (int k0 = 0; k0 < cin; k0 += 16) {
+    for (int e = threadIdx.x; e < 16 * 64; e += 256) {
+      const int kk = e & 15, rr = e >> 4;
+      const int k = k0 + kk;
+      xs[kk][rr] = (b0 + rr < nb && k < cin) ? X[(int64_t)(b0 + rr) * cin + k] : 0.f;
+      ws_[kk][rr] = (o0 + rr < cout && k < cin) ? W[(int64_t)(o0 + rr) * cin + k] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      float xv[4], wv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        xv[i] = xs[kk][ty * 4 + i];
+        wv[i] = ws_[kk][tx * 4 + i];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(xv[i], wv[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int bb = b0 + ty * 4 + i;
+    if (bb >= nb) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int o = o0 + tx * 4 + j;
+      if (o >= cout) continue;
+      float v = acc[i][j] + (bias ? bias[o] : 0.f);
+      if (act == 1) v = mmr::gelu_erf(v);
+      Y[(int64_t)bb * cout + o] = v;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void l2_normalize_rows(float* __restrict__ y, int nb, int d) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= nb) return;
+  float* p = y + (int64_t)row * d;
+  float s = 0.f;
+  for (int k = lane; k < d; k += 64) s += p[k] * p[k];
+  s = mmr::wave_sum(s);
+  const float inv = s > 0.f ? rsqrtf(s) : 0.f;
+  for (int k = lane; k < d; k += 64) p[k] *= inv;
+}
+
+}  // namespace
+
+// ================================================================== C ABI
+extern "C" {
+
+mmr_status mmr_layernorm_bf16(const uint16_t* x, const float* gamma, const float* beta,
+                              uint16_t* y, int64_t rows, int32_t c, float eps, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && gamma && beta && y, "mmr_layernorm_bf16: NULL pointer");
+  MMR_REQUIRE(c > 0 && c % 8 == 0 && rows >= 0, "mmr_layernorm_bf16: c=%d must be a positive multiple of 8", c);
+  if (rows == 0) return MMR_OK;
+  layernorm_bf16<<<dim3((unsigned)mmr::ceil_div(rows, 4)), 256, 0, mmr::as_stream(stream)>>>(
+      x, gamma, beta, y, rows, c, eps);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_bert_embed(const int64_t* ids, const float* word, const float* pos,
+                          const float* type0, const float* gamma, const float* beta, uint16_t* y,
+                          int32_t b, int32_t l, int32_t c, float eps, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(ids && word && pos && type0 && gamma && beta && y, "mmr_bert_embed: NULL pointer");
+  MMR_REQUIRE(b >= 0 && l > 0 && c > 0, "mmr_bert_embed: bad shape");
+  const int64_t ntok = (int64_t)b * l;
+  if (ntok == 0) return MMR_OK;
+  bert_embed<<<dim3((unsigned)mmr::ceil_div(ntok, 4)), 256, 0, mmr::as_stream(stream)>>>(
+      ids, word, pos, type0, gamma, beta, y, ntok, l, c, eps);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_bert_attention(const uint16_t* qkv, const int64_t* mask01, uint16_t* ctx,
+                              int32_t b, int32_t l, int32_t h, int32_t dh, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(qkv && mask01 && ctx, "mmr_bert_attention: NULL pointer");
+  MMR_REQUIRE(dh == BA_DH, "mmr_bert_attention: head_dim %d (only 64 built)", dh);
+  MMR_REQUIRE(l > 0 && l <= 512 && l % 32 == 0, "mmr_bert_attention: L=%d must be a multiple of 32 <= 512", l);
+  MMR_REQUIRE(b >= 0 && h > 0, "mmr_bert_attention: bad shape");
+  if (b == 0) return MMR_OK;
+  const size_t lds = (size_t)l * BA_DH * 2 + (size_t)BA_DH * (l + 4) * 2 + (size_t)l * 4;
+  bert_attention<<<dim3((unsigned)(b * h)), 256, lds, mmr::as_stream(stream)>>>(qkv, mask01, ctx, l, h);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_swin_window_attention(const uint16_t* qkv, const float* relpos_table,
+                                     uint16_t* out, int32_t b, int32_t hw, int32_t c,
+                                     int32_t heads, int32_t ws, int32_t shift, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(qkv && relpos_table && out, "mmr_swin_window_attention: NULL pointer");
+  MMR_REQUIRE(heads > 0 && c == heads * SW_DH, "mmr_swin_window_attention: c=%d heads=%d (head_dim 32 only)", c, heads);
+  MMR_REQUIRE(ws > 0 && ws * ws <= 64 && hw % ws == 0, "mmr_swin_window_attention: window %d / resolution %d", ws, hw);
+  MMR_REQUIRE(shift >= 0 && shift < ws, "mmr_swin_window_attention: shift %d", shift);
+  if (b == 0) return MMR_OK;
+  const int64_t units = (int64_t)b * (hw / ws) * (hw / ws) * heads;
+  swin_window_attention<<<dim3((unsigned)mmr::ceil_div(units, 4)), 256, 0, mmr::as_stream(stream)>>>(
+      qkv, relpos_table, out, units, hw, c, heads, ws, shift);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_patch_im2col(const float* image, uint16_t* cols, int32_t b, int32_t cin,
+                            int32_t hw, int32_t patch, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(image && cols, "mmr_patch_im2col: NULL pointer");
+  MMR_REQUIRE(cin * patch * patch <= 64 && hw % patch == 0, "mmr_patch_im2col: cin*patch^2 must be <= 64");
+  const int64_t ntok = (int64_t)b * (hw / patch) * (hw / patch);
+  if (ntok == 0) return MMR_OK;
+  patch_im2col<<<dim3((unsigned)mmr::ceil_div(ntok * 8, 256)), 256, 0, mmr::as_stream(stream)>>>(
+      image, cols, ntok, cin, hw, patch);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_patch_merge_ln(const uint16_t* x, const float* gamma, const float* beta,
+                              uint16_t* y, int32_t b, int32_t hw, int32_t c, float eps,
+                              void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && gamma && beta && y, "mmr_patch_merge_ln: NULL pointer");
+  MMR_REQUIRE(hw % 2 == 0 && c % 8 == 0, "mmr_patch_merge_ln: hw=%d c=%d", hw, c);
+  const int64_t nout = (int64_t)b * (hw / 2) * (hw / 2);
+  if (nout == 0) return MMR_OK;
+  patch_merge_ln<<<dim3((unsigned)mmr::ceil_div(nout, 4)), 256, 0, mmr::as_stream(stream)>>>(
+      x, gamma, beta, y, nout, hw, c, eps);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_swin_head(const uint16_t* x, const float* gamma, const float* beta, float* patches,
+                         float* global, float* pool, int32_t b, int32_t t, int32_t c, float eps,
+                         void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && gamma && beta, "mmr_swin_head: NULL pointer");
+  MMR_REQUIRE(c % 64 == 0 && c <= 64 * SH_MAXPL && t > 0, "mmr_swin_head: c=%d must be a multiple of 64 <= 1024", c);
+  if (b == 0) return MMR_OK;
+  swin_head<<<dim3((unsigned)b), 256, 0, mmr::as_stream(stream)>>>(x, gamma, beta, patches, global,
+                                                                   pool, t, c, eps);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_mean_tokens(const uint16_t* x, float* y, int32_t b, int32_t l, int32_t c,
+                           void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && y && l > 0 && c > 0, "mmr_mean_tokens: bad arguments");
+  if (b == 0) return MMR_OK;
+  mean_tokens<<<dim3((unsigned)mmr::ceil_div(c, 256), (unsigned)b), 256, 0, mmr::as_stream(stream)>>>(x, y, l, c);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_proj_head(const float* x, const float* wp, const float* bp, const float* w1,
+                         const float* b1, const float* w2, const float* b2, float* y, int32_t b,
+                         int32_t cin, int32_t d, int32_t l2norm, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && wp && y && b >= 0 && cin > 0 && d > 0, "mmr_proj_head: bad arguments");
+  MMR_REQUIRE((w1 == nullptr) == (w2 == nullptr), "mmr_proj_head: w1/w2 must both be set or both NULL");
+  if (b == 0) return MMR_OK;
+  hipStream_t st = mmr::as_stream(stream);
+  const dim3 blk(256);
+  if (w1 == nullptr) {
+    linear_f32<<<dim3((unsigned)mmr::ceil_div(d, 64), (unsigned)mmr::ceil_div(b, 64)), blk, 0, st>>>(
+        x, wp, bp, y, b, cin, d, 0);
+    MMR_LAUNCH_CHECK();
+  } else {
+    float *t0 = nullptr, *t1 = nullptr;
+    MMR_CHECK_HIP(hipMallocAsync((void**)&t0, sizeof(float) * (size_t)b * d, st));
+    MMR_CHECK_HIP(hipMallocAsync((void**)&t1, sizeof(float) * (size_t)b * 2 * d, st));
+    linear_f32<<<dim3((unsigned)mmr::ceil_div(d, 64), (unsigned)mmr::ceil_div(b, 64)), blk, 0, st>>>(
+        x, wp, bp, t0, b, cin, d, 0);
+    linear_f32<<<dim3((unsigned)mmr::ceil_div(2 * d, 64), (unsigned)mmr::ceil_div(b, 64)), blk, 0, st>>>(
+        t0, w1, b1, t1, b, d, 2 * d, 1);
+    linear_f32<<<dim3((unsigned)mmr::ceil_div(d, 64), (unsigned)mmr::ceil_div(b, 64)), blk, 0, st>>>(
+        t1, w2, b2, y, b, 2 * d, d, 0);
+    MMR_LAUNCH_CHECK();
+    MMR_CHECK_HIP(hipFreeAsync(t0, st));
+    MMR_CHECK_HIP(hipFreeAsync(t1, st));
+  }
+  if (l2norm) {
+    l2_normalize_rows<<<dim3((unsigned)mmr::ceil_div(b, 4)), blk, 0, st>>>(y, b, d);
+    MMR_LAUNCH_CHECK();
+  }
+  return MMR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,111 @@
+"""Thin torch-facing wrappers over the libmmr tower ops (include/mmr.h).  Every op launches a
+hand-written gfx950 kernel on torch's current stream and raises if the library or the GPU is
+missing — there is no torch fallback.  bf16 activations travel as torch.bfloat16 tensors (same
+bits as the C ABI's uint16)."""
+import torch
+
+from . import _lib
+
+
+def _L():
+    return _lib.lib()
+
+
+def _s(t):
+    return _lib.stream_ptr(t.device)
+
+
+def _chk(status, what):
+    _lib.check(status, what)
+
+
+def linear(x, w, bias=None, residual=None, act=0, out=None):
+    """act(x @ w.T + bias) (+ residual); x (..., K) bf16, w (N, K) bf16, bias f32."""
+    _lib.require_gpu(x)
+    K = x.shape[-1]
+    N = w.shape[0]
+    M = x.numel() // K
+    y = out if out is not None else torch.empty(x.shape[:-1] + (N,), dtype=torch.bfloat16, device=x.device)
+    _chk(_L().mmr_linear_bf16(_lib.ptr(x), _lib.ptr(w), _lib.ptr(bias), _lib.ptr(residual), _lib.ptr(y),
+                              M, N, K, act, _s(x)), "mmr_linear_bf16")
+    return y
+
+
+def layernorm(x, g, b, eps, out=None):
+    _lib.require_gpu(x)
+    c = x.shape[-1]
+    y = out if out is not None else torch.empty_like(x)
+    _chk(_L().mmr_layernorm_bf16(_lib.ptr(x), _lib.ptr(g), _lib.ptr(b), _lib.ptr(y), x.numel() // c, c,
+                                 float(eps), _s(x)), "mmr_layernorm_bf16")
+    return y
+
+
+def bert_embed(ids, word, pos, type0, g, b, eps):
+    _lib.require_gpu(ids)
+    B, L = ids.shape
+    C = word.shape[1]
+    y = torch.empty((B, L, C), dtype=torch.bfloat16, device=ids.device)
+    _chk(_L().mmr_bert_embed(_lib.ptr(ids), _lib.ptr(word), _lib.ptr(pos), _lib.ptr(type0), _lib.ptr(g),
+                             _lib.ptr(b), _lib.ptr(y), B, L, C, float(eps), _s(ids)), "mmr_bert_embed")
+    return y
+
+
+def bert_attention(qkv, mask, heads, dh=64):
+    B, L, C3 = qkv.shape
+    ctx = torch.empty((B, L, C3 // 3), dtype=torch.bfloat16, device=qkv.device)
+    _chk(_L().mmr_bert_attention(_lib.ptr(qkv), _lib.ptr(mask), _lib.ptr(ctx), B, L, heads, dh, _s(qkv)),
+         "mmr_bert_attention")
+    return ctx
+
+
+def swin_window_attention(qkv, table, hw, heads, ws, shift):
+    B = qkv.shape[0]
+    C = qkv.shape[-1] // 3
+    out = torch.empty(qkv.shape[:-1] + (C,), dtype=torch.bfloat16, device=qkv.device)
+    _chk(_L().mmr_swin_window_attention(_lib.ptr(qkv), _lib.ptr(table), _lib.ptr(out), B, hw, C, heads, ws,
+                                        shift, _s(qkv)), "mmr_swin_window_attention")
+    return out
+
+
+def patch_im2col(img, patch=4):
+    B, Cin, H, W = img.shape
+    g = H // patch
+    cols = torch.empty((B, g * g, 64), dtype=torch.bfloat16, device=img.device)
+    _chk(_L().mmr_patch_im2col(_lib.ptr(img), _lib.ptr(cols), B, Cin, H, patch, _s(img)), "mmr_patch_im2col")
+    return cols
+
+
+def patch_merge_ln(x, g, b, eps):
+    B, H, W, C = x.shape
+    y = torch.empty((B, H // 2, W // 2, 4 * C), dtype=torch.bfloat16, device=x.device)
+    _chk(_L().mmr_patch_merge_ln(_lib.ptr(x), _lib.ptr(g), _lib.ptr(b), _lib.ptr(y), B, H, C, float(eps),
+                                 _s(x)), "mmr_patch_merge_ln")
+    return y
+
+
+def swin_head(x, g, b, eps, want_patches=True):
+    """x (B, T, C) bf16 pre-final-norm tokens -> (patches f32 (B,T,C) | None, global f32, pool f32)."""
+    B, T, C = x.shape
+    dev = x.device
+    patches = torch.empty((B, T, C), dtype=torch.float32, device=dev) if want_patches else None
+    glob = torch.empty((B, C), dtype=torch.float32, device=dev)
+    pool = torch.empty((B, C), dtype=torch.float32, device=dev)
+    _chk(_L().mmr_swin_head(_lib.ptr(x), _lib.ptr(g), _lib.ptr(b), _lib.ptr(patches), _lib.ptr(glob),
+                            _lib.ptr(pool), B, T, C, float(eps), _s(x)), "mmr_swin_head")
+    return patches, glob, pool
+
+
+def mean_tokens(x):
+    B, L, C = x.shape
+    y = torch.empty((B, C), dtype=torch.float32, device=x.device)
+    _chk(_L().mmr_mean_tokens(_lib.ptr(x), _lib.ptr(y), B, L, C, _s(x)), "mmr_mean_tokens")
+    return y
+
+
+def proj_head(x, wp, bp, w1=None, b1=None, w2=None, b2=None, l2norm=False):
+    B, Cin = x.shape
+    D = wp.shape[0]
+    y = torch.empty((B, D), dtype=torch.float32, device=x.device)
+    _chk(_L().mmr_proj_head(_lib.ptr(x), _lib.ptr(wp), _lib.ptr(bp), _lib.ptr(w1), _lib.ptr(b1), _lib.ptr(w2),
+                            _lib.ptr(b2), _lib.ptr(y), B, Cin, D, int(bool(l2norm)), _s(x)), "mmr_proj_head")
+    return y

@@ -1,0 +1,213 @@
+"""Swin-Tiny image tower and ClinicalBERT (BERT-base geometry) text tower on libmmr kernels.
+
+Weights load from reference-style state dicts (timm key names for Swin — what
+Backbones.__init__ builds with timm.create_model, fusion.py:81-110 — and HF BertModel key names
+for the text tower, fusion.py:186) and are laid out once for the device:
+linear weights bf16 [out][in] (QKV fused into one [3C][C] GEMM), biases / LN / rel-pos tables f32,
+the 4x4/s4 patch-embed conv as a [96][64] bf16 GEMM weight (K = 3*16 zero-padded to 64).
+
+Per-block dataflow (all hand-written kernels, bf16 activations, f32 accumulation):
+  Swin block   LN1 -> QKV GEMM(+bias) -> window attention (roll/partition/bias/mask/softmax/PV/
+               reverse/roll fused) -> proj GEMM(+bias +residual) -> LN2 -> fc1 GEMM(+bias, GELU)
+               -> fc2 GEMM(+bias +residual)
+  PatchMerge   gather 2x2 + LN(4C) fused -> reduction GEMM (no bias)
+  BERT layer   QKV GEMM(+bias) -> masked attention -> out GEMM(+bias +residual) -> LN ->
+               FFN1 GEMM(+bias, GELU) -> FFN2 GEMM(+bias +residual) -> LN
+"""
+import torch
+
+from . import ops
+
+SWIN_T = dict(embed_dim=96, depths=[2, 2, 6, 2], num_heads=[3, 6, 12, 24], window_size=7, img_size=224,
+              patch=4, in_chans=3)
+BERT_BASE = dict(vocab_size=28996, hidden_size=768, num_hidden_layers=12, num_attention_heads=12,
+                 intermediate_size=3072, max_position_embeddings=512, type_vocab_size=2)
+
+
+def _bf(t, dev):
+    return t.detach().to(device=dev, dtype=torch.bfloat16).contiguous()
+
+
+def _f(t, dev):
+    return t.detach().to(device=dev, dtype=torch.float32).contiguous()
+
+
+class SwinTower:
+    """timm SwinTransformer.forward_features semantics (see oracle/towers.py for the restatement)."""
+
+    def __init__(self, sd, cfg=SWIN_T, device="cuda"):
+        self.cfg = dict(SWIN_T, **cfg)
+        dev = torch.device(device)
+        self.device = dev
+        E = self.cfg["embed_dim"]
+        w = sd["patch_embed.proj.weight"].reshape(E, -1)          # [E][cin*16], (c, ky, kx) order
+        wp = torch.zeros((E, 64), dtype=torch.float32)
+        wp[:, :w.shape[1]] = w
+        self.pe_w, self.pe_b = _bf(wp, dev), _f(sd["patch_embed.proj.bias"], dev)
+        self.pe_g, self.pe_beta = _f(sd["patch_embed.norm.weight"], dev), _f(sd["patch_embed.norm.bias"], dev)
+        self.stages = []
+        for i, depth in enumerate(self.cfg["depths"]):
+            st = {"blocks": []}
+            if i > 0:
+                p = f"layers.{i}.downsample."
+                st["ds_g"], st["ds_b"] = _f(sd[p + "norm.weight"], dev), _f(sd[p + "norm.bias"], dev)
+                st["ds_w"] = _bf(sd[p + "reduction.weight"], dev)
+            for j in range(depth):
+                p = f"layers.{i}.blocks.{j}."
+                st["blocks"].append({
+                    "n1g": _f(sd[p + "norm1.weight"], dev), "n1b": _f(sd[p + "norm1.bias"], dev),
+                    "qkv_w": _bf(sd[p + "attn.qkv.weight"], dev), "qkv_b": _f(sd[p + "attn.qkv.bias"], dev),
+                    "table": _f(sd[p + "attn.relative_position_bias_table"], dev),
+                    "proj_w": _bf(sd[p + "attn.proj.weight"], dev), "proj_b": _f(sd[p + "attn.proj.bias"], dev),
+                    "n2g": _f(sd[p + "norm2.weight"], dev), "n2b": _f(sd[p + "norm2.bias"], dev),
+                    "fc1_w": _bf(sd[p + "mlp.fc1.weight"], dev), "fc1_b": _f(sd[p + "mlp.fc1.bias"], dev),
+                    "fc2_w": _bf(sd[p + "mlp.fc2.weight"], dev), "fc2_b": _f(sd[p + "mlp.fc2.bias"], dev),
+                })
+            self.stages.append(st)
+        self.norm_g, self.norm_b = _f(sd["norm.weight"], dev), _f(sd["norm.bias"], dev)
+        self.num_features = E * 2 ** (len(self.cfg["depths"]) - 1)
+
+    def tokens(self, image):
+        """(B,3,H,W) f32 -> (B, h, w, C) bf16 tokens BEFORE the final norm."""
+        cfg = self.cfg
+        image = image.to(self.device, torch.float32).contiguous()
+        B = image.shape[0]
+        g = cfg["img_size"] // cfg["patch"]
+        cols = ops.patch_im2col(image, cfg["patch"])
+        x = ops.linear(cols, self.pe_w, self.pe_b)                   # (B, g*g, E)
+        x = ops.layernorm(x, self.pe_g, self.pe_beta, 1e-5).view(B, g, g, -1)
+        ws0 = cfg["window_size"]
+        for i, st in enumerate(self.stages):
+            if i > 0:
+                x = ops.linear(ops.patch_merge_ln(x, st["ds_g"], st["ds_b"], 1e-5), st["ds_w"])
+            H = x.shape[1]
+            C = x.shape[-1]
+            heads = cfg["num_heads"][i]
+            ws = min(ws0, H)
+            for j, bk in enumerate(st["blocks"]):
+                shift = 0 if (j % 2 == 0 or H <= ws0) else ws0 // 2
+                h = ops.layernorm(x, bk["n1g"], bk["n1b"], 1e-5)
+                qkv = ops.linear(h, bk["qkv_w"], bk["qkv_b"])
+                a = ops.swin_window_attention(qkv, bk["table"], H, heads, ws, shift)
+                x = ops.linear(a, bk["proj_w"], bk["proj_b"], residual=x)
+                h = ops.layernorm(x, bk["n2g"], bk["n2b"], 1e-5)
+                h = ops.linear(h, bk["fc1_w"], bk["fc1_b"], act=1)
+                x = ops.linear(h, bk["fc2_w"], bk["fc2_b"], residual=x)
+            del C
+        return x
+
+    def forward_features(self, image):
+        """timm forward_features: (B, h, w, C) NHWC after the final norm (bf16)."""
+        x = self.tokens(image)
+        return ops.layernorm(x, self.norm_g, self.norm_b, 1e-5)
+
+
+class BertTower:
+    """HF BertModel(input_ids, attention_mask).last_hidden_state semantics (eval)."""
+
+    def __init__(self, sd, cfg=BERT_BASE, device="cuda"):
+        self.cfg = dict(BERT_BASE, **cfg)
+        dev = torch.device(device)
+        self.device = dev
+        self.word = _f(sd["embeddings.word_embeddings.weight"], dev)
+        self.pos = _f(sd["embeddings.position_embeddings.weight"], dev)
+        self.type0 = _f(sd["embeddings.token_type_embeddings.weight"][0], dev)
+        self.eg, self.eb = _f(sd["embeddings.LayerNorm.weight"], dev), _f(sd["embeddings.LayerNorm.bias"], dev)
+        self.layers = []
+        for i in range(self.cfg["num_hidden_layers"]):
+            p = f"encoder.layer.{i}."
+            qkv_w = torch.cat([sd[p + f"attention.self.{n}.weight"] for n in ("query", "key", "value")], 0)
+            qkv_b = torch.cat([sd[p + f"attention.self.{n}.bias"] for n in ("query", "key", "value")], 0)
+            self.layers.append({
+                "qkv_w": _bf(qkv_w, dev), "qkv_b": _f(qkv_b, dev),
+                "o_w": _bf(sd[p + "attention.output.dense.weight"], dev),
+                "o_b": _f(sd[p + "attention.output.dense.bias"], dev),
+                "ln1_g": _f(sd[p + "attention.output.LayerNorm.weight"], dev),
+                "ln1_b": _f(sd[p + "attention.output.LayerNorm.bias"], dev),
+                "i_w": _bf(sd[p + "intermediate.dense.weight"], dev), "i_b": _f(sd[p + "intermediate.dense.bias"], dev),
+                "f_w": _bf(sd[p + "output.dense.weight"], dev), "f_b": _f(sd[p + "output.dense.bias"], dev),
+                "ln2_g": _f(sd[p + "output.LayerNorm.weight"], dev), "ln2_b": _f(sd[p + "output.LayerNorm.bias"], dev),
+            })
+        self.hidden = self.word.shape[1]
+
+    def forward(self, input_ids, attention_mask=None):
+        """(B, L) ids/mask -> (B, L, C) bf16 last_hidden_state.  L is truncated to
+        max_position_embeddings like fusion.py:315-320."""
+        cfg = self.cfg
+        ids = input_ids.to(self.device, torch.int64)
+        if attention_mask is None:
+            attention_mask = torch.ones_like(ids)
+        mask = attention_mask.to(self.device, torch.int64)
+        max_len = cfg["max_position_embeddings"]
+        if ids.shape[1] > max_len:
+            ids, mask = ids[:, :max_len], mask[:, :max_len]
+        ids, mask = ids.contiguous(), mask.contiguous()
+        heads = cfg["num_attention_heads"]
+        h = ops.bert_embed(ids, self.word, self.pos, self.type0, self.eg, self.eb, 1e-12)
+        for ly in self.layers:
+            qkv = ops.linear(h, ly["qkv_w"], ly["qkv_b"])
+            ctx = ops.bert_attention(qkv, mask, heads, self.hidden // heads)
+            a = ops.linear(ctx, ly["o_w"], ly["o_b"], residual=h)
+            h = ops.layernorm(a, ly["ln1_g"], ly["ln1_b"], 1e-12)
+            f = ops.linear(h, ly["i_w"], ly["i_b"], act=1)
+            f = ops.linear(f, ly["f_w"], ly["f_b"], residual=h)
+            h = ops.layernorm(f, ly["ln2_g"], ly["ln2_b"], 1e-12)
+        return h
+
+
+# ---------------------------------------------------------------- synthetic weights (bench)
+def init_swin_state(cfg=SWIN_T, seed=2709):
+    """Random-init Swin state dict in timm naming (trunc-normal(0.02) linears, LN (1, 0))."""
+    cfg = dict(SWIN_T, **cfg)
+    g = torch.Generator().manual_seed(seed)
+
+    def rn(*shape):
+        return (torch.randn(*shape, generator=g) * 0.02).clamp_(-0.04, 0.04)
+    E = cfg["embed_dim"]
+    ws = cfg["window_size"]
+    sd = {"patch_embed.proj.weight": rn(E, cfg["in_chans"], cfg["patch"], cfg["patch"]),
+          "patch_embed.proj.bias": torch.zeros(E), "patch_embed.norm.weight": torch.ones(E),
+          "patch_embed.norm.bias": torch.zeros(E)}
+    C = E
+    for i, depth in enumerate(cfg["depths"]):
+        if i > 0:
+            p = f"layers.{i}.downsample."
+            sd[p + "norm.weight"], sd[p + "norm.bias"] = torch.ones(4 * C), torch.zeros(4 * C)
+            sd[p + "reduction.weight"] = rn(2 * C, 4 * C)
+            C *= 2
+        for j in range(depth):
+            p = f"layers.{i}.blocks.{j}."
+            sd.update({p + "norm1.weight": torch.ones(C), p + "norm1.bias": torch.zeros(C),
+                       p + "attn.qkv.weight": rn(3 * C, C), p + "attn.qkv.bias": rn(3 * C),
+                       p + "attn.relative_position_bias_table": rn((2 * ws - 1) ** 2, cfg["num_heads"][i]),
+                       p + "attn.proj.weight": rn(C, C), p + "attn.proj.bias": rn(C),
+                       p + "norm2.weight": torch.ones(C), p + "norm2.bias": torch.zeros(C),
+                       p + "mlp.fc1.weight": rn(4 * C, C), p + "mlp.fc1.bias": rn(4 * C),
+                       p + "mlp.fc2.weight": rn(C, 4 * C), p + "mlp.fc2.bias": rn(C)})
+    sd["norm.weight"], sd["norm.bias"] = torch.ones(C), torch.zeros(C)
+    return sd
+
+
+def init_bert_state(cfg=BERT_BASE, seed=2710):
+    cfg = dict(BERT_BASE, **cfg)
+    g = torch.Generator().manual_seed(seed)
+
+    def rn(*shape):
+        return torch.randn(*shape, generator=g) * 0.02
+    C, I = cfg["hidden_size"], cfg["intermediate_size"]
+    sd = {"embeddings.word_embeddings.weight": rn(cfg["vocab_size"], C),
+          "embeddings.position_embeddings.weight": rn(cfg["max_position_embeddings"], C),
+          "embeddings.token_type_embeddings.weight": rn(cfg["type_vocab_size"], C),
+          "embeddings.LayerNorm.weight": torch.ones(C), "embeddings.LayerNorm.bias": torch.zeros(C)}
+    for i in range(cfg["num_hidden_layers"]):
+        p = f"encoder.layer.{i}."
+        for n in ("query", "key", "value"):
+            sd[p + f"attention.self.{n}.weight"] = rn(C, C)
+            sd[p + f"attention.self.{n}.bias"] = rn(C)
+        sd.update({p + "attention.output.dense.weight": rn(C, C), p + "attention.output.dense.bias": rn(C),
+                   p + "attention.output.LayerNorm.weight": torch.ones(C),
+                   p + "attention.output.LayerNorm.bias": torch.zeros(C),
+                   p + "intermediate.dense.weight": rn(I, C), p + "intermediate.dense.bias": rn(I),
+                   p + "output.dense.weight": rn(C, I), p + "output.dense.bias": rn(C),
+                   p + "output.LayerNorm.weight": torch.ones(C), p + "output.LayerNorm.bias": torch.zeros(C)})
+    return sd
