@@ -31,40 +31,61 @@ __device__ __forceinline__ void store8(uint16_t* p, const float* v) {
   *(bf16x8*)p = x;
 }
 
-// ------------------------------------------------------------------ LayerNorm (one wave per row)
-// Two passes over the row (mean, then centred variance — torch's biased variance), re-reads hit
-// L1/L2.  Rows of c channels, c % 8 == 0.
+// ------------------------------------------------------------------ LayerNorm
+// LPR lanes per row (64/LPR rows per wave) so narrow Swin rows (C = 96..384) keep every lane busy;
+// the row stays in registers (<= 8 chunks of 8 per lane): one read, one write, exact two-pass
+// (centred) variance like torch.
+template <int LPR>
 __global__ __launch_bounds__(256) void layernorm_bf16(const uint16_t* __restrict__ x,
                                                       const float* __restrict__ g,
                                                       const float* __restrict__ b,
                                                       uint16_t* __restrict__ y, int64_t rows,
                                                       int c, float eps) {
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  constexpr int RPW = 64 / LPR;
   const int lane = threadIdx.x & 63;
-  if (row >= rows) return;
-  const uint16_t* xr = x + row * c;
+  const int sub = lane % LPR;
+  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  const bool ok = row < rows;
+  const uint16_t* xr = x + (ok ? row : 0) * c;
+  const int nch = c / 8;
+  float v[8][8];
   float s = 0.f;
-  for (int k = lane * 8; k < c; k += 512) {
-    float v[8];
-    load8(xr + k, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += v[j];
+  for (int i = 0; i < 8; ++i) {
+    const int ch = sub + i * LPR;
+    if (ok && ch < nch) {
+      load8(xr + ch * 8, v[i]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[i][j];
+    }
   }
-  const float mean = mmr::wave_sum(s) / c;
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mean = s / c;
   float ss = 0.f;
-  for (int k = lane * 8; k < c; k += 512) {
-    float v[8];
-    load8(xr + k, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) ss += (v[j] - mean) * (v[j] - mean);
+  for (int i = 0; i < 8; ++i) {
+    const int ch = sub + i * LPR;
+    if (ok && ch < nch) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += (v[i][j] - mean) * (v[i][j] - mean);
+    }
   }
-  const float rstd = rsqrtf(mmr::wave_sum(ss) / c + eps);
-  for (int k = lane * 8; k < c; k += 512) {
-    float v[8];
-    load8(xr + k, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (v[j] - mean) * rstd * g[k + j] + b[k + j];
-    store8(y + row * c + k, v);
+  for (int o = LPR / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  const float rstd = rsqrtf(ss / c + eps);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int ch = sub + i * LPR;
+    if (ok && ch < nch) {
+      const float4 g0 = *(const float4*)(g + ch * 8), g1 = *(const float4*)(g + ch * 8 + 4);
+      const float4 b0 = *(const float4*)(b + ch * 8), b1 = *(const float4*)(b + ch * 8 + 4);
+      const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = (v[i][j] - mean) * rstd * gg[j] + bb[j];
+      store8(y + row * c + ch * 8, v[i]);
+    }
   }
 }
 
@@ -537,52 +558,43 @@ __global__ __launch_bounds__(256) void mean_tokens(const uint16_t* __restrict__ 
 }
 
 // ------------------------------------------------------------------ small f32 linear (heads)
-// Y[b][o] = act(sum_i X[b][i] W[o][i] + bias[o]); 64x64 output tile, 16-deep K slabs in LDS,
-// 4x4 outputs per thread.  The heads are ~1 MFLOP per query: latency, not throughput, matters.
+// Y[b][o] = act(sum_i X[b][i] W[o][i] + bias[o]) in exact f32 (v_mfma_f32_32x32x2_f32); one wave
+// per 32x32 output tile, operands straight to VGPRs as float4 with the k-permutation of
+// knn_scores (lane half h owns k = kb+8h..kb+8h+7).  cin % 16 == 0, cout % 32 == 0.
 __global__ __launch_bounds__(256) void linear_f32(const float* __restrict__ X,
                                                   const float* __restrict__ W,
                                                   const float* __restrict__ bias,
                                                   float* __restrict__ Y, int nb, int cin, int cout,
                                                   int act) {
-  __shared__ float xs[16][64 + 1], ws_[16][64 + 1];
-  const int b0 = blockIdx.y * 64, o0 = blockIdx.x * 64;
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  float acc[4][4] = {};
-  for (int k0 = 0; k0 < cin; k0 += 16) {
-    for (int e = threadIdx.x; e < 16 * 64; e += 256) {
-      const int kk = e & 15, rr = e >> 4;
-      const int k = k0 + kk;
-      xs[kk][rr] = (b0 + rr < nb && k < cin) ? X[(int64_t)(b0 + rr) * cin + k] : 0.f;
-      ws_[kk][rr] = (o0 + rr < cout && k < cin) ? W[(int64_t)(o0 + rr) * cin + k] : 0.f;
-    }
-    __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int tiles_o = cout / 32;
+  const int t = blockIdx.x * 4 + wave;
+  const int tb = t / tiles_o, to = t % tiles_o;
+  if (tb * 32 >= nb) return;
+  const int r = lane & 31, h = lane >> 5;
+  const int b = tb * 32 + r;
+  const bool bok = b < nb;
+  const float* xa = X + (int64_t)(bok ? b : 0) * cin + 8 * h;
+  const float* wb = W + (int64_t)(to * 32 + r) * cin + 8 * h;
+  f32x16 acc = {0};
+  for (int kb = 0; kb < cin; kb += 16) {
+    float4 a0 = *(const float4*)(xa + kb), a1 = *(const float4*)(xa + kb + 4);
+    const float4 b0 = *(const float4*)(wb + kb), b1 = *(const float4*)(wb + kb + 4);
+    if (!bok) a0 = a1 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
-      float xv[4], wv[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        xv[i] = xs[kk][ty * 4 + i];
-        wv[i] = ws_[kk][tx * 4 + i];
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(xv[i], wv[j], acc[i][j]);
-    }
-    __syncthreads();
+    for (int s8 = 0; s8 < 8; ++s8) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s8], bv[s8], acc, 0, 0, 0);
   }
+  const int o = to * 32 + r;
+  const float bo = bias ? bias[o] : 0.f;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int bb = b0 + ty * 4 + i;
+  for (int rg = 0; rg < 16; ++rg) {
+    const int bb = tb * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * h;
     if (bb >= nb) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int o = o0 + tx * 4 + j;
-      if (o >= cout) continue;
-      float v = acc[i][j] + (bias ? bias[o] : 0.f);
-      if (act == 1) v = mmr::gelu_erf(v);
-      Y[(int64_t)bb * cout + o] = v;
-    }
+    float v = acc[rg] + bo;
+    if (act == 1) v = mmr::gelu_erf(v);
+    Y[(int64_t)bb * cout + o] = v;
   }
 }
 
@@ -608,9 +620,18 @@ mmr_status mmr_layernorm_bf16(const uint16_t* x, const float* gamma, const float
   mmr::clear_error();
   MMR_REQUIRE(x && gamma && beta && y, "mmr_layernorm_bf16: NULL pointer");
   MMR_REQUIRE(c > 0 && c % 8 == 0 && rows >= 0, "mmr_layernorm_bf16: c=%d must be a positive multiple of 8", c);
+  MMR_REQUIRE(c <= 4096, "mmr_layernorm_bf16: c=%d > 4096", c);
   if (rows == 0) return MMR_OK;
-  layernorm_bf16<<<dim3((unsigned)mmr::ceil_div(rows, 4)), 256, 0, mmr::as_stream(stream)>>>(
-      x, gamma, beta, y, rows, c, eps);
+  hipStream_t st = mmr::as_stream(stream);
+  const int nch = c / 8;
+  int lpr = 64;
+  while (lpr > 8 && nch <= (lpr / 2) * 2) lpr /= 2;  // <= 2 chunks per lane for narrow rows
+  const int64_t rows_per_block = 4 * (64 / lpr);
+  const dim3 grid((unsigned)mmr::ceil_div(rows, rows_per_block));
+  if (lpr == 8) layernorm_bf16<8><<<grid, 256, 0, st>>>(x, gamma, beta, y, rows, c, eps);
+  else if (lpr == 16) layernorm_bf16<16><<<grid, 256, 0, st>>>(x, gamma, beta, y, rows, c, eps);
+  else if (lpr == 32) layernorm_bf16<32><<<grid, 256, 0, st>>>(x, gamma, beta, y, rows, c, eps);
+  else layernorm_bf16<64><<<grid, 256, 0, st>>>(x, gamma, beta, y, rows, c, eps);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }
@@ -714,24 +735,25 @@ mmr_status mmr_proj_head(const float* x, const float* wp, const float* bp, const
                          int32_t cin, int32_t d, int32_t l2norm, void* stream) {
   mmr::clear_error();
   MMR_REQUIRE(x && wp && y && b >= 0 && cin > 0 && d > 0, "mmr_proj_head: bad arguments");
+  MMR_REQUIRE(cin % 16 == 0 && d % 32 == 0, "mmr_proj_head: cin=%d must be a multiple of 16, d=%d of 32", cin, d);
   MMR_REQUIRE((w1 == nullptr) == (w2 == nullptr), "mmr_proj_head: w1/w2 must both be set or both NULL");
   if (b == 0) return MMR_OK;
   hipStream_t st = mmr::as_stream(stream);
   const dim3 blk(256);
+  auto lin = [&](const float* xi, const float* w, const float* bb, float* yo, int ci, int co, int act) {
+    const int64_t tiles = mmr::ceil_div(b, 32) * (co / 32);
+    linear_f32<<<dim3((unsigned)mmr::ceil_div(tiles, 4)), blk, 0, st>>>(xi, w, bb, yo, b, ci, co, act);
+  };
   if (w1 == nullptr) {
-    linear_f32<<<dim3((unsigned)mmr::ceil_div(d, 64), (unsigned)mmr::ceil_div(b, 64)), blk, 0, st>>>(
-        x, wp, bp, y, b, cin, d, 0);
+    lin(x, wp, bp, y, cin, d, 0);
     MMR_LAUNCH_CHECK();
   } else {
     float *t0 = nullptr, *t1 = nullptr;
     MMR_CHECK_HIP(hipMallocAsync((void**)&t0, sizeof(float) * (size_t)b * d, st));
     MMR_CHECK_HIP(hipMallocAsync((void**)&t1, sizeof(float) * (size_t)b * 2 * d, st));
-    linear_f32<<<dim3((unsigned)mmr::ceil_div(d, 64), (unsigned)mmr::ceil_div(b, 64)), blk, 0, st>>>(
-        x, wp, bp, t0, b, cin, d, 0);
-    linear_f32<<<dim3((unsigned)mmr::ceil_div(2 * d, 64), (unsigned)mmr::ceil_div(b, 64)), blk, 0, st>>>(
-        t0, w1, b1, t1, b, d, 2 * d, 1);
-    linear_f32<<<dim3((unsigned)mmr::ceil_div(d, 64), (unsigned)mmr::ceil_div(b, 64)), blk, 0, st>>>(
-        t1, w2, b2, y, b, 2 * d, d, 0);
+    lin(x, wp, bp, t0, cin, d, 0);
+    lin(t0, w1, b1, t1, d, 2 * d, 1);
+    lin(t1, w2, b2, y, 2 * d, d, 0);
     MMR_LAUNCH_CHECK();
     MMR_CHECK_HIP(hipFreeAsync(t0, st));
     MMR_CHECK_HIP(hipFreeAsync(t1, st));
