@@ -57,6 +57,10 @@ mmr_status mmr_index_info(const mmr_index* index, int64_t* n, int32_t* d, int64_
  * (required before capturing a search into a HIP graph). */
 mmr_status mmr_index_reserve(mmr_index* index, int64_t max_q);
 
+/* Scan precision of the candidate pass (the ranking is always exact f64): 0 = f32 MFMA,
+ * 1 = bf16 3-term split MFMA (default; ~5x the f32 rate at the same bytes). */
+mmr_status mmr_index_set_mode(mmr_index* index, int32_t mode);
+
 /* Exact cosine top-K of q (q, d) f32 device queries against the gallery.
  * Semantics: s(q,g) = <q,g> / (|q| |g|) in f64 (0 when either norm is 0 — sklearn's normalize()
  * leaves zero rows at 0), ranked by score descending, ties by lower gallery index.  Outputs
@@ -100,11 +104,17 @@ mmr_status mmr_bert_attention(const uint16_t* qkv, const int64_t* mask01, uint16
 
 /* Swin (shifted-)window attention core (timm WindowAttention + cyclic shift, eval):
  * qkv bf16 (b*hw*hw, 3*c) in natural token order; the kernel applies roll(-shift), window
- * partition, q*dh^-0.5, k^T, + rel-pos bias (table f32 [(2ws-1)^2][heads]) + shift mask (-100),
- * softmax, v, window reverse and roll(+shift) -> out bf16 (b*hw*hw, c).  ws = 7, dh = 32. */
-mmr_status mmr_swin_window_attention(const uint16_t* qkv, const float* relpos_table,
-                                     uint16_t* out, int32_t b, int32_t hw, int32_t c,
-                                     int32_t heads, int32_t ws, int32_t shift, void* stream);
+ * partition, q*dh^-0.5, k^T, + the dense bias from mmr_swin_attn_bias, softmax, v, window reverse
+ * and roll(+shift) -> out bf16 (b*hw*hw, c).  ws*ws <= 64, head_dim 32. */
+mmr_status mmr_swin_window_attention(const uint16_t* qkv, const float* bias, uint16_t* out,
+                                     int32_t b, int32_t hw, int32_t c, int32_t heads, int32_t ws,
+                                     int32_t shift, void* stream);
+/* Dense additive attention bias for one Swin block, built once at load: f32
+ * [t][heads][64][64], t = 4 window types when shift > 0 (2*last-row + last-col), else 1:
+ * relative_position_bias_table[(yi-yj+ws-1)*(2ws-1) + (xi-xj+ws-1)][head] (timm index), + -100
+ * where the shift regions of i and j differ, -FLT_MAX for padded keys j >= ws*ws. */
+mmr_status mmr_swin_attn_bias(const float* relpos_table, float* bias, int32_t heads, int32_t ws,
+                              int32_t hw, int32_t shift, void* stream);
 
 /* Swin patch embedding im2col: image f32 NCHW (b,3,224,224) -> bf16 (b*56*56, 48) columns in
  * conv-weight order (cin, kh, kw) for a 4x4/s4 conv as a GEMM. */

@@ -24,6 +24,7 @@ SIGNATURES = {
     "mmr_index_destroy": [c_vp],
     "mmr_index_info": [c_vp, ctypes.POINTER(c_i64), ctypes.POINTER(c_i32), ctypes.POINTER(c_i64)],
     "mmr_index_reserve": [c_vp, c_i64],
+    "mmr_index_set_mode": [c_vp, c_i32],
     "mmr_index_search": [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
     "mmr_merge_topk": [c_vp, c_vp, c_i32, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp],
     "mmr_linear_bf16": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp],
@@ -31,6 +32,7 @@ SIGNATURES = {
     "mmr_bert_embed": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp],
     "mmr_bert_attention": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_swin_window_attention": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp],
+    "mmr_swin_attn_bias": [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_patch_im2col": [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_patch_merge_ln": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp],
     "mmr_swin_head": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp],

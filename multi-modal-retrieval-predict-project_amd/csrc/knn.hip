@@ -6,7 +6,14 @@
 //
 // Pipeline per search (all on the caller's stream):
 //   1. knn_prep_queries   q -> qn = q/|q| (f32, padded [Qp][Dp]) + |q| in f64.
-//   2. knn_scores         S[Qp][Np] = (qn . g) * (1/|g|) with v_mfma_f32_32x32x2_f32 (exact f32
+//   2. knn_scores_x3      (default) S = (qn . g) / |g| as a bf16 "3-term split" MFMA GEMM: every
+//                         operand is split into hi + lo bf16 (hi = bf16(x), lo = bf16(x - hi)) and
+//                         s ~= q_hi.g_hi + q_hi.g_lo + q_lo.g_hi (dropped terms <= 3*2^-16 |q||g|),
+//                         run as ONE K' = 3D GEMM on v_mfma_f32_16x16x32_bf16 (16x the f32 MFMA
+//                         rate; 5.3x after the 3 terms).  Gallery stored [hi c | lo c] per
+//                         64-wide chunk c (4 B/element, the f32 byte count); the k-tile 3c+2 re-reads
+//                         hi c from L2.  Queries stored [hi c | hi c | lo c].
+//      knn_scores         (mode f32) S[Qp][Np] = (qn . g) * (1/|g|) with v_mfma_f32_32x32x2_f32 (exact f32
 //                         products, f32 accumulate).  MFMA-bound for Q >~ 40, HBM-bound below.
 //                         Wave tile 64 queries x 64 gallery rows (2x2 MFMA tiles, 64 acc regs);
 //                         operands loaded straight to VGPRs as float4 with a k-permutation (lane
@@ -17,7 +24,8 @@
 //                         (D) rare fallback: exact radix select over the row if (C) overflowed;
 //                         (E) re-score candidates in f64 from the raw rows, rank by
 //                         (score desc, index asc), write the top K.
-//      delta bounds |s_f32 - s_f64| (D+16 ulps of 1.0), so every true top-K row is a candidate:
+//      delta bounds |s_approx - s_f64| (f32: (D+16) 2^-24; x3: (3D+16) 2^-24 + 4 2^-16), so every
+//      true top-K row is a candidate:
 //      the K rows with s32 >= t (t = K-th largest s32) all have s64 >= t - delta, hence the K-th
 //      largest s64 is >= t - delta and any true top-K row has s32 >= t - 2 delta >= b - 2 delta.
 #include <float.h>
@@ -165,6 +173,141 @@ __global__ __launch_bounds__(256) void knn_scores(const float* __restrict__ qn,
     s0[32] = c01[reg] * ig1;
     s1[0] = c10[reg] * ig0;
     s1[32] = c11[reg] * ig1;
+  }
+}
+
+// ------------------------------------------------------------------ bf16x3 split scores GEMM
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ void split_bf16(float x, uint16_t& hi, uint16_t& lo) {
+  hi = mmr::f2bf(x);
+  lo = mmr::f2bf(x - mmr::bf2f(hi));
+}
+
+// gal f32 [Np][Dp] -> gs bf16 [Np][2Dp], chunk c (64 wide): [hi c | lo c]
+__global__ __launch_bounds__(256) void knn_split_gallery(const float* __restrict__ gal, int Dp,
+                                                         int64_t total, uint16_t* __restrict__ gs) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // element index in [Np][Dp]
+  if (i >= total) return;
+  const int64_t row = i / Dp;
+  const int k = (int)(i % Dp);
+  uint16_t hi, lo;
+  split_bf16(gal[i], hi, lo);
+  uint16_t* o = gs + row * 2 * Dp + (k / 64) * 128 + (k % 64);
+  o[0] = hi;
+  o[64] = lo;
+}
+
+// qn f32 [Qp][Dp] -> qs bf16 [Qp][3Dp], chunk c: [hi c | hi c | lo c]
+__global__ __launch_bounds__(256) void knn_split_queries(const float* __restrict__ qn, int Dp,
+                                                         int64_t total, uint16_t* __restrict__ qs) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int64_t row = i / Dp;
+  const int k = (int)(i % Dp);
+  uint16_t hi, lo;
+  split_bf16(qn[i], hi, lo);
+  uint16_t* o = qs + row * 3 * Dp + (k / 64) * 192 + (k % 64);
+  o[0] = hi;
+  o[64] = hi;
+  o[128] = lo;
+}
+
+
+__device__ __forceinline__ int xswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+// S[m][n] = inv_g[n] * sum_k' Qs[m][k'] Gs'[n][k'] over K' = 3 Dp; tile 128 x 128 x 64, 4 waves
+// (2x2) of 64x64, glds-staged double buffer with source-address swizzle (same structure as
+// gemm.hip).  Rows of the query block past Qp / gallery past Np never exist (both padded).
+__global__ __launch_bounds__(256, 2) void knn_scores_x3(const uint16_t* __restrict__ qs,
+                                                         const uint16_t* __restrict__ gs,
+                                                         const float* __restrict__ inv_g,
+                                                         float* __restrict__ scores, int Dp,
+                                                         int64_t ldS, int tiles_m, int tiles_n) {
+  constexpr int BK = 64, TILE = 128 * 64;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * TILE];
+  // gallery tiles outer, query tiles inner: the tiles_m query blocks of one gallery tile are
+  // consecutive in the remapped order and share the XCD (and its L2) -> gallery read once
+  const int nwg = tiles_m * tiles_n;
+  const int orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int tn = wg / tiles_m, tm = wg % tiles_m;
+  const int64_t m0 = (int64_t)tm * 128, n0 = (int64_t)tn * 128;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int K3 = 3 * Dp;
+  const int prow_in = lane >> 3, pch = lane & 7;
+  const uint16_t* srcA[4];
+  const uint16_t* srcB[4];
+  int lchk[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = wave * 32 + j * 8 + prow_in;
+    lchk[j] = xswz(row, pch) * 8;
+    srcA[j] = qs + (m0 + row) * K3;
+    srcB[j] = gs + (n0 + row) * 2 * Dp;
+  }
+  auto stage = [&](int sbuf, int t) {
+    const int c = t / 3, part = t % 3;
+    const int ka = t * BK;
+    const int kb = c * 128 + (part == 1 ? 64 : 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint16_t* la = lds + (sbuf * 2 + 0) * TILE + (wave * 32 + j * 8) * BK;
+      uint16_t* lb = lds + (sbuf * 2 + 1) * TILE + (wave * 32 + j * 8) * BK;
+      __builtin_amdgcn_global_load_lds((const void*)(srcA[j] + ka + lchk[j]), (lds_ptr_t)la, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(srcB[j] + kb + lchk[j]), (lds_ptr_t)lb, 16, 0, 0);
+    }
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int nk = K3 / BK;
+  const int fr = lane & 15, fq = lane >> 4;
+  stage(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int sb = kt & 1;
+    if (kt + 1 < nk) stage(sb ^ 1, kt + 1);
+    const uint16_t* la = lds + (sb * 2 + 0) * TILE;
+    const uint16_t* lb = lds + (sb * 2 + 1) * TILE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 a[4], b[4];
+      const int ch = ks * 4 + fq;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rowa = wm * 64 + i * 16 + fr;
+        const int rowb = wn * 64 + i * 16 + fr;
+        a[i] = *(const bf16x8*)(la + rowa * BK + xswz(rowa, ch) * 8);
+        b[i] = *(const bf16x8*)(lb + rowb * BK + xswz(rowb, ch) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // C[row][col]: col = lane&15 (gallery row), row = 4*(lane>>4) + reg (query)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t n = n0 + wn * 64 + j * 16 + fr;
+    const float ig = inv_g[n];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int64_t m = m0 + wm * 64 + i * 16 + fq * 4 + rg;
+        scores[m * ldS + n] = acc[i][j][rg] * ig;
+      }
+    }
   }
 }
 
@@ -411,12 +554,15 @@ struct mmr_index {
   float* gal = nullptr;       // [Np][Dp]
   float* inv_norm = nullptr;  // [Np]
   double* norm64 = nullptr;   // [Np]
+  uint16_t* gs = nullptr;     // [Np][2Dp] bf16 hi/lo split (mode x3)
+  int mode = 1;               // 0: f32 MFMA scores, 1: bf16x3 split scores
   // workspace (single; guarded by mu — searches on one index serialise their enqueue)
   std::mutex mu;
   int64_t ws_q = 0;  // queries the workspace holds
   float* qn = nullptr;
   double* qnorm64 = nullptr;
   float* scores = nullptr;
+  uint16_t* qs = nullptr;  // [ws_q][3Dp]
 };
 
 namespace {
@@ -436,8 +582,10 @@ mmr_status ensure_ws(mmr_index* ix, int64_t nq) {
   if (ix->qn) (void)hipFree(ix->qn);
   if (ix->qnorm64) (void)hipFree(ix->qnorm64);
   if (ix->scores) (void)hipFree(ix->scores);
-  ix->qn = nullptr; ix->qnorm64 = nullptr; ix->scores = nullptr; ix->ws_q = 0;
+  if (ix->qs) (void)hipFree(ix->qs);
+  ix->qn = nullptr; ix->qnorm64 = nullptr; ix->scores = nullptr; ix->qs = nullptr; ix->ws_q = 0;
   MMR_CHECK_HIP(hipMalloc(&ix->qn, sizeof(float) * want * ix->Dp));
+  MMR_CHECK_HIP(hipMalloc(&ix->qs, sizeof(uint16_t) * want * 3 * ix->Dp));
   MMR_CHECK_HIP(hipMalloc(&ix->qnorm64, sizeof(double) * want));
   MMR_CHECK_HIP(hipMalloc(&ix->scores, sizeof(float) * want * ix->Np));
   ix->ws_q = want;
@@ -478,7 +626,7 @@ mmr_status mmr_index_create(const void* gallery, int64_t n, int32_t d, mmr_dtype
   ix->device = device;
   ix->n = n;
   ix->d = d;
-  ix->Dp = (int)round_up(d, 16);
+  ix->Dp = (int)round_up(d, 64);
   ix->Np = round_up(n > 0 ? n : 1, kRowPad);
   ix->idx_base = idx_base;
   auto fail = [&](mmr_status s) {
@@ -488,7 +636,8 @@ mmr_status mmr_index_create(const void* gallery, int64_t n, int32_t d, mmr_dtype
   hipError_t e;
   if ((e = hipMalloc(&ix->gal, sizeof(float) * ix->Np * ix->Dp)) != hipSuccess ||
       (e = hipMalloc(&ix->inv_norm, sizeof(float) * ix->Np)) != hipSuccess ||
-      (e = hipMalloc(&ix->norm64, sizeof(double) * ix->Np)) != hipSuccess) {
+      (e = hipMalloc(&ix->norm64, sizeof(double) * ix->Np)) != hipSuccess ||
+      (e = hipMalloc(&ix->gs, sizeof(uint16_t) * ix->Np * 2 * ix->Dp)) != hipSuccess) {
     mmr::set_error("mmr_index_create: hipMalloc failed: %s", hipGetErrorString(e));
     return fail(MMR_ERR_OOM);
   }
@@ -510,6 +659,11 @@ mmr_status mmr_index_create(const void* gallery, int64_t n, int32_t d, mmr_dtype
   knn_prep_gallery<<<dim3((unsigned)ceil_div(ix->Np, 4)), dim3(256)>>>(
       raw, n, d, ix->gal, ix->Dp, ix->Np, ix->inv_norm, ix->norm64);
   e = hipGetLastError();
+  if (e == hipSuccess) {
+    const int64_t total = ix->Np * ix->Dp;
+    knn_split_gallery<<<dim3((unsigned)ceil_div(total, 256)), dim3(256)>>>(ix->gal, ix->Dp, total, ix->gs);
+    e = hipGetLastError();
+  }
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (raw) (void)hipFree(raw);
   if (e != hipSuccess) {
@@ -526,6 +680,8 @@ mmr_status mmr_index_destroy(mmr_index* ix) {
   if (ix->gal) (void)hipFree(ix->gal);
   if (ix->inv_norm) (void)hipFree(ix->inv_norm);
   if (ix->norm64) (void)hipFree(ix->norm64);
+  if (ix->gs) (void)hipFree(ix->gs);
+  if (ix->qs) (void)hipFree(ix->qs);
   if (ix->qn) (void)hipFree(ix->qn);
   if (ix->qnorm64) (void)hipFree(ix->qnorm64);
   if (ix->scores) (void)hipFree(ix->scores);
@@ -564,38 +720,62 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
   mmr_status s = ensure_ws(ix, nq);
   if (s != MMR_OK) return s;
   hipStream_t st = mmr::as_stream(stream);
-  // |s32 - s64| <= delta; threshold margin 2*delta
-  const float two_delta = 2.0f * (float)(ix->Dp + 16) * 5.9604645e-8f;
+  // |s_approx - s64| <= delta; threshold margin 2*delta
+  const float two_delta =
+      ix->mode == 0 ? 2.0f * (float)(ix->Dp + 16) * 5.9604645e-8f
+                    : 2.0f * ((float)(3 * ix->Dp + 16) * 5.9604645e-8f + 4.0f * 1.5258789e-5f);
   const int64_t chunk = ix->ws_q;
   for (int64_t c0 = 0; c0 < nq; c0 += chunk) {
     const int64_t cq = nq - c0 < chunk ? nq - c0 : chunk;
     const float* qc = q + c0 * ix->d;
     int64_t Qp;
-    int wq, wn;
-    if (cq <= 64) { wq = 1; wn = 4; } else if (cq <= 128) { wq = 2; wn = 2; } else { wq = 4; wn = 1; }
-    Qp = round_up(cq, 64 * wq);
-    knn_prep_queries<<<dim3((unsigned)ceil_div(Qp, 4)), dim3(256), 0, st>>>(
-        qc, cq, ix->d, ix->qn, ix->Dp, Qp, ix->qnorm64);
-    MMR_LAUNCH_CHECK();
-    const int n_qblocks = (int)(Qp / (64 * wq));
-    const int n_gtiles = (int)ceil_div(ix->Np, 64 * wn);
-    const unsigned grid = (unsigned)(round_up(n_gtiles, 8) * n_qblocks);
-    if (wq == 1)
-      knn_scores<1, 4><<<grid, 256, 0, st>>>(ix->qn, ix->gal, ix->inv_norm, ix->scores, ix->Dp,
-                                              ix->Np, n_gtiles, n_qblocks);
-    else if (wq == 2)
-      knn_scores<2, 2><<<grid, 256, 0, st>>>(ix->qn, ix->gal, ix->inv_norm, ix->scores, ix->Dp,
-                                              ix->Np, n_gtiles, n_qblocks);
-    else
-      knn_scores<4, 1><<<grid, 256, 0, st>>>(ix->qn, ix->gal, ix->inv_norm, ix->scores, ix->Dp,
-                                              ix->Np, n_gtiles, n_qblocks);
-    MMR_LAUNCH_CHECK();
+    if (ix->mode == 1) {
+      Qp = round_up(cq, 128);
+      knn_prep_queries<<<dim3((unsigned)ceil_div(Qp, 4)), dim3(256), 0, st>>>(
+          qc, cq, ix->d, ix->qn, ix->Dp, Qp, ix->qnorm64);
+      MMR_LAUNCH_CHECK();
+      const int64_t total = Qp * ix->Dp;
+      knn_split_queries<<<dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, st>>>(ix->qn, ix->Dp, total, ix->qs);
+      MMR_LAUNCH_CHECK();
+      const int tiles_m = (int)(Qp / 128), tiles_n = (int)(ix->Np / 128);
+      knn_scores_x3<<<dim3((unsigned)(tiles_m * tiles_n)), dim3(256), 0, st>>>(
+          ix->qs, ix->gs, ix->inv_norm, ix->scores, ix->Dp, ix->Np, tiles_m, tiles_n);
+      MMR_LAUNCH_CHECK();
+    } else {
+      int wq, wn;
+      if (cq <= 64) { wq = 1; wn = 4; } else if (cq <= 128) { wq = 2; wn = 2; } else { wq = 4; wn = 1; }
+      Qp = round_up(cq, 64 * wq);
+      knn_prep_queries<<<dim3((unsigned)ceil_div(Qp, 4)), dim3(256), 0, st>>>(
+          qc, cq, ix->d, ix->qn, ix->Dp, Qp, ix->qnorm64);
+      MMR_LAUNCH_CHECK();
+      const int n_qblocks = (int)(Qp / (64 * wq));
+      const int n_gtiles = (int)ceil_div(ix->Np, 64 * wn);
+      const unsigned grid = (unsigned)(round_up(n_gtiles, 8) * n_qblocks);
+      if (wq == 1)
+        knn_scores<1, 4><<<grid, 256, 0, st>>>(ix->qn, ix->gal, ix->inv_norm, ix->scores, ix->Dp,
+                                                ix->Np, n_gtiles, n_qblocks);
+      else if (wq == 2)
+        knn_scores<2, 2><<<grid, 256, 0, st>>>(ix->qn, ix->gal, ix->inv_norm, ix->scores, ix->Dp,
+                                                ix->Np, n_gtiles, n_qblocks);
+      else
+        knn_scores<4, 1><<<grid, 256, 0, st>>>(ix->qn, ix->gal, ix->inv_norm, ix->scores, ix->Dp,
+                                                ix->Np, n_gtiles, n_qblocks);
+      MMR_LAUNCH_CHECK();
+    }
     knn_select<<<dim3((unsigned)cq), dim3(kSelThreads), 0, st>>>(
         ix->scores, ix->Np, ix->n, k, two_delta, qc, ix->d, ix->qnorm64, ix->gal, ix->Dp,
         ix->norm64, ix->idx_base, out_idx + c0 * k, out_score ? out_score + c0 * k : nullptr,
         out_score64 ? out_score64 + c0 * k : nullptr, out_status ? out_status + c0 : nullptr);
     MMR_LAUNCH_CHECK();
   }
+  return MMR_OK;
+}
+
+mmr_status mmr_index_set_mode(mmr_index* ix, int32_t mode) {
+  mmr::clear_error();
+  MMR_REQUIRE(ix != nullptr && (mode == 0 || mode == 1), "mmr_index_set_mode: bad arguments");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  ix->mode = mode;
   return MMR_OK;
 }
 

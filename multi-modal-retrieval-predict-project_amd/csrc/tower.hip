@@ -259,17 +259,44 @@ __global__ __launch_bounds__(256) void bert_attention(const uint16_t* __restrict
 // One wave per (image, window, head); 4 units per block.  Window of ws*ws = 49 tokens padded to
 // 64, head_dim 32.  The cyclic shift + window partition are folded into the token gather (and
 // the reverse shift into the scatter of the output): rolled coordinate (hr, wr) reads token
-// ((hr+shift)%H, (wr+shift)%W).  S^T = K . Q^T (2x2 tiles of 32x32x16, 2 k-steps), + relative
-// position bias table[(yi-yj+ws-1)*(2ws-1) + (xi-xj+ws-1)][head] + shift-region mask (-100),
-// softmax over keys in registers, O^T = V^T . P^T with V^T staged per wave in LDS.
+// ((hr+shift)%H, (wr+shift)%W).  S^T = K . Q^T (2x2 tiles of 32x32x16, 2 k-steps), + a dense
+// additive bias (relative-position bias + shift-region mask -100 + padded keys -inf) prepared
+// once per block by swin_attn_bias for the <= 4 window types (interior / last column / last row
+// / corner), softmax over keys in registers, O^T = V^T . P^T with V^T staged per wave in LDS.
 constexpr int SW_DH = 32;
 
 __device__ __forceinline__ int region_of(int rc, int H, int ws, int shift) {
   return rc < H - ws ? 0 : (rc < H - shift ? 1 : 2);
 }
 
+// bias[type][head][i][j] (64x64, f32): type = 2*(last window row) + (last window column)
+__global__ __launch_bounds__(256) void swin_attn_bias(const float* __restrict__ table,
+                                                      float* __restrict__ bias, int heads, int ws,
+                                                      int H, int shift, int ntypes) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)ntypes * heads * 64 * 64) return;
+  const int j = (int)(idx % 64), i = (int)((idx / 64) % 64);
+  const int hh = (int)((idx / 4096) % heads), type = (int)(idx / (4096 * (int64_t)heads));
+  const int N = ws * ws;
+  float v = 0.f;
+  if (j >= N) {
+    v = -FLT_MAX;
+  } else if (i < N) {
+    const int yi = i / ws, xi = i % ws, yj = j / ws, xj = j % ws;
+    v = table[((yi - yj + ws - 1) * (2 * ws - 1) + (xi - xj + ws - 1)) * heads + hh];
+    if (shift > 0) {
+      const int nw = H / ws;
+      const int wy = (type >> 1) ? nw - 1 : 0, wx = (type & 1) ? nw - 1 : 0;
+      const int ri = region_of(wy * ws + yi, H, ws, shift) * 3 + region_of(wx * ws + xi, H, ws, shift);
+      const int rj = region_of(wy * ws + yj, H, ws, shift) * 3 + region_of(wx * ws + xj, H, ws, shift);
+      if (ri != rj) v += -100.0f;
+    }
+  }
+  bias[idx] = v;
+}
+
 __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __restrict__ qkv,
-                                                             const float* __restrict__ table,
+                                                             const float* __restrict__ bias,
                                                              uint16_t* __restrict__ out,
                                                              int64_t units, int H, int C,
                                                              int heads, int ws, int shift) {
@@ -286,9 +313,10 @@ __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __r
   const int64_t bi = wi / (nwin1 * nwin1);
   const int wy = win / nwin1, wx = win % nwin1;
   const int N = ws * ws;
+  const int type = shift > 0 ? ((wy == nwin1 - 1) ? 2 : 0) + ((wx == nwin1 - 1) ? 1 : 0) : 0;
+  const float* bt = bias + ((int64_t)type * heads + hh) * 4096;
   uint16_t(*vt)[64 + 4] = vt_all[wave];
   int* tok = tok_all[wave];
-  // token of local index i (padded entries -> -1)
   {
     const int i = lane;
     int t = -1;
@@ -300,7 +328,6 @@ __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __r
     tok[i] = t;
   }
   __builtin_amdgcn_wave_barrier();
-  // V^T staging: 64 keys x 32 d = 256 chunks of 8 -> 4 per lane
   for (int c = lane; c < 256; c += 64) {
     const int key = c >> 2, ch = c & 3;
     const int t = tok[key];
@@ -314,7 +341,6 @@ __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __r
 
   const int r = lane & 31, hf = lane >> 5;
   const float scale = 0.17677669529663687f;  // 32^-0.5
-  // Q fragments (B operand) for the two query tiles, K fragments (A operand) for two key tiles
   bf16x8 qf[2][2], kf[2][2];
 #pragma unroll
   for (int t2 = 0; t2 < 2; ++t2) {
@@ -326,15 +352,9 @@ __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __r
       kf[t2][ks] = tq >= 0 ? *(const bf16x8*)(qkv + (int64_t)tq * 3 * C + C + hh * SW_DH + ks * 16 + 8 * hf) : z;
     }
   }
-  const int tsz = 2 * ws - 1;
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int qi = qt * 32 + r;  // this lane's query (local index)
-    const bool qvalid = qi < N;
-    const int qy = qi / ws, qx = qi % ws;
-    int qreg = 0;
-    if (shift > 0 && qvalid)
-      qreg = region_of(wy * ws + qy, H, ws, shift) * 3 + region_of(wx * ws + qx, H, ws, shift);
     f32x16 s[2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
@@ -343,23 +363,20 @@ __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __r
       for (int ks = 0; ks < 2; ++ks)
         s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kt][ks], qf[qt][ks], s[kt], 0, 0, 0);
     }
+    const float* brow = bt + qi * 64;
     float mloc = -FLT_MAX;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
-      for (int rg = 0; rg < 16; ++rg) {
-        const int kj = kt * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * hf;
-        float v = -FLT_MAX;
-        if (kj < N && qvalid) {
-          const int ky = kj / ws, kx = kj % ws;
-          v = s[kt][rg] * scale + table[((qy - ky + ws - 1) * tsz + (qx - kx + ws - 1)) * heads + hh];
-          if (shift > 0) {
-            const int kreg = region_of(wy * ws + ky, H, ws, shift) * 3 + region_of(wx * ws + kx, H, ws, shift);
-            if (kreg != qreg) v += -100.0f;
-          }
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 bb = *(const float4*)(brow + kt * 32 + 8 * g4 + 4 * hf);
+        const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = s[kt][4 * g4 + e] * scale + bv[e];
+          s[kt][4 * g4 + e] = v;
+          mloc = fmaxf(mloc, v);
         }
-        s[kt][rg] = v;
-        mloc = fmaxf(mloc, v);
       }
     }
     mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
@@ -368,8 +385,7 @@ __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __r
     for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
       for (int rg = 0; rg < 16; ++rg) {
-        const int kj = kt * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * hf;
-        const float p = kj < N ? __expf(s[kt][rg] - mloc) : 0.0f;
+        const float p = __expf(s[kt][rg] - mloc);
         s[kt][rg] = p;
         psum += p;
       }
@@ -390,7 +406,7 @@ __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __r
         o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o, 0, 0, 0);
       }
     }
-    if (qvalid) {
+    if (qi < N) {
       const float inv = 1.0f / psum;
       uint16_t* orow = out + (int64_t)tok[qi] * C + hh * SW_DH;
 #pragma unroll
@@ -664,18 +680,32 @@ mmr_status mmr_bert_attention(const uint16_t* qkv, const int64_t* mask01, uint16
   return MMR_OK;
 }
 
-mmr_status mmr_swin_window_attention(const uint16_t* qkv, const float* relpos_table,
-                                     uint16_t* out, int32_t b, int32_t hw, int32_t c,
-                                     int32_t heads, int32_t ws, int32_t shift, void* stream) {
+mmr_status mmr_swin_attn_bias(const float* relpos_table, float* bias, int32_t heads, int32_t ws,
+                              int32_t hw, int32_t shift, void* stream) {
   mmr::clear_error();
-  MMR_REQUIRE(qkv && relpos_table && out, "mmr_swin_window_attention: NULL pointer");
+  MMR_REQUIRE(relpos_table && bias, "mmr_swin_attn_bias: NULL pointer");
+  MMR_REQUIRE(heads > 0 && ws > 0 && ws * ws <= 64 && hw % ws == 0 && shift >= 0 && shift < ws,
+              "mmr_swin_attn_bias: heads=%d ws=%d hw=%d shift=%d", heads, ws, hw, shift);
+  const int ntypes = shift > 0 ? 4 : 1;
+  const int64_t n = (int64_t)ntypes * heads * 4096;
+  swin_attn_bias<<<dim3((unsigned)mmr::ceil_div(n, 256)), 256, 0, mmr::as_stream(stream)>>>(
+      relpos_table, bias, heads, ws, hw, shift, ntypes);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_swin_window_attention(const uint16_t* qkv, const float* bias, uint16_t* out,
+                                     int32_t b, int32_t hw, int32_t c, int32_t heads, int32_t ws,
+                                     int32_t shift, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(qkv && bias && out, "mmr_swin_window_attention: NULL pointer");
   MMR_REQUIRE(heads > 0 && c == heads * SW_DH, "mmr_swin_window_attention: c=%d heads=%d (head_dim 32 only)", c, heads);
   MMR_REQUIRE(ws > 0 && ws * ws <= 64 && hw % ws == 0, "mmr_swin_window_attention: window %d / resolution %d", ws, hw);
   MMR_REQUIRE(shift >= 0 && shift < ws, "mmr_swin_window_attention: shift %d", shift);
   if (b == 0) return MMR_OK;
   const int64_t units = (int64_t)b * (hw / ws) * (hw / ws) * heads;
   swin_window_attention<<<dim3((unsigned)mmr::ceil_div(units, 4)), 256, 0, mmr::as_stream(stream)>>>(
-      qkv, relpos_table, out, units, hw, c, heads, ws, shift);
+      qkv, bias, out, units, hw, c, heads, ws, shift);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }

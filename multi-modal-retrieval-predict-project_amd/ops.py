@@ -58,11 +58,20 @@ def bert_attention(qkv, mask, heads, dh=64):
     return ctx
 
 
-def swin_window_attention(qkv, table, hw, heads, ws, shift):
+def swin_attn_bias(table, heads, ws, hw, shift):
+    """Dense [types][heads][64][64] f32 bias (rel-pos + shift mask + padded keys) for one block."""
+    nt = 4 if shift > 0 else 1
+    bias = torch.empty((nt, heads, 64, 64), dtype=torch.float32, device=table.device)
+    _chk(_L().mmr_swin_attn_bias(_lib.ptr(table), _lib.ptr(bias), heads, ws, hw, shift, _s(table)),
+         "mmr_swin_attn_bias")
+    return bias
+
+
+def swin_window_attention(qkv, bias, hw, heads, ws, shift):
     B = qkv.shape[0]
     C = qkv.shape[-1] // 3
     out = torch.empty(qkv.shape[:-1] + (C,), dtype=torch.bfloat16, device=qkv.device)
-    _chk(_L().mmr_swin_window_attention(_lib.ptr(qkv), _lib.ptr(table), _lib.ptr(out), B, hw, C, heads, ws,
+    _chk(_L().mmr_swin_window_attention(_lib.ptr(qkv), _lib.ptr(bias), _lib.ptr(out), B, hw, C, heads, ws,
                                         shift, _s(qkv)), "mmr_swin_window_attention")
     return out
 

@@ -51,7 +51,7 @@ class RetrievalEngine(abc.ABC):
 class GalleryIndex:
     """Owning wrapper of an mmr_index (one device-resident gallery shard)."""
 
-    def __init__(self, embs, device=None, idx_base: int = 0):
+    def __init__(self, embs, device=None, idx_base: int = 0, mode: str = "x3"):
         _lib.require_gpu()
         L = _lib.lib()
         if device is None:
@@ -77,6 +77,9 @@ class GalleryIndex:
                    "mmr_index_create")
         del keep
         self._h = h
+        if mode not in ("x3", "f32"):
+            raise ValueError(f"scan mode {mode!r} (x3 | f32)")
+        _lib.check(L.mmr_index_set_mode(h, 1 if mode == "x3" else 0), "mmr_index_set_mode")
         self.n, self.d, self.idx_base = int(n), int(d), int(idx_base)
 
     def reserve(self, max_q: int):

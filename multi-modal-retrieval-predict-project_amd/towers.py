@@ -46,18 +46,26 @@ class SwinTower:
         self.pe_w, self.pe_b = _bf(wp, dev), _f(sd["patch_embed.proj.bias"], dev)
         self.pe_g, self.pe_beta = _f(sd["patch_embed.norm.weight"], dev), _f(sd["patch_embed.norm.bias"], dev)
         self.stages = []
+        res = self.cfg["img_size"] // self.cfg["patch"]
+        ws0 = self.cfg["window_size"]
         for i, depth in enumerate(self.cfg["depths"]):
+            if i > 0:
+                res //= 2
             st = {"blocks": []}
             if i > 0:
                 p = f"layers.{i}.downsample."
                 st["ds_g"], st["ds_b"] = _f(sd[p + "norm.weight"], dev), _f(sd[p + "norm.bias"], dev)
                 st["ds_w"] = _bf(sd[p + "reduction.weight"], dev)
+            ws = min(ws0, res)
             for j in range(depth):
                 p = f"layers.{i}.blocks.{j}."
+                shift = 0 if (j % 2 == 0 or res <= ws0) else ws0 // 2
+                table = _f(sd[p + "attn.relative_position_bias_table"], dev)
                 st["blocks"].append({
+                    "shift": shift,
+                    "bias": ops.swin_attn_bias(table, self.cfg["num_heads"][i], ws, res, shift),
                     "n1g": _f(sd[p + "norm1.weight"], dev), "n1b": _f(sd[p + "norm1.bias"], dev),
                     "qkv_w": _bf(sd[p + "attn.qkv.weight"], dev), "qkv_b": _f(sd[p + "attn.qkv.bias"], dev),
-                    "table": _f(sd[p + "attn.relative_position_bias_table"], dev),
                     "proj_w": _bf(sd[p + "attn.proj.weight"], dev), "proj_b": _f(sd[p + "attn.proj.bias"], dev),
                     "n2g": _f(sd[p + "norm2.weight"], dev), "n2b": _f(sd[p + "norm2.bias"], dev),
                     "fc1_w": _bf(sd[p + "mlp.fc1.weight"], dev), "fc1_b": _f(sd[p + "mlp.fc1.bias"], dev),
@@ -85,10 +93,9 @@ class SwinTower:
             heads = cfg["num_heads"][i]
             ws = min(ws0, H)
             for j, bk in enumerate(st["blocks"]):
-                shift = 0 if (j % 2 == 0 or H <= ws0) else ws0 // 2
                 h = ops.layernorm(x, bk["n1g"], bk["n1b"], 1e-5)
                 qkv = ops.linear(h, bk["qkv_w"], bk["qkv_b"])
-                a = ops.swin_window_attention(qkv, bk["table"], H, heads, ws, shift)
+                a = ops.swin_window_attention(qkv, bk["bias"], H, heads, ws, bk["shift"])
                 x = ops.linear(a, bk["proj_w"], bk["proj_b"], residual=x)
                 h = ops.layernorm(x, bk["n2g"], bk["n2b"], 1e-5)
                 h = ops.linear(h, bk["fc1_w"], bk["fc1_b"], act=1)

@@ -26,8 +26,8 @@ def _search(G, Q, K, **kw):
     return i.cpu().numpy(), s.cpu().numpy(), s64.cpu().numpy(), st.cpu().numpy()
 
 
-def _exact_check(G, Q, K):
-    gi, gs, g64, st = _search(G, Q, K)
+def _exact_check(G, Q, K, mode="x3"):
+    gi, gs, g64, st = _search(G, Q, K, mode=mode)
     assert (st == 0).all()
     ei, es = oknn.exact_topk(Q, G, K)
     kk = ei.shape[1]
@@ -55,6 +55,13 @@ def test_knn_matches_reference_golden(name):
             gi, gs = _exact_check(G, Qm, K)
             ok, msg = oknn.topk_equivalent(f[key], f[f"score_k{K}"], gi, gs, tie_tol=1e-6, score_tol=1e-4)
             assert ok, msg
+
+
+@pytest.mark.parametrize("mode", ["x3", "f32"])
+def test_knn_scan_modes_agree(mode):
+    G = synthetic.gauss_gallery(20000, 768, 41)
+    Qm = synthetic.gauss_gallery(200, 768, 42)
+    _exact_check(G, Qm, 50, mode=mode)
 
 
 @pytest.mark.parametrize("N,D,Q,K", [(1, 8, 3, 5), (7, 100, 1, 10), (300, 64, 65, 256), (1000, 1024, 129, 50),

@@ -121,7 +121,8 @@ def test_swin_window_attention(H, heads, shift):
     qkv = torch.randn(B, H, H, 3 * C, generator=g)
     table = torch.randn(169, heads, generator=g)
     ref = _swin_attn_ref(bf(qkv).float(), table, H, heads, ws, shift)
-    y = ops.swin_window_attention(bf(qkv).to(DEV), table.to(DEV), H, heads, ws, shift)
+    y = ops.swin_window_attention(bf(qkv).to(DEV), ops.swin_attn_bias(table.to(DEV), heads, ws, H, shift),
+                                  H, heads, ws, shift)
     assert rel_err(y, ref) < 2e-2
 
 
