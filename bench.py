@@ -102,11 +102,11 @@ def main():
             e1.record(stream)
             ev_pairs.append((e0, e1))
         if world > 1:
-            gi = torch.empty((world,) + tuple(i.shape), dtype=i.dtype, device=dev)
-            gs = torch.empty((world,) + tuple(s64.shape), dtype=s64.dtype, device=dev)
+            gi = torch.empty((world * i.shape[0], K), dtype=i.dtype, device=dev)
+            gs = torch.empty((world * s64.shape[0], K), dtype=s64.dtype, device=dev)
             dist.all_gather_into_tensor(gi, i)
             dist.all_gather_into_tensor(gs, s64)
-            i, s, _ = merge_topk(gs, gi, K)
+            i, s, _ = merge_topk(gs.view(world, -1, K), gi.view(world, -1, K), K)
         return i, s
 
     for _ in range(a.warmup):
@@ -152,7 +152,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(a, G, qbatch if model is None else out_q_for_cpu(model, imgs, ids, mask))
+        cpu = cpu_baseline(a, G, qbatch) if model is None else cpu_baseline_full(a, G)
 
     if rank == 0:
         line = {
@@ -178,29 +178,38 @@ def main():
         dist.destroy_process_group()
 
 
-def out_q_for_cpu(model, imgs, ids, mask):
-    return None
-
-
-def cpu_baseline(a, G, qdev):
-    """Oracle CPU path (tests-only infrastructure, timed here as the baseline): cosine + top-K in
-    numpy f32/BLAS on a bounded query sample, all host cores."""
+def cpu_baseline_full(a, G):
+    """Oracle CPU path (tests-only infrastructure, timed here as the baseline) on a bounded sample:
+    Swin-T + BERT-base fp32 towers (torch CPU, all host cores) + text/image heads + numpy cosine
+    top-K over the same gallery — the reference's PyTorch-CPU path restated (oracle/towers.py)."""
     import numpy as np
     import torch
+    from mmr_amd import synthetic
+    from mmr_amd.model import init_head_state
+    from mmr_amd.towers import BERT_BASE, SWIN_T, init_bert_state, init_swin_state
     from oracle import knn as oknn
+    from oracle import towers as otw
     threads = torch.get_num_threads()
-    nq = a.cpu_sample_queries or 64
-    Q = qdev[:nq].float().cpu().numpy() if qdev is not None else np.random.default_rng(0).standard_normal((nq, a.dim), dtype=np.float32)
-    oknn.sklearn_topk(Q[:4], G, a.k)  # warm-up
-    ts = []
-    for _ in range(3):
-        t0 = time.perf_counter()
-        oknn.sklearn_topk(Q, G, a.k)
-        ts.append(time.perf_counter() - t0)
-    t = sorted(ts)[1]
-    return {"value": nq * G.shape[0] / t, "unit": "cosine_pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{nq} queries x {G.shape[0]}x{G.shape[1]} gallery, numpy cosine + argsort top-{a.k} "
-                      f"(restated sklearn path), median of 3, CPU: {cpu_model()}"}
+    nb = a.cpu_sample_queries or 8
+    ssd, bsd = init_swin_state(SWIN_T, 2709), init_bert_state(BERT_BASE, 2710)
+    hsd = init_head_state(768, 768, a.dim, 2711)
+    img = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(nb, synthetic.SEED)))
+    ids, mask = (torch.from_numpy(x) for x in synthetic.reports(nb, 128, synthetic.SEED + 100))
+
+    def run(n):
+        with torch.no_grad():
+            (g, p), t = otw.backbones_forward(img[:n], ids[:n], mask[:n], ssd, bsd, SWIN_T, BERT_BASE)
+            qi = otw.heads(g, p, t, hsd, "image")["joint_emb"]
+            qt = otw.heads(g, p, t, hsd, "text")["joint_emb"]
+        oknn.sklearn_topk(torch.cat([qi, qt]).numpy(), G, a.k)
+    run(1)
+    t0 = time.perf_counter()
+    run(nb)
+    t = time.perf_counter() - t0
+    return {"value": nb / t, "unit": "query_embeddings/s", "cores": threads, "kind": "port",
+            "sample": f"{nb} (image, 128-token report) pairs: fp32 torch-CPU Swin-T + BERT-base + image/text "
+                      f"heads + numpy cosine/argsort top-{a.k} over {G.shape[0]}x{G.shape[1]} (oracle/towers.py, "
+                      f"oracle/knn.py), one timed run after warm-up, CPU: {cpu_model()}"}
 
 
 if __name__ == "__main__":
