@@ -136,6 +136,9 @@ class BertTower:
                 "ln2_g": _f(sd[p + "output.LayerNorm.weight"], dev), "ln2_b": _f(sd[p + "output.LayerNorm.bias"], dev),
             })
         self.hidden = self.word.shape[1]
+        # optional list: (start, end) torch.cuda.Event pairs around every FFN1 GEMM launch (bench
+        # roofline of the dominant kernel; events ride torch's current stream = the launch stream)
+        self.ffn1_events = None
 
     def forward(self, input_ids, attention_mask=None):
         """(B, L) ids/mask -> (B, L, C) bf16 last_hidden_state.  L is truncated to
@@ -156,7 +159,14 @@ class BertTower:
             ctx = ops.bert_attention(qkv, mask, heads, self.hidden // heads)
             a = ops.linear(ctx, ly["o_w"], ly["o_b"], residual=h)
             h = ops.layernorm(a, ly["ln1_g"], ly["ln1_b"], 1e-12)
-            f = ops.linear(h, ly["i_w"], ly["i_b"], act=1)
+            if self.ffn1_events is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                f = ops.linear(h, ly["i_w"], ly["i_b"], act=1)
+                e1.record()
+                self.ffn1_events.append((e0, e1))
+            else:
+                f = ops.linear(h, ly["i_w"], ly["i_b"], act=1)
             f = ops.linear(f, ly["f_w"], ly["f_b"], residual=h)
             h = ops.layernorm(f, ly["ln2_g"], ly["ln2_b"], 1e-12)
         return h

@@ -4,11 +4,12 @@ import sqlite3
 import sys
 
 
-def summary(db):
+def summary(db, by_grid=False):
     c = sqlite3.connect(db)
+    grp = "name, grid_x" if by_grid else "name"
     rows = c.execute("select name, count(*), avg(duration), min(duration), max(duration), sum(duration), "
                      "max(vgpr_count), max(accum_vgpr_count), max(lds_size), max(grid_x), max(workgroup_x) "
-                     "from kernels group by name order by sum(duration) desc").fetchall()
+                     f"from kernels group by {grp} order by sum(duration) desc").fetchall()
     tot = sum(r[5] for r in rows) or 1
     out = [f"{'kernel':<70} {'calls':>6} {'avg_us':>10} {'min_us':>10} {'max_us':>10} {'total_ms':>10} {'pct':>6}  vgpr agpr lds grid wg"]
     for r in rows:
@@ -20,7 +21,8 @@ def summary(db):
 
 
 if __name__ == "__main__":
-    s = summary(sys.argv[1])
+    args = [x for x in sys.argv[1:] if not x.startswith("--")]
+    s = summary(args[0], by_grid="--by-grid" in sys.argv)
     print(s)
-    if len(sys.argv) > 2:
-        open(sys.argv[2], "w").write(s + "\n")
+    if len(args) > 1:
+        open(args[1], "w").write(s + "\n")
