@@ -34,7 +34,10 @@ def bf(x):
 
 @pytest.mark.parametrize("M,N,K,act,bias,res", [(1000, 96, 96, 0, True, False), (513, 2304, 768, 0, True, False),
                                                 (300, 3072, 768, 1, True, False), (257, 768, 3072, 0, True, True),
-                                                (4096, 192, 384, 0, False, False), (77, 288, 64, 1, True, True)])
+                                                (4096, 192, 384, 0, False, False), (77, 288, 64, 1, True, True),
+                                                (16461, 3072, 768, 1, True, False),     # 256x256 tiles, M tail
+                                                (32768, 768, 768, 0, True, True),       # 256x128 tiles
+                                                (32000, 768, 3072, 0, True, True)])
 def test_linear_bf16(M, N, K, act, bias, res):
     g = torch.Generator().manual_seed(M + N + K)
     x = torch.randn(M, K, generator=g)
