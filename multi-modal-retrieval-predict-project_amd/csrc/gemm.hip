@@ -160,14 +160,19 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tn(const uint16_t* __restric
 
 // ---------------------------------------------------------------- large-tile variant
 // For the big MFMA-bound shapes (BERT: M = B*128, N >= 768, K >= 768; Swin stage 3-4): 512
-// threads = 8 waves (WM x WN), wave tile (MT*16) x (NT*16), workgroup tile BM x BN with BM = 256
-// and BN = 256 (2x4 waves of 128x64) or 128 (4x2 waves of 64x64).  One workgroup per CU (LDS
-// 96-128 KiB), 2 waves per SIMD.  Same glds + source-swizzle staging; the loads of k-tile t+1 are
-// ALL issued at the start of tile t (before its 2*MT*NT MFMAs per wave), so the end-of-tile
-// vmcnt(0) + barrier finds them landed: arithmetic intensity per staged byte doubles vs 128x128.
+// threads = 8 waves (WM x WN), wave tile (MT*16) x (NT*16), workgroup tile TBM x TBN (256 x 256
+// or 256 x 128), one workgroup per CU, 2 waves per SIMD.  K is staged in KB-deep slices through
+// a STAGES-deep LDS ring filled by glds (source-swizzled, lane-linear per wave instruction);
+// STAGES-2 slices stay in flight across each barrier (counted vmcnt + raw s_barrier —
+// __syncthreads would drain them, cdna_hip_programming.md §5 "Pipelining across barriers").
 constexpr int vmcnt_imm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14); }
 
-template <int WM, int WN, int MT, int NT, int STAGES, int ACT, bool HAS_BIAS, bool HAS_RES>
+template <int KB>
+__device__ __forceinline__ int swzk(int row, int chunk) {
+  return KB == 64 ? (chunk ^ ((row >> 1) & 7)) : (chunk ^ ((row >> 1) & 3));  // conflict-free b128 reads
+}
+
+template <int WM, int WN, int MT, int NT, int KB, int STAGES, int ACT, bool HAS_BIAS, bool HAS_RES>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_tn_big(const uint16_t* __restrict__ X,
                                                            const uint16_t* __restrict__ W,
                                                            const float* __restrict__ bias,
@@ -175,9 +180,12 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_tn_big(const uint16_t* __res
                                                            uint16_t* __restrict__ Y, int64_t M,
                                                            int N, int K, int tiles_m, int tiles_n) {
   constexpr int TBM = WM * MT * 16, TBN = WN * NT * 16;
-  constexpr int TA = TBM * BK, TB = TBN * BK;       // bf16 elements per stage
-  constexpr int CA = TBM * 8 / 512, CB = TBN * 8 / 512;  // glds per thread per operand per stage
-  extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];  // [2][TA + TB]
+  constexpr int CH = KB / 8;                 // 16-B chunks per LDS row
+  constexpr int RPI = 64 / CH;               // rows per glds wave instruction (1 KiB)
+  constexpr int TA = TBM * KB, TB = TBN * KB;  // bf16 elements per stage
+  constexpr int CA = TBM * CH / 512, CB = TBN * CH / 512;  // glds per thread per operand
+  constexpr int KS = KB / 32;                // 32-deep MFMA k-steps per slice
+  extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];  // [STAGES][TA + TB]
 
   const int nwg = tiles_m * tiles_n;
   const int orig = blockIdx.x;
@@ -189,41 +197,42 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_tn_big(const uint16_t* __res
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
 
-  // glds: instruction j of wave w covers LDS rows 8*(w + 8j) .. +7 of an operand tile
-  const int prow_in = lane >> 3, pch = lane & 7;
+  const int prow_in = lane / CH, pch = lane % CH;
   const uint16_t* srcA[CA];
   const uint16_t* srcB[CB];
   int lcA[CA], lcB[CB];
 #pragma unroll
   for (int j = 0; j < CA; ++j) {
-    const int row = 8 * (wave + 8 * j) + prow_in;
-    lcA[j] = swz(row, pch) * 8;
+    const int row = RPI * (wave + 8 * j) + prow_in;
+    lcA[j] = swzk<KB>(row, pch) * 8;
     const int64_t gm = m0 + row;
     srcA[j] = gm < M ? X + gm * K : nullptr;
   }
 #pragma unroll
   for (int j = 0; j < CB; ++j) {
-    const int row = 8 * (wave + 8 * j) + prow_in;
-    lcB[j] = swz(row, pch) * 8;
+    const int row = RPI * (wave + 8 * j) + prow_in;
+    lcB[j] = swzk<KB>(row, pch) * 8;
     const int gn = n0 + row;
     srcB[j] = gn < N ? W + (int64_t)gn * K : nullptr;
   }
   const uint16_t* zp = (const uint16_t*)g_zero_page;
-  auto stage = [&](int s, int k0) {
+  // one glds piece (1 KiB per wave): pieces 0..CA-1 stage A, CA..CA+CB-1 stage B
+  auto stage_piece = [&](int s, int k0, int p) {
     uint16_t* la = dsm + s * (TA + TB);
-    uint16_t* lb = la + TA;
-#pragma unroll
-    for (int j = 0; j < CA; ++j) {
-      const int k = k0 + lcA[j];
-      const uint16_t* a = (srcA[j] && k < K) ? srcA[j] + k : zp;
-      __builtin_amdgcn_global_load_lds((const void*)a, (lds_ptr_t)(la + 8 * (wave + 8 * j) * BK), 16, 0, 0);
-    }
-#pragma unroll
-    for (int j = 0; j < CB; ++j) {
+    if (p < CA) {
+      const int k = k0 + lcA[p];
+      const uint16_t* a = (srcA[p] && k < K) ? srcA[p] + k : zp;
+      __builtin_amdgcn_global_load_lds((const void*)a, (lds_ptr_t)(la + RPI * (wave + 8 * p) * KB), 16, 0, 0);
+    } else {
+      const int j = p - CA;
       const int k = k0 + lcB[j];
       const uint16_t* b = (srcB[j] && k < K) ? srcB[j] + k : zp;
-      __builtin_amdgcn_global_load_lds((const void*)b, (lds_ptr_t)(lb + 8 * (wave + 8 * j) * BK), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)b, (lds_ptr_t)(la + TA + RPI * (wave + 8 * j) * KB), 16, 0, 0);
     }
+  };
+  auto stage = [&](int s, int k0) {
+#pragma unroll
+    for (int p = 0; p < CA + CB; ++p) stage_piece(s, k0, p);
   };
 
   f32x4 acc[MT][NT];
@@ -232,67 +241,94 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_tn_big(const uint16_t* __res
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (K + BK - 1) / BK;
+  const int nk = (K + KB - 1) / KB;
   const int fr = lane & 15, fq = lane >> 4;
-  constexpr int PER_TILE = CA + CB;  // glds per thread per k-tile
-  // STAGES-deep ring: tiles kt+1 .. kt+STAGES-2 stay in flight across the barrier (counted vmcnt,
-  // raw s_barrier — __syncthreads would drain them, cdna_hip_programming.md §5 "Pipelining
-  // across barriers"); tile kt+STAGES-1 is issued right after the barrier into the slot read
-  // in iteration kt-1.
+  constexpr int PER_TILE = CA + CB;
 #pragma unroll
   for (int p = 0; p < STAGES - 1; ++p)
-    if (p < nk) stage(p, p * BK);
+    if (p < nk) stage(p, p * KB);
   for (int kt = 0; kt < nk; ++kt) {
-    const int after = min(STAGES - 2, nk - 1 - kt);  // tiles issued after kt still allowed in flight
-    if (STAGES >= 4 && after >= 2) __builtin_amdgcn_s_waitcnt(vmcnt_imm(2 * PER_TILE));
-    else if (STAGES >= 3 && after >= 1) __builtin_amdgcn_s_waitcnt(vmcnt_imm(PER_TILE));
-    else __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+    const int after = min(STAGES - 2, nk - 1 - kt);  // slices issued after kt allowed in flight
+    if (STAGES >= 4 && after >= 2) {
+      if (STAGES >= 5 && after >= 3) __builtin_amdgcn_s_waitcnt(vmcnt_imm(3 * PER_TILE));
+      else __builtin_amdgcn_s_waitcnt(vmcnt_imm(2 * PER_TILE));
+    } else if (STAGES >= 3 && after >= 1) {
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(PER_TILE));
+    } else {
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+    }
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + STAGES - 1 < nk) stage((kt + STAGES - 1) % STAGES, (kt + STAGES - 1) * BK);
+    const bool more = kt + STAGES - 1 < nk;
+    const int s_next = (kt + STAGES - 1) % STAGES, k_next = (kt + STAGES - 1) * KB;
     const int s = kt % STAGES;
-    const uint16_t* la = dsm + s * (TA + TB);    const uint16_t* lb = la + TA;
-    // every fragment of the tile's two 32-deep k-steps is requested up front (in-order LDS
-    // returns let the compiler's counted lgkmcnt release the first MFMAs early), instead of the
-    // load-pair / wait / 8-MFMA serialisation hipcc produces for the naive loop
-    bf16x8 a[2][MT], b[2][NT];
+    const uint16_t* la = dsm + s * (TA + TB);
+    const uint16_t* lb = la + TA;
+    auto rdA = [&](int ks, int i) {
+      const int rowa = wm * MT * 16 + i * 16 + fr;
+      return *(const bf16x8*)(la + rowa * KB + swzk<KB>(rowa, ks * 4 + fq) * 8);
+    };
+    auto rdB = [&](int ks, int j) {
+      const int rowb = wn * NT * 16 + j * 16 + fr;
+      return *(const bf16x8*)(lb + rowb * KB + swzk<KB>(rowb, ks * 4 + fq) * 8);
+    };
+    if (KS == 2 && MT == 8 && NT == 4 && CA + CB == 8) {
+      // hand-placed interleave (glds are scheduling barriers for hipcc, so source order holds):
+      // k-step-0 fragments; then per A row-tile i: one glds piece of the next slice, the
+      // k-step-1 fragment(s), 4 k-step-0 MFMAs; then the 32 k-step-1 MFMAs.
+      bf16x8 a0[MT], b0[NT], a1[MT], b1[NT];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int ch = ks * 4 + fq;
+      for (int j = 0; j < NT; ++j) b0[j] = rdB(0, j);
 #pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int rowb = wn * NT * 16 + j * 16 + fr;
-        b[ks][j] = *(const bf16x8*)(lb + rowb * BK + swz(rowb, ch) * 8);
-      }
+      for (int i = 0; i < MT; ++i) a0[i] = rdA(0, i);
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
-        const int rowa = wm * MT * 16 + i * 16 + fr;
-        a[ks][i] = *(const bf16x8*)(la + rowa * BK + swz(rowa, ch) * 8);
-      }
-    }
+        if (more) stage_piece(s_next, k_next, i);
+        a1[i] = rdA(1, i);
+        if (i < NT) b1[i] = rdB(1, i);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], b0[j], acc[i][j], 0, 0, 0);
+      }
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks][i], b[ks][j], acc[i][j], 0, 0, 0);
-    // pin the order (T19): k-step 0 fragments, then k-step 1 fragments interleaved with the
-    // k-step-0 MFMAs, then the k-step-1 MFMAs
-    __builtin_amdgcn_sched_group_barrier(0x100, MT + NT, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
+    } else {
+      if (more) stage(s_next, k_next);
+      bf16x8 a[KS][MT], b[KS][NT];
 #pragma unroll
-    for (int g = 0; g < MT + NT; ++g) {
-      __builtin_amdgcn_sched_group_barrier(0x008, MT * NT / (MT + NT) > 0 ? MT * NT / (MT + NT) : 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) b[ks][j] = rdB(ks, j);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) a[ks][i] = rdA(ks, i);
+      }
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NT; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks][i], b[ks][j], acc[i][j], 0, 0, 0);
+      if (KS == 2) {
+        __builtin_amdgcn_sched_group_barrier(0x100, MT + NT, 0);
+#pragma unroll
+        for (int g = 0; g < MT + NT; ++g) {
+          __builtin_amdgcn_sched_group_barrier(0x008, MT * NT / (MT + NT) > 0 ? MT * NT / (MT + NT) : 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * MT * NT, 0);
+      }
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 2 * MT * NT, 0);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this tile's fragment reads have returned
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this slice's fragment reads returned
   }
 
   // epilogue in 64-row halves of the wave tile through LDS (bf16), 16-B row stores (measured:
   // 8-B register-direct stores of a C^T product are 15-20 % slower on these shapes)
-  __syncthreads();  // every wave done with the staging ring before the epilogue reuses it
+  __syncthreads();
   uint16_t* et = dsm + wave * 64 * EPI_LD;
   constexpr int HALVES = MT / 4;
 #pragma unroll
@@ -316,7 +352,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_tn_big(const uint16_t* __res
     __builtin_amdgcn_wave_barrier();
     constexpr int CPR = NT * 16 / 8;  // 16-B chunks per row of the wave tile
 #pragma unroll
-    for (int it = 0; it < 64 * CPR / 64; ++it) {
+    for (int it = 0; it < CPR; ++it) {
       const int c = it * 64 + lane;
       const int rl = c / CPR, cc = (c % CPR) * 8;
       const int64_t m = m0 + wm * MT * 16 + hh * 64 + rl;
@@ -340,21 +376,27 @@ void launch(const uint16_t* x, const uint16_t* w, const float* b, const uint16_t
             int64_t m, int n, int k, hipStream_t st) {
   // big tiles when the grid still fills >= ~2 rounds of 256 CUs and K is deep enough
   static const int cfg = [] {
-    const char* e = getenv("MMR_GEMM_BIG");  // diagnostic override: 0 off, 1 256x128x3 only, 2 both
-    return e ? atoi(e) : 2;
+    // diagnostic override: 0 off; 1 256x256 KB64 x2; 2 256x256 KB32 x4; 3 256x128 KB64 x3
+    const char* e = getenv("MMR_GEMM_BIG");
+    return e ? atoi(e) : 1;
   }();
   const int64_t t256 = mmr::ceil_div(m, 256);
   if (cfg != 0 && k >= 256 && m >= 4096) {
-    if (cfg == 2 && n % 256 == 0 && t256 * (n / 256) >= 512) {
+    if (cfg <= 2 && n % 256 == 0 && t256 * (n / 256) >= 512) {
       const int tm = (int)t256, tn = n / 256;
-      const size_t lds = 2 * (256 + 256) * BK * 2;
-      gemm_bf16_tn_big<2, 4, 8, 4, 2, ACT, HB, HR><<<dim3(tm * tn), dim3(512), lds, st>>>(x, w, b, r, y, m, n, k, tm, tn);
+      if (cfg == 1) {
+        const size_t lds = 2 * (256 + 256) * 64 * 2;
+        gemm_bf16_tn_big<2, 4, 8, 4, 64, 2, ACT, HB, HR><<<dim3(tm * tn), dim3(512), lds, st>>>(x, w, b, r, y, m, n, k, tm, tn);
+      } else {
+        const size_t lds = 4 * (256 + 256) * 32 * 2;
+        gemm_bf16_tn_big<2, 4, 8, 4, 32, 4, ACT, HB, HR><<<dim3(tm * tn), dim3(512), lds, st>>>(x, w, b, r, y, m, n, k, tm, tn);
+      }
       return;
     }
     if (n % 128 == 0 && t256 * (n / 128) >= 512) {
       const int tm = (int)t256, tn = n / 128;
-      const size_t lds = 3 * (256 + 128) * BK * 2;
-      gemm_bf16_tn_big<4, 2, 4, 4, 3, ACT, HB, HR><<<dim3(tm * tn), dim3(512), lds, st>>>(x, w, b, r, y, m, n, k, tm, tn);
+      const size_t lds = 3 * (256 + 128) * 64 * 2;
+      gemm_bf16_tn_big<4, 2, 4, 4, 64, 3, ACT, HB, HR><<<dim3(tm * tn), dim3(512), lds, st>>>(x, w, b, r, y, m, n, k, tm, tn);
       return;
     }
   }
