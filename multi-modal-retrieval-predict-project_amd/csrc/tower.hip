@@ -307,10 +307,13 @@ __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __r
   const bool active = unit < units;
   const int nwin1 = H / ws;
   const int64_t u = active ? unit : 0;
-  const int hh = (int)(u % heads);
-  const int64_t wi = u / heads;
-  const int win = (int)(wi % (nwin1 * nwin1));
-  const int64_t bi = wi / (nwin1 * nwin1);
+  // unit order (image, head, window): the 4 waves of a block share one head, so its dense bias
+  // tile (16 KiB per window type) is re-read from L1/L2 instead of once per unit from farther out
+  const int nwin = nwin1 * nwin1;
+  const int win = (int)(u % nwin);
+  const int64_t bh = u / nwin;
+  const int hh = (int)(bh % heads);
+  const int64_t bi = bh / heads;
   const int wy = win / nwin1, wx = win % nwin1;
   const int N = ws * ws;
   const int type = shift > 0 ? ((wy == nwin1 - 1) ? 2 : 0) + ((wx == nwin1 - 1) ? 1 : 0) : 0;
