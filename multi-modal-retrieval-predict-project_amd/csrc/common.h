@@ -23,6 +23,13 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return (uint16_t)(u >> 16);
 }
 
+// two f32 -> packed bf16x2 (RNE) in one v_cvt_pk_bf16_f32
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack2bf(float a, float b) {
+  const bf16x2_t v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
 // GELU(erf) with erf from Abramowitz-Stegun 7.1.26 (|err| <= 1.5e-7): branch-free, one exp + one
 // rcp instead of ocml's erff.
 __device__ __forceinline__ float erf_as(float x) {

@@ -116,26 +116,34 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tn(const uint16_t* __restric
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
     }
     __syncthreads();  // waits the in-flight glds (vmcnt(0)) and every wave's reads of stage s
   }
 
-  // ---- epilogue: bias/act in registers -> bf16 tile in LDS -> 16-B row chunks (+ residual)
+  // ---- epilogue: bias/act in registers -> bf16 tile in LDS -> 16-B row chunks (+ residual).
+  // acc holds C^T tiles (operands swapped): lane l has row m = 16i + (l&15) and the 4
+  // consecutive columns n = 16j + 4(l>>4) + 0..3, written to LDS as one 8-byte store.
   uint16_t* et = lds + wave * 64 * EPI_LD;  // reuses the (now idle) staging buffers
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int nl = j * 16 + fr;
+    const int nl = j * 16 + fq * 4;
     const int n = n0 + wn * 64 + nl;
-    const float bv = (HAS_BIAS && n < N) ? bias[n] : 0.0f;
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (HAS_BIAS && n < N) bv = *(const float4*)(bias + n);
+    const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+      float v[4];
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg) {
-        float v = acc[i][j][rg] + bv;
-        if (ACT == 1) v = mmr::gelu_erf(v);
-        et[(i * 16 + fq * 4 + rg) * EPI_LD + nl] = mmr::f2bf(v);
+        v[rg] = acc[i][j][rg] + bb[rg];
+        if (ACT == 1) v[rg] = mmr::gelu_erf(v[rg]);
       }
+      uint2 pk;
+      pk.x = mmr::pack2bf(v[0], v[1]);
+      pk.y = mmr::pack2bf(v[2], v[3]);
+      *(uint2*)(et + (i * 16 + fr) * EPI_LD + nl) = pk;
     }
   }
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes landed
@@ -150,9 +158,12 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tn(const uint16_t* __restric
     bf16x8 v = *(const bf16x8*)(et + rl * EPI_LD + cc);
     if (HAS_RES) {
       const bf16x8 rr = *(const bf16x8*)(R + m * N + n);
+      uint32_t o[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        v[e] = (short)mmr::f2bf(mmr::bf2f((uint16_t)v[e]) + mmr::bf2f((uint16_t)rr[e]));
+      for (int e = 0; e < 4; ++e)
+        o[e] = mmr::pack2bf(mmr::bf2f((uint16_t)v[2 * e]) + mmr::bf2f((uint16_t)rr[2 * e]),
+                            mmr::bf2f((uint16_t)v[2 * e + 1]) + mmr::bf2f((uint16_t)rr[2 * e + 1]));
+      v = __builtin_bit_cast(bf16x8, make_uint4(o[0], o[1], o[2], o[3]));
     }
     *(bf16x8*)(Y + m * N + n) = v;
   }
@@ -172,8 +183,9 @@ __device__ __forceinline__ int swzk(int row, int chunk) {
   return KB == 64 ? (chunk ^ ((row >> 1) & 7)) : (chunk ^ ((row >> 1) & 3));  // conflict-free b128 reads
 }
 
-template <int WM, int WN, int MT, int NT, int KB, int STAGES, int ACT, bool HAS_BIAS, bool HAS_RES>
-__global__ __launch_bounds__(512, 1) void gemm_bf16_tn_big(const uint16_t* __restrict__ X,
+template <int WM, int WN, int MT, int NT, int KB, int STAGES, int ACT, bool HAS_BIAS, bool HAS_RES,
+          int OCC = 1>
+__global__ __launch_bounds__(512, OCC) void gemm_bf16_tn_big(const uint16_t* __restrict__ X,
                                                            const uint16_t* __restrict__ W,
                                                            const float* __restrict__ bias,
                                                            const uint16_t* __restrict__ R,
@@ -289,13 +301,13 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_tn_big(const uint16_t* __res
         if (i < NT) b1[i] = rdB(1, i);
 #pragma unroll
         for (int j = 0; j < NT; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], b0[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j], a0[i], acc[i][j], 0, 0, 0);
       }
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a1[i], acc[i][j], 0, 0, 0);
     } else {
       if (more) stage(s_next, k_next);
       bf16x8 a[KS][MT], b[KS][NT];
@@ -312,7 +324,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_tn_big(const uint16_t* __res
         for (int i = 0; i < MT; ++i)
 #pragma unroll
           for (int j = 0; j < NT; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks][i], b[ks][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], a[ks][i], acc[i][j], 0, 0, 0);
       if (KS == 2) {
         __builtin_amdgcn_sched_group_barrier(0x100, MT + NT, 0);
 #pragma unroll
@@ -333,19 +345,26 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_tn_big(const uint16_t* __res
   constexpr int HALVES = MT / 4;
 #pragma unroll
   for (int hh = 0; hh < HALVES; ++hh) {
+    // C^T tiles (operands swapped): lane has row m = 16i + (l&15), columns 16j + 4(l>>4) + 0..3
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      const int nl = j * 16 + fr;
+      const int nl = j * 16 + fq * 4;
       const int n = n0 + wn * NT * 16 + nl;
-      const float bv = (HAS_BIAS && n < N) ? bias[n] : 0.0f;
+      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (HAS_BIAS && n < N) bv = *(const float4*)(bias + n);
+      const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
       for (int i4 = 0; i4 < 4; ++i4) {
+        float v[4];
 #pragma unroll
         for (int rg = 0; rg < 4; ++rg) {
-          float v = acc[hh * 4 + i4][j][rg] + bv;
-          if (ACT == 1) v = mmr::gelu_erf(v);
-          et[(i4 * 16 + fq * 4 + rg) * EPI_LD + nl] = mmr::f2bf(v);
+          v[rg] = acc[hh * 4 + i4][j][rg] + bb[rg];
+          if (ACT == 1) v[rg] = mmr::gelu_erf(v[rg]);
         }
+        uint2 pk;
+        pk.x = mmr::pack2bf(v[0], v[1]);
+        pk.y = mmr::pack2bf(v[2], v[3]);
+        *(uint2*)(et + (i4 * 16 + fr) * EPI_LD + nl) = pk;
       }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -361,9 +380,12 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_tn_big(const uint16_t* __res
       bf16x8 v = *(const bf16x8*)(et + rl * EPI_LD + cc);
       if (HAS_RES) {
         const bf16x8 rr = *(const bf16x8*)(R + m * N + n);
+        uint32_t o[4];
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          v[e] = (short)mmr::f2bf(mmr::bf2f((uint16_t)v[e]) + mmr::bf2f((uint16_t)rr[e]));
+        for (int e = 0; e < 4; ++e)
+          o[e] = mmr::pack2bf(mmr::bf2f((uint16_t)v[2 * e]) + mmr::bf2f((uint16_t)rr[2 * e]),
+                              mmr::bf2f((uint16_t)v[2 * e + 1]) + mmr::bf2f((uint16_t)rr[2 * e + 1]));
+        v = __builtin_bit_cast(bf16x8, make_uint4(o[0], o[1], o[2], o[3]));
       }
       *(bf16x8*)(Y + m * N + n) = v;
     }
@@ -390,6 +412,17 @@ void launch(const uint16_t* x, const uint16_t* w, const float* b, const uint16_t
       } else {
         const size_t lds = 4 * (256 + 256) * 32 * 2;
         gemm_bf16_tn_big<2, 4, 8, 4, 32, 4, ACT, HB, HR><<<dim3(tm * tn), dim3(512), lds, st>>>(x, w, b, r, y, m, n, k, tm, tn);
+      }
+      return;
+    }
+    if (cfg >= 4 && n % 128 == 0) {  // 256x128, KB=32: 2 workgroups per CU (epilogue overlap)
+      const int tm = (int)t256, tn = n / 128;
+      if (cfg == 4) {
+        const size_t lds = 2 * (256 + 128) * 32 * 2;
+        gemm_bf16_tn_big<4, 2, 4, 4, 32, 2, ACT, HB, HR, 2><<<dim3(tm * tn), dim3(512), lds, st>>>(x, w, b, r, y, m, n, k, tm, tn);
+      } else {
+        const size_t lds = 3 * (256 + 128) * 32 * 2;
+        gemm_bf16_tn_big<4, 2, 4, 4, 32, 3, ACT, HB, HR, 2><<<dim3(tm * tn), dim3(512), lds, st>>>(x, w, b, r, y, m, n, k, tm, tn);
       }
       return;
     }

@@ -25,10 +25,8 @@ __device__ __forceinline__ void load8(const uint16_t* p, float* v) {
   for (int j = 0; j < 8; ++j) v[j] = bf2f((uint16_t)x[j]);
 }
 __device__ __forceinline__ void store8(uint16_t* p, const float* v) {
-  bf16x8 x;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) x[j] = (short)f2bf(v[j]);
-  *(bf16x8*)p = x;
+  *(uint4*)p = make_uint4(mmr::pack2bf(v[0], v[1]), mmr::pack2bf(v[2], v[3]), mmr::pack2bf(v[4], v[5]),
+                          mmr::pack2bf(v[6], v[7]));
 }
 
 // ------------------------------------------------------------------ LayerNorm
