@@ -116,6 +116,18 @@ mmr_status mmr_swin_window_attention(const uint16_t* qkv, const float* bias, uin
 mmr_status mmr_swin_attn_bias(const float* relpos_table, float* bias, int32_t heads, int32_t ws,
                               int32_t hw, int32_t shift, void* stream);
 
+/* Fused Swin MLP sub-block for C in {96, 192} (the memory-bound stages 1-2):
+ * y = x + fc2(GELU(fc1(LayerNorm(x)))) with the 4C hidden activation kept on chip.
+ * x, y bf16 (tokens, C) (x != y); ln_g/ln_b, b1 (4C), b2 (C) f32; `pack` = weights repacked once by
+ * mmr_swin_mlp_pack from fc1.weight [4C][C] and fc2.weight [C][4C] (bf16) into
+ * mmr_swin_mlp_pack_elems(C) bf16 elements. */
+int64_t mmr_swin_mlp_pack_elems(int32_t c);
+mmr_status mmr_swin_mlp_pack(const uint16_t* w1, const uint16_t* w2, uint16_t* pack, int32_t c,
+                             void* stream);
+mmr_status mmr_swin_mlp(const uint16_t* x, const float* ln_g, const float* ln_b,
+                        const uint16_t* pack, const float* b1, const float* b2, uint16_t* y,
+                        int64_t tokens, int32_t c, float eps, void* stream);
+
 /* Swin patch embedding im2col: image f32 NCHW (b,3,224,224) -> bf16 (b*56*56, 48) columns in
  * conv-weight order (cin, kh, kw) for a 4x4/s4 conv as a GEMM. */
 mmr_status mmr_patch_im2col(const float* image, uint16_t* cols, int32_t b, int32_t cin,

@@ -118,3 +118,25 @@ def proj_head(x, wp, bp, w1=None, b1=None, w2=None, b2=None, l2norm=False):
     _chk(_L().mmr_proj_head(_lib.ptr(x), _lib.ptr(wp), _lib.ptr(bp), _lib.ptr(w1), _lib.ptr(b1), _lib.ptr(w2),
                             _lib.ptr(b2), _lib.ptr(y), B, Cin, D, int(bool(l2norm)), _s(x)), "mmr_proj_head")
     return y
+
+
+def swin_mlp_pack(w1, w2):
+    """fc1.weight [4C][C], fc2.weight [C][4C] (bf16, device) -> packed chunks for swin_mlp, or None if
+    C is not one of the fused widths."""
+    C = w1.shape[1]
+    n = _L().mmr_swin_mlp_pack_elems(C)
+    if n <= 0:
+        return None
+    pack = torch.empty((n,), dtype=torch.bfloat16, device=w1.device)
+    _chk(_L().mmr_swin_mlp_pack(_lib.ptr(w1.contiguous()), _lib.ptr(w2.contiguous()), _lib.ptr(pack), C, _s(w1)),
+         "mmr_swin_mlp_pack")
+    return pack
+
+
+def swin_mlp(x, g, b, pack, b1, b2, eps):
+    """x + fc2(GELU(fc1(LN(x)))) fused (C in {96, 192})."""
+    C = x.shape[-1]
+    y = torch.empty_like(x)
+    _chk(_L().mmr_swin_mlp(_lib.ptr(x), _lib.ptr(g), _lib.ptr(b), _lib.ptr(pack), _lib.ptr(b1), _lib.ptr(b2),
+                           _lib.ptr(y), x.numel() // C, C, float(eps), _s(x)), "mmr_swin_mlp")
+    return y

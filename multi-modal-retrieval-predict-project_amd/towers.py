@@ -9,7 +9,8 @@ the 4x4/s4 patch-embed conv as a [96][64] bf16 GEMM weight (K = 3*16 zero-padded
 Per-block dataflow (all hand-written kernels, bf16 activations, f32 accumulation):
   Swin block   LN1 -> QKV GEMM(+bias) -> window attention (roll/partition/bias/mask/softmax/PV/
                reverse/roll fused) -> proj GEMM(+bias +residual) -> LN2 -> fc1 GEMM(+bias, GELU)
-               -> fc2 GEMM(+bias +residual)
+               -> fc2 GEMM(+bias +residual); for C = 96 / 192 the MLP half is ONE fused kernel
+               (mmr_swin_mlp: LN2 + fc1 + GELU + fc2 + residual, hidden kept on chip)
   PatchMerge   gather 2x2 + LN(4C) fused -> reduction GEMM (no bias)
   BERT layer   QKV GEMM(+bias) -> masked attention -> out GEMM(+bias +residual) -> LN ->
                FFN1 GEMM(+bias, GELU) -> FFN2 GEMM(+bias +residual) -> LN
@@ -35,8 +36,9 @@ def _f(t, dev):
 class SwinTower:
     """timm SwinTransformer.forward_features semantics (see oracle/towers.py for the restatement)."""
 
-    def __init__(self, sd, cfg=SWIN_T, device="cuda"):
+    def __init__(self, sd, cfg=SWIN_T, device="cuda", fused_mlp=True):
         self.cfg = dict(SWIN_T, **cfg)
+        self.fused_mlp = fused_mlp
         dev = torch.device(device)
         self.device = dev
         E = self.cfg["embed_dim"]
@@ -71,6 +73,8 @@ class SwinTower:
                     "fc1_w": _bf(sd[p + "mlp.fc1.weight"], dev), "fc1_b": _f(sd[p + "mlp.fc1.bias"], dev),
                     "fc2_w": _bf(sd[p + "mlp.fc2.weight"], dev), "fc2_b": _f(sd[p + "mlp.fc2.bias"], dev),
                 })
+                bk = st["blocks"][-1]
+                bk["mlp_pack"] = ops.swin_mlp_pack(bk["fc1_w"], bk["fc2_w"]) if self.fused_mlp else None
             self.stages.append(st)
         self.norm_g, self.norm_b = _f(sd["norm.weight"], dev), _f(sd["norm.bias"], dev)
         self.num_features = E * 2 ** (len(self.cfg["depths"]) - 1)
@@ -97,9 +101,12 @@ class SwinTower:
                 qkv = ops.linear(h, bk["qkv_w"], bk["qkv_b"])
                 a = ops.swin_window_attention(qkv, bk["bias"], H, heads, ws, bk["shift"])
                 x = ops.linear(a, bk["proj_w"], bk["proj_b"], residual=x)
-                h = ops.layernorm(x, bk["n2g"], bk["n2b"], 1e-5)
-                h = ops.linear(h, bk["fc1_w"], bk["fc1_b"], act=1)
-                x = ops.linear(h, bk["fc2_w"], bk["fc2_b"], residual=x)
+                if bk["mlp_pack"] is not None:
+                    x = ops.swin_mlp(x, bk["n2g"], bk["n2b"], bk["mlp_pack"], bk["fc1_b"], bk["fc2_b"], 1e-5)
+                else:
+                    h = ops.layernorm(x, bk["n2g"], bk["n2b"], 1e-5)
+                    h = ops.linear(h, bk["fc1_w"], bk["fc1_b"], act=1)
+                    x = ops.linear(h, bk["fc2_w"], bk["fc2_b"], residual=x)
             del C
         return x
 

@@ -56,6 +56,28 @@ def test_linear_bf16(M, N, K, act, bias, res):
     assert rel_err(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize("T,C", [(1000, 96), (3136 * 4 + 17, 96), (64, 192), (784 * 8 + 5, 192), (1, 96)])
+def test_swin_mlp_fused(T, C):
+    """mmr_swin_mlp == x + fc2(GELU(fc1(LN(x)))) (fusion.py:198-199 via timm Mlp), ragged token counts;
+    hidden activation rounded to bf16 as in the unfused path.  Tolerance: 2e-2 * max|ref|."""
+    g = torch.Generator().manual_seed(T + C)
+    x = bf(torch.randn(T, C, generator=g) * 2)
+    lg, lb = 1 + 0.1 * torch.randn(C, generator=g), 0.1 * torch.randn(C, generator=g)
+    w1, b1 = bf(torch.randn(4 * C, C, generator=g) * C ** -0.5), 0.1 * torch.randn(4 * C, generator=g)
+    w2, b2 = bf(torch.randn(C, 4 * C, generator=g) * (4 * C) ** -0.5), 0.1 * torch.randn(C, generator=g)
+    h = bf(F.layer_norm(x.float(), (C,), lg, lb, 1e-5)).float()
+    h = bf(F.gelu(h @ w1.float().T + b1)).float()
+    ref = h @ w2.float().T + b2 + x.float()
+    pack = ops.swin_mlp_pack(w1.to(DEV), w2.to(DEV))
+    y = ops.swin_mlp(x.to(DEV), lg.to(DEV), lb.to(DEV), pack, b1.to(DEV), b2.to(DEV), 1e-5)
+    assert rel_err(y, ref) < 2e-2
+    # the unfused kernels agree too (same bf16 rounding points)
+    h2 = ops.layernorm(x.to(DEV), lg.to(DEV), lb.to(DEV), 1e-5)
+    h2 = ops.linear(h2, w1.to(DEV), b1.to(DEV), act=1)
+    y2 = ops.linear(h2, w2.to(DEV), b2.to(DEV), residual=x.to(DEV))
+    assert rel_err(y, y2.float().cpu()) < 2e-2
+
+
 def test_layernorm_bf16():
     x = torch.randn(1000, 768) * 3 + 1
     g, b = torch.randn(768), torch.randn(768)
