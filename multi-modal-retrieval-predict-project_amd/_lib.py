@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmmr.so")
+LIB_PATH = os.environ.get("MMR_LIBMMR", os.path.join(_HERE, "libmmr.so"))  # override: diagnostic builds
 
 c_i32, c_i64, c_f32, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 

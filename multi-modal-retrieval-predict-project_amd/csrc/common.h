@@ -34,15 +34,28 @@ __device__ __forceinline__ uint32_t pack2bf(float a, float b) {
 // rcp instead of ocml's erff.
 __device__ __forceinline__ float erf_as(float x) {
   const float a = fabsf(x);
-  const float t = __frcp_rn(fmaf(0.3275911f, a, 1.0f));
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.0f));  // v_rcp_f32 (1 ulp), not a division
   float p = fmaf(1.061405429f, t, -1.453152027f);
   p = fmaf(p, t, 1.421413741f);
   p = fmaf(p, t, -0.284496736f);
   p = fmaf(p, t, 0.254829592f);
-  const float y = 1.0f - p * t * __expf(-a * a);
+  const float y = fmaf(-p * t, __builtin_amdgcn_exp2f(-1.44269504088896341f * a * a), 1.0f);  // v_exp_f32
   return copysignf(y, x);
 }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_as(x * 0.70710678118654752f)); }
+// GELU(x) = x * Phi(x) as x * sigmoid(x * P(x^2)), P least-squares-fitted to the erf form on
+// [-7, 7]: |err| < 1.2e-5 everywhere (40x below a bf16 half-ulp at |y| ~ 1), 7 VALU + v_exp + v_rcp
+// instead of 11 VALU + v_exp + v_rcp.  Used where GELU output is rounded to bf16 (GEMM epilogues,
+// fused Swin MLP); tools/gelu_fit.py holds the fit.
+__device__ __forceinline__ float gelu_fast(float v) {
+  const float x2 = v * v;
+  float p = fmaf(3.275317185739523e-06f, x2, -7.756018138382363e-05f);
+  p = fmaf(p, x2, -0.00016997469037563395f);
+  p = fmaf(p, x2, 0.07280746695679054f);
+  p = fmaf(p, x2, 1.5957042563586181f);
+  const float e = __builtin_amdgcn_exp2f(-1.4426950408889634f * v * p);
+  return v * __builtin_amdgcn_rcpf(1.0f + e);
+}
 
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {

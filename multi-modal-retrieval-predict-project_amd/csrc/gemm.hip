@@ -1,3 +1,4 @@
+#include <algorithm>
 // bf16 "linear" GEMM with fused epilogue for the towers (gfx950):
 //   Y[m][n] = act(sum_k X[m][k] * W[n][k] + bias[n]) (+ R[m][n]),  X, W, R, Y bf16, f32 accumulate.
 // nn.Linear layout (W = [out][in]): both operands K-contiguous, so both MFMA fragments are 16-byte
@@ -28,6 +29,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int BM = 128, BN = 128, BK = 64;
 constexpr int TILE = BM * BK;          // bf16 elements per operand per stage (16 KiB)
 constexpr int EPI_LD = 64 + 8;         // bf16 row stride of a wave's 64x64 epilogue tile
+constexpr size_t EPI_BIG_B = 8 * 64 * EPI_LD * 2;  // epilogue staging of the 8-wave kernels
 
 __device__ __attribute__((aligned(16))) uint4 g_zero_page[4];  // zero-initialised
 
@@ -138,7 +140,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_tn(const uint16_t* __restric
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg) {
         v[rg] = acc[i][j][rg] + bb[rg];
-        if (ACT == 1) v[rg] = mmr::gelu_erf(v[rg]);
+        if (ACT == 1) v[rg] = mmr::gelu_fast(v[rg]);
       }
       uint2 pk;
       pk.x = mmr::pack2bf(v[0], v[1]);
@@ -185,7 +187,7 @@ __device__ __forceinline__ int swzk(int row, int chunk) {
 
 template <int WM, int WN, int MT, int NT, int KB, int STAGES, int ACT, bool HAS_BIAS, bool HAS_RES,
           int OCC = 1>
-__global__ __launch_bounds__(512, OCC) void gemm_bf16_tn_big(const uint16_t* __restrict__ X,
+__global__ __launch_bounds__(512, 2 * OCC) void gemm_bf16_tn_big(const uint16_t* __restrict__ X,
                                                            const uint16_t* __restrict__ W,
                                                            const float* __restrict__ bias,
                                                            const uint16_t* __restrict__ R,
@@ -340,9 +342,23 @@ __global__ __launch_bounds__(512, OCC) void gemm_bf16_tn_big(const uint16_t* __r
 
   // epilogue in 64-row halves of the wave tile through LDS (bf16), 16-B row stores (measured:
   // 8-B register-direct stores of a C^T product are 15-20 % slower on these shapes)
+  constexpr int HALVES = MT / 4;
+  constexpr int CPR = NT * 16 / 8;  // 16-B chunks per row of the wave tile
+  // residual rows are fetched first, so their latency overlaps the LDS staging below
+  bf16x8 rres[HAS_RES ? HALVES : 1][HAS_RES ? CPR : 1];
+  if constexpr (HAS_RES) {
+#pragma unroll
+    for (int hh = 0; hh < HALVES; ++hh)
+#pragma unroll
+      for (int it = 0; it < CPR; ++it) {
+        const int c = it * 64 + lane;
+        const int64_t m = m0 + wm * MT * 16 + hh * 64 + c / CPR;
+        const int n = n0 + wn * NT * 16 + (c % CPR) * 8;
+        rres[hh][it] = (m < M && n < N) ? *(const bf16x8*)(R + m * N + n) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+      }
+  }
   __syncthreads();
   uint16_t* et = dsm + wave * 64 * EPI_LD;
-  constexpr int HALVES = MT / 4;
 #pragma unroll
   for (int hh = 0; hh < HALVES; ++hh) {
     // C^T tiles (operands swapped): lane has row m = 16i + (l&15), columns 16j + 4(l>>4) + 0..3
@@ -359,7 +375,7 @@ __global__ __launch_bounds__(512, OCC) void gemm_bf16_tn_big(const uint16_t* __r
 #pragma unroll
         for (int rg = 0; rg < 4; ++rg) {
           v[rg] = acc[hh * 4 + i4][j][rg] + bb[rg];
-          if (ACT == 1) v[rg] = mmr::gelu_erf(v[rg]);
+          if (ACT == 1) v[rg] = mmr::gelu_fast(v[rg]);
         }
         uint2 pk;
         pk.x = mmr::pack2bf(v[0], v[1]);
@@ -369,7 +385,6 @@ __global__ __launch_bounds__(512, OCC) void gemm_bf16_tn_big(const uint16_t* __r
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_wave_barrier();
-    constexpr int CPR = NT * 16 / 8;  // 16-B chunks per row of the wave tile
 #pragma unroll
     for (int it = 0; it < CPR; ++it) {
       const int c = it * 64 + lane;
@@ -379,7 +394,7 @@ __global__ __launch_bounds__(512, OCC) void gemm_bf16_tn_big(const uint16_t* __r
       if (m >= M || n >= N) continue;
       bf16x8 v = *(const bf16x8*)(et + rl * EPI_LD + cc);
       if (HAS_RES) {
-        const bf16x8 rr = *(const bf16x8*)(R + m * N + n);
+        const bf16x8 rr = rres[HAS_RES ? hh : 0][HAS_RES ? it : 0];
         uint32_t o[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e)
@@ -407,10 +422,10 @@ void launch(const uint16_t* x, const uint16_t* w, const float* b, const uint16_t
     if (cfg <= 2 && n % 256 == 0 && t256 * (n / 256) >= 512) {
       const int tm = (int)t256, tn = n / 256;
       if (cfg == 1) {
-        const size_t lds = 2 * (256 + 256) * 64 * 2;
+        const size_t lds = std::max<size_t>(2 * (256 + 256) * 64 * 2, EPI_BIG_B);
         gemm_bf16_tn_big<2, 4, 8, 4, 64, 2, ACT, HB, HR><<<dim3(tm * tn), dim3(512), lds, st>>>(x, w, b, r, y, m, n, k, tm, tn);
       } else {
-        const size_t lds = 4 * (256 + 256) * 32 * 2;
+        const size_t lds = std::max<size_t>(4 * (256 + 256) * 32 * 2, EPI_BIG_B);
         gemm_bf16_tn_big<2, 4, 8, 4, 32, 4, ACT, HB, HR><<<dim3(tm * tn), dim3(512), lds, st>>>(x, w, b, r, y, m, n, k, tm, tn);
       }
       return;
@@ -418,17 +433,17 @@ void launch(const uint16_t* x, const uint16_t* w, const float* b, const uint16_t
     if (cfg >= 4 && n % 128 == 0) {  // 256x128, KB=32: 2 workgroups per CU (epilogue overlap)
       const int tm = (int)t256, tn = n / 128;
       if (cfg == 4) {
-        const size_t lds = 2 * (256 + 128) * 32 * 2;
+        const size_t lds = std::max<size_t>(2 * (256 + 128) * 32 * 2, EPI_BIG_B);
         gemm_bf16_tn_big<4, 2, 4, 4, 32, 2, ACT, HB, HR, 2><<<dim3(tm * tn), dim3(512), lds, st>>>(x, w, b, r, y, m, n, k, tm, tn);
       } else {
-        const size_t lds = 3 * (256 + 128) * 32 * 2;
+        const size_t lds = std::max<size_t>(3 * (256 + 128) * 32 * 2, EPI_BIG_B);
         gemm_bf16_tn_big<4, 2, 4, 4, 32, 3, ACT, HB, HR, 2><<<dim3(tm * tn), dim3(512), lds, st>>>(x, w, b, r, y, m, n, k, tm, tn);
       }
       return;
     }
     if (n % 128 == 0 && t256 * (n / 128) >= 512) {
       const int tm = (int)t256, tn = n / 128;
-      const size_t lds = 3 * (256 + 128) * 64 * 2;
+      const size_t lds = std::max<size_t>(3 * (256 + 128) * 64 * 2, EPI_BIG_B);
       gemm_bf16_tn_big<4, 2, 4, 4, 64, 3, ACT, HB, HR><<<dim3(tm * tn), dim3(512), lds, st>>>(x, w, b, r, y, m, n, k, tm, tn);
       return;
     }

@@ -1,14 +1,20 @@
 // Fused Swin MLP sub-block for the narrow, memory-bound stages (C = 96, 192):
 //   y = x + fc2(GELU(fc1(LN2(x))))            (timm SwinTransformerBlock, fusion.py:198-199)
-// The 4C-wide hidden activation never leaves the CU: per 64-token tile, each wave owns 16 tokens,
-// LayerNorms them in registers (row split over the 4 lanes that share a token), and walks the
-// hidden dimension in HC-wide chunks: fc1 (C^T orientation, so the GELU'd hidden values land in
-// exactly the registers fc2 needs as its B operand under a k-permutation that the A operand —
-// W2 read from LDS — mirrors), bias + GELU, then accumulate fc2.  Weights are repacked once at
-// load into per-chunk [W1 rows | W2 columns] slabs with padded rows (conflict-free ds_read_b128 /
-// ds_read_b64) and streamed through a 2-deep LDS ring by global_load_lds.
-// HBM traffic per token: 2C (x) + 2C (y) bytes, vs 2C + 8C + 8C + 2C + 2C (+LN pass) for the
-// LN -> GEMM -> GEMM chain.
+// The 4C-wide hidden activation never leaves the CU.  Each wave owns 32 tokens, LayerNorms them in
+// registers (row split over the lane pair that shares a token) straight into the fc1 B operand,
+// and walks the hidden dimension 32 units at a time: fc1 (C^T orientation, 32x32x16 MFMA, so the
+// GELU'd hidden values land in exactly the registers fc2 needs as its B operand under a
+// k-permutation that the packed W2 columns mirror), bias + GELU, then accumulate fc2 (C^T, A = W2
+// from LDS).  Weights are repacked once at load into per-64-hidden-unit chunks
+// [W1 rows | W2 columns] that are exact, bank-conflict-free LDS images.
+//   C = 96  (swin_mlp_res): all of W1 + W2 (147 KiB) resident in LDS, one persistent workgroup per
+//           CU, waves walk token tiles independently (no barriers), next tile's x prefetched.
+//   C = 192 (swin_mlp): 590 KiB of weights streamed through a 3-deep LDS ring by global_load_lds,
+//           shared by the workgroup's 256 tokens.
+// HBM traffic per token: 2C (x) + 2C (y) bytes, vs ~24C for the LN -> GEMM -> GEMM chain.
+// The kernel is VALU-bound on GELU (308M evaluations per stage-1 call), hence the
+// x*sigmoid(x*P(x^2)) form below.
+#include <algorithm>
 #include <float.h>
 #include <math.h>
 
@@ -17,181 +23,442 @@
 namespace {
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
-typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+// NOTE: LDS reads below use native vector types on purpose.  A HIP float4 (struct) load carries no
+// TBAA info, and hipcc then makes every such ds_read wait vmcnt(0) for all in-flight
+// global_load_lds — draining the weight ring each time.
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <int C, int HC>
-struct MlpCfg {
-  static constexpr int LD1 = C + 8;        // W1 chunk row stride (elements): 16-row reads conflict-free
-  static constexpr int LD2 = HC + 4;       // W2 chunk row stride: 8-B reads conflict-free
-  static constexpr int W1E = HC * LD1;
-  static constexpr int W2E = C * LD2;
-  static constexpr int CHUNK_E = (W1E + W2E + 511) / 512 * 512;  // whole 1-KiB glds pieces
-  static constexpr int NCH = 4 * C / HC;
+constexpr int vmcnt_n(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14); }
+
+// Geometry.  NW waves per workgroup, 32 tokens per wave (the N side of
+// v_mfma_f32_32x32x16_bf16).  Hidden units are walked in HC-wide chunks; a chunk is
+// [W1 rows HC*ch.. : HC x C][W2 columns HC*ch.. : C x HC] = 4*HC*C bytes, an exact LDS image (16-B
+// units permuted so every ds_read_b128 is bank-conflict-free, no padding), loaded as 1-KiB
+// global_load_lds pieces spread evenly over the waves, through an R-deep ring.  The f32
+// parameters (LN gamma/beta, fc1 bias) sit in a separate static LDS array.
+template <int C, int NW, int HC, int R>
+struct MlpGeo {
+  static constexpr int U1 = C / 8;        // 16-B units per W1 row
+  static constexpr int U2 = HC / 8;       // 16-B units per W2 row
+  static constexpr int KS1 = C / 16;      // fc1 k-steps (k = 16)
+  static constexpr int NU = C / 32;       // fc2 output tiles (32 channels)
+  static constexpr int NT = HC / 32;      // 32-wide hidden tiles per chunk
+  static constexpr int NCH = 4 * C / HC;  // chunks
+  static constexpr int W1B = HC * C * 2;
+  static constexpr int CHUNK_B = 2 * W1B;
+  static constexpr int PW = CHUNK_B / 1024 / NW;  // glds pieces per wave per chunk
+  static constexpr int TOK = 32 * NW;     // tokens per workgroup
+  static constexpr int LDS_B = R * CHUNK_B;
+  static_assert(CHUNK_B % (1024 * NW) == 0, "chunk must split evenly over the waves");
+  static_assert(R == 2 || R == 3, "ring depth");
 };
 
-template <int C, int HC>
+// physical 16-B unit of logical unit q in row r (conflict-free for the b128 lane groups; checked
+// exhaustively for the 32x32x16 A-operand access pattern)
+template <int U>
+__host__ __device__ __forceinline__ int unit_swz(int r, int q) {
+  if constexpr (U == 12) return (q + ((r >> 2) & 3)) % 12;
+  else if constexpr (U == 4) return q ^ ((r >> 2) & 3);
+  else return q ^ ((r >> 1) & 7);  // U = 8, 24
+}
+
+// W2 column order inside each 16-wide group: stored position 8h + j holds hidden
+// 8(j>>2) + 4h + (j&3) — the order in which fc1's 32x32 C fragment leaves GELU'd values in lane
+// half h, so one ds_read_b128 fetches the A fragment that matches the packed B fragment.
+__host__ __device__ __forceinline__ int w2_hidden(int pos) {
+  const int h = (pos >> 3) & 1, j = pos & 7;
+  return (pos & ~15) + 8 * (j >> 2) + 4 * h + (j & 3);
+}
+
+// Output-row order for the resident kernel: MFMA C row 8i + 4h + rr of output tile u holds channel
+// 32u + 16(i>>1) + 8h + 4(i&1) + rr, so lane half h ends up with channels 32u + 8h + 0..7 and
+// 32u + 16 + 8h + 0..7 — exactly the channels it loaded for LayerNorm (residual from registers,
+// 16-B stores).
+__host__ __device__ __forceinline__ int w2_channel(int row) {
+  const int u = row >> 5, rho = row & 31, i = rho >> 3, h = (rho >> 2) & 1, rr = rho & 3;
+  return 32 * u + 16 * (i >> 1) + 8 * h + 4 * (i & 1) + rr;
+}
+
+template <int C, int HC, bool PERM>
 __global__ __launch_bounds__(256) void swin_mlp_pack(const uint16_t* __restrict__ w1,
                                                      const uint16_t* __restrict__ w2,
                                                      uint16_t* __restrict__ pack) {
-  using Cf = MlpCfg<C, HC>;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (int64_t)Cf::NCH * Cf::CHUNK_E) return;
-  const int ch = (int)(i / Cf::CHUNK_E), e = (int)(i % Cf::CHUNK_E);
-  uint16_t v = 0;
-  if (e < Cf::W1E) {
-    const int r = e / Cf::LD1, k = e % Cf::LD1;
-    if (k < C) v = w1[(int64_t)(ch * HC + r) * C + k];  // fc1.weight [4C][C]
-  } else if (e < Cf::W1E + Cf::W2E) {
-    const int e2 = e - Cf::W1E;
-    const int c = e2 / Cf::LD2, j = e2 % Cf::LD2;
-    if (j < HC) v = w2[(int64_t)c * 4 * C + ch * HC + j];  // fc2.weight [C][4C]
+  constexpr int CE = 2 * HC * C, W1E = HC * C;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // logical element
+  if (i >= (int64_t)8 * C * C) return;
+  const int ch = (int)(i / CE), e = (int)(i % CE);
+  if (e < W1E) {
+    const int r = e / C, k = e % C, q = k >> 3;
+    pack[(int64_t)ch * CE + r * C + 8 * unit_swz<C / 8>(r, q) + (k & 7)] = w1[(int64_t)(HC * ch + r) * C + k];
+  } else {
+    const int e2 = e - W1E, c = e2 / HC, pos = e2 % HC, q = pos >> 3;
+    pack[(int64_t)ch * CE + W1E + c * HC + 8 * unit_swz<HC / 8>(c, q) + (pos & 7)] =
+        w2[(int64_t)(PERM ? w2_channel(c) : c) * 4 * C + HC * ch + w2_hidden(pos)];
   }
-  pack[i] = v;
 }
 
-template <int C, int HC>
-__global__ __launch_bounds__(256) void swin_mlp(const uint16_t* __restrict__ x,
-                                                const float* __restrict__ lng,
-                                                const float* __restrict__ lnb,
-                                                const uint16_t* __restrict__ pack,
-                                                const float* __restrict__ b1,
-                                                const float* __restrict__ b2,
-                                                uint16_t* __restrict__ y, int64_t T, float eps) {
-  using Cf = MlpCfg<C, HC>;
-  constexpr int KS1 = C / 32;       // fc1 k-steps
-  constexpr int NT1 = HC / 16;      // fc1 n-tiles per chunk
-  constexpr int KS2 = HC / 32;      // fc2 k-steps per chunk
-  constexpr int NU = C / 16;        // fc2 output tiles
-  constexpr int PIECES = Cf::CHUNK_E / 512;
-  extern __shared__ __attribute__((aligned(16))) uint16_t sm[];  // [2][CHUNK_E]
+template <bool FAST>
+__device__ __forceinline__ float gelu_t(float v) {
+  if constexpr (FAST) return mmr::gelu_fast(v);
+  else return mmr::gelu_erf(v);
+}
+
+template <int C, int NW, int HC, int R, bool FAST>
+__global__ __launch_bounds__(64 * NW) void swin_mlp(const uint16_t* __restrict__ x,
+                                                         const float* __restrict__ lng,
+                                                         const float* __restrict__ lnb,
+                                                         const uint16_t* __restrict__ pack,
+                                                         const float* __restrict__ b1,
+                                                         const float* __restrict__ b2,
+                                                         uint16_t* __restrict__ y, int64_t T, float eps) {
+  using G = MlpGeo<C, NW, HC, R>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // the weight ring only
+  __shared__ __attribute__((aligned(16))) float Pg[6 * C];
+  const float* Pb = Pg + C;
+  const float* Pb1 = Pg + 2 * C;
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int fr = lane & 15, g4 = lane >> 4;
-  const int64_t m = (int64_t)blockIdx.x * 64 + wave * 16 + fr;
-  const bool mok = m < T;
-  const uint16_t* xr = x + (mok ? m : 0) * C;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t tok = (int64_t)blockIdx.x * G::TOK + wave * 32 + r;
+  const bool ok = tok < T;
+  const uint16_t* xr = x + (ok ? tok : 0) * C;
 
-  auto stage = [&](int ch, int buf) {
-    const uint16_t* src = pack + (int64_t)ch * Cf::CHUNK_E;
-    uint16_t* dst = sm + buf * Cf::CHUNK_E;
-    for (int p = wave; p < PIECES; p += 4)
-      __builtin_amdgcn_global_load_lds((const void*)(src + p * 512 + lane * 8), (lds_ptr_t)(dst + p * 512),
-                                       16, 0, 0);
+  for (int i = threadIdx.x; i < 6 * C; i += 64 * NW)
+    Pg[i] = i < C ? lng[i] : (i < 2 * C ? lnb[i - C] : b1[i - 2 * C]);
+  bf16x8 xb[G::KS1];
+#pragma unroll
+  for (int ks = 0; ks < G::KS1; ++ks)
+    xb[ks] = ok ? *(const bf16x8*)(xr + 16 * ks + 8 * h) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+
+  auto stage = [&](int ch) {
+    const unsigned char* src = (const unsigned char*)pack + (size_t)ch * G::CHUNK_B;
+    unsigned char* dst = smem + (ch % R) * G::CHUNK_B;
+#pragma unroll
+    for (int p = 0; p < G::PW; ++p) {
+      const int piece = wave * G::PW + p;
+      __builtin_amdgcn_global_load_lds((const void*)(src + piece * 1024 + lane * 16),
+                                       (lds_ptr_t)(dst + piece * 1024), 16, 0, 0);
+    }
   };
-  stage(0, 0);
+  stage(0);
+  if constexpr (R == 3) stage(1);
+  // x and the parameters were issued before the chunk(s): wait for them only
+  __builtin_amdgcn_s_waitcnt(vmcnt_n((R - 1) * G::PW));
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): parameter stores landed
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 
-  // LayerNorm of this lane's token (row split over the 4 lanes g4 = 0..3 sharing fr)
-  float xv[KS1][8];
-  float s = 0.f;
+  // LayerNorm (row split over the lane pair h = 0, 1), written back over xb as the fc1 B operand
+  {
+    float s = 0.f;
 #pragma unroll
-  for (int ks = 0; ks < KS1; ++ks) {
-    const bf16x8 v = mok ? *(const bf16x8*)(xr + 32 * ks + 8 * g4) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+    for (int ks = 0; ks < G::KS1; ++ks)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      xv[ks][j] = mmr::bf2f((uint16_t)v[j]);
-      s += xv[ks][j];
-    }
-  }
-  s += __shfl_xor(s, 16, 64);
-  s += __shfl_xor(s, 32, 64);
-  const float mean = s / C;
-  float ss = 0.f;
+      for (int j = 0; j < 8; ++j) s += mmr::bf2f((uint16_t)xb[ks][j]);
+    s += __shfl_xor(s, 32, 64);
+    const float mean = s * (1.0f / C);
+    float ss = 0.f;
 #pragma unroll
-  for (int ks = 0; ks < KS1; ++ks)
+    for (int ks = 0; ks < G::KS1; ++ks)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) ss += (xv[ks][j] - mean) * (xv[ks][j] - mean);
-  ss += __shfl_xor(ss, 16, 64);
-  ss += __shfl_xor(ss, 32, 64);
-  const float rstd = rsqrtf(ss / C + eps);
-  bf16x8 hB[KS1];
-#pragma unroll
-  for (int ks = 0; ks < KS1; ++ks) {
-    const int k0 = 32 * ks + 8 * g4;
-    float h[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) h[j] = (xv[ks][j] - mean) * rstd * lng[k0 + j] + lnb[k0 + j];
-    hB[ks] = __builtin_bit_cast(bf16x8, make_uint4(mmr::pack2bf(h[0], h[1]), mmr::pack2bf(h[2], h[3]),
-                                                   mmr::pack2bf(h[4], h[5]), mmr::pack2bf(h[6], h[7])));
-  }
-
-  f32x4 acc2[NU];
-#pragma unroll
-  for (int u = 0; u < NU; ++u) acc2[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  for (int ch = 0; ch < Cf::NCH; ++ch) {
-    __builtin_amdgcn_s_waitcnt(0x0070 | 0x0F00);  // vmcnt(0): this wave's pieces of chunk ch landed
-    __syncthreads();                                 // ... and every wave's; buffer ch+1 is free
-    if (ch + 1 < Cf::NCH) stage(ch + 1, (ch + 1) & 1);
-    const uint16_t* W1s = sm + (ch & 1) * Cf::CHUNK_E;
-    const uint16_t* W2s = W1s + Cf::W1E;
-    // fc1 (C^T): hidden n = ch*HC + 16t + 4*g4 + rg for token fr
-    float hv[NT1][4];
-#pragma unroll
-    for (int t = 0; t < NT1; ++t) {
-      f32x4 a1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < KS1; ++ks) {
-        const bf16x8 w = *(const bf16x8*)(W1s + (16 * t + fr) * Cf::LD1 + 32 * ks + 8 * g4);
-        a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, hB[ks], a1, 0, 0, 0);
+      for (int j = 0; j < 8; ++j) {
+        const float d = mmr::bf2f((uint16_t)xb[ks][j]) - mean;
+        ss += d * d;
       }
-      const float4 bb = *(const float4*)(b1 + ch * HC + 16 * t + 4 * g4);
-      hv[t][0] = mmr::gelu_erf(a1[0] + bb.x);
-      hv[t][1] = mmr::gelu_erf(a1[1] + bb.y);
-      hv[t][2] = mmr::gelu_erf(a1[2] + bb.z);
-      hv[t][3] = mmr::gelu_erf(a1[3] + bb.w);
+    ss += __shfl_xor(ss, 32, 64);
+    const float rstd = rsqrtf(ss * (1.0f / C) + eps);
+#pragma unroll
+    for (int ks = 0; ks < G::KS1; ++ks) {
+      const int k0 = 16 * ks + 8 * h;
+      const f32x4 g0 = *(const f32x4*)(Pg + k0), g1 = *(const f32x4*)(Pg + k0 + 4);
+      const f32x4 c0 = *(const f32x4*)(Pb + k0), c1 = *(const f32x4*)(Pb + k0 + 4);
+      const float gg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+      const float cc[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (mmr::bf2f((uint16_t)xb[ks][j]) - mean) * rstd * gg[j] + cc[j];
+      xb[ks] = __builtin_bit_cast(bf16x8, make_uint4(mmr::pack2bf(v[0], v[1]), mmr::pack2bf(v[2], v[3]),
+                                                     mmr::pack2bf(v[4], v[5]), mmr::pack2bf(v[6], v[7])));
     }
-    // fc2 (C^T): k-step s covers hidden 32s + 16(j>>2) + 4*g4 + (j&3) for fragment element j
+  }
+
+  f32x16 acc2[G::NU];
 #pragma unroll
-    for (int s2 = 0; s2 < KS2; ++s2) {
-      const bf16x8 hf = __builtin_bit_cast(
-          bf16x8, make_uint4(mmr::pack2bf(hv[2 * s2][0], hv[2 * s2][1]), mmr::pack2bf(hv[2 * s2][2], hv[2 * s2][3]),
-                             mmr::pack2bf(hv[2 * s2 + 1][0], hv[2 * s2 + 1][1]),
-                             mmr::pack2bf(hv[2 * s2 + 1][2], hv[2 * s2 + 1][3])));
+  for (int u = 0; u < G::NU; ++u)
 #pragma unroll
-      for (int u = 0; u < NU; ++u) {
-        const uint16_t* wr = W2s + (16 * u + fr) * Cf::LD2 + 32 * s2 + 4 * g4;
-        const bf16x4 lo = *(const bf16x4*)(wr);
-        const bf16x4 hi = *(const bf16x4*)(wr + 16);
-        const bf16x8 wf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        acc2[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hf, acc2[u], 0, 0, 0);
+    for (int e = 0; e < 16; ++e) acc2[u][e] = 0.f;
+
+  for (int ch = 0; ch < G::NCH; ++ch) {
+    if (R == 3 && ch + 1 < G::NCH) __builtin_amdgcn_s_waitcnt(vmcnt_n(G::PW));  // chunk ch landed
+    else __builtin_amdgcn_s_waitcnt(vmcnt_n(0));
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's pieces landed; the slot refilled next is free
+    asm volatile("" ::: "memory");
+    if (ch + R - 1 < G::NCH) stage(ch + R - 1);
+    const unsigned char* W1s = smem + (ch % R) * G::CHUNK_B;
+    const unsigned char* W2s = W1s + G::W1B;
+#pragma unroll
+    for (int t = 0; t < G::NT; ++t) {  // 32 hidden units per step
+      f32x16 a1;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) a1[e] = 0.f;
+      const int row = 32 * t + r;
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks) {
+        const bf16x8 w = *(const bf16x8*)(W1s + (row * G::U1 + unit_swz<G::U1>(row, 2 * ks + h)) * 16);
+        a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w, xb[ks], a1, 0, 0, 0);
+      }
+      // lane holds hidden HC*ch + 32t + 8i + 4h + rr (i, rr = 0..3) of token r
+      uint32_t hp[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 bb = *(const f32x4*)(Pb1 + HC * ch + 32 * t + 8 * i + 4 * h);
+        hp[2 * i] = mmr::pack2bf(gelu_t<FAST>(a1[4 * i] + bb[0]), gelu_t<FAST>(a1[4 * i + 1] + bb[1]));
+        hp[2 * i + 1] = mmr::pack2bf(gelu_t<FAST>(a1[4 * i + 2] + bb[2]), gelu_t<FAST>(a1[4 * i + 3] + bb[3]));
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {  // k-step over hidden 32t + 16 s2 .. +15
+        const bf16x8 hf = __builtin_bit_cast(bf16x8, make_uint4(hp[4 * s2], hp[4 * s2 + 1], hp[4 * s2 + 2],
+                                                                hp[4 * s2 + 3]));
+        const int q = 2 * (2 * t + s2) + h;
+#pragma unroll
+        for (int u = 0; u < G::NU; ++u) {
+          const int c = 32 * u + r;
+          const bf16x8 w = *(const bf16x8*)(W2s + (c * G::U2 + unit_swz<G::U2>(c, q)) * 16);
+          acc2[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w, hf, acc2[u], 0, 0, 0);
+        }
       }
     }
   }
 
-  // y[m][c] = x + b2 + fc2; lane holds c = 16u + 4*g4 + 0..3 of token fr
-  if (mok) {
+  // y[tok][c] = x + b2 + fc2, c = 32u + 8i + 4h + rr
+  if (ok) {
 #pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      const int c = 16 * u + 4 * g4;
-      const float4 bb = *(const float4*)(b2 + c);
-      const uint2 xr2 = *(const uint2*)(xr + c);
-      const float v0 = acc2[u][0] + bb.x + __uint_as_float(xr2.x << 16);
-      const float v1 = acc2[u][1] + bb.y + __uint_as_float(xr2.x & 0xFFFF0000u);
-      const float v2 = acc2[u][2] + bb.z + __uint_as_float(xr2.y << 16);
-      const float v3 = acc2[u][3] + bb.w + __uint_as_float(xr2.y & 0xFFFF0000u);
-      *(uint2*)(y + m * C + c) = make_uint2(mmr::pack2bf(v0, v1), mmr::pack2bf(v2, v3));
+    for (int u = 0; u < G::NU; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = 32 * u + 8 * i + 4 * h;
+        const float4 bb = *(const float4*)(b2 + c);
+        const uint2 xv = *(const uint2*)(xr + c);
+        const float v0 = acc2[u][4 * i] + bb.x + __uint_as_float(xv.x << 16);
+        const float v1 = acc2[u][4 * i + 1] + bb.y + __uint_as_float(xv.x & 0xFFFF0000u);
+        const float v2 = acc2[u][4 * i + 2] + bb.z + __uint_as_float(xv.y << 16);
+        const float v3 = acc2[u][4 * i + 3] + bb.w + __uint_as_float(xv.y & 0xFFFF0000u);
+        *(uint2*)(y + tok * C + c) = make_uint2(mmr::pack2bf(v0, v1), mmr::pack2bf(v2, v3));
+      }
+  }
+}
+
+
+// Resident-weight variant (C = 96: W1 + W2 = 147 KiB fit in one CU's LDS).  One workgroup per CU,
+// persistent: each wave walks 32-token tiles on its own (no barrier after the one-time weight
+// load), prefetching the next tile's x into registers while it computes the current one.
+template <int C, int NW, bool FAST, bool XRES>
+__global__ __launch_bounds__(64 * NW) void swin_mlp_res(const uint16_t* __restrict__ x,
+                                                        const float* __restrict__ lng,
+                                                        const float* __restrict__ lnb,
+                                                        const uint16_t* __restrict__ pack,
+                                                        const float* __restrict__ b1,
+                                                        const float* __restrict__ b2,
+                                                        uint16_t* __restrict__ y, int64_t T, float eps) {
+  using G = MlpGeo<C, NW, 64, 2>;
+  constexpr int WB = G::NCH * G::CHUNK_B;
+  constexpr int PWW = WB / 1024 / NW;
+  static_assert(WB % (1024 * NW) == 0, "weights must split evenly over the waves");
+  // all weight chunks, then the f32 parameters (one dynamic LDS object: reads of a separate static
+  // array after global_load_lds draw a conservative vmcnt(0) from hipcc)
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* Pg = (float*)(smem + WB);
+  const float* Pb = Pg + C;
+  const float* Pb1 = Pg + 2 * C;
+  const float* Pb2 = Pg + 6 * C;
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t ntile = (T + 31) / 32, stride = (int64_t)gridDim.x * NW;
+  int64_t tile = (int64_t)blockIdx.x * NW + wave;
+
+  for (int i = threadIdx.x; i < 7 * C; i += 64 * NW)
+    Pg[i] = i < C ? lng[i] : (i < 2 * C ? lnb[i - C] : (i < 6 * C ? b1[i - 2 * C] : b2[i - 6 * C]));
+#pragma unroll
+  for (int p = 0; p < PWW; ++p) {
+    const int piece = wave * PWW + p;
+    __builtin_amdgcn_global_load_lds((const void*)((const unsigned char*)pack + piece * 1024 + lane * 16),
+                                     (lds_ptr_t)(smem + piece * 1024), 16, 0, 0);
+  }
+  auto load_x = [&](int64_t tl, bf16x8* dst) {
+    const int64_t tk = tl * 32 + r;
+    const bool ok = tl < ntile && tk < T;
+    const uint16_t* xr = x + (ok ? tk : 0) * C;
+#pragma unroll
+    for (int ks = 0; ks < G::KS1; ++ks)
+      dst[ks] = ok ? *(const bf16x8*)(xr + 16 * ks + 8 * h) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+  };
+  bf16x8 xn[G::KS1];
+  load_x(tile, xn);
+  __builtin_amdgcn_s_waitcnt(vmcnt_n(0));
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  for (; tile < ntile; tile += stride) {
+    asm volatile("" ::: "memory");  // keep the LN/bias parameter reads in the loop (LICM would pin
+                                    // ~100 VGPRs of them across it)
+    bf16x8 xr[G::KS1], xb[G::KS1];
+#pragma unroll
+    for (int ks = 0; ks < G::KS1; ++ks) xr[ks] = xn[ks];
+    load_x(tile + stride, xn);  // next tile's x in flight during this one
+    const int64_t tok = tile * 32 + r;
+
+    // LayerNorm (row split over the lane pair h = 0, 1) -> fc1 B operand
+    {
+      float s = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += mmr::bf2f((uint16_t)xr[ks][j]);
+      s += __shfl_xor(s, 32, 64);
+      const float mean = s * (1.0f / C);
+      float ss = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = mmr::bf2f((uint16_t)xr[ks][j]) - mean;
+          ss += d * d;
+        }
+      ss += __shfl_xor(ss, 32, 64);
+      const float rstd = rsqrtf(ss * (1.0f / C) + eps);
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks) {
+        const int k0 = 16 * ks + 8 * h;
+        const f32x4 g0 = *(const f32x4*)(Pg + k0), g1 = *(const f32x4*)(Pg + k0 + 4);
+        const f32x4 c0 = *(const f32x4*)(Pb + k0), c1 = *(const f32x4*)(Pb + k0 + 4);
+        const float gg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+        const float cc[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (mmr::bf2f((uint16_t)xr[ks][j]) - mean) * rstd * gg[j] + cc[j];
+        xb[ks] = __builtin_bit_cast(bf16x8, make_uint4(mmr::pack2bf(v[0], v[1]), mmr::pack2bf(v[2], v[3]),
+                                                       mmr::pack2bf(v[4], v[5]), mmr::pack2bf(v[6], v[7])));
+      }
+    }
+
+    f32x16 acc2[G::NU];
+#pragma unroll
+    for (int u = 0; u < G::NU; ++u)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc2[u][e] = 0.f;
+
+    // hidden loop, software-pipelined: the W1 fragments of step t+1 and the W2 fragments of step t
+    // are in flight while step t's GELU runs
+    auto rd_w1 = [&](int t, bf16x8* f) {
+      const unsigned char* W1s = smem + (t >> 1) * G::CHUNK_B;
+      const int row = 32 * (t & 1) + r;
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks)
+        f[ks] = *(const bf16x8*)(W1s + (row * G::U1 + unit_swz<G::U1>(row, 2 * ks + h)) * 16);
+    };
+    auto rd_w2 = [&](int t, bf16x8* f) {
+      const unsigned char* W2s = smem + (t >> 1) * G::CHUNK_B + G::W1B;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int u = 0; u < G::NU; ++u) {
+          const int c = 32 * u + r, q = 2 * (2 * (t & 1) + s2) + h;
+          f[s2 * G::NU + u] = *(const bf16x8*)(W2s + (c * G::U2 + unit_swz<G::U2>(c, q)) * 16);
+        }
+    };
+    bf16x8 w1f[G::KS1], w2f[2 * G::NU];
+    rd_w1(0, w1f);
+#pragma unroll 1
+    for (int t = 0; t < 4 * C / 32; ++t) {  // 32 hidden units per step
+      f32x16 a1;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) a1[e] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks) a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1f[ks], xb[ks], a1, 0, 0, 0);
+      rd_w2(t, w2f);
+      if (t + 1 < 4 * C / 32) rd_w1(t + 1, w1f);
+      uint32_t hp[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 bb = *(const f32x4*)(Pb1 + 32 * t + 8 * i + 4 * h);
+        hp[2 * i] = mmr::pack2bf(gelu_t<FAST>(a1[4 * i] + bb[0]), gelu_t<FAST>(a1[4 * i + 1] + bb[1]));
+        hp[2 * i + 1] = mmr::pack2bf(gelu_t<FAST>(a1[4 * i + 2] + bb[2]), gelu_t<FAST>(a1[4 * i + 3] + bb[3]));
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 hf = __builtin_bit_cast(bf16x8, make_uint4(hp[4 * s2], hp[4 * s2 + 1], hp[4 * s2 + 2],
+                                                                hp[4 * s2 + 3]));
+#pragma unroll
+        for (int u = 0; u < G::NU; ++u)
+          acc2[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2f[s2 * G::NU + u], hf, acc2[u], 0, 0, 0);
+      }
+    }
+
+    // y = x + b2 + fc2: lane half h holds channels 32u + 16 half + 8h + 0..7 (w2_channel order)
+    if (tok < T) {
+#pragma unroll
+      for (int u = 0; u < G::NU; ++u)
+#pragma unroll
+        for (int hf2 = 0; hf2 < 2; ++hf2) {
+          const int c0 = 32 * u + 16 * hf2 + 8 * h;
+          const f32x4 bl = *(const f32x4*)(Pb2 + c0), bh = *(const f32x4*)(Pb2 + c0 + 4);
+          const bf16x8 xv = XRES ? xr[2 * u + hf2] : *(const bf16x8*)(x + tok * C + c0);
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            v[j] = acc2[u][8 * hf2 + j] + (j < 4 ? bl[j] : bh[j - 4]) + mmr::bf2f((uint16_t)xv[j]);
+          *(uint4*)(y + tok * C + c0) = make_uint4(mmr::pack2bf(v[0], v[1]), mmr::pack2bf(v[2], v[3]),
+                                                   mmr::pack2bf(v[4], v[5]), mmr::pack2bf(v[6], v[7]));
+        }
     }
   }
 }
 
-template <int C, int HC>
-mmr_status launch_pack(const uint16_t* w1, const uint16_t* w2, uint16_t* pack, hipStream_t st) {
-  using Cf = MlpCfg<C, HC>;
-  const int64_t n = (int64_t)Cf::NCH * Cf::CHUNK_E;
-  swin_mlp_pack<C, HC><<<dim3((unsigned)mmr::ceil_div(n, 256)), 256, 0, st>>>(w1, w2, pack);
+int cu_count() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
+template <int C, int NW, bool FAST, bool XRES>
+mmr_status launch_res(const uint16_t* x, const float* g, const float* b, const uint16_t* pack,
+                      const float* b1, const float* b2, uint16_t* y, int64_t T, float eps,
+                      hipStream_t st) {
+  using G = MlpGeo<C, NW, 64, 2>;
+  const int64_t wave_tiles = (T + 31) / 32;
+  const int64_t grid = std::min<int64_t>(cu_count(), (wave_tiles + NW - 1) / NW);
+  swin_mlp_res<C, NW, FAST, XRES><<<dim3((unsigned)grid), 64 * NW, G::NCH * G::CHUNK_B + 7 * C * 4, st>>>(
+      x, g, b, pack, b1, b2, y, T, eps);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }
 
-template <int C, int HC>
-mmr_status launch_mlp(const uint16_t* x, const float* g, const float* b, const uint16_t* pack,
-                      const float* b1, const float* b2, uint16_t* y, int64_t T, float eps,
-                      hipStream_t st) {
-  using Cf = MlpCfg<C, HC>;
-  const size_t lds = 2 * Cf::CHUNK_E * sizeof(uint16_t);
-  swin_mlp<C, HC><<<dim3((unsigned)mmr::ceil_div(T, 64)), 256, lds, st>>>(x, g, b, pack, b1, b2, y, T, eps);
+template <int C, int HC, bool PERM>
+mmr_status launch_pack(const uint16_t* w1, const uint16_t* w2, uint16_t* pack, hipStream_t st) {
+  const int64_t n = (int64_t)8 * C * C;
+  swin_mlp_pack<C, HC, PERM><<<dim3((unsigned)mmr::ceil_div(n, 256)), 256, 0, st>>>(w1, w2, pack);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+template <int C, int NW, int HC, int R, bool FAST>
+mmr_status launch_stream(const uint16_t* x, const float* g, const float* b, const uint16_t* pack,
+                         const float* b1, const float* b2, uint16_t* y, int64_t T, float eps,
+                         hipStream_t st) {
+  using G = MlpGeo<C, NW, HC, R>;
+  swin_mlp<C, NW, HC, R, FAST><<<dim3((unsigned)mmr::ceil_div(T, G::TOK)), 64 * NW, G::LDS_B, st>>>(
+      x, g, b, pack, b1, b2, y, T, eps);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }
@@ -201,9 +468,7 @@ mmr_status launch_mlp(const uint16_t* x, const float* g, const float* b, const u
 extern "C" {
 
 int64_t mmr_swin_mlp_pack_elems(int32_t c) {
-  if (c == 96) return (int64_t)MlpCfg<96, 64>::NCH * MlpCfg<96, 64>::CHUNK_E;
-  if (c == 192) return (int64_t)MlpCfg<192, 32>::NCH * MlpCfg<192, 32>::CHUNK_E;
-  return 0;
+  return (c == 96 || c == 192) ? (int64_t)8 * c * c : 0;
 }
 
 mmr_status mmr_swin_mlp_pack(const uint16_t* w1, const uint16_t* w2, uint16_t* pack, int32_t c,
@@ -211,8 +476,9 @@ mmr_status mmr_swin_mlp_pack(const uint16_t* w1, const uint16_t* w2, uint16_t* p
   mmr::clear_error();
   MMR_REQUIRE(w1 && w2 && pack, "mmr_swin_mlp_pack: NULL pointer");
   hipStream_t st = mmr::as_stream(stream);
-  if (c == 96) return launch_pack<96, 64>(w1, w2, pack, st);
-  if (c == 192) return launch_pack<192, 32>(w1, w2, pack, st);
+  // C = 96: resident kernel (W2 rows in w2_channel order); C = 192: streamed chunks
+  if (c == 96) return launch_pack<96, 64, true>(w1, w2, pack, st);
+  if (c == 192) return launch_pack<192, 64, false>(w1, w2, pack, st);
   mmr::set_error("mmr_swin_mlp_pack: C=%d not built (96, 192)", c);
   return MMR_ERR_UNSUPPORTED;
 }
@@ -226,8 +492,8 @@ mmr_status mmr_swin_mlp(const uint16_t* x, const float* ln_g, const float* ln_b,
   MMR_REQUIRE(x != y, "mmr_swin_mlp: in-place not supported");
   if (tokens == 0) return MMR_OK;
   hipStream_t st = mmr::as_stream(stream);
-  if (c == 96) return launch_mlp<96, 64>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
-  if (c == 192) return launch_mlp<192, 32>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
+  if (c == 96) return launch_res<96, 8, true, true>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
+  if (c == 192) return launch_stream<192, 8, 64, 3, true>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
   mmr::set_error("mmr_swin_mlp: C=%d not built (96, 192)", c);
   return MMR_ERR_UNSUPPORTED;
 }
