@@ -91,6 +91,13 @@ mmr_status mmr_linear_bf16(const uint16_t* x, const uint16_t* w, const float* bi
 mmr_status mmr_layernorm_bf16(const uint16_t* x, const float* gamma, const float* beta,
                               uint16_t* y, int64_t rows, int32_t c, float eps, void* stream);
 
+/* Post-LN residual block: y = LayerNorm(x + residual) (sum in f32), bf16 in / out.  BERT's
+ * BertSelfOutput / BertOutput (HF modeling_bert; reference fusion.py:322-325 via AutoModel):
+ * the attention-output and FFN2 GEMMs then need no residual epilogue. */
+mmr_status mmr_add_layernorm_bf16(const uint16_t* x, const uint16_t* residual, const float* gamma,
+                                  const float* beta, uint16_t* y, int64_t rows, int32_t c,
+                                  float eps, void* stream);
+
 /* BERT embeddings (HF BertEmbeddings): LN(word[id] + pos[l] + type[0]) -> bf16 (b*l, c). */
 mmr_status mmr_bert_embed(const int64_t* ids, const float* word, const float* pos,
                           const float* type0, const float* gamma, const float* beta, uint16_t* y,

@@ -29,6 +29,7 @@ SIGNATURES = {
     "mmr_merge_topk": [c_vp, c_vp, c_i32, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp],
     "mmr_linear_bf16": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp],
     "mmr_layernorm_bf16": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp],
+    "mmr_add_layernorm_bf16": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp],
     "mmr_bert_embed": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp],
     "mmr_bert_attention": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_swin_window_attention": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp],

@@ -408,16 +408,257 @@ __global__ __launch_bounds__(512, 2 * OCC) void gemm_bf16_tn_big(const uint16_t*
   }
 }
 
+
+// ---------------------------------------------------------------- 4-wave persistent large-tile GEMM
+// One wave per SIMD with a 128 x 16NT wave tile (NT = 8: 256 x 256 workgroup tile; NT = 6:
+// 256 x 192): twice the MFMA work per LDS fragment byte of the 8-wave 64x64 layout; the 8 x NT
+// accumulators (<= 256 f32) live in AGPRs.  KB = 64, two LDS stages.
+// Persistent: one workgroup per CU walks its XCD's share of the tiles (consecutive tiles, so the
+// X row panel and W stay in that XCD's L2).  The last slice of a tile issues the glds of the NEXT
+// tile's first slice, and the epilogue stages 16 rows at a time through a small per-wave LDS
+// area outside the two stages, so the next tile's loads are in flight while this tile's bias /
+// GELU / residual / 16-B row stores run; the next tile's first wait counts the stores out
+// (vmcnt(NSTORE)) instead of draining them.
+constexpr int EPI4_PAD = 8;
+
+template <int NT>
+constexpr size_t w4_lds_bytes() {
+  return 2ull * (256 + 32 * NT) * 64 * 2 + 4ull * 16 * (16 * NT + EPI4_PAD) * 2;
+}
+
+template <int NT, int ACT, bool HAS_BIAS, bool HAS_RES>
+__global__ __launch_bounds__(256) void gemm_bf16_tn_w4(const uint16_t* __restrict__ X,
+                                                       const uint16_t* __restrict__ W,
+                                                       const float* __restrict__ bias,
+                                                       const uint16_t* __restrict__ R,
+                                                       uint16_t* __restrict__ Y, int64_t M, int N,
+                                                       int K, int tiles_m, int tiles_n) {
+  constexpr int MT = 8, KB = 64, RPI = 8;
+  constexpr int TBM = 256, TBN = 32 * NT;
+  constexpr int TA = TBM * KB, TB = TBN * KB;  // bf16 elements per stage
+  constexpr int PA = TBM / RPI / 4, PB = TBN / RPI / 4;  // glds pieces per wave per stage
+  constexpr int ELD = 16 * NT + EPI4_PAD;
+  constexpr int CPR = 2 * NT;            // 16-B chunks per wave-tile row
+  constexpr int CPL = 16 * CPR / 64;     // chunks per lane per 16-row group
+  constexpr int NSTORE = MT * CPL;       // global stores per wave per tile
+  constexpr int NLOADS = HAS_BIAS ? NT : 0;  // bias, fetched during slice 0
+  static_assert(NSTORE <= 63 && NLOADS <= 63, "vmcnt range");
+  extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];  // [2][TA + TB] + epilogue
+
+  const int ntiles = tiles_m * tiles_n;
+  const int per = gridDim.x / 8, xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
+  const int lo = (int)((int64_t)ntiles * xcd / 8), hi = (int)((int64_t)ntiles * (xcd + 1) / 8);
+  int t = lo + slot;
+  if (t >= hi) return;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nk = K / KB;
+
+  // glds sources: piece p of A covers rows RPI*(wave + 4p) .. +7, lane -> (row, swizzled chunk).
+  // 32-bit element offsets from the uniform base (saddr form, one VGPR per piece); rows past M are
+  // clamped to M-1 (their products are never stored); N % TBN == 0 and K % 64 == 0 (launcher).
+  // Per-lane byte offsets inside a tile's row panels are tile-independent (one VGPR per piece,
+  // glds in saddr form); a tile contributes only uniform bases.  The last row tile is shifted up
+  // to end at row M (M >= 256): its first rows recompute rows of the previous tile, and writing
+  // those identical values twice is harmless — no per-row clamping or zero page in the loop.
+  const int prow_in = lane >> 3, pch = lane & 7;
+  uint32_t offA[PA], offB[PB];
+#pragma unroll
+  for (int j = 0; j < PA; ++j) {
+    const int row = RPI * (wave + 4 * j) + prow_in;
+    offA[j] = (uint32_t)((row * K + swz(row, pch) * 8) * 2);
+  }
+#pragma unroll
+  for (int j = 0; j < PB; ++j) {
+    const int row = RPI * (wave + 4 * j) + prow_in;
+    offB[j] = (uint32_t)((row * K + swz(row, pch) * 8) * 2);
+  }
+  const char* Xt = nullptr;  // this tile's panels (uniform)
+  const char* Wt = nullptr;
+  uint32_t kofs = 0;         // byte offset of the next slice to load
+  auto tile_m0 = [&](int tile) { return std::min<int64_t>((int64_t)(tile / tiles_n) * TBM, M - TBM); };
+  auto setup = [&](int tile) {
+    Xt = (const char*)(X + tile_m0(tile) * K);
+    Wt = (const char*)(W + (int64_t)(tile % tiles_n) * TBN * K);
+    kofs = 0;
+  };
+  auto piece = [&](int s, int p, uint32_t ko) {
+    uint16_t* la = dsm + s * (TA + TB);
+    if (p < PA)
+      __builtin_amdgcn_global_load_lds((const void*)(Xt + (offA[p] + ko)), (lds_ptr_t)(la + RPI * (wave + 4 * p) * KB), 16, 0, 0);
+    else
+      __builtin_amdgcn_global_load_lds((const void*)(Wt + (offB[p - PA] + ko)), (lds_ptr_t)(la + TA + RPI * (wave + 4 * (p - PA)) * KB), 16, 0, 0);
+  };
+
+  setup(t);
+#pragma unroll
+  for (int p = 0; p < PA + PB; ++p) piece(0, p, 0);
+  kofs = KB * 2;
+  int sb = 0;            // stage holding the slice about to be consumed
+  bool stores_out = false;  // previous tile's epilogue stores may still be in flight
+  uint16_t* et = dsm + 2 * (TA + TB) + wave * 16 * ELD;
+
+  while (true) {
+    const int64_t m0 = tile_m0(t);
+    const int n0 = (t % tiles_n) * TBN;
+    const int tnext = t + per;
+    const bool has_next = tnext < hi;
+
+    f32x4 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    // bias is fetched during slice 0 (after its glds) and stays in registers across the main
+    // loop; the residual (accumulator layout) is fetched whole at the start of the epilogue
+    f32x4 bq[NT];
+    uint2 rq[HAS_RES ? MT : 1][HAS_RES ? NT : 1];
+    for (int kt = 0; kt < nk; ++kt) {
+      // glds of this slice were issued before: the previous tile's stores (kt = 0) or this tile's
+      // epilogue operands (kt = 1) may stay in flight
+      if (kt == 0 && stores_out) __builtin_amdgcn_s_waitcnt(vmcnt_imm(NSTORE));
+      else if (kt == 1) __builtin_amdgcn_s_waitcnt(vmcnt_imm(NLOADS));
+      else __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // slice landed for every wave; the other stage is free
+      asm volatile("" ::: "memory");
+      const bool last = kt + 1 == nk;
+      if (last && has_next) setup(tnext);  // the last slice prefetches the next tile's first
+      // after the very last slice the loads are issued anyway (branch-free), re-reading slice 0
+      const uint32_t ko = (last && !has_next) ? 0u : kofs;
+      const int s = sb;
+      const uint16_t* la = dsm + s * (TA + TB);
+      const uint16_t* lb = la + TA;
+      auto rdA = [&](int ks, int i) {
+        const int rowa = wm * 128 + i * 16 + fr;
+        return *(const bf16x8*)(la + rowa * KB + swz(rowa, ks * 4 + fq) * 8);
+      };
+      auto rdB = [&](int ks, int j) {
+        const int rowb = wn * 16 * NT + j * 16 + fr;
+        return *(const bf16x8*)(lb + rowb * KB + swz(rowb, ks * 4 + fq) * 8);
+      };
+      bf16x8 a0[MT], b0[NT], a1[MT], b1[NT];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) b0[j] = rdB(0, j);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) a0[i] = rdA(0, i);
+      // k-step 0: per A row-tile i, the next slice's glds pieces (source order is kept: glds are
+      // scheduling barriers for hipcc) and one k-step-1 fragment, then NT MFMAs
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+#pragma unroll
+        for (int p = i * (PA + PB) / MT; p < (i + 1) * (PA + PB) / MT; ++p) piece(s ^ 1, p, ko);
+        a1[i] = rdA(1, i);
+        if (i < NT) b1[i] = rdB(1, i);
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j], a0[i], acc[i][j], 0, 0, 0);
+      }
+      kofs += KB * 2;
+      if (kt == 0) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int n = n0 + wn * 16 * NT + j * 16 + fq * 4;
+          bq[j] = HAS_BIAS ? *(const f32x4*)(bias + n) : (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a1[i], acc[i][j], 0, 0, 0);
+      sb ^= 1;
+    }
+
+    // epilogue, 16 rows at a time: act(acc + bias) (+ residual) in f32 -> bf16 in the wave's LDS
+    // area -> 16-B row chunks -> Y
+    if constexpr (HAS_RES) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          rq[i][j] = *(const uint2*)(R + (m0 + wm * 128 + i * 16 + fr) * N + n0 + wn * 16 * NT + j * 16 + fq * 4);
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        float v[4];
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) {
+          v[rg] = acc[i][j][rg] + bq[j][rg];
+          if (ACT == 1) v[rg] = mmr::gelu_fast(v[rg]);
+        }
+        if constexpr (HAS_RES) {
+          const uint2 q = rq[i][j];
+          v[0] += __uint_as_float(q.x << 16);
+          v[1] += __uint_as_float(q.x & 0xFFFF0000u);
+          v[2] += __uint_as_float(q.y << 16);
+          v[3] += __uint_as_float(q.y & 0xFFFF0000u);
+        }
+        *(uint2*)(et + fr * ELD + j * 16 + fq * 4) = make_uint2(mmr::pack2bf(v[0], v[1]), mmr::pack2bf(v[2], v[3]));
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        const int idx = c * 64 + lane;
+        const int64_t m = m0 + wm * 128 + i * 16 + idx / CPR;
+        const int n = n0 + wn * 16 * NT + (idx % CPR) * 8;
+        *(bf16x8*)(Y + m * N + n) = *(const bf16x8*)(et + (idx / CPR) * ELD + (idx % CPR) * 8);
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (!has_next) break;
+    t = tnext;
+    stores_out = true;
+  }
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // no LDS-DMA may land after the workgroup retires
+}
+
+int cu_count() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
 template <int ACT, bool HB, bool HR>
 void launch(const uint16_t* x, const uint16_t* w, const float* b, const uint16_t* r, uint16_t* y,
             int64_t m, int n, int k, hipStream_t st) {
   // big tiles when the grid still fills >= ~2 rounds of 256 CUs and K is deep enough
-  static const int cfg = [] {
-    // diagnostic override: 0 off; 1 256x256 KB64 x2; 2 256x256 KB32 x4; 3 256x128 KB64 x3
-    const char* e = getenv("MMR_GEMM_BIG");
-    return e ? atoi(e) : 1;
-  }();
+  // diagnostic override: 0 off; 1 256x256 KB64 x2; 2 256x256 KB32 x4; 3 256x128 KB64 x3
+  const char* cfge = getenv("MMR_GEMM_BIG");
+  const int cfg = cfge ? atoi(cfge) : 1;
   const int64_t t256 = mmr::ceil_div(m, 256);
+  const char* w4e = getenv("MMR_GEMM_W4");  // diagnostic: 0 off, 1 on (default), 2 256x192 only
+  const int w4 = w4e ? atoi(w4e) : 1;
+  // the persistent 4-wave kernel for epilogues without a residual (its 1-wave-per-SIMD epilogue
+  // cannot hide a residual tile's fetch); residual GEMMs keep the 8-wave kernels
+  if (w4 && !HR && k >= 256 && k % 64 == 0 && m >= 4096) {
+    // persistent grid: a multiple of 8 workgroups (one per CU), tiles split evenly per XCD
+    const int grid = std::max(8, cu_count() / 8 * 8);
+    if constexpr (!HR) {  // 128x128 wave tiles: no registers left for a residual tile
+      if (w4 == 1 && n % 256 == 0 && (t256 * (n / 256)) % grid == 0) {
+        const int tm = (int)t256, tn = n / 256;
+        gemm_bf16_tn_w4<8, ACT, HB, HR><<<dim3(std::min<int64_t>(grid, (int64_t)tm * tn)), dim3(256), w4_lds_bytes<8>(), st>>>(x, w, b, r, y, m, n, k, tm, tn);
+        return;
+      }
+    }
+    if (n % 192 == 0) {
+      const int tm = (int)t256, tn = n / 192;
+      gemm_bf16_tn_w4<6, ACT, HB, HR><<<dim3(std::min<int64_t>(grid, (int64_t)tm * tn)), dim3(256), w4_lds_bytes<6>(), st>>>(x, w, b, r, y, m, n, k, tm, tn);
+      return;
+    }
+  }
   if (cfg != 0 && k >= 256 && m >= 4096) {
     if (cfg <= 2 && n % 256 == 0 && t256 * (n / 256) >= 512) {
       const int tm = (int)t256, tn = n / 256;

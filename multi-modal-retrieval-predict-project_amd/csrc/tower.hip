@@ -33,8 +33,9 @@ __device__ __forceinline__ void store8(uint16_t* p, const float* v) {
 // LPR lanes per row (64/LPR rows per wave) so narrow Swin rows (C = 96..384) keep every lane busy;
 // the row stays in registers (<= 8 chunks of 8 per lane): one read, one write, exact two-pass
 // (centred) variance like torch.
-template <int LPR>
+template <int LPR, bool ADD>
 __global__ __launch_bounds__(256) void layernorm_bf16(const uint16_t* __restrict__ x,
+                                                      const uint16_t* __restrict__ r,
                                                       const float* __restrict__ g,
                                                       const float* __restrict__ b,
                                                       uint16_t* __restrict__ y, int64_t rows,
@@ -53,6 +54,12 @@ __global__ __launch_bounds__(256) void layernorm_bf16(const uint16_t* __restrict
     const int ch = sub + i * LPR;
     if (ok && ch < nch) {
       load8(xr + ch * 8, v[i]);
+      if (ADD) {  // post-LN residual: LN(x + r), the sum kept in f32
+        float w[8];
+        load8(r + (ok ? row : 0) * c + ch * 8, w);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] += w[j];
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += v[i][j];
     }
@@ -632,12 +639,12 @@ __global__ __launch_bounds__(256) void l2_normalize_rows(float* __restrict__ y, 
 // ================================================================== C ABI
 extern "C" {
 
-mmr_status mmr_layernorm_bf16(const uint16_t* x, const float* gamma, const float* beta,
-                              uint16_t* y, int64_t rows, int32_t c, float eps, void* stream) {
-  mmr::clear_error();
-  MMR_REQUIRE(x && gamma && beta && y, "mmr_layernorm_bf16: NULL pointer");
-  MMR_REQUIRE(c > 0 && c % 8 == 0 && rows >= 0, "mmr_layernorm_bf16: c=%d must be a positive multiple of 8", c);
-  MMR_REQUIRE(c <= 4096, "mmr_layernorm_bf16: c=%d > 4096", c);
+static mmr_status layernorm_launch(const uint16_t* x, const uint16_t* r, const float* gamma,
+                                   const float* beta, uint16_t* y, int64_t rows, int32_t c,
+                                   float eps, void* stream, const char* who) {
+  MMR_REQUIRE(x && gamma && beta && y, "%s: NULL pointer", who);
+  MMR_REQUIRE(c > 0 && c % 8 == 0 && rows >= 0, "%s: c=%d must be a positive multiple of 8", who, c);
+  MMR_REQUIRE(c <= 4096, "%s: c=%d > 4096", who, c);
   if (rows == 0) return MMR_OK;
   hipStream_t st = mmr::as_stream(stream);
   const int nch = c / 8;
@@ -645,12 +652,30 @@ mmr_status mmr_layernorm_bf16(const uint16_t* x, const float* gamma, const float
   while (lpr > 8 && nch <= (lpr / 2) * 2) lpr /= 2;  // <= 2 chunks per lane for narrow rows
   const int64_t rows_per_block = 4 * (64 / lpr);
   const dim3 grid((unsigned)mmr::ceil_div(rows, rows_per_block));
-  if (lpr == 8) layernorm_bf16<8><<<grid, 256, 0, st>>>(x, gamma, beta, y, rows, c, eps);
-  else if (lpr == 16) layernorm_bf16<16><<<grid, 256, 0, st>>>(x, gamma, beta, y, rows, c, eps);
-  else if (lpr == 32) layernorm_bf16<32><<<grid, 256, 0, st>>>(x, gamma, beta, y, rows, c, eps);
-  else layernorm_bf16<64><<<grid, 256, 0, st>>>(x, gamma, beta, y, rows, c, eps);
+#define MMR_LN(L)                                                                           \
+  (r ? layernorm_bf16<L, true><<<grid, 256, 0, st>>>(x, r, gamma, beta, y, rows, c, eps)    \
+     : layernorm_bf16<L, false><<<grid, 256, 0, st>>>(x, r, gamma, beta, y, rows, c, eps))
+  if (lpr == 8) MMR_LN(8);
+  else if (lpr == 16) MMR_LN(16);
+  else if (lpr == 32) MMR_LN(32);
+  else MMR_LN(64);
+#undef MMR_LN
   MMR_LAUNCH_CHECK();
   return MMR_OK;
+}
+
+mmr_status mmr_layernorm_bf16(const uint16_t* x, const float* gamma, const float* beta,
+                              uint16_t* y, int64_t rows, int32_t c, float eps, void* stream) {
+  mmr::clear_error();
+  return layernorm_launch(x, nullptr, gamma, beta, y, rows, c, eps, stream, "mmr_layernorm_bf16");
+}
+
+mmr_status mmr_add_layernorm_bf16(const uint16_t* x, const uint16_t* residual, const float* gamma,
+                                  const float* beta, uint16_t* y, int64_t rows, int32_t c,
+                                  float eps, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(residual, "mmr_add_layernorm_bf16: NULL residual");
+  return layernorm_launch(x, residual, gamma, beta, y, rows, c, eps, stream, "mmr_add_layernorm_bf16");
 }
 
 mmr_status mmr_bert_embed(const int64_t* ids, const float* word, const float* pos,

@@ -40,6 +40,17 @@ def layernorm(x, g, b, eps, out=None):
     return y
 
 
+def add_layernorm(x, r, g, b, eps, out=None):
+    """LayerNorm(x + r) (post-LN residual block), sum in f32."""
+    _lib.require_gpu(x)
+    c = x.shape[-1]
+    assert r.shape == x.shape
+    y = out if out is not None else torch.empty_like(x)
+    _chk(_L().mmr_add_layernorm_bf16(_lib.ptr(x), _lib.ptr(r), _lib.ptr(g), _lib.ptr(b), _lib.ptr(y),
+                                     x.numel() // c, c, float(eps), _s(x)), "mmr_add_layernorm_bf16")
+    return y
+
+
 def bert_embed(ids, word, pos, type0, g, b, eps):
     _lib.require_gpu(ids)
     B, L = ids.shape

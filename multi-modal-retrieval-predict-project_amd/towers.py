@@ -12,8 +12,9 @@ Per-block dataflow (all hand-written kernels, bf16 activations, f32 accumulation
                -> fc2 GEMM(+bias +residual); for C = 96 / 192 the MLP half is ONE fused kernel
                (mmr_swin_mlp: LN2 + fc1 + GELU + fc2 + residual, hidden kept on chip)
   PatchMerge   gather 2x2 + LN(4C) fused -> reduction GEMM (no bias)
-  BERT layer   QKV GEMM(+bias) -> masked attention -> out GEMM(+bias +residual) -> LN ->
-               FFN1 GEMM(+bias, GELU) -> FFN2 GEMM(+bias +residual) -> LN
+  BERT layer   QKV GEMM(+bias) -> masked attention -> out GEMM(+bias) -> LN(+residual) ->
+               FFN1 GEMM(+bias, GELU) -> FFN2 GEMM(+bias) -> LN(+residual)   (post-LN residual
+               adds ride in the LayerNorm kernel, so the GEMMs run the residual-free epilogue)
 """
 import torch
 
@@ -164,8 +165,8 @@ class BertTower:
         for ly in self.layers:
             qkv = ops.linear(h, ly["qkv_w"], ly["qkv_b"])
             ctx = ops.bert_attention(qkv, mask, heads, self.hidden // heads)
-            a = ops.linear(ctx, ly["o_w"], ly["o_b"], residual=h)
-            h = ops.layernorm(a, ly["ln1_g"], ly["ln1_b"], 1e-12)
+            a = ops.linear(ctx, ly["o_w"], ly["o_b"])
+            h = ops.add_layernorm(a, h, ly["ln1_g"], ly["ln1_b"], 1e-12)
             if self.ffn1_events is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -174,8 +175,8 @@ class BertTower:
                 self.ffn1_events.append((e0, e1))
             else:
                 f = ops.linear(h, ly["i_w"], ly["i_b"], act=1)
-            f = ops.linear(f, ly["f_w"], ly["f_b"], residual=h)
-            h = ops.layernorm(f, ly["ln2_g"], ly["ln2_b"], 1e-12)
+            f = ops.linear(f, ly["f_w"], ly["f_b"])
+            h = ops.add_layernorm(f, h, ly["ln2_g"], ly["ln2_b"], 1e-12)
         return h
 
 

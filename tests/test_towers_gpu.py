@@ -86,6 +86,17 @@ def test_layernorm_bf16():
     assert rel_err(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize("rows,c", [(1000, 768), (77, 384), (4096, 96)])
+def test_add_layernorm_bf16(rows, c):
+    """LN(x + r) as HF BertSelfOutput/BertOutput compute it (sum then LayerNorm), tolerance 1e-2."""
+    g = torch.Generator().manual_seed(rows + c)
+    x, r = bf(torch.randn(rows, c, generator=g)), bf(torch.randn(rows, c, generator=g) * 2)
+    ga, be = 1 + 0.1 * torch.randn(c, generator=g), 0.1 * torch.randn(c, generator=g)
+    ref = F.layer_norm(x.float() + r.float(), (c,), ga, be, 1e-12)
+    y = ops.add_layernorm(x.to(DEV), r.to(DEV), ga.to(DEV), be.to(DEV), 1e-12)
+    assert rel_err(y, ref) < 1e-2
+
+
 def test_bert_attention_masked():
     B, L, H, dh = 3, 128, 12, 64
     g = torch.Generator().manual_seed(1)
