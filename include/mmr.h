@@ -135,6 +135,20 @@ mmr_status mmr_swin_mlp(const uint16_t* x, const float* ln_g, const float* ln_b,
                         const uint16_t* pack, const float* b1, const float* b2, uint16_t* y,
                         int64_t tokens, int32_t c, float eps, void* stream);
 
+/* Fused Swin attention sub-block for C = 96 (3 heads of 32, window 7; Swin-T stage 1):
+ * y = x + proj(W-MSA(LayerNorm1(x))) with torch.roll shift, window partition / reverse,
+ * relative-position bias and shift mask (timm SwinTransformerBlock, fusion.py:198-199).
+ * x, y bf16 (b, hw, hw, 96) (x != y); `bias` = the block's dense table from mmr_swin_attn_bias;
+ * `pack` = mmr_swin_attn_block_pack_bytes(96) bytes built once from attn.qkv.weight [288][96] /
+ * .bias, attn.proj.weight [96][96] / .bias (bf16 weights, f32 vectors) and norm1.weight / .bias. */
+int64_t mmr_swin_attn_block_pack_bytes(int32_t c);
+mmr_status mmr_swin_attn_block_pack(const uint16_t* qkv_w, const float* qkv_b, const uint16_t* proj_w,
+                                    const float* proj_b, const float* ln_g, const float* ln_b,
+                                    void* pack, int32_t c, void* stream);
+mmr_status mmr_swin_attn_block(const uint16_t* x, const void* pack, const float* bias, uint16_t* y,
+                               int32_t b, int32_t hw, int32_t c, int32_t ws, int32_t shift, float eps,
+                               void* stream);
+
 /* Swin patch embedding im2col: image f32 NCHW (b,3,224,224) -> bf16 (b*56*56, 48) columns in
  * conv-weight order (cin, kh, kw) for a 4x4/s4 conv as a GEMM. */
 mmr_status mmr_patch_im2col(const float* image, uint16_t* cols, int32_t b, int32_t cin,

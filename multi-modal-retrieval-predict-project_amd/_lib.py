@@ -34,6 +34,9 @@ SIGNATURES = {
     "mmr_bert_attention": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_swin_window_attention": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_swin_attn_bias": [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp],
+    "mmr_swin_attn_block_pack_bytes": [c_i32],
+    "mmr_swin_attn_block_pack": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp],
+    "mmr_swin_attn_block": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_f32, c_vp],
     "mmr_swin_mlp_pack_elems": [c_i32],
     "mmr_swin_mlp_pack": [c_vp, c_vp, c_vp, c_i32, c_vp],
     "mmr_swin_mlp": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp],
@@ -44,7 +47,7 @@ SIGNATURES = {
     "mmr_proj_head": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp],
 }
 _RESTYPES = {"mmr_last_error": ctypes.c_char_p, "mmr_version": ctypes.c_int, "mmr_max_k": ctypes.c_int,
-             "mmr_swin_mlp_pack_elems": ctypes.c_int64}
+             "mmr_swin_mlp_pack_elems": ctypes.c_int64, "mmr_swin_attn_block_pack_bytes": ctypes.c_int64}
 
 _lib = None
 

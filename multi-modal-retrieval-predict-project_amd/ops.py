@@ -151,3 +151,26 @@ def swin_mlp(x, g, b, pack, b1, b2, eps):
     _chk(_L().mmr_swin_mlp(_lib.ptr(x), _lib.ptr(g), _lib.ptr(b), _lib.ptr(pack), _lib.ptr(b1), _lib.ptr(b2),
                            _lib.ptr(y), x.numel() // C, C, float(eps), _s(x)), "mmr_swin_mlp")
     return y
+
+
+def swin_attn_block_pack(qkv_w, qkv_b, proj_w, proj_b, ln_g, ln_b):
+    """Weights of one Swin block's attention half -> packed LDS image for swin_attn_block, or None
+    if C is not a fused width."""
+    C = qkv_w.shape[1]
+    n = _L().mmr_swin_attn_block_pack_bytes(C)
+    if n <= 0:
+        return None
+    pack = torch.empty((n,), dtype=torch.uint8, device=qkv_w.device)
+    _chk(_L().mmr_swin_attn_block_pack(_lib.ptr(qkv_w), _lib.ptr(qkv_b), _lib.ptr(proj_w), _lib.ptr(proj_b),
+                                       _lib.ptr(ln_g), _lib.ptr(ln_b), _lib.ptr(pack), C, _s(qkv_w)),
+         "mmr_swin_attn_block_pack")
+    return pack
+
+
+def swin_attn_block(x, pack, bias, ws, shift, eps):
+    """x + proj(W-MSA(LN1(x))) for x (B, H, H, C), fused (C = 96)."""
+    B, H, _, C = x.shape
+    y = torch.empty_like(x)
+    _chk(_L().mmr_swin_attn_block(_lib.ptr(x), _lib.ptr(pack), _lib.ptr(bias), _lib.ptr(y), B, H, C, ws, shift,
+                                  float(eps), _s(x)), "mmr_swin_attn_block")
+    return y

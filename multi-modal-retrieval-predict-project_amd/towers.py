@@ -8,7 +8,8 @@ the 4x4/s4 patch-embed conv as a [96][64] bf16 GEMM weight (K = 3*16 zero-padded
 
 Per-block dataflow (all hand-written kernels, bf16 activations, f32 accumulation):
   Swin block   LN1 -> QKV GEMM(+bias) -> window attention (roll/partition/bias/mask/softmax/PV/
-               reverse/roll fused) -> proj GEMM(+bias +residual) -> LN2 -> fc1 GEMM(+bias, GELU)
+               reverse/roll fused) -> proj GEMM(+bias +residual) [for C = 96 the whole attention
+               half is ONE kernel, mmr_swin_attn_block] -> LN2 -> fc1 GEMM(+bias, GELU)
                -> fc2 GEMM(+bias +residual); for C = 96 / 192 the MLP half is ONE fused kernel
                (mmr_swin_mlp: LN2 + fc1 + GELU + fc2 + residual, hidden kept on chip)
   PatchMerge   gather 2x2 + LN(4C) fused -> reduction GEMM (no bias)
@@ -37,9 +38,10 @@ def _f(t, dev):
 class SwinTower:
     """timm SwinTransformer.forward_features semantics (see oracle/towers.py for the restatement)."""
 
-    def __init__(self, sd, cfg=SWIN_T, device="cuda", fused_mlp=True):
+    def __init__(self, sd, cfg=SWIN_T, device="cuda", fused_mlp=True, fused_attn=True):
         self.cfg = dict(SWIN_T, **cfg)
         self.fused_mlp = fused_mlp
+        self.fused_attn = fused_attn
         dev = torch.device(device)
         self.device = dev
         E = self.cfg["embed_dim"]
@@ -76,6 +78,10 @@ class SwinTower:
                 })
                 bk = st["blocks"][-1]
                 bk["mlp_pack"] = ops.swin_mlp_pack(bk["fc1_w"], bk["fc2_w"]) if self.fused_mlp else None
+                bk["attn_pack"] = None
+                if self.fused_attn and E * 2 ** i == 96 and self.cfg["num_heads"][i] == 3 and ws == 7:
+                    bk["attn_pack"] = ops.swin_attn_block_pack(bk["qkv_w"], bk["qkv_b"], bk["proj_w"], bk["proj_b"],
+                                                               bk["n1g"], bk["n1b"])
             self.stages.append(st)
         self.norm_g, self.norm_b = _f(sd["norm.weight"], dev), _f(sd["norm.bias"], dev)
         self.num_features = E * 2 ** (len(self.cfg["depths"]) - 1)
@@ -98,10 +104,13 @@ class SwinTower:
             heads = cfg["num_heads"][i]
             ws = min(ws0, H)
             for j, bk in enumerate(st["blocks"]):
-                h = ops.layernorm(x, bk["n1g"], bk["n1b"], 1e-5)
-                qkv = ops.linear(h, bk["qkv_w"], bk["qkv_b"])
-                a = ops.swin_window_attention(qkv, bk["bias"], H, heads, ws, bk["shift"])
-                x = ops.linear(a, bk["proj_w"], bk["proj_b"], residual=x)
+                if bk["attn_pack"] is not None:
+                    x = ops.swin_attn_block(x, bk["attn_pack"], bk["bias"], ws, bk["shift"], 1e-5)
+                else:
+                    h = ops.layernorm(x, bk["n1g"], bk["n1b"], 1e-5)
+                    qkv = ops.linear(h, bk["qkv_w"], bk["qkv_b"])
+                    a = ops.swin_window_attention(qkv, bk["bias"], H, heads, ws, bk["shift"])
+                    x = ops.linear(a, bk["proj_w"], bk["proj_b"], residual=x)
                 if bk["mlp_pack"] is not None:
                     x = ops.swin_mlp(x, bk["n2g"], bk["n2b"], bk["mlp_pack"], bk["fc1_b"], bk["fc2_b"], 1e-5)
                 else:

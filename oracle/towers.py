@@ -64,7 +64,8 @@ def window_reverse(w, ws, H, W):
     return w.view(B, H // ws, W // ws, ws, ws, C).permute(0, 1, 3, 2, 4, 5).reshape(B, H, W, C)
 
 
-def swin_block(x, sd, p, heads, ws, shift, eps=1e-5):
+def swin_attn_half(x, sd, p, heads, ws, shift, eps=1e-5):
+    """x + proj(W-MSA(norm1(x))): the attention half of timm SwinTransformerBlock.forward."""
     B, H, W, C = x.shape
     hd = C // heads
     N = ws * ws
@@ -88,7 +89,11 @@ def swin_block(x, sd, p, heads, ws, shift, eps=1e-5):
     o = window_reverse(o.view(-1, ws, ws, C), ws, H, W)
     if shift:
         o = torch.roll(o, shifts=(shift, shift), dims=(1, 2))
-    x = x + o
+    return x + o
+
+
+def swin_block(x, sd, p, heads, ws, shift, eps=1e-5):
+    x = swin_attn_half(x, sd, p, heads, ws, shift, eps)
     y = _ln(x, sd[p + "norm2.weight"], sd[p + "norm2.bias"], eps)
     y = _lin(F.gelu(_lin(y, sd, p + "mlp.fc1")), sd, p + "mlp.fc2")
     return x + y

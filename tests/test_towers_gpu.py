@@ -162,6 +162,34 @@ def test_swin_window_attention(H, heads, shift):
     assert rel_err(y, ref) < 2e-2
 
 
+@pytest.mark.parametrize("B,shift", [(2, 0), (2, 3), (5, 3)])
+def test_swin_attn_block_fused(B, shift):
+    """mmr_swin_attn_block == oracle swin_attn_half (timm: x + proj(W-MSA(norm1(x))) with roll,
+    rel-pos bias and shift mask) at stage-1 geometry; tolerance 3e-2 * max|ref| (bf16 Q/K/V/P)."""
+    g = torch.Generator().manual_seed(B * 10 + shift)
+    C, H, heads, ws = 96, 56, 3, 7
+    sd = {"b.norm1.weight": 1 + 0.1 * torch.randn(C, generator=g), "b.norm1.bias": 0.1 * torch.randn(C, generator=g),
+          "b.attn.qkv.weight": bf(torch.randn(3 * C, C, generator=g) * C ** -0.5).float(),
+          "b.attn.qkv.bias": 0.1 * torch.randn(3 * C, generator=g),
+          "b.attn.proj.weight": bf(torch.randn(C, C, generator=g) * C ** -0.5).float(),
+          "b.attn.proj.bias": 0.1 * torch.randn(C, generator=g),
+          "b.attn.relative_position_bias_table": torch.randn(169, heads, generator=g)}
+    x = bf(torch.randn(B, H, H, C, generator=g))
+    ref = otw.swin_attn_half(x.float(), sd, "b.", heads, ws, shift)
+    d = lambda k: sd["b." + k].to(DEV)
+    pack = ops.swin_attn_block_pack(bf(d("attn.qkv.weight")), d("attn.qkv.bias"), bf(d("attn.proj.weight")),
+                                    d("attn.proj.bias"), d("norm1.weight"), d("norm1.bias"))
+    bias = ops.swin_attn_bias(d("attn.relative_position_bias_table"), heads, ws, H, shift)
+    y = ops.swin_attn_block(x.to(DEV), pack, bias, ws, shift, 1e-5)
+    assert rel_err(y, ref) < 3e-2
+    # and the unfused kernel chain agrees
+    h = ops.layernorm(x.to(DEV), d("norm1.weight"), d("norm1.bias"), 1e-5)
+    qkv = ops.linear(h, bf(d("attn.qkv.weight")), d("attn.qkv.bias"))
+    a = ops.swin_window_attention(qkv, bias, H, heads, ws, shift)
+    y2 = ops.linear(a, bf(d("attn.proj.weight")), d("attn.proj.bias"), residual=x.to(DEV))
+    assert rel_err(y, y2.float().cpu()) < 3e-2
+
+
 def test_patch_im2col_and_merge():
     img = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(2, 3)))
     cols = ops.patch_im2col(img.to(DEV)).float().cpu()
