@@ -180,6 +180,47 @@ mmr_status mmr_proj_head(const float* x, const float* wp, const float* bp, const
                          const float* b1, const float* w2, const float* b2, float* y, int32_t b,
                          int32_t cin, int32_t d, int32_t l2norm, void* stream);
 
+/* Small exact-f32 linear on strided rows: y[i*ldy + o] = act(x[i*ldx + :] . w[o][:] + bias[o])
+ * (+ residual[i*ldr + o]); residual may alias y (in-place x += f(x)).  cin % 16 == 0,
+ * cout % 32 == 0, ldx % 4 == 0.  The per-query vectors of the fusion stack (model.py:431-449). */
+mmr_status mmr_linear_f32(const float* x, int64_t ldx, const float* w, const float* bias,
+                          const float* residual, int64_t ldr, float* y, int64_t ldy, int32_t b,
+                          int32_t cin, int32_t cout, int32_t act, void* stream);
+
+/* ---------------------------------------------------------------- multimodal fusion stack */
+/* model_type="multimodal": CrossModalFusion (src/Model/fusion.py:334-471) x num_fusion_layers +
+ * the combiner (src/Model/model.py:375-459), eval.  Orchestrated host-side over these ops and
+ * mmr_linear_bf16 / mmr_linear_f32. */
+
+/* nn.MultiheadAttention core (no masks): per (batch, head) softmax(q k^T * scale) v.
+ * q row (bi*lq + i) at q + row*ldq + head*dh (k, v likewise with lk); out (b*lq, ldo) bf16 and/or
+ * mean_out (b, heads*dh) f32 = the mean over the lq query rows (either may be NULL, not both).
+ * dh % 8 == 0, dh <= 192; strides multiples of 8 elements; K/V tile must fit the 160 KB LDS. */
+mmr_status mmr_mha(const uint16_t* q, int64_t ldq, const uint16_t* k, int64_t ldk, const uint16_t* v,
+                   int64_t ldv, uint16_t* out, int64_t ldo, float* mean_out, int32_t b, int32_t lq,
+                   int32_t lk, int32_t heads, int32_t dh, float scale, void* stream);
+
+/* y = x + pos[row % l] -> bf16 (rows, c); x f32 (x_is_f32) or bf16; pos f32 [>= l][c]
+ * (PreFusionEnhancer.pos_embed fusion.py:32). c % 8 == 0. */
+mmr_status mmr_add_pos_bf16(const void* x, int32_t x_is_f32, const float* pos, uint16_t* y, int64_t rows,
+                            int32_t l, int32_t c, void* stream);
+
+/* y = LayerNorm(alpha*x + residual) (+ post_scale*post), per row of c <= 1024 channels.
+ * alpha / post_scale are DEVICE f32 scalars (learned parameters) or NULL (= 1); residual / post
+ * may be NULL.  io_bf16: x, residual, y bf16 (else f32); post is always f32. */
+mmr_status mmr_ln_rows(const void* x, int64_t ldx, const float* alpha, const void* residual, int64_t ldr,
+                       const float* gamma, const float* beta, const float* post, int64_t ldp,
+                       const float* post_scale, void* y, int64_t ldy, int64_t rows, int32_t c, float eps,
+                       int32_t io_bf16, void* stream);
+
+/* seq (b, np+2, c) bf16 = [x1; patches_fused; x2] + pe[0..np+2) (fusion.py:468 + model.py:397);
+ * x1, x2 f32 (b, c), patches_fused bf16 (b*np, c), pe f32 [>= np+2][c]. */
+mmr_status mmr_assemble_seq(const float* x1, const uint16_t* patches_fused, const float* x2, const float* pe,
+                            uint16_t* seq, int32_t b, int32_t np, int32_t c, void* stream);
+
+/* y (b, c) f32 = x[i*ldx + 0..c) (bf16 rows, e.g. the CLS token of each sequence). */
+mmr_status mmr_rows_to_f32(const uint16_t* x, int64_t ldx, float* y, int32_t b, int32_t c, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -45,6 +45,14 @@ SIGNATURES = {
     "mmr_swin_head": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp],
     "mmr_mean_tokens": [c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
     "mmr_proj_head": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp],
+    "mmr_linear_f32": [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp],
+    "mmr_mha": [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_f32,
+                c_vp],
+    "mmr_add_pos_bf16": [c_vp, c_i32, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp],
+    "mmr_ln_rows": [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_i32, c_f32,
+                    c_i32, c_vp],
+    "mmr_assemble_seq": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
+    "mmr_rows_to_f32": [c_vp, c_i64, c_vp, c_i32, c_i32, c_vp],
 }
 _RESTYPES = {"mmr_last_error": ctypes.c_char_p, "mmr_version": ctypes.c_int, "mmr_max_k": ctypes.c_int,
              "mmr_swin_mlp_pack_elems": ctypes.c_int64, "mmr_swin_attn_block_pack_bytes": ctypes.c_int64}

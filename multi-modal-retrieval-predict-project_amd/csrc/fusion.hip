@@ -1,0 +1,401 @@
+// Multimodal fusion stack (model_type="multimodal"): the small-sequence attention core and the
+// elementwise / row kernels around the GEMMs (gemm.hip) and f32 linears (tower.hip).
+//
+// Reference (semantics): CrossModalFusion.forward src/Model/fusion.py:390-471, PreFusionEnhancer
+// fusion.py:20-35, MultiModalRetrievalModel.forward model.py:375-459, torch.nn.MultiheadAttention
+// (batch_first, eval, no masks).  Host-side orchestration + weight folding: fusion.py in the package.
+#include <float.h>
+#include <math.h>
+
+#include <algorithm>
+
+#include "common.h"
+
+namespace {
+
+using mmr::bf2f;
+using mmr::f2bf;
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ------------------------------------------------------------------ small-sequence MHA core
+// softmax(q k^T * scale) v per (batch, head) for the fusion's short sequences (text L <= 512,
+// 49 patches, 51-token fused sequence), no masks.  Block = (batch, head); each wave owns 32-query
+// tiles.  As in bert_attention (tower.hip): the swapped product S^T = K . Q^T on
+// v_mfma_f32_32x32x16_bf16 puts the query on the lane, the softmax reductions stay in registers,
+// and P^T feeds the P.V MFMA as its B operand with no data movement (V^T read in the matching key
+// permutation).  head_dim is padded to DT*32 with zeros (dh % 8 == 0); ragged query/key counts
+// are padded to 32 (padded keys -> -inf, padded queries never stored).  Operands are strided rows
+// (q row (b*lq + i) at q + row*ldq + head*dh), so Q/K/V are read in place from packed projection
+// outputs.  Optional f32 mean over the lq query rows (mean_out (b, heads*dh)): the fusion only
+// needs mean_L of several attention outputs (fusion.py:441,448, model.py:431), and
+// mean_L(A) W^T + b == mean_L(A W^T + b), so those out-projections shrink to one row per batch.
+template <int DT>
+__global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q, int64_t ldq,
+                                                 const uint16_t* __restrict__ k, int64_t ldk,
+                                                 const uint16_t* __restrict__ v, int64_t ldv,
+                                                 uint16_t* __restrict__ out, int64_t ldo,
+                                                 float* __restrict__ mean_out, int lq, int lk,
+                                                 int heads, int dh, float scale) {
+  constexpr int DHP = DT * 32;
+  constexpr int KS = DHP / 16;
+  constexpr int KROW = DHP + 8;  // padded K row (elements): 16-B skew between consecutive keys
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int bi = blockIdx.x / heads, hh = blockIdx.x % heads;
+  const int lkp = (lk + 31) & ~31;
+  const int vts = lkp + 4;                   // V^T row stride (elements)
+  uint16_t* Ks = (uint16_t*)smem;            // [lkp][KROW]
+  uint16_t* Vt = Ks + lkp * KROW;            // [DHP][vts]
+  float* msum = (float*)(Vt + DHP * vts);    // [DHP]
+  const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6, nwave = nthr >> 6;
+  constexpr int NCH = DHP / 8;
+  const uint16_t* kbase = k + (int64_t)bi * lk * ldk + hh * dh;
+  const uint16_t* vbase = v + (int64_t)bi * lk * ldv + hh * dh;
+  for (int c = tid; c < lkp * NCH; c += nthr) {
+    const int key = c / NCH, ch = c % NCH;
+    bf16x8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (key < lk && ch * 8 < dh) {
+      kv = *(const bf16x8*)(kbase + key * ldk + ch * 8);
+      vv = *(const bf16x8*)(vbase + key * ldv + ch * 8);
+    }
+    *(bf16x8*)(Ks + key * KROW + ch * 8) = kv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Vt[(ch * 8 + j) * vts + key] = (uint16_t)vv[j];
+  }
+  for (int d = tid; d < DHP; d += nthr) msum[d] = 0.f;
+  __syncthreads();
+
+  const int r = lane & 31, hf = lane >> 5;
+  const int nqt = (lq + 31) / 32;
+  for (int qt = wave; qt < nqt; qt += nwave) {
+    const int qi = qt * 32 + r;
+    const bool qok = qi < lq;
+    const uint16_t* qrow = q + ((int64_t)bi * lq + (qok ? qi : 0)) * ldq + hh * dh;
+    bf16x8 qf[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int c8 = ks * 2 + hf;
+      qf[ks] = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+      if (qok && c8 * 8 < dh) qf[ks] = *(const bf16x8*)(qrow + c8 * 8);
+    }
+    f32x16 o[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[dt] = (f32x16){0};
+    float m_run = -FLT_MAX, l_run = 0.f;
+    for (int kb = 0; kb < lkp; kb += 64) {
+      const int nt = min(64, lkp - kb) / 32;
+      f32x16 s[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        s[t] = (f32x16){0};
+        if (t < nt) {
+          const int key = kb + t * 32 + r;
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            const bf16x8 kf = *(const bf16x8*)(Ks + key * KROW + (ks * 2 + hf) * 8);
+            s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[t], 0, 0, 0);
+          }
+        }
+      }
+      float mloc = -FLT_MAX;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        if (t < nt) {
+#pragma unroll
+          for (int rg = 0; rg < 16; ++rg) {
+            const int key = kb + t * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * hf;
+            const float x = key < lk ? s[t][rg] * scale : -FLT_MAX;
+            s[t][rg] = x;
+            mloc = fmaxf(mloc, x);
+          }
+        }
+      }
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      const float m_new = fmaxf(m_run, mloc);
+      const float alpha = __expf(m_run - m_new);
+      m_run = m_new;
+      float psum = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        if (t < nt) {
+#pragma unroll
+          for (int rg = 0; rg < 16; ++rg) {
+            const float p = __expf(s[t][rg] - m_new);
+            s[t][rg] = p;
+            psum += p;
+          }
+        }
+      }
+      l_run = l_run * alpha + psum;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int rg = 0; rg < 16; ++rg) o[dt][rg] *= alpha;
+      // O^T[d][q] += V^T[d][key] . P^T[key][q]
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        if (t < nt) {
+#pragma unroll
+          for (int sidx = 0; sidx < 2; ++sidx) {
+            bf16x8 pf;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pf[j] = (short)f2bf(s[t][8 * sidx + j]);
+            const int kk = kb + t * 32 + 16 * sidx + 4 * hf;
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+              const uint16_t* vrow = Vt + (dt * 32 + r) * vts;
+              const bf16x4 lo = *(const bf16x4*)(vrow + kk);
+              const bf16x4 hi = *(const bf16x4*)(vrow + kk + 8);
+              const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+              o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[dt], 0, 0, 0);
+            }
+          }
+        }
+      }
+    }
+    const float inv = 1.0f / (l_run + __shfl_xor(l_run, 32, 64));
+    if (out != nullptr && qok) {
+      uint16_t* orow = out + ((int64_t)bi * lq + qi) * ldo + hh * dh;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d = dt * 32 + 8 * g4 + 4 * hf;
+          if (d < dh) {
+            bf16x4 w;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w[j] = (short)f2bf(o[dt][4 * g4 + j] * inv);
+            *(bf16x4*)(orow + d) = w;
+          }
+        }
+    }
+    if (mean_out != nullptr) {
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int rg = 0; rg < 16; ++rg) {
+          float x = qok ? o[dt][rg] * inv : 0.f;
+#pragma unroll
+          for (int off = 1; off < 32; off <<= 1) x += __shfl_xor(x, off, 64);
+          const int d = dt * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * hf;
+          if (r == 0 && d < dh) atomicAdd(&msum[d], x);
+        }
+    }
+  }
+  if (mean_out != nullptr) {
+    __syncthreads();
+    for (int d = tid; d < dh; d += nthr)
+      mean_out[(int64_t)bi * heads * dh + hh * dh + d] = msum[d] / (float)lq;
+  }
+}
+
+// ------------------------------------------------------------------ x + positional table -> bf16
+// y[b][t][c] = x[b][t][c] + pos[t][c] (PreFusionEnhancer.pos_embed fusion.py:32, PositionalEncoding
+// model.py:99-107); x f32 or bf16, pos f32 [>= l][c], 8 channels per thread.
+template <typename TX>
+__global__ __launch_bounds__(256) void add_pos_bf16(const TX* __restrict__ x, const float* __restrict__ pos,
+                                                    uint16_t* __restrict__ y, int64_t rows, int l, int c) {
+  const int nch = c / 8;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * nch) return;
+  const int64_t row = i / nch;
+  const int ch = (int)(i % nch);
+  const int t = (int)(row % l);
+  float v[8];
+  if constexpr (sizeof(TX) == 4) {
+    const float4 a = *(const float4*)((const float*)x + row * c + ch * 8);
+    const float4 b = *(const float4*)((const float*)x + row * c + ch * 8 + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+    const bf16x8 a = *(const bf16x8*)((const uint16_t*)x + row * c + ch * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = bf2f((uint16_t)a[j]);
+  }
+  const float4 p0 = *(const float4*)(pos + (int64_t)t * c + ch * 8);
+  const float4 p1 = *(const float4*)(pos + (int64_t)t * c + ch * 8 + 4);
+  v[0] += p0.x; v[1] += p0.y; v[2] += p0.z; v[3] += p0.w;
+  v[4] += p1.x; v[5] += p1.y; v[6] += p1.z; v[7] += p1.w;
+  *(uint4*)(y + row * c + ch * 8) = make_uint4(mmr::pack2bf(v[0], v[1]), mmr::pack2bf(v[2], v[3]),
+                                               mmr::pack2bf(v[4], v[5]), mmr::pack2bf(v[6], v[7]));
+}
+
+// ------------------------------------------------------------------ scaled-residual LayerNorm
+// y = LN(a*x + r) * g + b  (+ ps*post), one row per wave.  x/r/y bf16 or f32 (template), a and ps
+// read from device scalars (learned nn.Parameter(1), no host sync) or 1 when NULL, r/post optional.
+// Covers PreFusionEnhancer norm1(alpha*x + x2) (fusion.py:34), ln_img / ln_txt (fusion.py:443,449),
+// norm1_i(joint) + alpha*fused and norm2_i (model.py:437-441).  Row kept in registers
+// (c <= 1024), centred two-pass variance like torch.
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void ln_rows(const TI* __restrict__ x, int64_t ldx, const float* __restrict__ a,
+                                               const TI* __restrict__ r, int64_t ldr,
+                                               const float* __restrict__ g, const float* __restrict__ b,
+                                               const float* __restrict__ post, int64_t ldp,
+                                               const float* __restrict__ ps, TO* __restrict__ y, int64_t ldy,
+                                               int64_t rows, int c, float eps) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  auto ld = [](const TI* p, int64_t i) -> float {
+    if constexpr (sizeof(TI) == 4) return ((const float*)p)[i];
+    else return bf2f(((const uint16_t*)p)[i]);
+  };
+  const float av = a ? *a : 1.f;
+  float v[16];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int ch = lane + 64 * i;
+    v[i] = 0.f;
+    if (ch < c) {
+      float t = av * ld(x, row * ldx + ch);
+      if (r) t += ld(r, row * ldr + ch);
+      v[i] = t;
+      s += t;
+    }
+  }
+  const float mean = mmr::wave_sum(s) / c;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (lane + 64 * i < c) ss += (v[i] - mean) * (v[i] - mean);
+  const float rstd = rsqrtf(mmr::wave_sum(ss) / c + eps);
+  const float pv = ps ? *ps : 1.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int ch = lane + 64 * i;
+    if (ch < c) {
+      float t = (v[i] - mean) * rstd * g[ch] + b[ch];
+      if (post) t += pv * post[row * ldp + ch];
+      if constexpr (sizeof(TO) == 4) ((float*)y)[row * ldy + ch] = t;
+      else ((uint16_t*)y)[row * ldy + ch] = f2bf(t);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ fused-sequence assembly
+// seq[b] = [x1[b]; patches_fused[b][0..np); x2[b]] + pe[0..np+2)  -> bf16 (b, np+2, c)
+// (fusion.py:451-468 cat, model.py:396-397 dropout(eval) + pos_encoder).
+__global__ __launch_bounds__(256) void assemble_seq(const float* __restrict__ x1, const uint16_t* __restrict__ pf,
+                                                    const float* __restrict__ x2, const float* __restrict__ pe,
+                                                    uint16_t* __restrict__ seq, int nb, int np, int c) {
+  const int ls = np + 2;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)nb * ls * c) return;
+  const int ch = (int)(i % c);
+  const int64_t row = i / c;
+  const int t = (int)(row % ls);
+  const int64_t bi = row / ls;
+  float v;
+  if (t == 0) v = x1[bi * c + ch];
+  else if (t == ls - 1) v = x2[bi * c + ch];
+  else v = bf2f(pf[(bi * np + t - 1) * c + ch]);
+  seq[i] = f2bf(v + pe[(int64_t)t * c + ch]);
+}
+
+// ------------------------------------------------------------------ strided bf16 -> f32 row gather
+// y[b][:] = f32(x[b*ldx + :]) — e.g. the CLS row of each text sequence (fusion.py:447 txt_p[:, 0]).
+__global__ __launch_bounds__(256) void rows_to_f32(const uint16_t* __restrict__ x, int64_t ldx,
+                                                   float* __restrict__ y, int nb, int c) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)nb * c) return;
+  y[i] = bf2f(x[(i / c) * ldx + (i % c)]);
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+}  // namespace
+
+// ================================================================== C ABI
+extern "C" {
+
+mmr_status mmr_mha(const uint16_t* q, int64_t ldq, const uint16_t* k, int64_t ldk, const uint16_t* v,
+                   int64_t ldv, uint16_t* out, int64_t ldo, float* mean_out, int32_t b, int32_t lq,
+                   int32_t lk, int32_t heads, int32_t dh, float scale, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(q && k && v && (out || mean_out), "mmr_mha: NULL pointer");
+  MMR_REQUIRE(b >= 0 && lq > 0 && lk > 0 && heads > 0, "mmr_mha: bad shape b=%d lq=%d lk=%d heads=%d", b, lq, lk, heads);
+  MMR_REQUIRE(dh > 0 && dh % 8 == 0 && dh <= 192, "mmr_mha: head_dim %d must be a multiple of 8 <= 192", dh);
+  MMR_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && (!out || ldo % 4 == 0),
+              "mmr_mha: row strides must be multiples of 8 elements (16 B)");
+  MMR_REQUIRE(ldq >= (int64_t)heads * dh && ldk >= (int64_t)heads * dh && ldv >= (int64_t)heads * dh &&
+              (!out || ldo >= (int64_t)heads * dh), "mmr_mha: row stride below heads*dh");
+  MMR_REQUIRE(aligned16(q) && aligned16(k) && aligned16(v) && (!out || ((uintptr_t)out & 7u) == 0),
+              "mmr_mha: operands must be 16-B aligned");
+  if (b == 0) return MMR_OK;
+  const int dt = (dh + 31) / 32;
+  const int lkp = (lk + 31) & ~31;
+  const size_t lds = (size_t)lkp * (dt * 32 + 8) * 2 + (size_t)dt * 32 * (lkp + 4) * 2 + (size_t)dt * 32 * 4;
+  MMR_REQUIRE(lds <= 160 * 1024, "mmr_mha: lk=%d x head_dim=%d exceeds the 160 KB LDS", lk, dh);
+  const int nqt = (lq + 31) / 32;
+  const dim3 grid((unsigned)((int64_t)b * heads)), blk(64 * std::min(4, nqt));
+  hipStream_t st = mmr::as_stream(stream);
+#define MMR_MHA(D) mha_small<D><<<grid, blk, lds, st>>>(q, ldq, k, ldk, v, ldv, out, ldo, mean_out, lq, lk, heads, dh, scale)
+  switch (dt) {
+    case 1: MMR_MHA(1); break;
+    case 2: MMR_MHA(2); break;
+    case 3: MMR_MHA(3); break;
+    case 4: MMR_MHA(4); break;
+    case 5: MMR_MHA(5); break;
+    default: MMR_MHA(6); break;
+  }
+#undef MMR_MHA
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_add_pos_bf16(const void* x, int32_t x_is_f32, const float* pos, uint16_t* y, int64_t rows,
+                            int32_t l, int32_t c, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && pos && y && l > 0 && c > 0 && c % 8 == 0 && rows >= 0, "mmr_add_pos_bf16: bad arguments");
+  if (rows == 0) return MMR_OK;
+  const dim3 grid((unsigned)mmr::ceil_div(rows * (c / 8), 256));
+  hipStream_t st = mmr::as_stream(stream);
+  if (x_is_f32) add_pos_bf16<float><<<grid, 256, 0, st>>>((const float*)x, pos, y, rows, l, c);
+  else add_pos_bf16<uint16_t><<<grid, 256, 0, st>>>((const uint16_t*)x, pos, y, rows, l, c);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_ln_rows(const void* x, int64_t ldx, const float* alpha, const void* residual, int64_t ldr,
+                       const float* gamma, const float* beta, const float* post, int64_t ldp,
+                       const float* post_scale, void* y, int64_t ldy, int64_t rows, int32_t c, float eps,
+                       int32_t io_bf16, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && gamma && beta && y && rows >= 0 && c > 0 && c <= 1024, "mmr_ln_rows: bad arguments (c <= 1024)");
+  if (rows == 0) return MMR_OK;
+  const dim3 grid((unsigned)mmr::ceil_div(rows, 4));
+  hipStream_t st = mmr::as_stream(stream);
+  if (io_bf16)
+    ln_rows<uint16_t, uint16_t><<<grid, 256, 0, st>>>((const uint16_t*)x, ldx, alpha, (const uint16_t*)residual, ldr,
+                                                      gamma, beta, post, ldp, post_scale, (uint16_t*)y, ldy, rows, c, eps);
+  else
+    ln_rows<float, float><<<grid, 256, 0, st>>>((const float*)x, ldx, alpha, (const float*)residual, ldr, gamma, beta,
+                                                post, ldp, post_scale, (float*)y, ldy, rows, c, eps);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_assemble_seq(const float* x1, const uint16_t* patches_fused, const float* x2, const float* pe,
+                            uint16_t* seq, int32_t b, int32_t np, int32_t c, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x1 && patches_fused && x2 && pe && seq && b >= 0 && np > 0 && c > 0, "mmr_assemble_seq: bad arguments");
+  if (b == 0) return MMR_OK;
+  const int64_t n = (int64_t)b * (np + 2) * c;
+  assemble_seq<<<dim3((unsigned)mmr::ceil_div(n, 256)), 256, 0, mmr::as_stream(stream)>>>(x1, patches_fused, x2, pe,
+                                                                                          seq, b, np, c);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_rows_to_f32(const uint16_t* x, int64_t ldx, float* y, int32_t b, int32_t c, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && y && b >= 0 && c > 0 && ldx >= c, "mmr_rows_to_f32: bad arguments");
+  if (b == 0) return MMR_OK;
+  rows_to_f32<<<dim3((unsigned)mmr::ceil_div((int64_t)b * c, 256)), 256, 0, mmr::as_stream(stream)>>>(x, ldx, y, b, c);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+}  // extern "C"

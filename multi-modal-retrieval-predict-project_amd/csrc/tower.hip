@@ -584,12 +584,16 @@ __global__ __launch_bounds__(256) void mean_tokens(const uint16_t* __restrict__ 
 // ------------------------------------------------------------------ small f32 linear (heads)
 // Y[b][o] = act(sum_i X[b][i] W[o][i] + bias[o]) in exact f32 (v_mfma_f32_32x32x2_f32); one wave
 // per 32x32 output tile, operands straight to VGPRs as float4 with the k-permutation of
-// knn_scores (lane half h owns k = kb+8h..kb+8h+7).  cin % 16 == 0, cout % 32 == 0.
+// knn_scores (lane half h owns k = kb+8h..kb+8h+7).  cin % 16 == 0, cout % 32 == 0.  Rows are
+// strided (ldx, ldy; ldx % 4 == 0); optional residual R (ldr) added after the activation.
 __global__ __launch_bounds__(256) void linear_f32(const float* __restrict__ X,
                                                   const float* __restrict__ W,
                                                   const float* __restrict__ bias,
-                                                  float* __restrict__ Y, int nb, int cin, int cout,
-                                                  int act) {
+                                                  float* Y, int nb, int cin, int cout,
+                                                  int act, int64_t ldx = -1, int64_t ldy = -1,
+                                                  const float* R = nullptr, int64_t ldr = 0) {
+  if (ldx < 0) ldx = cin;
+  if (ldy < 0) ldy = cout;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int tiles_o = cout / 32;
   const int t = blockIdx.x * 4 + wave;
@@ -598,7 +602,7 @@ __global__ __launch_bounds__(256) void linear_f32(const float* __restrict__ X,
   const int r = lane & 31, h = lane >> 5;
   const int b = tb * 32 + r;
   const bool bok = b < nb;
-  const float* xa = X + (int64_t)(bok ? b : 0) * cin + 8 * h;
+  const float* xa = X + (int64_t)(bok ? b : 0) * ldx + 8 * h;
   const float* wb = W + (int64_t)(to * 32 + r) * cin + 8 * h;
   f32x16 acc = {0};
   for (int kb = 0; kb < cin; kb += 16) {
@@ -618,7 +622,8 @@ __global__ __launch_bounds__(256) void linear_f32(const float* __restrict__ X,
     if (bb >= nb) continue;
     float v = acc[rg] + bo;
     if (act == 1) v = mmr::gelu_erf(v);
-    Y[(int64_t)bb * cout + o] = v;
+    if (R) v += R[(int64_t)bb * ldr + o];
+    Y[(int64_t)bb * ldy + o] = v;
   }
 }
 
@@ -818,6 +823,24 @@ mmr_status mmr_proj_head(const float* x, const float* wp, const float* bp, const
     l2_normalize_rows<<<dim3((unsigned)mmr::ceil_div(b, 4)), blk, 0, st>>>(y, b, d);
     MMR_LAUNCH_CHECK();
   }
+  return MMR_OK;
+}
+
+mmr_status mmr_linear_f32(const float* x, int64_t ldx, const float* w, const float* bias,
+                          const float* residual, int64_t ldr, float* y, int64_t ldy, int32_t b,
+                          int32_t cin, int32_t cout, int32_t act, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && w && y && b >= 0 && cin > 0 && cout > 0, "mmr_linear_f32: bad arguments");
+  MMR_REQUIRE(cin % 16 == 0 && cout % 32 == 0, "mmr_linear_f32: cin=%d must be a multiple of 16, cout=%d of 32", cin, cout);
+  MMR_REQUIRE(ldx >= cin && ldx % 4 == 0 && ldy >= cout && (!residual || ldr >= cout),
+              "mmr_linear_f32: bad row strides");
+  MMR_REQUIRE(((uintptr_t)x & 15u) == 0 && ((uintptr_t)w & 15u) == 0, "mmr_linear_f32: x / w must be 16-B aligned");
+  MMR_REQUIRE(act == 0 || act == 1, "mmr_linear_f32: act=%d", act);
+  if (b == 0) return MMR_OK;
+  const int64_t tiles = mmr::ceil_div(b, 32) * (cout / 32);
+  linear_f32<<<dim3((unsigned)mmr::ceil_div(tiles, 4)), 256, 0, mmr::as_stream(stream)>>>(
+      x, w, bias, y, b, cin, cout, act, ldx, ldy, residual, ldr);
+  MMR_LAUNCH_CHECK();
   return MMR_OK;
 }
 

@@ -17,6 +17,10 @@ heads                  MultiModalRetrievalModel.forward (model.py:365-373, 462-4
                        txt_emb (unmasked mean over ALL L positions incl. PAD), text / image heads
                        through MultiHeadMLP (model.py:61-75; ffn[0] since use_shared_ffn=False,
                        configs/config.yaml).
+multimodal             model_type="multimodal" (model.py:375-459): num_fusion_layers x
+                       CrossModalFusion (fusion.py:334-471, PreFusionEnhancer fusion.py:20-35) +
+                       pos_encoder + self_attn (nn.MultiheadAttention restated in `mha`) + residual /
+                       LayerNorm / FFN / adapter chain; eval mode (dropout, stochastic depth off).
 """
 import math
 
@@ -163,7 +167,7 @@ def multi_head_mlp(x, sd, p):
     return _lin(F.gelu(_lin(x, sd, p + "linear1")), sd, p + "linear2")
 
 
-def heads(img_global, img_patches, txt_feats, hsd, model_type, ffn_prefix="ffn.0."):
+def heads(img_global, img_patches, txt_feats, hsd, model_type, ffn_prefix="ffn.0.", mm_cfg=None):
     img_emb = _lin(img_global, hsd, "img_proj") if img_global is not None else None
     txt_emb = _lin(txt_feats.mean(dim=1), hsd, "txt_proj") if txt_feats is not None else None
     if model_type == "text":
@@ -173,5 +177,82 @@ def heads(img_global, img_patches, txt_feats, hsd, model_type, ffn_prefix="ffn.0
         p = _lin(img_patches, hsd, "img_proj")
         joint = multi_head_mlp(torch.cat([g.unsqueeze(1), p], 1).mean(1), hsd, ffn_prefix)
     else:
-        raise NotImplementedError("multimodal fusion stack is a §8f 'next' row")
+        joint = multimodal(img_global, img_patches, txt_feats, hsd, **(mm_cfg or {}))
     return {"joint_emb": joint, "img_emb": img_emb, "txt_emb": txt_emb}
+
+
+def mha(q_in, k_in, v_in, sd, p, heads):
+    """torch.nn.MultiheadAttention(batch_first=True).forward in eval, no masks: packed
+    in_proj_weight [3E][E] (q|k|v), per-head softmax(q k^T / sqrt(dh)) v, out_proj."""
+    E = sd[p + "in_proj_weight"].shape[1]
+    W, b = sd[p + "in_proj_weight"], sd[p + "in_proj_bias"]
+    q = F.linear(q_in, W[:E], b[:E])
+    k = F.linear(k_in, W[E:2 * E], b[E:2 * E])
+    v = F.linear(v_in, W[2 * E:], b[2 * E:])
+    B, Lq, _ = q.shape
+    Lk = k.shape[1]
+    dh = E // heads
+
+    def hd(t, L):
+        return t.view(B, L, heads, dh).transpose(1, 2)
+    a = (hd(q, Lq) @ hd(k, Lk).transpose(-1, -2) / math.sqrt(dh)).softmax(-1) @ hd(v, Lk)
+    return _lin(a.transpose(1, 2).reshape(B, Lq, E), sd, p + "out_proj")
+
+
+def prefusion_enhancer(x, sd, p, heads, eps=1e-5):
+    """PreFusionEnhancer.forward (src/Model/fusion.py:30-35), eval (dropout = identity)."""
+    L = x.shape[1]
+    x = x + sd[p + "pos_embed"][:, :L]
+    x2 = mha(x, x, x, sd, p + "self_attn.", heads)
+    return _ln(sd[p + "alpha"] * x + x2, sd[p + "norm1.weight"], sd[p + "norm1.bias"], eps)
+
+
+def cross_modal_fusion(img_global, img_patch, txt_feats, sd, p, heads, use_cls_only=False, eps=1e-5):
+    """CrossModalFusion.forward (fusion.py:390-471) -> (B, 1+Np+1, D) sequence (use_cls_only:
+    (B, D) comb_mlp vector)."""
+    if txt_feats is None:  # learnable default text token (fusion.py:404-407)
+        txt_feats = sd[p + "default_txt_token"].expand(img_patch.shape[0], -1, -1)
+    txt = prefusion_enhancer(txt_feats, sd, p + "txt_self_attn.", heads, eps)
+    g = prefusion_enhancer(img_global.unsqueeze(1), sd, p + "img_global_self_attn.", heads, eps).squeeze(1)
+    pt = prefusion_enhancer(img_patch, sd, p + "img_patch_self_attn.", heads, eps)
+    tp = txt[:, 0:1] if use_cls_only else txt
+    att_t2i = mha(_lin(tp, sd, p + "query_txt"), _lin(pt, sd, p + "key_img"), _lin(pt, sd, p + "value_img"),
+                  sd, p + "attn_txt2img.", heads)
+    att_i2t = mha(_lin(pt, sd, p + "query_img"), _lin(tp, sd, p + "key_txt"), _lin(tp, sd, p + "value_txt"),
+                  sd, p + "attn_img2txt.", heads)
+    patches_fused = _lin(pt, sd, p + "img_patch_proj") + att_i2t
+    x1 = _ln(_lin(g, sd, p + "img_global_proj") + att_t2i.mean(1), sd[p + "ln_img.weight"], sd[p + "ln_img.bias"], eps)
+    x2 = _ln(_lin(txt, sd, p + "txt_proj")[:, 0] + att_i2t.mean(1), sd[p + "ln_txt.weight"], sd[p + "ln_txt.bias"], eps)
+    if use_cls_only:
+        cat = torch.cat([x1, patches_fused.mean(1), x2], 1)
+        return _lin(F.gelu(_lin(cat, sd, p + "comb_mlp.0")), sd, p + "comb_mlp.3")
+    return torch.cat([x1.unsqueeze(1), patches_fused, x2.unsqueeze(1)], 1)
+
+
+def multimodal(img_global, img_patches, txt_feats, sd, num_heads=4, num_fusion_layers=None,
+               use_shared_ffn=False, use_cls_only=False, eps=1e-5):
+    """MultiModalRetrievalModel.forward, model_type="multimodal" (model.py:375-459), eval:
+    per layer i the fusion of the SAME backbone features, + pos_encoder, self_attn, mean over the
+    sequence; x = fused (i == 0) or norm1_i(joint) + alpha * fused; x += ffn(norm2_i(x));
+    x += adapter_i(x)."""
+    if use_cls_only:
+        # model.py:428-429 indexes fused_out[:, 0, :] on the 2-D comb_mlp output: the reference
+        # raises there, so there is no multimodal use_cls_only result to restate
+        raise ValueError("multimodal with use_cls_only fails in the reference (model.py:428-429)")
+    if num_fusion_layers is None:
+        num_fusion_layers = 1 + max(int(k.split(".")[1]) for k in sd if k.startswith("fusion_layers."))
+    joint = None
+    for i in range(num_fusion_layers):
+        seq = cross_modal_fusion(img_global, img_patches, txt_feats, sd, f"fusion_layers.{i}.", num_heads,
+                                 False, eps)
+        seq = seq + sd["pos_encoder.pe"][:, :seq.shape[1]]
+        fused = mha(seq, seq, seq, sd, "self_attn.", num_heads).mean(1)
+        if i == 0:
+            x = fused
+        else:
+            x = _ln(joint, sd[f"norm1_layers.{i}.weight"], sd[f"norm1_layers.{i}.bias"], eps) + sd["alpha"] * fused
+        xf = _ln(x, sd[f"norm2_layers.{i}.weight"], sd[f"norm2_layers.{i}.bias"], eps)
+        x = x + multi_head_mlp(xf, sd, "shared_ffn." if use_shared_ffn else f"ffn.{i}.")
+        x = x + _lin(F.gelu(_lin(x, sd, f"adapters.{i}.0")), sd, f"adapters.{i}.2")
+        joint = x
+    return joint
