@@ -3,8 +3,10 @@
 
 python bench.py --gpus N --steps K --warmup W [--mode full|knn]
   full (default): one step = Swin-T tower on B synthetic 224x224 images + ClinicalBERT-geometry
-        tower on B synthetic 128-token reports (bf16) -> projection / heads -> exact cosine
-        top-10 of the B query embeddings over the gallery (config 2: B=256, 100k x 768 f32).
+        tower on B synthetic 128-token reports (bf16) -> joint-embedding head (default: the
+        reference's default model_type "multimodal", 5 fusion layers x 8 heads; --model-type
+        text|image runs both single-modality heads) -> exact cosine top-10 of the query embeddings
+        over the gallery (config 2: B=256, 100k x 768 f32).
   knn:  one step = exact cosine top-K of B resident queries over the gallery (kNN leg only).
 N>1 (torch.distributed.run): the gallery is row-sharded (N x rows per rank: weak scaling), every
 rank runs its own query batch through the towers and searches its shard for ALL ranks' queries
@@ -32,6 +34,9 @@ def parse():
     p.add_argument("--gallery", type=int, default=100_000, help="gallery rows per GPU")
     p.add_argument("--dim", type=int, default=768)
     p.add_argument("--k", type=int, default=10)
+    p.add_argument("--model-type", choices=["multimodal", "text", "image"], default="multimodal",
+                   help="joint-embedding head: multimodal (reference default, model.py:137; 5 fusion "
+                        "layers, 8 heads) or the single-modality heads (text + image both run)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-queries", type=int, default=0)
     return p.parse_args()
@@ -74,7 +79,7 @@ def main():
     model = None
     if a.mode == "full":
         from mmr_amd.model import build_bench_model
-        model = build_bench_model(device=dev, joint_dim=d)
+        model = build_bench_model(device=dev, joint_dim=d, model_type=a.model_type)
         imgs = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(B, synthetic.SEED + rank))).to(dev)
         ids_np, mask_np = synthetic.reports(B, 128, synthetic.SEED + 100 + rank)
         ids, mask = torch.from_numpy(ids_np).to(dev), torch.from_numpy(mask_np).to(dev)
@@ -133,7 +138,8 @@ def main():
 
     # whole-job throughput: every rank embeds B queries; every query is scored against the whole
     # world*n gallery (each rank scores all world*B queries against its n rows)
-    nq_step = (2 * B) if model is not None else B   # full mode: image-head + text-head queries
+    # full mode: one multimodal joint embedding per (image, report) pair, or image-head + text-head
+    nq_step = (2 * B) if (model is not None and a.model_type != "multimodal") else B
     q_per_s = world * B * a.steps / elapsed
     pairs_per_s = (world * nq_step) * (world * n) * a.steps / elapsed
     # roofline of the dominant kernel, per launch on one GPU
@@ -190,7 +196,9 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16 towers / f32 kNN (f64 re-rank)" if a.mode == "full" else "f32 (f64 re-rank)",
             "data": "synthetic (seeded N(0,1) gallery; random-init weights)",
-            "config": {"workload": ("cfg2: Swin-T + BERT-base towers, B=%d, top-%d over %dx%d f32 per GPU" % (B, K, n, d))
+            "config": {"workload": ("cfg2: Swin-T + BERT-base towers + %s head, B=%d, top-%d over %dx%d f32 per GPU"
+                                    % ("5-layer multimodal fusion" if a.model_type == "multimodal" else "image+text",
+                                       B, K, n, d))
                        if a.mode == "full" else ("kNN only: Q=%d, top-%d over %dx%d f32 per GPU" % (B, K, n, d)),
                        "global_batch": world * B, "gallery_rows": world * n, "dim": d, "k": K,
                        "parallelism": f"gallery row-shard x{world}" if world > 1 else "single"},
@@ -248,22 +256,29 @@ def cpu_baseline_full(a, G):
     nb = a.cpu_sample_queries or 8
     ssd, bsd = init_swin_state(SWIN_T, 2709), init_bert_state(BERT_BASE, 2710)
     hsd = init_head_state(768, 768, a.dim, 2711)
+    if a.model_type == "multimodal":
+        from mmr_amd.model import init_fusion_state
+        hsd.update(init_fusion_state(768, 768, a.dim, 8, 5, 2712))
     img = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(nb, synthetic.SEED)))
     ids, mask = (torch.from_numpy(x) for x in synthetic.reports(nb, 128, synthetic.SEED + 100))
 
     def run(n):
         with torch.no_grad():
             (g, p), t = otw.backbones_forward(img[:n], ids[:n], mask[:n], ssd, bsd, SWIN_T, BERT_BASE)
-            qi = otw.heads(g, p, t, hsd, "image")["joint_emb"]
-            qt = otw.heads(g, p, t, hsd, "text")["joint_emb"]
+            if a.model_type == "multimodal":
+                qi = otw.heads(g, p, t, hsd, "multimodal", mm_cfg={"num_heads": 8})["joint_emb"]
+                qt = qi[:0]
+            else:
+                qi = otw.heads(g, p, t, hsd, "image")["joint_emb"]
+                qt = otw.heads(g, p, t, hsd, "text")["joint_emb"]
         oknn.sklearn_topk(torch.cat([qi, qt]).numpy(), G, a.k)
     run(1)
     t0 = time.perf_counter()
     run(nb)
     t = time.perf_counter() - t0
     return {"value": nb / t, "unit": "query_embeddings/s", "cores": threads, "kind": "port",
-            "sample": f"{nb} (image, 128-token report) pairs: fp32 torch-CPU Swin-T + BERT-base + image/text "
-                      f"heads + numpy cosine/argsort top-{a.k} over {G.shape[0]}x{G.shape[1]} (oracle/towers.py, "
+            "sample": f"{nb} (image, 128-token report) pairs: fp32 torch-CPU Swin-T + BERT-base + {a.model_type} "
+                      f"head(s) + numpy cosine/argsort top-{a.k} over {G.shape[0]}x{G.shape[1]} (oracle/towers.py, "
                       f"oracle/knn.py), one timed run after warm-up, CPU: {cpu_model()}"}
 
 

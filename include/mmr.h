@@ -195,7 +195,9 @@ mmr_status mmr_linear_f32(const float* x, int64_t ldx, const float* w, const flo
 /* nn.MultiheadAttention core (no masks): per (batch, head) softmax(q k^T * scale) v.
  * q row (bi*lq + i) at q + row*ldq + head*dh (k, v likewise with lk); out (b*lq, ldo) bf16 and/or
  * mean_out (b, heads*dh) f32 = the mean over the lq query rows (either may be NULL, not both).
- * dh % 8 == 0, dh <= 192; strides multiples of 8 elements; K/V tile must fit the 160 KB LDS. */
+ * dh % 8 == 0, dh <= 192; strides multiples of 8 elements; any lq / lk (keys stream through LDS).
+ * mean_out is bitwise deterministic for lq <= 128; longer query sets add per-128-row partials with
+ * float atomics. */
 mmr_status mmr_mha(const uint16_t* q, int64_t ldq, const uint16_t* k, int64_t ldk, const uint16_t* v,
                    int64_t ldv, uint16_t* out, int64_t ldo, float* mean_out, int32_t b, int32_t lq,
                    int32_t lk, int32_t heads, int32_t dh, float scale, void* stream);

@@ -22,16 +22,21 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // ------------------------------------------------------------------ small-sequence MHA core
 // softmax(q k^T * scale) v per (batch, head) for the fusion's short sequences (text L <= 512,
-// 49 patches, 51-token fused sequence), no masks.  Block = (batch, head); each wave owns 32-query
-// tiles.  As in bert_attention (tower.hip): the swapped product S^T = K . Q^T on
-// v_mfma_f32_32x32x16_bf16 puts the query on the lane, the softmax reductions stay in registers,
-// and P^T feeds the P.V MFMA as its B operand with no data movement (V^T read in the matching key
-// permutation).  head_dim is padded to DT*32 with zeros (dh % 8 == 0); ragged query/key counts
-// are padded to 32 (padded keys -> -inf, padded queries never stored).  Operands are strided rows
-// (q row (b*lq + i) at q + row*ldq + head*dh), so Q/K/V are read in place from packed projection
-// outputs.  Optional f32 mean over the lq query rows (mean_out (b, heads*dh)): the fusion only
-// needs mean_L of several attention outputs (fusion.py:441,448, model.py:431), and
-// mean_L(A) W^T + b == mean_L(A W^T + b), so those out-projections shrink to one row per batch.
+// 49 patches, 51-token fused sequence), no masks.  Block = (batch*head, chunk of 128 queries), one
+// 32-query tile per wave; keys stream through LDS in blocks of MHA_KB with an online softmax.  As
+// in bert_attention (tower.hip): the swapped product S^T = K . Q^T on v_mfma_f32_32x32x16_bf16 puts
+// the query on the lane, the softmax reductions stay in registers, and P^T feeds the P.V MFMA as
+// its B operand with no data movement (V^T read in the matching key permutation).  head_dim is
+// padded to DT*32 with zeros (dh % 8 == 0); ragged query/key counts are padded to 32 (padded keys
+// -> -inf, padded queries never stored).  Operands are strided rows (q row (b*lq + i) at
+// q + row*ldq + head*dh), so Q/K/V are read in place from packed projection outputs.  Optional f32
+// mean over the lq query rows (mean_out (b, heads*dh)): the fusion only needs mean_L of several
+// attention outputs (fusion.py:441,448, model.py:431), and mean_L(A) W^T + b == mean_L(A W^T + b),
+// so those out-projections shrink to one row per batch.  With one query chunk (lq <= 128, every
+// fusion call at L = 128) the mean is reduced in LDS and stored; with several chunks each adds its
+// partial into the (pre-zeroed) output with a float atomic.
+constexpr int MHA_KB = 128;
+
 template <int DT>
 __global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q, int64_t ldq,
                                                  const uint16_t* __restrict__ k, int64_t ldk,
@@ -41,51 +46,56 @@ __global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q,
                                                  int heads, int dh, float scale) {
   constexpr int DHP = DT * 32;
   constexpr int KS = DHP / 16;
-  constexpr int KROW = DHP + 8;  // padded K row (elements): 16-B skew between consecutive keys
+  constexpr int KROW = DHP + 8;       // padded K row (elements): 16-B skew between consecutive keys
+  constexpr int VTS = MHA_KB + 4;     // V^T row stride (elements)
+  constexpr int NCH = DHP / 8;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int bi = blockIdx.x / heads, hh = blockIdx.x % heads;
   const int lkp = (lk + 31) & ~31;
-  const int vts = lkp + 4;                   // V^T row stride (elements)
-  uint16_t* Ks = (uint16_t*)smem;            // [lkp][KROW]
-  uint16_t* Vt = Ks + lkp * KROW;            // [DHP][vts]
-  float* msum = (float*)(Vt + DHP * vts);    // [DHP]
-  const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6, nwave = nthr >> 6;
-  constexpr int NCH = DHP / 8;
+  uint16_t* Ks = (uint16_t*)smem;            // [MHA_KB][KROW]
+  uint16_t* Vt = Ks + MHA_KB * KROW;         // [DHP][VTS]
+  float* msum = (float*)(Vt + DHP * VTS);    // [waves][DHP] per-wave partial means
+  const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6;
   const uint16_t* kbase = k + (int64_t)bi * lk * ldk + hh * dh;
   const uint16_t* vbase = v + (int64_t)bi * lk * ldv + hh * dh;
-  for (int c = tid; c < lkp * NCH; c += nthr) {
-    const int key = c / NCH, ch = c % NCH;
-    bf16x8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (key < lk && ch * 8 < dh) {
-      kv = *(const bf16x8*)(kbase + key * ldk + ch * 8);
-      vv = *(const bf16x8*)(vbase + key * ldv + ch * 8);
-    }
-    *(bf16x8*)(Ks + key * KROW + ch * 8) = kv;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) Vt[(ch * 8 + j) * vts + key] = (uint16_t)vv[j];
-  }
-  for (int d = tid; d < DHP; d += nthr) msum[d] = 0.f;
-  __syncthreads();
 
   const int r = lane & 31, hf = lane >> 5;
-  const int nqt = (lq + 31) / 32;
-  for (int qt = wave; qt < nqt; qt += nwave) {
-    const int qi = qt * 32 + r;
-    const bool qok = qi < lq;
+  const int q0 = blockIdx.y * 128 + wave * 32;
+  const bool active = q0 < lq;               // wave-uniform
+  const int qi = q0 + r;
+  const bool qok = qi < lq;
+  bf16x8 qf[KS];
+  {
     const uint16_t* qrow = q + ((int64_t)bi * lq + (qok ? qi : 0)) * ldq + hh * dh;
-    bf16x8 qf[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int c8 = ks * 2 + hf;
       qf[ks] = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
       if (qok && c8 * 8 < dh) qf[ks] = *(const bf16x8*)(qrow + c8 * 8);
     }
-    f32x16 o[DT];
+  }
+  f32x16 o[DT];
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt) o[dt] = (f32x16){0};
-    float m_run = -FLT_MAX, l_run = 0.f;
-    for (int kb = 0; kb < lkp; kb += 64) {
-      const int nt = min(64, lkp - kb) / 32;
+  for (int dt = 0; dt < DT; ++dt) o[dt] = (f32x16){0};
+  float m_run = -FLT_MAX, l_run = 0.f;
+  for (int k0 = 0; k0 < lkp; k0 += MHA_KB) {
+    const int kn = min(MHA_KB, lkp - k0);   // keys staged this round (multiple of 32)
+    __syncthreads();                          // previous key block consumed
+    for (int c = tid; c < kn * NCH; c += nthr) {
+      const int key = c / NCH, ch = c % NCH;
+      bf16x8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (k0 + key < lk && ch * 8 < dh) {
+        kv = *(const bf16x8*)(kbase + (int64_t)(k0 + key) * ldk + ch * 8);
+        vv = *(const bf16x8*)(vbase + (int64_t)(k0 + key) * ldv + ch * 8);
+      }
+      *(bf16x8*)(Ks + key * KROW + ch * 8) = kv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Vt[(ch * 8 + j) * VTS + key] = (uint16_t)vv[j];
+    }
+    __syncthreads();
+    if (!active) continue;
+    for (int kb = 0; kb < kn; kb += 64) {
+      const int nt = min(64, kn - kb) / 32;
       f32x16 s[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -105,7 +115,7 @@ __global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q,
         if (t < nt) {
 #pragma unroll
           for (int rg = 0; rg < 16; ++rg) {
-            const int key = kb + t * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * hf;
+            const int key = k0 + kb + t * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * hf;
             const float x = key < lk ? s[t][rg] * scale : -FLT_MAX;
             s[t][rg] = x;
             mloc = fmaxf(mloc, x);
@@ -145,7 +155,7 @@ __global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q,
             const int kk = kb + t * 32 + 16 * sidx + 4 * hf;
 #pragma unroll
             for (int dt = 0; dt < DT; ++dt) {
-              const uint16_t* vrow = Vt + (dt * 32 + r) * vts;
+              const uint16_t* vrow = Vt + (dt * 32 + r) * VTS;
               const bf16x4 lo = *(const bf16x4*)(vrow + kk);
               const bf16x4 hi = *(const bf16x4*)(vrow + kk + 8);
               const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -155,6 +165,8 @@ __global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q,
         }
       }
     }
+  }
+  if (active) {
     const float inv = 1.0f / (l_run + __shfl_xor(l_run, 32, 64));
     if (out != nullptr && qok) {
       uint16_t* orow = out + ((int64_t)bi * lq + qi) * ldo + hh * dh;
@@ -180,14 +192,21 @@ __global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q,
 #pragma unroll
           for (int off = 1; off < 32; off <<= 1) x += __shfl_xor(x, off, 64);
           const int d = dt * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * hf;
-          if (r == 0 && d < dh) atomicAdd(&msum[d], x);
+          if (r == 0) msum[wave * DHP + d] = x;
         }
     }
   }
   if (mean_out != nullptr) {
     __syncthreads();
-    for (int d = tid; d < dh; d += nthr)
-      mean_out[(int64_t)bi * heads * dh + hh * dh + d] = msum[d] / (float)lq;
+    const int nw = nthr >> 6;
+    for (int d = tid; d < dh; d += nthr) {
+      float s = 0.f;
+      for (int w = 0; w < nw; ++w)  // fixed order: deterministic
+        if (blockIdx.y * 128 + w * 32 < lq) s += msum[w * DHP + d];
+      float* dst = mean_out + (int64_t)bi * heads * dh + hh * dh + d;
+      if (gridDim.y == 1) *dst = s / (float)lq;
+      else atomicAdd(dst, s / (float)lq);
+    }
   }
 }
 
@@ -325,12 +344,12 @@ mmr_status mmr_mha(const uint16_t* q, int64_t ldq, const uint16_t* k, int64_t ld
               "mmr_mha: operands must be 16-B aligned");
   if (b == 0) return MMR_OK;
   const int dt = (dh + 31) / 32;
-  const int lkp = (lk + 31) & ~31;
-  const size_t lds = (size_t)lkp * (dt * 32 + 8) * 2 + (size_t)dt * 32 * (lkp + 4) * 2 + (size_t)dt * 32 * 4;
-  MMR_REQUIRE(lds <= 160 * 1024, "mmr_mha: lk=%d x head_dim=%d exceeds the 160 KB LDS", lk, dh);
-  const int nqt = (lq + 31) / 32;
-  const dim3 grid((unsigned)((int64_t)b * heads)), blk(64 * std::min(4, nqt));
+  const size_t lds = (size_t)MHA_KB * (dt * 32 + 8) * 2 + (size_t)dt * 32 * (MHA_KB + 4) * 2 + (size_t)4 * dt * 32 * 4;
+  const int nqt = (lq + 31) / 32, nchunk = (lq + 127) / 128;
+  const dim3 grid((unsigned)((int64_t)b * heads), (unsigned)nchunk), blk(64 * std::min(4, nqt));
   hipStream_t st = mmr::as_stream(stream);
+  if (mean_out && nchunk > 1)  // query chunks accumulate their partial means
+    MMR_CHECK_HIP(hipMemsetAsync(mean_out, 0, sizeof(float) * (size_t)b * heads * dh, st));
 #define MMR_MHA(D) mha_small<D><<<grid, blk, lds, st>>>(q, ldq, k, ldk, v, ldv, out, ldo, mean_out, lq, lk, heads, dh, scale)
   switch (dt) {
     case 1: MMR_MHA(1); break;

@@ -1,0 +1,191 @@
+"""Multimodal fusion stack on libmmr kernels — model_type="multimodal" of MultiModalRetrievalModel.
+
+Reference (eval semantics): CrossModalFusion.forward src/Model/fusion.py:390-471,
+PreFusionEnhancer fusion.py:20-35, MultiModalRetrievalModel.forward model.py:375-459 (pos_encoder
+model.py:91-107, self_attn = nn.MultiheadAttention(joint_dim, num_heads), StochasticDepth = plain
+residual in eval, MultiHeadMLP model.py:61-75, adapters model.py:262-268).  Restated in plain torch
+in oracle/towers.py:multimodal and pinned there against the reference's own outputs.
+
+Every fusion layer reads the SAME backbone features (img_global, img_patches, txt_feats); only the
+(B, D) joint vector chains through the layers.  Per layer the device work is:
+
+  text enhancer    X = T + pos  ->  QKV GEMM  ->  mha(L x L)  ->  out GEMM  ->  LN(a*X + .)      [B*L rows]
+  patch enhancer   same over the 49 patch tokens                                                [B*49 rows]
+  global enhancer  a 1-token self-attention is exactly out_proj(v_proj(x)): ONE folded f32 linear
+  cross attention  nn.MultiheadAttention re-projects its inputs (in_proj after query_txt/key_img/...),
+                   two affine maps in a row: folded at load into one weight (W_in . W, W_in . b + b_in),
+                   so text -> [q_t2i | k_i2t | v_i2t] and patches -> [k_t2i | v_t2i | q_i2t] are one
+                   GEMM each; txt2img only enters through its mean over L, and mean commutes with the
+                   affine out_proj, so mha emits the mean directly (no B*L x D out_proj GEMM)
+  fused sequence   [ln_img(.); img_patch_proj(P) + out_proj(img2txt); ln_txt(.)] + pe  ->  QKV GEMM
+                   -> mha with mean output -> one f32 out_proj row per batch (model.py:431 mean)
+  joint chain      f32 (B, D): norm1 / alpha residual, norm2 -> FFN, adapter (exact f32 MFMA linears)
+
+bf16 activations / f32 accumulation for the token-level work, f32 for every per-query vector.
+"""
+import math
+
+import torch
+
+from . import ops
+
+
+def _f(t, dev):
+    return t.detach().to(device=dev, dtype=torch.float32).contiguous()
+
+
+def _bf(t, dev):
+    return t.detach().to(device=dev, dtype=torch.bfloat16).contiguous()
+
+
+def _fold(w_in, b_in, w, b):
+    """(W_in, b_in) o (W, b) = (W_in W, W_in b + b_in), computed in f64."""
+    w_in, b_in, w, b = (t.detach().double().cpu() for t in (w_in, b_in, w, b))
+    return w_in @ w, w_in @ b + b_in
+
+
+class _Enhancer:
+    """PreFusionEnhancer weights (fusion.py:20-35)."""
+
+    def __init__(self, sd, p, heads, dev):
+        C = sd[p + "self_attn.in_proj_weight"].shape[1]
+        self.C, self.heads, self.dh = C, heads, C // heads
+        self.pos = _f(sd[p + "pos_embed"][0], dev)                       # [max_len][C]
+        self.w_in, self.b_in = _bf(sd[p + "self_attn.in_proj_weight"], dev), _f(sd[p + "self_attn.in_proj_bias"], dev)
+        self.w_o, self.b_o = _bf(sd[p + "self_attn.out_proj.weight"], dev), _f(sd[p + "self_attn.out_proj.bias"], dev)
+        self.alpha = _f(sd[p + "alpha"].reshape(1), dev)
+        self.g, self.b = _f(sd[p + "norm1.weight"], dev), _f(sd[p + "norm1.bias"], dev)
+
+    def __call__(self, x, B, L, eps):
+        """x (B*L, C) f32 or bf16 -> LN(alpha*(x + pos) + MHA(x + pos)) bf16 (B*L, C)."""
+        X = ops.add_pos(x, self.pos, L)
+        qkv = ops.linear(X, self.w_in, self.b_in)
+        a = torch.empty_like(X)
+        C = self.C
+        ops.mha(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], B, L, L, self.heads, self.dh,
+                1.0 / math.sqrt(self.dh), out=a)
+        x2 = ops.linear(a, self.w_o, self.b_o)
+        return ops.ln_rows(X, self.g, self.b, eps, alpha=self.alpha, residual=x2)
+
+
+class FusionStack:
+    """The multimodal head: num_fusion_layers x CrossModalFusion + combiner (model.py:375-459)."""
+
+    def __init__(self, sd, num_heads, device="cuda", use_shared_ffn=False, eps=1e-5):
+        dev = torch.device(device)
+        self.device, self.heads, self.eps = dev, num_heads, eps
+        n = 1 + max(int(k.split(".")[1]) for k in sd if k.startswith("fusion_layers."))
+        self.layers = []
+        D = sd["self_attn.in_proj_weight"].shape[1]
+        self.D = D
+        for i in range(n):
+            p = f"fusion_layers.{i}."
+            g = lambda k: sd[p + k]  # noqa: E731
+            L = {"txt": _Enhancer(sd, p + "txt_self_attn.", num_heads, dev),
+                 "patch": _Enhancer(sd, p + "img_patch_self_attn.", num_heads, dev)}
+            # global enhancer: softmax over ONE key is 1 -> x2 = Wo (Wv x + bv) + bo; with x = G + pos0
+            # and the LN input alpha*x + x2 = alpha*G + (Wov G + Wov pos0 + bov + alpha*pos0)
+            pg = "img_global_self_attn."
+            Ci = g(pg + "self_attn.in_proj_weight").shape[1]
+            wv = g(pg + "self_attn.in_proj_weight")[2 * Ci:]
+            bv = g(pg + "self_attn.in_proj_bias")[2 * Ci:]
+            wov, bov = _fold(g(pg + "self_attn.out_proj.weight"), g(pg + "self_attn.out_proj.bias"), wv, bv)
+            pos0 = g(pg + "pos_embed")[0, 0].double()
+            alpha_g = g(pg + "alpha").double().reshape(())
+            L["g_w"] = _f(wov, dev)
+            L["g_b"] = _f(wov @ pos0 + bov + alpha_g * pos0, dev)
+            L["g_alpha"] = _f(g(pg + "alpha").reshape(1), dev)
+            L["g_ln"] = (_f(g(pg + "norm1.weight"), dev), _f(g(pg + "norm1.bias"), dev))
+            # cross attention: fold the pre-projections into nn.MultiheadAttention's in_proj
+            wi1, bi1 = g("attn_txt2img.in_proj_weight"), g("attn_txt2img.in_proj_bias")
+            wi2, bi2 = g("attn_img2txt.in_proj_weight"), g("attn_img2txt.in_proj_bias")
+            sl = [slice(0, D), slice(D, 2 * D), slice(2 * D, 3 * D)]
+            qt = _fold(wi1[sl[0]], bi1[sl[0]], g("query_txt.weight"), g("query_txt.bias"))
+            kt = _fold(wi2[sl[1]], bi2[sl[1]], g("key_txt.weight"), g("key_txt.bias"))
+            vt = _fold(wi2[sl[2]], bi2[sl[2]], g("value_txt.weight"), g("value_txt.bias"))
+            ki = _fold(wi1[sl[1]], bi1[sl[1]], g("key_img.weight"), g("key_img.bias"))
+            vi = _fold(wi1[sl[2]], bi1[sl[2]], g("value_img.weight"), g("value_img.bias"))
+            qi = _fold(wi2[sl[0]], bi2[sl[0]], g("query_img.weight"), g("query_img.bias"))
+            L["t_w"] = _bf(torch.cat([qt[0], kt[0], vt[0]]), dev)
+            L["t_b"] = _f(torch.cat([qt[1], kt[1], vt[1]]), dev)
+            L["p_w"] = _bf(torch.cat([ki[0], vi[0], qi[0]]), dev)
+            L["p_b"] = _f(torch.cat([ki[1], vi[1], qi[1]]), dev)
+            L["pp_w"], L["pp_b"] = _bf(g("img_patch_proj.weight"), dev), _f(g("img_patch_proj.bias"), dev)
+            L["o1_w"], L["o1_b"] = _f(g("attn_txt2img.out_proj.weight"), dev), _f(g("attn_txt2img.out_proj.bias"), dev)
+            L["o2_wb"] = _bf(g("attn_img2txt.out_proj.weight"), dev)
+            L["o2_w"], L["o2_b"] = _f(g("attn_img2txt.out_proj.weight"), dev), _f(g("attn_img2txt.out_proj.bias"), dev)
+            L["gp_w"], L["gp_b"] = _f(g("img_global_proj.weight"), dev), _f(g("img_global_proj.bias"), dev)
+            L["tp_w"], L["tp_b"] = _f(g("txt_proj.weight"), dev), _f(g("txt_proj.bias"), dev)
+            L["ln_img"] = (_f(g("ln_img.weight"), dev), _f(g("ln_img.bias"), dev))
+            L["ln_txt"] = (_f(g("ln_txt.weight"), dev), _f(g("ln_txt.bias"), dev))
+            L["default_txt"] = _bf(g("default_txt_token").reshape(1, -1), dev)
+            # combiner (model.py:227-268) for layer i
+            L["n1"] = (_f(sd[f"norm1_layers.{i}.weight"], dev), _f(sd[f"norm1_layers.{i}.bias"], dev))
+            L["n2"] = (_f(sd[f"norm2_layers.{i}.weight"], dev), _f(sd[f"norm2_layers.{i}.bias"], dev))
+            fp = "shared_ffn." if use_shared_ffn else f"ffn.{i}."
+            L["ffn"] = tuple(_f(sd[fp + k], dev) for k in ("linear1.weight", "linear1.bias", "linear2.weight",
+                                                           "linear2.bias"))
+            L["ad"] = tuple(_f(sd[f"adapters.{i}.{k}"], dev) for k in ("0.weight", "0.bias", "2.weight", "2.bias"))
+            self.layers.append(L)
+        self.s_w, self.s_b = _bf(sd["self_attn.in_proj_weight"], dev), _f(sd["self_attn.in_proj_bias"], dev)
+        self.s_ow, self.s_ob = _f(sd["self_attn.out_proj.weight"], dev), _f(sd["self_attn.out_proj.bias"], dev)
+        self.pe = _f(sd["pos_encoder.pe"][0], dev)
+        self.alpha = _f(sd["alpha"].reshape(1), dev)
+
+    def layer_seq(self, L, G, P, T, B, Lt, Np):
+        """CrossModalFusion.forward -> fused-sequence mean (B, D) f32 (model.py:396-431)."""
+        D, h, eps = self.D, self.heads, self.eps
+        dh = D // h
+        sc = 1.0 / math.sqrt(dh)
+        Te = L["txt"](T, B, Lt, eps)                                   # (B*Lt, Ct) bf16
+        Pe = L["patch"](P, B, Np, eps)                                 # (B*Np, Ci) bf16
+        Ge = ops.linear_f32(G, L["g_w"], L["g_b"])                     # folded 1-token attention
+        Ge = ops.ln_rows(G, *L["g_ln"], eps, alpha=L["g_alpha"], residual=Ge)
+        TQ = ops.linear(Te, L["t_w"], L["t_b"])                        # (B*Lt, 3D): q_t2i | k_i2t | v_i2t
+        PQ = ops.linear(Pe, L["p_w"], L["p_b"])                        # (B*Np, 3D): k_t2i | v_t2i | q_i2t
+        PP = ops.linear(Pe, L["pp_w"], L["pp_b"])                      # img_patch_proj
+        m1 = torch.empty((B, D), dtype=torch.float32, device=self.device)
+        ops.mha(TQ[:, :D], PQ[:, :D], PQ[:, D:2 * D], B, Lt, Np, h, dh, sc, mean_out=m1)
+        a2 = torch.empty((B * Np, D), dtype=torch.bfloat16, device=self.device)
+        m2 = torch.empty((B, D), dtype=torch.float32, device=self.device)
+        ops.mha(PQ[:, 2 * D:], TQ[:, D:2 * D], TQ[:, 2 * D:], B, Np, Lt, h, dh, sc, out=a2, mean_out=m2)
+        PF = ops.linear(a2, L["o2_wb"], L["o2_b"], residual=PP)       # patches_fused (fusion.py:437)
+        t2i = ops.linear_f32(m1, L["o1_w"], L["o1_b"])                 # mean_L att_txt2img
+        x1 = ops.linear_f32(Ge, L["gp_w"], L["gp_b"], residual=t2i)
+        x1 = ops.ln_rows(x1, *L["ln_img"], eps)
+        i2t = ops.linear_f32(m2, L["o2_w"], L["o2_b"])                 # mean_Np att_img2txt
+        cls = ops.rows_to_f32(Te, B, Te.shape[1], Lt * Te.shape[1])
+        x2 = ops.linear_f32(cls, L["tp_w"], L["tp_b"], residual=i2t)
+        x2 = ops.ln_rows(x2, *L["ln_txt"], eps)
+        S = ops.assemble_seq(x1, PF, x2, self.pe, Np).view(B * (Np + 2), D)
+        SQ = ops.linear(S, self.s_w, self.s_b)
+        m3 = torch.empty((B, D), dtype=torch.float32, device=self.device)
+        ops.mha(SQ[:, :D], SQ[:, D:2 * D], SQ[:, 2 * D:], B, Np + 2, Np + 2, h, dh, sc, mean_out=m3)
+        return ops.linear_f32(m3, self.s_ow, self.s_ob)               # mean of self_attn output
+
+    def forward(self, img_global, img_patches, txt_feats):
+        """img_global (B, Ci) f32, img_patches (B, Np, Ci) f32, txt_feats (B, L, Ct) bf16/f32 or None
+        -> joint_emb (B, D) f32."""
+        B, Np, Ci = img_patches.shape
+        G = img_global.float().contiguous()
+        P = img_patches.contiguous().view(B * Np, Ci)
+        joint = None
+        eps = self.eps
+        for i, L in enumerate(self.layers):
+            if txt_feats is None:  # learnable default text token (fusion.py:404-407)
+                T, Lt = L["default_txt"].expand(B, -1).contiguous(), 1
+            else:
+                Lt = txt_feats.shape[1]
+                T = txt_feats.to(torch.bfloat16).contiguous().view(B * Lt, -1)
+            fused = self.layer_seq(L, G, P, T, B, Lt, Np)
+            if i == 0:
+                x = fused
+            else:  # norm1(joint) + alpha * fused  (StochasticDepth in eval = plain residual)
+                x = ops.ln_rows(joint, *L["n1"], eps, post=fused, post_scale=self.alpha)
+            xf = ops.ln_rows(x, *L["n2"], eps)
+            w1, b1, w2, b2 = L["ffn"]
+            ops.linear_f32(ops.linear_f32(xf, w1, b1, act=1), w2, b2, residual=x, out=x)
+            a1, c1, a2, c2 = L["ad"]
+            ops.linear_f32(ops.linear_f32(x, a1, c1, act=1), a2, c2, residual=x, out=x)
+            joint = x
+        return joint

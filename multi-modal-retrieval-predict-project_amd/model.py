@@ -13,12 +13,14 @@ MultiModalRetrievalModel.forward(...) -> {"joint_emb", "img_emb", "txt_emb", "lo
                                           = ffn0(img_proj(mean(cat[g, p])))  (affine proj)
     ffn0 = MultiHeadMLP (Linear D->2D, GELU, Linear 2D->D), model.py:61-75; shared_ffn when
     use_shared_ffn (reference default True, configs/config.yaml false).
-    "multimodal" (5x CrossModalFusion, fusion.py:334-471) is the next row of SURVEY.md §8f and
-    raises NotImplementedError; the classifier (logits) is classification, out of scope -> None.
+    "multimodal" = num_fusion_layers x CrossModalFusion (fusion.py:334-471) + combiner
+    (model.py:375-459) on libmmr kernels (mmr_amd/fusion.py); the classifier (logits) is
+    classification, out of scope -> None; attention maps (return_attention) are not produced.
 """
 import torch
 
 from . import ops
+from .fusion import FusionStack
 from .towers import BERT_BASE, SWIN_T, BertTower, SwinTower, init_bert_state, init_swin_state
 
 
@@ -93,6 +95,14 @@ class MultiModalRetrievalModel:
         self.txt_proj = (f("txt_proj.weight"), f("txt_proj.bias"))
         pre = "shared_ffn." if use_shared_ffn else "ffn.0."
         self.ffn = (f(pre + "linear1.weight"), f(pre + "linear1.bias"), f(pre + "linear2.weight"), f(pre + "linear2.bias"))
+        self.num_heads = num_heads
+        self.fusion = None
+        if model_type == "multimodal":
+            if use_cls_only:  # model.py:428-429 indexes the 2-D comb_mlp output: the reference raises
+                raise ValueError("model_type='multimodal' with use_cls_only fails in the reference (model.py:428)")
+            if not any(k.startswith("fusion_layers.") for k in hs):
+                raise ValueError("head_state has no fusion_layers.* weights for model_type='multimodal'")
+            self.fusion = FusionStack(hs, num_heads, device=self.device, use_shared_ffn=use_shared_ffn)
 
     @classmethod
     def from_reference_state_dict(cls, sd, swin_cfg, bert_cfg, joint_dim, model_type="text", device="cuda",
@@ -114,16 +124,20 @@ class MultiModalRetrievalModel:
         return ops.proj_head(x, proj[0], proj[1], *self.ffn, l2norm=l2norm)
 
     def forward(self, image, input_ids, attention_mask, return_attention=False):
-        if self.model_type == "multimodal":
-            raise NotImplementedError("multimodal fusion stack (fusion.py:334-471) is SURVEY.md §8f row 1 (next)")
-        img_global = pool = txt_mean = None
+        mm = self.model_type == "multimodal"
+        img_global = patches = pool = txt_mean = txt = None
         if image is not None:
-            img_global, _, pool = self.backbones.encode_image(image, want_patches=False)
+            img_global, patches, pool = self.backbones.encode_image(image, want_patches=mm)
+        elif mm:  # CrossModalFusion unpacks img_patch.shape (fusion.py:421): the reference needs the image
+            raise ValueError("model_type='multimodal' needs an image (fusion.py:421)")
         if input_ids is not None:
-            txt_mean = self._txt_pool(self.backbones.encode_text(input_ids, attention_mask))
+            txt = self.backbones.encode_text(input_ids, attention_mask)
+            txt_mean = self._txt_pool(txt)
         img_emb = ops.proj_head(img_global, *self.img_proj) if img_global is not None else None
         txt_emb = ops.proj_head(txt_mean, *self.txt_proj) if txt_mean is not None else None
-        if self.model_type == "image":
+        if mm:
+            joint = self.fusion.forward(img_global, patches, txt)
+        elif self.model_type == "image":
             joint = self._head(pool, self.img_proj)
         else:
             joint = self._head(txt_mean, self.txt_proj)
@@ -132,8 +146,11 @@ class MultiModalRetrievalModel:
     __call__ = forward
 
     def query_embeddings(self, image, input_ids, attention_mask):
-        """Both single-modality heads on one (image, report) batch: (2B, D) f32 = [image-head joint
-        embeddings; text-head joint embeddings] — the retrieval keys of model_type image / text."""
+        """Retrieval keys of one (image, report) batch.  multimodal: (B, D) f32 joint embeddings;
+        image / text: both single-modality heads, (2B, D) = [image-head; text-head] joint embeddings."""
+        if self.model_type == "multimodal":
+            g, p, _ = self.backbones.encode_image(image, want_patches=True)
+            return self.fusion.forward(g, p, self.backbones.encode_text(input_ids, attention_mask))
         _, _, pool = self.backbones.encode_image(image, want_patches=False)
         txt_mean = self._txt_pool(self.backbones.encode_text(input_ids, attention_mask))
         return torch.cat([self._head(pool, self.img_proj), self._head(txt_mean, self.txt_proj)], 0)
@@ -153,6 +170,68 @@ def init_head_state(img_dim, txt_dim, joint_dim, seed=2711):
     return sd
 
 
-def build_bench_model(device="cuda", joint_dim=768, seed=2709):
-    """Swin-Tiny + ClinicalBERT-base geometry, random init (no checkpoints offline)."""
-    return MultiModalRetrievalModel(joint_dim=joint_dim, model_type="text", device=device, seed=seed)
+def init_fusion_state(img_dim, txt_dim, joint_dim, num_heads=8, num_fusion_layers=5, seed=2712,
+                      pos_len=512, use_shared_ffn=False):
+    """Random weights under the reference's key names for the multimodal head (fusion_layers.*,
+    self_attn, norm1/2_layers, pos_encoder, alpha, ffn.i / shared_ffn, adapters.i); nn.Linear-like
+    fan-in scaling, LayerNorm affine near identity, positional tables std 0.02."""
+    g = torch.Generator().manual_seed(seed)
+    D = joint_dim
+
+    def lin(sd, p, o, i):
+        sd[p + ".weight"] = torch.randn(o, i, generator=g) * i ** -0.5
+        sd[p + ".bias"] = torch.randn(o, generator=g) * 0.02
+
+    def ln(sd, p, c):
+        sd[p + ".weight"] = 1 + 0.05 * torch.randn(c, generator=g)
+        sd[p + ".bias"] = 0.05 * torch.randn(c, generator=g)
+
+    def mha(sd, p, e):
+        sd[p + "in_proj_weight"] = torch.randn(3 * e, e, generator=g) * e ** -0.5
+        sd[p + "in_proj_bias"] = torch.randn(3 * e, generator=g) * 0.02
+        lin(sd, p + "out_proj", e, e)
+
+    sd = {}
+    for i in range(num_fusion_layers):
+        p = f"fusion_layers.{i}."
+        for name, c in (("txt_self_attn.", txt_dim), ("img_patch_self_attn.", img_dim), ("img_global_self_attn.", img_dim)):
+            sd[p + name + "pos_embed"] = torch.randn(1, pos_len, c, generator=g) * 0.02
+            mha(sd, p + name + "self_attn.", c)
+            ln(sd, p + name + "norm1", c)
+            sd[p + name + "alpha"] = torch.ones(1)
+        ln(sd, p + "ln_img", D)
+        ln(sd, p + "ln_txt", D)
+        for name, c in (("query_txt", txt_dim), ("key_img", img_dim), ("value_img", img_dim), ("query_img", img_dim),
+                        ("key_txt", txt_dim), ("value_txt", txt_dim), ("txt_proj", txt_dim),
+                        ("img_patch_proj", img_dim), ("img_global_proj", img_dim)):
+            lin(sd, p + name, D, c)
+        mha(sd, p + "attn_txt2img.", D)
+        mha(sd, p + "attn_img2txt.", D)
+        sd[p + "default_txt_token"] = torch.randn(1, 1, txt_dim, generator=g) * 0.02
+        lin(sd, p + "comb_mlp.0", D, 3 * D)
+        lin(sd, p + "comb_mlp.3", D, D)
+        ln(sd, f"norm1_layers.{i}", D)
+        ln(sd, f"norm2_layers.{i}", D)
+        if not use_shared_ffn:
+            lin(sd, f"ffn.{i}.linear1", 2 * D, D)
+            lin(sd, f"ffn.{i}.linear2", D, 2 * D)
+        lin(sd, f"adapters.{i}.0", D // 2, D)
+        lin(sd, f"adapters.{i}.2", D, D // 2)
+    mha(sd, "self_attn.", D)
+    sd["alpha"] = torch.ones(1)
+    sd["pos_encoder.pe"] = torch.randn(1, txt_dim, D, generator=g) * 0.02
+    if use_shared_ffn:
+        lin(sd, "shared_ffn.linear1", 2 * D, D)
+        lin(sd, "shared_ffn.linear2", D, 2 * D)
+    return sd
+
+
+def build_bench_model(device="cuda", joint_dim=768, seed=2709, model_type="multimodal", num_heads=8,
+                      num_fusion_layers=5):
+    """Swin-Tiny + ClinicalBERT-base geometry, random init (no checkpoints offline); multimodal head
+    with configs/config.yaml's num_heads 8 / num_fusion_layers 5 at joint_dim 768."""
+    hs = init_head_state(768, 768, joint_dim, seed + 2)
+    if model_type == "multimodal":
+        hs.update(init_fusion_state(768, 768, joint_dim, num_heads, num_fusion_layers, seed + 3))
+    return MultiModalRetrievalModel(joint_dim=joint_dim, num_heads=num_heads, model_type=model_type,
+                                    head_state=hs, device=device, seed=seed)

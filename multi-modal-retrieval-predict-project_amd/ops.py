@@ -131,6 +131,67 @@ def proj_head(x, wp, bp, w1=None, b1=None, w2=None, b2=None, l2norm=False):
     return y
 
 
+def linear_f32(x, w, bias=None, residual=None, act=0, out=None):
+    """act(x @ w.T + bias) (+ residual) in exact f32; x (B, cin) f32 rows (may be a strided view with
+    unit column stride), residual may be `out` (in-place accumulate)."""
+    _lib.require_gpu(x)
+    assert x.dim() == 2 and x.stride(1) == 1
+    B, cin = x.shape
+    cout = w.shape[0]
+    y = out if out is not None else torch.empty((B, cout), dtype=torch.float32, device=x.device)
+    ldr = residual.stride(0) if residual is not None else 0
+    _chk(_L().mmr_linear_f32(_lib.ptr(x), x.stride(0), _lib.ptr(w), _lib.ptr(bias), _lib.ptr(residual), ldr,
+                             _lib.ptr(y), y.stride(0), B, cin, cout, act, _s(x)), "mmr_linear_f32")
+    return y
+
+
+def mha(q, k, v, b, lq, lk, heads, dh, scale, out=None, mean_out=None):
+    """Attention core over strided row views: q (b*lq, >=heads*dh) etc. (unit column stride)."""
+    _lib.require_gpu(q)
+    _chk(_L().mmr_mha(_lib.ptr(q), q.stride(0), _lib.ptr(k), k.stride(0), _lib.ptr(v), v.stride(0),
+                      _lib.ptr(out), out.stride(0) if out is not None else 0, _lib.ptr(mean_out), b, lq, lk,
+                      heads, dh, float(scale), _s(q)), "mmr_mha")
+    return out, mean_out
+
+
+def add_pos(x, pos, l):
+    """bf16 (rows, c) = x + pos[row % l] for x (..., c) f32 or bf16 contiguous, pos f32 [>= l][c]."""
+    _lib.require_gpu(x)
+    c = x.shape[-1]
+    y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    _chk(_L().mmr_add_pos_bf16(_lib.ptr(x), int(x.dtype == torch.float32), _lib.ptr(pos), _lib.ptr(y),
+                               x.numel() // c, l, c, _s(x)), "mmr_add_pos_bf16")
+    return y
+
+
+def ln_rows(x, g, b, eps, alpha=None, residual=None, post=None, post_scale=None, out=None):
+    """LN(alpha*x + residual) * g + b (+ post_scale*post) over 2-D row views (f32 or bf16 in/out)."""
+    _lib.require_gpu(x)
+    assert x.dim() == 2 and x.stride(1) == 1
+    rows, c = x.shape
+    y = out if out is not None else torch.empty((rows, c), dtype=x.dtype, device=x.device)
+    _chk(_L().mmr_ln_rows(_lib.ptr(x), x.stride(0), _lib.ptr(alpha), _lib.ptr(residual),
+                          residual.stride(0) if residual is not None else 0, _lib.ptr(g), _lib.ptr(b),
+                          _lib.ptr(post), post.stride(0) if post is not None else 0, _lib.ptr(post_scale),
+                          _lib.ptr(y), y.stride(0), rows, c, float(eps), int(x.dtype == torch.bfloat16), _s(x)),
+         "mmr_ln_rows")
+    return y
+
+
+def assemble_seq(x1, pf, x2, pe, np_):
+    B, c = x1.shape
+    seq = torch.empty((B, np_ + 2, c), dtype=torch.bfloat16, device=x1.device)
+    _chk(_L().mmr_assemble_seq(_lib.ptr(x1), _lib.ptr(pf), _lib.ptr(x2), _lib.ptr(pe), _lib.ptr(seq), B, np_, c,
+                               _s(x1)), "mmr_assemble_seq")
+    return seq
+
+
+def rows_to_f32(x, b, c, ldx):
+    y = torch.empty((b, c), dtype=torch.float32, device=x.device)
+    _chk(_L().mmr_rows_to_f32(_lib.ptr(x), ldx, _lib.ptr(y), b, c, _s(x)), "mmr_rows_to_f32")
+    return y
+
+
 def swin_mlp_pack(w1, w2):
     """fc1.weight [4C][C], fc2.weight [C][4C] (bf16, device) -> packed chunks for swin_mlp, or None if
     C is not one of the fused widths."""

@@ -1,0 +1,150 @@
+"""GPU parity of the multimodal fusion stack (model_type="multimodal", model.py:375-459) and its
+kernels against plain-torch fp32 (oracle/towers.py: mha / cross_modal_fusion / multimodal, pinned to
+the reference by tests/golden/towers_mini.npz in test_oracle_golden.py).
+
+Tolerances: attention core (bf16 q/k/v, bf16 P) max|err| <= 2e-2 * max|ref|; exact-f32 kernels
+(linear_f32, ln_rows f32) 1e-5; end-to-end multimodal joint embeddings cosine >= 0.999 per row and
+max|err| <= 4e-2 * max|ref| (bf16 token activations through the stack)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mmr_amd import ops, synthetic
+from mmr_amd.model import Backbones, MultiModalRetrievalModel, init_fusion_state, init_head_state
+from mmr_amd.towers import BERT_BASE, SWIN_T, init_bert_state, init_swin_state
+from oracle import towers as otw
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel_err(got, ref):
+    got = got.detach().float().cpu()
+    ref = ref.detach().float().cpu()
+    return (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-12)
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("B,lq,lk,heads,dh", [(2, 128, 128, 8, 96), (3, 49, 128, 8, 96), (2, 128, 49, 4, 16),
+                                              (2, 51, 51, 8, 96), (2, 1, 1, 4, 32), (1, 77, 300, 2, 64),
+                                              (2, 40, 512, 3, 128), (1, 33, 65, 1, 192), (2, 300, 512, 8, 96)])
+def test_mha_strided_and_mean(B, lq, lk, heads, dh):
+    """mmr_mha == softmax(q k^T / sqrt(dh)) v on strided row views of packed projections; mean over
+    the query rows; ragged lq / lk (padded to 32 in-kernel)."""
+    g = torch.Generator().manual_seed(B * 1000 + lq + lk + dh)
+    E = heads * dh
+    qp = bf(torch.randn(B * lq, 3 * E, generator=g))          # q in cols [E, 2E) of a packed row
+    kvp = bf(torch.randn(B * lk, 2 * E + 16, generator=g))    # k | v | pad (row stride 2E + 16)
+    q, k, v = qp[:, E:2 * E], kvp[:, :E], kvp[:, E:2 * E]
+    hd = lambda t, L: t.float().reshape(B, L, heads, dh).transpose(1, 2)  # noqa: E731
+    ref = ((hd(q, lq) @ hd(k, lk).transpose(-1, -2)) / math.sqrt(dh)).softmax(-1) @ hd(v, lk)
+    ref = ref.transpose(1, 2).reshape(B * lq, E)
+    qd, kvd = qp.to(DEV), kvp.to(DEV)
+    out = torch.empty((B * lq, E), dtype=torch.bfloat16, device=DEV)
+    mean = torch.empty((B, E), dtype=torch.float32, device=DEV)
+    ops.mha(qd[:, E:2 * E], kvd[:, :E], kvd[:, E:2 * E], B, lq, lk, heads, dh, 1 / math.sqrt(dh), out=out,
+            mean_out=mean)
+    assert rel_err(out, ref) < 2e-2
+    assert rel_err(mean, ref.view(B, lq, E).mean(1)) < 2e-2
+    # mean-only launch gives the same mean
+    mean2 = torch.empty_like(mean)
+    ops.mha(qd[:, E:2 * E], kvd[:, :E], kvd[:, E:2 * E], B, lq, lk, heads, dh, 1 / math.sqrt(dh), mean_out=mean2)
+    if lq <= 128:  # single query chunk: deterministic LDS reduction
+        assert torch.equal(mean, mean2)
+    else:
+        assert rel_err(mean2, mean.cpu()) < 1e-5
+
+
+def test_linear_f32_strided_residual_inplace():
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(70, 200, generator=g)
+    w, b = torch.randn(96, 128, generator=g) * 0.1, torch.randn(96, generator=g)
+    r = torch.randn(70, 96, generator=g)
+    xd = x.to(DEV)
+    y = r.to(DEV).clone()
+    ops.linear_f32(xd[:, 16:144], w.to(DEV), b.to(DEV), residual=y, out=y)     # strided x, in-place residual
+    ref = x[:, 16:144] @ w.T + b + r
+    assert rel_err(y, ref) < 1e-5
+    y2 = ops.linear_f32(xd[:, 16:144], w.to(DEV), b.to(DEV), act=1)
+    assert rel_err(y2, F.gelu(x[:, 16:144] @ w.T + b)) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_ln_rows(dtype):
+    g = torch.Generator().manual_seed(7)
+    x, r = torch.randn(37, 768, generator=g).to(dtype), torch.randn(37, 768, generator=g).to(dtype)
+    ga, be = 1 + 0.1 * torch.randn(768, generator=g), 0.1 * torch.randn(768, generator=g)
+    post = torch.randn(37, 768, generator=g)
+    a, ps = torch.tensor([0.7]), torch.tensor([1.3])
+    ref = F.layer_norm(a * x.float() + r.float(), (768,), ga, be, 1e-5)
+    y = ops.ln_rows(x.to(DEV), ga.to(DEV), be.to(DEV), 1e-5, alpha=a.to(DEV), residual=r.to(DEV))
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel_err(y, ref) < tol
+    if dtype == torch.float32:
+        y = ops.ln_rows(x.to(DEV), ga.to(DEV), be.to(DEV), 1e-5, post=post.to(DEV), post_scale=ps.to(DEV))
+        assert rel_err(y, F.layer_norm(x, (768,), ga, be, 1e-5) + 1.3 * post) < 1e-5
+
+
+def test_add_pos_and_assemble():
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(3, 49, 96, generator=g)
+    pos = torch.randn(512, 96, generator=g)
+    y = ops.add_pos(x.to(DEV), pos.to(DEV), 49)
+    assert rel_err(y, x + pos[:49]) < 1e-2
+    x1, x2 = torch.randn(3, 64, generator=g), torch.randn(3, 64, generator=g)
+    pf = bf(torch.randn(3 * 5, 64, generator=g))
+    pe = torch.randn(10, 64, generator=g)
+    s = ops.assemble_seq(x1.to(DEV), pf.to(DEV), x2.to(DEV), pe.to(DEV), 5)
+    ref = torch.cat([x1[:, None], pf.float().view(3, 5, 64), x2[:, None]], 1) + pe[:7]
+    assert rel_err(s, ref) < 1e-2
+
+
+def _check_emb(got, ref, tol=4e-2):
+    got = got.detach().float().cpu()
+    ref = ref.detach().float().cpu()
+    cos = F.cosine_similarity(got, ref, dim=1)
+    assert cos.min().item() >= 0.999, cos
+    assert rel_err(got, ref) <= tol
+
+
+@pytest.mark.parametrize("text", [True, False])
+def test_fusion_stack_vs_oracle_on_backbone_features(text):
+    """FusionStack on fixed backbone features (B=3, L=128, joint 768, 8 heads, 3 layers) vs the
+    oracle restatement; text=False exercises the learnable default text token (fusion.py:404-407)."""
+    g = torch.Generator().manual_seed(11)
+    B, Lt, Np, C, D = 3, 128, 49, 768, 768
+    hs = init_head_state(C, C, D, 21)
+    hs.update(init_fusion_state(C, C, D, 8, 3, 22))
+    G = torch.randn(B, C, generator=g)
+    P = torch.randn(B, Np, C, generator=g)
+    T = bf(torch.randn(B, Lt, C, generator=g)).float() if text else None
+    with torch.no_grad():
+        ref = otw.multimodal(G, P, T, hs, num_heads=8)
+    from mmr_amd.fusion import FusionStack
+    fs = FusionStack(hs, 8, device=DEV)
+    got = fs.forward(G.to(DEV), P.to(DEV), T.to(DEV) if text else None)
+    _check_emb(got, ref)
+
+
+def test_full_size_multimodal_vs_oracle():
+    """Swin-T + BERT-base + 5-layer multimodal head (joint 768, 8 heads) end to end, B=2."""
+    ssd, bsd = init_swin_state(SWIN_T, 5), init_bert_state(BERT_BASE, 6)
+    hs = init_head_state(768, 768, 768, 7)
+    hs.update(init_fusion_state(768, 768, 768, 8, 5, 8))
+    bb = Backbones(swin_state=ssd, bert_state=bsd, device=DEV)
+    m = MultiModalRetrievalModel(joint_dim=768, num_heads=8, model_type="multimodal", backbones=bb,
+                                 head_state=hs, device=DEV)
+    img = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(2, 9)))
+    ids, mask = (torch.from_numpy(a) for a in synthetic.reports(2, 128, 10))
+    o = m(img.to(DEV), ids.to(DEV), mask.to(DEV))
+    q = m.query_embeddings(img.to(DEV), ids.to(DEV), mask.to(DEV))
+    with torch.no_grad():
+        (rg, rp), rt = otw.backbones_forward(img, ids, mask, ssd, bsd, SWIN_T, BERT_BASE)
+        ref = otw.heads(rg, rp, rt, hs, "multimodal", mm_cfg={"num_heads": 8})["joint_emb"]
+    _check_emb(o["joint_emb"], ref)
+    assert torch.equal(o["joint_emb"], q)

@@ -122,6 +122,17 @@ def test_oracle_towers_match_reference():
             np.testing.assert_allclose(o["joint_emb"].numpy(), f[f"{mt}_joint_emb"], atol=1e-5, rtol=1e-5)
             np.testing.assert_allclose(o["img_emb"].numpy(), f[f"{mt}_img_emb"], atol=1e-5, rtol=1e-5)
             np.testing.assert_allclose(o["txt_emb"].numpy(), f[f"{mt}_txt_emb"], atol=1e-5, rtol=1e-5)
+        # multimodal: 2 fusion layers x CrossModalFusion + combiner (model.py:375-459)
+        o = otw.heads(torch.from_numpy(f["img_global"]), torch.from_numpy(f["img_patches"]),
+                      torch.from_numpy(f["txt_feats"]), head, "multimodal", mm_cfg={"num_heads": cfg["num_heads"]})
+        np.testing.assert_allclose(o["joint_emb"].numpy(), f["multimodal_joint_emb"], atol=1e-5, rtol=1e-5)
+
+
+def test_oracle_multimodal_cls_only_raises_like_reference():
+    f, cfg, swin, bert, head, image, ids, mask = mini_towers()
+    with pytest.raises(ValueError):
+        otw.multimodal(torch.from_numpy(f["img_global"]), torch.from_numpy(f["img_patches"]),
+                       torch.from_numpy(f["txt_feats"]), head, num_heads=4, use_cls_only=True)
 
 
 def test_package_imports_without_gpu():

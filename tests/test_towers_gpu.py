@@ -257,9 +257,9 @@ def test_mini_towers_match_reference_golden():
     _check_emb(g, torch.from_numpy(f["img_global"]))
     _check_emb(p, torch.from_numpy(f["img_patches"]))
     _check_emb(t, torch.from_numpy(f["txt_feats"]))
-    for mt in ("text", "image"):
-        m = MultiModalRetrievalModel(joint_dim=cfg["joint_dim"], model_type=mt, backbones=bb, head_state=head,
-                                     device=DEV)
+    for mt in ("text", "image", "multimodal"):
+        m = MultiModalRetrievalModel(joint_dim=cfg["joint_dim"], num_heads=cfg["num_heads"], model_type=mt,
+                                     backbones=bb, head_state=head, device=DEV)
         o = m(image, ids, mask)
         _check_emb(o["joint_emb"], torch.from_numpy(f[f"{mt}_joint_emb"]))
         _check_emb(o["img_emb"], torch.from_numpy(f[f"{mt}_img_emb"]))
