@@ -582,49 +582,80 @@ __global__ __launch_bounds__(256) void mean_tokens(const uint16_t* __restrict__ 
 }
 
 // ------------------------------------------------------------------ small f32 linear (heads)
-// Y[b][o] = act(sum_i X[b][i] W[o][i] + bias[o]) in exact f32 (v_mfma_f32_32x32x2_f32); one wave
-// per 32x32 output tile, operands straight to VGPRs as float4 with the k-permutation of
-// knn_scores (lane half h owns k = kb+8h..kb+8h+7).  cin % 16 == 0, cout % 32 == 0.  Rows are
-// strided (ldx, ldy; ldx % 4 == 0); optional residual R (ldr) added after the activation.
-__global__ __launch_bounds__(256) void linear_f32(const float* __restrict__ X,
+// Y[b][o] = act(sum_i X[b][i] W[o][i] + bias[o]) in exact f32 (v_mfma_f32_32x32x2_f32) for the
+// per-query vectors (a few hundred rows): pure latency, so one 32x32 output tile per 512-thread
+// block with K split over the 8 waves, each wave issuing the loads of LF_CH 16-wide k-steps before
+// their MFMAs (one memory round trip per chunk instead of one per step), partial tiles summed in
+// LDS in a fixed order.  Operands straight to VGPRs as float4 with the k-permutation of knn_scores
+// (lane half h owns k = kb+8h..kb+8h+7).  cin % 16 == 0, cout % 32 == 0.  Rows are strided (ldx,
+// ldy; ldx % 4 == 0); optional residual R (ldr, may alias Y) added after the activation.
+constexpr int LF_WAVES = 8;
+constexpr int LF_CH = 6;
+
+__global__ __launch_bounds__(512) void linear_f32(const float* __restrict__ X,
                                                   const float* __restrict__ W,
                                                   const float* __restrict__ bias,
                                                   float* Y, int nb, int cin, int cout,
-                                                  int act, int64_t ldx = -1, int64_t ldy = -1,
-                                                  const float* R = nullptr, int64_t ldr = 0) {
-  if (ldx < 0) ldx = cin;
-  if (ldy < 0) ldy = cout;
+                                                  int act, int64_t ldx, int64_t ldy,
+                                                  const float* R, int64_t ldr) {
+  __shared__ float part[LF_WAVES][1024];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int tiles_o = cout / 32;
-  const int t = blockIdx.x * 4 + wave;
-  const int tb = t / tiles_o, to = t % tiles_o;
-  if (tb * 32 >= nb) return;
+  const int tb = blockIdx.x / tiles_o, to = blockIdx.x % tiles_o;
   const int r = lane & 31, h = lane >> 5;
   const int b = tb * 32 + r;
   const bool bok = b < nb;
   const float* xa = X + (int64_t)(bok ? b : 0) * ldx + 8 * h;
   const float* wb = W + (int64_t)(to * 32 + r) * cin + 8 * h;
+  const int nsteps = cin / 16;
+  const int per = (nsteps + LF_WAVES - 1) / LF_WAVES;
+  const int s0 = wave * per, s1 = min(nsteps, s0 + per);
   f32x16 acc = {0};
-  for (int kb = 0; kb < cin; kb += 16) {
-    float4 a0 = *(const float4*)(xa + kb), a1 = *(const float4*)(xa + kb + 4);
-    const float4 b0 = *(const float4*)(wb + kb), b1 = *(const float4*)(wb + kb + 4);
-    if (!bok) a0 = a1 = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-    const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+  for (int sc = s0; sc < s1; sc += LF_CH) {
+    float4 a[LF_CH][2], w[LF_CH][2];
 #pragma unroll
-    for (int s8 = 0; s8 < 8; ++s8) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s8], bv[s8], acc, 0, 0, 0);
+    for (int c = 0; c < LF_CH; ++c) {
+      const int kb = (sc + c) * 16;
+      if (sc + c < s1) {
+        a[c][0] = *(const float4*)(xa + kb);
+        a[c][1] = *(const float4*)(xa + kb + 4);
+        w[c][0] = *(const float4*)(wb + kb);
+        w[c][1] = *(const float4*)(wb + kb + 4);
+      } else {
+        a[c][0] = a[c][1] = w[c][0] = w[c][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      if (!bok) a[c][0] = a[c][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int c = 0; c < LF_CH; ++c) {
+      const float av[8] = {a[c][0].x, a[c][0].y, a[c][0].z, a[c][0].w, a[c][1].x, a[c][1].y, a[c][1].z, a[c][1].w};
+      const float bv[8] = {w[c][0].x, w[c][0].y, w[c][0].z, w[c][0].w, w[c][1].x, w[c][1].y, w[c][1].z, w[c][1].w};
+#pragma unroll
+      for (int s8 = 0; s8 < 8; ++s8) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s8], bv[s8], acc, 0, 0, 0);
+    }
   }
-  const int o = to * 32 + r;
-  const float bo = bias ? bias[o] : 0.f;
 #pragma unroll
-  for (int rg = 0; rg < 16; ++rg) {
-    const int bb = tb * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * h;
+  for (int rg = 0; rg < 16; ++rg) part[wave][lane * 16 + rg] = acc[rg];
+  __syncthreads();
+  for (int e = threadIdx.x; e < 1024; e += blockDim.x) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < LF_WAVES; ++w) v += part[w][e];
+    const int ln = e >> 4, rg = e & 15;
+    const int bb = tb * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * (ln >> 5);
+    const int o = to * 32 + (ln & 31);
     if (bb >= nb) continue;
-    float v = acc[rg] + bo;
+    v += bias ? bias[o] : 0.f;
     if (act == 1) v = mmr::gelu_erf(v);
     if (R) v += R[(int64_t)bb * ldr + o];
     Y[(int64_t)bb * ldy + o] = v;
   }
+}
+
+void launch_linear_f32(const float* x, const float* w, const float* b, float* y, int nb, int cin, int cout,
+                       int act, int64_t ldx, int64_t ldy, const float* r, int64_t ldr, hipStream_t st) {
+  const int64_t tiles = mmr::ceil_div(nb, 32) * (cout / 32);
+  linear_f32<<<dim3((unsigned)tiles), dim3(64 * LF_WAVES), 0, st>>>(x, w, b, y, nb, cin, cout, act, ldx, ldy, r, ldr);
 }
 
 __global__ __launch_bounds__(256) void l2_normalize_rows(float* __restrict__ y, int nb, int d) {
@@ -802,8 +833,7 @@ mmr_status mmr_proj_head(const float* x, const float* wp, const float* bp, const
   hipStream_t st = mmr::as_stream(stream);
   const dim3 blk(256);
   auto lin = [&](const float* xi, const float* w, const float* bb, float* yo, int ci, int co, int act) {
-    const int64_t tiles = mmr::ceil_div(b, 32) * (co / 32);
-    linear_f32<<<dim3((unsigned)mmr::ceil_div(tiles, 4)), blk, 0, st>>>(xi, w, bb, yo, b, ci, co, act);
+    launch_linear_f32(xi, w, bb, yo, b, ci, co, act, ci, co, nullptr, 0, st);
   };
   if (w1 == nullptr) {
     lin(x, wp, bp, y, cin, d, 0);
@@ -837,9 +867,7 @@ mmr_status mmr_linear_f32(const float* x, int64_t ldx, const float* w, const flo
   MMR_REQUIRE(((uintptr_t)x & 15u) == 0 && ((uintptr_t)w & 15u) == 0, "mmr_linear_f32: x / w must be 16-B aligned");
   MMR_REQUIRE(act == 0 || act == 1, "mmr_linear_f32: act=%d", act);
   if (b == 0) return MMR_OK;
-  const int64_t tiles = mmr::ceil_div(b, 32) * (cout / 32);
-  linear_f32<<<dim3((unsigned)mmr::ceil_div(tiles, 4)), 256, 0, mmr::as_stream(stream)>>>(
-      x, w, bias, y, b, cin, cout, act, ldx, ldy, residual, ldr);
+  launch_linear_f32(x, w, bias, y, b, cin, cout, act, ldx, ldy, residual, ldr, mmr::as_stream(stream));
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }
