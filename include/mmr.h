@@ -73,6 +73,29 @@ mmr_status mmr_index_search(mmr_index* index, const float* q, int64_t nq, int32_
 /* out_score64 (q, k) f64 (may be NULL): the exact scores the ranking used; the shard merge ranks
  * on these so a row-sharded search returns exactly the single-device result. */
 
+/* DLS link graph (DLSRetrievalEngine._build_link_graph, src/Retrieval/retrieval.py:121-138): the
+ * self-join of gallery rows [row0, row0+nrows) against the whole index — per row its neighbours
+ * in exact-cosine order (score desc, index asc), the row itself excluded (the reference's diagonal
+ * -1), score >= threshold, at most max_links.  out_nbr (nrows, max_links) int64 LOCAL row indices,
+ * -1 padded; out_cnt (nrows,) int32.  Device buffers, asynchronous on `stream`. */
+mmr_status mmr_index_link_graph(mmr_index* index, double threshold, int32_t max_links, int64_t row0,
+                                 int64_t nrows, int64_t* out_nbr, int32_t* out_cnt, void* stream);
+
+/* KG / label reranker fused after the top-K (Reranker.rerank, src/Retrieval/reranker.py:240-333):
+ * per query the kc candidates cand (nq, kc) int64 (global indices into this index, -1 = empty,
+ * kc <= 64) are re-scored with alpha*minmax(cos(q_emb, row)) + beta*minmax(Jaccard(label sets)) +
+ * gamma*minmax(cos(kg vectors)) — cosines in f64, 0 for a zero norm — and the first topk written
+ * in final-score order (equal finals: later candidate first, as np.argsort(final)[::-1]).
+ * q_emb (nq, d) f32; q_labels (nq) / g_labels (n) uint64 label bitsets; q_kg (nq, dk) /
+ * g_kg (n, dk) f32 record KG vectors (g_* in local row order).  Outputs (nq, topk): out_idx int64
+ * (-1 beyond the valid candidates), optional out_final / out_emb / out_lab / out_kg f64 (the
+ * scaled components, like the reference's result tuples). */
+mmr_status mmr_index_rerank(const mmr_index* index, const float* q_emb, int64_t nq, const int64_t* cand,
+                            int32_t kc, const uint64_t* q_labels, const uint64_t* g_labels, const float* q_kg,
+                            const float* g_kg, int32_t dk, double alpha, double beta, double gamma,
+                            int32_t topk, int64_t* out_idx, double* out_final, double* out_emb,
+                            double* out_lab, double* out_kg, void* stream);
+
 /* Merge n_lists per-shard lists laid out [n_lists][nq][k_in] (f64 scores, int64 idx; empty slots
  * idx -1) into the global top-k_out per query: score desc, then index asc.  out_score f32 (may be
  * NULL), out_score64 f64 (may be NULL). */

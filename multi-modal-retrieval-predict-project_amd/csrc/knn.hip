@@ -544,6 +544,125 @@ __global__ __launch_bounds__(256) void knn_merge(const double* __restrict__ scor
   }
 }
 
+// ------------------------------------------------------------------ DLS link-graph filter
+// Row i of a self-join (queries = gallery rows r0..r0+nq): drop i itself (the reference sets the
+// diagonal to -1), keep neighbours with exact score >= threshold in rank order (score desc, index
+// asc), first max_links (DLSRetrievalEngine._build_link_graph, retrieval.py:121-138).
+__global__ __launch_bounds__(256) void knn_link_filter(const int64_t* __restrict__ idx,
+                                                       const double* __restrict__ s64, int k,
+                                                       int64_t nq, int64_t r0, int64_t idx_base,
+                                                       double threshold, int max_links,
+                                                       int64_t* __restrict__ nbr,
+                                                       int32_t* __restrict__ cnt) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= nq) return;
+  const int64_t self = r0 + q;
+  int c = 0;
+  for (int j = 0; j < k && c < max_links; ++j) {
+    const int64_t g = idx[q * k + j];
+    if (g < 0) break;
+    const int64_t loc = g - idx_base;
+    if (loc == self) continue;
+    if (!(s64[q * k + j] >= threshold)) break;  // ranked: nothing later passes either
+    nbr[q * max_links + c++] = loc;
+  }
+  for (int j = c; j < max_links; ++j) nbr[q * max_links + j] = -1;
+  cnt[q] = c;
+}
+
+// ------------------------------------------------------------------ KG / label reranker
+// Reranker.rerank (src/Retrieval/reranker.py:240-333) fused after the top-K, one wave per query,
+// one candidate per lane (kc <= 64): embedding cosine (exact f64 of the raw f32 rows; 0 for a
+// zero norm, safe_cos :134-142), label Jaccard on 64-bit label sets (:144-149), KG-vector cosine,
+// each min-max scaled over the valid candidates (:151-159, constant -> 0), final = a*e + b*l + g*k,
+// ranked by final desc with equal finals -> later candidate first (the reference's
+// np.argsort(final)[::-1] over a short, insertion-sorted list), first topk written.
+__device__ __forceinline__ double wave_min_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_max_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ double minmax_lane(double x, bool valid) {
+  const double lo = wave_min_d(valid ? x : INFINITY), hi = wave_max_d(valid ? x : -INFINITY);
+  return (hi - lo == 0.0) ? 0.0 : (x - lo) / (hi - lo);
+}
+
+__global__ __launch_bounds__(64) void knn_rerank(
+    const float* __restrict__ qe, int d, const float* __restrict__ gal, int Dp,
+    const double* __restrict__ gnorm64, int64_t n, int64_t idx_base, const int64_t* __restrict__ cand,
+    int kc, const uint64_t* __restrict__ qlab, const uint64_t* __restrict__ glab,
+    const float* __restrict__ qkg, const float* __restrict__ gkg, int dk, double wa, double wb,
+    double wg, int topk, int64_t* __restrict__ out_idx, double* __restrict__ out_final,
+    double* __restrict__ out_emb, double* __restrict__ out_lab, double* __restrict__ out_kg) {
+  const int64_t qi = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int64_t* cq = cand + qi * kc;
+  const float* qr = qe + qi * (int64_t)d;
+  const float* qk = qkg + qi * (int64_t)dk;
+  double qq = 0.0, kk = 0.0;
+  for (int t = lane; t < d; t += 64) qq += (double)qr[t] * (double)qr[t];
+  for (int t = lane; t < dk; t += 64) kk += (double)qk[t] * (double)qk[t];
+  const double qn = sqrt(mmr::wave_sum(qq)), qkn = sqrt(mmr::wave_sum(kk));
+  double e = 0.0, kgs = 0.0;
+  int64_t my = -1;
+  for (int c = 0; c < kc; ++c) {  // wave-cooperative dot products, candidate c lands on lane c
+    const int64_t g = cq[c] - idx_base;
+    const bool ok = cq[c] >= 0 && g >= 0 && g < n;
+    double de = 0.0, dkg = 0.0, gk = 0.0;
+    if (ok) {
+      const float* gr = gal + g * Dp;
+      const float* gq = gkg + g * (int64_t)dk;
+      for (int t = lane; t < d; t += 64) de += (double)qr[t] * (double)gr[t];
+      for (int t = lane; t < dk; t += 64) {
+        dkg += (double)qk[t] * (double)gq[t];
+        gk += (double)gq[t] * (double)gq[t];
+      }
+    }
+    de = mmr::wave_sum(de);
+    dkg = mmr::wave_sum(dkg);
+    gk = mmr::wave_sum(gk);
+    if (lane == c && ok) {
+      my = g;
+      const double gn = gnorm64[g];
+      e = (qn > 0.0 && gn > 0.0) ? de / (qn * gn) : 0.0;
+      const double gkn = sqrt(gk);
+      kgs = (qkn > 0.0 && gkn > 0.0) ? dkg / (qkn * gkn) : 0.0;
+    }
+  }
+  const bool valid = lane < kc && my >= 0;
+  double lab = 0.0;
+  if (valid) {
+    const uint64_t a = qlab[qi], b = glab[my];
+    const int u = __popcll(a | b);
+    lab = u == 0 ? 0.0 : (double)__popcll(a & b) / (double)u;
+  }
+  const double en = minmax_lane(e, valid), ln = minmax_lane(lab, valid), kn = minmax_lane(kgs, valid);
+  const double f = wa * en + wb * ln + wg * kn;
+  int rank = 0;
+  for (int j = 0; j < 64; ++j) {
+    const double fj = __shfl(f, j, 64);
+    const bool vj = __shfl((int)valid, j, 64) != 0;
+    rank += vj && (fj > f || (fj == f && j > lane));
+  }
+  if (valid && rank < topk) {
+    const int64_t o = qi * topk + rank;
+    out_idx[o] = my + idx_base;
+    if (out_final) out_final[o] = f;
+    if (out_emb) out_emb[o] = en;
+    if (out_lab) out_lab[o] = ln;
+    if (out_kg) out_kg[o] = kn;
+  }
+  int nvalid = 0;
+  for (int j = 0; j < 64; ++j) nvalid += __shfl((int)valid, j, 64);
+  for (int r = nvalid + lane; r < topk; r += 64) out_idx[qi * topk + r] = -1;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ index object
@@ -768,6 +887,65 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
         out_score64 ? out_score64 + c0 * k : nullptr, out_status ? out_status + c0 : nullptr);
     MMR_LAUNCH_CHECK();
   }
+  return MMR_OK;
+}
+
+mmr_status mmr_index_link_graph(mmr_index* ix, double threshold, int32_t max_links, int64_t row0,
+                                 int64_t nrows, int64_t* out_nbr, int32_t* out_cnt, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(ix != nullptr, "mmr_index_link_graph: index is NULL");
+  MMR_REQUIRE(max_links >= 1 && max_links < kMaxK, "mmr_index_link_graph: max_links=%d outside [1, %d)", max_links, kMaxK);
+  MMR_REQUIRE(row0 >= 0 && nrows >= 0 && row0 + nrows <= ix->n, "mmr_index_link_graph: rows [%lld, +%lld) outside the gallery",
+              (long long)row0, (long long)nrows);
+  if (nrows == 0) return MMR_OK;
+  MMR_REQUIRE(out_nbr && out_cnt, "mmr_index_link_graph: NULL output");
+  DeviceGuard g(ix->device);
+  hipStream_t st = mmr::as_stream(stream);
+  const int k = max_links + 1;  // + the row itself
+  int64_t* ti = nullptr;
+  double* ts = nullptr;
+  float* qc = nullptr;
+  MMR_CHECK_HIP(hipMallocAsync((void**)&ti, sizeof(int64_t) * nrows * k, st));
+  MMR_CHECK_HIP(hipMallocAsync((void**)&ts, sizeof(double) * nrows * k, st));
+  const float* q = ix->gal + row0 * ix->Dp;  // padded rows double as queries when d == Dp
+  if (ix->d != ix->Dp) {
+    MMR_CHECK_HIP(hipMallocAsync((void**)&qc, sizeof(float) * nrows * ix->d, st));
+    MMR_CHECK_HIP(hipMemcpy2DAsync(qc, sizeof(float) * ix->d, q, sizeof(float) * ix->Dp, sizeof(float) * ix->d,
+                                   nrows, hipMemcpyDeviceToDevice, st));
+    q = qc;
+  }
+  mmr_status s = mmr_index_search(ix, q, nrows, k, ti, nullptr, ts, nullptr, stream);
+  if (s == MMR_OK) {
+    knn_link_filter<<<dim3((unsigned)ceil_div(nrows, 256)), dim3(256), 0, st>>>(
+        ti, ts, k, nrows, row0, ix->idx_base, threshold, max_links, out_nbr, out_cnt);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      mmr::set_error("knn_link_filter launch failed: %s", hipGetErrorString(e));
+      s = MMR_ERR_HIP;
+    }
+  }
+  (void)hipFreeAsync(ti, st);
+  (void)hipFreeAsync(ts, st);
+  if (qc) (void)hipFreeAsync(qc, st);
+  return s;
+}
+
+mmr_status mmr_index_rerank(const mmr_index* ix, const float* q_emb, int64_t nq, const int64_t* cand,
+                            int32_t kc, const uint64_t* q_labels, const uint64_t* g_labels, const float* q_kg,
+                            const float* g_kg, int32_t dk, double alpha, double beta, double gamma,
+                            int32_t topk, int64_t* out_idx, double* out_final, double* out_emb,
+                            double* out_lab, double* out_kg, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(ix != nullptr, "mmr_index_rerank: index is NULL");
+  MMR_REQUIRE(kc >= 1 && kc <= 64 && topk >= 1 && topk <= kc && dk >= 1 && nq >= 0,
+              "mmr_index_rerank: kc=%d (1..64), topk=%d (1..kc), dk=%d", kc, topk, dk);
+  if (nq == 0) return MMR_OK;
+  MMR_REQUIRE(q_emb && cand && q_labels && g_labels && q_kg && g_kg && out_idx, "mmr_index_rerank: NULL pointer");
+  DeviceGuard g(ix->device);
+  knn_rerank<<<dim3((unsigned)nq), dim3(64), 0, mmr::as_stream(stream)>>>(
+      q_emb, ix->d, ix->gal, ix->Dp, ix->norm64, ix->n, ix->idx_base, cand, kc, q_labels, g_labels, q_kg,
+      g_kg, dk, alpha, beta, gamma, topk, out_idx, out_final, out_emb, out_lab, out_kg);
+  MMR_LAUNCH_CHECK();
   return MMR_OK;
 }
 

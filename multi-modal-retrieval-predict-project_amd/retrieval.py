@@ -4,11 +4,10 @@ RetrievalEngine            retrieval.py:18-50   (.npy f32 gallery + ids.json, id
 MI355XRetrievalEngine      exact brute-force cosine top-K on the GPU (libmmr, include/mmr.h) with
                            the reference's exact-path semantics (retrieval_overlap.py:84-90):
                            cosine of the raw rows, descending; ties -> lower gallery index.
+DLSRetrievalEngine         retrieval.py:53-271: link graph = exact GPU self-join (SURVEY.md §8f row
+                           2); the approximate random-seeded greedy walk (3.75 % recall@10 vs exact in
+                           the survey probe, §8a-a11) stays the reference's host algorithm.
 make_retrieval_engine      retrieval.py:273-304  (string switch; unknown method -> ValueError)
-
-The reference's default engine, DLS (retrieval.py:53-271), is an approximate random-seeded graph
-walk (3.75 % recall@10 vs exact in the survey probe) and is out of scope:
-method="dls" raises with a pointer to the exact engine.
 """
 import abc
 import ctypes
@@ -109,6 +108,35 @@ class GalleryIndex:
             out.append(st)
         return tuple(out)
 
+    def link_graph(self, threshold: float, max_links: int, batch: int = 8192, stream_dev=None):
+        """DLS link graph of this shard (retrieval.py:121-138) on the device: (nbr (n, max_links)
+        int64 local indices, -1 padded; cnt (n,) int32) as device tensors."""
+        dev = torch.device(f"cuda:{self.device}")
+        nbr = torch.empty((self.n, max_links), dtype=torch.int64, device=dev)
+        cnt = torch.empty((self.n,), dtype=torch.int32, device=dev)
+        for r0 in range(0, self.n, batch):
+            nr = min(batch, self.n - r0)
+            _lib.check(_lib.lib().mmr_index_link_graph(self._h, float(threshold), int(max_links), r0, nr,
+                                                       _lib.ptr(nbr[r0:]), _lib.ptr(cnt[r0:]), _lib.stream_ptr(dev)),
+                       "mmr_index_link_graph")
+        return nbr, cnt
+
+    def rerank(self, q_emb, cand, q_labels, g_labels, q_kg, g_kg, topk, alpha=0.6, beta=0.25, gamma=0.15,
+               want_components=True):
+        """Fused KG / label rerank of device top-K candidates (mmr_index_rerank).  Returns
+        (idx (nq, topk) int64, final, emb_n, lab_n, kg_n (nq, topk) f64 or None)."""
+        q_emb = q_emb.to(torch.float32).contiguous()
+        nq, kc = cand.shape
+        dev = cand.device
+        out_i = torch.empty((nq, topk), dtype=torch.int64, device=dev)
+        outs = [torch.empty((nq, topk), dtype=torch.float64, device=dev) if want_components else None
+                for _ in range(4)]
+        _lib.check(_lib.lib().mmr_index_rerank(
+            self._h, _lib.ptr(q_emb), nq, _lib.ptr(cand.contiguous()), kc, _lib.ptr(q_labels), _lib.ptr(g_labels),
+            _lib.ptr(q_kg), _lib.ptr(g_kg), q_kg.shape[1], float(alpha), float(beta), float(gamma), int(topk),
+            _lib.ptr(out_i), *(_lib.ptr(o) for o in outs), _lib.stream_ptr(dev)), "mmr_index_rerank")
+        return (out_i, *outs)
+
     def close(self):
         h, self._h = getattr(self, "_h", None), None
         if h:
@@ -187,9 +215,114 @@ class MI355XRetrievalEngine(RetrievalEngine):
         self.index.close()
 
 
+class DLSRetrievalEngine(MI355XRetrievalEngine):
+    """DenseLinkSearch (retrieval.py:53-271).  The O(N^2) part — the link graph of
+    _build_link_graph (retrieval.py:121-138) — is an exact self-join on the GPU
+    (mmr_index_link_graph: the row itself excluded, score >= link_threshold, first max_links by
+    score desc / index asc).  The query-time greedy walk (retrieval.py:140-271) is the reference's
+    sequential, approximate host algorithm (random seeds, a (-sim, idx) heap, the visited set) and
+    runs here exactly as there; exact retrieval is MI355XRetrievalEngine.search.
+    The graph cache is an .npz (offsets + flat neighbours + dim), never a pickle."""
+
+    def __init__(self, features_path: Optional[str] = None, ids_path: Optional[str] = None,
+                 link_threshold: float = 0.5, max_links: int = 10, fdb_path: Optional[str] = None,
+                 name: Optional[str] = None, device=None, embs=None, ids=None, **_ignored):
+        super().__init__(features_path, ids_path, device=device, embs=embs, ids=ids)
+        self.fdb_path = None
+        if fdb_path or name:
+            p = str(fdb_path or name)
+            self.fdb_path = p[:-4] + ".npz" if p.endswith(".pkl") else p
+        graph = self._load_cache()
+        if graph is None:
+            graph = self._build_link_graph(link_threshold, max_links)
+            self._save_cache(graph)
+        self.link_graph = graph
+
+    def _load_cache(self):
+        import os
+        if not self.fdb_path or not os.path.exists(self.fdb_path):
+            return None
+        try:
+            f = np.load(self.fdb_path, allow_pickle=False)
+            off, flat, dim = f["offsets"], f["flat"], int(f["dim"])
+        except (OSError, KeyError, ValueError):
+            return None
+        if len(off) - 1 != self.embs.shape[0] or dim != self.embs.shape[1]:
+            return None  # shape mismatch -> rebuild (retrieval.py:102-108)
+        return [flat[off[i]:off[i + 1]].tolist() for i in range(len(off) - 1)]
+
+    def _save_cache(self, graph):
+        if not self.fdb_path:
+            return
+        off = np.cumsum([0] + [len(x) for x in graph]).astype(np.int64)
+        flat = np.array([j for x in graph for j in x], np.int64)
+        np.savez(self.fdb_path, offsets=off, flat=flat, dim=np.int64(self.embs.shape[1]))
+
+    def _build_link_graph(self, threshold: float, max_links: int) -> List[List[int]]:
+        nbr, cnt = self.index.link_graph(threshold, max_links)
+        nbr, cnt = nbr.cpu().numpy(), cnt.cpu().numpy()
+        return [nbr[i, :cnt[i]].tolist() for i in range(len(cnt))]
+
+    def retrieve(self, query_emb, K: int = 5, seed_size: int = 5, max_steps: int = 100,
+                 candidate_multiplier: int = 10, reranker=None, query_id=None, rerank_topk=None,
+                 seed=None, **kwargs):
+        import heapq
+        q = np.asarray(query_emb).astype("float32").reshape(-1)
+        N = self.embs.shape[0]
+        if len(self.link_graph) != N:
+            raise RuntimeError(f"Link graph size {len(self.link_graph)} != embeddings {N}. Rebuild or delete "
+                               f"your cache.")
+        if seed is not None:
+            np.random.seed(seed)
+        elif query_id is not None:
+            np.random.seed(abs(hash(str(query_id))) % (2 ** 32))  # process-salted, as in the reference
+        else:
+            np.random.seed(None)
+        seeds = np.random.choice(N, size=min(seed_size, N), replace=False).tolist()
+        visited = set(seeds)
+        q_norm = np.linalg.norm(q) + 1e-6
+
+        def sim(i):
+            e = self.embs[i]
+            return float(e @ q / (np.linalg.norm(e) * q_norm + 1e-12))
+        heap = []
+        for i in seeds:
+            heapq.heappush(heap, (-sim(i), i))
+        R = max(candidate_multiplier * K, seed_size)
+        steps = 0
+        while steps < max_steps and heap:
+            _, best = heapq.heappop(heap)
+            improved = False
+            for nbr in self.link_graph[best]:
+                if nbr < 0 or nbr >= N or nbr in visited:
+                    continue
+                visited.add(nbr)
+                heapq.heappush(heap, (-sim(nbr), nbr))
+                improved = True
+            if len(heap) > R:
+                heap = heapq.nsmallest(R, heap)
+                heapq.heapify(heap)
+            if not improved:
+                break
+            steps += 1
+        top = sorted([(-ns, i) for ns, i in heapq.nsmallest(K, heap)], reverse=True)
+        ids = [self.ids[i] for _, i in top]
+        scores = [s for s, _ in top]
+        if reranker is not None and query_id is not None:
+            cand_embs = self.get_embeddings_for_ids(ids)
+            lookup = {str(r): e for r, e in zip(ids, cand_embs)}
+            lookup[str(query_id)] = (self.embs[self.id2idx[str(query_id)]] if str(query_id) in self.id2idx else q)
+            out = reranker.rerank(query_id=query_id, candidate_ids=ids, candidate_embs=cand_embs,
+                                  candidate_emb_lookup=lookup, topk=rerank_topk or K)
+            ids = [t[0] for t in out]
+            scores = [t[1] for t in out]
+        return ids, scores
+
+
 def make_retrieval_engine(features_path: str, ids_path: str, method: str = "mi355x", **kwargs) -> RetrievalEngine:
     """Factory (retrieval.py:273-304). method: "mi355x" (aliases "exact", "brute") -> exact GPU
-    engine; "mi355x_sharded" -> row-sharded over torch.distributed ranks; "dls" -> not provided."""
+    engine; "mi355x_sharded" -> row-sharded over torch.distributed ranks; "dls" -> DenseLinkSearch
+    with the GPU-built link graph (link_threshold, max_links, fdb_path, name as in the reference)."""
     method = method.lower()
     if method in ("mi355x", "exact", "brute", "bruteforce"):
         return MI355XRetrievalEngine(features_path, ids_path, device=kwargs.get("device"),
@@ -198,6 +331,7 @@ def make_retrieval_engine(features_path: str, ids_path: str, method: str = "mi35
         from .parallel import ShardedRetrievalEngine
         return ShardedRetrievalEngine(features_path, ids_path, dtype=kwargs.get("dtype", "fp32"))
     if method == "dls":
-        raise ValueError("method 'dls' (approximate graph walk, retrieval.py:53-271) is not provided by "
-                         "mmr_amd; use method='mi355x' for exact brute-force retrieval")
+        return DLSRetrievalEngine(features_path, ids_path, link_threshold=kwargs.get("link_threshold", 0.5),
+                                  max_links=kwargs.get("max_links", 10), fdb_path=kwargs.get("fdb_path"),
+                                  name=kwargs.get("name"), device=kwargs.get("device"))
     raise ValueError(f"Unknown retrieval method: {method}")

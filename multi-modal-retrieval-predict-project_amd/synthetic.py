@@ -36,6 +36,37 @@ def labelled_gallery(n, d, seed=SEED, noise=0.6, centre_seed=SEED):
     return x.astype(np.float32), labels
 
 
+DLS_N, DLS_D, DLS_Q = 1200, 128, 24
+DLS_ZERO, DLS_DUP = [5, 77], (10, 20)      # zero rows; row DUP[1] := row DUP[0] (exact ties)
+LABEL_NAMES = [f"Finding {i}" if i % 5 == 0 else f"L{i}" for i in range(NUM_LABELS)]  # some with spaces
+
+
+def dls_gallery():
+    """Labelled gallery of the DLS / reranker fixture (tests/golden/dls_rerank.npz): two zero rows,
+    one exact duplicate pair, one record with no labels."""
+    G, gl = labelled_gallery(DLS_N, DLS_D, SEED + 11)
+    G[DLS_ZERO] = 0.0
+    G[DLS_DUP[1]] = G[DLS_DUP[0]]
+    gl[DLS_DUP[1]] = gl[DLS_DUP[0]]
+    gl[DLS_ZERO[0]] = 0
+    return G, gl
+
+
+def kg_node2id(n_records=DLS_N):
+    """Synthetic KG node table: report nodes for every 3rd record ("report:r<i>"), label nodes under
+    the key forms the reference's Reranker.get_record_kg_vec tries (reranker.py:190-207), one label
+    without a node."""
+    node2id = {}
+    for i in range(0, n_records, 3):
+        node2id[f"report:r{i}"] = len(node2id)
+    for j, name in enumerate(LABEL_NAMES):
+        if j == 42:
+            continue
+        key = [f"label:{name}", name, name.lower(), name.replace(" ", "_")][j % 4]
+        node2id[key] = len(node2id)
+    return node2id
+
+
 def image_u8(b, seed=SEED, hw=224):
     return np.random.default_rng(seed).integers(0, 256, size=(b, hw, hw), dtype=np.uint8)
 

@@ -333,9 +333,85 @@ def gen_towers(rm):
     print("wrote towers_mini.npz", sum(v.nbytes for v in rec.values()) / 1e6, "MB raw")
 
 
+DLS_N, DLS_Q, DLS_ZERO, DLS_DUP, LABEL_NAMES = odata.DLS_N, odata.DLS_Q, odata.DLS_ZERO, odata.DLS_DUP, odata.LABEL_NAMES
+
+
+def gen_dls_rerank(rm):
+    """DLSRetrievalEngine._build_link_graph (retrieval.py:121-138) at two (threshold, max_links)
+    settings, its greedy walk retrieve (retrieval.py:140-271, explicit seed), and Reranker.rerank
+    (reranker.py:240-333) over exact top-15 candidates, with synthetic KG / labels files."""
+    import pandas as pd
+    tmp = Path(tempfile.mkdtemp(prefix="mmr_golden_dls_"))
+    for n in list(sys.modules):
+        if n == "Retrieval" or n.startswith("Retrieval."):
+            del sys.modules[n]
+    _pkg("Retrieval", REF / "Retrieval")
+    rer = _load_file("Retrieval.reranker", REF / "Retrieval" / "reranker.py")
+    sys.modules["Retrieval"].reranker = rer
+    retr = _load_file("Retrieval.retrieval", REF / "Retrieval" / "retrieval.py")
+
+    G, gl = odata.dls_gallery()
+    ids = [f"r{i}" for i in range(DLS_N)]
+    np.save(tmp / "g.npy", G)
+    (tmp / "ids.json").write_text(json.dumps(ids))
+    rec = {"N": DLS_N, "D": odata.DLS_D, "seed": SEED + 11, "g_sum": np.float64(G.astype(np.float64).sum())}
+    for tag, thr, ml in (("t50_m10", 0.5, 10), ("t30_m8", 0.3, 8)):
+        eng = retr.make_retrieval_engine(str(tmp / "g.npy"), str(tmp / "ids.json"), method="dls",
+                                         link_threshold=thr, max_links=ml, fdb_path=str(tmp / f"{tag}.pkl"))
+        graph = eng.link_graph
+        rec[f"graph_{tag}_offsets"] = np.cumsum([0] + [len(x) for x in graph]).astype(np.int64)
+        rec[f"graph_{tag}_flat"] = np.array([j for x in graph for j in x], np.int64)
+        if tag == "t50_m10":
+            Qm, _ = odata.labelled_gallery(DLS_Q, odata.DLS_D, SEED + 12)
+            out_i, out_s = [], []
+            for qi in range(DLS_Q):
+                r_ids, r_sc = eng.retrieve(Qm[qi], K=5, seed=SEED + qi)
+                out_i.append([int(x[1:]) for x in r_ids] + [-1] * (5 - len(r_ids)))
+                out_s.append(list(r_sc) + [np.nan] * (5 - len(r_sc)))
+            rec["walk_idx"] = np.array(out_i, np.int64)
+            rec["walk_score"] = np.array(out_s, np.float64)
+
+    # reranker: synthetic KG dir + labels CSV
+    rng = np.random.default_rng(SEED + 13)
+    node2id = odata.kg_node2id(DLS_N)
+    nemb = rng.standard_normal((len(node2id), 300)).astype(np.float32)
+    kg = tmp / "kg"
+    kg.mkdir()
+    (kg / "node2id.json").write_text(json.dumps(node2id))
+    np.save(kg / "node_embeddings_best.npy", nemb)
+    df = pd.DataFrame(gl.astype(np.int64), columns=LABEL_NAMES)
+    df.insert(0, "id", ids)
+    df["report"] = ["text"] * DLS_N                       # non-numeric column (skipped)
+    df.to_csv(tmp / "labels.csv", index=False)
+    R = rer.Reranker(kg_dir=kg, labels_csv=tmp / "labels.csv")
+    from sklearn.metrics.pairwise import cosine_similarity
+    qrows = list(range(0, 4 * DLS_Q, 4)) + [DLS_ZERO[0], DLS_DUP[0]]
+    sim = cosine_similarity(G[qrows], G)
+    cand = np.stack([np.argsort(sim[i])[::-1][:15] for i in range(len(qrows))])
+    r_order, r_final, r_e, r_l, r_k = [], [], [], [], []
+    for qn, qi in enumerate(qrows):
+        cids = [ids[j] for j in cand[qn]]
+        lookup = {c: G[j] for c, j in zip(cids, cand[qn])}
+        lookup[ids[qi]] = G[qi]
+        out = R.rerank(ids[qi], cids, candidate_embs=G[cand[qn]], candidate_emb_lookup=lookup, topk=10)
+        r_order.append([int(t[0][1:]) for t in out])
+        r_final.append([t[1] for t in out])
+        r_e.append([t[2] for t in out])
+        r_l.append([t[3] for t in out])
+        r_k.append([t[4] for t in out])
+    rec.update(rr_queries=np.array(qrows, np.int64), rr_cand=cand.astype(np.int64),
+               rr_order=np.array(r_order, np.int64), rr_final=np.array(r_final), rr_emb=np.array(r_e),
+               rr_lab=np.array(r_l), rr_kg=np.array(r_k), kg_node_emb=nemb,
+               kg_node2id=np.frombuffer(json.dumps(node2id).encode(), np.uint8))
+    np.savez_compressed(OUT / "dls_rerank.npz", **rec)
+    print("wrote dls_rerank.npz")
+
+
 if __name__ == "__main__":
     rm = install_stubs()
-    which = sys.argv[1:] or ["knn", "ranking", "towers"]
+    which = sys.argv[1:] or ["knn", "ranking", "towers", "dls"]
+    if "dls" in which:
+        gen_dls_rerank(rm)
     if "knn" in which:
         gen_knn(rm)
     if "ranking" in which:
