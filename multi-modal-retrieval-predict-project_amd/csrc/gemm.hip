@@ -19,6 +19,10 @@
 //    residual add) as 16-byte row chunks — coalesced 128-B rows instead of 2-byte scatters.
 #include <stdlib.h>
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "common.h"
 
 namespace {
@@ -631,16 +635,19 @@ int cu_count() {
   return n;
 }
 
+// Kernel variants: (w4, cfg) pairs the launcher understands.  w4: 0 no persistent kernel, 1 the
+// 4-wave persistent kernel (256x256 or 256x192 tiles), 2 persistent 256x192 only; cfg: the 8-wave
+// tile when w4 does not apply (0 off -> 128x128; 1 256x256 KB64 x2; 2 256x256 KB32 x4;
+// 3 256x128 KB64 x3; 4 / 5 256x128 KB32 x2 / x3).
+constexpr int kVariants = 8;
+constexpr int kVarW4[kVariants] = {1, 2, 0, 0, 0, 0, 0, 0};
+constexpr int kVarCfg[kVariants] = {1, 1, 1, 2, 3, 4, 5, 0};
+
 template <int ACT, bool HB, bool HR>
 void launch(const uint16_t* x, const uint16_t* w, const float* b, const uint16_t* r, uint16_t* y,
-            int64_t m, int n, int k, hipStream_t st) {
+            int64_t m, int n, int k, hipStream_t st, int w4, int cfg) {
   // big tiles when the grid still fills >= ~2 rounds of 256 CUs and K is deep enough
-  // diagnostic override: 0 off; 1 256x256 KB64 x2; 2 256x256 KB32 x4; 3 256x128 KB64 x3
-  const char* cfge = getenv("MMR_GEMM_BIG");
-  const int cfg = cfge ? atoi(cfge) : 1;
   const int64_t t256 = mmr::ceil_div(m, 256);
-  const char* w4e = getenv("MMR_GEMM_W4");  // diagnostic: 0 off, 1 on (default), 2 256x192 only
-  const int w4 = w4e ? atoi(w4e) : 1;
   // the persistent 4-wave kernel for epilogues without a residual (its 1-wave-per-SIMD epilogue
   // cannot hide a residual tile's fetch); residual GEMMs keep the 8-wave kernels
   if (w4 && !HR && k >= 256 && k % 64 == 0 && m >= 4096) {
@@ -693,6 +700,68 @@ void launch(const uint16_t* x, const uint16_t* w, const float* b, const uint16_t
   gemm_bf16_tn<ACT, HB, HR><<<dim3(tm * tn), dim3(256), 0, st>>>(x, w, b, r, y, m, n, k, tm, tn);
 }
 
+// Per-shape variant choice: the first call with a (M, N, K, epilogue) key times every variant on
+// the caller's stream (HIP events, 3 launches each after one warm-up) and keeps the fastest for
+// the rest of the process — tile shape / persistence / pipeline depth trade off differently per
+// shape (K = 96 ... 3072, N = 96 ... 3072).  Skipped (default variant) while the stream is being
+// captured, when the output aliases an input, or with MMR_GEMM_TUNE=0.
+struct TuneKey {
+  int64_t m;
+  int n, k, act, hb, hr;
+  bool operator<(const TuneKey& o) const {
+    if (m != o.m) return m < o.m;
+    if (n != o.n) return n < o.n;
+    if (k != o.k) return k < o.k;
+    if (act != o.act) return act < o.act;
+    if (hb != o.hb) return hb < o.hb;
+    return hr < o.hr;
+  }
+};
+std::mutex g_tune_mu;
+std::map<std::pair<int, TuneKey>, int> g_tuned;  // (device, key) -> variant
+
+template <class Run>
+int tuned_variant(int64_t m, int n, int k, int act, bool hb, bool hr, const void* x, const void* r, const void* y,
+                  hipStream_t st, Run&& run) {
+  const char* te = getenv("MMR_GEMM_TUNE");
+  if (te && atoi(te) == 0) return 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  const auto key = std::make_pair(dev, TuneKey{m, n, k, act, (int)hb, (int)hr});
+  {
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    auto it = g_tuned.find(key);
+    if (it != g_tuned.end()) return it->second;
+  }
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return 0;
+  if (y == x || y == r) return 0;
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess) return 0;
+  if (hipEventCreate(&e1) != hipSuccess) {
+    (void)hipEventDestroy(e0);
+    return 0;
+  }
+  float best = 1e30f;
+  int bv = 0;
+  for (int v = 0; v < kVariants; ++v) {
+    run(kVarW4[v], kVarCfg[v]);
+    (void)hipEventRecord(e0, st);
+    for (int rep = 0; rep < 3; ++rep) run(kVarW4[v], kVarCfg[v]);
+    (void)hipEventRecord(e1, st);
+    float ms = 1e30f;
+    if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms < best) {
+      best = ms;
+      bv = v;
+    }
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  g_tuned[key] = bv;
+  return bv;
+}
+
 }  // namespace
 
 extern "C" mmr_status mmr_linear_bf16(const uint16_t* x, const uint16_t* w, const float* bias,
@@ -707,16 +776,28 @@ extern "C" mmr_status mmr_linear_bf16(const uint16_t* x, const uint16_t* w, cons
   if (m == 0) return MMR_OK;
   hipStream_t st = mmr::as_stream(stream);
   const bool hb = bias != nullptr, hr = residual != nullptr;
-  if (act == 0) {
-    if (hb && hr) launch<0, true, true>(x, w, bias, residual, y, m, n, k, st);
-    else if (hb) launch<0, true, false>(x, w, bias, residual, y, m, n, k, st);
-    else if (hr) launch<0, false, true>(x, w, bias, residual, y, m, n, k, st);
-    else launch<0, false, false>(x, w, bias, residual, y, m, n, k, st);
+  auto run = [&](int w4, int cfg) {
+    if (act == 0) {
+      if (hb && hr) launch<0, true, true>(x, w, bias, residual, y, m, n, k, st, w4, cfg);
+      else if (hb) launch<0, true, false>(x, w, bias, residual, y, m, n, k, st, w4, cfg);
+      else if (hr) launch<0, false, true>(x, w, bias, residual, y, m, n, k, st, w4, cfg);
+      else launch<0, false, false>(x, w, bias, residual, y, m, n, k, st, w4, cfg);
+    } else {
+      if (hb && hr) launch<1, true, true>(x, w, bias, residual, y, m, n, k, st, w4, cfg);
+      else if (hb) launch<1, true, false>(x, w, bias, residual, y, m, n, k, st, w4, cfg);
+      else if (hr) launch<1, false, true>(x, w, bias, residual, y, m, n, k, st, w4, cfg);
+      else launch<1, false, false>(x, w, bias, residual, y, m, n, k, st, w4, cfg);
+    }
+  };
+  // diagnostic overrides (MMR_GEMM_W4 / MMR_GEMM_BIG) pin one variant; otherwise the shape's tuned
+  // variant (tuned once per process on the first call with that shape)
+  const char* w4e = getenv("MMR_GEMM_W4");
+  const char* cfge = getenv("MMR_GEMM_BIG");
+  if (w4e || cfge) {
+    run(w4e ? atoi(w4e) : 1, cfge ? atoi(cfge) : 1);
   } else {
-    if (hb && hr) launch<1, true, true>(x, w, bias, residual, y, m, n, k, st);
-    else if (hb) launch<1, true, false>(x, w, bias, residual, y, m, n, k, st);
-    else if (hr) launch<1, false, true>(x, w, bias, residual, y, m, n, k, st);
-    else launch<1, false, false>(x, w, bias, residual, y, m, n, k, st);
+    const int v = tuned_variant(m, n, k, act, hb, hr, x, residual, y, st, run);
+    run(kVarW4[v], kVarCfg[v]);
   }
   MMR_LAUNCH_CHECK();
   return MMR_OK;

@@ -1,0 +1,41 @@
+"""Time one GEMM shape under the launcher's diagnostic variants (env MMR_GEMM_W4 / MMR_GEMM_BIG are
+read per launch) plus torch F.linear (hipBLASLt) for the plain GEMM.
+usage: python tools/gemm_variants.py M N K act [res]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from mmr_amd import ops  # noqa: E402
+
+
+def timeit(fn, iters=30):
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3
+
+
+M, N, K, act = (int(v) for v in sys.argv[1:5])
+res = len(sys.argv) > 5 and sys.argv[5] == "1"
+x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+b = torch.randn(N, device="cuda")
+r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16) if res else None
+fl = 2.0 * M * N * K
+out = [f"M={M} N={N} K={K} act={act} res={int(res)}"]
+for w4, big in (("1", "1"), ("2", "1"), ("0", "1"), ("0", "2"), ("0", "3"), ("0", "4"), ("0", "5"), ("0", "0")):
+    os.environ["MMR_GEMM_W4"], os.environ["MMR_GEMM_BIG"] = w4, big
+    t = timeit(lambda: ops.linear(x, w, b, r, act=act))
+    out.append(f"  w4={w4} big={big}: {t:8.1f} us  {fl / t / 1e6:7.0f} TF/s")
+t = timeit(lambda: F.linear(x, w, b.to(torch.bfloat16)))
+out.append(f"  hipBLASLt plain: {t:8.1f} us  {fl / t / 1e6:7.0f} TF/s")
+print("\n".join(out), flush=True)
