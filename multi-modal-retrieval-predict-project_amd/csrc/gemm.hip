@@ -427,7 +427,7 @@ constexpr int EPI4_PAD = 8;
 
 template <int NT>
 constexpr size_t w4_lds_bytes() {
-  return 2ull * (256 + 32 * NT) * 64 * 2 + 4ull * 16 * (16 * NT + EPI4_PAD) * 2;
+  return 2ull * (256 + 32 * NT) * 64 * 2 + 4ull * 16 * (16 * NT + EPI4_PAD) * 2 + 32ull * NT * 4;
 }
 
 template <int NT, int ACT, bool HAS_BIAS, bool HAS_RES>
@@ -445,7 +445,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_tn_w4(const uint16_t* __restric
   constexpr int CPR = 2 * NT;            // 16-B chunks per wave-tile row
   constexpr int CPL = 16 * CPR / 64;     // chunks per lane per 16-row group
   constexpr int NSTORE = MT * CPL;       // global stores per wave per tile
-  constexpr int NLOADS = HAS_BIAS ? NT : 0;  // bias, fetched during slice 0
+  constexpr int NLOADS = 0;  // the bias tile travels by LDS-DMA with slice 0 (no registers in the loop)
   static_assert(NSTORE <= 63 && NLOADS <= 63, "vmcnt range");
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];  // [2][TA + TB] + epilogue
 
@@ -503,6 +503,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_tn_w4(const uint16_t* __restric
   int sb = 0;            // stage holding the slice about to be consumed
   bool stores_out = false;  // previous tile's epilogue stores may still be in flight
   uint16_t* et = dsm + 2 * (TA + TB) + wave * 16 * ELD;
+  float* lbias = (float*)(dsm + 2 * (TA + TB) + 4 * 16 * ELD);  // [TBN] f32
 
   while (true) {
     const int64_t m0 = tile_m0(t);
@@ -516,9 +517,9 @@ __global__ __launch_bounds__(256) void gemm_bf16_tn_w4(const uint16_t* __restric
 #pragma unroll
       for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-    // bias is fetched during slice 0 (after its glds) and stays in registers across the main
-    // loop; the residual (accumulator layout) is fetched whole at the start of the epilogue
-    f32x4 bq[NT];
+    // the bias tile (TBN floats) lands in LDS by one LDS-DMA issued with slice 0, so no bias
+    // registers live across the main loop; the residual (accumulator layout) is fetched whole at
+    // the start of the epilogue
     uint2 rq[HAS_RES ? MT : 1][HAS_RES ? NT : 1];
     for (int kt = 0; kt < nk; ++kt) {
       // glds of this slice were issued before: the previous tile's stores (kt = 0) or this tile's
@@ -529,6 +530,8 @@ __global__ __launch_bounds__(256) void gemm_bf16_tn_w4(const uint16_t* __restric
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();  // slice landed for every wave; the other stage is free
       asm volatile("" ::: "memory");
+      if (HAS_BIAS && kt == 0 && wave == 0 && lane < TBN / 4)  // previous epilogue is past the barrier
+        __builtin_amdgcn_global_load_lds((const void*)(bias + n0 + lane * 4), (lds_ptr_t)lbias, 16, 0, 0);
       const bool last = kt + 1 == nk;
       if (last && has_next) setup(tnext);  // the last slice prefetches the next tile's first
       // after the very last slice the loads are issued anyway (branch-free), re-reading slice 0
@@ -562,13 +565,6 @@ __global__ __launch_bounds__(256) void gemm_bf16_tn_w4(const uint16_t* __restric
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j], a0[i], acc[i][j], 0, 0, 0);
       }
       kofs += KB * 2;
-      if (kt == 0) {
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-          const int n = n0 + wn * 16 * NT + j * 16 + fq * 4;
-          bq[j] = HAS_BIAS ? *(const f32x4*)(bias + n) : (f32x4){0.f, 0.f, 0.f, 0.f};
-        }
-      }
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -591,9 +587,10 @@ __global__ __launch_bounds__(256) void gemm_bf16_tn_w4(const uint16_t* __restric
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         float v[4];
+        const f32x4 bq = HAS_BIAS ? *(const f32x4*)(lbias + wn * 16 * NT + j * 16 + fq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int rg = 0; rg < 4; ++rg) {
-          v[rg] = acc[i][j][rg] + bq[j][rg];
+          v[rg] = acc[i][j][rg] + bq[rg];
           if (ACT == 1) v[rg] = mmr::gelu_fast(v[rg]);
         }
         if constexpr (HAS_RES) {

@@ -311,7 +311,144 @@ __global__ __launch_bounds__(256, 2) void knn_scores_x3(const uint16_t* __restri
   }
 }
 
+// Same GEMM, fused epilogue: instead of the (Qp x Np) score matrix, each lane keeps the max of its
+// 4 gallery rows {B + fr + 16j : j < 4} (B = the wave's 64-row block) per query — a "row group" —
+// and writes one float per (query, group): gmax[m][g], g = (B/64)*16 + fr, ldG = Np/4.  Rows >= n
+// (padding) are -inf.  4x fewer bytes than the scores and no extra VALU beyond 3 max per value.
+__global__ __launch_bounds__(256, 2) void knn_scores_x3_gmax(const uint16_t* __restrict__ qs,
+                                                              const uint16_t* __restrict__ gs,
+                                                              const float* __restrict__ inv_g,
+                                                              float* __restrict__ gmax, int Dp,
+                                                              int64_t ldG, int64_t n, int tiles_m,
+                                                              int tiles_n) {
+  constexpr int BK = 64, TILE = 128 * 64;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * TILE];
+  const int nwg = tiles_m * tiles_n;
+  const int orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int tn = wg / tiles_m, tm = wg % tiles_m;
+  const int64_t m0 = (int64_t)tm * 128, n0 = (int64_t)tn * 128;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int K3 = 3 * Dp;
+  const int prow_in = lane >> 3, pch = lane & 7;
+  const uint16_t* srcA[4];
+  const uint16_t* srcB[4];
+  int lchk[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = wave * 32 + j * 8 + prow_in;
+    lchk[j] = xswz(row, pch) * 8;
+    srcA[j] = qs + (m0 + row) * K3;
+    srcB[j] = gs + (n0 + row) * 2 * Dp;
+  }
+  auto stage = [&](int sbuf, int t) {
+    const int c = t / 3, part = t % 3;
+    const int ka = t * BK;
+    const int kb = c * 128 + (part == 1 ? 64 : 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint16_t* la = lds + (sbuf * 2 + 0) * TILE + (wave * 32 + j * 8) * BK;
+      uint16_t* lb = lds + (sbuf * 2 + 1) * TILE + (wave * 32 + j * 8) * BK;
+      __builtin_amdgcn_global_load_lds((const void*)(srcA[j] + ka + lchk[j]), (lds_ptr_t)la, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(srcB[j] + kb + lchk[j]), (lds_ptr_t)lb, 16, 0, 0);
+    }
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int nk = K3 / BK;
+  const int fr = lane & 15, fq = lane >> 4;
+  stage(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int sb = kt & 1;
+    if (kt + 1 < nk) stage(sb ^ 1, kt + 1);
+    const uint16_t* la = lds + (sb * 2 + 0) * TILE;
+    const uint16_t* lb = lds + (sb * 2 + 1) * TILE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 a[4], b[4];
+      const int ch = ks * 4 + fq;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rowa = wm * 64 + i * 16 + fr;
+        const int rowb = wn * 64 + i * 16 + fr;
+        a[i] = *(const bf16x8*)(la + rowa * BK + xswz(rowa, ch) * 8);
+        b[i] = *(const bf16x8*)(lb + rowb * BK + xswz(rowb, ch) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // C[row][col]: col = lane&15 (gallery row), row = 4*(lane>>4) + reg (query)
+  float ig[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t g = n0 + wn * 64 + j * 16 + fr;
+    ig[j] = g < n ? inv_g[g] : 0.f;
+    if (g >= n) ig[j] = -INFINITY;  // marks padding rows (never a candidate)
+  }
+  const int64_t gcol = (n0 + wn * 64) / 64 * 16 + fr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mx = fmaxf(mx, ig[j] == -INFINITY ? -INFINITY : acc[i][j][rg] * ig[j]);
+      const int64_t m = m0 + wm * 64 + i * 16 + fq * 4 + rg;
+      gmax[m * ldG + gcol] = mx;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ per-query selection
+// Digit pick of one radix pass, by wave 0: the largest digit dg whose bins [dg..255] hold >= krem
+// keys, and the rank left inside that bin.  Lane l owns bins 4l..4l+3; a suffix sum over the
+// lanes (shuffles) replaces a 256-step serial walk of the histogram.
+__device__ __forceinline__ void pick_digit(const uint32_t* hist, uint32_t krem, uint32_t prefix, int shift,
+                                           uint32_t* bcast) {
+  if (threadIdx.x >= 64) return;
+  const int l = threadIdx.x;
+  const uint32_t h0 = hist[4 * l], h1 = hist[4 * l + 1], h2 = hist[4 * l + 2], h3 = hist[4 * l + 3];
+  const uint32_t own = h0 + h1 + h2 + h3;
+  uint32_t suf = own;  // inclusive suffix sum over lanes >= l
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_down(suf, o, 64);
+    if (l + o < 64) suf += v;
+  }
+  const uint32_t above = suf - own;  // keys in bins of higher lanes
+  const uint32_t total = __shfl(suf, 0, 64);
+  if (krem > total) {  // fewer keys than the rank asked for: digit 0 (as a full downward walk ends)
+    if (l == 0) {
+      bcast[0] = prefix;
+      bcast[1] = krem - (total - h0);
+    }
+    return;
+  }
+  if (above < krem && krem <= suf) {  // exactly one lane
+    uint32_t acc = above;
+    int dg = 4 * l + 3;
+    const uint32_t hb[4] = {h0, h1, h2, h3};
+    for (int e = 3; e > 0; --e) {
+      if (acc + hb[e] >= krem) break;
+      acc += hb[e];
+      dg = 4 * l + e - 1;
+    }
+    bcast[0] = prefix | ((uint32_t)dg << shift);
+    bcast[1] = krem - acc;
+  }
+}
+
 // Block-wide radix select: the kth (1-based) largest key among keys[0..m) (LDS).  All threads
 // return the same key.  hist: 256-entry LDS scratch.
 __device__ uint32_t block_select_kth(const uint32_t* keys, int m, int kth, uint32_t* hist,
@@ -327,16 +464,7 @@ __device__ uint32_t block_select_kth(const uint32_t* keys, int m, int kth, uint3
       if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      uint32_t acc = 0;
-      int dg = 255;
-      for (; dg > 0; --dg) {
-        if (acc + hist[dg] >= krem) break;
-        acc += hist[dg];
-      }
-      bcast[0] = prefix | ((uint32_t)dg << shift);
-      bcast[1] = krem - acc;
-    }
+    pick_digit(hist, krem, prefix, shift, bcast);
     __syncthreads();
     prefix = bcast[0];
     krem = bcast[1];
@@ -360,16 +488,7 @@ __device__ uint32_t row_select_kth(const float* row, int64_t n, int kth, uint32_
       if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      uint32_t acc = 0;
-      int dg = 255;
-      for (; dg > 0; --dg) {
-        if (acc + hist[dg] >= krem) break;
-        acc += hist[dg];
-      }
-      bcast[0] = prefix | ((uint32_t)dg << shift);
-      bcast[1] = krem - acc;
-    }
+    pick_digit(hist, krem, prefix, shift, bcast);
     __syncthreads();
     prefix = bcast[0];
     krem = bcast[1];
@@ -492,6 +611,167 @@ __global__ __launch_bounds__(kSelThreads) void knn_select(
     }
     if (rank < kk) {
       oi[rank] = (int64_t)ic + idx_base;
+      if (os) os[rank] = (float)sc;
+      if (os64) os64[rank] = sc;
+    }
+  }
+  if (tid == 0 && status) status[qi] = st;
+}
+
+// Selection on row-group maxima (after knn_scores_x3_gmax): one 1024-thread workgroup per query.
+// (A) per-thread max over a strided slice of the query's group maxima; (B) b = K-th largest of
+// those (each is a distinct group's max, hence a distinct row's score: b <= the K-th largest
+// approximate score t); (C) collect every group whose max >= b - 2 delta — a true top-K row j has
+// s(j) >= t - 2 delta >= b - 2 delta, and its group's max >= s(j); (D) if more than kGrpCap groups
+// qualify, the exact K-th largest group max replaces b (same argument) and the set is rebuilt;
+// (E) every row of the collected groups is re-scored in f64 from the raw rows and (F) ranked by
+// (score desc, index asc).
+constexpr int kGrpCap = kCandCap / 4;
+
+__global__ __launch_bounds__(kSelThreads) void knn_select_groups(
+    const float* __restrict__ gmax, int64_t ldG, int64_t n, int k, float two_delta,
+    const float* __restrict__ q_raw, int d, const double* __restrict__ qnorm64,
+    const float* __restrict__ gal, int Dp, const double* __restrict__ gnorm64, int64_t idx_base,
+    int64_t* __restrict__ out_idx, float* __restrict__ out_score, double* __restrict__ out_score64,
+    int32_t* __restrict__ status) {
+  __shared__ uint32_t tmax[kSelThreads];
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t bcast[4];
+  __shared__ int cand_g[kGrpCap];
+  __shared__ double cand_d[kCandCap];
+
+  const int64_t qi = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float* row = gmax + qi * ldG;
+  const int kk = (int)(n < (int64_t)k ? n : (int64_t)k);
+  int64_t* oi = out_idx + qi * k;
+  float* os = out_score ? out_score + qi * k : nullptr;
+  double* os64 = out_score64 ? out_score64 + qi * k : nullptr;
+  for (int r = kk + tid; r < k; r += kSelThreads) {
+    oi[r] = -1;
+    if (os) os[r] = -INFINITY;
+    if (os64) os64[r] = -INFINITY;
+  }
+  if (kk <= 0) {
+    if (tid == 0 && status) status[qi] = 0;
+    return;
+  }
+  const int64_t ng = ldG;       // groups per query row (Np / 4, a multiple of 64)
+  const int64_t n4 = ng >> 2;
+  float m = -INFINITY;
+  for (int64_t i = tid; i < n4; i += kSelThreads) {
+    const float4 v = ((const float4*)row)[i];
+    m = fmaxf(fmaxf(m, v.x), fmaxf(fmaxf(v.y, v.z), v.w));
+  }
+  tmax[tid] = f2key(m);
+  if (tid == 0) bcast[2] = 0;
+  __syncthreads();
+  float thr = lower_threshold(key2f(block_select_kth(tmax, kSelThreads, kk, hist, bcast)), two_delta);
+  auto collect = [&](float th) {
+    for (int64_t i = tid; i < n4; i += kSelThreads) {
+      const float4 v = ((const float4*)row)[i];
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (vv[e] >= th && vv[e] > -INFINITY) {
+          const uint32_t p = atomicAdd(&bcast[2], 1u);
+          if (p < kGrpCap) cand_g[p] = (int)(4 * i + e);
+        }
+    }
+    __syncthreads();
+  };
+  collect(thr);
+  int cnt = (int)bcast[2];
+  int st = 0;
+  if (cnt > kGrpCap) {
+    __syncthreads();
+    const float t = key2f(row_select_kth(row, ng, kk, hist, bcast));
+    thr = lower_threshold(t, two_delta);
+    if (tid == 0) bcast[2] = 0;
+    __syncthreads();
+    collect(thr);
+    cnt = (int)bcast[2];
+    if (cnt > kGrpCap) {
+      st = 1;
+      cnt = kGrpCap;
+    }
+  }
+  // (E) f64 re-score of every row of the collected groups (slot s: group s/4, member s%4)
+  const int nslot = 4 * cnt;
+  const float* qr = q_raw + qi * (int64_t)d;
+  const double qn = qnorm64[qi];
+  auto slot_row = [&](int s) -> int64_t {
+    const int g = cand_g[s >> 2];
+    return (int64_t)(g >> 4) * 64 + (g & 15) + 16 * (s & 3);
+  };
+  if (d <= 1024) {
+    // latency-bound: each wave issues the float4 loads of RB rows before reducing any of them;
+    // the query row stays in registers (lane owns elements 4(64c + lane) .. +3)
+    constexpr int RB = 2;
+    float qv[4][4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int kq = (c * 64 + lane) * 4 + e;
+        qv[c][e] = kq < d ? qr[kq] : 0.f;
+      }
+    for (int s0 = wave * RB; s0 < nslot; s0 += (kSelThreads / 64) * RB) {
+      float4 gv[RB][4];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const int s = s0 + r;
+        const int64_t gi = s < nslot ? slot_row(s) : n;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int k0 = (c * 64 + lane) * 4;
+          gv[r][c] = (gi < n && k0 < Dp) ? *(const float4*)(gal + gi * Dp + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        double acc = 0.0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          acc += (double)qv[c][0] * gv[r][c].x + (double)qv[c][1] * gv[r][c].y + (double)qv[c][2] * gv[r][c].z +
+                 (double)qv[c][3] * gv[r][c].w;
+        acc = mmr::wave_sum(acc);
+        const int s = s0 + r;
+        if (lane == 0 && s < nslot) {
+          const int64_t gi = slot_row(s);
+          const double gn = gi < n ? gnorm64[gi] : 0.0;
+          cand_d[s] = gi >= n ? -INFINITY : ((qn > 0.0 && gn > 0.0) ? acc / (qn * gn) : 0.0);
+        }
+      }
+    }
+  } else {
+    for (int s = wave; s < nslot; s += kSelThreads / 64) {
+      const int64_t gi = slot_row(s);
+      double sc = -INFINITY;
+      if (gi < n) {
+        const float* gr = gal + gi * Dp;
+        double acc = 0.0;
+        for (int kq = lane; kq < d; kq += 64) acc += (double)qr[kq] * (double)gr[kq];
+        acc = mmr::wave_sum(acc);
+        const double gn = gnorm64[gi];
+        sc = (qn > 0.0 && gn > 0.0) ? acc / (qn * gn) : 0.0;
+      }
+      if (lane == 0) cand_d[s] = sc;
+    }
+  }
+  __syncthreads();
+  // (F) rank among the valid slots
+  for (int s = tid; s < nslot; s += kSelThreads) {
+    const double sc = cand_d[s];
+    if (sc == -INFINITY) continue;
+    const int64_t ic = slot_row(s);
+    int rank = 0;
+    for (int j2 = 0; j2 < nslot; ++j2) {
+      const double sj = cand_d[j2];
+      rank += (sj > sc) || (sj == sc && slot_row(j2) < ic);
+    }
+    if (rank < kk) {
+      oi[rank] = ic + idx_base;
       if (os) os[rank] = (float)sc;
       if (os64) os64[rank] = sc;
     }
@@ -857,9 +1137,15 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
       knn_split_queries<<<dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, st>>>(ix->qn, ix->Dp, total, ix->qs);
       MMR_LAUNCH_CHECK();
       const int tiles_m = (int)(Qp / 128), tiles_n = (int)(ix->Np / 128);
-      knn_scores_x3<<<dim3((unsigned)(tiles_m * tiles_n)), dim3(256), 0, st>>>(
-          ix->qs, ix->gs, ix->inv_norm, ix->scores, ix->Dp, ix->Np, tiles_m, tiles_n);
+      knn_scores_x3_gmax<<<dim3((unsigned)(tiles_m * tiles_n)), dim3(256), 0, st>>>(
+          ix->qs, ix->gs, ix->inv_norm, ix->scores, ix->Dp, ix->Np / 4, ix->n, tiles_m, tiles_n);
       MMR_LAUNCH_CHECK();
+      knn_select_groups<<<dim3((unsigned)cq), dim3(kSelThreads), 0, st>>>(
+          ix->scores, ix->Np / 4, ix->n, k, two_delta, qc, ix->d, ix->qnorm64, ix->gal, ix->Dp,
+          ix->norm64, ix->idx_base, out_idx + c0 * k, out_score ? out_score + c0 * k : nullptr,
+          out_score64 ? out_score64 + c0 * k : nullptr, out_status ? out_status + c0 : nullptr);
+      MMR_LAUNCH_CHECK();
+      continue;
     } else {
       int wq, wn;
       if (cq <= 64) { wq = 1; wn = 4; } else if (cq <= 128) { wq = 2; wn = 2; } else { wq = 4; wn = 1; }
