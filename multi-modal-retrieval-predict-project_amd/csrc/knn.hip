@@ -6,19 +6,23 @@
 //
 // Pipeline per search (all on the caller's stream):
 //   1. knn_prep_queries   q -> qn = q/|q| (f32, padded [Qp][Dp]) + |q| in f64.
-//   2. knn_scores_x3      (default) S = (qn . g) / |g| as a bf16 "3-term split" MFMA GEMM: every
+//   2. knn_scores_x3_gmax (default) S = (qn . g) / |g| as a bf16 "3-term split" MFMA GEMM: every
 //                         operand is split into hi + lo bf16 (hi = bf16(x), lo = bf16(x - hi)) and
 //                         s ~= q_hi.g_hi + q_hi.g_lo + q_lo.g_hi (dropped terms <= 3*2^-16 |q||g|),
 //                         run as ONE K' = 3D GEMM on v_mfma_f32_16x16x32_bf16 (16x the f32 MFMA
 //                         rate; 5.3x after the 3 terms).  Gallery stored [hi c | lo c] per
 //                         64-wide chunk c (4 B/element, the f32 byte count); the k-tile 3c+2 re-reads
-//                         hi c from L2.  Queries stored [hi c | hi c | lo c].
+//                         hi c from L2.  Queries stored [hi c | hi c | lo c].  The epilogue keeps
+//                         only the max of each lane's 4-row group per query (gmax, 1/4 of the
+//                         score bytes; the score matrix is never written) and
+//                         knn_select_groups re-scores every row of the groups whose max clears
+//                         b - 2*delta (same bound, argued at the kernel).
 //      knn_scores         (mode f32) S[Qp][Np] = (qn . g) * (1/|g|) with v_mfma_f32_32x32x2_f32 (exact f32
 //                         products, f32 accumulate).  MFMA-bound for Q >~ 40, HBM-bound below.
 //                         Wave tile 64 queries x 64 gallery rows (2x2 MFMA tiles, 64 acc regs);
 //                         operands loaded straight to VGPRs as float4 with a k-permutation (lane
 //                         half h owns k = kb+8h..kb+8h+7), which the dot product does not see.
-//   3. knn_select         one 1024-thread workgroup per query: (A) per-thread max over a strided
+//   3. knn_select         (mode f32) one 1024-thread workgroup per query: (A) per-thread max over a strided
 //                         slice of the row; (B) b = K-th largest of the 1024 maxima (a lower bound
 //                         of the K-th largest score); (C) collect every s >= b - 2*delta into LDS;
 //                         (D) rare fallback: exact radix select over the row if (C) overflowed;
@@ -221,96 +225,8 @@ __device__ __forceinline__ int xswz(int row, int chunk) { return chunk ^ ((row >
 // S[m][n] = inv_g[n] * sum_k' Qs[m][k'] Gs'[n][k'] over K' = 3 Dp; tile 128 x 128 x 64, 4 waves
 // (2x2) of 64x64, glds-staged double buffer with source-address swizzle (same structure as
 // gemm.hip).  Rows of the query block past Qp / gallery past Np never exist (both padded).
-__global__ __launch_bounds__(256, 2) void knn_scores_x3(const uint16_t* __restrict__ qs,
-                                                         const uint16_t* __restrict__ gs,
-                                                         const float* __restrict__ inv_g,
-                                                         float* __restrict__ scores, int Dp,
-                                                         int64_t ldS, int tiles_m, int tiles_n) {
-  constexpr int BK = 64, TILE = 128 * 64;
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * TILE];
-  // gallery tiles outer, query tiles inner: the tiles_m query blocks of one gallery tile are
-  // consecutive in the remapped order and share the XCD (and its L2) -> gallery read once
-  const int nwg = tiles_m * tiles_n;
-  const int orig = blockIdx.x;
-  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int tn = wg / tiles_m, tm = wg % tiles_m;
-  const int64_t m0 = (int64_t)tm * 128, n0 = (int64_t)tn * 128;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int K3 = 3 * Dp;
-  const int prow_in = lane >> 3, pch = lane & 7;
-  const uint16_t* srcA[4];
-  const uint16_t* srcB[4];
-  int lchk[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int row = wave * 32 + j * 8 + prow_in;
-    lchk[j] = xswz(row, pch) * 8;
-    srcA[j] = qs + (m0 + row) * K3;
-    srcB[j] = gs + (n0 + row) * 2 * Dp;
-  }
-  auto stage = [&](int sbuf, int t) {
-    const int c = t / 3, part = t % 3;
-    const int ka = t * BK;
-    const int kb = c * 128 + (part == 1 ? 64 : 0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      uint16_t* la = lds + (sbuf * 2 + 0) * TILE + (wave * 32 + j * 8) * BK;
-      uint16_t* lb = lds + (sbuf * 2 + 1) * TILE + (wave * 32 + j * 8) * BK;
-      __builtin_amdgcn_global_load_lds((const void*)(srcA[j] + ka + lchk[j]), (lds_ptr_t)la, 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(srcB[j] + kb + lchk[j]), (lds_ptr_t)lb, 16, 0, 0);
-    }
-  };
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const int nk = K3 / BK;
-  const int fr = lane & 15, fq = lane >> 4;
-  stage(0, 0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int sb = kt & 1;
-    if (kt + 1 < nk) stage(sb ^ 1, kt + 1);
-    const uint16_t* la = lds + (sb * 2 + 0) * TILE;
-    const uint16_t* lb = lds + (sb * 2 + 1) * TILE;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 a[4], b[4];
-      const int ch = ks * 4 + fq;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int rowa = wm * 64 + i * 16 + fr;
-        const int rowb = wn * 64 + i * 16 + fr;
-        a[i] = *(const bf16x8*)(la + rowa * BK + xswz(rowa, ch) * 8);
-        b[i] = *(const bf16x8*)(lb + rowb * BK + xswz(rowb, ch) * 8);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
-    __syncthreads();
-  }
-  // C[row][col]: col = lane&15 (gallery row), row = 4*(lane>>4) + reg (query)
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t n = n0 + wn * 64 + j * 16 + fr;
-    const float ig = inv_g[n];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        const int64_t m = m0 + wm * 64 + i * 16 + fq * 4 + rg;
-        scores[m * ldS + n] = acc[i][j][rg] * ig;
-      }
-    }
-  }
-}
-
+// Gallery tiles outer, query tiles inner: the tiles_m query blocks of one gallery tile are
+// consecutive in the remapped order and share the XCD (and its L2) -> gallery read once.
 // Same GEMM, fused epilogue: instead of the (Qp x Np) score matrix, each lane keeps the max of its
 // 4 gallery rows {B + fr + 16j : j < 4} (B = the wave's 64-row block) per query — a "row group" —
 // and writes one float per (query, group): gmax[m][g], g = (B/64)*16 + fr, ldG = Np/4.  Rows >= n

@@ -106,13 +106,13 @@ class MultiModalRetrievalModel:
 
     @classmethod
     def from_reference_state_dict(cls, sd, swin_cfg, bert_cfg, joint_dim, model_type="text", device="cuda",
-                                  use_shared_ffn=False):
+                                  use_shared_ffn=False, num_heads=4):
         """Build from a reference checkpoint state dict (model.py:282-287 layout)."""
         vis = _sub(sd, "backbones.vision.")
         bb = Backbones(swin_state=vis, bert_state=_sub(sd, "backbones.bert."), swin_cfg=swin_cfg,
                        bert_cfg=bert_cfg, device=device)
-        return cls(joint_dim=joint_dim, model_type=model_type, backbones=bb, head_state=sd, device=device,
-                   use_shared_ffn=use_shared_ffn)
+        return cls(joint_dim=joint_dim, num_heads=num_heads, model_type=model_type, backbones=bb, head_state=sd,
+                   device=device, use_shared_ffn=use_shared_ffn)
 
     def set_retriever(self, retriever):
         self.retriever = retriever
