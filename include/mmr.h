@@ -121,6 +121,13 @@ mmr_status mmr_add_layernorm_bf16(const uint16_t* x, const uint16_t* residual, c
                                   const float* beta, uint16_t* y, int64_t rows, int32_t c,
                                   float eps, void* stream);
 
+/* y = LayerNorm(alpha * x + residual) with alpha a DEVICE f32 scalar (NULL = 1) and residual may be
+ * NULL: PreFusionEnhancer's norm1(alpha * x + x2) (src/Model/fusion.py:34) on the vectorised
+ * row kernel.  bf16 in / out, contiguous rows of c channels (c % 8 == 0). */
+mmr_status mmr_scaled_add_layernorm_bf16(const uint16_t* x, const float* alpha, const uint16_t* residual,
+                                         const float* gamma, const float* beta, uint16_t* y, int64_t rows,
+                                         int32_t c, float eps, void* stream);
+
 /* BERT embeddings (HF BertEmbeddings): LN(word[id] + pos[l] + type[0]) -> bf16 (b*l, c). */
 mmr_status mmr_bert_embed(const int64_t* ids, const float* word, const float* pos,
                           const float* type0, const float* gamma, const float* beta, uint16_t* y,
@@ -210,6 +217,14 @@ mmr_status mmr_linear_f32(const float* x, int64_t ldx, const float* w, const flo
                           const float* residual, int64_t ldr, float* y, int64_t ldy, int32_t b,
                           int32_t cin, int32_t cout, int32_t act, void* stream);
 
+/* nbatch independent mmr_linear_f32 problems in one launch; problem i reads x + i*bsx, w + i*bsw,
+ * bias + i*bsb, residual + i*bsr and writes y + i*bsy (element strides; bsx, bsw % 4 == 0): the
+ * per-query work of all fusion layers at once (each layer has its own weights). */
+mmr_status mmr_linear_f32_batched(const float* x, int64_t ldx, int64_t bsx, const float* w, int64_t bsw,
+                                  const float* bias, int64_t bsb, const float* residual, int64_t ldr,
+                                  int64_t bsr, float* y, int64_t ldy, int64_t bsy, int32_t nbatch, int32_t b,
+                                  int32_t cin, int32_t cout, int32_t act, void* stream);
+
 /* ---------------------------------------------------------------- multimodal fusion stack */
 /* model_type="multimodal": CrossModalFusion (src/Model/fusion.py:334-471) x num_fusion_layers +
  * the combiner (src/Model/model.py:375-459), eval.  Orchestrated host-side over these ops and
@@ -232,11 +247,14 @@ mmr_status mmr_add_pos_bf16(const void* x, int32_t x_is_f32, const float* pos, u
 
 /* y = LayerNorm(alpha*x + residual) (+ post_scale*post), per row of c <= 1024 channels.
  * alpha / post_scale are DEVICE f32 scalars (learned parameters) or NULL (= 1); residual / post
- * may be NULL.  io_bf16: x, residual, y bf16 (else f32); post is always f32. */
+ * may be NULL.  io_bf16: x, residual, y bf16 (else f32); post is always f32.  Row r uses parameter
+ * set g = (r / group_div) % groups — gamma/beta + g*c, alpha/post_scale + g — so one launch
+ * normalises the rows of several layers (groups = layers; group_div = 1 for [..][layer][c] rows,
+ * = rows per layer for [layer][..][c]). */
 mmr_status mmr_ln_rows(const void* x, int64_t ldx, const float* alpha, const void* residual, int64_t ldr,
                        const float* gamma, const float* beta, const float* post, int64_t ldp,
                        const float* post_scale, void* y, int64_t ldy, int64_t rows, int32_t c, float eps,
-                       int32_t io_bf16, void* stream);
+                       int32_t io_bf16, int32_t groups, int64_t group_div, void* stream);
 
 /* seq (b, np+2, c) bf16 = [x1; patches_fused; x2] + pe[0..np+2) (fusion.py:468 + model.py:397);
  * x1, x2 f32 (b, c), patches_fused bf16 (b*np, c), pe f32 [>= np+2][c]. */

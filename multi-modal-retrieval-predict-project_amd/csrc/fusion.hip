@@ -252,10 +252,15 @@ __global__ __launch_bounds__(256) void ln_rows(const TI* __restrict__ x, int64_t
                                                const float* __restrict__ g, const float* __restrict__ b,
                                                const float* __restrict__ post, int64_t ldp,
                                                const float* __restrict__ ps, TO* __restrict__ y, int64_t ldy,
-                                               int64_t rows, int c, float eps) {
+                                               int64_t rows, int c, float eps, int groups, int64_t gdiv) {
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
+  const int grp = (int)((row / gdiv) % groups);  // per-row parameter set (layers batched in one launch)
+  g += (int64_t)grp * c;
+  b += (int64_t)grp * c;
+  if (a) a += grp;
+  if (ps) ps += grp;
   auto ld = [](const TI* p, int64_t i) -> float {
     if constexpr (sizeof(TI) == 4) return ((const float*)p)[i];
     else return bf2f(((const uint16_t*)p)[i]);
@@ -380,18 +385,21 @@ mmr_status mmr_add_pos_bf16(const void* x, int32_t x_is_f32, const float* pos, u
 mmr_status mmr_ln_rows(const void* x, int64_t ldx, const float* alpha, const void* residual, int64_t ldr,
                        const float* gamma, const float* beta, const float* post, int64_t ldp,
                        const float* post_scale, void* y, int64_t ldy, int64_t rows, int32_t c, float eps,
-                       int32_t io_bf16, void* stream) {
+                       int32_t io_bf16, int32_t groups, int64_t group_div, void* stream) {
   mmr::clear_error();
-  MMR_REQUIRE(x && gamma && beta && y && rows >= 0 && c > 0 && c <= 1024, "mmr_ln_rows: bad arguments (c <= 1024)");
+  MMR_REQUIRE(x && gamma && beta && y && rows >= 0 && c > 0 && c <= 1024 && groups >= 1 && group_div >= 1,
+              "mmr_ln_rows: bad arguments (c <= 1024, groups >= 1, group_div >= 1)");
   if (rows == 0) return MMR_OK;
   const dim3 grid((unsigned)mmr::ceil_div(rows, 4));
   hipStream_t st = mmr::as_stream(stream);
   if (io_bf16)
     ln_rows<uint16_t, uint16_t><<<grid, 256, 0, st>>>((const uint16_t*)x, ldx, alpha, (const uint16_t*)residual, ldr,
-                                                      gamma, beta, post, ldp, post_scale, (uint16_t*)y, ldy, rows, c, eps);
+                                                      gamma, beta, post, ldp, post_scale, (uint16_t*)y, ldy, rows, c, eps,
+                                                      groups, group_div);
   else
     ln_rows<float, float><<<grid, 256, 0, st>>>((const float*)x, ldx, alpha, (const float*)residual, ldr, gamma, beta,
-                                                post, ldp, post_scale, (float*)y, ldy, rows, c, eps);
+                                                post, ldp, post_scale, (float*)y, ldy, rows, c, eps, groups,
+                                                group_div);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }

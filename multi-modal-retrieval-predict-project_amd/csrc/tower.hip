@@ -39,7 +39,8 @@ __global__ __launch_bounds__(256) void layernorm_bf16(const uint16_t* __restrict
                                                       const float* __restrict__ g,
                                                       const float* __restrict__ b,
                                                       uint16_t* __restrict__ y, int64_t rows,
-                                                      int c, float eps) {
+                                                      int c, float eps,
+                                                      const float* __restrict__ alpha = nullptr) {
   constexpr int RPW = 64 / LPR;
   const int lane = threadIdx.x & 63;
   const int sub = lane % LPR;
@@ -47,6 +48,7 @@ __global__ __launch_bounds__(256) void layernorm_bf16(const uint16_t* __restrict
   const bool ok = row < rows;
   const uint16_t* xr = x + (ok ? row : 0) * c;
   const int nch = c / 8;
+  const float av = alpha ? *alpha : 1.f;  // learned scale of x (PreFusionEnhancer alpha, fusion.py:34)
   float v[8][8];
   float s = 0.f;
 #pragma unroll
@@ -54,6 +56,10 @@ __global__ __launch_bounds__(256) void layernorm_bf16(const uint16_t* __restrict
     const int ch = sub + i * LPR;
     if (ok && ch < nch) {
       load8(xr + ch * 8, v[i]);
+      if (alpha) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] *= av;
+      }
       if (ADD) {  // post-LN residual: LN(x + r), the sum kept in f32
         float w[8];
         load8(r + (ok ? row : 0) * c + ch * 8, w);
@@ -597,8 +603,16 @@ __global__ __launch_bounds__(512) void linear_f32(const float* __restrict__ X,
                                                   const float* __restrict__ bias,
                                                   float* Y, int nb, int cin, int cout,
                                                   int act, int64_t ldx, int64_t ldy,
-                                                  const float* R, int64_t ldr) {
+                                                  const float* R, int64_t ldr, int64_t bsx = 0,
+                                                  int64_t bsw = 0, int64_t bsb = 0, int64_t bsr = 0,
+                                                  int64_t bsy = 0) {
   __shared__ float part[LF_WAVES][1024];
+  // batched form (blockIdx.y = problem index): independent problems at fixed element strides
+  X += blockIdx.y * bsx;
+  W += blockIdx.y * bsw;
+  if (bias) bias += blockIdx.y * bsb;
+  if (R) R += blockIdx.y * bsr;
+  Y += blockIdx.y * bsy;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int tiles_o = cout / 32;
   const int tb = blockIdx.x / tiles_o, to = blockIdx.x % tiles_o;
@@ -653,9 +667,12 @@ __global__ __launch_bounds__(512) void linear_f32(const float* __restrict__ X,
 }
 
 void launch_linear_f32(const float* x, const float* w, const float* b, float* y, int nb, int cin, int cout,
-                       int act, int64_t ldx, int64_t ldy, const float* r, int64_t ldr, hipStream_t st) {
+                       int act, int64_t ldx, int64_t ldy, const float* r, int64_t ldr, hipStream_t st,
+                       int nbatch = 1, int64_t bsx = 0, int64_t bsw = 0, int64_t bsb = 0, int64_t bsr = 0,
+                       int64_t bsy = 0) {
   const int64_t tiles = mmr::ceil_div(nb, 32) * (cout / 32);
-  linear_f32<<<dim3((unsigned)tiles), dim3(64 * LF_WAVES), 0, st>>>(x, w, b, y, nb, cin, cout, act, ldx, ldy, r, ldr);
+  linear_f32<<<dim3((unsigned)tiles, (unsigned)nbatch), dim3(64 * LF_WAVES), 0, st>>>(
+      x, w, b, y, nb, cin, cout, act, ldx, ldy, r, ldr, bsx, bsw, bsb, bsr, bsy);
 }
 
 __global__ __launch_bounds__(256) void l2_normalize_rows(float* __restrict__ y, int nb, int d) {
@@ -677,7 +694,8 @@ extern "C" {
 
 static mmr_status layernorm_launch(const uint16_t* x, const uint16_t* r, const float* gamma,
                                    const float* beta, uint16_t* y, int64_t rows, int32_t c,
-                                   float eps, void* stream, const char* who) {
+                                   float eps, void* stream, const char* who,
+                                   const float* alpha = nullptr) {
   MMR_REQUIRE(x && gamma && beta && y, "%s: NULL pointer", who);
   MMR_REQUIRE(c > 0 && c % 8 == 0 && rows >= 0, "%s: c=%d must be a positive multiple of 8", who, c);
   MMR_REQUIRE(c <= 4096, "%s: c=%d > 4096", who, c);
@@ -689,8 +707,8 @@ static mmr_status layernorm_launch(const uint16_t* x, const uint16_t* r, const f
   const int64_t rows_per_block = 4 * (64 / lpr);
   const dim3 grid((unsigned)mmr::ceil_div(rows, rows_per_block));
 #define MMR_LN(L)                                                                           \
-  (r ? layernorm_bf16<L, true><<<grid, 256, 0, st>>>(x, r, gamma, beta, y, rows, c, eps)    \
-     : layernorm_bf16<L, false><<<grid, 256, 0, st>>>(x, r, gamma, beta, y, rows, c, eps))
+  (r ? layernorm_bf16<L, true><<<grid, 256, 0, st>>>(x, r, gamma, beta, y, rows, c, eps, alpha)    \
+     : layernorm_bf16<L, false><<<grid, 256, 0, st>>>(x, r, gamma, beta, y, rows, c, eps, alpha))
   if (lpr == 8) MMR_LN(8);
   else if (lpr == 16) MMR_LN(16);
   else if (lpr == 32) MMR_LN(32);
@@ -712,6 +730,14 @@ mmr_status mmr_add_layernorm_bf16(const uint16_t* x, const uint16_t* residual, c
   mmr::clear_error();
   MMR_REQUIRE(residual, "mmr_add_layernorm_bf16: NULL residual");
   return layernorm_launch(x, residual, gamma, beta, y, rows, c, eps, stream, "mmr_add_layernorm_bf16");
+}
+
+mmr_status mmr_scaled_add_layernorm_bf16(const uint16_t* x, const float* alpha, const uint16_t* residual,
+                                         const float* gamma, const float* beta, uint16_t* y, int64_t rows,
+                                         int32_t c, float eps, void* stream) {
+  mmr::clear_error();
+  return layernorm_launch(x, residual, gamma, beta, y, rows, c, eps, stream, "mmr_scaled_add_layernorm_bf16",
+                          alpha);
 }
 
 mmr_status mmr_bert_embed(const int64_t* ids, const float* word, const float* pos,
@@ -868,6 +894,25 @@ mmr_status mmr_linear_f32(const float* x, int64_t ldx, const float* w, const flo
   MMR_REQUIRE(act == 0 || act == 1, "mmr_linear_f32: act=%d", act);
   if (b == 0) return MMR_OK;
   launch_linear_f32(x, w, bias, y, b, cin, cout, act, ldx, ldy, residual, ldr, mmr::as_stream(stream));
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_linear_f32_batched(const float* x, int64_t ldx, int64_t bsx, const float* w, int64_t bsw,
+                                  const float* bias, int64_t bsb, const float* residual, int64_t ldr,
+                                  int64_t bsr, float* y, int64_t ldy, int64_t bsy, int32_t nbatch, int32_t b,
+                                  int32_t cin, int32_t cout, int32_t act, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && w && y && b >= 0 && cin > 0 && cout > 0 && nbatch >= 1, "mmr_linear_f32_batched: bad arguments");
+  MMR_REQUIRE(cin % 16 == 0 && cout % 32 == 0, "mmr_linear_f32_batched: cin=%d must be a multiple of 16, cout=%d of 32",
+              cin, cout);
+  MMR_REQUIRE(ldx >= cin && ldx % 4 == 0 && ldy >= cout && (!residual || ldr >= cout) && bsx % 4 == 0 && bsw % 4 == 0,
+              "mmr_linear_f32_batched: bad strides");
+  MMR_REQUIRE(((uintptr_t)x & 15u) == 0 && ((uintptr_t)w & 15u) == 0, "mmr_linear_f32_batched: x / w must be 16-B aligned");
+  MMR_REQUIRE(act == 0 || act == 1, "mmr_linear_f32_batched: act=%d", act);
+  if (b == 0) return MMR_OK;
+  launch_linear_f32(x, w, bias, y, b, cin, cout, act, ldx, ldy, residual, ldr, mmr::as_stream(stream), nbatch, bsx,
+                    bsw, bsb, bsr, bsy);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }

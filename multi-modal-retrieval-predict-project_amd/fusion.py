@@ -65,7 +65,7 @@ class _Enhancer:
         ops.mha(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], B, L, L, self.heads, self.dh,
                 1.0 / math.sqrt(self.dh), out=a)
         x2 = ops.linear(a, self.w_o, self.b_o)
-        return ops.ln_rows(X, self.g, self.b, eps, alpha=self.alpha, residual=x2)
+        return ops.scaled_add_layernorm(X, self.alpha, x2, self.g, self.b, eps)
 
 
 class FusionStack:
@@ -131,61 +131,89 @@ class FusionStack:
         self.s_ow, self.s_ob = _f(sd["self_attn.out_proj.weight"], dev), _f(sd["self_attn.out_proj.bias"], dev)
         self.pe = _f(sd["pos_encoder.pe"][0], dev)
         self.alpha = _f(sd["alpha"].reshape(1), dev)
-
-    def layer_seq(self, L, G, P, T, B, Lt, Np):
-        """CrossModalFusion.forward -> fused-sequence mean (B, D) f32 (model.py:396-431)."""
-        D, h, eps = self.D, self.heads, self.eps
-        dh = D // h
-        sc = 1.0 / math.sqrt(dh)
-        Te = L["txt"](T, B, Lt, eps)                                   # (B*Lt, Ct) bf16
-        Pe = L["patch"](P, B, Np, eps)                                 # (B*Np, Ci) bf16
-        Ge = ops.linear_f32(G, L["g_w"], L["g_b"])                     # folded 1-token attention
-        Ge = ops.ln_rows(G, *L["g_ln"], eps, alpha=L["g_alpha"], residual=Ge)
-        TQ = ops.linear(Te, L["t_w"], L["t_b"])                        # (B*Lt, 3D): q_t2i | k_i2t | v_i2t
-        PQ = ops.linear(Pe, L["p_w"], L["p_b"])                        # (B*Np, 3D): k_t2i | v_t2i | q_i2t
-        PP = ops.linear(Pe, L["pp_w"], L["pp_b"])                      # img_patch_proj
-        m1 = torch.empty((B, D), dtype=torch.float32, device=self.device)
-        ops.mha(TQ[:, :D], PQ[:, :D], PQ[:, D:2 * D], B, Lt, Np, h, dh, sc, mean_out=m1)
-        a2 = torch.empty((B * Np, D), dtype=torch.bfloat16, device=self.device)
-        m2 = torch.empty((B, D), dtype=torch.float32, device=self.device)
-        ops.mha(PQ[:, 2 * D:], TQ[:, D:2 * D], TQ[:, 2 * D:], B, Np, Lt, h, dh, sc, out=a2, mean_out=m2)
-        PF = ops.linear(a2, L["o2_wb"], L["o2_b"], residual=PP)       # patches_fused (fusion.py:437)
-        t2i = ops.linear_f32(m1, L["o1_w"], L["o1_b"])                 # mean_L att_txt2img
-        x1 = ops.linear_f32(Ge, L["gp_w"], L["gp_b"], residual=t2i)
-        x1 = ops.ln_rows(x1, *L["ln_img"], eps)
-        i2t = ops.linear_f32(m2, L["o2_w"], L["o2_b"])                 # mean_Np att_img2txt
-        cls = ops.rows_to_f32(Te, B, Te.shape[1], Lt * Te.shape[1])
-        x2 = ops.linear_f32(cls, L["tp_w"], L["tp_b"], residual=i2t)
-        x2 = ops.ln_rows(x2, *L["ln_txt"], eps)
-        S = ops.assemble_seq(x1, PF, x2, self.pe, Np).view(B * (Np + 2), D)
-        SQ = ops.linear(S, self.s_w, self.s_b)
-        m3 = torch.empty((B, D), dtype=torch.float32, device=self.device)
-        ops.mha(SQ[:, :D], SQ[:, D:2 * D], SQ[:, 2 * D:], B, Np + 2, Np + 2, h, dh, sc, mean_out=m3)
-        return ops.linear_f32(m3, self.s_ow, self.s_ob)               # mean of self_attn output
+        # per-query work of all layers batched (stacked per-layer parameters):
+        #  global enhancer  LN(alpha*G + Wov G + b) = LN((Wov + alpha I) G + b): ONE linear over the
+        #                   concatenated weights (same input G) + one grouped LayerNorm
+        Ls = self.layers
+        eye = torch.eye(Ls[0]["g_w"].shape[0], device=dev)
+        self.g_w_all = torch.cat([L["g_w"] + L["g_alpha"] * eye for L in Ls]).contiguous()
+        self.g_b_all = torch.cat([L["g_b"] for L in Ls]).contiguous()
+        self.g_ln_all = tuple(torch.stack([L["g_ln"][k] for L in Ls]).contiguous() for k in (0, 1))
+        st = lambda k: torch.stack([L[k] for L in Ls]).contiguous()  # noqa: E731
+        self.o1_w_all, self.o1_b_all = st("o1_w"), st("o1_b")
+        self.o2_w_all, self.o2_b_all = st("o2_w"), st("o2_b")
+        self.gp_w_all, self.gp_b_all = st("gp_w"), st("gp_b")
+        self.tp_w_all, self.tp_b_all = st("tp_w"), st("tp_b")
+        self.ln_img_all = tuple(torch.stack([L["ln_img"][k] for L in Ls]).contiguous() for k in (0, 1))
+        self.ln_txt_all = tuple(torch.stack([L["ln_txt"][k] for L in Ls]).contiguous() for k in (0, 1))
 
     def forward(self, img_global, img_patches, txt_feats):
         """img_global (B, Ci) f32, img_patches (B, Np, Ci) f32, txt_feats (B, L, Ct) bf16/f32 or None
-        -> joint_emb (B, D) f32."""
+        -> joint_emb (B, D) f32.
+
+        Phase 1 (per layer, token level): enhancers, folded cross projections, the two cross
+        attentions (means only where only means are used), patches_fused.
+        Phase 2 (all layers in single launches): global enhancer, txt2img / img2txt out-projections
+        of the means, ln_img / ln_txt — batched linears and grouped LayerNorms.
+        Phase 3 (all layers together): sequence assembly, the shared self_attn QKV GEMM over
+        nl*B*(Np+2) rows, its attention means and out-projection.
+        Phase 4 (sequential): the joint chain (norm1 / alpha, norm2 -> FFN, adapter)."""
         B, Np, Ci = img_patches.shape
+        D, h, eps, dev = self.D, self.heads, self.eps, self.device
+        nl = len(self.layers)
+        dh = D // h
+        sc = 1.0 / math.sqrt(dh)
         G = img_global.float().contiguous()
         P = img_patches.contiguous().view(B * Np, Ci)
-        joint = None
-        eps = self.eps
+        m1 = torch.empty((nl, B, D), dtype=torch.float32, device=dev)
+        m2 = torch.empty((nl, B, D), dtype=torch.float32, device=dev)
+        PF = torch.empty((nl, B * Np, D), dtype=torch.bfloat16, device=dev)
+        cls = None
         for i, L in enumerate(self.layers):
             if txt_feats is None:  # learnable default text token (fusion.py:404-407)
                 T, Lt = L["default_txt"].expand(B, -1).contiguous(), 1
             else:
                 Lt = txt_feats.shape[1]
                 T = txt_feats.to(torch.bfloat16).contiguous().view(B * Lt, -1)
-            fused = self.layer_seq(L, G, P, T, B, Lt, Np)
+            Te = L["txt"](T, B, Lt, eps)                               # (B*Lt, Ct) bf16
+            Pe = L["patch"](P, B, Np, eps)                             # (B*Np, Ci) bf16
+            Ct = Te.shape[1]
+            if cls is None:
+                cls = torch.empty((nl, B, Ct), dtype=torch.float32, device=dev)
+            ops.rows_to_f32(Te, B, Ct, Lt * Ct, out=cls[i])            # CLS rows (fusion.py:447)
+            TQ = ops.linear(Te, L["t_w"], L["t_b"])                    # (B*Lt, 3D): q_t2i | k_i2t | v_i2t
+            PQ = ops.linear(Pe, L["p_w"], L["p_b"])                    # (B*Np, 3D): k_t2i | v_t2i | q_i2t
+            PP = ops.linear(Pe, L["pp_w"], L["pp_b"])                  # img_patch_proj
+            ops.mha(TQ[:, :D], PQ[:, :D], PQ[:, D:2 * D], B, Lt, Np, h, dh, sc, mean_out=m1[i])
+            a2 = torch.empty((B * Np, D), dtype=torch.bfloat16, device=dev)
+            ops.mha(PQ[:, 2 * D:], TQ[:, D:2 * D], TQ[:, 2 * D:], B, Np, Lt, h, dh, sc, out=a2, mean_out=m2[i])
+            ops.linear(a2, L["o2_wb"], L["o2_b"], residual=PP, out=PF[i])  # patches_fused (fusion.py:437)
+        # phase 2: per-query vectors of all layers
+        Ge = ops.linear_f32(G, self.g_w_all, self.g_b_all)             # (B, nl*Ci), layer-minor
+        Ge = ops.ln_rows(Ge.view(B * nl, Ci), *self.g_ln_all, eps, groups=nl).view(B, nl * Ci)
+        t2i = ops.linear_f32_batched(m1, self.o1_w_all, self.o1_b_all, nl, B)          # mean_L att_txt2img
+        x1 = ops.linear_f32_batched(Ge, self.gp_w_all, self.gp_b_all, nl, B, residual=t2i, ldx=nl * Ci, bsx=Ci)
+        x1 = ops.ln_rows(x1.view(nl * B, D), *self.ln_img_all, eps, groups=nl, group_div=B)
+        i2t = ops.linear_f32_batched(m2, self.o2_w_all, self.o2_b_all, nl, B)          # mean_Np att_img2txt
+        x2 = ops.linear_f32_batched(cls, self.tp_w_all, self.tp_b_all, nl, B, residual=i2t)
+        x2 = ops.ln_rows(x2.view(nl * B, D), *self.ln_txt_all, eps, groups=nl, group_div=B)
+        # phase 3: the shared combiner self-attention over every layer's fused sequence
+        S = ops.assemble_seq(x1, PF.view(nl * B * Np, D), x2, self.pe, Np).view(nl * B * (Np + 2), D)
+        SQ = ops.linear(S, self.s_w, self.s_b)
+        m3 = torch.empty((nl * B, D), dtype=torch.float32, device=dev)
+        ops.mha(SQ[:, :D], SQ[:, D:2 * D], SQ[:, 2 * D:], nl * B, Np + 2, Np + 2, h, dh, sc, mean_out=m3)
+        fused = ops.linear_f32(m3, self.s_ow, self.s_ob).view(nl, B, D)  # mean of self_attn output
+        # phase 4: the joint chain
+        joint = None
+        for i, L in enumerate(self.layers):
             if i == 0:
-                x = fused
+                x = fused[0]
             else:  # norm1(joint) + alpha * fused  (StochasticDepth in eval = plain residual)
-                x = ops.ln_rows(joint, *L["n1"], eps, post=fused, post_scale=self.alpha)
+                x = ops.ln_rows(joint, *L["n1"], eps, post=fused[i], post_scale=self.alpha)
             xf = ops.ln_rows(x, *L["n2"], eps)
             w1, b1, w2, b2 = L["ffn"]
             ops.linear_f32(ops.linear_f32(xf, w1, b1, act=1), w2, b2, residual=x, out=x)
             a1, c1, a2, c2 = L["ad"]
             ops.linear_f32(ops.linear_f32(x, a1, c1, act=1), a2, c2, residual=x, out=x)
             joint = x
-        return joint
+        return joint.contiguous()

@@ -51,6 +51,19 @@ def add_layernorm(x, r, g, b, eps, out=None):
     return y
 
 
+def scaled_add_layernorm(x, alpha, r, g, b, eps, out=None):
+    """LayerNorm(alpha * x + r), alpha a device scalar tensor (vectorised row kernel, bf16)."""
+    _lib.require_gpu(x)
+    c = x.shape[-1]
+    if r is not None:
+        assert r.shape == x.shape
+    y = out if out is not None else torch.empty_like(x)
+    _chk(_L().mmr_scaled_add_layernorm_bf16(_lib.ptr(x), _lib.ptr(alpha), _lib.ptr(r), _lib.ptr(g), _lib.ptr(b),
+                                            _lib.ptr(y), x.numel() // c, c, float(eps), _s(x)),
+         "mmr_scaled_add_layernorm_bf16")
+    return y
+
+
 def bert_embed(ids, word, pos, type0, g, b, eps):
     _lib.require_gpu(ids)
     B, L = ids.shape
@@ -164,8 +177,10 @@ def add_pos(x, pos, l):
     return y
 
 
-def ln_rows(x, g, b, eps, alpha=None, residual=None, post=None, post_scale=None, out=None):
-    """LN(alpha*x + residual) * g + b (+ post_scale*post) over 2-D row views (f32 or bf16 in/out)."""
+def ln_rows(x, g, b, eps, alpha=None, residual=None, post=None, post_scale=None, out=None, groups=1, group_div=1):
+    """LN(alpha*x + residual) * g + b (+ post_scale*post) over 2-D row views (f32 or bf16 in/out);
+    with groups > 1, row r uses parameter set (r // group_div) % groups of g/b [groups][c] and
+    alpha/post_scale [groups]."""
     _lib.require_gpu(x)
     assert x.dim() == 2 and x.stride(1) == 1
     rows, c = x.shape
@@ -173,8 +188,30 @@ def ln_rows(x, g, b, eps, alpha=None, residual=None, post=None, post_scale=None,
     _chk(_L().mmr_ln_rows(_lib.ptr(x), x.stride(0), _lib.ptr(alpha), _lib.ptr(residual),
                           residual.stride(0) if residual is not None else 0, _lib.ptr(g), _lib.ptr(b),
                           _lib.ptr(post), post.stride(0) if post is not None else 0, _lib.ptr(post_scale),
-                          _lib.ptr(y), y.stride(0), rows, c, float(eps), int(x.dtype == torch.bfloat16), _s(x)),
-         "mmr_ln_rows")
+                          _lib.ptr(y), y.stride(0), rows, c, float(eps), int(x.dtype == torch.bfloat16), groups,
+                          group_div, _s(x)), "mmr_ln_rows")
+    return y
+
+
+def linear_f32_batched(x, w, bias, nbatch, b, residual=None, act=0, out=None, ldx=None, bsx=None, ldy=None,
+                       bsy=None, ldr=None, bsr=None):
+    """nbatch independent f32 linears: problem i reads rows of x at x + i*bsx (row stride ldx), weights
+    w[i] (w (nbatch, cout, cin)), bias[i], residual + i*bsr and writes out + i*bsy (row stride ldy).
+    Defaults: contiguous (nbatch, b, cin) -> (nbatch, b, cout)."""
+    _lib.require_gpu(x)
+    cout, cin = w.shape[1], w.shape[2]
+    ldx = cin if ldx is None else ldx
+    bsx = b * ldx if bsx is None else bsx
+    y = out if out is not None else torch.empty((nbatch, b, cout), dtype=torch.float32, device=x.device)
+    ldy = cout if ldy is None else ldy
+    bsy = b * ldy if bsy is None else bsy
+    if residual is not None:
+        ldr = cout if ldr is None else ldr
+        bsr = b * ldr if bsr is None else bsr
+    _chk(_L().mmr_linear_f32_batched(_lib.ptr(x), ldx, bsx, _lib.ptr(w), cout * cin, _lib.ptr(bias),
+                                     cout if bias is not None else 0, _lib.ptr(residual), ldr or 0, bsr or 0,
+                                     _lib.ptr(y), ldy, bsy, nbatch, b, cin, cout, act, _s(x)),
+         "mmr_linear_f32_batched")
     return y
 
 
@@ -186,8 +223,8 @@ def assemble_seq(x1, pf, x2, pe, np_):
     return seq
 
 
-def rows_to_f32(x, b, c, ldx):
-    y = torch.empty((b, c), dtype=torch.float32, device=x.device)
+def rows_to_f32(x, b, c, ldx, out=None):
+    y = out if out is not None else torch.empty((b, c), dtype=torch.float32, device=x.device)
     _chk(_L().mmr_rows_to_f32(_lib.ptr(x), ldx, _lib.ptr(y), b, c, _s(x)), "mmr_rows_to_f32")
     return y
 
