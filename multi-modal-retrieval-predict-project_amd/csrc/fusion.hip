@@ -47,14 +47,16 @@ __global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q,
   constexpr int DHP = DT * 32;
   constexpr int KS = DHP / 16;
   constexpr int KROW = DHP + 8;       // padded K row (elements): 16-B skew between consecutive keys
-  constexpr int VTS = MHA_KB + 4;     // V^T row stride (elements)
+  // V row stride: (stride in 4-B banks) = 16 or 48 mod 64, so the 4 rows x 64 B of one half-wave's
+  // transposed reads land on disjoint banks
+  constexpr int VROW = DHP + ((DT & 1) ? 0 : 16);
   constexpr int NCH = DHP / 8;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int bi = blockIdx.x / heads, hh = blockIdx.x % heads;
   const int lkp = (lk + 31) & ~31;
   uint16_t* Ks = (uint16_t*)smem;            // [MHA_KB][KROW]
-  uint16_t* Vt = Ks + MHA_KB * KROW;         // [DHP][VTS]
-  float* msum = (float*)(Vt + DHP * VTS);    // [waves][DHP] per-wave partial means
+  uint16_t* Vs = Ks + MHA_KB * KROW;         // [MHA_KB][VROW], natural (key-major) layout
+  float* msum = (float*)(Vs + MHA_KB * VROW);  // [waves][DHP] per-wave partial means
   const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6;
   const uint16_t* kbase = k + (int64_t)bi * lk * ldk + hh * dh;
   const uint16_t* vbase = v + (int64_t)bi * lk * ldv + hh * dh;
@@ -89,8 +91,7 @@ __global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q,
         vv = *(const bf16x8*)(vbase + (int64_t)(k0 + key) * ldv + ch * 8);
       }
       *(bf16x8*)(Ks + key * KROW + ch * 8) = kv;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) Vt[(ch * 8 + j) * VTS + key] = (uint16_t)vv[j];
+      *(bf16x8*)(Vs + key * VROW + ch * 8) = vv;
     }
     __syncthreads();
     if (!active) continue;
@@ -143,7 +144,11 @@ __global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q,
       for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
         for (int rg = 0; rg < 16; ++rg) o[dt][rg] *= alpha;
-      // O^T[d][q] += V^T[d][key] . P^T[key][q]
+      // O^T[d][q] += V^T[d][key] . P^T[key][q]; the V^T fragment (lane: d = its row, keys
+      // kk..kk+3 and kk+8..kk+11 in P^T's register order) comes from the key-major V image by two
+      // ds_read_b64_tr_b16: in each 16-lane group, lane 4q+p addresses row (key) r0+q, columns
+      // c0+4p..+3, and lane i receives column c0+i of the 4 rows (cdna_hip_programming.md T10)
+      const int grp = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         if (t < nt) {
@@ -152,12 +157,14 @@ __global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q,
             bf16x8 pf;
 #pragma unroll
             for (int j = 0; j < 8; ++j) pf[j] = (short)f2bf(s[t][8 * sidx + j]);
-            const int kk = kb + t * 32 + 16 * sidx + 4 * hf;
+            const int r0 = kb + t * 32 + 16 * sidx + 4 * (grp >> 1);
 #pragma unroll
             for (int dt = 0; dt < DT; ++dt) {
-              const uint16_t* vrow = Vt + (dt * 32 + r) * VTS;
-              const bf16x4 lo = *(const bf16x4*)(vrow + kk);
-              const bf16x4 hi = *(const bf16x4*)(vrow + kk + 8);
+              const int c0 = dt * 32 + (grp & 1) * 16;
+              const uint16_t* va = Vs + (r0 + tq) * VROW + c0 + 4 * tp;
+              const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4*)va);
+              const bf16x4 hi =
+                  __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4*)(va + 8 * VROW));
               const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
               o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[dt], 0, 0, 0);
             }
@@ -349,7 +356,8 @@ mmr_status mmr_mha(const uint16_t* q, int64_t ldq, const uint16_t* k, int64_t ld
               "mmr_mha: operands must be 16-B aligned");
   if (b == 0) return MMR_OK;
   const int dt = (dh + 31) / 32;
-  const size_t lds = (size_t)MHA_KB * (dt * 32 + 8) * 2 + (size_t)dt * 32 * (MHA_KB + 4) * 2 + (size_t)4 * dt * 32 * 4;
+  const size_t lds = (size_t)MHA_KB * (dt * 32 + 8) * 2 + (size_t)MHA_KB * (dt * 32 + ((dt & 1) ? 0 : 16)) * 2 +
+                     (size_t)4 * dt * 32 * 4;
   const int nqt = (lq + 31) / 32, nchunk = (lq + 127) / 128;
   const dim3 grid((unsigned)((int64_t)b * heads), (unsigned)nchunk), blk(64 * std::min(4, nqt));
   hipStream_t st = mmr::as_stream(stream);

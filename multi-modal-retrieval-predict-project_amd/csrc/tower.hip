@@ -7,6 +7,7 @@
 // MultiModalRetrievalModel heads (model.py:365-373, 462-479), MultiHeadMLP (model.py:61-75).
 #include <float.h>
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.h"
 
@@ -702,8 +703,17 @@ static mmr_status layernorm_launch(const uint16_t* x, const uint16_t* r, const f
   if (rows == 0) return MMR_OK;
   hipStream_t st = mmr::as_stream(stream);
   const int nch = c / 8;
-  int lpr = 64;
-  while (lpr > 8 && nch <= (lpr / 2) * 2) lpr /= 2;  // <= 2 chunks per lane for narrow rows
+  // lanes per row: the narrowest LPR that splits the row's 16-B chunks evenly into <= 6 per lane
+  // (no idle lanes, several loads in flight per lane; measured best on the BERT/Swin widths);
+  // otherwise <= 2 chunks per lane for narrow rows
+  int lpr = 0;
+  for (int l = 8; l <= 64 && !lpr; l *= 2)
+    if (nch % l == 0 && nch / l <= 6) lpr = l;
+  if (!lpr) {
+    lpr = 64;
+    while (lpr > 8 && nch <= (lpr / 2) * 2) lpr /= 2;
+  }
+  if (const char* e = getenv("MMR_LN_LPR")) lpr = atoi(e);  // diagnostic override (8/16/32/64)
   const int64_t rows_per_block = 4 * (64 / lpr);
   const dim3 grid((unsigned)mmr::ceil_div(rows, rows_per_block));
 #define MMR_LN(L)                                                                           \

@@ -1,0 +1,71 @@
+"""Per-op time breakdown of one bench step (multimodal default): wraps the mmr_amd.ops entry points
+with HIP events on the current stream and prints, per (op, shape), calls / total ms / TF/s for the
+GEMMs.  Diagnostic only.
+usage: python tools/step_breakdown.py [--model-type multimodal|text]"""
+import collections
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import mmr_amd  # noqa: E402,F401
+from mmr_amd import ops, synthetic  # noqa: E402
+from mmr_amd.model import build_bench_model  # noqa: E402
+
+mt = sys.argv[2] if len(sys.argv) > 2 and sys.argv[1] == "--model-type" else "multimodal"
+torch.cuda.set_device(0)
+dev = torch.device("cuda:0")
+model = build_bench_model(device=dev, joint_dim=768, model_type=mt)
+B = 256
+imgs = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(B, synthetic.SEED))).to(dev)
+ids_np, mask_np = synthetic.reports(B, 128, synthetic.SEED + 100)
+ids, mask = torch.from_numpy(ids_np).to(dev), torch.from_numpy(mask_np).to(dev)
+
+rec = []
+names = ["linear", "layernorm", "add_layernorm", "scaled_add_layernorm", "bert_embed", "bert_attention",
+         "swin_window_attention", "patch_im2col", "patch_merge_ln", "swin_head", "mean_tokens", "proj_head",
+         "swin_mlp", "swin_attn_block", "linear_f32", "linear_f32_batched", "mha", "add_pos", "ln_rows",
+         "assemble_seq", "rows_to_f32"]
+
+
+def wrap(name, fn):
+    def w(*a, **k):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = fn(*a, **k)
+        e1.record()
+        key = name
+        if name == "linear":
+            x, wt = a[0], a[1]
+            K = x.shape[-1]
+            key = (name, x.numel() // K, wt.shape[0], K, k.get("act", a[4] if len(a) > 4 else 0),
+                   (k.get("residual") if "residual" in k else (a[3] if len(a) > 3 else None)) is not None)
+        rec.append((key, e0, e1))
+        return out
+    return w
+
+
+for n in names:
+    setattr(ops, n, wrap(n, getattr(ops, n)))
+# the modules imported ops functions by module reference (ops.linear), so the wrappers are seen
+for _ in range(3):
+    model.query_embeddings(imgs, ids, mask)
+torch.cuda.synchronize()
+rec.clear()
+for _ in range(3):
+    model.query_embeddings(imgs, ids, mask)
+torch.cuda.synchronize()
+agg = collections.defaultdict(lambda: [0, 0.0])
+for key, e0, e1 in rec:
+    agg[key][0] += 1
+    agg[key][1] += e0.elapsed_time(e1) / 3
+tot = sum(v[1] for v in agg.values())
+print(f"total {tot:.3f} ms per step (sum of op times)")
+for key, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+    if isinstance(key, tuple):
+        _, M, N, K, act, res = key
+        tf = 2.0 * M * N * K * (c / 3) / (t * 1e-3) / 1e12
+        print(f"{t:8.3f} ms {c // 3:4d}x  linear M={M:7d} N={N:5d} K={K:5d} act={act} res={int(res)}  {tf:6.0f} TF/s")
+    else:
+        print(f"{t:8.3f} ms {c // 3:4d}x  {key}")
