@@ -36,6 +36,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // fusion call at L = 128) the mean is reduced in LDS and stored; with several chunks each adds its
 // partial into the (pre-zeroed) output with a float atomic.
 constexpr int MHA_KB = 128;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 template <int DT>
 __global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q, int64_t ldq,
@@ -50,13 +51,14 @@ __global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q,
   // V row stride: (stride in 4-B banks) = 16 or 48 mod 64, so the 4 rows x 64 B of one half-wave's
   // transposed reads land on disjoint banks
   constexpr int VROW = DHP + ((DT & 1) ? 0 : 16);
-  constexpr int NCH = DHP / 8;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int bi = blockIdx.x / heads, hh = blockIdx.x % heads;
   const int lkp = (lk + 31) & ~31;
   uint16_t* Ks = (uint16_t*)smem;            // [MHA_KB][KROW]
   uint16_t* Vs = Ks + MHA_KB * KROW;         // [MHA_KB][VROW], natural (key-major) layout
-  float* msum = (float*)(Vs + MHA_KB * VROW);  // [waves][DHP] per-wave partial means
+  // [waves][DHP] per-wave partial means, after the larger of the K/V image and the epilogue area
+  constexpr int KV_BYTES = MHA_KB * (KROW + VROW) * 2, RED_BYTES = 4 * DHP * 33 * 4;
+  float* msum = (float*)(smem + (KV_BYTES > RED_BYTES ? KV_BYTES : RED_BYTES));
   const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6;
   const uint16_t* kbase = k + (int64_t)bi * lk * ldk + hh * dh;
   const uint16_t* vbase = v + (int64_t)bi * lk * ldv + hh * dh;
@@ -83,15 +85,32 @@ __global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q,
   for (int k0 = 0; k0 < lkp; k0 += MHA_KB) {
     const int kn = min(MHA_KB, lkp - k0);   // keys staged this round (multiple of 32)
     __syncthreads();                          // previous key block consumed
-    for (int c = tid; c < kn * NCH; c += nthr) {
-      const int key = c / NCH, ch = c % NCH;
-      bf16x8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (k0 + key < lk && ch * 8 < dh) {
-        kv = *(const bf16x8*)(kbase + (int64_t)(k0 + key) * ldk + ch * 8);
-        vv = *(const bf16x8*)(vbase + (int64_t)(k0 + key) * ldv + ch * 8);
+    // HBM -> LDS by global_load_lds (16 B per lane, lane-linear per wave instruction): LDS slot j of
+    // the padded image is filled from whichever global chunk belongs there, so every load of the
+    // block is in flight at once with no VGPR staging.  Pad slots, chunks past dh and keys past lk
+    // read a clamped in-bounds chunk: finite values that the zero Q columns / the -inf key mask /
+    // the discarded O columns make irrelevant.
+    {
+      constexpr int KSL = KROW / 8, VSL = VROW / 8;
+      const int nk = kn * KSL, nv = kn * VSL, nw64 = nthr;
+      for (int b0 = wave * 64; b0 < nk; b0 += nw64) {
+        const int slot = b0 + lane;
+        if (slot < nk) {
+          const int key = slot / KSL, ch = slot % KSL;
+          const int ks = min(k0 + key, lk - 1), cs = (ch * 8 < dh) ? ch : 0;
+          __builtin_amdgcn_global_load_lds((const void*)(kbase + (int64_t)ks * ldk + cs * 8),
+                                           (lds_ptr_t)(Ks + b0 * 8), 16, 0, 0);
+        }
       }
-      *(bf16x8*)(Ks + key * KROW + ch * 8) = kv;
-      *(bf16x8*)(Vs + key * VROW + ch * 8) = vv;
+      for (int b0 = wave * 64; b0 < nv; b0 += nw64) {
+        const int slot = b0 + lane;
+        if (slot < nv) {
+          const int key = slot / VSL, ch = slot % VSL;
+          const int ks = min(k0 + key, lk - 1), cs = (ch * 8 < dh) ? ch : 0;
+          __builtin_amdgcn_global_load_lds((const void*)(vbase + (int64_t)ks * ldv + cs * 8),
+                                           (lds_ptr_t)(Vs + b0 * 8), 16, 0, 0);
+        }
+      }
     }
     __syncthreads();
     if (!active) continue;
@@ -173,34 +192,56 @@ __global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q,
       }
     }
   }
+  // epilogue through LDS (the K/V image is free once every wave is past its last key block):
+  //  - out: the wave's O tile is staged as bf16 [32 q][DHP + 4] and written back as contiguous 8-B
+  //    chunks per query row (coalesced), instead of 4 scattered 8-B stores per MFMA tile;
+  //  - mean: lane (q = r) writes its O^T column into red[d][q], then lane l sums rows d = l, l + 64,
+  //    ... (no cross-lane shuffle chains).  Both use the wave's own region, one after the other.
+  constexpr int RLD = 33, OROW = DHP + 4;
+  float* red = (float*)smem + wave * DHP * RLD;
+  __syncthreads();
   if (active) {
     const float inv = 1.0f / (l_run + __shfl_xor(l_run, 32, 64));
-    if (out != nullptr && qok) {
-      uint16_t* orow = out + ((int64_t)bi * lq + qi) * ldo + hh * dh;
+    if (out != nullptr) {
+      uint16_t* st = (uint16_t*)red;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           const int d = dt * 32 + 8 * g4 + 4 * hf;
-          if (d < dh) {
-            bf16x4 w;
+          bf16x4 w;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) w[j] = (short)f2bf(o[dt][4 * g4 + j] * inv);
-            *(bf16x4*)(orow + d) = w;
-          }
+          for (int j = 0; j < 4; ++j) w[j] = (short)f2bf(o[dt][4 * g4 + j] * inv);
+          *(bf16x4*)(st + r * OROW + d) = w;
         }
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes landed
+      __builtin_amdgcn_wave_barrier();
+      const int nc4 = dh / 4;
+      for (int c = lane; c < 32 * nc4; c += 64) {
+        const int row = c / nc4, ch = c % nc4;
+        if (q0 + row < lq)
+          *(bf16x4*)(out + ((int64_t)bi * lq + q0 + row) * ldo + hh * dh + ch * 4) =
+              *(const bf16x4*)(st + row * OROW + ch * 4);
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_wave_barrier();
     }
     if (mean_out != nullptr) {
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
         for (int rg = 0; rg < 16; ++rg) {
-          float x = qok ? o[dt][rg] * inv : 0.f;
-#pragma unroll
-          for (int off = 1; off < 32; off <<= 1) x += __shfl_xor(x, off, 64);
           const int d = dt * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * hf;
-          if (r == 0) msum[wave * DHP + d] = x;
+          red[d * RLD + r] = qok ? o[dt][rg] * inv : 0.f;
         }
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_wave_barrier();
+      for (int d = lane; d < DHP; d += 64) {
+        float acc = 0.f;
+#pragma unroll 8
+        for (int j = 0; j < 32; ++j) acc += red[d * RLD + j];
+        msum[wave * DHP + d] = acc;
+      }
     }
   }
   if (mean_out != nullptr) {
@@ -356,8 +397,8 @@ mmr_status mmr_mha(const uint16_t* q, int64_t ldq, const uint16_t* k, int64_t ld
               "mmr_mha: operands must be 16-B aligned");
   if (b == 0) return MMR_OK;
   const int dt = (dh + 31) / 32;
-  const size_t lds = (size_t)MHA_KB * (dt * 32 + 8) * 2 + (size_t)MHA_KB * (dt * 32 + ((dt & 1) ? 0 : 16)) * 2 +
-                     (size_t)4 * dt * 32 * 4;
+  const size_t kv_bytes = (size_t)MHA_KB * (dt * 32 + 8) * 2 + (size_t)MHA_KB * (dt * 32 + ((dt & 1) ? 0 : 16)) * 2;
+  const size_t lds = std::max(kv_bytes, (size_t)4 * dt * 32 * 33 * 4) + (size_t)4 * dt * 32 * 4;
   const int nqt = (lq + 31) / 32, nchunk = (lq + 127) / 128;
   const dim3 grid((unsigned)((int64_t)b * heads), (unsigned)nchunk), blk(64 * std::min(4, nqt));
   hipStream_t st = mmr::as_stream(stream);
