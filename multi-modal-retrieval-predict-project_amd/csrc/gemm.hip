@@ -189,6 +189,86 @@ __device__ __forceinline__ int swzk(int row, int chunk) {
   return KB == 64 ? (chunk ^ ((row >> 1) & 7)) : (chunk ^ ((row >> 1) & 3));  // conflict-free b128 reads
 }
 
+// Epilogue of the 8-wave kernels (wave tile MT*16 x NT*16 at (wm, wn)): in 64-row halves of the
+// wave tile through LDS (bf16), 16-B row stores (measured: 8-B register-direct stores of a C^T
+// product are 15-20 % slower on these shapes).  Starts with a block barrier (the LDS stages are
+// reused as staging).
+// ROWS: rows of the wave tile staged per round (64, or 32 when the staging must fit in one free
+// LDS stage); SYNC: open with __syncthreads (else the caller has already made dsm free).
+template <int MT, int NT, int ACT, bool HAS_BIAS, bool HAS_RES, int ROWS = 64, bool SYNC = true>
+__device__ __forceinline__ void big_epilogue(f32x4 (&acc)[MT][NT], uint16_t* dsm, const float* __restrict__ bias,
+                                             const uint16_t* __restrict__ R, uint16_t* __restrict__ Y,
+                                             int64_t M, int N, int64_t m0, int n0, int wm, int wn, int wave,
+                                             int lane) {
+  const int fr = lane & 15, fq = lane >> 4;
+  constexpr int HALVES = MT * 16 / ROWS, MPH = ROWS / 16;  // staging rounds, m-tiles per round
+  constexpr int CPR = NT * 16 / 8;  // 16-B chunks per row of the wave tile
+  // residual rows are fetched first, so their latency overlaps the LDS staging below
+  constexpr int NIT = (ROWS * CPR + 63) / 64;  // 16-B chunks per lane per staging round
+  bf16x8 rres[HAS_RES ? HALVES : 1][HAS_RES ? NIT : 1];
+  if constexpr (HAS_RES) {
+#pragma unroll
+    for (int hh = 0; hh < HALVES; ++hh)
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int c = it * 64 + lane;
+        const int64_t m = m0 + wm * MT * 16 + hh * ROWS + c / CPR;
+        const int n = n0 + wn * NT * 16 + (c % CPR) * 8;
+        if (c >= ROWS * CPR) continue;
+        rres[hh][it] = (m < M && n < N) ? *(const bf16x8*)(R + m * N + n) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+      }
+  }
+  if constexpr (SYNC) __syncthreads();
+  uint16_t* et = dsm + wave * ROWS * EPI_LD;
+#pragma unroll
+  for (int hh = 0; hh < HALVES; ++hh) {
+    // C^T tiles (operands swapped): lane has row m = 16i + (l&15), columns 16j + 4(l>>4) + 0..3
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int nl = j * 16 + fq * 4;
+      const int n = n0 + wn * NT * 16 + nl;
+      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (HAS_BIAS && n < N) bv = *(const float4*)(bias + n);
+      const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+      for (int i4 = 0; i4 < MPH; ++i4) {
+        float v[4];
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) {
+          v[rg] = acc[hh * MPH + i4][j][rg] + bb[rg];
+          if (ACT == 1) v[rg] = mmr::gelu_fast(v[rg]);
+        }
+        uint2 pk;
+        pk.x = mmr::pack2bf(v[0], v[1]);
+        pk.y = mmr::pack2bf(v[2], v[3]);
+        *(uint2*)(et + (i4 * 16 + fr) * EPI_LD + nl) = pk;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int it = 0; it < (ROWS * CPR + 63) / 64; ++it) {
+      const int c = it * 64 + lane;
+      const int rl = c / CPR, cc = (c % CPR) * 8;
+      const int64_t m = m0 + wm * MT * 16 + hh * ROWS + rl;
+      const int n = n0 + wn * NT * 16 + cc;
+      if (c >= ROWS * CPR || m >= M || n >= N) continue;
+      bf16x8 v = *(const bf16x8*)(et + rl * EPI_LD + cc);
+      if (HAS_RES) {
+        const bf16x8 rr = rres[HAS_RES ? hh : 0][HAS_RES ? it : 0];
+        uint32_t o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          o[e] = mmr::pack2bf(mmr::bf2f((uint16_t)v[2 * e]) + mmr::bf2f((uint16_t)rr[2 * e]),
+                              mmr::bf2f((uint16_t)v[2 * e + 1]) + mmr::bf2f((uint16_t)rr[2 * e + 1]));
+        v = __builtin_bit_cast(bf16x8, make_uint4(o[0], o[1], o[2], o[3]));
+      }
+      *(bf16x8*)(Y + m * N + n) = v;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 template <int WM, int WN, int MT, int NT, int KB, int STAGES, int ACT, bool HAS_BIAS, bool HAS_RES,
           int OCC = 1>
 __global__ __launch_bounds__(512, 2 * OCC) void gemm_bf16_tn_big(const uint16_t* __restrict__ X,
@@ -291,7 +371,7 @@ __global__ __launch_bounds__(512, 2 * OCC) void gemm_bf16_tn_big(const uint16_t*
       const int rowb = wn * NT * 16 + j * 16 + fr;
       return *(const bf16x8*)(lb + rowb * KB + swzk<KB>(rowb, ks * 4 + fq) * 8);
     };
-    if (KS == 2 && MT == 8 && NT == 4 && CA + CB == 8) {
+    if (KS == 2 && MT == 8 && NT <= 4 && CA + CB <= MT) {
       // hand-placed interleave (glds are scheduling barriers for hipcc, so source order holds):
       // k-step-0 fragments; then per A row-tile i: one glds piece of the next slice, the
       // k-step-1 fragment(s), 4 k-step-0 MFMAs; then the 32 k-step-1 MFMAs.
@@ -302,7 +382,7 @@ __global__ __launch_bounds__(512, 2 * OCC) void gemm_bf16_tn_big(const uint16_t*
       for (int i = 0; i < MT; ++i) a0[i] = rdA(0, i);
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
-        if (more) stage_piece(s_next, k_next, i);
+        if (more && i < CA + CB) stage_piece(s_next, k_next, i);
         a1[i] = rdA(1, i);
         if (i < NT) b1[i] = rdB(1, i);
 #pragma unroll
@@ -344,72 +424,7 @@ __global__ __launch_bounds__(512, 2 * OCC) void gemm_bf16_tn_big(const uint16_t*
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this slice's fragment reads returned
   }
 
-  // epilogue in 64-row halves of the wave tile through LDS (bf16), 16-B row stores (measured:
-  // 8-B register-direct stores of a C^T product are 15-20 % slower on these shapes)
-  constexpr int HALVES = MT / 4;
-  constexpr int CPR = NT * 16 / 8;  // 16-B chunks per row of the wave tile
-  // residual rows are fetched first, so their latency overlaps the LDS staging below
-  bf16x8 rres[HAS_RES ? HALVES : 1][HAS_RES ? CPR : 1];
-  if constexpr (HAS_RES) {
-#pragma unroll
-    for (int hh = 0; hh < HALVES; ++hh)
-#pragma unroll
-      for (int it = 0; it < CPR; ++it) {
-        const int c = it * 64 + lane;
-        const int64_t m = m0 + wm * MT * 16 + hh * 64 + c / CPR;
-        const int n = n0 + wn * NT * 16 + (c % CPR) * 8;
-        rres[hh][it] = (m < M && n < N) ? *(const bf16x8*)(R + m * N + n) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-      }
-  }
-  __syncthreads();
-  uint16_t* et = dsm + wave * 64 * EPI_LD;
-#pragma unroll
-  for (int hh = 0; hh < HALVES; ++hh) {
-    // C^T tiles (operands swapped): lane has row m = 16i + (l&15), columns 16j + 4(l>>4) + 0..3
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const int nl = j * 16 + fq * 4;
-      const int n = n0 + wn * NT * 16 + nl;
-      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (HAS_BIAS && n < N) bv = *(const float4*)(bias + n);
-      const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
-#pragma unroll
-      for (int i4 = 0; i4 < 4; ++i4) {
-        float v[4];
-#pragma unroll
-        for (int rg = 0; rg < 4; ++rg) {
-          v[rg] = acc[hh * 4 + i4][j][rg] + bb[rg];
-          if (ACT == 1) v[rg] = mmr::gelu_fast(v[rg]);
-        }
-        uint2 pk;
-        pk.x = mmr::pack2bf(v[0], v[1]);
-        pk.y = mmr::pack2bf(v[2], v[3]);
-        *(uint2*)(et + (i4 * 16 + fr) * EPI_LD + nl) = pk;
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int it = 0; it < CPR; ++it) {
-      const int c = it * 64 + lane;
-      const int rl = c / CPR, cc = (c % CPR) * 8;
-      const int64_t m = m0 + wm * MT * 16 + hh * 64 + rl;
-      const int n = n0 + wn * NT * 16 + cc;
-      if (m >= M || n >= N) continue;
-      bf16x8 v = *(const bf16x8*)(et + rl * EPI_LD + cc);
-      if (HAS_RES) {
-        const bf16x8 rr = rres[HAS_RES ? hh : 0][HAS_RES ? it : 0];
-        uint32_t o[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          o[e] = mmr::pack2bf(mmr::bf2f((uint16_t)v[2 * e]) + mmr::bf2f((uint16_t)rr[2 * e]),
-                              mmr::bf2f((uint16_t)v[2 * e + 1]) + mmr::bf2f((uint16_t)rr[2 * e + 1]));
-        v = __builtin_bit_cast(bf16x8, make_uint4(o[0], o[1], o[2], o[3]));
-      }
-      *(bf16x8*)(Y + m * N + n) = v;
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
+  big_epilogue<MT, NT, ACT, HAS_BIAS, HAS_RES>(acc, dsm, bias, R, Y, M, N, m0, n0, wm, wn, wave, lane);
 }
 
 
@@ -635,10 +650,11 @@ int cu_count() {
 // Kernel variants: (w4, cfg) pairs the launcher understands.  w4: 0 no persistent kernel, 1 the
 // 4-wave persistent kernel (256x256 or 256x192 tiles), 2 persistent 256x192 only; cfg: the 8-wave
 // tile when w4 does not apply (0 off -> 128x128; 1 256x256 KB64 x2; 2 256x256 KB32 x4;
-// 3 256x128 KB64 x3; 4 / 5 256x128 KB32 x2 / x3).
-constexpr int kVariants = 8;
-constexpr int kVarW4[kVariants] = {1, 2, 0, 0, 0, 0, 0, 0};
-constexpr int kVarCfg[kVariants] = {1, 1, 1, 2, 3, 4, 5, 0};
+// 3 256x128 KB64 x3; 4 / 5 256x128 KB32 x2 / x3; 6 256x192 KB64 x2 — N = 768 / 2304 / 3072 at
+// M = 32768 give 512 / 1536 / 2048 tiles, whole rounds of 256 CUs where 256x256 leaves 1.5 / 4.5).
+constexpr int kVariants = 9;
+constexpr int kVarW4[kVariants] = {1, 2, 0, 0, 0, 0, 0, 0, 0};
+constexpr int kVarCfg[kVariants] = {1, 1, 1, 2, 3, 4, 5, 6, 0};
 
 template <int ACT, bool HB, bool HR>
 void launch(const uint16_t* x, const uint16_t* w, const float* b, const uint16_t* r, uint16_t* y,
@@ -675,7 +691,13 @@ void launch(const uint16_t* x, const uint16_t* w, const float* b, const uint16_t
       }
       return;
     }
-    if (cfg >= 4 && n % 128 == 0) {  // 256x128, KB=32: 2 workgroups per CU (epilogue overlap)
+    if (cfg == 6 && n % 192 == 0 && t256 * (n / 192) >= 256) {
+      const int tm = (int)t256, tn = n / 192;
+      const size_t lds = std::max<size_t>(2 * (256 + 192) * 64 * 2, EPI_BIG_B);
+      gemm_bf16_tn_big<2, 4, 8, 3, 64, 2, ACT, HB, HR><<<dim3(tm * tn), dim3(512), lds, st>>>(x, w, b, r, y, m, n, k, tm, tn);
+      return;
+    }
+    if (cfg >= 4 && cfg <= 5 && n % 128 == 0) {  // 256x128, KB=32: 2 workgroups per CU (epilogue overlap)
       const int tm = (int)t256, tn = n / 128;
       if (cfg == 4) {
         const size_t lds = std::max<size_t>(2 * (256 + 128) * 32 * 2, EPI_BIG_B);

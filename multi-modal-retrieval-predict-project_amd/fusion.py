@@ -24,6 +24,7 @@ Every fusion layer reads the SAME backbone features (img_global, img_patches, tx
 bf16 activations / f32 accumulation for the token-level work, f32 for every per-query vector.
 """
 import math
+import os
 
 import torch
 
@@ -147,6 +148,11 @@ class FusionStack:
         self.ln_img_all = tuple(torch.stack([L["ln_img"][k] for L in Ls]).contiguous() for k in (0, 1))
         self.ln_txt_all = tuple(torch.stack([L["ln_txt"][k] for L in Ls]).contiguous() for k in (0, 1))
 
+    def _side_stream(self):
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(self.device)
+        return self._side
+
     def forward(self, img_global, img_patches, txt_feats):
         """img_global (B, Ci) f32, img_patches (B, Np, Ci) f32, txt_feats (B, L, Ct) bf16/f32 or None
         -> joint_emb (B, D) f32.
@@ -169,6 +175,29 @@ class FusionStack:
         m2 = torch.empty((nl, B, D), dtype=torch.float32, device=dev)
         PF = torch.empty((nl, B * Np, D), dtype=torch.bfloat16, device=dev)
         cls = None
+        # the patch-side token work of every layer (enhancer, folded k/v/q projection, patch
+        # projection) depends only on the image tower: it runs on a side stream, ahead of and
+        # concurrently with the text-side work, which waits per layer on an event before the
+        # cross attentions (MMR_FUSION_STREAMS=0: one stream)
+        two = os.environ.get("MMR_FUSION_STREAMS", "1") != "0"
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream() if two else main
+        pq, pp, ev = [], [], []
+        if two:
+            side.wait_stream(main)
+        with torch.cuda.stream(side):
+            for L in self.layers:
+                Pe = L["patch"](P, B, Np, eps)                         # (B*Np, Ci) bf16
+                pq.append(ops.linear(Pe, L["p_w"], L["p_b"]))          # (B*Np, 3D): k_t2i | v_t2i | q_i2t
+                pp.append(ops.linear(Pe, L["pp_w"], L["pp_b"]))        # img_patch_proj
+                if two:
+                    e = torch.cuda.Event()
+                    e.record(side)
+                    ev.append(e)
+        if two:
+            P.record_stream(side)
+            for t in pq + pp:
+                t.record_stream(main)
         for i, L in enumerate(self.layers):
             if txt_feats is None:  # learnable default text token (fusion.py:404-407)
                 T, Lt = L["default_txt"].expand(B, -1).contiguous(), 1
@@ -176,18 +205,19 @@ class FusionStack:
                 Lt = txt_feats.shape[1]
                 T = txt_feats.to(torch.bfloat16).contiguous().view(B * Lt, -1)
             Te = L["txt"](T, B, Lt, eps)                               # (B*Lt, Ct) bf16
-            Pe = L["patch"](P, B, Np, eps)                             # (B*Np, Ci) bf16
             Ct = Te.shape[1]
             if cls is None:
                 cls = torch.empty((nl, B, Ct), dtype=torch.float32, device=dev)
             ops.rows_to_f32(Te, B, Ct, Lt * Ct, out=cls[i])            # CLS rows (fusion.py:447)
             TQ = ops.linear(Te, L["t_w"], L["t_b"])                    # (B*Lt, 3D): q_t2i | k_i2t | v_i2t
-            PQ = ops.linear(Pe, L["p_w"], L["p_b"])                    # (B*Np, 3D): k_t2i | v_t2i | q_i2t
-            PP = ops.linear(Pe, L["pp_w"], L["pp_b"])                  # img_patch_proj
+            if two:
+                main.wait_event(ev[i])
+            PQ, PP = pq[i], pp[i]
             ops.mha(TQ[:, :D], PQ[:, :D], PQ[:, D:2 * D], B, Lt, Np, h, dh, sc, mean_out=m1[i])
             a2 = torch.empty((B * Np, D), dtype=torch.bfloat16, device=dev)
             ops.mha(PQ[:, 2 * D:], TQ[:, D:2 * D], TQ[:, 2 * D:], B, Np, Lt, h, dh, sc, out=a2, mean_out=m2[i])
             ops.linear(a2, L["o2_wb"], L["o2_b"], residual=PP, out=PF[i])  # patches_fused (fusion.py:437)
+        del pq, pp
         # phase 2: per-query vectors of all layers
         Ge = ops.linear_f32(G, self.g_w_all, self.g_b_all)             # (B, nl*Ci), layer-minor
         Ge = ops.ln_rows(Ge.view(B * nl, Ci), *self.g_ln_all, eps, groups=nl).view(B, nl * Ci)

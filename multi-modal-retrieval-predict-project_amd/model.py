@@ -17,6 +17,8 @@ MultiModalRetrievalModel.forward(...) -> {"joint_emb", "img_emb", "txt_emb", "lo
     (model.py:375-459) on libmmr kernels (mmr_amd/fusion.py); the classifier (logits) is
     classification, out of scope -> None; attention maps (return_attention) are not produced.
 """
+import os
+
 import torch
 
 from . import ops
@@ -88,6 +90,7 @@ class MultiModalRetrievalModel:
         self.use_shared_ffn = use_shared_ffn
         self.use_cls_only = use_cls_only
         self.retriever = retriever
+        self._side = None
         hs = head_state if head_state is not None else init_head_state(self.backbones.img_dim,
                                                                        self.backbones.txt_dim, joint_dim, seed + 2)
         f = lambda k: hs[k].detach().to(self.device, torch.float32).contiguous()  # noqa: E731
@@ -148,12 +151,33 @@ class MultiModalRetrievalModel:
     def query_embeddings(self, image, input_ids, attention_mask):
         """Retrieval keys of one (image, report) batch.  multimodal: (B, D) f32 joint embeddings;
         image / text: both single-modality heads, (2B, D) = [image-head; text-head] joint embeddings."""
-        if self.model_type == "multimodal":
-            g, p, _ = self.backbones.encode_image(image, want_patches=True)
-            return self.fusion.forward(g, p, self.backbones.encode_text(input_ids, attention_mask))
-        _, _, pool = self.backbones.encode_image(image, want_patches=False)
-        txt_mean = self._txt_pool(self.backbones.encode_text(input_ids, attention_mask))
-        return torch.cat([self._head(pool, self.img_proj), self._head(txt_mean, self.txt_proj)], 0)
+        mm = self.model_type == "multimodal"
+        (g, p, pool), txt = self._towers(image, input_ids, attention_mask, mm)
+        if mm:
+            return self.fusion.forward(g, p, txt)
+        return torch.cat([self._head(pool, self.img_proj), self._head(self._txt_pool(txt), self.txt_proj)], 0)
+
+    def _towers(self, image, input_ids, attention_mask, want_patches):
+        """Both towers, the Swin tower on a side stream so its kernels fill the CUs the BERT
+        kernels leave idle (wave-quantisation tails, small LayerNorm / attention launches); the
+        two towers share no data until the heads.  MMR_TOWER_STREAMS=0 runs them in sequence."""
+        if os.environ.get("MMR_TOWER_STREAMS", "1") == "0":
+            return (self.backbones.encode_image(image, want_patches=want_patches),
+                    self.backbones.encode_text(input_ids, attention_mask))
+        main = torch.cuda.current_stream(self.device)
+        if self._side is None:
+            self._side = torch.cuda.Stream(self.device)
+        side = self._side
+        side.wait_stream(main)                        # the image batch is ready
+        with torch.cuda.stream(side):
+            img = self.backbones.encode_image(image, want_patches=want_patches)
+        image.record_stream(side)                     # caching allocator: in use on the side stream
+        txt = self.backbones.encode_text(input_ids, attention_mask)
+        main.wait_stream(side)
+        for t in img:
+            if t is not None:
+                t.record_stream(main)
+        return img, txt
 
 
 def init_head_state(img_dim, txt_dim, joint_dim, seed=2711):

@@ -32,10 +32,17 @@ b = torch.randn(N, device="cuda")
 r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16) if res else None
 fl = 2.0 * M * N * K
 out = [f"M={M} N={N} K={K} act={act} res={int(res)}"]
-for w4, big in (("1", "1"), ("2", "1"), ("0", "1"), ("0", "2"), ("0", "3"), ("0", "4"), ("0", "5"), ("0", "0")):
+ref = x.float() @ w.float().t() + b
+if act == 1:
+    ref = F.gelu(ref)
+if res:
+    ref = ref + r.float()
+for w4, big in (("1", "1"), ("2", "1"), ("0", "1"), ("0", "2"), ("0", "3"), ("0", "4"), ("0", "5"), ("0", "6"),
+                ("0", "0")):
     os.environ["MMR_GEMM_W4"], os.environ["MMR_GEMM_BIG"] = w4, big
     t = timeit(lambda: ops.linear(x, w, b, r, act=act))
-    out.append(f"  w4={w4} big={big}: {t:8.1f} us  {fl / t / 1e6:7.0f} TF/s")
+    err = (ops.linear(x, w, b, r, act=act).float() - ref).abs().max().item()
+    out.append(f"  w4={w4} big={big}: {t:8.1f} us  {fl / t / 1e6:7.0f} TF/s  max|err| {err:.3g}")
 t = timeit(lambda: F.linear(x, w, b.to(torch.bfloat16)))
 out.append(f"  hipBLASLt plain: {t:8.1f} us  {fl / t / 1e6:7.0f} TF/s")
 print("\n".join(out), flush=True)
