@@ -15,6 +15,14 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 __host__ __device__ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 __host__ __device__ inline int64_t ceil_div(int64_t x, int64_t m) { return (x + m - 1) / m; }
 
+// blockIdx -> work index such that the blocks the dispatcher places on one XCD (orig % 8) get a
+// contiguous run of work indices (bijective for any n): neighbouring work units — the heads of
+// one batch row, sharing 128-B lines of a fused QKV row — then meet in the same XCD's L2.
+__device__ __forceinline__ int xcd_contiguous(int orig, int n) {
+  const int q = n / 8, r8 = n % 8, xcd = orig % 8;
+  return (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
+}
+
 // bf16 <-> f32 (bit patterns as uint16; RNE, inputs finite)
 __device__ __forceinline__ float bf2f(uint16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
 __device__ __forceinline__ uint16_t f2bf(float f) {

@@ -38,12 +38,15 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int MHA_KB = 128;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <int DT>
-__global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q, int64_t ldq,
+// occupancy targets (waves per SIMD; without them hipcc splits o into AGPRs and lands at 2 / 1):
+// head_dim <= 32 -> 4, <= 96 -> 3 (BERT 64, fusion 96), else 2
+template <int DT, bool MASK>
+__global__ __launch_bounds__(256, DT == 1 ? 4 : (DT <= 3 ? 3 : 2)) void mha_small(const uint16_t* __restrict__ q, int64_t ldq,
                                                  const uint16_t* __restrict__ k, int64_t ldk,
                                                  const uint16_t* __restrict__ v, int64_t ldv,
                                                  uint16_t* __restrict__ out, int64_t ldo,
-                                                 float* __restrict__ mean_out, int lq, int lk,
+                                                 float* __restrict__ mean_out,
+                                                 const int64_t* __restrict__ kmask, int lq, int lk,
                                                  int heads, int dh, float scale) {
   constexpr int DHP = DT * 32;
   constexpr int KS = DHP / 16;
@@ -52,13 +55,15 @@ __global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q,
   // transposed reads land on disjoint banks
   constexpr int VROW = DHP + ((DT & 1) ? 0 : 16);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int bi = blockIdx.x / heads, hh = blockIdx.x % heads;
+  const int unit = mmr::xcd_contiguous(blockIdx.x, gridDim.x);
+  const int bi = unit / heads, hh = unit % heads;
   const int lkp = (lk + 31) & ~31;
   uint16_t* Ks = (uint16_t*)smem;            // [MHA_KB][KROW]
   uint16_t* Vs = Ks + MHA_KB * KROW;         // [MHA_KB][VROW], natural (key-major) layout
   // [waves][DHP] per-wave partial means, after the larger of the K/V image and the epilogue area
   constexpr int KV_BYTES = MHA_KB * (KROW + VROW) * 2, RED_BYTES = 4 * DHP * 33 * 4;
   float* msum = (float*)(smem + (KV_BYTES > RED_BYTES ? KV_BYTES : RED_BYTES));
+  float* madd = msum + 4 * DHP;  // [MHA_KB] additive key mask of the current key block (kmask)
   const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6;
   const uint16_t* kbase = k + (int64_t)bi * lk * ldk + hh * dh;
   const uint16_t* vbase = v + (int64_t)bi * lk * ldv + hh * dh;
@@ -82,6 +87,7 @@ __global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q,
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) o[dt] = (f32x16){0};
   float m_run = -FLT_MAX, l_run = 0.f;
+  const float c2 = scale * 1.4426950408889634f;  // scale * log2(e)
   for (int k0 = 0; k0 < lkp; k0 += MHA_KB) {
     const int kn = min(MHA_KB, lkp - k0);   // keys staged this round (multiple of 32)
     __syncthreads();                          // previous key block consumed
@@ -112,15 +118,29 @@ __global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q,
         }
       }
     }
+    if constexpr (MASK)
+      for (int i = tid; i < kn; i += nthr) {
+        const int key = k0 + i;
+        madd[i] = (key < lk && kmask[(int64_t)bi * lk + key] != 0) ? 0.f : -FLT_MAX;
+      }
     __syncthreads();
     if (!active) continue;
     for (int kb = 0; kb < kn; kb += 64) {
       const int nt = min(64, kn - kb) / 32;
+      // with a key mask, 32-key tiles whose keys are all masked contribute exactly 0 (p = 2^-huge)
+      // once any key has been seen: skipped (BERT reports are padded to L, ~40 % of the keys)
+      bool live[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        live[t] = t < nt;
+        if (MASK && live[t] && k0 + kb + t * 32 > 0)
+          live[t] = __ballot(madd[kb + t * 32 + r] == 0.f) != 0;
+      }
       f32x16 s[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         s[t] = (f32x16){0};
-        if (t < nt) {
+        if (live[t]) {
           const int key = kb + t * 32 + r;
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks) {
@@ -129,40 +149,57 @@ __global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q,
           }
         }
       }
+      // softmax on raw scores with the scale folded into the exponent: p = 2^(s c - m c),
+      // c = scale * log2(e) (one fma + v_exp per score); without a key mask, keys past lk are
+      // masked only in the tile that holds them
       float mloc = -FLT_MAX;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        if (t < nt) {
+        if (live[t]) {
+          if constexpr (MASK) {
 #pragma unroll
-          for (int rg = 0; rg < 16; ++rg) {
-            const int key = k0 + kb + t * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * hf;
-            const float x = key < lk ? s[t][rg] * scale : -FLT_MAX;
-            s[t][rg] = x;
-            mloc = fmaxf(mloc, x);
+            for (int g = 0; g < 4; ++g) {
+              const float4 mv = *(const float4*)(madd + kb + t * 32 + 8 * g + 4 * hf);
+              s[t][4 * g] += mv.x;
+              s[t][4 * g + 1] += mv.y;
+              s[t][4 * g + 2] += mv.z;
+              s[t][4 * g + 3] += mv.w;
+            }
+          } else if (k0 + kb + t * 32 + 32 > lk) {  // wave-uniform
+#pragma unroll
+            for (int rg = 0; rg < 16; ++rg) {
+              const int key = k0 + kb + t * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * hf;
+              if (key >= lk) s[t][rg] = -FLT_MAX;
+            }
           }
+#pragma unroll
+          for (int rg = 0; rg < 16; ++rg) mloc = fmaxf(mloc, s[t][rg]);
         }
       }
       mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
       const float m_new = fmaxf(m_run, mloc);
-      const float alpha = __expf(m_run - m_new);
+      const float mc = m_new * c2;
+      const float alpha = __builtin_amdgcn_exp2f(fmaf(m_run, c2, -mc));  // 0 on the first block
       m_run = m_new;
       float psum = 0.f;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        if (t < nt) {
+        if (live[t]) {
 #pragma unroll
           for (int rg = 0; rg < 16; ++rg) {
-            const float p = __expf(s[t][rg] - m_new);
+            const float p = __builtin_amdgcn_exp2f(fmaf(s[t][rg], c2, -mc));
             s[t][rg] = p;
             psum += p;
           }
         }
       }
       l_run = l_run * alpha + psum;
+      if (k0 + kb > 0) {  // O is still zero before the first key block: nothing to rescale
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
+        for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-        for (int rg = 0; rg < 16; ++rg) o[dt][rg] *= alpha;
+          for (int rg = 0; rg < 16; ++rg) o[dt][rg] *= alpha;
+      }
       // O^T[d][q] += V^T[d][key] . P^T[key][q]; the V^T fragment (lane: d = its row, keys
       // kk..kk+3 and kk+8..kk+11 in P^T's register order) comes from the key-major V image by two
       // ds_read_b64_tr_b16: in each 16-lane group, lane 4q+p addresses row (key) r0+q, columns
@@ -170,12 +207,13 @@ __global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q,
       const int grp = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        if (t < nt) {
+        if (live[t]) {
 #pragma unroll
           for (int sidx = 0; sidx < 2; ++sidx) {
-            bf16x8 pf;
+            uint32_t pw[4];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) pf[j] = (short)f2bf(s[t][8 * sidx + j]);
+            for (int j = 0; j < 4; ++j) pw[j] = mmr::pack2bf(s[t][8 * sidx + 2 * j], s[t][8 * sidx + 2 * j + 1]);
+            const bf16x8 pf = __builtin_bit_cast(bf16x8, make_uint4(pw[0], pw[1], pw[2], pw[3]));
             const int r0 = kb + t * 32 + 16 * sidx + 4 * (grp >> 1);
 #pragma unroll
             for (int dt = 0; dt < DT; ++dt) {
@@ -209,10 +247,10 @@ __global__ __launch_bounds__(256) void mha_small(const uint16_t* __restrict__ q,
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           const int d = dt * 32 + 8 * g4 + 4 * hf;
-          bf16x4 w;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) w[j] = (short)f2bf(o[dt][4 * g4 + j] * inv);
-          *(bf16x4*)(st + r * OROW + d) = w;
+          uint2 w;
+          w.x = mmr::pack2bf(o[dt][4 * g4] * inv, o[dt][4 * g4 + 1] * inv);
+          w.y = mmr::pack2bf(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
+          *(uint2*)(st + r * OROW + d) = w;
         }
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes landed
       __builtin_amdgcn_wave_barrier();
@@ -377,34 +415,39 @@ __global__ __launch_bounds__(256) void rows_to_f32(const uint16_t* __restrict__ 
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
-}  // namespace
-
-// ================================================================== C ABI
-extern "C" {
-
-mmr_status mmr_mha(const uint16_t* q, int64_t ldq, const uint16_t* k, int64_t ldk, const uint16_t* v,
-                   int64_t ldv, uint16_t* out, int64_t ldo, float* mean_out, int32_t b, int32_t lq,
-                   int32_t lk, int32_t heads, int32_t dh, float scale, void* stream) {
-  mmr::clear_error();
-  MMR_REQUIRE(q && k && v && (out || mean_out), "mmr_mha: NULL pointer");
-  MMR_REQUIRE(b >= 0 && lq > 0 && lk > 0 && heads > 0, "mmr_mha: bad shape b=%d lq=%d lk=%d heads=%d", b, lq, lk, heads);
-  MMR_REQUIRE(dh > 0 && dh % 8 == 0 && dh <= 192, "mmr_mha: head_dim %d must be a multiple of 8 <= 192", dh);
+mmr_status launch_mha(const char* who, const uint16_t* q, int64_t ldq, const uint16_t* k, int64_t ldk,
+                      const uint16_t* v, int64_t ldv, uint16_t* out, int64_t ldo, float* mean_out,
+                      const int64_t* kmask, int32_t b, int32_t lq, int32_t lk, int32_t heads, int32_t dh,
+                      float scale, void* stream) {
+  MMR_REQUIRE(q && k && v && (out || mean_out), "%s: NULL pointer", who);
+  MMR_REQUIRE(b >= 0 && lq > 0 && lk > 0 && heads > 0, "%s: bad shape b=%d lq=%d lk=%d heads=%d", who, b, lq, lk,
+              heads);
+  MMR_REQUIRE(dh > 0 && dh % 8 == 0 && dh <= 192, "%s: head_dim %d must be a multiple of 8 <= 192", who, dh);
   MMR_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && (!out || ldo % 4 == 0),
-              "mmr_mha: row strides must be multiples of 8 elements (16 B)");
+              "%s: row strides must be multiples of 8 elements (16 B)", who);
   MMR_REQUIRE(ldq >= (int64_t)heads * dh && ldk >= (int64_t)heads * dh && ldv >= (int64_t)heads * dh &&
-              (!out || ldo >= (int64_t)heads * dh), "mmr_mha: row stride below heads*dh");
+              (!out || ldo >= (int64_t)heads * dh), "%s: row stride below heads*dh", who);
   MMR_REQUIRE(aligned16(q) && aligned16(k) && aligned16(v) && (!out || ((uintptr_t)out & 7u) == 0),
-              "mmr_mha: operands must be 16-B aligned");
+              "%s: operands must be 16-B aligned", who);
   if (b == 0) return MMR_OK;
   const int dt = (dh + 31) / 32;
   const size_t kv_bytes = (size_t)MHA_KB * (dt * 32 + 8) * 2 + (size_t)MHA_KB * (dt * 32 + ((dt & 1) ? 0 : 16)) * 2;
-  const size_t lds = std::max(kv_bytes, (size_t)4 * dt * 32 * 33 * 4) + (size_t)4 * dt * 32 * 4;
+  const size_t lds =
+      std::max(kv_bytes, (size_t)4 * dt * 32 * 33 * 4) + (size_t)4 * dt * 32 * 4 + (size_t)MHA_KB * 4;
   const int nqt = (lq + 31) / 32, nchunk = (lq + 127) / 128;
   const dim3 grid((unsigned)((int64_t)b * heads), (unsigned)nchunk), blk(64 * std::min(4, nqt));
   hipStream_t st = mmr::as_stream(stream);
   if (mean_out && nchunk > 1)  // query chunks accumulate their partial means
     MMR_CHECK_HIP(hipMemsetAsync(mean_out, 0, sizeof(float) * (size_t)b * heads * dh, st));
-#define MMR_MHA(D) mha_small<D><<<grid, blk, lds, st>>>(q, ldq, k, ldk, v, ldv, out, ldo, mean_out, lq, lk, heads, dh, scale)
+#define MMR_MHA(D)                                                                                             \
+  do {                                                                                                         \
+    if (kmask)                                                                                                 \
+      mha_small<D, true><<<grid, blk, lds, st>>>(q, ldq, k, ldk, v, ldv, out, ldo, mean_out, kmask, lq, lk,    \
+                                                 heads, dh, scale);                                            \
+    else                                                                                                       \
+      mha_small<D, false><<<grid, blk, lds, st>>>(q, ldq, k, ldk, v, ldv, out, ldo, mean_out, nullptr, lq, lk, \
+                                                  heads, dh, scale);                                           \
+  } while (0)
   switch (dt) {
     case 1: MMR_MHA(1); break;
     case 2: MMR_MHA(2); break;
@@ -416,6 +459,31 @@ mmr_status mmr_mha(const uint16_t* q, int64_t ldq, const uint16_t* k, int64_t ld
 #undef MMR_MHA
   MMR_LAUNCH_CHECK();
   return MMR_OK;
+}
+
+}  // namespace
+
+// ================================================================== C ABI
+extern "C" {
+
+mmr_status mmr_mha(const uint16_t* q, int64_t ldq, const uint16_t* k, int64_t ldk, const uint16_t* v,
+                   int64_t ldv, uint16_t* out, int64_t ldo, float* mean_out, int32_t b, int32_t lq,
+                   int32_t lk, int32_t heads, int32_t dh, float scale, void* stream) {
+  mmr::clear_error();
+  return launch_mha("mmr_mha", q, ldq, k, ldk, v, ldv, out, ldo, mean_out, nullptr, b, lq, lk, heads, dh, scale,
+                    stream);
+}
+
+// BERT self-attention (HF BertSelfAttention, eval) on the same kernel: Q / K / V are the column
+// blocks of the fused QKV rows; key padding mask01 (0 -> masked; fully masked 32-key tiles skipped)
+mmr_status mmr_bert_attention(const uint16_t* qkv, const int64_t* mask01, uint16_t* ctx, int32_t b, int32_t l,
+                              int32_t h, int32_t dh, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(qkv && mask01 && ctx, "mmr_bert_attention: NULL pointer");
+  MMR_REQUIRE(h > 0 && dh > 0, "mmr_bert_attention: bad shape h=%d dh=%d", h, dh);
+  const int64_t C = (int64_t)h * dh;
+  return launch_mha("mmr_bert_attention", qkv, 3 * C, qkv + C, 3 * C, qkv + 2 * C, 3 * C, ctx, C, nullptr, mask01,
+                    b, l, l, h, dh, 1.0f / sqrtf((float)dh), stream);
 }
 
 mmr_status mmr_add_pos_bf16(const void* x, int32_t x_is_f32, const float* pos, uint16_t* y, int64_t rows,

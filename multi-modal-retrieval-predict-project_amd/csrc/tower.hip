@@ -129,144 +129,6 @@ __global__ __launch_bounds__(256) void bert_embed(const int64_t* __restrict__ id
     y[tok * c + k] = f2bf((wr[k] + pr[k] + type0[k] - mean) * rstd * g[k] + b[k]);
 }
 
-// ------------------------------------------------------------------ BERT self-attention core
-// Block = (batch, head), 4 waves; each wave owns 32-query tiles.  Swapped product S^T = K . Q^T
-// with v_mfma_f32_32x32x16_bf16 puts the query on the lane and the keys in the registers, so the
-// softmax row reductions are in-register + one lane^32 exchange, and P^T feeds the P.V MFMA as
-// its B operand with no data movement (cdna_hip_programming.md §3).  K is staged in LDS as
-// 128-B rows (swizzled 16-B chunks), V transposed as [d][key] rows padded by 8 B (conflict-free
-// ds_read_b64).  Keys are processed in blocks of 128 with an online softmax (L <= 512).
-constexpr int BA_DH = 64;
-constexpr int BA_KBLK = 128;
-
-__device__ __forceinline__ int kswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
-
-__global__ __launch_bounds__(256) void bert_attention(const uint16_t* __restrict__ qkv,
-                                                      const int64_t* __restrict__ mask01,
-                                                      uint16_t* __restrict__ ctx, int l, int h) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int C = h * BA_DH;
-  const int bi = blockIdx.x / h, hh = blockIdx.x % h;
-  const int vt_stride = l + 4;  // bf16 elements per V^T row (l*2 + 8 bytes)
-  uint16_t* Ks = (uint16_t*)smem;                 // [l][64]
-  uint16_t* Vt = Ks + (size_t)l * BA_DH;          // [64][l+4]
-  float* madd = (float*)(Vt + (size_t)BA_DH * vt_stride);  // [l] additive mask
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint16_t* base = qkv + (int64_t)bi * l * 3 * C;
-
-  // stage K (swizzled rows) and V^T
-  for (int c = tid; c < l * 8; c += 256) {
-    const int key = c >> 3, ch = c & 7;
-    const uint16_t* src = base + (int64_t)key * 3 * C + hh * BA_DH;
-    *(bf16x8*)(Ks + key * BA_DH + kswz(key, ch) * 8) = *(const bf16x8*)(src + C + ch * 8);
-    bf16x8 v = *(const bf16x8*)(src + 2 * C + ch * 8);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) Vt[(ch * 8 + j) * vt_stride + key] = (uint16_t)v[j];
-  }
-  for (int k = tid; k < l; k += 256) madd[k] = mask01[(int64_t)bi * l + k] ? 0.0f : -FLT_MAX;
-  __syncthreads();
-
-  const float scale = 0.125f;  // 1/sqrt(64)
-  const int r = lane & 31, hf = lane >> 5;
-  for (int qt = wave; qt < l / 32; qt += 4) {
-    const int q = qt * 32 + r;
-    const uint16_t* qrow = base + (int64_t)q * 3 * C + hh * BA_DH;
-    bf16x8 qf[4];
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) qf[ks] = *(const bf16x8*)(qrow + ks * 16 + 8 * hf);
-    f32x16 o0 = {0}, o1 = {0};
-    float m_run = -FLT_MAX, l_run = 0.f;
-    for (int kb = 0; kb < l; kb += BA_KBLK) {
-      const int nt = min(BA_KBLK, l - kb) / 32;
-      f32x16 s[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        s[t] = (f32x16){0};
-        if (t < nt) {
-          const int key = kb + t * 32 + r;
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks) {
-            const bf16x8 kf = *(const bf16x8*)(Ks + key * BA_DH + kswz(key, ks * 2 + hf) * 8);
-            s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[t], 0, 0, 0);
-          }
-        }
-      }
-      // scale + mask, block max
-      float mloc = -FLT_MAX;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        if (t < nt) {
-#pragma unroll
-          for (int rg = 0; rg < 16; ++rg) {
-            const int key = kb + t * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * hf;
-            const float v = s[t][rg] * scale + madd[key];
-            s[t][rg] = v;
-            mloc = fmaxf(mloc, v);
-          }
-        }
-      }
-      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-      const float m_new = fmaxf(m_run, mloc);
-      const float alpha = __expf(m_run - m_new);
-      m_run = m_new;
-      float psum = 0.f;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        if (t < nt) {
-#pragma unroll
-          for (int rg = 0; rg < 16; ++rg) {
-            const float p = __expf(s[t][rg] - m_new);
-            s[t][rg] = p;
-            psum += p;
-          }
-        }
-      }
-      l_run = l_run * alpha + psum;
-#pragma unroll
-      for (int rg = 0; rg < 16; ++rg) {
-        o0[rg] *= alpha;
-        o1[rg] *= alpha;
-      }
-      // O^T[d][q] += V^T[d][key] . P^T[key][q]
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        if (t < nt) {
-#pragma unroll
-          for (int sidx = 0; sidx < 2; ++sidx) {
-            bf16x8 pf;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) pf[j] = (short)f2bf(s[t][8 * sidx + j]);
-            const int kbase = kb + t * 32 + 16 * sidx + 4 * hf;
-#pragma unroll
-            for (int dt = 0; dt < 2; ++dt) {
-              const uint16_t* vrow = Vt + (dt * 32 + r) * vt_stride;
-              const bf16x4 lo = *(const bf16x4*)(vrow + kbase);
-              const bf16x4 hi = *(const bf16x4*)(vrow + kbase + 8);
-              const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-              if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o0, 0, 0, 0);
-              else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o1, 0, 0, 0);
-            }
-          }
-        }
-      }
-    }
-    const float inv = 1.0f / (l_run + __shfl_xor(l_run, 32, 64));
-    uint16_t* orow = ctx + ((int64_t)bi * l + q) * C + hh * BA_DH;
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int d = 8 * g4 + 4 * hf;
-      bf16x4 w0, w1;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        w0[j] = (short)f2bf(o0[4 * g4 + j] * inv);
-        w1[j] = (short)f2bf(o1[4 * g4 + j] * inv);
-      }
-      *(bf16x4*)(orow + d) = w0;
-      *(bf16x4*)(orow + 32 + d) = w1;
-    }
-  }
-}
-
 // ------------------------------------------------------------------ Swin (shifted) window attention
 // One wave per (image, window, head); 4 units per block.  Window of ws*ws = 49 tokens padded to
 // 64, head_dim 32.  The cyclic shift + window partition are folded into the token gather (and
@@ -760,20 +622,6 @@ mmr_status mmr_bert_embed(const int64_t* ids, const float* word, const float* po
   if (ntok == 0) return MMR_OK;
   bert_embed<<<dim3((unsigned)mmr::ceil_div(ntok, 4)), 256, 0, mmr::as_stream(stream)>>>(
       ids, word, pos, type0, gamma, beta, y, ntok, l, c, eps);
-  MMR_LAUNCH_CHECK();
-  return MMR_OK;
-}
-
-mmr_status mmr_bert_attention(const uint16_t* qkv, const int64_t* mask01, uint16_t* ctx,
-                              int32_t b, int32_t l, int32_t h, int32_t dh, void* stream) {
-  mmr::clear_error();
-  MMR_REQUIRE(qkv && mask01 && ctx, "mmr_bert_attention: NULL pointer");
-  MMR_REQUIRE(dh == BA_DH, "mmr_bert_attention: head_dim %d (only 64 built)", dh);
-  MMR_REQUIRE(l > 0 && l <= 512 && l % 32 == 0, "mmr_bert_attention: L=%d must be a multiple of 32 <= 512", l);
-  MMR_REQUIRE(b >= 0 && h > 0, "mmr_bert_attention: bad shape");
-  if (b == 0) return MMR_OK;
-  const size_t lds = (size_t)l * BA_DH * 2 + (size_t)BA_DH * (l + 4) * 2 + (size_t)l * 4;
-  bert_attention<<<dim3((unsigned)(b * h)), 256, lds, mmr::as_stream(stream)>>>(qkv, mask01, ctx, l, h);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }
