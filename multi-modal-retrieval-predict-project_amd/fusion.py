@@ -179,7 +179,9 @@ class FusionStack:
         # projection) depends only on the image tower: it runs on a side stream, ahead of and
         # concurrently with the text-side work, which waits per layer on an event before the
         # cross attentions (MMR_FUSION_STREAMS=0: one stream)
-        two = os.environ.get("MMR_FUSION_STREAMS", "1") != "0"
+        # (first call in sequence: see MultiModalRetrievalModel._towers)
+        two = getattr(self, "_warm", False) and os.environ.get("MMR_FUSION_STREAMS", "1") != "0"
+        self._warm = True
         main = torch.cuda.current_stream(dev)
         side = self._side_stream() if two else main
         pq, pp, ev = [], [], []

@@ -91,6 +91,7 @@ class MultiModalRetrievalModel:
         self.use_cls_only = use_cls_only
         self.retriever = retriever
         self._side = None
+        self._warm = False
         hs = head_state if head_state is not None else init_head_state(self.backbones.img_dim,
                                                                        self.backbones.txt_dim, joint_dim, seed + 2)
         f = lambda k: hs[k].detach().to(self.device, torch.float32).contiguous()  # noqa: E731
@@ -160,8 +161,12 @@ class MultiModalRetrievalModel:
     def _towers(self, image, input_ids, attention_mask, want_patches):
         """Both towers, the Swin tower on a side stream so its kernels fill the CUs the BERT
         kernels leave idle (wave-quantisation tails, small LayerNorm / attention launches); the
-        two towers share no data until the heads.  MMR_TOWER_STREAMS=0 runs them in sequence."""
-        if os.environ.get("MMR_TOWER_STREAMS", "1") == "0":
+        two towers share no data until the heads.  The first call runs them in sequence: the GEMM
+        launcher times its variants per shape on first use, which concurrent kernels would skew.
+        MMR_TOWER_STREAMS=0 always runs them in sequence."""
+        first = not self._warm
+        self._warm = True
+        if first or os.environ.get("MMR_TOWER_STREAMS", "1") == "0":
             return (self.backbones.encode_image(image, want_patches=want_patches),
                     self.backbones.encode_text(input_ids, attention_mask))
         main = torch.cuda.current_stream(self.device)
