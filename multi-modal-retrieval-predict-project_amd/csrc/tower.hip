@@ -32,9 +32,10 @@ __device__ __forceinline__ void store8(uint16_t* p, const float* v) {
 
 // ------------------------------------------------------------------ LayerNorm
 // LPR lanes per row (64/LPR rows per wave) so narrow Swin rows (C = 96..384) keep every lane busy;
-// the row stays in registers (<= 8 chunks of 8 per lane): one read, one write, exact two-pass
+// the row stays in registers (<= NC chunks of 8 per lane; NC sized to the launch so the register
+// file, and with it the occupancy, follows the row width): one read, one write, exact two-pass
 // (centred) variance like torch.
-template <int LPR, bool ADD>
+template <int LPR, int NC, bool ADD>
 __global__ __launch_bounds__(256) void layernorm_bf16(const uint16_t* __restrict__ x,
                                                       const uint16_t* __restrict__ r,
                                                       const float* __restrict__ g,
@@ -50,10 +51,10 @@ __global__ __launch_bounds__(256) void layernorm_bf16(const uint16_t* __restrict
   const uint16_t* xr = x + (ok ? row : 0) * c;
   const int nch = c / 8;
   const float av = alpha ? *alpha : 1.f;  // learned scale of x (PreFusionEnhancer alpha, fusion.py:34)
-  float v[8][8];
+  float v[NC][8];
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < NC; ++i) {
     const int ch = sub + i * LPR;
     if (ok && ch < nch) {
       load8(xr + ch * 8, v[i]);
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(256) void layernorm_bf16(const uint16_t* __restrict
   const float mean = s / c;
   float ss = 0.f;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < NC; ++i) {
     const int ch = sub + i * LPR;
     if (ok && ch < nch) {
 #pragma unroll
@@ -87,7 +88,7 @@ __global__ __launch_bounds__(256) void layernorm_bf16(const uint16_t* __restrict
   for (int o = LPR / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
   const float rstd = rsqrtf(ss / c + eps);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < NC; ++i) {
     const int ch = sub + i * LPR;
     if (ok && ch < nch) {
       const float4 g0 = *(const float4*)(g + ch * 8), g1 = *(const float4*)(g + ch * 8 + 4);
@@ -565,27 +566,35 @@ static mmr_status layernorm_launch(const uint16_t* x, const uint16_t* r, const f
   if (rows == 0) return MMR_OK;
   hipStream_t st = mmr::as_stream(stream);
   const int nch = c / 8;
-  // lanes per row: the narrowest LPR that splits the row's 16-B chunks evenly into <= 6 per lane
-  // (no idle lanes, several loads in flight per lane; measured best on the BERT/Swin widths);
-  // otherwise <= 2 chunks per lane for narrow rows
+  // lanes per row: the narrowest LPR that splits the row's 16-B chunks evenly into <= 3 per lane
+  // (no idle lanes, the NC = 3 instantiation at 56 VGPRs = 8 waves/SIMD; measured 3-6 % faster
+  // than <= 6 per lane on the BERT/Swin widths, tools/ln_bench.py); then <= 6; otherwise <= 2
+  // chunks per lane for narrow rows
   int lpr = 0;
-  for (int l = 8; l <= 64 && !lpr; l *= 2)
-    if (nch % l == 0 && nch / l <= 6) lpr = l;
+  for (int lim = 3; lim <= 6 && !lpr; lim += 3)
+    for (int l = 8; l <= 64 && !lpr; l *= 2)
+      if (nch % l == 0 && nch / l <= lim) lpr = l;
   if (!lpr) {
     lpr = 64;
     while (lpr > 8 && nch <= (lpr / 2) * 2) lpr /= 2;
   }
-  if (const char* e = getenv("MMR_LN_LPR")) lpr = atoi(e);  // diagnostic override (8/16/32/64)
+  if (const char* e = getenv("MMR_LN_LPR")) {  // diagnostic override (8/16/32/64; <= 8 chunks per lane)
+    const int l = atoi(e);
+    if ((l == 8 || l == 16 || l == 32 || l == 64) && (nch + l - 1) / l <= 8) lpr = l;
+  }
+  const int cpl = (nch + lpr - 1) / lpr;                   // chunks per lane
   const int64_t rows_per_block = 4 * (64 / lpr);
   const dim3 grid((unsigned)mmr::ceil_div(rows, rows_per_block));
-#define MMR_LN(L)                                                                           \
-  (r ? layernorm_bf16<L, true><<<grid, 256, 0, st>>>(x, r, gamma, beta, y, rows, c, eps, alpha)    \
-     : layernorm_bf16<L, false><<<grid, 256, 0, st>>>(x, r, gamma, beta, y, rows, c, eps, alpha))
+#define MMR_LN2(L, N)                                                                                \
+  (r ? layernorm_bf16<L, N, true><<<grid, 256, 0, st>>>(x, r, gamma, beta, y, rows, c, eps, alpha) \
+     : layernorm_bf16<L, N, false><<<grid, 256, 0, st>>>(x, r, gamma, beta, y, rows, c, eps, alpha))
+#define MMR_LN(L) (cpl <= 3 ? MMR_LN2(L, 3) : (cpl <= 6 ? MMR_LN2(L, 6) : MMR_LN2(L, 8)))
   if (lpr == 8) MMR_LN(8);
   else if (lpr == 16) MMR_LN(16);
   else if (lpr == 32) MMR_LN(32);
   else MMR_LN(64);
 #undef MMR_LN
+#undef MMR_LN2
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }
