@@ -116,8 +116,6 @@ def main():
 
     for _ in range(a.warmup):
         step(False)
-    if model is not None:
-        model.backbones.bert.ffn1_events = []
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -135,6 +133,21 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_search = sum(e0.elapsed_time(e1) for e0, e1 in ev_pairs) / max(len(ev_pairs), 1)
+    if model is not None:
+        # roofline kernel (BERT FFN1) timed in a short pass right after the timed region with the
+        # towers in sequence: inside the timed steps the Swin tower runs concurrently on a side
+        # stream, and events around one kernel would also count the co-running kernels' share
+        saved = {k: os.environ.get(k) for k in ("MMR_TOWER_STREAMS", "MMR_FUSION_STREAMS")}
+        os.environ.update({k: "0" for k in saved})
+        model.backbones.bert.ffn1_events = []
+        for _ in range(3):
+            step(False)
+        torch.cuda.synchronize(dev)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
     # whole-job throughput: every rank embeds B queries; every query is scored against the whole
     # world*n gallery (each rank scores all world*B queries against its n rows)
@@ -160,7 +173,8 @@ def main():
         fl = 2.0 * B * 128 * 3072 * 768
         roof = {"bound": "mfma", "achieved": fl / (ms_ffn1 / 1e3) / 1e12, "peak": peak_bf16 / 1e12,
                 "unit": "TFLOP/s", "traffic": None,
-                "kernel": "gemm_bf16_tn<GELU> BERT FFN1 (M=%d, N=3072, K=768), %d launches timed" % (B * 128, len(evs)),
+                "kernel": ("BERT FFN1 GEMM + GELU (M=%d, N=3072, K=768; tuned variant), %d launches timed in a "
+                           "towers-in-sequence pass after the timed region" % (B * 128, len(evs))),
                 "ms_per_launch": ms_ffn1, "flops_per_launch": fl, "knn": knn_roof}
     else:
         if knn_roof["bound"] == "mfma":
@@ -173,9 +187,15 @@ def main():
     # HBM traffic per launch from the committed PMC pass (tools/pmc_traffic.py; FETCH_SIZE x2 per the
     # gfx950 correction + WRITE_SIZE), for the same kernels at the same shapes
     tr = pmc_traffic()
-    if model is not None and "bert_ffn1" in tr:
-        roof["traffic"] = tr["bert_ffn1"]["hbm_bytes"]
-        roof["traffic_source"] = tr["bert_ffn1"]["source"]
+    if model is not None:
+        # the FFN1 launch variant the per-shape tuner settled on here; its PMC record if committed
+        from mmr_amd import _lib
+        var = int(_lib.lib().mmr_linear_bf16_variant(B * 128, 3072, 768, 1, 1, 0))
+        roof["variant"] = var
+        rec = tr.get(f"bert_ffn1_v{var}")
+        if rec is not None:
+            roof["traffic"] = rec["hbm_bytes"]
+            roof["traffic_source"] = rec["source"]
     if model is None and "knn_scores_x3" in tr and "knn_select" in tr and B == 256 and n == 100_000 and d == 768:
         roof["traffic"] = tr["knn_scores_x3"]["hbm_bytes"] + tr["knn_select"]["hbm_bytes"]
         roof["traffic_source"] = tr["knn_scores_x3"]["source"]

@@ -110,6 +110,12 @@ mmr_status mmr_linear_bf16(const uint16_t* x, const uint16_t* w, const float* bi
                            const uint16_t* residual, uint16_t* y, int64_t m, int32_t n, int32_t k,
                            int32_t act, void* stream);
 
+/* The launch variant mmr_linear_bf16 settled on for this shape / epilogue on the current device
+ * (the first call per shape times the variants and keeps the fastest), or -1 before that call.
+ * Diagnostic: lets a benchmark name the kernel it measured. */
+int32_t mmr_linear_bf16_variant(int64_t m, int32_t n, int32_t k, int32_t act, int32_t has_bias,
+                                int32_t has_residual);
+
 /* Row LayerNorm over c channels (bf16 in/out, f32 math, gamma/beta f32). */
 mmr_status mmr_layernorm_bf16(const uint16_t* x, const float* gamma, const float* beta,
                               uint16_t* y, int64_t rows, int32_t c, float eps, void* stream);

@@ -31,6 +31,7 @@ SIGNATURES = {
                          ctypes.c_double, ctypes.c_double, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "mmr_merge_topk": [c_vp, c_vp, c_i32, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp],
     "mmr_linear_bf16": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp],
+    "mmr_linear_bf16_variant": [c_i64, c_i32, c_i32, c_i32, c_i32, c_i32],
     "mmr_layernorm_bf16": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp],
     "mmr_add_layernorm_bf16": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp],
     "mmr_scaled_add_layernorm_bf16": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp],
@@ -61,6 +62,7 @@ SIGNATURES = {
     "mmr_rows_to_f32": [c_vp, c_i64, c_vp, c_i32, c_i32, c_vp],
 }
 _RESTYPES = {"mmr_last_error": ctypes.c_char_p, "mmr_version": ctypes.c_int, "mmr_max_k": ctypes.c_int,
+             "mmr_linear_bf16_variant": ctypes.c_int32,
              "mmr_swin_mlp_pack_elems": ctypes.c_int64, "mmr_swin_attn_block_pack_bytes": ctypes.c_int64}
 
 _lib = None

@@ -783,6 +783,15 @@ int tuned_variant(int64_t m, int n, int k, int act, bool hb, bool hr, const void
 
 }  // namespace
 
+extern "C" int32_t mmr_linear_bf16_variant(int64_t m, int32_t n, int32_t k, int32_t act, int32_t has_bias,
+                                           int32_t has_residual) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  auto it = g_tuned.find(std::make_pair(dev, TuneKey{m, n, k, act, has_bias ? 1 : 0, has_residual ? 1 : 0}));
+  return it == g_tuned.end() ? -1 : it->second;
+}
+
 extern "C" mmr_status mmr_linear_bf16(const uint16_t* x, const uint16_t* w, const float* bias,
                                       const uint16_t* residual, uint16_t* y, int64_t m, int32_t n,
                                       int32_t k, int32_t act, void* stream) {

@@ -40,5 +40,6 @@ def test_errors_without_gpu(lib):
     assert st == 1 and b"NULL" in L.mmr_last_error()
     st = L.mmr_linear_bf16(None, None, None, None, None, 4, 8, 8, 0, None)
     assert st == 1
-    st = L.mmr_bert_attention(ctypes.c_void_p(16), ctypes.c_void_p(16), ctypes.c_void_p(16), 1, 100, 12, 64, None)
-    assert st == 1 and b"L=100" in L.mmr_last_error()
+    st = L.mmr_bert_attention(ctypes.c_void_p(16), ctypes.c_void_p(16), ctypes.c_void_p(16), 1, 100, 12, 60, None)
+    assert st == 1 and b"head_dim 60" in L.mmr_last_error()
+    assert L.mmr_linear_bf16_variant(32768, 3072, 768, 1, 1, 0) == -1  # nothing tuned in this process

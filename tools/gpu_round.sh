@@ -23,7 +23,7 @@ for s in $STEPS; do
       timeout -k 10 300 python -u bench.py --mode knn > "$OUT/bench_knn.json" 2> "$OUT/bench_knn.err"
       cat "$OUT/bench_knn.json" ;;
     prof)
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o full \
+      MMR_TOWER_STREAMS=0 MMR_FUSION_STREAMS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o full \
         -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/prof_full.log" 2>&1
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o knn \
         -- python bench.py --mode knn --steps 20 --warmup 3 --no-cpu-baseline > "$OUT/prof_knn.log" 2>&1
@@ -39,6 +39,15 @@ for s in $STEPS; do
       timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc" -o kwrite \
         -- python bench.py --mode knn --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/pmc_kwrite.log" 2>&1
       ls -R "$OUT/pmc" | head -20 ;;
+    pmcg)
+      # FFN1 GEMM traffic per candidate launch variant (the tuner's pick varies by box)
+      for v in 0 1 2 7; do
+        for c in FETCH_SIZE WRITE_SIZE; do
+          timeout -s KILL 60 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmcg" -o "v${v}_$c" \
+            -- python tools/pmc_gemm.py 32768 3072 768 1 $v > "$OUT/pmcg_v${v}_$c.log" 2>&1
+        done
+      done
+      ls "$OUT/pmcg" | head -20 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

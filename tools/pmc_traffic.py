@@ -4,7 +4,8 @@ FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts exactly half t
 (16 B/lane) streaming reads — global_load and buffer_load ... lds alike — so it is doubled;
 WRITE_SIZE is exact for 16-B streaming stores.
 
-usage: python tools/pmc_traffic.py <out.json> <tag> name=<fetch.csv>,<write.csv>,<kernel substring> ...
+usage: python tools/pmc_traffic.py <out.json> <tag> name=<fetch.csv>,<write.csv>,<kernel substring>[@grid] ...
+(@grid: keep only dispatches with that Grid_Size, i.e. one GEMM shape of a kernel instantiation)
 Writes {name: {"kernel", "dispatches", "fetch_bytes", "write_bytes", "hbm_bytes", "source"}}."""
 import collections
 import csv
@@ -12,9 +13,11 @@ import json
 import sys
 
 
-def per_dispatch(path, sub, counter):
+def per_dispatch(path, sub, counter, grid=None):
     tot = collections.defaultdict(float)
     for r in csv.DictReader(open(path)):
+        if grid is not None and r["Grid_Size"] != grid:
+            continue
         if sub in r["Kernel_Name"] and r["Counter_Name"] == counter:
             tot[r["Dispatch_Id"]] += float(r["Counter_Value"])
     if not tot:
@@ -28,10 +31,13 @@ def main():
     for spec in sys.argv[3:]:
         name, rest = spec.split("=", 1)
         fetch_csv, write_csv, sub = rest.split(",", 2)
-        f_kib, nf = per_dispatch(fetch_csv, sub, "FETCH_SIZE")
-        w_kib, nw = per_dispatch(write_csv, sub, "WRITE_SIZE")
+        grid = None
+        if "@" in sub:
+            sub, grid = sub.rsplit("@", 1)
+        f_kib, nf = per_dispatch(fetch_csv, sub, "FETCH_SIZE", grid)
+        w_kib, nw = per_dispatch(write_csv, sub, "WRITE_SIZE", grid)
         fb, wb = 2.0 * f_kib * 1024.0, w_kib * 1024.0
-        res[name] = {"kernel": sub, "dispatches": [nf, nw], "fetch_bytes": fb, "write_bytes": wb,
+        res[name] = {"kernel": sub + (f" (grid {grid})" if grid else ""), "dispatches": [nf, nw], "fetch_bytes": fb, "write_bytes": wb,
                      "hbm_bytes": fb + wb, "source": f"{tag}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) / WRITE_SIZE"}
         print(f"{name:12s} fetch {fb / 1e6:9.2f} MB  write {wb / 1e6:9.2f} MB  per dispatch ({nf}/{nw} dispatches)")
     json.dump(res, open(out, "w"), indent=1)
