@@ -141,7 +141,7 @@ mmr_status mmr_bert_embed(const int64_t* ids, const float* word, const float* po
 
 /* BERT self-attention core (HF BertSelfAttention, eval): qkv bf16 (b*l, 3*h*dh) [q|k|v],
  * additive mask from mask01 (b, l) int64 (0 -> masked), softmax(q k^T / sqrt(dh)) v -> ctx bf16
- * (b*l, h*dh).  l <= 512, dh = 64. */
+ * (b*l, h*dh).  Any l; dh % 8 == 0, dh <= 192 (the mmr_mha kernel with a key mask). */
 mmr_status mmr_bert_attention(const uint16_t* qkv, const int64_t* mask01, uint16_t* ctx,
                               int32_t b, int32_t l, int32_t h, int32_t dh, void* stream);
 

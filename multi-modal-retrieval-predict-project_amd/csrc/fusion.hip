@@ -21,12 +21,13 @@ typedef short bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // ------------------------------------------------------------------ small-sequence MHA core
-// softmax(q k^T * scale) v per (batch, head) for the fusion's short sequences (text L <= 512,
-// 49 patches, 51-token fused sequence), no masks.  Block = (batch*head, chunk of 128 queries), one
-// 32-query tile per wave; keys stream through LDS in blocks of MHA_KB with an online softmax.  As
-// in bert_attention (tower.hip): the swapped product S^T = K . Q^T on v_mfma_f32_32x32x16_bf16 puts
-// the query on the lane, the softmax reductions stay in registers, and P^T feeds the P.V MFMA as
-// its B operand with no data movement (V^T read in the matching key permutation).  head_dim is
+// softmax(q k^T * scale) v per (batch, head): the fusion's short sequences (text L <= 512,
+// 49 patches, 51-token fused sequence; no masks) and BERT self-attention (MASK: key-padding mask,
+// HF BertSelfAttention).  Block = (batch*head, chunk of 128 queries), one 32-query tile per wave;
+// keys stream through LDS in blocks of MHA_KB with an online softmax.  The swapped product
+// S^T = K . Q^T on v_mfma_f32_32x32x16_bf16 puts the query on the lane, the softmax reductions
+// stay in registers, and P^T feeds the P.V MFMA as its B operand with no data movement (V^T read
+// in the matching key permutation).  head_dim is
 // padded to DT*32 with zeros (dh % 8 == 0); ragged query/key counts are padded to 32 (padded keys
 // -> -inf, padded queries never stored).  Operands are strided rows (q row (b*lq + i) at
 // q + row*ldq + head*dh), so Q/K/V are read in place from packed projection outputs.  Optional f32
