@@ -6,6 +6,9 @@
 //
 // Pipeline per search (all on the caller's stream):
 //   1. knn_prep_queries   q -> qn = q/|q| (f32, padded [Qp][Dp]) + |q| in f64.
+//   (Q <= 32, mode x3)    skinny path instead of 2.: knn_scan_f32_gmax streams the tile16 copy of the
+//                         gallery once on f32 MFMA (HBM-bound, ~5.3 TB/s at 100k x 768) into the
+//                         same row-group maxima, then knn_select_groups with the f32-mode delta.
 //   2. knn_scores_x3_gmax (default) S = (qn . g) / |g| as a bf16 "3-term split" MFMA GEMM: every
 //                         operand is split into hi + lo bf16 (hi = bf16(x), lo = bf16(x - hi)) and
 //                         s ~= q_hi.g_hi + q_hi.g_lo + q_lo.g_hi (dropped terms <= 3*2^-16 |q||g|),
@@ -89,15 +92,23 @@ __global__ __launch_bounds__(256) void knn_prep_gallery(const float* __restrict_
   }
 }
 
+// MFMA-native 16-row tile layout of knn_scan_f32_gmax: element (row, k) of a [rows][Dp] matrix at
+// ((row/16)*(Dp/16) + k/16)*256 + ((k%16)/4*16 + row%16)*4 + k%4 — lane l = 16h + r of a wave then
+// reads rows r, floats 4h..4h+3 of a 16-float chunk as one contiguous 1-KB wave load.
+__host__ __device__ __forceinline__ int64_t tile16_index(int64_t row, int k, int Dp) {
+  return ((row >> 4) * (Dp >> 4) + (k >> 4)) * 256 + ((((k & 15) >> 2) << 4) + (row & 15)) * 4 + (k & 3);
+}
+
 __global__ __launch_bounds__(256) void knn_prep_queries(const float* __restrict__ q, int64_t nq,
                                                         int d, float* __restrict__ qn, int Dp,
-                                                        int64_t Qp, double* __restrict__ qnorm64) {
+                                                        int64_t Qp, double* __restrict__ qnorm64,
+                                                        int tiled = 0) {
   int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   int lane = threadIdx.x & 63;
   if (row >= Qp) return;
-  float* out = qn + row * Dp;
+  auto at = [&](int k) -> float& { return tiled ? qn[tile16_index(row, k, Dp)] : qn[row * Dp + k]; };
   if (row >= nq) {
-    for (int k = lane; k < Dp; k += 64) out[k] = 0.0f;
+    for (int k = lane; k < Dp; k += 64) at(k) = 0.0f;
     return;
   }
   const float* in = q + row * (int64_t)d;
@@ -106,7 +117,7 @@ __global__ __launch_bounds__(256) void knn_prep_queries(const float* __restrict_
   ss = mmr::wave_sum(ss);
   double nrm = sqrt(ss);
   float inv = nrm > 0.0 ? (float)(1.0 / nrm) : 0.0f;
-  for (int k = lane; k < Dp; k += 64) out[k] = k < d ? in[k] * inv : 0.0f;
+  for (int k = lane; k < Dp; k += 64) at(k) = k < d ? in[k] * inv : 0.0f;
   if (lane == 0) qnorm64[row] = nrm;
 }
 
@@ -219,6 +230,18 @@ __global__ __launch_bounds__(256) void knn_split_queries(const float* __restrict
   o[128] = lo;
 }
 
+// gal f32 [Np][Dp] -> gt (tile16 layout), one thread per float4 of the output
+__global__ __launch_bounds__(256) void knn_tile_gallery(const float* __restrict__ gal, int Dp,
+                                                        int64_t total4, float* __restrict__ gt) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // float4 index in gt
+  if (i >= total4) return;
+  const int64_t piece = i >> 6;  // 1-KB piece = (16-row tile, 16-float chunk)
+  const int l = (int)(i & 63), r = l & 15, h = l >> 4;
+  const int64_t tile = piece / (Dp >> 4);
+  const int c = (int)(piece % (Dp >> 4));
+  const int64_t row = tile * 16 + r;
+  ((float4*)gt)[i] = *(const float4*)(gal + row * Dp + c * 16 + 4 * h);
+}
 
 __device__ __forceinline__ int xswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
@@ -324,6 +347,100 @@ __global__ __launch_bounds__(256, 2) void knn_scores_x3_gmax(const uint16_t* __r
       gmax[m * ldG + gcol] = mx;
     }
   }
+}
+
+// ------------------------------------------------------------------ skinny-Q scan (f32 MFMA)
+// Few queries (Q <= 16*QT, QT <= 4): the gallery read (N*Dp*4 B) is the whole cost, so the scan is a
+// streaming kernel — every gallery byte from HBM exactly once, no LDS, no barriers — on exact-product
+// v_mfma_f32_16x16x4_f32 (f32 accumulate: the f32-mode delta applies).  One wave per 64-row block
+// (the gmax group format of knn_scores_x3_gmax, so knn_select_groups consumes it unchanged): lane
+// l = 16h + r owns row r of each of the 4 16-row tiles.  Gallery and queries are read from the
+// tile16 copies (tile16_index): load e of a KC-wide chunk gives lane l floats kc + 16e + 4h .. +3 of
+// its row, and the 64 lanes' float4 are one contiguous 1-KB piece — full-line, one-pass-per-16-lanes
+// loads straight into the MFMA operand layout (a row-major read would touch 16 rows per 16 lanes).
+// The MFMA k index of product (e, s) is kc + 16e + 4h + s for both operands (a permutation the dot
+// product does not see).  Queries (<= 196 KB, L2-resident) are loaded before the next chunk's gallery
+// loads: one chunk in flight while the current one is multiplied (sched_barrier keeps the order).
+template <int QT, int KC>
+__global__ __launch_bounds__(64) void knn_scan_f32_gmax(const float* __restrict__ qt16,
+                                                        const float* __restrict__ gt,
+                                                        const float* __restrict__ inv_g,
+                                                        float* __restrict__ gmax, int Dp, int64_t ldG,
+                                                        int64_t n) {
+  constexpr int L = KC / 16;  // 1-KB pieces per tile per chunk
+  const int lane = threadIdx.x;
+  const int64_t blk = blockIdx.x;
+  const int r = lane & 15, h = lane >> 4;
+  const int64_t g0 = blk * 64;
+  const int64_t tileB = 16 * (int64_t)Dp;  // floats per 16-row tile
+  const float* pb = gt + g0 * Dp + 4 * lane;
+  const float* pa = qt16 + 4 * lane;
+  f32x4 acc[QT][4];
+#pragma unroll
+  for (int t = 0; t < QT; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[t][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  f32x4 b[4][L];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < L; ++e) b[j][e] = __builtin_nontemporal_load((const f32x4*)(pb + j * tileB + 256 * e));
+  for (int kc = 0; kc < Dp; kc += KC) {
+    // queries first: vmcnt retires loads in issue order, so loads issued after the next chunk's
+    // gallery loads would make the MFMAs below wait for that chunk too
+    f32x4 a[QT][L];
+#pragma unroll
+    for (int t = 0; t < QT; ++t)
+#pragma unroll
+      for (int e = 0; e < L; ++e) a[t][e] = *(const f32x4*)(pa + t * tileB + 16 * kc + 256 * e);
+    // unconditional (the last chunk re-reads itself, an L2 hit): a branch here would make the
+    // compiler's vmcnt at the join wait for these loads before the MFMAs
+    f32x4 nb[4][L];
+    const int kn = kc + KC < Dp ? kc + KC : kc;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < L; ++e)
+        nb[j][e] = __builtin_nontemporal_load((const f32x4*)(pb + j * tileB + 16 * kn + 256 * e));
+    __builtin_amdgcn_sched_barrier(0);  // keep the whole next chunk issued ahead of the MFMAs
+#pragma unroll
+    for (int e = 0; e < L; ++e) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+#pragma unroll
+        for (int t = 0; t < QT; ++t) {
+          const float av = a[t][e][s];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float bv = b[j][e][s];
+            acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[t][j], 0, 0, 0);
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < L; ++e) b[j][e] = nb[j][e];
+  }
+  // C[i][c]: c = lane&15 (gallery row r of tile j), i = 4h + reg (query of tile t)
+  float ig[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t g = g0 + 16 * j + r;
+    ig[j] = g < n ? inv_g[g] : -INFINITY;  // -inf marks padding rows (never a candidate)
+  }
+  const int64_t gcol = blk * 16 + r;
+#pragma unroll
+  for (int t = 0; t < QT; ++t)
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mx = fmaxf(mx, ig[j] == -INFINITY ? -INFINITY : acc[t][j][rg] * ig[j]);
+      gmax[(int64_t)(16 * t + 4 * h + rg) * ldG + gcol] = mx;
+    }
 }
 
 // ------------------------------------------------------------------ per-query selection
@@ -870,6 +987,7 @@ struct mmr_index {
   float* inv_norm = nullptr;  // [Np]
   double* norm64 = nullptr;   // [Np]
   uint16_t* gs = nullptr;     // [Np][2Dp] bf16 hi/lo split (mode x3)
+  float* gt = nullptr;        // [Np][Dp] f32 in the tile16 layout (skinny scan)
   int mode = 1;               // 0: f32 MFMA scores, 1: bf16x3 split scores
   // workspace (single; guarded by mu — searches on one index serialise their enqueue)
   std::mutex mu;
@@ -905,6 +1023,18 @@ mmr_status ensure_ws(mmr_index* ix, int64_t nq) {
   MMR_CHECK_HIP(hipMalloc(&ix->scores, sizeof(float) * want * ix->Np));
   ix->ws_q = want;
   return MMR_OK;
+}
+
+// Largest query chunk routed to the skinny scan in mode x3 (MMR_KNN_SKINNY_MAX: 0 disables; <= 64).
+// Measured (100k x 768, MI355X): Q <= 16 scan 58 us (5.3 TB/s) vs the x3 GEMM's ~110 us; Q = 32
+// 132 vs ~145 us per search; Q = 64 (4 query tiles, MFMA-paced with ~1.5 waves per SIMD) 196 vs ~145.
+int64_t skinny_max_q() {
+  static const int64_t v = [] {
+    const char* e = getenv("MMR_KNN_SKINNY_MAX");
+    int64_t x = e ? atoll(e) : 32;
+    return x < 0 ? 0 : x > 64 ? 64 : x;
+  }();
+  return v;
 }
 
 struct DeviceGuard {
@@ -952,7 +1082,8 @@ mmr_status mmr_index_create(const void* gallery, int64_t n, int32_t d, mmr_dtype
   if ((e = hipMalloc(&ix->gal, sizeof(float) * ix->Np * ix->Dp)) != hipSuccess ||
       (e = hipMalloc(&ix->inv_norm, sizeof(float) * ix->Np)) != hipSuccess ||
       (e = hipMalloc(&ix->norm64, sizeof(double) * ix->Np)) != hipSuccess ||
-      (e = hipMalloc(&ix->gs, sizeof(uint16_t) * ix->Np * 2 * ix->Dp)) != hipSuccess) {
+      (e = hipMalloc(&ix->gs, sizeof(uint16_t) * ix->Np * 2 * ix->Dp)) != hipSuccess ||
+      (e = hipMalloc(&ix->gt, sizeof(float) * ix->Np * ix->Dp)) != hipSuccess) {
     mmr::set_error("mmr_index_create: hipMalloc failed: %s", hipGetErrorString(e));
     return fail(MMR_ERR_OOM);
   }
@@ -979,6 +1110,11 @@ mmr_status mmr_index_create(const void* gallery, int64_t n, int32_t d, mmr_dtype
     knn_split_gallery<<<dim3((unsigned)ceil_div(total, 256)), dim3(256)>>>(ix->gal, ix->Dp, total, ix->gs);
     e = hipGetLastError();
   }
+  if (e == hipSuccess) {
+    const int64_t total4 = ix->Np * ix->Dp / 4;
+    knn_tile_gallery<<<dim3((unsigned)ceil_div(total4, 256)), dim3(256)>>>(ix->gal, ix->Dp, total4, ix->gt);
+    e = hipGetLastError();
+  }
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (raw) (void)hipFree(raw);
   if (e != hipSuccess) {
@@ -996,6 +1132,7 @@ mmr_status mmr_index_destroy(mmr_index* ix) {
   if (ix->inv_norm) (void)hipFree(ix->inv_norm);
   if (ix->norm64) (void)hipFree(ix->norm64);
   if (ix->gs) (void)hipFree(ix->gs);
+  if (ix->gt) (void)hipFree(ix->gt);
   if (ix->qs) (void)hipFree(ix->qs);
   if (ix->qn) (void)hipFree(ix->qn);
   if (ix->qnorm64) (void)hipFree(ix->qnorm64);
@@ -1044,7 +1181,29 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
     const int64_t cq = nq - c0 < chunk ? nq - c0 : chunk;
     const float* qc = q + c0 * ix->d;
     int64_t Qp;
-    if (ix->mode == 1) {
+    if (ix->mode == 1 && cq <= skinny_max_q()) {
+      // skinny scan: HBM-streaming f32 MFMA, f32-mode delta
+      const int qt = cq <= 16 ? 1 : cq <= 32 ? 2 : 4;
+      Qp = 16 * qt;
+      knn_prep_queries<<<dim3((unsigned)ceil_div(Qp, 4)), dim3(256), 0, st>>>(
+          qc, cq, ix->d, ix->qn, ix->Dp, Qp, ix->qnorm64, 1);
+      MMR_LAUNCH_CHECK();
+      const dim3 grid((unsigned)(ix->Np / 64));
+      if (qt == 1)
+        knn_scan_f32_gmax<1, 64><<<grid, 64, 0, st>>>(ix->qn, ix->gt, ix->inv_norm, ix->scores, ix->Dp, ix->Np / 4, ix->n);
+      else if (qt == 2)
+        knn_scan_f32_gmax<2, 64><<<grid, 64, 0, st>>>(ix->qn, ix->gt, ix->inv_norm, ix->scores, ix->Dp, ix->Np / 4, ix->n);
+      else
+        knn_scan_f32_gmax<4, 32><<<grid, 64, 0, st>>>(ix->qn, ix->gt, ix->inv_norm, ix->scores, ix->Dp, ix->Np / 4, ix->n);
+      MMR_LAUNCH_CHECK();
+      const float two_delta32 = 2.0f * (float)(ix->Dp + 16) * 5.9604645e-8f;
+      knn_select_groups<<<dim3((unsigned)cq), dim3(kSelThreads), 0, st>>>(
+          ix->scores, ix->Np / 4, ix->n, k, two_delta32, qc, ix->d, ix->qnorm64, ix->gal, ix->Dp,
+          ix->norm64, ix->idx_base, out_idx + c0 * k, out_score ? out_score + c0 * k : nullptr,
+          out_score64 ? out_score64 + c0 * k : nullptr, out_status ? out_status + c0 : nullptr);
+      MMR_LAUNCH_CHECK();
+      continue;
+    } else if (ix->mode == 1) {
       Qp = round_up(cq, 128);
       knn_prep_queries<<<dim3((unsigned)ceil_div(Qp, 4)), dim3(256), 0, st>>>(
           qc, cq, ix->d, ix->qn, ix->Dp, Qp, ix->qnorm64);

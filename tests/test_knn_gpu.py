@@ -92,6 +92,25 @@ def test_knn_negative_scores_and_clustered():
     _exact_check(G, Qm, 64)
 
 
+@pytest.mark.parametrize("Q", [1, 5, 16, 17, 32, 33, 64])
+def test_knn_skinny_scan_query_tiles(Q):
+    """Q <= 64 runs the HBM-streaming f32 skinny scan (1, 2 or 4 query tiles of 16); duplicates and
+    padding rows (N not a multiple of 64) included."""
+    rng = np.random.default_rng(100 + Q)
+    G = rng.standard_normal((20_003, 768), dtype=np.float32)
+    G[7000:7016] = G[3]
+    Qm = np.concatenate([G[3:4] * 0.5, rng.standard_normal((Q - 1, 768), dtype=np.float32)])
+    gi, _ = _exact_check(G, Qm, 25)
+    assert gi[0, :17].tolist() == [3] + list(range(7000, 7016))
+
+
+@pytest.mark.parametrize("Q", [1, 64])
+def test_knn_100k_skinny_exact(Q):
+    G = synthetic.gauss_gallery(100_000, 768, synthetic.SEED)
+    Qm = synthetic.gauss_gallery(Q, 768, synthetic.SEED + 2)
+    _exact_check(G, Qm, 10)
+
+
 def test_knn_100k_full_size_exact():
     G = synthetic.gauss_gallery(100_000, 768, synthetic.SEED)
     Qm = synthetic.gauss_gallery(256, 768, synthetic.SEED + 1)
