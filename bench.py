@@ -205,7 +205,8 @@ def main():
                     "unit": "TFLOP/s"}
         else:
             roof = {"bound": "hbm", "achieved": knn_roof["achieved_gbs"], "peak": peak_hbm / 1e9, "unit": "GB/s"}
-        roof.update({"traffic": None, "kernel": knn_roof["kernel"], "ms_per_launch": ms_search})
+        roof.update({"traffic": None, "kernel": knn_roof["kernel"], "ms_per_launch": ms_search,
+                     "hbm_regime": knn_roof["hbm_regime"]})
     roof["frac"] = roof["achieved"] / roof["peak"]
     # HBM traffic per launch from the committed PMC pass (tools/pmc_traffic.py; FETCH_SIZE x2 per the
     # gfx950 correction + WRITE_SIZE), for the same kernels at the same shapes
