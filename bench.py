@@ -31,6 +31,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--mode", choices=["full", "knn"], default="full")
     p.add_argument("--batch", type=int, default=256)
+    p.add_argument("--knn-mode", choices=["x3", "f16"], default="f16",
+                   help="gallery scan: f16 (fp16 unit-row copy, default) or x3 (bf16 split GEMM; skinny f32 "
+                        "stream for Q <= 32); both exact (f64 re-rank from the f32 rows)")
     p.add_argument("--gallery", type=int, default=100_000, help="gallery rows per GPU")
     p.add_argument("--dim", type=int, default=768)
     p.add_argument("--k", type=int, default=10)
@@ -73,7 +76,7 @@ def main():
     # gallery shard: rows [rank*n, (rank+1)*n) of a virtual (world*n, d) N(0,1) gallery
     n, d, K, B = a.gallery, a.dim, a.k, a.batch
     G = synthetic.gauss_gallery(n, d, synthetic.SEED + 17 * rank)
-    index = GalleryIndex(G, device=local, idx_base=rank * n)
+    index = GalleryIndex(G, device=local, idx_base=rank * n, mode=a.knn_mode)
     index.reserve(2 * B * world)
 
     model = None
@@ -171,25 +174,36 @@ def main():
     pairs_per_s = (world * nq_step) * (world * n) * a.steps / elapsed
     # roofline of the dominant kernel, per launch on one GPU
     Qs = world * nq_step
-    # kNN search: algorithmic flops 2*Q*N*D; bytes = gallery once (N*D*4 as hi/lo bf16) + norms +
-    # queries + results.  Peak for the x3 scan = dense bf16 MFMA (3 bf16 products per f32 product).
-    knn_flops = 2.0 * Qs * n * d
-    knn_bytes = n * d * 4 + n * 4 + Qs * d * 4 + Qs * K * 12
+    # kNN search: algorithmic flops 2*Q*N*D; bytes = the scanned gallery copy once + norms + queries +
+    # results.  f16: fp16 unit rows (N*D*2), one fp16 MFMA product per f32 product (dense fp16 peak =
+    # bf16 peak), HBM-bound below Q ~ 312.  x3: hi/lo bf16 (N*D*4), 3 bf16 MFMA products per f32
+    # product; Q <= 32 streams the f32 tile16 copy (N*D*4) on f32 MFMA (HBM-bound).
     peak_bf16, peak_hbm = 2.5e15, 8.0e12
-    knn_roof = {"kernel": "mmr_index_search (prep + knn_scores_x3 bf16 MFMA + knn_select)",
+    gbytes = 2 if a.knn_mode == "f16" else 4
+    knn_flops = 2.0 * Qs * n * d
+    knn_bytes = n * d * gbytes + n * 4 + Qs * d * 4 + Qs * K * 12
+    mfma_work = knn_flops * (1 if a.knn_mode == "f16" else 3)
+    if a.knn_mode == "f16":
+        kname = "mmr_index_search (prep + knn_scan_f16_gmax fp16 MFMA stream + knn_select_groups f64 re-rank)"
+    elif Qs <= 32:
+        kname = "mmr_index_search (prep + knn_scan_f32_gmax skinny f32 MFMA stream + knn_select_groups)"
+    else:
+        kname = "mmr_index_search (prep + knn_scores_x3_gmax bf16x3 MFMA + knn_select_groups)"
+    mfma_bound = a.knn_mode == "x3" and Qs > 32 and mfma_work / peak_bf16 > knn_bytes / peak_hbm
+    if a.knn_mode == "f16":
+        mfma_bound = mfma_work / peak_bf16 > knn_bytes / peak_hbm
+    knn_roof = {"kernel": kname, "scan_mode": a.knn_mode,
                 "ms_per_launch": ms_search, "flops": knn_flops, "bytes": knn_bytes,
-                "bound": "mfma" if 3 * knn_flops / peak_bf16 > knn_bytes / peak_hbm else "hbm",
+                "bound": "mfma" if mfma_bound else "hbm",
                 "achieved_tflops_f32_equiv": knn_flops / (ms_search / 1e3) / 1e12,
                 "achieved_gbs": knn_bytes / (ms_search / 1e3) / 1e9}
-    if Qs <= 32:
-        knn_roof["kernel"] = "mmr_index_search (prep + knn_scan_f32_gmax skinny f32 MFMA stream + knn_select_groups)"
-        knn_roof["bound"] = "hbm"
-    small_bytes = n * d * 4 + n * 4 + q16.shape[0] * d * 4 + q16.shape[0] * K * 12
+    small_bytes = n * d * gbytes + n * 4 + q16.shape[0] * d * 4 + q16.shape[0] * K * 12
     knn_roof["hbm_regime"] = {
         "queries": int(q16.shape[0]), "ms_per_search": ms_small, "bytes": small_bytes,
         "achieved_gbs": small_bytes / (ms_small / 1e3) / 1e9,
         "frac": small_bytes / (ms_small / 1e3) / peak_hbm,
-        "kernel": "whole search call: prep + knn_scan_f32_gmax + knn_select_groups (events on the launch stream)"}
+        "kernel": "whole search call: prep + %s scan + knn_select_groups (events on the launch stream)"
+                  % ("knn_scan_f16_gmax" if a.knn_mode == "f16" else "knn_scan_f32_gmax")}
     if model is not None:
         evs = model.backbones.bert.ffn1_events
         ms_ffn1 = sum(e0.elapsed_time(e1) for e0, e1 in evs) / max(len(evs), 1)
@@ -201,7 +215,7 @@ def main():
                 "ms_per_launch": ms_ffn1, "flops_per_launch": fl, "knn": knn_roof}
     else:
         if knn_roof["bound"] == "mfma":
-            roof = {"bound": "mfma", "achieved": 3 * knn_flops / (ms_search / 1e3) / 1e12, "peak": peak_bf16 / 1e12,
+            roof = {"bound": "mfma", "achieved": mfma_work / (ms_search / 1e3) / 1e12, "peak": peak_bf16 / 1e12,
                     "unit": "TFLOP/s"}
         else:
             roof = {"bound": "hbm", "achieved": knn_roof["achieved_gbs"], "peak": peak_hbm / 1e9, "unit": "GB/s"}
@@ -220,9 +234,14 @@ def main():
         if rec is not None:
             roof["traffic"] = rec["hbm_bytes"]
             roof["traffic_source"] = rec["source"]
-    if model is None and "knn_scores_x3" in tr and "knn_select" in tr and B == 256 and n == 100_000 and d == 768:
+    if (model is None and a.knn_mode == "x3" and "knn_scores_x3" in tr and "knn_select" in tr and B == 256
+            and n == 100_000 and d == 768):
         roof["traffic"] = tr["knn_scores_x3"]["hbm_bytes"] + tr["knn_select"]["hbm_bytes"]
         roof["traffic_source"] = tr["knn_scores_x3"]["source"]
+    if (model is None and a.knn_mode == "f16" and "knn_scan_f16" in tr and "knn_select_f16" in tr and B == 256
+            and n == 100_000 and d == 768):
+        roof["traffic"] = tr["knn_scan_f16"]["hbm_bytes"] + tr["knn_select_f16"]["hbm_bytes"]
+        roof["traffic_source"] = tr["knn_scan_f16"]["source"]
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -238,7 +257,9 @@ def main():
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": elapsed / a.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16 towers / f32 kNN (f64 re-rank)" if a.mode == "full" else "f32 (f64 re-rank)",
+            "dtype": ("bf16 towers / " if a.mode == "full" else "") + (
+                "f32 gallery, fp16 unit-row scan copy, exact f64 re-rank" if a.knn_mode == "f16"
+                else "f32 gallery, bf16x3 scan, exact f64 re-rank"),
             "data": "synthetic (seeded N(0,1) gallery; random-init weights)",
             "config": {"workload": ("cfg2: Swin-T + BERT-base towers + %s head, B=%d, top-%d over %dx%d f32 per GPU"
                                     % ("5-layer multimodal fusion" if a.model_type == "multimodal" else "image+text",

@@ -58,7 +58,10 @@ mmr_status mmr_index_info(const mmr_index* index, int64_t* n, int32_t* d, int64_
 mmr_status mmr_index_reserve(mmr_index* index, int64_t max_q);
 
 /* Scan precision of the candidate pass (the ranking is always exact f64): 0 = f32 MFMA,
- * 1 = bf16 3-term split MFMA (default; ~5x the f32 rate at the same bytes). */
+ * 1 = bf16 3-term split MFMA (default; ~5x the f32 rate at the same bytes; queries chunks of
+ * <= 32 take the HBM-streaming f32 skinny scan), 2 = fp16 unit-row copy of the gallery (built on
+ * the first switch to this mode: half the scan bytes, one fp16 MFMA per product; the wider
+ * candidate margin can overflow the candidate buffer on heavily tied galleries -> status 1). */
 mmr_status mmr_index_set_mode(mmr_index* index, int32_t mode);
 
 /* Exact cosine top-K of q (q, d) f32 device queries against the gallery.

@@ -99,6 +99,13 @@ __host__ __device__ __forceinline__ int64_t tile16_index(int64_t row, int k, int
   return ((row >> 4) * (Dp >> 4) + (k >> 4)) * 256 + ((((k & 15) >> 2) << 4) + (row & 15)) * 4 + (k & 3);
 }
 
+// fp16 variant (skinny f16 scan): 16-row x 32-half pieces of 1 KB, lane l = 16h + r holding halfs
+// 8h..8h+7 of row r (the v_mfma_f32_16x16x32_f16 operand layout):
+// ((row/16)*(Dp/32) + k/32)*512 + ((k%32)/8*16 + row%16)*8 + k%8.
+__host__ __device__ __forceinline__ int64_t tile32h_index(int64_t row, int k, int Dp) {
+  return ((row >> 4) * (Dp >> 5) + (k >> 5)) * 512 + ((((k & 31) >> 3) << 4) + (row & 15)) * 8 + (k & 7);
+}
+
 __global__ __launch_bounds__(256) void knn_prep_queries(const float* __restrict__ q, int64_t nq,
                                                         int d, float* __restrict__ qn, int Dp,
                                                         int64_t Qp, double* __restrict__ qnorm64,
@@ -106,9 +113,14 @@ __global__ __launch_bounds__(256) void knn_prep_queries(const float* __restrict_
   int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   int lane = threadIdx.x & 63;
   if (row >= Qp) return;
-  auto at = [&](int k) -> float& { return tiled ? qn[tile16_index(row, k, Dp)] : qn[row * Dp + k]; };
+  // tiled: 0 row-major f32, 1 tile16 f32, 2 tile32h fp16 (qn reinterpreted as halfs)
+  auto put = [&](int k, float v) {
+    if (tiled == 2) ((_Float16*)qn)[tile32h_index(row, k, Dp)] = (_Float16)v;
+    else if (tiled == 1) qn[tile16_index(row, k, Dp)] = v;
+    else qn[row * Dp + k] = v;
+  };
   if (row >= nq) {
-    for (int k = lane; k < Dp; k += 64) at(k) = 0.0f;
+    for (int k = lane; k < Dp; k += 64) put(k, 0.0f);
     return;
   }
   const float* in = q + row * (int64_t)d;
@@ -117,7 +129,7 @@ __global__ __launch_bounds__(256) void knn_prep_queries(const float* __restrict_
   ss = mmr::wave_sum(ss);
   double nrm = sqrt(ss);
   float inv = nrm > 0.0 ? (float)(1.0 / nrm) : 0.0f;
-  for (int k = lane; k < Dp; k += 64) at(k) = k < d ? in[k] * inv : 0.0f;
+  for (int k = lane; k < Dp; k += 64) put(k, k < d ? in[k] * inv : 0.0f);
   if (lane == 0) qnorm64[row] = nrm;
 }
 
@@ -243,6 +255,26 @@ __global__ __launch_bounds__(256) void knn_tile_gallery(const float* __restrict_
   ((float4*)gt)[i] = *(const float4*)(gal + row * Dp + c * 16 + 4 * h);
 }
 
+// gal f32 [Np][Dp] -> gh: fp16 of the unit rows g/|g| in the tile32h layout, one thread per 8 halfs
+__global__ __launch_bounds__(256) void knn_tile_gallery_f16(const float* __restrict__ gal,
+                                                            const float* __restrict__ inv_g, int Dp,
+                                                            int64_t total8, uint16_t* __restrict__ gh) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // 16-B unit index in gh
+  if (i >= total8) return;
+  const int64_t piece = i >> 6;
+  const int l = (int)(i & 63), r = l & 15, h = l >> 4;
+  const int64_t tile = piece / (Dp >> 5);
+  const int c = (int)(piece % (Dp >> 5));
+  const int64_t row = tile * 16 + r;
+  const float ig = inv_g[row];
+  const float* src = gal + row * Dp + c * 32 + 8 * h;
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  h8 v;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = (_Float16)(src[e] * ig);
+  ((h8*)gh)[i] = v;
+}
+
 __device__ __forceinline__ int xswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
 // S[m][n] = inv_g[n] * sum_k' Qs[m][k'] Gs'[n][k'] over K' = 3 Dp; tile 128 x 128 x 64, 4 waves
@@ -347,6 +379,82 @@ __global__ __launch_bounds__(256, 2) void knn_scores_x3_gmax(const uint16_t* __r
       gmax[m * ldG + gcol] = mx;
     }
   }
+}
+
+// ------------------------------------------------------------------ fp16 scan (mode f16)
+// The gallery scanned as fp16 unit rows (gh = fp16(g/|g|), 2 B per element: half the bytes of every
+// f32 copy) against fp16 unit queries on v_mfma_f32_16x16x32_f16 (exact products, f32 accumulate);
+// the f64 re-score from the raw f32 rows (knn_select_groups) keeps the result exact, with the
+// candidate margin 2*delta_f16 (delta_f16 argued at mmr_index_search).  Same streaming structure as
+// knn_scan_f32_gmax: one wave per 64-row block, lane l = 16h + r on row r of each 16-row tile, every
+// wave load one contiguous 1-KB tile32h piece; QT query tiles of 16 from L2 (16*QT <= 256 queries per
+// pass, so the gallery is read from HBM once per 256 queries).  At QT = 16 the accumulators (256 f32)
+// sit in AGPRs.
+template <int QT, int KC>
+__global__ __launch_bounds__(64) void knn_scan_f16_gmax(const uint16_t* __restrict__ qh,
+                                                        const uint16_t* __restrict__ gh,
+                                                        float* __restrict__ gmax, int Dp, int64_t ldG,
+                                                        int64_t n) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  constexpr int L = KC / 32;  // 1-KB pieces per tile per chunk
+  const int lane = threadIdx.x;
+  const int64_t blk = blockIdx.x;
+  const int r = lane & 15, h = lane >> 4;
+  const int64_t g0 = blk * 64;
+  const int64_t tileB = 16 * (int64_t)Dp;  // halfs per 16-row tile
+  const uint16_t* pb = gh + g0 * Dp + 8 * lane;
+  const uint16_t* pa = qh + 8 * lane;
+  f32x4 acc[QT][4];
+#pragma unroll
+  for (int t = 0; t < QT; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[t][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  f32x4 b[4][L];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < L; ++e) b[j][e] = __builtin_nontemporal_load((const f32x4*)(pb + j * tileB + 512 * e));
+  for (int kc = 0; kc < Dp; kc += KC) {
+    f32x4 a[QT][L];
+#pragma unroll
+    for (int t = 0; t < QT; ++t)
+#pragma unroll
+      for (int e = 0; e < L; ++e) a[t][e] = *(const f32x4*)(pa + t * tileB + 16 * kc + 512 * e);
+    f32x4 nb[4][L];
+    const int kn = kc + KC < Dp ? kc + KC : kc;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < L; ++e)
+        nb[j][e] = __builtin_nontemporal_load((const f32x4*)(pb + j * tileB + 16 * kn + 512 * e));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int e = 0; e < L; ++e)
+#pragma unroll
+      for (int t = 0; t < QT; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a[t][e]),
+                                                             __builtin_bit_cast(h8, b[j][e]), acc[t][j], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < L; ++e) b[j][e] = nb[j][e];
+  }
+  const int64_t gcol = blk * 16 + r;
+  bool pad[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) pad[j] = g0 + 16 * j + r >= n;
+#pragma unroll
+  for (int t = 0; t < QT; ++t)
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mx = fmaxf(mx, pad[j] ? -INFINITY : acc[t][j][rg]);
+      gmax[(int64_t)(16 * t + 4 * h + rg) * ldG + gcol] = mx;
+    }
 }
 
 // ------------------------------------------------------------------ skinny-Q scan (f32 MFMA)
@@ -988,7 +1096,8 @@ struct mmr_index {
   double* norm64 = nullptr;   // [Np]
   uint16_t* gs = nullptr;     // [Np][2Dp] bf16 hi/lo split (mode x3)
   float* gt = nullptr;        // [Np][Dp] f32 in the tile16 layout (skinny scan)
-  int mode = 1;               // 0: f32 MFMA scores, 1: bf16x3 split scores
+  uint16_t* gh = nullptr;     // [Np][Dp] fp16 unit rows in the tile32h layout (mode f16; built on first use)
+  int mode = 1;               // 0: f32 MFMA scores, 1: bf16x3 split scores, 2: fp16 unit-row scan
   // workspace (single; guarded by mu — searches on one index serialise their enqueue)
   std::mutex mu;
   int64_t ws_q = 0;  // queries the workspace holds
@@ -1133,6 +1242,7 @@ mmr_status mmr_index_destroy(mmr_index* ix) {
   if (ix->norm64) (void)hipFree(ix->norm64);
   if (ix->gs) (void)hipFree(ix->gs);
   if (ix->gt) (void)hipFree(ix->gt);
+  if (ix->gh) (void)hipFree(ix->gh);
   if (ix->qs) (void)hipFree(ix->qs);
   if (ix->qn) (void)hipFree(ix->qn);
   if (ix->qnorm64) (void)hipFree(ix->qnorm64);
@@ -1181,7 +1291,41 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
     const int64_t cq = nq - c0 < chunk ? nq - c0 : chunk;
     const float* qc = q + c0 * ix->d;
     int64_t Qp;
-    if (ix->mode == 1 && cq <= skinny_max_q()) {
+    if (ix->mode == 2) {
+      // fp16 scan, passes of <= 256 queries (16 * QT, QT a power of two).  delta_f16 bounds
+      // |s_f16 - s64|: fp16 rounding of both unit vectors (2 * 2^-11 relative, Cauchy-Schwarz over
+      // sum |q_k g_k| <= 1) + fp16 subnormal half-ulps (2 * 2^-25 * sqrt(Dp)) + f32 accumulation and
+      // the f32 normalisation of both operands (the f32-mode (Dp + 16) 2^-24), rounded up.
+      const float two_delta16 =
+          2.0f * (9.765625e-4f + 9.5367432e-7f + (float)(2 * ix->Dp + 64) * 5.9604645e-8f);
+      for (int64_t p0 = 0; p0 < cq; p0 += 256) {
+        const int64_t pq = cq - p0 < 256 ? cq - p0 : 256;
+        int qt = 1;
+        while (16 * qt < pq) qt *= 2;
+        Qp = 16 * qt;
+        const float* qp = qc + p0 * ix->d;
+        knn_prep_queries<<<dim3((unsigned)ceil_div(Qp, 4)), dim3(256), 0, st>>>(
+            qp, pq, ix->d, ix->qn, ix->Dp, Qp, ix->qnorm64, 2);
+        MMR_LAUNCH_CHECK();
+        const dim3 grid((unsigned)(ix->Np / 64));
+        const uint16_t* qh = (const uint16_t*)ix->qn;
+        switch (qt) {
+          case 1: knn_scan_f16_gmax<1, 128><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n); break;
+          case 2: knn_scan_f16_gmax<2, 128><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n); break;
+          case 4: knn_scan_f16_gmax<4, 64><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n); break;
+          case 8: knn_scan_f16_gmax<8, 64><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n); break;
+          default: knn_scan_f16_gmax<16, 32><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n); break;
+        }
+        MMR_LAUNCH_CHECK();
+        const int64_t o = c0 + p0;
+        knn_select_groups<<<dim3((unsigned)pq), dim3(kSelThreads), 0, st>>>(
+            ix->scores, ix->Np / 4, ix->n, k, two_delta16, qp, ix->d, ix->qnorm64, ix->gal, ix->Dp,
+            ix->norm64, ix->idx_base, out_idx + o * k, out_score ? out_score + o * k : nullptr,
+            out_score64 ? out_score64 + o * k : nullptr, out_status ? out_status + o : nullptr);
+        MMR_LAUNCH_CHECK();
+      }
+      continue;
+    } else if (ix->mode == 1 && cq <= skinny_max_q()) {
       // skinny scan: HBM-streaming f32 MFMA, f32-mode delta
       const int qt = cq <= 16 ? 1 : cq <= 32 ? 2 : 4;
       Qp = 16 * qt;
@@ -1312,8 +1456,26 @@ mmr_status mmr_index_rerank(const mmr_index* ix, const float* q_emb, int64_t nq,
 
 mmr_status mmr_index_set_mode(mmr_index* ix, int32_t mode) {
   mmr::clear_error();
-  MMR_REQUIRE(ix != nullptr && (mode == 0 || mode == 1), "mmr_index_set_mode: bad arguments");
+  MMR_REQUIRE(ix != nullptr && mode >= 0 && mode <= 2, "mmr_index_set_mode: bad arguments");
   std::lock_guard<std::mutex> lk(ix->mu);
+  if (mode == 2 && ix->gh == nullptr) {
+    DeviceGuard g(ix->device);
+    hipError_t e = hipMalloc(&ix->gh, sizeof(uint16_t) * ix->Np * ix->Dp);
+    if (e != hipSuccess) {
+      ix->gh = nullptr;
+      mmr::set_error("mmr_index_set_mode: hipMalloc(fp16 copy) failed: %s", hipGetErrorString(e));
+      return MMR_ERR_OOM;
+    }
+    const int64_t total8 = ix->Np * ix->Dp / 8;
+    knn_tile_gallery_f16<<<dim3((unsigned)ceil_div(total8, 256)), dim3(256)>>>(ix->gal, ix->inv_norm, ix->Dp,
+                                                                             total8, ix->gh);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+      mmr::set_error("mmr_index_set_mode: fp16 copy kernel failed: %s", hipGetErrorString(e));
+      return MMR_ERR_HIP;
+    }
+  }
   ix->mode = mode;
   return MMR_OK;
 }

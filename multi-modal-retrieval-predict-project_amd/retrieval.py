@@ -48,7 +48,15 @@ class RetrievalEngine(abc.ABC):
 
 
 class GalleryIndex:
-    """Owning wrapper of an mmr_index (one device-resident gallery shard)."""
+    """Owning wrapper of an mmr_index (one device-resident gallery shard).
+
+    Scan modes (all exact: candidates re-scored in f64 from the f32 rows): "x3" bf16 3-term split
+    GEMM (default; Q <= 32 use the skinny f32 stream), "f32" f32 MFMA, "f16" fp16 unit-row copy of
+    the gallery (half the scan bytes; wider candidate margin, so heavily tied galleries can overflow
+    the candidate buffer — status 1, which MI355XRetrievalEngine answers by re-running those queries
+    in "x3")."""
+
+    MODES = {"f32": 0, "x3": 1, "f16": 2}
 
     def __init__(self, embs, device=None, idx_base: int = 0, mode: str = "x3"):
         _lib.require_gpu()
@@ -76,10 +84,17 @@ class GalleryIndex:
                    "mmr_index_create")
         del keep
         self._h = h
-        if mode not in ("x3", "f32"):
-            raise ValueError(f"scan mode {mode!r} (x3 | f32)")
-        _lib.check(L.mmr_index_set_mode(h, 1 if mode == "x3" else 0), "mmr_index_set_mode")
+        if mode not in self.MODES:
+            raise ValueError(f"scan mode {mode!r} (x3 | f32 | f16)")
+        _lib.check(L.mmr_index_set_mode(h, self.MODES[mode]), "mmr_index_set_mode")
+        self.mode = mode
         self.n, self.d, self.idx_base = int(n), int(d), int(idx_base)
+
+    def set_mode(self, mode: str):
+        if mode not in self.MODES:
+            raise ValueError(f"scan mode {mode!r} (x3 | f32 | f16)")
+        _lib.check(_lib.lib().mmr_index_set_mode(self._h, self.MODES[mode]), "mmr_index_set_mode")
+        self.mode = mode
 
     def reserve(self, max_q: int):
         _lib.check(_lib.lib().mmr_index_reserve(self._h, int(max_q)), "mmr_index_reserve")
@@ -169,9 +184,11 @@ class MI355XRetrievalEngine(RetrievalEngine):
     def __init__(self, features_path: Optional[str] = None, ids_path: Optional[str] = None,
                  device=None, dtype: str = "fp32", embs=None, ids=None, **_ignored):
         super().__init__(features_path, ids_path, embs=embs, ids=ids)
-        if dtype != "fp32":
-            raise ValueError(f"gallery dtype {dtype!r} not built in this round (fp32 only)")
-        self.index = GalleryIndex(self.embs, device=device)
+        if dtype not in ("fp32", "fp16"):
+            raise ValueError(f"gallery dtype {dtype!r} (fp32 | fp16)")
+        # fp16: the scan reads an fp16 copy of the unit rows (BASELINE cfg5's fp16 gallery); the f32
+        # rows stay resident for the exact f64 re-score, so results are identical to fp32
+        self.index = GalleryIndex(self.embs, device=device, mode="f16" if dtype == "fp16" else "x3")
         self.device = self.index.device
 
     def search(self, Q, K: int = 10, check: bool = True):
@@ -187,6 +204,15 @@ class MI355XRetrievalEngine(RetrievalEngine):
             e = torch.empty((q.shape[0], 0))
             return (e.long().numpy(), e.numpy()) if is_np else (e.long(), e)
         idx, sc, st = self.index.search(q, k_eff, want_status=True)
+        if self.index.mode == "f16" and st.numel() and int(st.max().item()) != 0:
+            # fp16 margin overflowed the candidate buffer on some queries: redo them in x3
+            bad = torch.nonzero(st != 0).flatten()
+            self.index.set_mode("x3")
+            try:
+                i2, s2, st2 = self.index.search(q[bad].contiguous(), k_eff, want_status=True)
+            finally:
+                self.index.set_mode("f16")
+            idx[bad], sc[bad], st[bad] = i2, s2, st2
         if check and int(st.max().item() if st.numel() else 0) != 0:
             raise RuntimeError("candidate buffer overflow in mmr_index_search (massively tied scores)")
         if is_np:

@@ -57,7 +57,7 @@ def test_knn_matches_reference_golden(name):
             assert ok, msg
 
 
-@pytest.mark.parametrize("mode", ["x3", "f32"])
+@pytest.mark.parametrize("mode", ["x3", "f32", "f16"])
 def test_knn_scan_modes_agree(mode):
     G = synthetic.gauss_gallery(20000, 768, 41)
     Qm = synthetic.gauss_gallery(200, 768, 42)
@@ -109,6 +109,47 @@ def test_knn_100k_skinny_exact(Q):
     G = synthetic.gauss_gallery(100_000, 768, synthetic.SEED)
     Qm = synthetic.gauss_gallery(Q, 768, synthetic.SEED + 2)
     _exact_check(G, Qm, 10)
+
+
+@pytest.mark.parametrize("Q", [1, 16, 17, 33, 64, 65, 128, 256, 300])
+def test_knn_f16_scan_query_tiles(Q):
+    """fp16 scan (mode f16): every QT in {1,2,4,8,16} and a second 256-query pass; duplicates,
+    padding rows and a zero row; exact indices and f64 scores as the other modes."""
+    rng = np.random.default_rng(300 + Q)
+    G = rng.standard_normal((10_007, 768), dtype=np.float32)
+    G[5000:5008] = G[3]
+    G[9000] = 0.0
+    Qm = np.concatenate([G[3:4] * 2.0, rng.standard_normal((Q - 1, 768), dtype=np.float32)])
+    gi, _ = _exact_check(G, Qm, 20, mode="f16")
+    assert gi[0, :9].tolist() == [3] + list(range(5000, 5008))
+
+
+def test_knn_f16_labelled_and_negative():
+    G, _ = synthetic.labelled_gallery(4000, 256, 11)
+    Qm, _ = synthetic.labelled_gallery(50, 256, 12)
+    _exact_check(G, Qm, 64, mode="f16")
+    _exact_check(-np.abs(G), np.abs(Qm), 10, mode="f16")
+
+
+def test_knn_100k_f16_exact():
+    G = synthetic.gauss_gallery(100_000, 768, synthetic.SEED)
+    Qm = synthetic.gauss_gallery(256, 768, synthetic.SEED + 1)
+    _exact_check(G, Qm, 10, mode="f16")
+
+
+def test_engine_fp16_gallery_matches_fp32_engine():
+    G, _ = synthetic.labelled_gallery(3000, 128, 21)
+    G[100:140] = G[7]                     # 40 exact ties: f16 margin may overflow -> x3 redo
+    Qm = np.concatenate([G[7:8], synthetic.labelled_gallery(20, 128, 22)[0]])
+    ids = [str(i) for i in range(len(G))]
+    e32 = MI355XRetrievalEngine(embs=G, ids=ids)
+    e16 = MI355XRetrievalEngine(embs=G, ids=ids, dtype="fp16")
+    a_i, a_s = e32.search(Qm, K=50)
+    b_i, b_s = e16.search(Qm, K=50)
+    np.testing.assert_array_equal(a_i, b_i)
+    np.testing.assert_array_equal(a_s, b_s)
+    e32.close()
+    e16.close()
 
 
 def test_knn_100k_full_size_exact():

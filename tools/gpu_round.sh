@@ -39,6 +39,13 @@ for s in $STEPS; do
       timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc" -o kwrite \
         -- python bench.py --mode knn --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/pmc_kwrite.log" 2>&1
       ls -R "$OUT/pmc" | head -20 ;;
+    pmck)
+      # kNN-mode HBM traffic only (default scan mode), FETCH_SIZE and WRITE_SIZE in separate passes
+      timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o kfetch \
+        -- python bench.py --mode knn --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/pmc_kfetch.log" 2>&1
+      timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc" -o kwrite \
+        -- python bench.py --mode knn --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/pmc_kwrite.log" 2>&1
+      ls -R "$OUT/pmc" | head -20 ;;
     pmcg)
       # FFN1 GEMM traffic per candidate launch variant (the tuner's pick varies by box)
       for v in 0 1 2 7; do
