@@ -125,6 +125,27 @@ __global__ __launch_bounds__(256) void knn_prep_queries(const float* __restrict_
   }
   const float* in = q + row * (int64_t)d;
   double ss = 0.0;
+  if (Dp <= 1024) {
+    // all loads of the row issued together (a runtime-count loop waits for each load in turn)
+    float v[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const int k = lane + 64 * c;
+      v[c] = k < d ? in[k] : 0.0f;
+    }
+#pragma unroll
+    for (int c = 0; c < 16; ++c) ss += (double)v[c] * (double)v[c];
+    ss = mmr::wave_sum(ss);
+    const double nrm = sqrt(ss);
+    const float inv = nrm > 0.0 ? (float)(1.0 / nrm) : 0.0f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const int k = lane + 64 * c;
+      if (k < Dp) put(k, v[c] * inv);
+    }
+    if (lane == 0) qnorm64[row] = nrm;
+    return;
+  }
   for (int k = lane; k < d; k += 64) ss += (double)in[k] * (double)in[k];
   ss = mmr::wave_sum(ss);
   double nrm = sqrt(ss);
@@ -801,6 +822,16 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_groups(
     if (tid == 0 && status) status[qi] = 0;
     return;
   }
+  // the raw query row (f64 re-score, phase E) is loaded first: its latency hides under phases A-D
+  const float* qr = q_raw + qi * (int64_t)d;
+  float qv[4][4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int kq = (c * 64 + lane) * 4 + e;
+      qv[c][e] = (d <= 1024 && kq < d) ? qr[kq] : 0.f;
+    }
   const int64_t ng = ldG;       // groups per query row (Np / 4, a multiple of 64)
   const int64_t n4 = ng >> 2;
   // the first kRegF4 float4 of each thread's strided slice stay in registers for (C): one HBM/L2
@@ -860,7 +891,6 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_groups(
   }
   // (E) f64 re-score of every row of the collected groups (slot s: group s/4, member s%4)
   const int nslot = 4 * cnt;
-  const float* qr = q_raw + qi * (int64_t)d;
   const double qn = qnorm64[qi];
   auto slot_row = [&](int s) -> int64_t {
     const int g = cand_g[s >> 2];
@@ -870,20 +900,16 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_groups(
     // latency-bound: each wave issues the float4 loads of RB rows before reducing any of them;
     // the query row stays in registers (lane owns elements 4(64c + lane) .. +3)
     constexpr int RB = 2;
-    float qv[4][4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int kq = (c * 64 + lane) * 4 + e;
-        qv[c][e] = kq < d ? qr[kq] : 0.f;
-      }
     for (int s0 = wave * RB; s0 < nslot; s0 += (kSelThreads / 64) * RB) {
       float4 gv[RB][4];
+      double gnr[RB];  // row norms loaded with the rows (not after the reduction: one round trip)
+      int64_t gir[RB];
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
         const int s = s0 + r;
         const int64_t gi = s < nslot ? slot_row(s) : n;
+        gir[r] = gi;
+        gnr[r] = gi < n ? gnorm64[gi] : 0.0;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const int k0 = (c * 64 + lane) * 4;
@@ -900,9 +926,8 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_groups(
         acc = mmr::wave_sum(acc);
         const int s = s0 + r;
         if (lane == 0 && s < nslot) {
-          const int64_t gi = slot_row(s);
-          const double gn = gi < n ? gnorm64[gi] : 0.0;
-          cand_d[s] = gi >= n ? -INFINITY : ((qn > 0.0 && gn > 0.0) ? acc / (qn * gn) : 0.0);
+          const double gn = gnr[r];
+          cand_d[s] = gir[r] >= n ? -INFINITY : ((qn > 0.0 && gn > 0.0) ? acc / (qn * gn) : 0.0);
         }
       }
     }
