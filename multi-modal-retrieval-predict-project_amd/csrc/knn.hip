@@ -617,11 +617,13 @@ __device__ __forceinline__ void pick_digit(const uint32_t* hist, uint32_t krem, 
 
 // Block-wide radix select: the kth (1-based) largest key among keys[0..m) (LDS).  All threads
 // return the same key.  hist: 256-entry LDS scratch.
+// passes < 4: only the top 8*passes bits are resolved and the smallest key with that prefix is
+// returned — a lower bound of the kth key (all a threshold needs), one radix pass (~1 us) less each.
 __device__ uint32_t block_select_kth(const uint32_t* keys, int m, int kth, uint32_t* hist,
-                                     uint32_t* bcast) {
+                                     uint32_t* bcast, int passes = 4) {
   uint32_t prefix = 0, pmask = 0;
   uint32_t krem = (uint32_t)kth;
-  for (int pass = 0; pass < 4; ++pass) {
+  for (int pass = 0; pass < passes; ++pass) {
     const int shift = 24 - 8 * pass;
     for (int i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
     __syncthreads();
@@ -794,6 +796,15 @@ __global__ __launch_bounds__(kSelThreads) void knn_select(
 // (score desc, index asc).
 constexpr int kGrpCap = kCandCap / 4;
 
+// Phase clock of block 0 (tools/select_trace.hip builds this file with MMR_SELECT_TRACE; off in libmmr)
+#ifdef MMR_SELECT_TRACE
+__device__ long long g_sel_trace[16];
+#define SEL_MARK(i) \
+  if (blockIdx.x == 0 && threadIdx.x == 0) g_sel_trace[i] = wall_clock64();
+#else
+#define SEL_MARK(i)
+#endif
+
 __global__ __launch_bounds__(kSelThreads) void knn_select_groups(
     const float* __restrict__ gmax, int64_t ldG, int64_t n, int k, float two_delta,
     const float* __restrict__ q_raw, int d, const double* __restrict__ qnorm64,
@@ -805,7 +816,10 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_groups(
   __shared__ uint32_t bcast[4];
   __shared__ int cand_g[kGrpCap];
   __shared__ double cand_d[kCandCap];
+  __shared__ int rank_s[kCandCap];
+  __shared__ int row_s[kCandCap];
 
+  SEL_MARK(0)
   const int64_t qi = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* row = gmax + qi * ldG;
@@ -854,7 +868,13 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_groups(
   tmax[tid] = f2key(m);
   if (tid == 0) bcast[2] = 0;
   __syncthreads();
-  float thr = lower_threshold(key2f(block_select_kth(tmax, kSelThreads, kk, hist, bcast)), two_delta);
+  SEL_MARK(1)
+  // 16-bit prefix (sign, exponent, 7 mantissa bits: 2^-7 relative) of the K-th largest thread max,
+  // clamped to -inf's key (smaller keys are NaN patterns)
+  uint32_t bkey = block_select_kth(tmax, kSelThreads, kk, hist, bcast, 2);
+  if (bkey < f2key(-INFINITY)) bkey = f2key(-INFINITY);
+  float thr = lower_threshold(key2f(bkey), two_delta);
+  SEL_MARK(2)
 #define MMR_TAKE(I, V, TH)                                                \
   {                                                                       \
     const float4 v_ = (V);                                                \
@@ -874,6 +894,7 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_groups(
     __syncthreads();
   };
   collect(thr, true);
+  SEL_MARK(3)
   int cnt = (int)bcast[2];
   int st = 0;
   if (cnt > kGrpCap) {
@@ -947,23 +968,34 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_groups(
     }
   }
   __syncthreads();
-  // (F) rank among the valid slots
+  SEL_MARK(4)
+  // (F) rank among the valid slots: the nslot^2 (slot, other) comparisons spread over all threads,
+  // ranks counted in LDS (a per-slot serial loop over nslot LDS reads took ~5 us at 44 slots)
+  for (int s = tid; s < nslot; s += kSelThreads) {
+    rank_s[s] = 0;
+    row_s[s] = (int)slot_row(s);
+  }
+  __syncthreads();
+  const int npair = nslot * nslot;
+  for (int p = tid; p < npair; p += kSelThreads) {
+    const int s = p / nslot, j2 = p - s * nslot;
+    const double sc = cand_d[s], sj = cand_d[j2];
+    if ((sj > sc) || (sj == sc && row_s[j2] < row_s[s])) atomicAdd(&rank_s[s], 1);
+  }
+  __syncthreads();
   for (int s = tid; s < nslot; s += kSelThreads) {
     const double sc = cand_d[s];
-    if (sc == -INFINITY) continue;
-    const int64_t ic = slot_row(s);
-    int rank = 0;
-    for (int j2 = 0; j2 < nslot; ++j2) {
-      const double sj = cand_d[j2];
-      rank += (sj > sc) || (sj == sc && slot_row(j2) < ic);
-    }
-    if (rank < kk) {
-      oi[rank] = ic + idx_base;
-      if (os) os[rank] = (float)sc;
-      if (os64) os64[rank] = sc;
-    }
+    const int rank = rank_s[s];
+    if (sc == -INFINITY || rank >= kk) continue;
+    oi[rank] = (int64_t)row_s[s] + idx_base;
+    if (os) os[rank] = (float)sc;
+    if (os64) os64[rank] = sc;
   }
   if (tid == 0 && status) status[qi] = st;
+  SEL_MARK(5)
+#ifdef MMR_SELECT_TRACE
+  if (blockIdx.x == 0 && threadIdx.x == 0) g_sel_trace[6] = cnt;
+#endif
 }
 
 // ------------------------------------------------------------------ shard merge

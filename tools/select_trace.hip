@@ -1,0 +1,49 @@
+// Phase clock of knn_select_groups (block 0): builds csrc/knn.hip with MMR_SELECT_TRACE into a
+// standalone binary, runs searches over a 100k x 768 Gaussian gallery and prints per-phase times.
+// build: hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -I include tools/select_trace.hip \
+//          multi-modal-retrieval-predict-project_amd/csrc/capi.cpp -o tools/select_trace.bin
+// run:   tools/select_trace.bin [Q] [mode]
+#define MMR_SELECT_TRACE
+#include "../multi-modal-retrieval-predict-project_amd/csrc/knn.hip"
+
+#include <random>
+
+int main(int argc, char** argv) {
+  const int Q = argc > 1 ? atoi(argv[1]) : 16, mode = argc > 2 ? atoi(argv[2]) : 2;
+  const int64_t n = 100000;
+  const int d = 768, K = 10;
+  std::vector<float> g((size_t)n * d), q((size_t)Q * d);
+  std::mt19937 rng(7);
+  std::normal_distribution<float> nd;
+  for (auto& x : g) x = nd(rng);
+  for (auto& x : q) x = nd(rng);
+  mmr_index* ix = nullptr;
+  if (mmr_index_create(g.data(), n, d, MMR_F32, 1, 0, 0, &ix) != MMR_OK || mmr_index_set_mode(ix, mode) != MMR_OK) {
+    printf("create failed: %s\n", mmr_last_error());
+    return 1;
+  }
+  float* qd;
+  int64_t* oi;
+  float* os;
+  hipMalloc(&qd, sizeof(float) * Q * d);
+  hipMalloc(&oi, sizeof(int64_t) * Q * K);
+  hipMalloc(&os, sizeof(float) * Q * K);
+  hipMemcpy(qd, q.data(), sizeof(float) * Q * d, hipMemcpyHostToDevice);
+  const char* names[] = {"A: query row + thread maxima", "B: radix threshold", "C: collect", "E: f64 re-score",
+                         "F: rank + write"};
+  for (int it = 0; it < 6; ++it) {
+    if (mmr_index_search(ix, qd, Q, K, oi, os, nullptr, nullptr, nullptr) != MMR_OK) {
+      printf("search failed: %s\n", mmr_last_error());
+      return 1;
+    }
+    hipDeviceSynchronize();
+    long long t[16];
+    hipMemcpyFromSymbol(t, HIP_SYMBOL(g_sel_trace), sizeof(t));
+    if (it < 2) continue;
+    printf("Q=%d mode=%d run %d: groups collected %lld, total %.2f us |", Q, mode, it, t[6], (t[5] - t[0]) * 0.01);
+    for (int p = 0; p < 5; ++p) printf(" %s %.2f |", names[p], (t[p + 1] - t[p]) * 0.01);
+    printf("\n");
+  }
+  mmr_index_destroy(ix);
+  return 0;
+}
