@@ -818,10 +818,11 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_groups(
   __shared__ double cand_d[kCandCap];
   __shared__ int rank_s[kCandCap];
   __shared__ int row_s[kCandCap];
+  __shared__ __attribute__((aligned(16))) float qrow[kSelThreads];  // query row (d <= 1024)
 
   SEL_MARK(0)
   const int64_t qi = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   const float* row = gmax + qi * ldG;
   const int kk = (int)(n < (int64_t)k ? n : (int64_t)k);
   int64_t* oi = out_idx + qi * k;
@@ -836,16 +837,10 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_groups(
     if (tid == 0 && status) status[qi] = 0;
     return;
   }
-  // the raw query row (f64 re-score, phase E) is loaded first: its latency hides under phases A-D
+  // the raw query row (f64 re-score, phase E) is staged in LDS first: its latency hides under
+  // phases A-D and it holds no registers meanwhile
   const float* qr = q_raw + qi * (int64_t)d;
-  float qv[4][4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int kq = (c * 64 + lane) * 4 + e;
-      qv[c][e] = (d <= 1024 && kq < d) ? qr[kq] : 0.f;
-    }
+  if (d <= 1024) qrow[tid] = tid < d ? qr[tid] : 0.f;
   const int64_t ng = ldG;       // groups per query row (Np / 4, a multiple of 64)
   const int64_t n4 = ng >> 2;
   // the first kRegF4 float4 of each thread's strided slice stay in registers for (C): one HBM/L2
@@ -918,8 +913,9 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_groups(
     return (int64_t)(g >> 4) * 64 + (g & 15) + 16 * (s & 3);
   };
   if (d <= 1024) {
-    // latency-bound: each wave issues the float4 loads of RB rows before reducing any of them;
-    // the query row stays in registers (lane owns elements 4(64c + lane) .. +3)
+    // latency-bound: each wave issues the float4 loads of RB rows before reducing any of them
+    // (RB = 3 spills at the 128-VGPR budget of 1024 threads); the query row from LDS
+    // (lane owns elements 4(64c + lane) .. +3)
     constexpr int RB = 2;
     for (int s0 = wave * RB; s0 < nslot; s0 += (kSelThreads / 64) * RB) {
       float4 gv[RB][4];
@@ -931,19 +927,22 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_groups(
         const int64_t gi = s < nslot ? slot_row(s) : n;
         gir[r] = gi;
         gnr[r] = gi < n ? gnorm64[gi] : 0.0;
+        // one row pointer (padding slots read row 0; their score is discarded below)
+        const float* gr = gal + (gi < n ? gi : 0) * Dp + lane * 4;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int k0 = (c * 64 + lane) * 4;
-          gv[r][c] = (gi < n && k0 < Dp) ? *(const float4*)(gal + gi * Dp + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+        for (int c = 0; c < 4; ++c)
+          gv[r][c] = (c * 256 + lane * 4 < Dp) ? *(const float4*)(gr + c * 256) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
         double acc = 0.0;
 #pragma unroll
         for (int c = 0; c < 4; ++c)
-          acc += (double)qv[c][0] * gv[r][c].x + (double)qv[c][1] * gv[r][c].y + (double)qv[c][2] * gv[r][c].z +
-                 (double)qv[c][3] * gv[r][c].w;
+        {
+          const float4 qv = *(const float4*)(qrow + (c * 64 + lane) * 4);
+          acc += (double)qv.x * gv[r][c].x + (double)qv.y * gv[r][c].y + (double)qv.z * gv[r][c].z +
+                 (double)qv.w * gv[r][c].w;
+        }
         acc = mmr::wave_sum(acc);
         const int s = s0 + r;
         if (lane == 0 && s < nslot) {
