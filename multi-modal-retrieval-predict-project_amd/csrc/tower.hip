@@ -117,6 +117,42 @@ __global__ __launch_bounds__(256) void bert_embed(const int64_t* __restrict__ id
   const int p = (int)(tok % l);
   const float* wr = word + ids[tok] * (int64_t)c;
   const float* pr = pos + (int64_t)p * c;
+  if (c % 256 == 0 && c <= 1024) {
+    // the row in registers: lane owns floats 4(64j + lane) .. +3, every load issued at once
+    // (three runtime-count passes re-reading the row waited on each load in turn: 67 -> 34 us at 256 x 128)
+    float4 v[4];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = 4 * (64 * j + lane);
+      if (k < c) {
+        const float4 a = *(const float4*)(wr + k), bq = *(const float4*)(pr + k), t0 = *(const float4*)(type0 + k);
+        v[j] = make_float4(a.x + bq.x + t0.x, a.y + bq.y + t0.y, a.z + bq.z + t0.z, a.w + bq.w + t0.w);
+        s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+      }
+    }
+    const float mean = mmr::wave_sum(s) / c;
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (4 * (64 * j + lane) < c) {
+        const float d0 = v[j].x - mean, d1 = v[j].y - mean, d2 = v[j].z - mean, d3 = v[j].w - mean;
+        ss += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+      }
+    const float rstd = rsqrtf(mmr::wave_sum(ss) / c + eps);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = 4 * (64 * j + lane);
+      if (k < c) {
+        const float4 gg = *(const float4*)(g + k), bb = *(const float4*)(b + k);
+        uint2 o;
+        o.x = mmr::pack2bf((v[j].x - mean) * rstd * gg.x + bb.x, (v[j].y - mean) * rstd * gg.y + bb.y);
+        o.y = mmr::pack2bf((v[j].z - mean) * rstd * gg.z + bb.z, (v[j].w - mean) * rstd * gg.w + bb.w);
+        *(uint2*)(y + tok * c + k) = o;
+      }
+    }
+    return;
+  }
   float s = 0.f;
   for (int k = lane; k < c; k += 64) s += wr[k] + pr[k] + type0[k];
   const float mean = mmr::wave_sum(s) / c;
@@ -324,6 +360,30 @@ __global__ __launch_bounds__(256) void patch_im2col(const float* __restrict__ im
   store8(cols + t * kp + ch * 8, v);
 }
 
+// Swin's patch 4 / 3 channels, fewer than 2^31 image elements: thread (token, 8-chunk) ch < 6 reads
+// channel ch/2, kernel rows 2(ch%2), 2(ch%2)+1 as two float4 (k = c*16 + ky*4 + kx), ch 6-7 are the
+// zero K padding; 32-bit index math (generic form with 64-bit divisions: 100 us, this one 40 us at 256 images).
+__global__ __launch_bounds__(256) void patch_im2col_p4c3(const float* __restrict__ img,
+                                                         uint16_t* __restrict__ cols, uint32_t ntok,
+                                                         uint32_t hw) {
+  const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
+  if (idx >= ntok * 8u) return;
+  const uint32_t t = idx >> 3, ch = idx & 7u;
+  const uint32_t g = hw >> 2, gg = g * g;
+  const uint32_t bi = t / gg, r = t - bi * gg, py = r / g, px = r - py * g;
+  float v[8];
+  if (ch < 6) {
+    const uint32_t c = ch >> 1, ky = (ch & 1u) * 2u;
+    const float* p0 = img + ((bi * 3u + c) * hw + py * 4u + ky) * hw + px * 4u;
+    const float4 a = *(const float4*)p0, b = *(const float4*)(p0 + hw);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.f;
+  }
+  store8(cols + (size_t)t * 64 + ch * 8, v);
+}
+
 // ------------------------------------------------------------------ PatchMerging gather + LN(4c)
 __global__ __launch_bounds__(256) void patch_merge_ln(const uint16_t* __restrict__ x,
                                                       const float* __restrict__ g,
@@ -370,21 +430,25 @@ __global__ __launch_bounds__(256) void patch_merge_ln(const uint16_t* __restrict
 
 // ------------------------------------------------------------------ Swin head: LN, LN(LN), means
 constexpr int SH_MAXPL = 16;  // c <= 1024, c % 64 == 0
-__global__ __launch_bounds__(256) void swin_head(const uint16_t* __restrict__ x,
+// 16 waves per image, tokens strided over the waves (4 waves: one token at a time per wave, 49 /
+// 4 dependent load-reduce rounds: 103 -> 37 us at 256 x 49 x 768); per-wave partial sums reduced through
+// one 64-KB LDS array in two rounds (acc1, then acc2).
+constexpr int SH_WAVES = 16;
+__global__ __launch_bounds__(64 * SH_WAVES) void swin_head(const uint16_t* __restrict__ x,
                                                  const float* __restrict__ g,
                                                  const float* __restrict__ b,
                                                  float* __restrict__ patches,
                                                  float* __restrict__ glob,
                                                  float* __restrict__ pool, int t, int c,
                                                  float eps) {
-  __shared__ float part[4][2][1024];
+  __shared__ float part[SH_WAVES][1024];
   const int bi = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int per = c / 64;
   float acc1[SH_MAXPL], acc2[SH_MAXPL];
 #pragma unroll
   for (int e = 0; e < SH_MAXPL; ++e) acc1[e] = acc2[e] = 0.f;
-  for (int tk = wave; tk < t; tk += 4) {
+  for (int tk = wave; tk < t; tk += SH_WAVES) {
     const uint16_t* xr = x + ((int64_t)bi * t + tk) * c;
     float v[SH_MAXPL];
     float s = 0.f;
@@ -425,14 +489,19 @@ __global__ __launch_bounds__(256) void swin_head(const uint16_t* __restrict__ x,
   }
 #pragma unroll
   for (int e = 0; e < SH_MAXPL; ++e)
-    if (e < per) {
-      part[wave][0][lane + 64 * e] = acc1[e];
-      part[wave][1][lane + 64 * e] = acc2[e];
-    }
+    if (e < per) part[wave][lane + 64 * e] = acc1[e];
   __syncthreads();
-  for (int k = threadIdx.x; k < c; k += 256) {
-    const float s1 = part[0][0][k] + part[1][0][k] + part[2][0][k] + part[3][0][k];
-    const float s2 = part[0][1][k] + part[1][1][k] + part[2][1][k] + part[3][1][k];
+  const int k = threadIdx.x;  // blockDim = 1024 >= c
+  float s1 = 0.f, s2 = 0.f;
+  if (k < c)
+    for (int w = 0; w < SH_WAVES; ++w) s1 += part[w][k];  // fixed order: deterministic
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < SH_MAXPL; ++e)
+    if (e < per) part[wave][lane + 64 * e] = acc2[e];
+  __syncthreads();
+  if (k < c) {
+    for (int w = 0; w < SH_WAVES; ++w) s2 += part[w][k];
     const float gm = s1 / t;
     if (glob) glob[(int64_t)bi * c + k] = gm;
     if (pool) pool[(int64_t)bi * c + k] = (gm + s2) / (t + 1);
@@ -672,8 +741,13 @@ mmr_status mmr_patch_im2col(const float* image, uint16_t* cols, int32_t b, int32
   MMR_REQUIRE(cin * patch * patch <= 64 && hw % patch == 0, "mmr_patch_im2col: cin*patch^2 must be <= 64");
   const int64_t ntok = (int64_t)b * (hw / patch) * (hw / patch);
   if (ntok == 0) return MMR_OK;
-  patch_im2col<<<dim3((unsigned)mmr::ceil_div(ntok * 8, 256)), 256, 0, mmr::as_stream(stream)>>>(
-      image, cols, ntok, cin, hw, patch);
+  if (patch == 4 && cin == 3 && hw % 4 == 0 && (int64_t)b * 3 * hw * hw < (int64_t(1) << 31) &&
+      ((uintptr_t)image & 15u) == 0)
+    patch_im2col_p4c3<<<dim3((unsigned)mmr::ceil_div(ntok * 8, 256)), 256, 0, mmr::as_stream(stream)>>>(
+        image, cols, (uint32_t)ntok, (uint32_t)hw);
+  else
+    patch_im2col<<<dim3((unsigned)mmr::ceil_div(ntok * 8, 256)), 256, 0, mmr::as_stream(stream)>>>(
+        image, cols, ntok, cin, hw, patch);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }
@@ -699,7 +773,7 @@ mmr_status mmr_swin_head(const uint16_t* x, const float* gamma, const float* bet
   MMR_REQUIRE(x && gamma && beta, "mmr_swin_head: NULL pointer");
   MMR_REQUIRE(c % 64 == 0 && c <= 64 * SH_MAXPL && t > 0, "mmr_swin_head: c=%d must be a multiple of 64 <= 1024", c);
   if (b == 0) return MMR_OK;
-  swin_head<<<dim3((unsigned)b), 256, 0, mmr::as_stream(stream)>>>(x, gamma, beta, patches, global,
+  swin_head<<<dim3((unsigned)b), 64 * SH_WAVES, 0, mmr::as_stream(stream)>>>(x, gamma, beta, patches, global,
                                                                    pool, t, c, eps);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
