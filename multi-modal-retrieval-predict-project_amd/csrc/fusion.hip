@@ -306,9 +306,18 @@ __global__ __launch_bounds__(256) void add_pos_bf16(const TX* __restrict__ x, co
   const int nch = c / 8;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= rows * nch) return;
-  const int64_t row = i / nch;
-  const int ch = (int)(i % nch);
-  const int t = (int)(row % l);
+  int64_t row;
+  int ch, t;
+  if (rows * nch < (int64_t(1) << 31)) {  // 32-bit divisions (64-bit ones dominate this kernel)
+    const uint32_t i32 = (uint32_t)i, r32 = i32 / (uint32_t)nch;
+    row = r32;
+    ch = (int)(i32 - r32 * (uint32_t)nch);
+    t = (int)(r32 % (uint32_t)l);
+  } else {
+    row = i / nch;
+    ch = (int)(i % nch);
+    t = (int)(row % l);
+  }
   float v[8];
   if constexpr (sizeof(TX) == 4) {
     const float4 a = *(const float4*)((const float*)x + row * c + ch * 8);

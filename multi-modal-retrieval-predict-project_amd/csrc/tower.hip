@@ -403,6 +403,40 @@ __global__ __launch_bounds__(256) void patch_merge_ln(const uint16_t* __restrict
     const int yy = 2 * i + (p & 1), xx = 2 * j + (p >> 1);
     return x + ((bi * hw + yy) * hw + xx) * (int64_t)c + off;
   };
+  if (c4 <= 2048) {
+    // the 4c-wide merged row in registers (<= 4 chunks of 8 per lane), every load issued at once:
+    // one memory round trip instead of three passes that each wait on their loads
+    float v[4][8];
+    float s = 0.f;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int k = lane * 8 + 512 * it;
+      if (k < c4) {
+        load8(src(k), v[it]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += v[it][e];
+      }
+    }
+    const float mean = mmr::wave_sum(s) / c4;
+    float ss = 0.f;
+#pragma unroll
+    for (int it = 0; it < 4; ++it)
+      if (lane * 8 + 512 * it < c4) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ss += (v[it][e] - mean) * (v[it][e] - mean);
+      }
+    const float rstd = rsqrtf(mmr::wave_sum(ss) / c4 + eps);
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int k = lane * 8 + 512 * it;
+      if (k < c4) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[it][e] = (v[it][e] - mean) * rstd * g[k + e] + b[k + e];
+        store8(y + o * c4 + k, v[it]);
+      }
+    }
+    return;
+  }
   float s = 0.f;
   for (int k = lane * 8; k < c4; k += 512) {
     float v[8];
