@@ -1387,8 +1387,19 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
         const dim3 grid((unsigned)(ix->Np / 64));
         const uint16_t* qh = (const uint16_t*)ix->qn;
         switch (qt) {
-          case 1: knn_scan_f16_gmax<1, 128><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n); break;
-          case 2: knn_scan_f16_gmax<2, 128><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n); break;
+          // KC must divide Dp (a multiple of 64): the 128-wide chunk only when Dp % 128 == 0
+          case 1:
+            if (ix->Dp % 128 == 0)
+              knn_scan_f16_gmax<1, 128><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n);
+            else
+              knn_scan_f16_gmax<1, 64><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n);
+            break;
+          case 2:
+            if (ix->Dp % 128 == 0)
+              knn_scan_f16_gmax<2, 128><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n);
+            else
+              knn_scan_f16_gmax<2, 64><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n);
+            break;
           case 4: knn_scan_f16_gmax<4, 64><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n); break;
           case 8: knn_scan_f16_gmax<8, 64><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n); break;
           default: knn_scan_f16_gmax<16, 32><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n); break;

@@ -124,6 +124,24 @@ def test_knn_f16_scan_query_tiles(Q):
     assert gi[0, :9].tolist() == [3] + list(range(5000, 5008))
 
 
+@pytest.mark.parametrize("D", [8, 24, 150, 200, 1000])
+@pytest.mark.parametrize("Q", [1, 20, 40, 130])
+def test_knn_f16_dims_not_multiple_of_chunk(D, Q):
+    """fp16 scan with padded dims Dp = 64 / 192 / 256 / 1024: every chunk width must divide Dp."""
+    rng = np.random.default_rng(D * 1000 + Q)
+    G = rng.standard_normal((3000 + D, D), dtype=np.float32)
+    Qm = rng.standard_normal((Q, D), dtype=np.float32)
+    _exact_check(G, Qm, 10, mode="f16")
+
+
+@pytest.mark.parametrize("D", [8, 150])
+def test_knn_skinny_dims(D):
+    rng = np.random.default_rng(D)
+    G = rng.standard_normal((2500, D), dtype=np.float32)
+    _exact_check(G, rng.standard_normal((5, D), dtype=np.float32), 10)
+    _exact_check(G, rng.standard_normal((30, D), dtype=np.float32), 10)
+
+
 def test_knn_f16_labelled_and_negative():
     G, _ = synthetic.labelled_gallery(4000, 256, 11)
     Qm, _ = synthetic.labelled_gallery(50, 256, 12)
