@@ -433,20 +433,25 @@ __global__ __launch_bounds__(64 * WQ) void knn_scan_f16_gmax(const uint16_t* __r
   for (int t = 0; t < QT; ++t)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[t][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  f32x4 b[4][L];
+  f32x4 b[4][L], a[QT][L];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int e = 0; e < L; ++e) {
 #pragma unroll
-    for (int e = 0; e < L; ++e) b[j][e] = __builtin_nontemporal_load((const f32x4*)(pb + j * tileB + 512 * e));
-  #pragma unroll 1
+    for (int t = 0; t < QT; ++t) a[t][e] = *(const f32x4*)(pa + t * tileB + 512 * e);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j][e] = __builtin_nontemporal_load((const f32x4*)(pb + j * tileB + 512 * e));
+  }
+#pragma unroll 1
   for (int kc = 0; kc < Dp; kc += KC) {
-    f32x4 a[QT][L];
-#pragma unroll
-    for (int t = 0; t < QT; ++t)
-#pragma unroll
-      for (int e = 0; e < L; ++e) a[t][e] = *(const f32x4*)(pa + t * tileB + 16 * kc + 512 * e);
-    f32x4 nb[4][L];
+    // both operands of the NEXT chunk are issued before this chunk's MFMAs (queries first: vmcnt
+    // retires in issue order); the current ones were issued one iteration earlier.  Unconditional
+    // (the last chunk re-reads itself): a branch would make the vmcnt at the join wait for them.
     const int kn = kc + KC < Dp ? kc + KC : kc;
+    f32x4 na[QT][L], nb[4][L];
+#pragma unroll
+    for (int e = 0; e < L; ++e)
+#pragma unroll
+      for (int t = 0; t < QT; ++t) na[t][e] = *(const f32x4*)(pa + t * tileB + 16 * kn + 512 * e);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -463,9 +468,12 @@ __global__ __launch_bounds__(64 * WQ) void knn_scan_f16_gmax(const uint16_t* __r
                                                              __builtin_bit_cast(h8, b[j][e]), acc[t][j], 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int e = 0; e < L; ++e) {
 #pragma unroll
-      for (int e = 0; e < L; ++e) b[j][e] = nb[j][e];
+      for (int j = 0; j < 4; ++j) b[j][e] = nb[j][e];
+#pragma unroll
+      for (int t = 0; t < QT; ++t) a[t][e] = na[t][e];
+    }
   }
   const int64_t gcol = blk * 16 + r;
   bool pad[4];
