@@ -1,48 +1,68 @@
 """Benchmark of the hot path (BASELINE.json metric: query embeddings/sec + cosine-pairs/sec,
 100k x 768 gallery).
 
-python bench.py --gpus N --steps K --warmup W [--mode full|knn]
+python bench.py --gpus N --steps K --warmup W [--mode full|knn] [--preset cfg2|cfg3|cfg4]
   full (default): one step = Swin-T tower on B synthetic 224x224 images + ClinicalBERT-geometry
         tower on B synthetic 128-token reports (bf16) -> joint-embedding head (default: the
-        reference's default model_type "multimodal", 5 fusion layers x 8 heads; --model-type
-        text|image runs both single-modality heads) -> exact cosine top-10 of the query embeddings
-        over the gallery (config 2: B=256, 100k x 768 f32).
+        reference's default model_type "multimodal", 5 fusion layers x 8 heads) -> exact cosine
+        top-K of the query embeddings over the gallery (config 2: B=256, 100k x 768 f32, K=10).
+        --model-type text: text tower + text head only (config 3's text-only ClinicalBERT queries);
+        image: image tower + image head only; both: both single-modality heads (2B embeddings).
   knn:  one step = exact cosine top-K of B resident queries over the gallery (kNN leg only).
-N>1 (torch.distributed.run): the gallery is row-sharded (N x rows per rank: weak scaling), every
-rank runs its own query batch through the towers and searches its shard for ALL ranks' queries
-(all-gather of query embeddings), then per-shard top-K lists are all-gathered over RCCL and merged.
-Rank 0 prints ONE JSON line.
+Presets (BASELINE.json configs): cfg2 = the defaults; cfg3 = --model-type text --batch 1024
+  --gallery 1000000 --k 50; cfg4 = cfg2 with 1M gallery rows per GPU (8M at --gpus 8).
+N>1: `python bench.py --gpus N` starts N ranks itself (torch.distributed.run, one process per GPU,
+RCCL) unless it already runs under a launcher (WORLD_SIZE set, which must equal --gpus).  The
+gallery is row-sharded (--gallery rows per rank: weak scaling), every rank runs its own query batch
+through the towers and searches its shard for ALL ranks' queries (all-gather of query embeddings),
+then the per-shard top-K lists are all-gathered over RCCL and merged.  Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+PRESETS = {
+    "cfg2": {},
+    "cfg3": {"model_type": "text", "batch": 1024, "gallery": 1_000_000, "k": 50},
+    "cfg4": {"gallery": 1_000_000},
+}
 
-def parse():
+
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--mode", choices=["full", "knn"], default="full")
-    p.add_argument("--batch", type=int, default=256)
+    p.add_argument("--preset", choices=sorted(PRESETS), default="cfg2",
+                   help="BASELINE.json config: cfg2 (default), cfg3 (text-only B=1024, 1M x 768, top-50), "
+                        "cfg4 (1M rows per GPU); explicit flags override the preset")
+    p.add_argument("--batch", type=int, default=None)
     p.add_argument("--knn-mode", choices=["x3", "f16"], default="f16",
                    help="gallery scan: f16 (fp16 unit-row copy, default) or x3 (bf16 split GEMM; skinny f32 "
                         "stream for Q <= 32); both exact (f64 re-rank from the f32 rows)")
-    p.add_argument("--gallery", type=int, default=100_000, help="gallery rows per GPU")
+    p.add_argument("--gallery", type=int, default=None, help="gallery rows per GPU")
     p.add_argument("--dim", type=int, default=768)
-    p.add_argument("--k", type=int, default=10)
-    p.add_argument("--model-type", choices=["multimodal", "text", "image"], default="multimodal",
-                   help="joint-embedding head: multimodal (reference default, model.py:137; 5 fusion "
-                        "layers, 8 heads) or the single-modality heads (text + image both run)")
+    p.add_argument("--k", type=int, default=None)
+    p.add_argument("--model-type", choices=["multimodal", "text", "image", "both"], default=None,
+                   help="joint-embedding head: multimodal (reference default, model.py:137; 5 fusion layers, "
+                        "8 heads), text / image (one tower + its head), both (both single-modality heads)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-queries", type=int, default=0)
-    return p.parse_args()
+    a = p.parse_args(argv)
+    pre = dict({"batch": 256, "gallery": 100_000, "k": 10, "model_type": "multimodal"}, **PRESETS[a.preset])
+    for key, v in pre.items():
+        if getattr(a, key) is None:
+            setattr(a, key, v)
+    return a
 
 
 def cpu_model():
@@ -55,23 +75,57 @@ def cpu_model():
     return platform.processor()
 
 
+def usable_cpus():
+    """CPUs this process may actually run on: the affinity mask, capped by a cgroup CPU quota
+    (a GPU box exposes the whole machine's cores to os.cpu_count() but grants a share of them)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def launch_ranks(a):
+    """--gpus N > 1 outside a launcher: start N ranks (one process per GPU) through
+    torch.distributed.run on 127.0.0.1 and exit with its status.  Runs before anything touches the
+    GPU, as a child process (never an exec)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     a = parse()
+    if a.gpus < 1:
+        sys.exit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}: refusing to report a mismatched run")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     dev = torch.device(f"cuda:{local}")
 
-    import mmr_amd
+    import mmr_amd  # noqa: F401
     from mmr_amd import synthetic
-    from mmr_amd.retrieval import GalleryIndex, merge_topk
+    from mmr_amd.retrieval import GalleryIndex, check_status, merge_topk
 
     # gallery shard: rows [rank*n, (rank+1)*n) of a virtual (world*n, d) N(0,1) gallery
     n, d, K, B = a.gallery, a.dim, a.k, a.batch
@@ -80,21 +134,26 @@ def main():
     index.reserve(2 * B * world)
 
     model = None
+    imgs = ids = mask = None
     if a.mode == "full":
         from mmr_amd.model import build_bench_model
-        model = build_bench_model(device=dev, joint_dim=d, model_type=a.model_type)
-        imgs = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(B, synthetic.SEED + rank))).to(dev)
-        ids_np, mask_np = synthetic.reports(B, 128, synthetic.SEED + 100 + rank)
-        ids, mask = torch.from_numpy(ids_np).to(dev), torch.from_numpy(mask_np).to(dev)
+        mt = "text" if a.model_type == "both" else a.model_type
+        model = build_bench_model(device=dev, joint_dim=d, model_type=mt)
+        if a.model_type != "text":
+            imgs = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(B, synthetic.SEED + rank))).to(dev)
+        if a.model_type != "image":
+            ids_np, mask_np = synthetic.reports(B, 128, synthetic.SEED + 100 + rank)
+            ids, mask = torch.from_numpy(ids_np).to(dev), torch.from_numpy(mask_np).to(dev)
     else:
         qbatch = torch.from_numpy(synthetic.gauss_gallery(B, d, synthetic.SEED + 1 + rank)).to(dev)
 
     stream = torch.cuda.current_stream(dev)
     ev_pairs = []
+    st_max = torch.zeros((), dtype=torch.int32, device=dev)  # max per-query status over all searches
 
     def step(record):
         if model is not None:
-            q = model.query_embeddings(imgs, ids, mask)            # (B, d) f32
+            q = model.query_embeddings(imgs, ids, mask)            # (B or 2B, d) f32
         else:
             q = qbatch
         if world > 1:
@@ -105,17 +164,18 @@ def main():
         if record:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        i, s, s64 = index.search(allq, K, want_f64=True)
+        i, s, s64, st = index.search(allq, K, want_f64=True, want_status=True)
         if record:
             e1.record(stream)
             ev_pairs.append((e0, e1))
+        torch.maximum(st_max, st.max(), out=st_max)  # checked after the timed region (no sync here)
         if world > 1:
             gi = torch.empty((world * i.shape[0], K), dtype=i.dtype, device=dev)
             gs = torch.empty((world * s64.shape[0], K), dtype=s64.dtype, device=dev)
             dist.all_gather_into_tensor(gi, i)
             dist.all_gather_into_tensor(gs, s64)
             i, s, _ = merge_topk(gs.view(world, -1, K), gi.view(world, -1, K), K)
-        return i, s
+        return q, i, s
 
     for _ in range(a.warmup):
         step(False)
@@ -135,9 +195,13 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # every search of the timed region returned an exact list (status 0 for every query)
+    check_status(st_max.view(1))
     ms_search = sum(e0.elapsed_time(e1) for e0, e1 in ev_pairs) / max(len(ev_pairs), 1)
-    # HBM-bound regime probe (after the timed region): searches of 16 resident queries run the
-    # skinny scan (knn_scan_f32_gmax streams the gallery once), timed with events on the launch stream
+    q_last, i_last, _ = out
+    # HBM-bound regime probe (after the timed region): 16 resident queries — the f16 scan's one-tile
+    # stream (knn_scan_f16_gmax<1>) or, in x3 mode, the skinny f32 stream — timed with events on the
+    # launch stream, whole search call
     q16 = torch.from_numpy(synthetic.gauss_gallery(16, d, synthetic.SEED + 5 + rank)).to(dev)
     for _ in range(3):
         index.search(q16, K)
@@ -145,18 +209,21 @@ def main():
     for _ in range(20):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
-        index.search(q16, K)
+        _, _, st16 = index.search(q16, K, want_status=True)
         e1.record(stream)
         hev.append((e0, e1))
     torch.cuda.synchronize(dev)
+    check_status(st16)
     ms_small = sum(e0.elapsed_time(e1) for e0, e1 in hev) / len(hev)
-    if model is not None:
-        # roofline kernel (BERT FFN1) timed in a short pass right after the timed region with the
-        # towers in sequence: inside the timed steps the Swin tower runs concurrently on a side
-        # stream, and events around one kernel would also count the co-running kernels' share
+    gemm_ms = {}
+    if model is not None and a.model_type != "image":
+        # per-launch GEMM timings (BERT QKV / O-proj / FFN1 / FFN2) in a short pass right after the
+        # timed region with the towers in sequence: inside the timed steps the Swin tower runs
+        # concurrently on a side stream, and events around one kernel would also count the
+        # co-running kernels' share
         saved = {k: os.environ.get(k) for k in ("MMR_TOWER_STREAMS", "MMR_FUSION_STREAMS")}
         os.environ.update({k: "0" for k in saved})
-        model.backbones.bert.ffn1_events = []
+        model.backbones.bert.gemm_events = {}
         for _ in range(3):
             step(False)
         torch.cuda.synchronize(dev)
@@ -165,89 +232,32 @@ def main():
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
+        for name, evs in model.backbones.bert.gemm_events.items():
+            gemm_ms[name] = sum(e0.elapsed_time(e1) for e0, e1 in evs) / max(len(evs), 1)
+        model.backbones.bert.gemm_events = None
 
     # whole-job throughput: every rank embeds B queries; every query is scored against the whole
     # world*n gallery (each rank scores all world*B queries against its n rows)
-    # full mode: one multimodal joint embedding per (image, report) pair, or image-head + text-head
-    nq_step = (2 * B) if (model is not None and a.model_type != "multimodal") else B
-    q_per_s = world * B * a.steps / elapsed
+    nq_step = (2 * B) if (model is not None and a.model_type == "both") else B
+    q_per_s = world * nq_step * a.steps / elapsed
     pairs_per_s = (world * nq_step) * (world * n) * a.steps / elapsed
-    # roofline of the dominant kernel, per launch on one GPU
     Qs = world * nq_step
-    # kNN search: algorithmic flops 2*Q*N*D; bytes = the scanned gallery copy once + norms + queries +
-    # results.  f16: fp16 unit rows (N*D*2), one fp16 MFMA product per f32 product (dense fp16 peak =
-    # bf16 peak), HBM-bound below Q ~ 312.  x3: hi/lo bf16 (N*D*4), 3 bf16 MFMA products per f32
-    # product; Q <= 32 streams the f32 tile16 copy (N*D*4) on f32 MFMA (HBM-bound).
-    peak_bf16, peak_hbm = 2.5e15, 8.0e12
-    gbytes = 2 if a.knn_mode == "f16" else 4
-    knn_flops = 2.0 * Qs * n * d
-    knn_bytes = n * d * gbytes + n * 4 + Qs * d * 4 + Qs * K * 12
-    mfma_work = knn_flops * (1 if a.knn_mode == "f16" else 3)
-    if a.knn_mode == "f16":
-        kname = "mmr_index_search (prep + knn_scan_f16_gmax fp16 MFMA stream + knn_select_groups f64 re-rank)"
-    elif Qs <= 32:
-        kname = "mmr_index_search (prep + knn_scan_f32_gmax skinny f32 MFMA stream + knn_select_groups)"
-    else:
-        kname = "mmr_index_search (prep + knn_scores_x3_gmax bf16x3 MFMA + knn_select_groups)"
-    mfma_bound = a.knn_mode == "x3" and Qs > 32 and mfma_work / peak_bf16 > knn_bytes / peak_hbm
-    if a.knn_mode == "f16":
-        mfma_bound = mfma_work / peak_bf16 > knn_bytes / peak_hbm
-    knn_roof = {"kernel": kname, "scan_mode": a.knn_mode,
-                "ms_per_launch": ms_search, "flops": knn_flops, "bytes": knn_bytes,
-                "bound": "mfma" if mfma_bound else "hbm",
-                "achieved_tflops_f32_equiv": knn_flops / (ms_search / 1e3) / 1e12,
-                "achieved_gbs": knn_bytes / (ms_search / 1e3) / 1e9}
-    small_bytes = n * d * gbytes + n * 4 + q16.shape[0] * d * 4 + q16.shape[0] * K * 12
-    knn_roof["hbm_regime"] = {
-        "queries": int(q16.shape[0]), "ms_per_search": ms_small, "bytes": small_bytes,
-        "achieved_gbs": small_bytes / (ms_small / 1e3) / 1e9,
-        "frac": small_bytes / (ms_small / 1e3) / peak_hbm,
-        "kernel": "whole search call: prep + %s scan + knn_select_groups (events on the launch stream)"
-                  % ("knn_scan_f16_gmax" if a.knn_mode == "f16" else "knn_scan_f32_gmax")}
-    if model is not None:
-        evs = model.backbones.bert.ffn1_events
-        ms_ffn1 = sum(e0.elapsed_time(e1) for e0, e1 in evs) / max(len(evs), 1)
-        fl = 2.0 * B * 128 * 3072 * 768
-        roof = {"bound": "mfma", "achieved": fl / (ms_ffn1 / 1e3) / 1e12, "peak": peak_bf16 / 1e12,
-                "unit": "TFLOP/s", "traffic": None,
-                "kernel": ("BERT FFN1 GEMM + GELU (M=%d, N=3072, K=768; tuned variant), %d launches timed in a "
-                           "towers-in-sequence pass after the timed region" % (B * 128, len(evs))),
-                "ms_per_launch": ms_ffn1, "flops_per_launch": fl, "knn": knn_roof}
-    else:
-        if knn_roof["bound"] == "mfma":
-            roof = {"bound": "mfma", "achieved": mfma_work / (ms_search / 1e3) / 1e12, "peak": peak_bf16 / 1e12,
-                    "unit": "TFLOP/s"}
-        else:
-            roof = {"bound": "hbm", "achieved": knn_roof["achieved_gbs"], "peak": peak_hbm / 1e9, "unit": "GB/s"}
-        roof.update({"traffic": None, "kernel": knn_roof["kernel"], "ms_per_launch": ms_search,
-                     "hbm_regime": knn_roof["hbm_regime"]})
-    roof["frac"] = roof["achieved"] / roof["peak"]
-    # HBM traffic per launch from the committed PMC pass (tools/pmc_traffic.py; FETCH_SIZE x2 per the
-    # gfx950 correction + WRITE_SIZE), for the same kernels at the same shapes
-    tr = pmc_traffic()
-    if model is not None:
-        # the FFN1 launch variant the per-shape tuner settled on here; its PMC record if committed
-        from mmr_amd import _lib
-        var = int(_lib.lib().mmr_linear_bf16_variant(B * 128, 3072, 768, 1, 1, 0))
-        roof["variant"] = var
-        rec = tr.get(f"bert_ffn1_v{var}")
-        if rec is not None:
-            roof["traffic"] = rec["hbm_bytes"]
-            roof["traffic_source"] = rec["source"]
-    if (model is None and a.knn_mode == "x3" and "knn_scores_x3" in tr and "knn_select" in tr and B == 256
-            and n == 100_000 and d == 768):
-        roof["traffic"] = tr["knn_scores_x3"]["hbm_bytes"] + tr["knn_select"]["hbm_bytes"]
-        roof["traffic_source"] = tr["knn_scores_x3"]["source"]
-    if (model is None and a.knn_mode == "f16" and "knn_scan_f16" in tr and "knn_select_f16" in tr and B == 256
-            and n == 100_000 and d == 768):
-        roof["traffic"] = tr["knn_scan_f16"]["hbm_bytes"] + tr["knn_select_f16"]["hbm_bytes"]
-        roof["traffic_source"] = tr["knn_scan_f16"]["source"]
+    roof, knn_roof = roofline(a, n, d, K, Qs, ms_search, ms_small, q16.shape[0], gemm_ms, B)
 
-    cpu = None
+    cpu = cpu_knn = recall = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(a, G, qbatch) if model is None else cpu_baseline_full(a, G)
+        if model is None:
+            cpu = cpu_baseline_knn(a, G, qbatch.cpu().numpy())
+        else:
+            cpu, emb_cpu = cpu_baseline_full(a, G, imgs, ids, mask)
+            cpu_knn = cpu_baseline_knn(a, G, q_last[:64].cpu().numpy())
+            recall = recall_vs_cpu(index, q_last[:emb_cpu.shape[0]], emb_cpu, G, K)
 
     if rank == 0:
+        workload = {
+            "multimodal": "Swin-T + BERT-base towers + 5-layer multimodal fusion head",
+            "text": "text-only BERT-base tower + text head", "image": "Swin-T tower + image head",
+            "both": "Swin-T + BERT-base towers + image and text heads"}[a.model_type]
         line = {
             "metric": "query embeddings/sec + cosine-pairs/sec @ Recall@10, 100k x 768 gallery",
             "value": q_per_s if a.mode == "full" else pairs_per_s,
@@ -261,18 +271,103 @@ def main():
                 "f32 gallery, fp16 unit-row scan copy, exact f64 re-rank" if a.knn_mode == "f16"
                 else "f32 gallery, bf16x3 scan, exact f64 re-rank"),
             "data": "synthetic (seeded N(0,1) gallery; random-init weights)",
-            "config": {"workload": ("cfg2: Swin-T + BERT-base towers + %s head, B=%d, top-%d over %dx%d f32 per GPU"
-                                    % ("5-layer multimodal fusion" if a.model_type == "multimodal" else "image+text",
-                                       B, K, n, d))
-                       if a.mode == "full" else ("kNN only: Q=%d, top-%d over %dx%d f32 per GPU" % (B, K, n, d)),
+            "config": {"workload": ("%s: %s, B=%d, top-%d over %dx%d f32 per GPU" % (a.preset, workload, B, K, n, d))
+                       if a.mode == "full" else ("%s kNN only: Q=%d, top-%d over %dx%d f32 per GPU" % (a.preset, B, K, n, d)),
                        "global_batch": world * B, "gallery_rows": world * n, "dim": d, "k": K,
-                       "parallelism": f"gallery row-shard x{world}" if world > 1 else "single"},
+                       "parallelism": f"gallery row-shard x{world} + tower DP x{world}" if world > 1 else "single"},
             "roofline": roof,
+            "knn_status_ok": True,
+            "recall_at_10_vs_cpu": recall["recall_at_k"] if recall else None,
+            "recall_vs_cpu": recall,
             "cpu_baseline": cpu,
+            "cpu_baseline_knn": cpu_knn,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def roofline(a, n, d, K, Qs, ms_search, ms_small, q_small, gemm_ms, B):
+    """Roofline object of the dominant kernel (full: the BERT FFN1 GEMM, with the other BERT GEMM
+    families beside it; knn: the search call) + the kNN search's own roofline."""
+    # kNN search: algorithmic flops 2*Q*N*D; bytes = the scanned gallery copy once + norms + queries +
+    # results.  f16: fp16 unit rows (N*D*2), one fp16 MFMA product per f32 product (dense fp16 peak =
+    # bf16 peak), HBM-bound below Q ~ 312.  x3: hi/lo bf16 (N*D*4), 3 bf16 MFMA products per f32
+    # product; Q <= 32 streams the f32 tile16 copy (N*D*4) on f32 MFMA (HBM-bound).
+    peak_bf16, peak_hbm = 2.5e15, 8.0e12
+    gbytes = 2 if a.knn_mode == "f16" else 4
+    knn_flops = 2.0 * Qs * n * d
+    knn_bytes = n * d * gbytes + n * 4 + Qs * d * 4 + Qs * K * 12
+    mfma_work = knn_flops * (1 if a.knn_mode == "f16" else 3)
+    if a.knn_mode == "f16":
+        kname = "mmr_index_search (prep + fp16 MFMA scan + knn_select_t f64 re-rank)"
+    elif Qs <= 32:
+        kname = "mmr_index_search (prep + knn_scan_f32_gmax skinny f32 MFMA stream + knn_select_t)"
+    else:
+        kname = "mmr_index_search (prep + knn_scores_x3_gmax bf16x3 MFMA + knn_select_t)"
+    t_hbm, t_mfma = knn_bytes / peak_hbm, mfma_work / peak_bf16
+    if a.knn_mode == "x3" and Qs <= 32:
+        t_mfma = 0.0
+    knn_roof = {"kernel": kname, "scan_mode": a.knn_mode, "queries": Qs,
+                "ms_per_launch": ms_search, "flops": knn_flops, "bytes": knn_bytes,
+                "bound": "mfma" if t_mfma > t_hbm else "hbm",
+                "bound_ms": max(t_hbm, t_mfma) * 1e3,
+                "frac_of_bound": max(t_hbm, t_mfma) / (ms_search / 1e3),
+                "achieved_tflops_f32_equiv": knn_flops / (ms_search / 1e3) / 1e12,
+                "achieved_gbs": knn_bytes / (ms_search / 1e3) / 1e9}
+    small_bytes = n * d * gbytes + n * 4 + q_small * d * 4 + q_small * K * 12
+    knn_roof["hbm_regime"] = {
+        "queries": int(q_small), "ms_per_search": ms_small, "bytes": small_bytes,
+        "achieved_gbs": small_bytes / (ms_small / 1e3) / 1e9,
+        "frac": small_bytes / (ms_small / 1e3) / peak_hbm,
+        "kernel": "whole search call: prep + %s scan + knn_select_t (events on the launch stream)"
+                  % ("knn_scan_f16_gmax<1>" if a.knn_mode == "f16" else "knn_scan_f32_gmax<1>")}
+    if gemm_ms:
+        M = B * 128
+        shapes = {"qkv": (M, 2304, 768), "o": (M, 768, 768), "ffn1": (M, 3072, 768), "ffn2": (M, 768, 3072)}
+        fam = {}
+        for name, ms in gemm_ms.items():
+            m_, n_, k_ = shapes[name]
+            fl = 2.0 * m_ * n_ * k_
+            fam[name] = {"shape_mnk": [m_, n_, k_], "ms_per_launch": ms, "tflops": fl / (ms / 1e3) / 1e12,
+                         "frac": fl / (ms / 1e3) / peak_bf16}
+        ms_ffn1 = gemm_ms["ffn1"]
+        fl = 2.0 * M * 3072 * 768
+        roof = {"bound": "mfma", "achieved": fl / (ms_ffn1 / 1e3) / 1e12, "peak": peak_bf16 / 1e12,
+                "unit": "TFLOP/s", "traffic": None,
+                "kernel": ("BERT FFN1 GEMM + GELU (M=%d, N=3072, K=768; tuned variant), timed per launch with HIP "
+                           "events in a towers-in-sequence pass after the timed region" % M),
+                "ms_per_launch": ms_ffn1, "flops_per_launch": fl, "bert_gemms": fam, "knn": knn_roof}
+    elif a.mode == "full":
+        roof = dict(knn_roof, bound=knn_roof["bound"], unit="GB/s", achieved=knn_roof["achieved_gbs"],
+                    peak=peak_hbm / 1e9)
+    else:
+        if knn_roof["bound"] == "mfma":
+            roof = {"bound": "mfma", "achieved": mfma_work / (ms_search / 1e3) / 1e12, "peak": peak_bf16 / 1e12,
+                    "unit": "TFLOP/s"}
+        else:
+            roof = {"bound": "hbm", "achieved": knn_roof["achieved_gbs"], "peak": peak_hbm / 1e9, "unit": "GB/s"}
+        roof.update({"traffic": None, "kernel": knn_roof["kernel"], "ms_per_launch": ms_search,
+                     "bound_ms": knn_roof["bound_ms"], "frac_of_bound": knn_roof["frac_of_bound"],
+                     "hbm_regime": knn_roof["hbm_regime"]})
+    roof["frac"] = roof["achieved"] / roof["peak"]
+    # HBM traffic per launch from the committed PMC pass (tools/pmc_traffic.py; FETCH_SIZE x2 per the
+    # gfx950 correction + WRITE_SIZE), for the same kernels at the same shapes
+    tr = pmc_traffic()
+    if gemm_ms:
+        from mmr_amd import _lib
+        var = int(_lib.lib().mmr_linear_bf16_variant(B * 128, 3072, 768, 1, 1, 0))
+        roof["variant"] = var
+        rec = tr.get(f"bert_ffn1_v{var}") or tr.get("bert_ffn1")
+        if rec is not None:
+            roof["traffic"] = rec["hbm_bytes"]
+            roof["traffic_source"] = rec["source"]
+    elif a.mode == "knn" and B == 256 and n == 100_000 and d == 768:
+        keys = ("knn_scan_f16", "knn_select_f16") if a.knn_mode == "f16" else ("knn_scores_x3", "knn_select")
+        if all(k in tr for k in keys):
+            roof["traffic"] = sum(tr[k]["hbm_bytes"] for k in keys)
+            roof["traffic_source"] = tr[keys[0]]["source"]
+    return roof, knn_roof
 
 
 def pmc_traffic():
@@ -285,66 +380,113 @@ def pmc_traffic():
         return {}
 
 
-def cpu_baseline(a, G, qbatch):
+def timed_median(fn, reps=5):
+    """one warm-up run, then the median of `reps` timed runs (seconds)."""
+    fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def _cores():
+    import torch
+    used = usable_cpus()
+    torch.set_num_threads(used)
+    try:
+        from threadpoolctl import threadpool_limits
+        threadpool_limits(used)
+    except Exception:
+        pass
+    return used
+
+
+def cpu_baseline_knn(a, G, Q):
     """kNN-only baseline: the reference's exact path restated (oracle/knn.py sklearn_topk =
     retrieval_overlap.py:84-90: normalise + f32 sgemm + per-row argsort) on a bounded query sample
-    against the same gallery, numpy BLAS on all host cores."""
+    against the same gallery, numpy BLAS on the usable host cores, median of 5 after a warm-up."""
     from oracle import knn as oknn
-    nq = a.cpu_sample_queries or min(64, a.batch)
-    Q = qbatch[:nq].cpu().numpy()
-    oknn.sklearn_topk(Q[:1], G, a.k)
-    t0 = time.perf_counter()
-    oknn.sklearn_topk(Q, G, a.k)
-    t = time.perf_counter() - t0
-    try:
-        from threadpoolctl import threadpool_info
-        cores = max(int(p.get("num_threads", 1)) for p in threadpool_info() if p.get("user_api") == "blas")
-    except Exception:
-        cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": nq * G.shape[0] / t, "unit": "cosine_pairs/s", "cores": cores, "kind": "port",
+    used = _cores()
+    nq = a.cpu_sample_queries or (16 if G.shape[0] > 200_000 else 64)
+    nq = min(nq, Q.shape[0])
+    t = timed_median(lambda: oknn.sklearn_topk(Q[:nq], G, a.k))
+    return {"value": nq * G.shape[0] / t, "unit": "cosine_pairs/s", "cores": used, "cores_visible": os.cpu_count(),
+            "kind": "port",
             "sample": f"{nq} queries x {G.shape[0]}x{G.shape[1]} gallery: numpy normalise + sgemm + argsort "
-                      f"top-{a.k} (oracle/knn.py), one timed run after warm-up, CPU: {cpu_model()}"}
+                      f"top-{a.k} (oracle/knn.py), median of 5 after one warm-up, {used} threads (usable CPUs of "
+                      f"{os.cpu_count()} visible), CPU: {cpu_model()}"}
 
 
-def cpu_baseline_full(a, G):
-    """Oracle CPU path (tests-only infrastructure, timed here as the baseline) on a bounded sample:
-    Swin-T + BERT-base fp32 towers (torch CPU, all host cores) + text/image heads + numpy cosine
-    top-K over the same gallery — the reference's PyTorch-CPU path restated (oracle/towers.py)."""
-    import numpy as np
+def cpu_baseline_full(a, G, imgs, ids, mask):
+    """Oracle CPU path (tests-only infrastructure, timed here as the baseline) on a bounded sample of
+    the bench's own inputs: Swin-T / BERT-base fp32 towers (torch CPU) + the same head + numpy cosine
+    top-K over the same gallery — the reference's PyTorch-CPU path restated (oracle/towers.py).
+    Returns (baseline dict, the sample's oracle joint embeddings) — the latter feed the recall."""
     import torch
-    from mmr_amd import synthetic
-    from mmr_amd.model import init_head_state
+    from mmr_amd.model import init_fusion_state, init_head_state
     from mmr_amd.towers import BERT_BASE, SWIN_T, init_bert_state, init_swin_state
     from oracle import knn as oknn
     from oracle import towers as otw
-    threads = torch.get_num_threads()
+    used = _cores()
     nb = a.cpu_sample_queries or 8
     ssd, bsd = init_swin_state(SWIN_T, 2709), init_bert_state(BERT_BASE, 2710)
     hsd = init_head_state(768, 768, a.dim, 2711)
     if a.model_type == "multimodal":
-        from mmr_amd.model import init_fusion_state
         hsd.update(init_fusion_state(768, 768, a.dim, 8, 5, 2712))
-    img = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(nb, synthetic.SEED)))
-    ids, mask = (torch.from_numpy(x) for x in synthetic.reports(nb, 128, synthetic.SEED + 100))
+    img = imgs[:nb].cpu() if imgs is not None else None
+    ii = ids[:nb].cpu() if ids is not None else None
+    mm = mask[:nb].cpu() if mask is not None else None
+    res = {}
 
-    def run(n):
+    def run():
         with torch.no_grad():
-            (g, p), t = otw.backbones_forward(img[:n], ids[:n], mask[:n], ssd, bsd, SWIN_T, BERT_BASE)
-            if a.model_type == "multimodal":
-                qi = otw.heads(g, p, t, hsd, "multimodal", mm_cfg={"num_heads": 8})["joint_emb"]
-                qt = qi[:0]
+            if a.model_type == "text":
+                t = otw.bert_forward(ii, mm, bsd, BERT_BASE["num_hidden_layers"], BERT_BASE["num_attention_heads"])
+                q = otw.heads(None, None, t, hsd, "text")["joint_emb"]
+            elif a.model_type == "image":
+                g, p = otw.swin_image(img, ssd, SWIN_T)
+                q = otw.heads(g, p, None, hsd, "image")["joint_emb"]
             else:
-                qi = otw.heads(g, p, t, hsd, "image")["joint_emb"]
-                qt = otw.heads(g, p, t, hsd, "text")["joint_emb"]
-        oknn.sklearn_topk(torch.cat([qi, qt]).numpy(), G, a.k)
-    run(1)
-    t0 = time.perf_counter()
-    run(nb)
-    t = time.perf_counter() - t0
-    return {"value": nb / t, "unit": "query_embeddings/s", "cores": threads, "kind": "port",
-            "sample": f"{nb} (image, 128-token report) pairs: fp32 torch-CPU Swin-T + BERT-base + {a.model_type} "
-                      f"head(s) + numpy cosine/argsort top-{a.k} over {G.shape[0]}x{G.shape[1]} (oracle/towers.py, "
-                      f"oracle/knn.py), one timed run after warm-up, CPU: {cpu_model()}"}
+                (g, p), t = otw.backbones_forward(img, ii, mm, ssd, bsd, SWIN_T, BERT_BASE)
+                if a.model_type == "multimodal":
+                    q = otw.heads(g, p, t, hsd, "multimodal", mm_cfg={"num_heads": 8})["joint_emb"]
+                else:
+                    q = torch.cat([otw.heads(g, p, t, hsd, "image")["joint_emb"],
+                                   otw.heads(g, p, t, hsd, "text")["joint_emb"]])
+        res["q"] = q.numpy()
+        oknn.sklearn_topk(res["q"], G, a.k)
+    t = timed_median(run)
+    nq = nb * (2 if a.model_type == "both" else 1)
+    heads = {"multimodal": "multimodal head", "text": "text tower + text head", "image": "image tower + image head",
+             "both": "image and text heads"}[a.model_type]
+    return ({"value": nq / t, "unit": "query_embeddings/s", "cores": used, "cores_visible": os.cpu_count(),
+             "kind": "port",
+             "sample": f"{nb} of the bench's own inputs: fp32 torch-CPU towers + {heads} + numpy cosine/argsort "
+                       f"top-{a.k} over {G.shape[0]}x{G.shape[1]} (oracle/towers.py, oracle/knn.py), median of 5 "
+                       f"after one warm-up, {used} threads (usable CPUs of {os.cpu_count()} visible), "
+                       f"CPU: {cpu_model()}"}, res["q"])
+
+
+def recall_vs_cpu(index, q_gpu, emb_cpu, G, K):
+    """Recall@K of the GPU path against the reference CPU path on the same inputs: top-K of the GPU
+    (bf16-tower) embeddings through the GPU index vs top-K of the fp32 oracle embeddings through the
+    oracle's sklearn-path ranking (retrieval_overlap.py:84-90); recall = |GPU ∩ CPU| / K per query
+    (retrieval_eval.py:147-157 style overlap), plus the embedding cosine between the two paths."""
+    import numpy as np
+    from oracle import knn as oknn
+    gi, _ = index.search(q_gpu.contiguous(), K)
+    gi = gi.cpu().numpy() - index.idx_base
+    ci, _ = oknn.sklearn_topk(emb_cpu, G, K)
+    inter = [len(set(gi[r].tolist()) & set(ci[r].tolist())) / K for r in range(len(ci))]
+    qg = q_gpu.double().cpu().numpy()
+    cos = np.sum(qg * emb_cpu, 1) / (np.linalg.norm(qg, axis=1) * np.linalg.norm(emb_cpu, axis=1))
+    return {"recall_at_k": float(np.mean(inter)), "k": K, "queries": int(len(ci)),
+            "exact_list_match": float(np.mean([np.array_equal(gi[r], ci[r]) for r in range(len(ci))])),
+            "min_embedding_cosine": float(cos.min()),
+            "note": "GPU bf16 towers + GPU exact kNN vs fp32 oracle towers + sklearn-path kNN, same inputs"}
 
 
 if __name__ == "__main__":

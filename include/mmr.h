@@ -53,23 +53,27 @@ mmr_status mmr_index_create(const void* gallery, int64_t n, int32_t d, mmr_dtype
                             int gallery_is_host, int64_t idx_base, int device, mmr_index** out);
 mmr_status mmr_index_destroy(mmr_index* index);
 mmr_status mmr_index_info(const mmr_index* index, int64_t* n, int32_t* d, int64_t* idx_base);
-/* Pre-allocate the workspace for up to `max_q` queries so that later searches allocate nothing
- * (required before capturing a search into a HIP graph). */
+/* Pre-allocate the workspace for up to `max_q` queries in the CURRENT scan mode so that later
+ * searches allocate nothing (required before capturing a search into a HIP graph). */
 mmr_status mmr_index_reserve(mmr_index* index, int64_t max_q);
 
 /* Scan precision of the candidate pass (the ranking is always exact f64): 0 = f32 MFMA,
  * 1 = bf16 3-term split MFMA (default; ~5x the f32 rate at the same bytes; queries chunks of
  * <= 32 take the HBM-streaming f32 skinny scan), 2 = fp16 unit-row copy of the gallery (built on
- * the first switch to this mode: half the scan bytes, one fp16 MFMA per product; the wider
- * candidate margin can overflow the candidate buffer on heavily tied galleries -> status 1). */
+ * the first switch to this mode: half the scan bytes, one fp16 MFMA per product, a wider candidate
+ * margin — the same exact results). */
 mmr_status mmr_index_set_mode(mmr_index* index, int32_t mode);
 
 /* Exact cosine top-K of q (q, d) f32 device queries against the gallery.
  * Semantics: s(q,g) = <q,g> / (|q| |g|) in f64 (0 when either norm is 0 — sklearn's normalize()
  * leaves zero rows at 0), ranked by score descending, ties by lower gallery index.  Outputs
  * (q, k) int64 indices (+idx_base) and f32 scores; slots beyond n are (-1, -inf).
- * out_status (q,) int32 (may be NULL): 0 ok, 1 = candidate buffer overflow for that query.
- * Asynchronous on `stream`. */
+ * out_status (q,) int32 (may be NULL): per-query status, always 0 — more candidates inside the scan
+ * margin than the selection buffer holds (massive near-ties) are merged batch by batch inside the
+ * selection kernel, exactly, never truncated (a non-zero value would flag an inexact list).
+ * Asynchronous on `stream`.  Threading: calls on one index may come from several host threads and
+ * several streams; the index's workspace follows the stream (a search on a new stream first waits
+ * for the previous search's last use), so concurrent searches serialise on the device but never race. */
 mmr_status mmr_index_search(mmr_index* index, const float* q, int64_t nq, int32_t k,
                             int64_t* out_idx, float* out_score, double* out_score64,
                             int32_t* out_status, void* stream);

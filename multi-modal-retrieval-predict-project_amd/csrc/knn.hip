@@ -681,128 +681,20 @@ __device__ __forceinline__ float lower_threshold(float t, float two_delta) {
   return thr;
 }
 
-__global__ __launch_bounds__(kSelThreads) void knn_select(
-    const float* __restrict__ scores, int64_t ldS, int64_t n, int k, float two_delta,
-    const float* __restrict__ q_raw, int d, const double* __restrict__ qnorm64,
-    const float* __restrict__ gal, int Dp, const double* __restrict__ gnorm64, int64_t idx_base,
-    int64_t* __restrict__ out_idx, float* __restrict__ out_score, double* __restrict__ out_score64,
-    int32_t* __restrict__ status) {
-  __shared__ uint32_t tmax[kSelThreads];
-  __shared__ uint32_t hist[256];
-  __shared__ uint32_t bcast[4];
-  __shared__ int cand_i[kCandCap];
-  __shared__ double cand_d[kCandCap];
-
-  const int64_t qi = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const float* row = scores + qi * ldS;
-  const int kk = (int)(n < (int64_t)k ? n : (int64_t)k);
-  int64_t* oi = out_idx + qi * k;
-  float* os = out_score ? out_score + qi * k : nullptr;
-  double* os64 = out_score64 ? out_score64 + qi * k : nullptr;
-  for (int r = kk + tid; r < k; r += kSelThreads) {
-    oi[r] = -1;
-    if (os) os[r] = -INFINITY;
-    if (os64) os64[r] = -INFINITY;
-  }
-  if (kk <= 0) {
-    if (tid == 0 && status) status[qi] = 0;
-    return;
-  }
-
-  // (A) per-thread max over a strided slice (float4 body + scalar tail)
-  const int64_t n4 = n >> 2;
-  float m = -INFINITY;
-  for (int64_t i = tid; i < n4; i += kSelThreads) {
-    float4 v = ((const float4*)row)[i];
-    m = fmaxf(fmaxf(m, v.x), fmaxf(fmaxf(v.y, v.z), v.w));
-  }
-  for (int64_t i = (n4 << 2) + tid; i < n; i += kSelThreads) m = fmaxf(m, row[i]);
-  tmax[tid] = f2key(m);
-  if (tid == 0) bcast[2] = 0;
-  __syncthreads();
-  // (B) lower bound b of the K-th largest score
-  const float bnd = key2f(block_select_kth(tmax, kSelThreads, kk, hist, bcast));
-  float thr = lower_threshold(bnd, two_delta);
-  // (C) collect candidates
-  for (int64_t i = tid; i < n4; i += kSelThreads) {
-    float4 v = ((const float4*)row)[i];
-    const float vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (vv[e] >= thr) {
-        uint32_t p = atomicAdd(&bcast[2], 1u);
-        if (p < kCandCap) cand_i[p] = (int)(4 * i + e);
-      }
-  }
-  for (int64_t i = (n4 << 2) + tid; i < n; i += kSelThreads)
-    if (row[i] >= thr) {
-      uint32_t p = atomicAdd(&bcast[2], 1u);
-      if (p < kCandCap) cand_i[p] = (int)i;
-    }
-  __syncthreads();
-  int cnt = (int)bcast[2];
-  int st = 0;
-  if (cnt > kCandCap) {
-    // (D) fallback: exact K-th largest s32 over the whole row, then the tight threshold
-    __syncthreads();
-    const float t = key2f(row_select_kth(row, n, kk, hist, bcast));
-    thr = lower_threshold(t, two_delta);
-    if (tid == 0) bcast[2] = 0;
-    __syncthreads();
-    for (int64_t i = tid; i < n; i += kSelThreads)
-      if (row[i] >= thr) {
-        uint32_t p = atomicAdd(&bcast[2], 1u);
-        if (p < kCandCap) cand_i[p] = (int)i;
-      }
-    __syncthreads();
-    cnt = (int)bcast[2];
-    if (cnt > kCandCap) {
-      st = 1;
-      cnt = kCandCap;
-    }
-  }
-  // (E) f64 re-score from the raw rows
-  const float* qr = q_raw + qi * (int64_t)d;
-  const double qn = qnorm64[qi];
-  for (int c = wave; c < cnt; c += kSelThreads / 64) {
-    const int gi = cand_i[c];
-    const float* gr = gal + (int64_t)gi * Dp;
-    double acc = 0.0;
-    for (int kq = lane; kq < d; kq += 64) acc += (double)qr[kq] * (double)gr[kq];
-    acc = mmr::wave_sum(acc);
-    if (lane == 0) {
-      const double gn = gnorm64[gi];
-      cand_d[c] = (qn > 0.0 && gn > 0.0) ? acc / (qn * gn) : 0.0;
-    }
-  }
-  __syncthreads();
-  for (int c = tid; c < cnt; c += kSelThreads) {
-    const double sc = cand_d[c];
-    const int ic = cand_i[c];
-    int rank = 0;
-    for (int j2 = 0; j2 < cnt; ++j2) {
-      const double sj = cand_d[j2];
-      rank += (sj > sc) || (sj == sc && cand_i[j2] < ic);
-    }
-    if (rank < kk) {
-      oi[rank] = (int64_t)ic + idx_base;
-      if (os) os[rank] = (float)sc;
-      if (os64) os64[rank] = sc;
-    }
-  }
-  if (tid == 0 && status) status[qi] = st;
-}
-
-// Selection on row-group maxima (after knn_scores_x3_gmax): one 1024-thread workgroup per query.
-// (A) per-thread max over a strided slice of the query's group maxima; (B) b = K-th largest of
-// those (each is a distinct group's max, hence a distinct row's score: b <= the K-th largest
-// approximate score t); (C) collect every group whose max >= b - 2 delta — a true top-K row j has
-// s(j) >= t - 2 delta >= b - 2 delta, and its group's max >= s(j); (D) if more than kGrpCap groups
-// qualify, the exact K-th largest group max replaces b (same argument) and the set is rebuilt;
-// (E) every row of the collected groups is re-scored in f64 from the raw rows and (F) ranked by
-// (score desc, index asc).
-constexpr int kGrpCap = kCandCap / 4;
+// Per-query selection, one 1024-thread workgroup per query, over the scan's per-query value row.
+// Units (what one value covers): MODE 0 = one gallery row (f32-mode score matrix, knn_scores);
+// MODE 1 = a strided 4-row group {(u>>4)*64 + (u&15) + 16m : m < 4} (the gmax of knn_scores_x3_gmax /
+// knn_scan_f32_gmax / knn_scan_f16_gmax: one lane's 4 rows of a 64-row block); MODE 2 = 4 consecutive
+// rows {4u + m} (knn_scan_f16_tile).  A unit's value is >= the approximate score of each of its rows.
+// (A) per-thread max over a strided slice; (B) b = a lower bound of the K-th largest unit value (each
+// unit value is a distinct row's score, so b <= t, the K-th largest approximate row score); (C)
+// collect every unit with value >= b - 2 delta: a true top-K row j has s(j) >= t - 2 delta >= b - 2
+// delta, and its unit's value >= s(j); (D) more than kCandCap/GS units: the exact K-th largest unit
+// value replaces b (same argument) and the set is rebuilt; still more (massive near-ties): the units
+// are processed in position order, kCandCap/GS at a time, each batch re-scored and merged into a
+// carried exact top-K — slower, never inexact, so the status output is always 0; (E) every row of
+// the collected units is re-scored in f64 from the raw rows and (F) ranked by (score desc, index asc).
+constexpr int kSlotCap = kMaxK + kCandCap;  // [0, kMaxK): carried top-K; [kMaxK, +kCandCap): one batch
 
 // Phase clock of block 0 (tools/select_trace.hip builds this file with MMR_SELECT_TRACE; off in libmmr)
 #ifdef MMR_SELECT_TRACE
@@ -813,25 +705,41 @@ __device__ long long g_sel_trace[16];
 #define SEL_MARK(i)
 #endif
 
-__global__ __launch_bounds__(kSelThreads) void knn_select_groups(
-    const float* __restrict__ gmax, int64_t ldG, int64_t n, int k, float two_delta,
+template <int MODE>
+__device__ __forceinline__ int64_t unit_row(int64_t u, int m) {
+  if (MODE == 0) return u;
+  if (MODE == 1) return (u >> 4) * 64 + (u & 15) + 16 * m;
+  return 4 * u + m;
+}
+
+struct SelLds {
+  float qrow[kSelThreads];  // raw query row (d <= 1024), first member: 16-B aligned
+  uint32_t tmax[kSelThreads];
+  uint32_t hist[256];
+  uint32_t bcast[4];
+  int cand_u[kCandCap];
+  double cand_d[kSlotCap];
+  int rank_s[kSlotCap];
+  int row_s[kSlotCap];
+  double tmp_d[kMaxK];
+  int tmp_r[kMaxK];
+};
+
+template <int MODE>
+__global__ __launch_bounds__(kSelThreads) void knn_select_t(
+    const float* __restrict__ vals, int64_t ldV, int64_t nunits, int64_t n, int k, float two_delta,
     const float* __restrict__ q_raw, int d, const double* __restrict__ qnorm64,
     const float* __restrict__ gal, int Dp, const double* __restrict__ gnorm64, int64_t idx_base,
     int64_t* __restrict__ out_idx, float* __restrict__ out_score, double* __restrict__ out_score64,
     int32_t* __restrict__ status) {
-  __shared__ uint32_t tmax[kSelThreads];
-  __shared__ uint32_t hist[256];
-  __shared__ uint32_t bcast[4];
-  __shared__ int cand_g[kGrpCap];
-  __shared__ double cand_d[kCandCap];
-  __shared__ int rank_s[kCandCap];
-  __shared__ int row_s[kCandCap];
-  __shared__ __attribute__((aligned(16))) float qrow[kSelThreads];  // query row (d <= 1024)
+  constexpr int GS = MODE == 0 ? 1 : 4;      // rows per unit
+  constexpr int UC = kCandCap / GS;          // units per batch
+  __shared__ __attribute__((aligned(16))) SelLds L;
 
   SEL_MARK(0)
   const int64_t qi = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
-  const float* row = gmax + qi * ldG;
+  const float* row = vals + qi * ldV;
   const int kk = (int)(n < (int64_t)k ? n : (int64_t)k);
   int64_t* oi = out_idx + qi * k;
   float* os = out_score ? out_score + qi * k : nullptr;
@@ -841,18 +749,15 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_groups(
     if (os) os[r] = -INFINITY;
     if (os64) os64[r] = -INFINITY;
   }
-  if (kk <= 0) {
-    if (tid == 0 && status) status[qi] = 0;
-    return;
-  }
+  if (tid == 0 && status) status[qi] = 0;
+  if (kk <= 0) return;
   // the raw query row (f64 re-score, phase E) is staged in LDS first: its latency hides under
   // phases A-D and it holds no registers meanwhile
   const float* qr = q_raw + qi * (int64_t)d;
-  if (d <= 1024) qrow[tid] = tid < d ? qr[tid] : 0.f;
-  const int64_t ng = ldG;       // groups per query row (Np / 4, a multiple of 64)
-  const int64_t n4 = ng >> 2;
+  if (d <= 1024) L.qrow[tid] = tid < d ? qr[tid] : 0.f;
+  const int64_t n4 = nunits >> 2;
   // the first kRegF4 float4 of each thread's strided slice stay in registers for (C): one HBM/L2
-  // round trip for rows up to kRegF4 * 4 * 4 * 1024 = 131k gallery rows, all loads issued together
+  // round trip for rows up to kRegF4 * 4 * 1024 = 32k units, all loads issued together
   constexpr int kRegF4 = 8;
   float4 cache[kRegF4];
   float m = -INFINITY;
@@ -863,142 +768,176 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_groups(
   }
 #pragma unroll
   for (int it = 0; it < kRegF4; ++it)
-    m = fmaxf(fmaxf(m, cache[it].x), fmaxf(fmaxf(cache[it].y, cache[it].z), cache[it].w));
+    m = fmaxf(m, fmaxf(fmaxf(cache[it].x, cache[it].y), fmaxf(cache[it].z, cache[it].w)));
   for (int64_t i = tid + (int64_t)kRegF4 * kSelThreads; i < n4; i += kSelThreads) {
     const float4 v = ((const float4*)row)[i];
-    m = fmaxf(fmaxf(m, v.x), fmaxf(fmaxf(v.y, v.z), v.w));
+    m = fmaxf(m, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
   }
-  tmax[tid] = f2key(m);
-  if (tid == 0) bcast[2] = 0;
+  for (int64_t i = (n4 << 2) + tid; i < nunits; i += kSelThreads) m = fmaxf(m, row[i]);
+  L.tmax[tid] = f2key(m);
+  if (tid == 0) L.bcast[2] = 0;
   __syncthreads();
   SEL_MARK(1)
   // 16-bit prefix (sign, exponent, 7 mantissa bits: 2^-7 relative) of the K-th largest thread max,
   // clamped to -inf's key (smaller keys are NaN patterns)
-  uint32_t bkey = block_select_kth(tmax, kSelThreads, kk, hist, bcast, 2);
+  uint32_t bkey = block_select_kth(L.tmax, kSelThreads, kk, L.hist, L.bcast, 2);
   if (bkey < f2key(-INFINITY)) bkey = f2key(-INFINITY);
   float thr = lower_threshold(key2f(bkey), two_delta);
   SEL_MARK(2)
-#define MMR_TAKE(I, V, TH)                                                \
-  {                                                                       \
-    const float4 v_ = (V);                                                \
-    const float vv_[4] = {v_.x, v_.y, v_.z, v_.w};                        \
-    _Pragma("unroll") for (int e = 0; e < 4; ++e) if (vv_[e] >= (TH) && vv_[e] > -INFINITY) { \
-      const uint32_t p = atomicAdd(&bcast[2], 1u);                        \
-      if (p < kGrpCap) cand_g[p] = (int)(4 * (I) + e);                    \
-    }                                                                     \
-  }
-  auto collect = [&](float th, bool cached) {
+  auto take = [&](int64_t u, float v, float th) {
+    if (v >= th && v > -INFINITY) {
+      const uint32_t p = atomicAdd(&L.bcast[2], 1u);
+      if (p < (uint32_t)UC) L.cand_u[p] = (int)u;
+    }
+  };
+  // collect the units of [lo, hi) (float4-aligned lo) with value >= th into cand_u; returns the count
+  auto collect = [&](float th, bool cached, int64_t lo, int64_t hi) -> int {
+    const int64_t h4 = hi >> 2;
     if (cached) {
 #pragma unroll
-      for (int it = 0; it < kRegF4; ++it) MMR_TAKE(tid + (int64_t)it * kSelThreads, cache[it], th);
+      for (int it = 0; it < kRegF4; ++it) {
+        const int64_t i = tid + (int64_t)it * kSelThreads;
+        take(4 * i, cache[it].x, th);
+        take(4 * i + 1, cache[it].y, th);
+        take(4 * i + 2, cache[it].z, th);
+        take(4 * i + 3, cache[it].w, th);
+      }
     }
-    for (int64_t i = tid + (cached ? (int64_t)kRegF4 * kSelThreads : 0); i < n4; i += kSelThreads)
-      MMR_TAKE(i, ((const float4*)row)[i], th);
+    for (int64_t i = (lo >> 2) + tid + (cached ? (int64_t)kRegF4 * kSelThreads : 0); i < h4; i += kSelThreads) {
+      const float4 v = ((const float4*)row)[i];
+      take(4 * i, v.x, th);
+      take(4 * i + 1, v.y, th);
+      take(4 * i + 2, v.z, th);
+      take(4 * i + 3, v.w, th);
+    }
+    for (int64_t i = (h4 << 2 > lo ? h4 << 2 : lo) + tid; i < hi; i += kSelThreads) take(i, row[i], th);
     __syncthreads();
+    const int c = (int)L.bcast[2];
+    __syncthreads();
+    if (tid == 0) L.bcast[2] = 0;
+    __syncthreads();  // reset visible before any thread's next take()
+    return c;
   };
-  collect(thr, true);
-  SEL_MARK(3)
-  int cnt = (int)bcast[2];
-  int st = 0;
-  if (cnt > kGrpCap) {
-    __syncthreads();
-    const float t = key2f(row_select_kth(row, ng, kk, hist, bcast));
-    thr = lower_threshold(t, two_delta);
-    if (tid == 0) bcast[2] = 0;
-    __syncthreads();
-    collect(thr, false);
-    cnt = (int)bcast[2];
-    if (cnt > kGrpCap) {
-      st = 1;
-      cnt = kGrpCap;
-    }
-  }
-  // (E) f64 re-score of every row of the collected groups (slot s: group s/4, member s%4)
-  const int nslot = 4 * cnt;
   const double qn = qnorm64[qi];
-  auto slot_row = [&](int s) -> int64_t {
-    const int g = cand_g[s >> 2];
-    return (int64_t)(g >> 4) * 64 + (g & 15) + 16 * (s & 3);
+  // (E)+(F) for the cnt collected units: re-score their rows in f64 into slots [kMaxK, ...), rank
+  // them together with the `carry` carried rows [0, carry), keep the first kk in [0, kk); returns
+  // the number kept
+  auto process = [&](int cnt, int carry) -> int {
+    const int nslot = GS * cnt;
+    for (int s = tid; s < nslot; s += kSelThreads) {
+      const int64_t g = unit_row<MODE>(L.cand_u[s / GS], s % GS);
+      L.row_s[kMaxK + s] = (int)(g < n ? g : n);
+    }
+    __syncthreads();
+    if (d <= 1024) {
+      // latency-bound: each wave issues the float4 loads of RB rows before reducing any of them
+      // (RB = 3 spills at the 128-VGPR budget of 1024 threads); the query row from LDS
+      // (lane owns elements 4(64c + lane) .. +3)
+      constexpr int RB = 2;
+      for (int s0 = wave * RB; s0 < nslot; s0 += (kSelThreads / 64) * RB) {
+        float4 gv[RB][4];
+        double gnr[RB];  // row norms loaded with the rows (not after the reduction: one round trip)
+        int64_t gir[RB];
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const int s = s0 + r;
+          const int64_t gi = s < nslot ? L.row_s[kMaxK + s] : n;
+          gir[r] = gi;
+          gnr[r] = gi < n ? gnorm64[gi] : 0.0;
+          // one row pointer (padding slots read row 0; their score is discarded below)
+          const float* gr = gal + (gi < n ? gi : 0) * Dp + lane * 4;
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            gv[r][c] = (c * 256 + lane * 4 < Dp) ? *(const float4*)(gr + c * 256) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          double acc = 0.0;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float4 qv = *(const float4*)(L.qrow + (c * 64 + lane) * 4);
+            acc += (double)qv.x * gv[r][c].x + (double)qv.y * gv[r][c].y + (double)qv.z * gv[r][c].z +
+                   (double)qv.w * gv[r][c].w;
+          }
+          acc = mmr::wave_sum(acc);
+          const int s = s0 + r;
+          if (lane == 0 && s < nslot) {
+            const double gn = gnr[r];
+            L.cand_d[kMaxK + s] = gir[r] >= n ? -INFINITY : ((qn > 0.0 && gn > 0.0) ? acc / (qn * gn) : 0.0);
+          }
+        }
+      }
+    } else {
+      for (int s = wave; s < nslot; s += kSelThreads / 64) {
+        const int64_t gi = L.row_s[kMaxK + s];
+        double sc = -INFINITY;
+        if (gi < n) {
+          const float* gr = gal + gi * Dp;
+          double acc = 0.0;
+          for (int kq = lane; kq < d; kq += 64) acc += (double)qr[kq] * (double)gr[kq];
+          acc = mmr::wave_sum(acc);
+          const double gn = gnorm64[gi];
+          sc = (qn > 0.0 && gn > 0.0) ? acc / (qn * gn) : 0.0;
+        }
+        if (lane == 0) L.cand_d[kMaxK + s] = sc;
+      }
+    }
+    // (F) rank: the m^2 (slot, other) comparisons spread over all threads, ranks counted in LDS (a
+    // per-slot serial loop over the slots took ~5 us at 44 slots)
+    const int mtot = carry + nslot;
+    auto slot = [&](int u) { return u < carry ? u : kMaxK + u - carry; };
+    for (int u = tid; u < mtot; u += kSelThreads) L.rank_s[slot(u)] = 0;
+    __syncthreads();
+    const int npair = mtot * mtot;
+    for (int p = tid; p < npair; p += kSelThreads) {
+      const int a = slot(p / mtot), b = slot(p % mtot);
+      const double sa = L.cand_d[a], sb = L.cand_d[b];
+      if ((sb > sa) || (sb == sa && L.row_s[b] < L.row_s[a])) atomicAdd(&L.rank_s[a], 1);
+    }
+    __syncthreads();
+    for (int u = tid; u < mtot; u += kSelThreads) {
+      const int sl = slot(u);
+      const int rank = L.rank_s[sl];
+      if (L.cand_d[sl] == -INFINITY || rank >= kk) continue;
+      L.tmp_d[rank] = L.cand_d[sl];
+      L.tmp_r[rank] = L.row_s[sl];
+      atomicAdd(&L.bcast[3], 1u);
+    }
+    __syncthreads();
+    const int kept = (int)L.bcast[3];
+    for (int r = tid; r < kept; r += kSelThreads) {
+      L.cand_d[r] = L.tmp_d[r];
+      L.row_s[r] = L.tmp_r[r];
+    }
+    __syncthreads();
+    if (tid == 0) L.bcast[3] = 0;
+    return kept;
   };
-  if (d <= 1024) {
-    // latency-bound: each wave issues the float4 loads of RB rows before reducing any of them
-    // (RB = 3 spills at the 128-VGPR budget of 1024 threads); the query row from LDS
-    // (lane owns elements 4(64c + lane) .. +3)
-    constexpr int RB = 2;
-    for (int s0 = wave * RB; s0 < nslot; s0 += (kSelThreads / 64) * RB) {
-      float4 gv[RB][4];
-      double gnr[RB];  // row norms loaded with the rows (not after the reduction: one round trip)
-      int64_t gir[RB];
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        const int s = s0 + r;
-        const int64_t gi = s < nslot ? slot_row(s) : n;
-        gir[r] = gi;
-        gnr[r] = gi < n ? gnorm64[gi] : 0.0;
-        // one row pointer (padding slots read row 0; their score is discarded below)
-        const float* gr = gal + (gi < n ? gi : 0) * Dp + lane * 4;
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          gv[r][c] = (c * 256 + lane * 4 < Dp) ? *(const float4*)(gr + c * 256) : make_float4(0.f, 0.f, 0.f, 0.f);
+  if (tid == 0) L.bcast[3] = 0;
+  int cnt = collect(thr, true, 0, nunits);
+  SEL_MARK(3)
+  int kept = 0;
+  if (cnt > UC) {
+    const float t = key2f(row_select_kth(row, nunits, kk, L.hist, L.bcast));
+    thr = lower_threshold(t, two_delta);
+    cnt = collect(thr, false, 0, nunits);
+    if (cnt > UC) {
+      // massive near-ties: batches of UC units in position order (a batch cannot overflow), each
+      // merged into the carried exact top-K
+      for (int64_t lo = 0; lo < nunits; lo += UC) {
+        const int c = collect(thr, false, lo, lo + UC < nunits ? lo + UC : nunits);
+        if (c > 0) kept = process(c, kept);
       }
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        double acc = 0.0;
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-        {
-          const float4 qv = *(const float4*)(qrow + (c * 64 + lane) * 4);
-          acc += (double)qv.x * gv[r][c].x + (double)qv.y * gv[r][c].y + (double)qv.z * gv[r][c].z +
-                 (double)qv.w * gv[r][c].w;
-        }
-        acc = mmr::wave_sum(acc);
-        const int s = s0 + r;
-        if (lane == 0 && s < nslot) {
-          const double gn = gnr[r];
-          cand_d[s] = gir[r] >= n ? -INFINITY : ((qn > 0.0 && gn > 0.0) ? acc / (qn * gn) : 0.0);
-        }
-      }
-    }
-  } else {
-    for (int s = wave; s < nslot; s += kSelThreads / 64) {
-      const int64_t gi = slot_row(s);
-      double sc = -INFINITY;
-      if (gi < n) {
-        const float* gr = gal + gi * Dp;
-        double acc = 0.0;
-        for (int kq = lane; kq < d; kq += 64) acc += (double)qr[kq] * (double)gr[kq];
-        acc = mmr::wave_sum(acc);
-        const double gn = gnorm64[gi];
-        sc = (qn > 0.0 && gn > 0.0) ? acc / (qn * gn) : 0.0;
-      }
-      if (lane == 0) cand_d[s] = sc;
+      cnt = -1;
     }
   }
-  __syncthreads();
+  if (cnt >= 0) kept = process(cnt, 0);
   SEL_MARK(4)
-  // (F) rank among the valid slots: the nslot^2 (slot, other) comparisons spread over all threads,
-  // ranks counted in LDS (a per-slot serial loop over nslot LDS reads took ~5 us at 44 slots)
-  for (int s = tid; s < nslot; s += kSelThreads) {
-    rank_s[s] = 0;
-    row_s[s] = (int)slot_row(s);
+  for (int r = tid; r < kept; r += kSelThreads) {
+    oi[r] = (int64_t)L.row_s[r] + idx_base;
+    if (os) os[r] = (float)L.cand_d[r];
+    if (os64) os64[r] = L.cand_d[r];
   }
-  __syncthreads();
-  const int npair = nslot * nslot;
-  for (int p = tid; p < npair; p += kSelThreads) {
-    const int s = p / nslot, j2 = p - s * nslot;
-    const double sc = cand_d[s], sj = cand_d[j2];
-    if ((sj > sc) || (sj == sc && row_s[j2] < row_s[s])) atomicAdd(&rank_s[s], 1);
-  }
-  __syncthreads();
-  for (int s = tid; s < nslot; s += kSelThreads) {
-    const double sc = cand_d[s];
-    const int rank = rank_s[s];
-    if (sc == -INFINITY || rank >= kk) continue;
-    oi[rank] = (int64_t)row_s[s] + idx_base;
-    if (os) os[rank] = (float)sc;
-    if (os64) os64[rank] = sc;
-  }
-  if (tid == 0 && status) status[qi] = st;
   SEL_MARK(5)
 #ifdef MMR_SELECT_TRACE
   if (blockIdx.x == 0 && threadIdx.x == 0) g_sel_trace[6] = cnt;
@@ -1183,39 +1122,70 @@ struct mmr_index {
   float* gt = nullptr;        // [Np][Dp] f32 in the tile16 layout (skinny scan)
   uint16_t* gh = nullptr;     // [Np][Dp] fp16 unit rows in the tile32h layout (mode f16; built on first use)
   int mode = 1;               // 0: f32 MFMA scores, 1: bf16x3 split scores, 2: fp16 unit-row scan
-  // workspace (single; guarded by mu — searches on one index serialise their enqueue)
+  // Workspace: one set per index, sized by what the mode needs (grown on demand).  `mu` serialises
+  // the enqueue of searches; across streams the workspace follows the stream: a search records
+  // ws_event after its last use, and a search on another stream first waits for that event, so two
+  // streams never race on it (and a realloc waits for the last user).
   std::mutex mu;
-  int64_t ws_q = 0;  // queries the workspace holds
-  float* qn = nullptr;
-  double* qnorm64 = nullptr;
-  float* scores = nullptr;
-  uint16_t* qs = nullptr;  // [ws_q][3Dp]
+  int64_t ws_qrows = 0;       // query rows in qn / qnorm64
+  int64_t ws_vals = 0;        // floats in vals
+  int64_t ws_qsrows = 0;      // query rows in qs
+  float* qn = nullptr;        // [rows][Dp] f32 (or fp16 / tile layouts, same bytes or fewer)
+  double* qnorm64 = nullptr;  // [rows]
+  float* vals = nullptr;      // scores (f32 mode) or per-(query, unit) maxima
+  uint16_t* qs = nullptr;     // [rows][3Dp] bf16 split queries (x3 GEMM)
+  hipEvent_t ws_event = nullptr;
+  hipStream_t ws_stream = nullptr;
+  bool ws_used = false;
 };
 
 namespace {
 
-constexpr int64_t kScoresBudget = int64_t(4) << 30;  // bytes of score workspace per chunk
+constexpr int64_t kScoresBudget = int64_t(4) << 30;  // bytes of value workspace per query chunk
 
+// Queries per chunk: bounded by the value workspace (f32 mode: Np floats per query; x3: Np / 4).
+// The f16 scan runs passes of <= 256 queries whatever the chunk.
 int64_t chunk_queries(const mmr_index* ix) {
-  int64_t per = ix->Np * (int64_t)sizeof(float);
+  const int64_t per = (ix->mode == 0 ? ix->Np : ix->Np / 4) * (int64_t)sizeof(float);
   int64_t c = kScoresBudget / per;
   c = c / 256 * 256;
   return c < 256 ? 256 : c;
 }
 
+template <class T>
+mmr_status grow(mmr_index* ix, T*& buf, int64_t& have, int64_t want, size_t elem_bytes) {
+  if (want <= have) return MMR_OK;
+  if (buf) {
+    if (ix->ws_used) (void)hipEventSynchronize(ix->ws_event);  // the last search has released it
+    (void)hipFree(buf);
+  }
+  buf = nullptr;
+  have = 0;
+  MMR_CHECK_HIP(hipMalloc((void**)&buf, elem_bytes * want));
+  have = want;
+  return MMR_OK;
+}
+
+// Workspace for a search of nq queries in the current mode (rows rounded to 256).
 mmr_status ensure_ws(mmr_index* ix, int64_t nq) {
-  int64_t want = round_up(nq < chunk_queries(ix) ? nq : chunk_queries(ix), 256);
-  if (want <= ix->ws_q) return MMR_OK;
-  if (ix->qn) (void)hipFree(ix->qn);
-  if (ix->qnorm64) (void)hipFree(ix->qnorm64);
-  if (ix->scores) (void)hipFree(ix->scores);
-  if (ix->qs) (void)hipFree(ix->qs);
-  ix->qn = nullptr; ix->qnorm64 = nullptr; ix->scores = nullptr; ix->qs = nullptr; ix->ws_q = 0;
-  MMR_CHECK_HIP(hipMalloc(&ix->qn, sizeof(float) * want * ix->Dp));
-  MMR_CHECK_HIP(hipMalloc(&ix->qs, sizeof(uint16_t) * want * 3 * ix->Dp));
-  MMR_CHECK_HIP(hipMalloc(&ix->qnorm64, sizeof(double) * want));
-  MMR_CHECK_HIP(hipMalloc(&ix->scores, sizeof(float) * want * ix->Np));
-  ix->ws_q = want;
+  const int64_t cq = round_up(nq < chunk_queries(ix) ? nq : chunk_queries(ix), 256);
+  int64_t rows = cq, vals = 0, qs = 0;
+  if (ix->mode == 0) {
+    vals = cq * ix->Np;
+  } else if (ix->mode == 1) {
+    vals = cq * (ix->Np / 4);
+    qs = cq;
+  } else {
+    rows = 256;
+    vals = 256 * (ix->Np / 4);
+  }
+  int64_t hq = ix->ws_qrows, hq2 = ix->ws_qrows;
+  mmr_status s = grow(ix, ix->qn, hq, rows, sizeof(float) * ix->Dp);
+  if (s == MMR_OK) s = grow(ix, ix->qnorm64, hq2, rows, sizeof(double));
+  if (s != MMR_OK) return s;
+  ix->ws_qrows = hq < hq2 ? hq : hq2;
+  if ((s = grow(ix, ix->vals, ix->ws_vals, vals, sizeof(float))) != MMR_OK) return s;
+  if (qs > 0 && (s = grow(ix, ix->qs, ix->ws_qsrows, qs, sizeof(uint16_t) * 3 * ix->Dp)) != MMR_OK) return s;
   return MMR_OK;
 }
 
@@ -1241,6 +1211,15 @@ struct DeviceGuard {
     if (prev >= 0) (void)hipSetDevice(prev);
   }
 };
+
+template <int MODE>
+void launch_select(hipStream_t st, int64_t nq, const float* vals, int64_t ldV, int64_t nunits, const mmr_index* ix,
+                   int k, float two_delta, const float* q_raw, const double* qnorm64, int64_t* oi, float* os,
+                   double* os64, int32_t* ost) {
+  knn_select_t<MODE><<<dim3((unsigned)nq), dim3(kSelThreads), 0, st>>>(
+      vals, ldV, nunits, ix->n, k, two_delta, q_raw, ix->d, qnorm64, ix->gal, ix->Dp, ix->norm64, ix->idx_base,
+      oi, os, os64, ost);
+}
 
 }  // namespace
 
@@ -1273,6 +1252,11 @@ mmr_status mmr_index_create(const void* gallery, int64_t n, int32_t d, mmr_dtype
     return s;
   };
   hipError_t e;
+  if ((e = hipEventCreateWithFlags(&ix->ws_event, hipEventDisableTiming)) != hipSuccess) {
+    ix->ws_event = nullptr;
+    mmr::set_error("mmr_index_create: hipEventCreate failed: %s", hipGetErrorString(e));
+    return fail(MMR_ERR_HIP);
+  }
   if ((e = hipMalloc(&ix->gal, sizeof(float) * ix->Np * ix->Dp)) != hipSuccess ||
       (e = hipMalloc(&ix->inv_norm, sizeof(float) * ix->Np)) != hipSuccess ||
       (e = hipMalloc(&ix->norm64, sizeof(double) * ix->Np)) != hipSuccess ||
@@ -1331,7 +1315,8 @@ mmr_status mmr_index_destroy(mmr_index* ix) {
   if (ix->qs) (void)hipFree(ix->qs);
   if (ix->qn) (void)hipFree(ix->qn);
   if (ix->qnorm64) (void)hipFree(ix->qnorm64);
-  if (ix->scores) (void)hipFree(ix->scores);
+  if (ix->vals) (void)hipFree(ix->vals);
+  if (ix->ws_event) (void)hipEventDestroy(ix->ws_event);
   delete ix;
   return MMR_OK;
 }
@@ -1364,87 +1349,86 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
   MMR_REQUIRE(q != nullptr && out_idx != nullptr, "mmr_index_search: NULL query/output");
   DeviceGuard g(ix->device);
   std::lock_guard<std::mutex> lk(ix->mu);
+  hipStream_t st = mmr::as_stream(stream);
+  // the workspace follows the stream: wait for the previous search if it ran on another stream
+  if (ix->ws_used && ix->ws_stream != st) MMR_CHECK_HIP(hipStreamWaitEvent(st, ix->ws_event, 0));
   mmr_status s = ensure_ws(ix, nq);
   if (s != MMR_OK) return s;
-  hipStream_t st = mmr::as_stream(stream);
-  // |s_approx - s64| <= delta; threshold margin 2*delta
-  const float two_delta =
-      ix->mode == 0 ? 2.0f * (float)(ix->Dp + 16) * 5.9604645e-8f
-                    : 2.0f * ((float)(3 * ix->Dp + 16) * 5.9604645e-8f + 4.0f * 1.5258789e-5f);
-  const int64_t chunk = ix->ws_q;
+  // |s_approx - s64| <= delta; threshold margin 2*delta.
+  //  f32 (knn_scores, knn_scan_f32_gmax): (Dp + 16) 2^-24 — f32 products accumulated in f32 over Dp
+  //      terms of a unit query against g/|g| (|sum| <= 1), plus the normalisations;
+  //  x3: + the dropped lo*lo bf16 terms and the bf16 rounding of the split, (3Dp + 16) 2^-24 + 4 2^-16;
+  //  f16: fp16 rounding of both unit vectors, 2 * 2^-11 relative with sum |q_k g_k| <= 1
+  //      (Cauchy-Schwarz) -> 2^-10; fp16 subnormal half-ulps (components below 2^-14 are held to
+  //      2^-25 absolute): sum_k (|q_k| + |g_k|) 2^-25 <= 2 sqrt(Dp) 2^-25 (Cauchy-Schwarz again),
+  //      computed from Dp below; f32 accumulation (Dp terms) and the f32 normalisation of both
+  //      operands (the f32-mode bound, doubled: (2Dp + 64) 2^-24).
+  const float two_delta32 = 2.0f * (float)(ix->Dp + 16) * 5.9604645e-8f;
+  const float two_delta3 = 2.0f * ((float)(3 * ix->Dp + 16) * 5.9604645e-8f + 4.0f * 1.5258789e-5f);
+  const float two_delta16 = 2.0f * (9.765625e-4f + 2.0f * sqrtf((float)ix->Dp) * 2.9802322e-8f +
+                                    (float)(2 * ix->Dp + 64) * 5.9604645e-8f);
+  const int64_t chunk = chunk_queries(ix);
   for (int64_t c0 = 0; c0 < nq; c0 += chunk) {
     const int64_t cq = nq - c0 < chunk ? nq - c0 : chunk;
     const float* qc = q + c0 * ix->d;
-    int64_t Qp;
+    int64_t* oi = out_idx + c0 * k;
+    float* os = out_score ? out_score + c0 * k : nullptr;
+    double* os64 = out_score64 ? out_score64 + c0 * k : nullptr;
+    int32_t* ost = out_status ? out_status + c0 : nullptr;
     if (ix->mode == 2) {
-      // fp16 scan, passes of <= 256 queries (16 * QT, QT a power of two).  delta_f16 bounds
-      // |s_f16 - s64|: fp16 rounding of both unit vectors (2 * 2^-11 relative, Cauchy-Schwarz over
-      // sum |q_k g_k| <= 1) + fp16 subnormal half-ulps (2 * 2^-25 * sqrt(Dp)) + f32 accumulation and
-      // the f32 normalisation of both operands (the f32-mode (Dp + 16) 2^-24), rounded up.
-      const float two_delta16 =
-          2.0f * (9.765625e-4f + 9.5367432e-7f + (float)(2 * ix->Dp + 64) * 5.9604645e-8f);
+      // fp16 scan, passes of <= 256 queries (16 * QT, QT a power of two)
       for (int64_t p0 = 0; p0 < cq; p0 += 256) {
         const int64_t pq = cq - p0 < 256 ? cq - p0 : 256;
         int qt = 1;
         while (16 * qt < pq) qt *= 2;
-        Qp = 16 * qt;
+        const int64_t Qp = 16 * qt;
         const float* qp = qc + p0 * ix->d;
         knn_prep_queries<<<dim3((unsigned)ceil_div(Qp, 4)), dim3(256), 0, st>>>(
             qp, pq, ix->d, ix->qn, ix->Dp, Qp, ix->qnorm64, 2);
         MMR_LAUNCH_CHECK();
         const dim3 grid((unsigned)(ix->Np / 64));
         const uint16_t* qh = (const uint16_t*)ix->qn;
+        float* gm = ix->vals;
+        const int64_t ldG = ix->Np / 4;
         switch (qt) {
           // KC must divide Dp (a multiple of 64): the 128-wide chunk only when Dp % 128 == 0
           case 1:
-            if (ix->Dp % 128 == 0)
-              knn_scan_f16_gmax<1, 128><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n);
-            else
-              knn_scan_f16_gmax<1, 64><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n);
+            if (ix->Dp % 128 == 0) knn_scan_f16_gmax<1, 128><<<grid, 64, 0, st>>>(qh, ix->gh, gm, ix->Dp, ldG, ix->n);
+            else knn_scan_f16_gmax<1, 64><<<grid, 64, 0, st>>>(qh, ix->gh, gm, ix->Dp, ldG, ix->n);
             break;
           case 2:
-            if (ix->Dp % 128 == 0)
-              knn_scan_f16_gmax<2, 128><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n);
-            else
-              knn_scan_f16_gmax<2, 64><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n);
+            if (ix->Dp % 128 == 0) knn_scan_f16_gmax<2, 128><<<grid, 64, 0, st>>>(qh, ix->gh, gm, ix->Dp, ldG, ix->n);
+            else knn_scan_f16_gmax<2, 64><<<grid, 64, 0, st>>>(qh, ix->gh, gm, ix->Dp, ldG, ix->n);
             break;
-          case 4: knn_scan_f16_gmax<4, 64><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n); break;
-          case 8: knn_scan_f16_gmax<8, 64><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n); break;
-          default: knn_scan_f16_gmax<16, 32><<<grid, 64, 0, st>>>(qh, ix->gh, ix->scores, ix->Dp, ix->Np / 4, ix->n); break;
+          case 4: knn_scan_f16_gmax<4, 64><<<grid, 64, 0, st>>>(qh, ix->gh, gm, ix->Dp, ldG, ix->n); break;
+          case 8: knn_scan_f16_gmax<8, 64><<<grid, 64, 0, st>>>(qh, ix->gh, gm, ix->Dp, ldG, ix->n); break;
+          default: knn_scan_f16_gmax<16, 32><<<grid, 64, 0, st>>>(qh, ix->gh, gm, ix->Dp, ldG, ix->n); break;
         }
         MMR_LAUNCH_CHECK();
-        const int64_t o = c0 + p0;
-        knn_select_groups<<<dim3((unsigned)pq), dim3(kSelThreads), 0, st>>>(
-            ix->scores, ix->Np / 4, ix->n, k, two_delta16, qp, ix->d, ix->qnorm64, ix->gal, ix->Dp,
-            ix->norm64, ix->idx_base, out_idx + o * k, out_score ? out_score + o * k : nullptr,
-            out_score64 ? out_score64 + o * k : nullptr, out_status ? out_status + o : nullptr);
+        launch_select<1>(st, pq, gm, ldG, ldG, ix, k, two_delta16, qp, ix->qnorm64, oi + p0 * k,
+                         os ? os + p0 * k : nullptr, os64 ? os64 + p0 * k : nullptr, ost ? ost + p0 : nullptr);
         MMR_LAUNCH_CHECK();
       }
-      continue;
     } else if (ix->mode == 1 && cq <= skinny_max_q()) {
       // skinny scan: HBM-streaming f32 MFMA, f32-mode delta
       const int qt = cq <= 16 ? 1 : cq <= 32 ? 2 : 4;
-      Qp = 16 * qt;
+      const int64_t Qp = 16 * qt;
       knn_prep_queries<<<dim3((unsigned)ceil_div(Qp, 4)), dim3(256), 0, st>>>(
           qc, cq, ix->d, ix->qn, ix->Dp, Qp, ix->qnorm64, 1);
       MMR_LAUNCH_CHECK();
       const dim3 grid((unsigned)(ix->Np / 64));
+      const int64_t ldG = ix->Np / 4;
       if (qt == 1)
-        knn_scan_f32_gmax<1, 64><<<grid, 64, 0, st>>>(ix->qn, ix->gt, ix->inv_norm, ix->scores, ix->Dp, ix->Np / 4, ix->n);
+        knn_scan_f32_gmax<1, 64><<<grid, 64, 0, st>>>(ix->qn, ix->gt, ix->inv_norm, ix->vals, ix->Dp, ldG, ix->n);
       else if (qt == 2)
-        knn_scan_f32_gmax<2, 64><<<grid, 64, 0, st>>>(ix->qn, ix->gt, ix->inv_norm, ix->scores, ix->Dp, ix->Np / 4, ix->n);
+        knn_scan_f32_gmax<2, 64><<<grid, 64, 0, st>>>(ix->qn, ix->gt, ix->inv_norm, ix->vals, ix->Dp, ldG, ix->n);
       else
-        knn_scan_f32_gmax<4, 32><<<grid, 64, 0, st>>>(ix->qn, ix->gt, ix->inv_norm, ix->scores, ix->Dp, ix->Np / 4, ix->n);
+        knn_scan_f32_gmax<4, 32><<<grid, 64, 0, st>>>(ix->qn, ix->gt, ix->inv_norm, ix->vals, ix->Dp, ldG, ix->n);
       MMR_LAUNCH_CHECK();
-      const float two_delta32 = 2.0f * (float)(ix->Dp + 16) * 5.9604645e-8f;
-      knn_select_groups<<<dim3((unsigned)cq), dim3(kSelThreads), 0, st>>>(
-          ix->scores, ix->Np / 4, ix->n, k, two_delta32, qc, ix->d, ix->qnorm64, ix->gal, ix->Dp,
-          ix->norm64, ix->idx_base, out_idx + c0 * k, out_score ? out_score + c0 * k : nullptr,
-          out_score64 ? out_score64 + c0 * k : nullptr, out_status ? out_status + c0 : nullptr);
+      launch_select<1>(st, cq, ix->vals, ldG, ldG, ix, k, two_delta32, qc, ix->qnorm64, oi, os, os64, ost);
       MMR_LAUNCH_CHECK();
-      continue;
     } else if (ix->mode == 1) {
-      Qp = round_up(cq, 128);
+      const int64_t Qp = round_up(cq, 128);
       knn_prep_queries<<<dim3((unsigned)ceil_div(Qp, 4)), dim3(256), 0, st>>>(
           qc, cq, ix->d, ix->qn, ix->Dp, Qp, ix->qnorm64);
       MMR_LAUNCH_CHECK();
@@ -1452,19 +1436,16 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
       knn_split_queries<<<dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, st>>>(ix->qn, ix->Dp, total, ix->qs);
       MMR_LAUNCH_CHECK();
       const int tiles_m = (int)(Qp / 128), tiles_n = (int)(ix->Np / 128);
+      const int64_t ldG = ix->Np / 4;
       knn_scores_x3_gmax<<<dim3((unsigned)(tiles_m * tiles_n)), dim3(256), 0, st>>>(
-          ix->qs, ix->gs, ix->inv_norm, ix->scores, ix->Dp, ix->Np / 4, ix->n, tiles_m, tiles_n);
+          ix->qs, ix->gs, ix->inv_norm, ix->vals, ix->Dp, ldG, ix->n, tiles_m, tiles_n);
       MMR_LAUNCH_CHECK();
-      knn_select_groups<<<dim3((unsigned)cq), dim3(kSelThreads), 0, st>>>(
-          ix->scores, ix->Np / 4, ix->n, k, two_delta, qc, ix->d, ix->qnorm64, ix->gal, ix->Dp,
-          ix->norm64, ix->idx_base, out_idx + c0 * k, out_score ? out_score + c0 * k : nullptr,
-          out_score64 ? out_score64 + c0 * k : nullptr, out_status ? out_status + c0 : nullptr);
+      launch_select<1>(st, cq, ix->vals, ldG, ldG, ix, k, two_delta3, qc, ix->qnorm64, oi, os, os64, ost);
       MMR_LAUNCH_CHECK();
-      continue;
     } else {
       int wq, wn;
       if (cq <= 64) { wq = 1; wn = 4; } else if (cq <= 128) { wq = 2; wn = 2; } else { wq = 4; wn = 1; }
-      Qp = round_up(cq, 64 * wq);
+      const int64_t Qp = round_up(cq, 64 * wq);
       knn_prep_queries<<<dim3((unsigned)ceil_div(Qp, 4)), dim3(256), 0, st>>>(
           qc, cq, ix->d, ix->qn, ix->Dp, Qp, ix->qnorm64);
       MMR_LAUNCH_CHECK();
@@ -1472,22 +1453,19 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
       const int n_gtiles = (int)ceil_div(ix->Np, 64 * wn);
       const unsigned grid = (unsigned)(round_up(n_gtiles, 8) * n_qblocks);
       if (wq == 1)
-        knn_scores<1, 4><<<grid, 256, 0, st>>>(ix->qn, ix->gal, ix->inv_norm, ix->scores, ix->Dp,
-                                                ix->Np, n_gtiles, n_qblocks);
+        knn_scores<1, 4><<<grid, 256, 0, st>>>(ix->qn, ix->gal, ix->inv_norm, ix->vals, ix->Dp, ix->Np, n_gtiles, n_qblocks);
       else if (wq == 2)
-        knn_scores<2, 2><<<grid, 256, 0, st>>>(ix->qn, ix->gal, ix->inv_norm, ix->scores, ix->Dp,
-                                                ix->Np, n_gtiles, n_qblocks);
+        knn_scores<2, 2><<<grid, 256, 0, st>>>(ix->qn, ix->gal, ix->inv_norm, ix->vals, ix->Dp, ix->Np, n_gtiles, n_qblocks);
       else
-        knn_scores<4, 1><<<grid, 256, 0, st>>>(ix->qn, ix->gal, ix->inv_norm, ix->scores, ix->Dp,
-                                                ix->Np, n_gtiles, n_qblocks);
+        knn_scores<4, 1><<<grid, 256, 0, st>>>(ix->qn, ix->gal, ix->inv_norm, ix->vals, ix->Dp, ix->Np, n_gtiles, n_qblocks);
+      MMR_LAUNCH_CHECK();
+      launch_select<0>(st, cq, ix->vals, ix->Np, ix->n, ix, k, two_delta32, qc, ix->qnorm64, oi, os, os64, ost);
       MMR_LAUNCH_CHECK();
     }
-    knn_select<<<dim3((unsigned)cq), dim3(kSelThreads), 0, st>>>(
-        ix->scores, ix->Np, ix->n, k, two_delta, qc, ix->d, ix->qnorm64, ix->gal, ix->Dp,
-        ix->norm64, ix->idx_base, out_idx + c0 * k, out_score ? out_score + c0 * k : nullptr,
-        out_score64 ? out_score64 + c0 * k : nullptr, out_status ? out_status + c0 : nullptr);
-    MMR_LAUNCH_CHECK();
   }
+  MMR_CHECK_HIP(hipEventRecord(ix->ws_event, st));
+  ix->ws_stream = st;
+  ix->ws_used = true;
   return MMR_OK;
 }
 

@@ -150,9 +150,18 @@ class MultiModalRetrievalModel:
     __call__ = forward
 
     def query_embeddings(self, image, input_ids, attention_mask):
-        """Retrieval keys of one (image, report) batch.  multimodal: (B, D) f32 joint embeddings;
-        image / text: both single-modality heads, (2B, D) = [image-head; text-head] joint embeddings."""
+        """Retrieval keys of one batch.  multimodal: (B, D) f32 joint embeddings of (image, report)
+        pairs; image / text with both inputs: both single-modality heads, (2B, D) = [image-head;
+        text-head]; text with image=None: the text tower + text head only, (B, D) (BASELINE cfg3:
+        text-only ClinicalBERT queries, model.py:472-479); image with input_ids=None: the image
+        tower + image head only (model.py:462-469)."""
         mm = self.model_type == "multimodal"
+        if not mm and image is None:
+            txt = self.backbones.encode_text(input_ids, attention_mask)
+            return self._head(self._txt_pool(txt), self.txt_proj)
+        if not mm and input_ids is None:
+            _, _, pool = self.backbones.encode_image(image, want_patches=False)
+            return self._head(pool, self.img_proj)
         (g, p, pool), txt = self._towers(image, input_ids, attention_mask, mm)
         if mm:
             return self.fusion.forward(g, p, txt)

@@ -14,7 +14,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from .retrieval import GalleryIndex, RetrievalEngine, merge_topk
+from .retrieval import GalleryIndex, RetrievalEngine, check_status, merge_topk
 
 
 def shard_bounds(n, world):
@@ -51,30 +51,68 @@ def merge_topk_host(scores64, idx, k_out):
 
 
 class ShardedIndex:
-    """This rank's gallery shard + the collective search.  `local_search(q, k) -> (idx, f64)`
-    may be injected (tests); by default it is the rank's GPU GalleryIndex."""
+    """This rank's gallery shard + the collective search.
 
-    def __init__(self, gallery_rows, n_total, start, group=None, device=None, local_search=None):
+    `local_search(q, k) -> (idx, f64) or (idx, f64, status)` may be injected (tests); by default it
+    is the rank's GPU GalleryIndex in `mode` ("x3" | "f16" | "f32").  A non-zero per-query status
+    (candidate-buffer overflow — the library now resolves it in-kernel, so this is a guard) makes
+    those queries re-run through `fallback_search` (default: the same index in "x3", as
+    MI355XRetrievalEngine did) before the lists are exchanged, so every rank always contributes an
+    exact list."""
+
+    def __init__(self, gallery_rows, n_total, start, group=None, device=None, local_search=None, mode="x3",
+                 fallback_search=None):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.n_total, self.start = int(n_total), int(start)
         self.index = None
         if local_search is None:
-            self.index = GalleryIndex(gallery_rows, device=device, idx_base=start)
-
-            def local_search(q, k):
-                i, _, s64 = self.index.search(q, k, want_f64=True)
-                return i, s64
+            self.index = GalleryIndex(gallery_rows, device=device, idx_base=start, mode=mode)
+            local_search = self._index_search
+            if fallback_search is None:
+                fallback_search = self._index_search_x3
         self.local_search = local_search
+        self.fallback_search = fallback_search
+        self.reruns = 0  # queries re-run through fallback_search (diagnostic)
+
+    def _index_search(self, q, k):
+        i, _, s64, st = self.index.search(q, k, want_f64=True, want_status=True)
+        return i, s64, st
+
+    def _index_search_x3(self, q, k):
+        mode = self.index.mode
+        self.index.set_mode("x3")
+        try:
+            i, _, s64, st = self.index.search(q, k, want_f64=True, want_status=True)
+        finally:
+            self.index.set_mode(mode)
+        check_status(st)
+        return i, s64
 
     @classmethod
-    def from_full(cls, gallery, group=None, device=None, local_search=None):
+    def from_full(cls, gallery, group=None, device=None, local_search=None, mode="x3", fallback_search=None):
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
         s, e = shard_bounds(len(gallery), world)[rank]
         rows = gallery[s:e]
-        return cls(rows, len(gallery), s, group=group, device=device, local_search=local_search)
+        return cls(rows, len(gallery), s, group=group, device=device, local_search=local_search, mode=mode,
+                   fallback_search=fallback_search)
+
+    def _local(self, q, k):
+        out = self.local_search(q, k)
+        i, s64 = out[0], out[1]
+        st = out[2] if len(out) > 2 else None
+        if st is not None and st.numel() and int(st.max().item()) != 0:
+            if self.fallback_search is None:
+                check_status(st)
+            bad = torch.nonzero(st != 0).flatten()
+            i2, s2 = self.fallback_search(q[bad.to(q.device)].contiguous(), k)
+            i, s64 = i.clone(), s64.clone()
+            i[bad.to(i.device)] = i2.to(i.device, i.dtype)
+            s64[bad.to(s64.device)] = s2.to(s64.device, s64.dtype)
+            self.reruns += int(bad.numel())
+        return i, s64
 
     def search(self, q_local, k):
         """Collective: every rank passes its own (b, D) queries (same b on every rank); returns
@@ -83,7 +121,7 @@ class ShardedIndex:
         allq = torch.empty((self.world * b,) + tuple(q_local.shape[1:]), dtype=q_local.dtype,
                            device=q_local.device)
         dist.all_gather_into_tensor(allq, q_local.contiguous(), group=self.group)
-        i, s64 = self.local_search(allq, k)
+        i, s64 = self._local(allq, k)
         gi = torch.empty((self.world * i.shape[0], i.shape[1]), dtype=i.dtype, device=i.device)
         gs = torch.empty((self.world * s64.shape[0], s64.shape[1]), dtype=s64.dtype, device=s64.device)
         dist.all_gather_into_tensor(gi, i.contiguous(), group=self.group)
@@ -100,15 +138,18 @@ class ShardedIndex:
 
 class ShardedRetrievalEngine(RetrievalEngine):
     """make_retrieval_engine(method="mi355x_sharded"): every rank mmaps the .npy, keeps its row
-    shard on its GPU; retrieve()/search() are collective calls (all ranks, same batch size)."""
+    shard on its GPU; retrieve()/search() are collective calls (all ranks, same batch size).
+    dtype "fp32" scans the bf16x3 split copy, "fp16" the fp16 unit-row copy (BASELINE cfg5's fp16
+    gallery); both rank exactly (f64 re-score from the f32 rows), so results are identical."""
 
     def __init__(self, features_path=None, ids_path=None, dtype="fp32", embs=None, ids=None, group=None):
         if embs is None:
             embs = np.load(features_path, mmap_mode="r")
         super().__init__(features_path, ids_path, embs=embs, ids=ids)
-        if dtype != "fp32":
-            raise ValueError(f"gallery dtype {dtype!r} not built in this round (fp32 only)")
-        self.sharded = ShardedIndex.from_full(self.embs, group=group, device=torch.cuda.current_device())
+        if dtype not in ("fp32", "fp16"):
+            raise ValueError(f"gallery dtype {dtype!r} (fp32 | fp16)")
+        self.sharded = ShardedIndex.from_full(self.embs, group=group, device=torch.cuda.current_device(),
+                                              mode="f16" if dtype == "fp16" else "x3")
 
     def search(self, Q, K=10):
         is_np = not isinstance(Q, torch.Tensor)

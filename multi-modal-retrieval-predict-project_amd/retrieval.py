@@ -52,9 +52,10 @@ class GalleryIndex:
 
     Scan modes (all exact: candidates re-scored in f64 from the f32 rows): "x3" bf16 3-term split
     GEMM (default; Q <= 32 use the skinny f32 stream), "f32" f32 MFMA, "f16" fp16 unit-row copy of
-    the gallery (half the scan bytes; wider candidate margin, so heavily tied galleries can overflow
-    the candidate buffer — status 1, which MI355XRetrievalEngine answers by re-running those queries
-    in "x3")."""
+    the gallery (half the scan bytes, wider candidate margin).  Heavily tied galleries (more
+    candidates within the margin than the selection buffer holds) are handled inside the selection
+    kernel by batched exact merging, so the per-query status is always 0 (checked by callers that
+    ask for it)."""
 
     MODES = {"f32": 0, "x3": 1, "f16": 2}
 
@@ -164,6 +165,14 @@ class GalleryIndex:
             pass
 
 
+def check_status(st: torch.Tensor):
+    """Raise if mmr_index_search flagged a query (status != 0).  The selection kernel resolves
+    candidate-buffer overflow itself (batched exact merge), so this is a guard, not a code path."""
+    if st.numel() and int(st.max().item()) != 0:
+        raise RuntimeError(f"mmr_index_search returned status {int(st.max().item())} for "
+                           f"{int((st != 0).sum().item())} queries")
+
+
 def merge_topk(scores64: torch.Tensor, idx: torch.Tensor, k_out: int):
     """[L][B][k_in] f64 scores + int64 idx (-1 = empty) -> global top-k_out (idx, f32, f64) on device."""
     _lib.require_gpu(scores64)
@@ -204,17 +213,8 @@ class MI355XRetrievalEngine(RetrievalEngine):
             e = torch.empty((q.shape[0], 0))
             return (e.long().numpy(), e.numpy()) if is_np else (e.long(), e)
         idx, sc, st = self.index.search(q, k_eff, want_status=True)
-        if self.index.mode == "f16" and st.numel() and int(st.max().item()) != 0:
-            # fp16 margin overflowed the candidate buffer on some queries: redo them in x3
-            bad = torch.nonzero(st != 0).flatten()
-            self.index.set_mode("x3")
-            try:
-                i2, s2, st2 = self.index.search(q[bad].contiguous(), k_eff, want_status=True)
-            finally:
-                self.index.set_mode("f16")
-            idx[bad], sc[bad], st[bad] = i2, s2, st2
-        if check and int(st.max().item() if st.numel() else 0) != 0:
-            raise RuntimeError("candidate buffer overflow in mmr_index_search (massively tied scores)")
+        if check:
+            check_status(st)
         if is_np:
             return idx.cpu().numpy(), sc.cpu().numpy()
         return idx, sc
@@ -254,15 +254,38 @@ class DLSRetrievalEngine(MI355XRetrievalEngine):
                  link_threshold: float = 0.5, max_links: int = 10, fdb_path: Optional[str] = None,
                  name: Optional[str] = None, device=None, embs=None, ids=None, **_ignored):
         super().__init__(features_path, ids_path, device=device, embs=embs, ids=ids)
-        self.fdb_path = None
-        if fdb_path or name:
-            p = str(fdb_path or name)
-            self.fdb_path = p[:-4] + ".npz" if p.endswith(".pkl") else p
+        self.fdb_path = self.cache_path(features_path, fdb_path, name)
         graph = self._load_cache()
         if graph is None:
             graph = self._build_link_graph(link_threshold, max_links)
             self._save_cache(graph)
         self.link_graph = graph
+
+    @staticmethod
+    def cache_path(features_path, fdb_path=None, name=None):
+        """Link-graph cache file (retrieval.py:72-79): fdb_path if given, else `name` or
+        '<features stem>_link_graph' inside the feature-DB directory — $MMR_FEATURE_DB_DIR when set
+        (the reference's FEATURES_PATH), else the features file's directory; always an .npz (a '.pkl'
+        suffix is replaced, any other name gets '.npz' appended — np.savez would append it anyway).
+        The parent directory is created (retrieval.py:82).  None for an in-memory gallery with
+        neither a path nor a name."""
+        import os
+        db_dir = os.environ.get("MMR_FEATURE_DB_DIR")
+        if fdb_path:
+            p = str(fdb_path)
+        elif features_path is not None or (name and db_dir):
+            d = db_dir or os.path.dirname(os.path.abspath(str(features_path)))
+            stem = os.path.splitext(os.path.basename(str(features_path)))[0] if features_path is not None else ""
+            p = os.path.join(d, str(name) if name else f"{stem}_link_graph")
+        elif name:
+            p = str(name)
+        else:
+            return None
+        if p.endswith(".pkl"):
+            p = p[:-4]
+        p = p if p.endswith(".npz") else p + ".npz"
+        os.makedirs(os.path.dirname(os.path.abspath(p)), exist_ok=True)
+        return p
 
     def _load_cache(self):
         import os

@@ -153,9 +153,10 @@ class BertTower:
                 "ln2_g": _f(sd[p + "output.LayerNorm.weight"], dev), "ln2_b": _f(sd[p + "output.LayerNorm.bias"], dev),
             })
         self.hidden = self.word.shape[1]
-        # optional list: (start, end) torch.cuda.Event pairs around every FFN1 GEMM launch (bench
-        # roofline of the dominant kernel; events ride torch's current stream = the launch stream)
-        self.ffn1_events = None
+        # optional dict name -> list of (start, end) torch.cuda.Event pairs around every launch of the
+        # four GEMMs of a layer ("qkv", "o", "ffn1", "ffn2"): the bench's per-kernel roofline (events
+        # ride torch's current stream = the launch stream)
+        self.gemm_events = None
 
     def forward(self, input_ids, attention_mask=None):
         """(B, L) ids/mask -> (B, L, C) bf16 last_hidden_state.  L is truncated to
@@ -171,20 +172,24 @@ class BertTower:
         ids, mask = ids.contiguous(), mask.contiguous()
         heads = cfg["num_attention_heads"]
         h = ops.bert_embed(ids, self.word, self.pos, self.type0, self.eg, self.eb, 1e-12)
+        ev = self.gemm_events
+
+        def gemm(name, x, w, b, act=0):
+            if ev is None:
+                return ops.linear(x, w, b, act=act)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            y = ops.linear(x, w, b, act=act)
+            e1.record()
+            ev.setdefault(name, []).append((e0, e1))
+            return y
         for ly in self.layers:
-            qkv = ops.linear(h, ly["qkv_w"], ly["qkv_b"])
+            qkv = gemm("qkv", h, ly["qkv_w"], ly["qkv_b"])
             ctx = ops.bert_attention(qkv, mask, heads, self.hidden // heads)
-            a = ops.linear(ctx, ly["o_w"], ly["o_b"])
+            a = gemm("o", ctx, ly["o_w"], ly["o_b"])
             h = ops.add_layernorm(a, h, ly["ln1_g"], ly["ln1_b"], 1e-12)
-            if self.ffn1_events is not None:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                f = ops.linear(h, ly["i_w"], ly["i_b"], act=1)
-                e1.record()
-                self.ffn1_events.append((e0, e1))
-            else:
-                f = ops.linear(h, ly["i_w"], ly["i_b"], act=1)
-            f = ops.linear(f, ly["f_w"], ly["f_b"])
+            f = gemm("ffn1", h, ly["i_w"], ly["i_b"], act=1)
+            f = gemm("ffn2", f, ly["f_w"], ly["f_b"])
             h = ops.add_layernorm(f, h, ly["ln2_g"], ly["ln2_b"], 1e-12)
         return h
 

@@ -153,12 +153,18 @@ def bert_forward(ids, mask, sd, num_layers, num_heads, eps=1e-12):
     return h
 
 
-def backbones_forward(image, ids, mask, swin_sd, bert_sd, swin_cfg, bert_cfg):
+def swin_image(image, swin_sd, swin_cfg):
+    """Backbones.forward image branch (fusion.py:259-265): (img_global, img_patches)."""
     feats = swin_forward_features(image, swin_sd, swin_cfg["depths"], swin_cfg["num_heads"])
     B, H, W, C = feats.shape
     pf = feats.reshape(B, H * W, C)
     img_patches = _ln(pf, swin_sd["norm.weight"], swin_sd["norm.bias"], 1e-5)  # swin_norm again
     img_global = pf.mean(dim=1)
+    return img_global, img_patches
+
+
+def backbones_forward(image, ids, mask, swin_sd, bert_sd, swin_cfg, bert_cfg):
+    img_global, img_patches = swin_image(image, swin_sd, swin_cfg)
     txt = bert_forward(ids, mask, bert_sd, bert_cfg["num_hidden_layers"], bert_cfg["num_attention_heads"])
     return (img_global, img_patches), txt
 

@@ -83,3 +83,78 @@ def test_shard_bounds_and_host_merge_edges():
     mi, ms, m64 = merge_topk_host(s, i, 5)
     assert mi.tolist() == [[3, 7, 9, 2, -1]]
     assert m64[0, :4].tolist() == [0.9, 0.9, 0.7, 0.5] and np.isneginf(m64[0, 4].item())
+
+
+def _worker_status(rank, world, port, N, D, b, K, out_q):
+    """local_search flags every other query as overflowed (status 1) and returns garbage for it;
+    ShardedIndex must re-run exactly those through fallback_search before the exchange."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        G, _ = synthetic.labelled_gallery(N, D, 81)
+        Q, _ = synthetic.labelled_gallery(world * b, D, 82)
+        s, e = shard_bounds(N, world)[rank]
+        calls = []
+
+        def exact(q, k):
+            i, sc = oknn.exact_topk(q.numpy(), G[s:e], k)
+            return torch.from_numpy(np.where(i >= 0, i + s, -1).astype(np.int64)), torch.from_numpy(sc)
+
+        def local(q, k):
+            i, sc = exact(q, k)
+            st = torch.zeros(q.shape[0], dtype=torch.int32)
+            st[::2] = 1
+            i[::2] = 0                 # garbage for the flagged queries
+            sc[::2] = 9.0
+            return i, sc, st
+
+        def fallback(q, k):
+            calls.append(q.shape[0])
+            return exact(q, k)
+
+        sh = ShardedIndex(G[s:e], N, s, local_search=local, fallback_search=fallback)
+        mi, ms, m64 = sh.search(torch.from_numpy(Q[rank * b:(rank + 1) * b]), K)
+        out_q.put((rank, mi.numpy(), m64.numpy(), sh.reruns, calls))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_search_reruns_flagged_queries():
+    world, N, D, b, K = 2, 1500, 48, 5, 7
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_status, args=(r, world, port, N, D, b, K, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    G, _ = synthetic.labelled_gallery(N, D, 81)
+    Q, _ = synthetic.labelled_gallery(world * b, D, 82)
+    ei, es = oknn.exact_topk(Q, G, K)
+    for rank, mi, m64, reruns, calls in res:
+        assert reruns == (world * b + 1) // 2 and calls == [(world * b + 1) // 2]
+        np.testing.assert_array_equal(mi, ei[rank * b:(rank + 1) * b])
+        np.testing.assert_allclose(m64, es[rank * b:(rank + 1) * b], rtol=0, atol=1e-14)
+
+
+def test_dls_cache_path_naming(tmp_path, monkeypatch):
+    """DLS link-graph cache file (retrieval.py:72-79): explicit path, name / default stem inside the
+    feature-DB directory, always .npz (np.savez appends it to any other name)."""
+    from mmr_amd.retrieval import DLSRetrievalEngine
+    f = str(tmp_path / "emb" / "train_joint_embeddings.npy")
+    monkeypatch.delenv("MMR_FEATURE_DB_DIR", raising=False)
+    cp = DLSRetrievalEngine.cache_path
+    assert cp(f) == str(tmp_path / "emb" / "train_joint_embeddings_link_graph.npz")
+    assert cp(f, name="graph_cache") == str(tmp_path / "emb" / "graph_cache.npz")
+    assert cp(f, fdb_path=str(tmp_path / "x.pkl")) == str(tmp_path / "x.npz")
+    assert cp(f, fdb_path=str(tmp_path / "y")) == str(tmp_path / "y.npz")
+    monkeypatch.setenv("MMR_FEATURE_DB_DIR", str(tmp_path / "fdb"))
+    assert cp(f) == str(tmp_path / "fdb" / "train_joint_embeddings_link_graph.npz")
+    assert cp(None, name="g") == str(tmp_path / "fdb" / "g.npz")
+    assert (tmp_path / "fdb").is_dir()
+    monkeypatch.delenv("MMR_FEATURE_DB_DIR")
+    assert cp(None) is None

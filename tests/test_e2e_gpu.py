@@ -1,0 +1,119 @@
+"""GPU end-to-end retrieval parity: (image, report) inputs -> GPU towers + head -> GPU exact top-10,
+against the reference path restated on CPU (fp32 oracle towers + head -> sklearn-path top-10,
+src/Evaluate/retrieval_overlap.py:84-115), on the same inputs, over the same gallery.
+
+The kNN leg is exact given the same embeddings (test_knn_gpu.py); what differs here is the towers'
+bf16 arithmetic.  Reported per case: top-10 overlap (= Recall@10 of the GPU lists against the CPU
+lists, the overlap measure of retrieval_eval.py:147-157), and P@10 / R@10 / mAP@10 of both paths on
+synthetic labels (relevance = shares >= 1 of 43 labels, contructGT.py:69-81).  Bars: P@10 and R@10
+equal to the CPU path's within one relevant item per 10 queries, mean overlap >= 0.9."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from mmr_amd import metrics, synthetic
+from mmr_amd.model import Backbones, MultiModalRetrievalModel, init_fusion_state, init_head_state
+from mmr_amd.retrieval import MI355XRetrievalEngine
+from mmr_amd.towers import BERT_BASE, SWIN_T, init_bert_state, init_swin_state
+from oracle import knn as oknn
+from oracle import towers as otw
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _labels(n, seed):
+    rng = np.random.default_rng(seed)
+    lab = np.zeros((n, synthetic.NUM_LABELS), np.uint8)
+    for i in range(n):
+        lab[i, rng.choice(synthetic.NUM_LABELS, size=int(rng.integers(1, 4)), replace=False)] = 1
+    return synthetic.labels_to_bits(lab)
+
+
+def _compare(q_gpu, q_cpu, G, qbits, gbits, K=10):
+    eng = MI355XRetrievalEngine(embs=G, ids=[str(i) for i in range(len(G))], dtype="fp16")
+    gi, _ = eng.search(q_gpu, K=K)
+    gi = gi.cpu().numpy() if isinstance(gi, torch.Tensor) else gi
+    eng.close()
+    ci, _ = oknn.sklearn_topk(q_cpu, G, K)
+    overlap = float(np.mean([len(set(gi[r]) & set(ci[r])) / K for r in range(len(ci))]))
+
+    def pr(idx):
+        # P@K with the reference's precision_at_k (retrieval_metrics.py:4-11) on id lists; R@K, MRR
+        # from ranking_metrics (retrieval_overlap.py:84-115)
+        rel = [[str(j) for j in np.nonzero(gbits & qbits[q])[0]] for q in range(len(qbits))]
+        p = np.mean([metrics.precision_at_k([str(j) for j in idx[q]], rel[q], K) for q in range(len(qbits))])
+        mrr, _, rec = metrics.ranking_metrics(idx, qbits, gbits, K)
+        return {"P@10": float(p), "R@10": float(rec), "MRR": float(mrr)}
+    return overlap, pr(gi), pr(ci), gi, ci
+
+
+def _assert_parity(overlap, mg, mc, nq):
+    print(json.dumps({"top10_overlap": overlap, "gpu": mg, "cpu": mc}))
+    # P@10 / R@10 of the GPU path equal the CPU path's up to one relevant item swapped over the
+    # whole query set (a bf16 tower moving one near-tied neighbour across the cut)
+    assert abs(mg["P@10"] - mc["P@10"]) <= 1.0 / (10 * nq) + 1e-12
+    assert abs(mg["R@10"] - mc["R@10"]) <= 1.0 / nq
+    assert overlap >= 0.9
+
+
+def test_e2e_mini_towers_reference_weights_multimodal():
+    """The reference's own mini-tower weights (tests/golden/towers_mini.npz, exported from the
+    reference model), multimodal head: 64 query pairs against a gallery of 320 oracle-embedded
+    pairs (the reference would have built the gallery on its own path)."""
+    f = np.load(os.path.join(GOLDEN, "towers_mini.npz"), allow_pickle=False)
+    cfg = json.loads(bytes(f["cfg"]).decode())
+    w = {k[2:]: torch.from_numpy(synthetic.bf16_bits_to_f32(f[k]).copy()) for k in f.files if k.startswith("w:")}
+    swin = {k[5:]: v for k, v in w.items() if k.startswith("swin.")}
+    bert = {k[5:]: v for k, v in w.items() if k.startswith("bert.")}
+    head = {k[5:]: v for k, v in w.items() if k.startswith("head.")}
+    scfg = dict(SWIN_T, embed_dim=cfg["swin"]["embed_dim"], depths=cfg["swin"]["depths"],
+                num_heads=cfg["swin"]["num_heads"])
+    bcfg = dict(BERT_BASE, **cfg["bert"])
+    bb = Backbones(swin_state=swin, bert_state=bert, swin_cfg=scfg, bert_cfg=bcfg, device=DEV)
+    m = MultiModalRetrievalModel(joint_dim=cfg["joint_dim"], num_heads=cfg["num_heads"], model_type="multimodal",
+                                 backbones=bb, head_state=head, device=DEV)
+    nq, ng = 64, 320
+    img = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(nq + ng, 41)))
+    ids, mask = (torch.from_numpy(a) for a in synthetic.reports(nq + ng, 128, 42, vocab=bcfg["vocab_size"]))
+    q_gpu = m.query_embeddings(img[:nq].to(DEV), ids[:nq].to(DEV), mask[:nq].to(DEV))
+    mmcfg = {"num_heads": cfg["num_heads"]}
+    with torch.no_grad():
+        (g, p), t = otw.backbones_forward(img, ids, mask, swin, bert, scfg, bcfg)
+        emb = otw.heads(g, p, t, head, "multimodal", mm_cfg=mmcfg)["joint_emb"].numpy()
+    q_cpu, G = emb[:nq], np.ascontiguousarray(emb[nq:])
+    overlap, mg, mc, _, _ = _compare(q_gpu, q_cpu, G, _labels(nq, 43), _labels(ng, 44))
+    _assert_parity(overlap, mg, mc, nq)
+
+
+@pytest.mark.parametrize("model_type", ["multimodal", "text"])
+def test_e2e_full_size_batch_256(model_type):
+    """Swin-T + BERT-base (random init, the bench model) at the bench's batch of 256 through
+    query_embeddings (stream-overlapped after the first call); 24 of the 256 queries are re-embedded
+    by the fp32 oracle; top-10 over a 100k x 768 labelled gallery."""
+    from mmr_amd.model import build_bench_model
+    m = build_bench_model(device=DEV, joint_dim=768, model_type=model_type)
+    B, nq = 256, 24
+    img = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(B, 51)))
+    ids, mask = (torch.from_numpy(a) for a in synthetic.reports(B, 128, 52))
+    imgd = img.to(DEV) if model_type == "multimodal" else None
+    m.query_embeddings(imgd, ids.to(DEV), mask.to(DEV))
+    q_gpu = m.query_embeddings(imgd, ids.to(DEV), mask.to(DEV))[:nq]
+    ssd, bsd = init_swin_state(SWIN_T, 2709), init_bert_state(BERT_BASE, 2710)
+    hsd = init_head_state(768, 768, 768, 2711)
+    with torch.no_grad():
+        if model_type == "multimodal":
+            hsd.update(init_fusion_state(768, 768, 768, 8, 5, 2712))
+            (g, p), t = otw.backbones_forward(img[:nq], ids[:nq], mask[:nq], ssd, bsd, SWIN_T, BERT_BASE)
+            q_cpu = otw.heads(g, p, t, hsd, "multimodal", mm_cfg={"num_heads": 8})["joint_emb"].numpy()
+        else:
+            t = otw.bert_forward(ids[:nq], mask[:nq], bsd, 12, 12)
+            q_cpu = otw.heads(None, None, t, hsd, "text")["joint_emb"].numpy()
+    G, gl = synthetic.labelled_gallery(100_000, 768, 53)
+    overlap, mg, mc, _, _ = _compare(q_gpu, q_cpu, G, _labels(nq, 54), synthetic.labels_to_bits(gl))
+    _assert_parity(overlap, mg, mc, nq)

@@ -148,3 +148,45 @@ def test_full_size_multimodal_vs_oracle():
         ref = otw.heads(rg, rp, rt, hs, "multimodal", mm_cfg={"num_heads": 8})["joint_emb"]
     _check_emb(o["joint_emb"], ref)
     assert torch.equal(o["joint_emb"], q)
+
+
+@pytest.mark.parametrize("text", [True, False])
+def test_fusion_stack_reference_joint_dim_1024(text):
+    """The reference's configured head geometry (configs/config.yaml:14 joint_dim 1024, num_heads 8
+    -> head_dim 128, num_fusion_layers 5) on 768-wide backbone features, vs the oracle."""
+    g = torch.Generator().manual_seed(12)
+    B, Lt, Np, C, D = 3, 128, 49, 768, 1024
+    hs = init_head_state(C, C, D, 23)
+    hs.update(init_fusion_state(C, C, D, 8, 5, 24))
+    G = torch.randn(B, C, generator=g)
+    P = torch.randn(B, Np, C, generator=g)
+    T = bf(torch.randn(B, Lt, C, generator=g)).float() if text else None
+    with torch.no_grad():
+        ref = otw.multimodal(G, P, T, hs, num_heads=8)
+    from mmr_amd.fusion import FusionStack
+    fs = FusionStack(hs, 8, device=DEV)
+    got = fs.forward(G.to(DEV), P.to(DEV), T.to(DEV) if text else None)
+    assert got.shape == (B, D)
+    _check_emb(got, ref)
+
+
+def test_full_size_multimodal_joint_dim_1024_batch_256_vs_oracle():
+    """Swin-T + BERT-base + 5-layer multimodal head at joint_dim 1024 (config.yaml:14), B=256 through
+    query_embeddings (the bench's stream-overlapped path), compared with the oracle on 4 rows."""
+    ssd, bsd = init_swin_state(SWIN_T, 15), init_bert_state(BERT_BASE, 16)
+    hs = init_head_state(768, 768, 1024, 17)
+    hs.update(init_fusion_state(768, 768, 1024, 8, 5, 18))
+    bb = Backbones(swin_state=ssd, bert_state=bsd, device=DEV)
+    m = MultiModalRetrievalModel(joint_dim=1024, num_heads=8, model_type="multimodal", backbones=bb,
+                                 head_state=hs, device=DEV)
+    img = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(256, 19)))
+    ids, mask = (torch.from_numpy(a) for a in synthetic.reports(256, 128, 20))
+    q = m.query_embeddings(img.to(DEV), ids.to(DEV), mask.to(DEV))      # first call: towers in sequence
+    q2 = m.query_embeddings(img.to(DEV), ids.to(DEV), mask.to(DEV))     # overlapped streams
+    torch.cuda.synchronize()
+    assert q.shape == (256, 1024) and torch.equal(q, q2)
+    rows = [0, 77, 128, 255]
+    with torch.no_grad():
+        (rg, rp), rt = otw.backbones_forward(img[rows], ids[rows], mask[rows], ssd, bsd, SWIN_T, BERT_BASE)
+        ref = otw.heads(rg, rp, rt, hs, "multimodal", mm_cfg={"num_heads": 8})["joint_emb"]
+    _check_emb(q[rows], ref)

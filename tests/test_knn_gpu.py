@@ -218,3 +218,97 @@ def test_engine_retrieve_contract_and_precision_at_10(tmp_path):
              for q in range(len(Qm))]
     assert p_ref == p_got
     eng.close()
+
+
+@pytest.mark.parametrize("mode", ["x3", "f32", "f16"])
+def test_knn_massive_ties_batched_exact(mode):
+    """More exact ties inside the candidate margin than the selection buffer holds (2048 rows /
+    512 groups): the selection kernel merges the candidates batch by batch into an exact top-K —
+    status stays 0 and the lists equal the oracle's (ties by lower index), no host re-run."""
+    rng = np.random.default_rng(77)
+    G = rng.standard_normal((12_000, 128), dtype=np.float32)
+    G[1000:7000] = G[5]                      # 6001 identical rows
+    G[9000:9003] = G[5] * 2.0                # same direction, other norms: equal cosine too
+    Qm = np.concatenate([G[5:6], G[5:6] * -1.0, rng.standard_normal((3, 128), dtype=np.float32)])
+    for K in (10, 256):
+        gi, _ = _exact_check(G, Qm, K, mode=mode)
+        assert gi[0, 0] == 5 and gi[0, 1:K].tolist() == list(range(1000, 999 + K))
+
+
+def test_knn_f16_dim_above_1024():
+    """d > 1024 (Dp = 1536): the strided query prep and the d > 1024 re-score branch; the f16
+    margin term 2 sqrt(Dp) 2^-25 is computed from Dp."""
+    rng = np.random.default_rng(1536)
+    G = rng.standard_normal((4000, 1536), dtype=np.float32)
+    G[10:14] = G[2]
+    Qm = np.concatenate([G[2:3], rng.standard_normal((40, 1536), dtype=np.float32)])
+    for mode in ("f16", "x3", "f32"):
+        gi, _ = _exact_check(G, Qm, 16, mode=mode)
+        assert gi[0, :5].tolist() == [2, 10, 11, 12, 13]
+
+
+def _exact_topk_chunked(Q, G, K, chunk=131072):
+    """oracle.knn.exact_topk semantics over a large gallery in row chunks (f64 scores, score desc
+    then index asc) without an N x Q f64 matrix of the whole gallery."""
+    Q64 = np.asarray(Q, np.float64)
+    qn = np.linalg.norm(Q64, axis=1)
+    best_s = np.full((len(Q), 0), -np.inf)
+    best_i = np.zeros((len(Q), 0), np.int64)
+    for c0 in range(0, len(G), chunk):
+        Gc = np.asarray(G[c0:c0 + chunk], np.float64)
+        gn = np.linalg.norm(Gc, axis=1)
+        den = qn[:, None] * gn[None, :]
+        with np.errstate(invalid="ignore", divide="ignore"):
+            s = np.where(den > 0, (Q64 @ Gc.T) / np.where(den > 0, den, 1.0), 0.0)
+        cs = np.concatenate([best_s, s], 1)
+        ci = np.concatenate([best_i, np.broadcast_to(np.arange(c0, c0 + len(Gc)), s.shape)], 1)
+        order = np.lexsort((ci, -cs), axis=1)[:, :K]
+        best_s, best_i = np.take_along_axis(cs, order, 1), np.take_along_axis(ci, order, 1)
+    return best_i, best_s
+
+
+def test_knn_cfg3_1m_text_queries_top50():
+    """BASELINE cfg3's kNN leg: 1024 queries, top-50 over 1M x 768.  f16 and x3 scans return the
+    same exact lists for all 1024 queries; 32 of them equal the oracle's exact top-50."""
+    G = synthetic.gauss_gallery(1_000_000, 768, synthetic.SEED + 3)
+    G[123_456:123_460] = G[777]
+    Qm = synthetic.gauss_gallery(1024, 768, synthetic.SEED + 4)
+    Qm[0] = G[777] * 0.25
+    ix = GalleryIndex(G, mode="f16")
+    q = torch.from_numpy(Qm).cuda()
+    i16, _, s16, st16 = ix.search(q, 50, want_f64=True, want_status=True)
+    ix.set_mode("x3")
+    i3, _, s3, st3 = ix.search(q, 50, want_f64=True, want_status=True)
+    torch.cuda.synchronize()
+    assert int(st16.max()) == 0 and int(st3.max()) == 0
+    assert torch.equal(i16, i3) and torch.equal(s16, s3)
+    sub = np.r_[0, np.arange(1, 1024, 33)][:32]
+    ei, es = _exact_topk_chunked(Qm[sub], G, 50)
+    np.testing.assert_array_equal(i16.cpu().numpy()[sub], ei)
+    np.testing.assert_allclose(s16.cpu().numpy()[sub], es, rtol=0, atol=1e-12)
+    assert i16[0, :5].tolist() == [777, 123_456, 123_457, 123_458, 123_459]
+    ix.close()
+
+
+def test_knn_two_streams_share_one_index():
+    """Searches on one index from two streams: the workspace follows the stream (event hand-off),
+    so concurrent enqueues return the same lists as sequential ones."""
+    G = synthetic.gauss_gallery(50_000, 256, 91)
+    Qa = torch.from_numpy(synthetic.gauss_gallery(200, 256, 92)).cuda()
+    Qb = torch.from_numpy(synthetic.gauss_gallery(40, 256, 93)).cuda()
+    for mode in ("f16", "x3"):
+        ix = GalleryIndex(G, mode=mode)
+        ra = ix.search(Qa, 20)[0].clone()
+        rb = ix.search(Qb, 20)[0].clone()
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        outs = []
+        for _ in range(4):
+            with torch.cuda.stream(s1):
+                oa = ix.search(Qa, 20)[0]
+            with torch.cuda.stream(s2):
+                ob = ix.search(Qb, 20)[0]
+            outs.append((oa, ob))
+        torch.cuda.synchronize()
+        for oa, ob in outs:
+            assert torch.equal(oa, ra) and torch.equal(ob, rb)
+        ix.close()
