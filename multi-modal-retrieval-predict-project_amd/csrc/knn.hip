@@ -490,6 +490,245 @@ __global__ __launch_bounds__(64 * WQ) void knn_scan_f16_gmax(const uint16_t* __r
     }
 }
 
+// ------------------------------------------------------------------ fp16 tile scan (mode f16, Q > 32)
+// The same fp16 product as knn_scan_f16_gmax, as an LDS-staged MFMA GEMM for query passes of 64-256
+// queries.  Workgroup tile: RT = WR*MR gallery row tiles (16 rows each) x QT = WQ*MQ query tiles, one
+// 32-deep k-piece per slice; wave (wq, wr) computes MQ query tiles x MR row tiles.  Every operand is
+// a tile32h 1-KB piece (16 rows x 32 halfs, lane l holding 8 halfs of row l&15 — the
+// v_mfma_f32_16x16x32_f16 operand layout), so each piece lands in LDS by ONE global_load_lds
+// (lane-linear, no swizzle) and each fragment read is one conflict-free ds_read_b128.
+// The gallery is the A operand and the queries the B operand, so a lane's 4 accumulators are 4
+// CONSECUTIVE gallery rows of one query: the epilogue keeps their max (a contiguous 4-row unit,
+// knn_select_t<2>), one float per (query, 4 rows).
+// Schedule: an LDS ring of STAGES slices filled by glds (a wave issues either gallery or query pieces,
+// PW per slice); at each step the wave waits for the slice it needs next (own vmcnt, then one barrier
+// for every wave's pieces), refills the ring slot freed by the previous step and runs its MFMAs.  PF:
+// the fragments of slice s+1 are read during slice s's MFMAs (one fewer ring slot in flight).
+// Per-slice bookkeeping is incremental (uniform slice cursors, per-lane piece offsets computed once
+// per tile, a constant vmcnt in steady state): a first version computed tile / slice / ring indices by
+// division and 64-bit address math per piece per slice, and its instruction issue (SQ_ACTIVE_INST_ANY)
+// was 3-6x its MFMA time.
+// Persistent: workgroup w owns the 16-row tiles [n_rt*w/G, n_rt*(w+1)/G) (balanced to one row tile),
+// walked in tiles of RT row tiles; the ring runs across tile boundaries, so the next tile's slices
+// load under the epilogue.  In the last (partial) tile, row tiles past the range are clamped to its
+// last one (valid memory, results discarded) and a wave whose row tiles are all past it skips its MFMAs.
+// Epilogue: a 4x4 lane transpose (lanes qc + 16h x 4 row tiles) turns each lane's maxima of units
+// {4i + h} into 4 consecutive units, one 16-B store per (query tile, 4 row tiles): NST stores per wave
+// per tile, counted out of the next step's vmcnt wait instead of drained.
+template <int WQ, int MQ, int WR, int MR, bool PF>
+struct F16TileCfg {
+  static constexpr int NW = WQ * WR;             // waves
+  static constexpr int RT = WR * MR;             // gallery row tiles per tile
+  static constexpr int QT = WQ * MQ;             // query tiles
+  static constexpr int P = RT + QT;              // 1-KB pieces per slice
+  static constexpr int PW = P / NW;              // glds per wave per slice
+  static constexpr int SLICE_B = P * 1024;
+  static constexpr int STAGES = 163840 / SLICE_B > 8 ? 8 : 163840 / SLICE_B;
+  static constexpr int AHEAD = STAGES - (PF ? 3 : 2);  // slices in flight beyond the one waited for
+  static constexpr int NST = MQ * MR / 4;        // epilogue stores per wave per tile
+  static_assert(P % NW == 0 && MR % 4 == 0, "tile shape");
+  static_assert(AHEAD >= 1 && PW * AHEAD + NST <= 63, "ring depth / vmcnt range");
+};
+
+__device__ __forceinline__ void wait_vm(int n) {
+  // s_waitcnt vmcnt(n) for a wave-uniform runtime n in [0, 63] (rare path: the end of the stream)
+  switch (n) {
+#define MMR_VM(N) case N: __builtin_amdgcn_s_waitcnt(((N) & 15) | (7 << 4) | (15 << 8) | (((N) >> 4) << 14)); break;
+    MMR_VM(0) MMR_VM(1) MMR_VM(2) MMR_VM(3) MMR_VM(4) MMR_VM(5) MMR_VM(6) MMR_VM(7) MMR_VM(8) MMR_VM(9)
+    MMR_VM(10) MMR_VM(11) MMR_VM(12) MMR_VM(13) MMR_VM(14) MMR_VM(15) MMR_VM(16) MMR_VM(17) MMR_VM(18)
+    MMR_VM(19) MMR_VM(20) MMR_VM(21) MMR_VM(22) MMR_VM(23) MMR_VM(24) MMR_VM(25) MMR_VM(26) MMR_VM(27)
+    MMR_VM(28) MMR_VM(29) MMR_VM(30) MMR_VM(31) MMR_VM(32) MMR_VM(33) MMR_VM(34) MMR_VM(35) MMR_VM(36)
+    MMR_VM(37) MMR_VM(38) MMR_VM(39) MMR_VM(40) MMR_VM(41) MMR_VM(42) MMR_VM(43) MMR_VM(44) MMR_VM(45)
+    MMR_VM(46) MMR_VM(47) MMR_VM(48) MMR_VM(49) MMR_VM(50) MMR_VM(51) MMR_VM(52) MMR_VM(53) MMR_VM(54)
+    MMR_VM(55) MMR_VM(56) MMR_VM(57) MMR_VM(58) MMR_VM(59) MMR_VM(60) MMR_VM(61) MMR_VM(62)
+#undef MMR_VM
+    default: break;
+  }
+}
+template <int N>
+__device__ __forceinline__ void wait_vm_c() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// v[h] of lane (qc + 16c) -> out[c] of lane (qc + 16h): the 4x4 transpose of the epilogue
+__device__ __forceinline__ f32x4 transpose4(const float (&v)[4], int h, int qc) {
+  f32x4 out;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int give = (h - r) & 3, from = (h + r) & 3;  // this lane provides v[give], receives from lane `from`
+    const float send = give == 0 ? v[0] : give == 1 ? v[1] : give == 2 ? v[2] : v[3];
+    const float got = __shfl(send, qc + 16 * from, 64);
+    if (from == 0) out[0] = got;
+    else if (from == 1) out[1] = got;
+    else if (from == 2) out[2] = got;
+    else out[3] = got;
+  }
+  return out;
+}
+
+template <int WQ, int MQ, int WR, int MR, bool PF>
+__global__ __launch_bounds__(64 * WQ * WR) void knn_scan_f16_tile(const uint16_t* __restrict__ qh,
+                                                                  const uint16_t* __restrict__ gh,
+                                                                  float* __restrict__ gmax, int Dp, int64_t ldG,
+                                                                  int64_t n, int64_t n_rt) {
+  using C = F16TileCfg<WQ, MQ, WR, MR, PF>;
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];  // [STAGES][P][512] halfs
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave / WQ, wq = wave % WQ;
+  const int64_t lo = n_rt * blockIdx.x / gridDim.x, hi = n_rt * (blockIdx.x + 1) / gridDim.x;
+  if (lo >= hi) return;
+  const int KP = Dp / 32;                          // k-pieces = slices per tile
+  const int ntiles = (int)((hi - lo + C::RT - 1) / C::RT);
+  const int nslices = ntiles * KP;
+  const int64_t tile_b = (int64_t)KP * 1024;       // bytes of one 16-row tile (all k-pieces)
+  // this wave's glds pieces p0 .. p0+PW-1: gallery row tiles (p < RT), then query tiles
+  const int p0 = wave * C::PW;
+  uint32_t off[C::PW];  // per-lane byte offsets of the pieces inside the current tile's k-piece 0
+  auto set_offsets = [&](int64_t rt0) {
+    const int valid = (int)(hi - rt0 < C::RT ? hi - rt0 : C::RT);  // row tiles of this tile in range
+#pragma unroll
+    for (int i = 0; i < C::PW; ++i) {
+      const int p = p0 + i;
+      const int piece = p < C::RT ? (p < valid ? p : valid - 1) : p - C::RT;
+      off[i] = (uint32_t)(piece * tile_b) + lane * 16;
+    }
+  };
+  // issue cursor: the next slice to load (uniform bases of its gallery and query pieces)
+  int ic_tile = 0, ic_kp = 0, ic_stage = 0;
+  const char* ic_gbase = (const char*)gh + lo * tile_b;
+  const char* ic_qbase = (const char*)qh;
+  set_offsets(lo);
+  auto issue_next = [&]() {
+    if (ic_tile >= ntiles) return;
+    char* dst = (char*)dsm + ic_stage * C::SLICE_B + p0 * 1024;
+#pragma unroll
+    for (int i = 0; i < C::PW; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)((p0 + i < C::RT ? ic_gbase : ic_qbase) + off[i]),
+                                       (lds_ptr_t)(dst + i * 1024), 16, 0, 0);
+    ic_stage = ic_stage + 1 == C::STAGES ? 0 : ic_stage + 1;
+    ic_gbase += 1024;
+    ic_qbase += 1024;
+    if (++ic_kp == KP) {
+      ic_kp = 0;
+      ++ic_tile;
+      const int64_t rt0 = lo + (int64_t)C::RT * ic_tile;
+      ic_gbase = (const char*)gh + rt0 * tile_b;
+      ic_qbase = (const char*)qh;
+      if (ic_tile < ntiles) set_offsets(rt0);
+    }
+  };
+  const uint32_t lane_b = lane * 16;
+  auto frag = [&](int stage, int piece) {
+    return *(const h8*)((const char*)dsm + stage * C::SLICE_B + piece * 1024 + lane_b);
+  };
+  // wait until this wave's pieces of the slice `ahead_of` slices before the cursor end landed
+  int waited = 0;  // slices whose pieces this wave has waited for
+  bool stores_out = false;
+  auto wait_slice = [&]() {
+    const int issued_after = (ic_tile * KP + ic_kp) - (waited + 1);  // slices issued after the awaited one
+    if (issued_after == C::AHEAD) {
+      if (stores_out) wait_vm_c<C::PW * C::AHEAD + C::NST>();
+      else wait_vm_c<C::PW * C::AHEAD>();
+    } else {
+      wait_vm(C::PW * issued_after + (stores_out ? C::NST : 0));
+    }
+    stores_out = false;
+    ++waited;
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's pieces landed; every wave is past the previous step
+    asm volatile("" ::: "memory");
+  };
+  h8 fa[MR], fb0[MQ], fb1[MQ];
+  f32x4 acc[MQ][MR];
+  // prologue: STAGES-1 slices in flight
+#pragma unroll
+  for (int p = 0; p < C::STAGES - 1; ++p) issue_next();
+  int stage = 0;  // ring slot of the slice being computed
+  if constexpr (PF) {
+    wait_slice();  // slice 0
+#pragma unroll
+    for (int i = 0; i < MR; ++i) fa[i] = frag(0, wr * MR + i);
+#pragma unroll
+    for (int t = 0; t < MQ; ++t) fb0[t] = frag(0, C::RT + wq * MQ + t);
+  }
+  // one step: slice (tile, kp) in ring slot `stage`; with PF its fragments are in (fa, fb) and the
+  // next slice's are read into (fa, nb)
+  auto step = [&](int tile, int kp, int64_t rt0, bool active, h8 (&fb)[MQ], h8 (&nb)[MQ]) {
+    const bool more = tile + 1 < ntiles || kp + 1 < KP;
+    if (PF) {
+      if (more) wait_slice();  // slice s+1 (for the fragment prefetch)
+    } else {
+      wait_slice();            // slice s
+    }
+    issue_next();  // into the slot the previous step used
+    const int nstage = stage + 1 == C::STAGES ? 0 : stage + 1;
+    if (active) {
+      if (!PF) {
+#pragma unroll
+        for (int i = 0; i < MR; ++i) fa[i] = frag(stage, wr * MR + i);
+#pragma unroll
+        for (int t = 0; t < MQ; ++t) fb[t] = frag(stage, C::RT + wq * MQ + t);
+      }
+#pragma unroll
+      for (int i = 0; i < MR; ++i) {
+#pragma unroll
+        for (int t = 0; t < MQ; ++t) acc[t][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i], fb[t], acc[t][i], 0, 0, 0);
+        if (PF && more) {
+          fa[i] = frag(nstage, wr * MR + i);
+#pragma unroll
+          for (int t = i * MQ / MR; t < (i + 1) * MQ / MR; ++t) nb[t] = frag(nstage, C::RT + wq * MQ + t);
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this step's fragment reads returned
+    stage = nstage;
+    if (kp == KP - 1 && active) {
+      // epilogue: lane (query tile t, query qc, rows 16 rt + 4h .. +3) -> unit max; 4x4 lane transpose
+      // -> 4 consecutive units per lane -> one 16-B store per (t, block of 4 row tiles)
+      const int h = lane >> 4, qc = lane & 15;
+#pragma unroll
+      for (int t = 0; t < MQ; ++t) {
+        float* orow = gmax + (int64_t)(16 * (wq * MQ + t) + qc) * ldG;
+#pragma unroll
+        for (int b4 = 0; b4 < MR / 4; ++b4) {
+          const int64_t rtb = rt0 + wr * MR + 4 * b4;
+          float v[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int64_t r0 = (rtb + c) * 16 + 4 * h;
+            float mx = -INFINITY;
+#pragma unroll
+            for (int rg = 0; rg < 4; ++rg) mx = fmaxf(mx, r0 + rg < n ? acc[t][4 * b4 + c][rg] : -INFINITY);
+            v[c] = mx;
+          }
+          const f32x4 o = transpose4(v, h, qc);
+          if (rtb + h < hi) *(f32x4*)(orow + (rtb + h) * 4) = o;
+        }
+      }
+      stores_out = tile + 1 < ntiles;
+    }
+  };
+  for (int tile = 0; tile < ntiles; ++tile) {
+    const int64_t rt0 = lo + (int64_t)C::RT * tile;
+    const bool active = rt0 + wr * MR < hi;  // wave-uniform: some of this wave's row tiles are real
+#pragma unroll
+    for (int t = 0; t < MQ; ++t)
+#pragma unroll
+      for (int i = 0; i < MR; ++i) acc[t][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int kp = 0; kp < KP; kp += 2) {
+      step(tile, kp, rt0, active, fb0, fb1);
+      if (kp + 1 < KP) step(tile, kp + 1, rt0, active, fb1, fb0);
+    }
+    if (KP & 1) {  // odd slice count: the next tile starts with the sets swapped — keep fb0 current
+#pragma unroll
+      for (int t = 0; t < MQ; ++t) fb0[t] = fb1[t];
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (15 << 8));  // vmcnt(0): no LDS-DMA may land after the workgroup retires
+}
+
 // ------------------------------------------------------------------ skinny-Q scan (f32 MFMA)
 // Few queries (Q <= 16*QT, QT <= 4): the gallery read (N*Dp*4 B) is the whole cost, so the scan is a
 // streaming kernel — every gallery byte from HBM exactly once, no LDS, no barriers — on exact-product
@@ -1134,6 +1373,7 @@ struct mmr_index {
   double* qnorm64 = nullptr;  // [rows]
   float* vals = nullptr;      // scores (f32 mode) or per-(query, unit) maxima
   uint16_t* qs = nullptr;     // [rows][3Dp] bf16 split queries (x3 GEMM)
+  int n_cu = 256;             // compute units of `device` (persistent grids)
   hipEvent_t ws_event = nullptr;
   hipStream_t ws_stream = nullptr;
   bool ws_used = false;
@@ -1212,6 +1452,21 @@ struct DeviceGuard {
   }
 };
 
+// The LDS-staged fp16 tile scan for 33-256-query passes (MMR_KNN_F16_TILE=0: the one-wave stream
+// kernel instead, for A/B measurements).
+bool f16_tile_enabled() {
+  const char* e = getenv("MMR_KNN_F16_TILE");
+  return !(e && atoi(e) == 0);
+}
+
+template <int WQ, int MQ, int WR, int MR, bool PF>
+void launch_f16_tile(hipStream_t st, const mmr_index* ix, const uint16_t* qh, float* gm, int64_t ldG, int64_t n_rt) {
+  using C = F16TileCfg<WQ, MQ, WR, MR, PF>;
+  const size_t lds = (size_t)C::STAGES * C::SLICE_B;
+  knn_scan_f16_tile<WQ, MQ, WR, MR, PF><<<dim3((unsigned)ix->n_cu), dim3(64 * C::NW), lds, st>>>(
+      qh, ix->gh, gm, ix->Dp, ldG, ix->n, n_rt);
+}
+
 template <int MODE>
 void launch_select(hipStream_t st, int64_t nq, const float* vals, int64_t ldV, int64_t nunits, const mmr_index* ix,
                    int k, float two_delta, const float* q_raw, const double* qnorm64, int64_t* oi, float* os,
@@ -1252,6 +1507,8 @@ mmr_status mmr_index_create(const void* gallery, int64_t n, int32_t d, mmr_dtype
     return s;
   };
   hipError_t e;
+  if (hipDeviceGetAttribute(&ix->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ix->n_cu <= 0)
+    ix->n_cu = 256;
   if ((e = hipEventCreateWithFlags(&ix->ws_event, hipEventDisableTiming)) != hipSuccess) {
     ix->ws_event = nullptr;
     mmr::set_error("mmr_index_create: hipEventCreate failed: %s", hipGetErrorString(e));
@@ -1383,13 +1640,40 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
         while (16 * qt < pq) qt *= 2;
         const int64_t Qp = 16 * qt;
         const float* qp = qc + p0 * ix->d;
+        const uint16_t* qh = (const uint16_t*)ix->qn;
+        float* gm = ix->vals;
+        const int64_t ldG = ix->Np / 4;
+        if (pq > 32 && f16_tile_enabled()) {
+          // 33-256 queries: the LDS-staged tile scan (64 / 128 / 256-query tiles), contiguous units
+          const int wq = pq <= 64 ? 1 : pq <= 128 ? 2 : 4;
+          const int64_t Qt = 64 * wq;
+          knn_prep_queries<<<dim3((unsigned)ceil_div(Qt, 4)), dim3(256), 0, st>>>(
+              qp, pq, ix->d, ix->qn, ix->Dp, Qt, ix->qnorm64, 2);
+          MMR_LAUNCH_CHECK();
+          const int64_t n_rt = ix->Np / 16;
+          const char* ce = getenv("MMR_KNN_F16_CFG");  // tile shape (A/B measurements)
+          const int cfg = ce ? atoi(ce) : 0;
+          if (wq == 1) {
+            if (cfg == 1) launch_f16_tile<1, 4, 4, 4, true>(st, ix, qh, gm, ldG, n_rt);
+            else launch_f16_tile<1, 4, 4, 4, false>(st, ix, qh, gm, ldG, n_rt);
+          } else if (wq == 2) {
+            if (cfg == 1) launch_f16_tile<1, 8, 4, 4, true>(st, ix, qh, gm, ldG, n_rt);
+            else launch_f16_tile<2, 4, 4, 4, false>(st, ix, qh, gm, ldG, n_rt);
+          } else {
+            if (cfg == 1) launch_f16_tile<4, 4, 2, 8, true>(st, ix, qh, gm, ldG, n_rt);
+            else if (cfg == 2) launch_f16_tile<2, 8, 2, 8, true>(st, ix, qh, gm, ldG, n_rt);
+            else launch_f16_tile<4, 4, 2, 8, false>(st, ix, qh, gm, ldG, n_rt);
+          }
+          MMR_LAUNCH_CHECK();
+          launch_select<2>(st, pq, gm, ldG, ldG, ix, k, two_delta16, qp, ix->qnorm64, oi + p0 * k,
+                           os ? os + p0 * k : nullptr, os64 ? os64 + p0 * k : nullptr, ost ? ost + p0 : nullptr);
+          MMR_LAUNCH_CHECK();
+          continue;
+        }
         knn_prep_queries<<<dim3((unsigned)ceil_div(Qp, 4)), dim3(256), 0, st>>>(
             qp, pq, ix->d, ix->qn, ix->Dp, Qp, ix->qnorm64, 2);
         MMR_LAUNCH_CHECK();
         const dim3 grid((unsigned)(ix->Np / 64));
-        const uint16_t* qh = (const uint16_t*)ix->qn;
-        float* gm = ix->vals;
-        const int64_t ldG = ix->Np / 4;
         switch (qt) {
           // KC must divide Dp (a multiple of 64): the 128-wide chunk only when Dp % 128 == 0
           case 1:

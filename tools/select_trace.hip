@@ -1,4 +1,4 @@
-// Phase clock of knn_select_groups (block 0): builds csrc/knn.hip with MMR_SELECT_TRACE into a
+// Phase clock of knn_select_t (block 0): builds csrc/knn.hip with MMR_SELECT_TRACE into a
 // standalone binary, runs searches over a 100k x 768 Gaussian gallery and prints per-phase times.
 // build: hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -I include tools/select_trace.hip \
 //          multi-modal-retrieval-predict-project_amd/csrc/capi.cpp -o tools/select_trace.bin
@@ -29,8 +29,8 @@ int main(int argc, char** argv) {
   hipMalloc(&oi, sizeof(int64_t) * Q * K);
   hipMalloc(&os, sizeof(float) * Q * K);
   hipMemcpy(qd, q.data(), sizeof(float) * Q * d, hipMemcpyHostToDevice);
-  const char* names[] = {"A: query row + thread maxima", "B: radix threshold", "C: collect", "E: f64 re-score",
-                         "F: rank + write"};
+  const char* names[] = {"A: query row + thread maxima", "B: radix threshold", "C: collect",
+                         "E+F: f64 re-score + rank", "write"};
   for (int it = 0; it < 6; ++it) {
     if (mmr_index_search(ix, qd, Q, K, oi, os, nullptr, nullptr, nullptr) != MMR_OK) {
       printf("search failed: %s\n", mmr_last_error());
