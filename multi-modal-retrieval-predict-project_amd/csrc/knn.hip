@@ -119,6 +119,37 @@ __global__ __launch_bounds__(256) void knn_prep_queries(const float* __restrict_
     else if (tiled == 1) qn[tile16_index(row, k, Dp)] = v;
     else qn[row * Dp + k] = v;
   };
+  if (tiled == 2 && Dp <= 1024) {
+    // fp16 tile32h: lane owns the 8-half groups g = lane + 64j (j < 2) of the row — 16-B stores
+    // (one (row, 8-half) run is contiguous in tile32h) instead of 2-B scatters; loads unconditional
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    const float* in = q + (row < nq ? row : 0) * (int64_t)d;
+    float v[2][8];
+    double ss = 0.0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = 8 * (lane + 64 * j) + e;
+        const float x = in[k < d ? k : d - 1];
+        v[j][e] = (row < nq && k < d) ? x : 0.0f;
+        ss += (double)v[j][e] * (double)v[j][e];
+      }
+    ss = mmr::wave_sum(ss);
+    const double nrm = sqrt(ss);
+    const float inv = nrm > 0.0 ? (float)(1.0 / nrm) : 0.0f;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k0 = 8 * (lane + 64 * j);
+      if (k0 >= Dp) continue;
+      h8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (_Float16)(v[j][e] * inv);
+      *(h8*)((_Float16*)qn + tile32h_index(row, k0, Dp)) = o;
+    }
+    if (lane == 0) qnorm64[row] = row < nq ? nrm : 0.0;
+    return;
+  }
   if (row >= nq) {
     for (int k = lane; k < Dp; k += 64) put(k, 0.0f);
     return;
@@ -127,11 +158,14 @@ __global__ __launch_bounds__(256) void knn_prep_queries(const float* __restrict_
   double ss = 0.0;
   if (Dp <= 1024) {
     // all loads of the row issued together (a runtime-count loop waits for each load in turn)
+    // unconditional loads (index clamped, value masked): a "load or zero" select makes hipcc branch
+    // around each load and wait for it before the next, 16 serial round trips
     float v[16];
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
       const int k = lane + 64 * c;
-      v[c] = k < d ? in[k] : 0.0f;
+      const float x = in[k < d ? k : d - 1];
+      v[c] = k < d ? x : 0.0f;
     }
 #pragma unroll
     for (int c = 0; c < 16; ++c) ss += (double)v[c] * (double)v[c];
@@ -951,9 +985,10 @@ __device__ __forceinline__ int64_t unit_row(int64_t u, int m) {
   return 4 * u + m;
 }
 
+template <int T>
 struct SelLds {
-  float qrow[kSelThreads];  // raw query row (d <= 1024), first member: 16-B aligned
-  uint32_t tmax[kSelThreads];
+  float qrow[1024];  // raw query row (d <= 1024), first member: 16-B aligned
+  uint32_t tmax[T];
   uint32_t hist[256];
   uint32_t bcast[4];
   int cand_u[kCandCap];
@@ -962,10 +997,60 @@ struct SelLds {
   int row_s[kSlotCap];
   double tmp_d[kMaxK];
   int tmp_r[kMaxK];
+  double qn;
 };
 
-template <int MODE>
-__global__ __launch_bounds__(kSelThreads) void knn_select_t(
+// one 8-bit radix pass over the block's 1024 keys on the digit just below their common prefix
+// (from the block max / min): the smallest key of the digit bin holding the kth largest key — a
+// lower bound of it, resolved to 2^-8 of the keys' spread (a fixed top-down radix spends its first
+// passes on bits every key shares, with all 1024 LDS atomics on one bin)
+template <int T>
+__device__ uint32_t block_kth_lower(uint32_t key, int kth, uint32_t* hist, uint32_t* bcast) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t mx = key, mn = key;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+    mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+  }
+  if (lane == 0) {
+    hist[wave] = mx;
+    hist[32 + wave] = mn;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int nw = T / 64;
+    uint32_t a = lane < nw ? hist[lane] : 0u, b = lane < nw ? hist[32 + lane] : 0xFFFFFFFFu;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      a = max(a, (uint32_t)__shfl_xor((int)a, o, 64));
+      b = min(b, (uint32_t)__shfl_xor((int)b, o, 64));
+    }
+    if (lane == 0) {
+      bcast[0] = a;
+      bcast[1] = b;
+    }
+  }
+  __syncthreads();
+  const uint32_t kmax = bcast[0], diff = kmax ^ bcast[1];
+  __syncthreads();
+  if (diff == 0) return kmax;  // all keys equal (uniform)
+  const int p = 31 - __builtin_clz(diff);
+  const int shift = p > 7 ? p - 7 : 0;
+  const uint32_t prefix = shift + 8 >= 32 ? 0u : kmax & ~((1u << (shift + 8)) - 1u);
+  for (int i = tid; i < 256; i += T) hist[i] = 0;
+  __syncthreads();
+  atomicAdd(&hist[(key >> shift) & 255u], 1u);
+  __syncthreads();
+  pick_digit(hist, (uint32_t)kth, prefix, shift, bcast);
+  __syncthreads();
+  const uint32_t r = bcast[0];
+  __syncthreads();
+  return r;
+}
+
+template <int MODE, int NC, int T>
+__global__ __launch_bounds__(T) void knn_select_t(
     const float* __restrict__ vals, int64_t ldV, int64_t nunits, int64_t n, int k, float two_delta,
     const float* __restrict__ q_raw, int d, const double* __restrict__ qnorm64,
     const float* __restrict__ gal, int Dp, const double* __restrict__ gnorm64, int64_t idx_base,
@@ -973,7 +1058,7 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_t(
     int32_t* __restrict__ status) {
   constexpr int GS = MODE == 0 ? 1 : 4;      // rows per unit
   constexpr int UC = kCandCap / GS;          // units per batch
-  __shared__ __attribute__((aligned(16))) SelLds L;
+  __shared__ __attribute__((aligned(16))) SelLds<T> L;
 
   SEL_MARK(0)
   const int64_t qi = blockIdx.x;
@@ -983,7 +1068,8 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_t(
   int64_t* oi = out_idx + qi * k;
   float* os = out_score ? out_score + qi * k : nullptr;
   double* os64 = out_score64 ? out_score64 + qi * k : nullptr;
-  for (int r = kk + tid; r < k; r += kSelThreads) {
+  (void)qnorm64;
+  for (int r = kk + tid; r < k; r += T) {
     oi[r] = -1;
     if (os) os[r] = -INFINITY;
     if (os64) os64[r] = -INFINITY;
@@ -993,7 +1079,12 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_t(
   // the raw query row (f64 re-score, phase E) is staged in LDS first: its latency hides under
   // phases A-D and it holds no registers meanwhile
   const float* qr = q_raw + qi * (int64_t)d;
-  if (d <= 1024) L.qrow[tid] = tid < d ? qr[tid] : 0.f;
+  if (NC > 0) {
+    for (int e = tid; e < 1024; e += T) {
+      const float x = qr[e < d ? e : d - 1];  // unconditional load (see knn_prep_queries)
+      L.qrow[e] = e < d ? x : 0.f;
+    }
+  }
   const int64_t n4 = nunits >> 2;
   // the first kRegF4 float4 of each thread's strided slice stay in registers for (C): one HBM/L2
   // round trip for rows up to kRegF4 * 4 * 1024 = 32k units, all loads issued together
@@ -1002,24 +1093,26 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_t(
   float m = -INFINITY;
 #pragma unroll
   for (int it = 0; it < kRegF4; ++it) {
-    const int64_t i = tid + (int64_t)it * kSelThreads;
-    cache[it] = i < n4 ? ((const float4*)row)[i] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    // unconditional loads (clamped index, masked value): see knn_prep_queries
+    const int64_t i = tid + (int64_t)it * T;
+    const float4 v = ((const float4*)row)[i < n4 ? i : (n4 > 0 ? n4 - 1 : 0)];
+    cache[it] = i < n4 ? v : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
   }
 #pragma unroll
   for (int it = 0; it < kRegF4; ++it)
     m = fmaxf(m, fmaxf(fmaxf(cache[it].x, cache[it].y), fmaxf(cache[it].z, cache[it].w)));
-  for (int64_t i = tid + (int64_t)kRegF4 * kSelThreads; i < n4; i += kSelThreads) {
+  for (int64_t i = tid + (int64_t)kRegF4 * T; i < n4; i += T) {
     const float4 v = ((const float4*)row)[i];
     m = fmaxf(m, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
   }
-  for (int64_t i = (n4 << 2) + tid; i < nunits; i += kSelThreads) m = fmaxf(m, row[i]);
-  L.tmax[tid] = f2key(m);
-  if (tid == 0) L.bcast[2] = 0;
-  __syncthreads();
+  for (int64_t i = (n4 << 2) + tid; i < nunits; i += T) m = fmaxf(m, row[i]);
+  if (tid == 0) {
+    L.bcast[2] = 0;
+    L.bcast[3] = 0;
+  }
   SEL_MARK(1)
-  // 16-bit prefix (sign, exponent, 7 mantissa bits: 2^-7 relative) of the K-th largest thread max,
-  // clamped to -inf's key (smaller keys are NaN patterns)
-  uint32_t bkey = block_select_kth(L.tmax, kSelThreads, kk, L.hist, L.bcast, 2);
+  // (B) lower bound of the K-th largest thread max, clamped to -inf's key (smaller keys are NaNs)
+  uint32_t bkey = block_kth_lower<T>(f2key(m), kk, L.hist, L.bcast);
   if (bkey < f2key(-INFINITY)) bkey = f2key(-INFINITY);
   float thr = lower_threshold(key2f(bkey), two_delta);
   SEL_MARK(2)
@@ -1035,21 +1128,21 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_t(
     if (cached) {
 #pragma unroll
       for (int it = 0; it < kRegF4; ++it) {
-        const int64_t i = tid + (int64_t)it * kSelThreads;
+        const int64_t i = tid + (int64_t)it * T;
         take(4 * i, cache[it].x, th);
         take(4 * i + 1, cache[it].y, th);
         take(4 * i + 2, cache[it].z, th);
         take(4 * i + 3, cache[it].w, th);
       }
     }
-    for (int64_t i = (lo >> 2) + tid + (cached ? (int64_t)kRegF4 * kSelThreads : 0); i < h4; i += kSelThreads) {
+    for (int64_t i = (lo >> 2) + tid + (cached ? (int64_t)kRegF4 * T : 0); i < h4; i += T) {
       const float4 v = ((const float4*)row)[i];
       take(4 * i, v.x, th);
       take(4 * i + 1, v.y, th);
       take(4 * i + 2, v.z, th);
       take(4 * i + 3, v.w, th);
     }
-    for (int64_t i = (h4 << 2 > lo ? h4 << 2 : lo) + tid; i < hi; i += kSelThreads) take(i, row[i], th);
+    for (int64_t i = (h4 << 2 > lo ? h4 << 2 : lo) + tid; i < hi; i += T) take(i, row[i], th);
     __syncthreads();
     const int c = (int)L.bcast[2];
     __syncthreads();
@@ -1057,43 +1150,66 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_t(
     __syncthreads();  // reset visible before any thread's next take()
     return c;
   };
-  const double qn = qnorm64[qi];
-  // (E)+(F) for the cnt collected units: re-score their rows in f64 into slots [kMaxK, ...), rank
-  // them together with the `carry` carried rows [0, carry), keep the first kk in [0, kk); returns
-  // the number kept
-  auto process = [&](int cnt, int carry) -> int {
+  // |q| in f64 in the gallery norms' order (knn_prep_gallery: lane sums elements lane + 64c over c,
+  // then the xor tree), so a query equal to a gallery row scores exactly 1 whatever the scan path
+  double qn = 0.0;
+  auto query_norm = [&]() {
+    if (wave == 0) {
+      double ss = 0.0;
+      if constexpr (NC > 0) {
+        for (int e = lane; e < 1024; e += 64) ss += (double)L.qrow[e] * (double)L.qrow[e];
+      } else {
+        for (int e = lane; e < Dp; e += 64) {
+          const double x = e < d ? (double)qr[e] : 0.0;
+          ss += x * x;
+        }
+      }
+      ss = mmr::wave_sum(ss);
+      if (lane == 0) L.qn = sqrt(ss);
+    }
+  };
+  // (E) re-score the rows of cnt collected units in f64 into slots [kMaxK, ...)
+  auto rescore = [&](int cnt) -> int {
     const int nslot = GS * cnt;
-    for (int s = tid; s < nslot; s += kSelThreads) {
+    for (int s = tid; s < nslot; s += T) {
       const int64_t g = unit_row<MODE>(L.cand_u[s / GS], s % GS);
       L.row_s[kMaxK + s] = (int)(g < n ? g : n);
     }
     __syncthreads();
-    if (d <= 1024) {
-      // latency-bound: each wave issues the float4 loads of RB rows before reducing any of them
-      // (RB = 3 spills at the 128-VGPR budget of 1024 threads); the query row from LDS
-      // (lane owns elements 4(64c + lane) .. +3)
-      constexpr int RB = 2;
-      for (int s0 = wave * RB; s0 < nslot; s0 += (kSelThreads / 64) * RB) {
-        float4 gv[RB][4];
+    qn = L.qn;
+    SEL_MARK(8)
+    if constexpr (NC > 0) {
+      // latency-bound: each wave issues the float4 loads of its RB rows (NC 256-float chunks each)
+      // before reducing any of them, so up to 16*RB rows (48 at Dp = 768: a usual 11-unit candidate
+      // set) take one round trip; the query row from LDS (lane owns elements 4(64c + lane) .. +3)
+      constexpr int RB = NC <= 2 ? 4 : NC == 3 ? 3 : 2;  // (a 256-thread variant with 8-12 rows per wave: 2x slower)
+      for (int s0 = wave * RB; s0 < nslot; s0 += (T / 64) * RB) {
+        float4 gv[RB][NC];
         double gnr[RB];  // row norms loaded with the rows (not after the reduction: one round trip)
         int64_t gir[RB];
+        // every load unconditional (a "load or zero" select makes hipcc branch around each load and
+        // wait for it before the next — 9 serial round trips, measured 5 us of the 12 us select):
+        // padding slots read row 0 (score discarded), lanes past Dp re-read the row's last float4
+        // (their query elements in LDS are 0, so the product is 0)
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
           const int s = s0 + r;
           const int64_t gi = s < nslot ? L.row_s[kMaxK + s] : n;
           gir[r] = gi;
-          gnr[r] = gi < n ? gnorm64[gi] : 0.0;
-          // one row pointer (padding slots read row 0; their score is discarded below)
-          const float* gr = gal + (gi < n ? gi : 0) * Dp + lane * 4;
+          const int64_t gl = gi < n ? gi : 0;
+          gnr[r] = gnorm64[gl];
+          const float* gr = gal + gl * Dp;
 #pragma unroll
-          for (int c = 0; c < 4; ++c)
-            gv[r][c] = (c * 256 + lane * 4 < Dp) ? *(const float4*)(gr + c * 256) : make_float4(0.f, 0.f, 0.f, 0.f);
+          for (int c = 0; c < NC; ++c) {
+            const int e = c * 256 + lane * 4;
+            gv[r][c] = *(const float4*)(gr + (e < Dp ? e : Dp - 4));
+          }
         }
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
           double acc = 0.0;
 #pragma unroll
-          for (int c = 0; c < 4; ++c) {
+          for (int c = 0; c < NC; ++c) {
             const float4 qv = *(const float4*)(L.qrow + (c * 64 + lane) * 4);
             acc += (double)qv.x * gv[r][c].x + (double)qv.y * gv[r][c].y + (double)qv.z * gv[r][c].z +
                    (double)qv.w * gv[r][c].w;
@@ -1107,7 +1223,7 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_t(
         }
       }
     } else {
-      for (int s = wave; s < nslot; s += kSelThreads / 64) {
+      for (int s = wave; s < nslot; s += T / 64) {
         const int64_t gi = L.row_s[kMaxK + s];
         double sc = -INFINITY;
         if (gi < n) {
@@ -1121,61 +1237,81 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_t(
         if (lane == 0) L.cand_d[kMaxK + s] = sc;
       }
     }
-    // (F) rank: the m^2 (slot, other) comparisons spread over all threads, ranks counted in LDS (a
-    // per-slot serial loop over the slots took ~5 us at 44 slots)
+    SEL_MARK(9)
+    return nslot;
+  };
+  // (F) rank the carried rows [0, carry) with the re-scored slots [kMaxK, +nslot): the m^2 (slot,
+  // other) comparisons spread over all threads, ranks counted in LDS; `direct` writes the first kk
+  // to the outputs, else they become the new carried top-K in [0, kk)
+  auto rank = [&](int carry, int nslot, bool direct) -> int {
     const int mtot = carry + nslot;
     auto slot = [&](int u) { return u < carry ? u : kMaxK + u - carry; };
-    for (int u = tid; u < mtot; u += kSelThreads) L.rank_s[slot(u)] = 0;
+    for (int u = tid; u < mtot; u += T) L.rank_s[slot(u)] = 0;
     __syncthreads();
     const int npair = mtot * mtot;
-    for (int p = tid; p < npair; p += kSelThreads) {
+    for (int p = tid; p < npair; p += T) {
       const int a = slot(p / mtot), b = slot(p % mtot);
       const double sa = L.cand_d[a], sb = L.cand_d[b];
       if ((sb > sa) || (sb == sa && L.row_s[b] < L.row_s[a])) atomicAdd(&L.rank_s[a], 1);
     }
     __syncthreads();
-    for (int u = tid; u < mtot; u += kSelThreads) {
+    for (int u = tid; u < mtot; u += T) {
       const int sl = slot(u);
-      const int rank = L.rank_s[sl];
-      if (L.cand_d[sl] == -INFINITY || rank >= kk) continue;
-      L.tmp_d[rank] = L.cand_d[sl];
-      L.tmp_r[rank] = L.row_s[sl];
-      atomicAdd(&L.bcast[3], 1u);
+      const int rk = L.rank_s[sl];
+      const double sc = L.cand_d[sl];
+      if (sc == -INFINITY || rk >= kk) continue;
+      if (direct) {
+        oi[rk] = (int64_t)L.row_s[sl] + idx_base;
+        if (os) os[rk] = (float)sc;
+        if (os64) os64[rk] = sc;
+      } else {
+        L.tmp_d[rk] = sc;
+        L.tmp_r[rk] = L.row_s[sl];
+        atomicAdd(&L.bcast[3], 1u);
+      }
     }
+    if (direct) return kk;
     __syncthreads();
     const int kept = (int)L.bcast[3];
-    for (int r = tid; r < kept; r += kSelThreads) {
+    for (int r = tid; r < kept; r += T) {
       L.cand_d[r] = L.tmp_d[r];
       L.row_s[r] = L.tmp_r[r];
     }
     __syncthreads();
     if (tid == 0) L.bcast[3] = 0;
+    __syncthreads();
     return kept;
   };
-  if (tid == 0) L.bcast[3] = 0;
   int cnt = collect(thr, true, 0, nunits);
+  query_norm();  // read after rescore's first barrier
   SEL_MARK(3)
-  int kept = 0;
   if (cnt > UC) {
     const float t = key2f(row_select_kth(row, nunits, kk, L.hist, L.bcast));
     thr = lower_threshold(t, two_delta);
     cnt = collect(thr, false, 0, nunits);
-    if (cnt > UC) {
-      // massive near-ties: batches of UC units in position order (a batch cannot overflow), each
-      // merged into the carried exact top-K
-      for (int64_t lo = 0; lo < nunits; lo += UC) {
-        const int c = collect(thr, false, lo, lo + UC < nunits ? lo + UC : nunits);
-        if (c > 0) kept = process(c, kept);
-      }
-      cnt = -1;
-    }
   }
-  if (cnt >= 0) kept = process(cnt, 0);
-  SEL_MARK(4)
-  for (int r = tid; r < kept; r += kSelThreads) {
-    oi[r] = (int64_t)L.row_s[r] + idx_base;
-    if (os) os[r] = (float)L.cand_d[r];
-    if (os64) os64[r] = L.cand_d[r];
+  if (cnt <= UC) {
+    const int ns = rescore(cnt);
+    __syncthreads();
+    SEL_MARK(4)
+    rank(0, ns, true);
+  } else {
+    // massive near-ties: batches of UC units in position order (a batch cannot overflow), each
+    // merged into the carried exact top-K
+    int kept = 0;
+    for (int64_t lo = 0; lo < nunits; lo += UC) {
+      const int c = collect(thr, false, lo, lo + UC < nunits ? lo + UC : nunits);
+      if (c == 0) continue;
+      const int ns = rescore(c);
+      __syncthreads();
+      kept = rank(kept, ns, false);
+    }
+    SEL_MARK(4)
+    for (int r = tid; r < kept; r += T) {
+      oi[r] = (int64_t)L.row_s[r] + idx_base;
+      if (os) os[r] = (float)L.cand_d[r];
+      if (os64) os64[r] = L.cand_d[r];
+    }
   }
   SEL_MARK(5)
 #ifdef MMR_SELECT_TRACE
@@ -1471,9 +1607,20 @@ template <int MODE>
 void launch_select(hipStream_t st, int64_t nq, const float* vals, int64_t ldV, int64_t nunits, const mmr_index* ix,
                    int k, float two_delta, const float* q_raw, const double* qnorm64, int64_t* oi, float* os,
                    double* os64, int32_t* ost) {
-  knn_select_t<MODE><<<dim3((unsigned)nq), dim3(kSelThreads), 0, st>>>(
-      vals, ldV, nunits, ix->n, k, two_delta, q_raw, ix->d, qnorm64, ix->gal, ix->Dp, ix->norm64, ix->idx_base,
-      oi, os, os64, ost);
+  const dim3 g((unsigned)nq), b(kSelThreads);
+#define MMR_SEL(NC)                                                                                              \
+  knn_select_t<MODE, NC, kSelThreads><<<g, b, 0, st>>>(vals, ldV, nunits, ix->n, k, two_delta, q_raw, ix->d,     \
+                                                       qnorm64, ix->gal, ix->Dp, ix->norm64, ix->idx_base, oi, os, \
+                                                       os64, ost)
+  // NC = 256-float chunks of a row in the f64 re-score (0: d > 1024, strided loop)
+  switch (ix->d > 1024 ? 0 : (int)ceil_div(ix->Dp, 256)) {
+    case 1: MMR_SEL(1); break;
+    case 2: MMR_SEL(2); break;
+    case 3: MMR_SEL(3); break;
+    case 4: MMR_SEL(4); break;
+    default: MMR_SEL(0); break;
+  }
+#undef MMR_SEL
 }
 
 }  // namespace

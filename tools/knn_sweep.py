@@ -39,17 +39,16 @@ def main():
         times = {v: [] for v in a.variants.split(",")}
         for _ in range(a.rounds):
             for v in times:
-                ix.set_mode("x3" if v == "x3" else "f16")
+                ix.set_mode("x3" if v.startswith("x3") else "f16")
                 os.environ["MMR_KNN_F16_TILE"] = "0" if v == "f16_stream" else "1"
-                os.environ["MMR_KNN_F16_TILE_DBG"] = {"f16_noB": "1", "f16_noA": "2"}.get(v, "0")
-                os.environ["MMR_KNN_F16_CFG"] = v[5:] if v.startswith("f16_c") else "0"
+                os.environ["MMR_KNN_F16_CFG"] = v[5:6] if v.startswith("f16_c") else "0"
                 for _ in range(3):
                     i, s, stt = ix.search(Q, a.k, want_status=True)
                 torch.cuda.synchronize()
                 check_status(stt)
                 if ref is None:
                     ref = i.clone()
-                elif not v.startswith("f16_no") and not torch.equal(ref, i):
+                elif not torch.equal(ref, i):
                     raise SystemExit(f"variant {v} Q={q}: lists differ from the first variant")
                 evs = []
                 for _ in range(a.reps):
@@ -63,10 +62,10 @@ def main():
         for v, ts in times.items():
             ts.sort()
             us = ts[len(ts) // 2]
-            gb = 2 if v != "x3" else 4
+            gb = 4 if v.startswith("x3") else 2
             byts = a.n * a.d * gb + a.n * 4 + q * a.d * 4 + q * a.k * 12
-            fl = 2.0 * q * a.n * a.d * (1 if v != "x3" else 3)
-            bound = max(byts / 8e12, fl / 2.5e15 if not (v == "x3" and q <= 32) else 0.0)
+            fl = 2.0 * q * a.n * a.d * (3 if v.startswith("x3") else 1)
+            bound = max(byts / 8e12, fl / 2.5e15 if not (v.startswith("x3") and q <= 32) else 0.0)
             res[(v, q)] = us
             print(json.dumps({"variant": v, "q": q, "n": a.n, "d": a.d, "k": a.k, "us_median": round(us, 2),
                               "us_min": round(ts[0], 2), "bound_us": round(bound * 1e6, 2),

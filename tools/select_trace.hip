@@ -10,7 +10,7 @@
 
 int main(int argc, char** argv) {
   const int Q = argc > 1 ? atoi(argv[1]) : 16, mode = argc > 2 ? atoi(argv[2]) : 2;
-  const int64_t n = 100000;
+  const int64_t n = argc > 3 ? atoll(argv[3]) : 100000;
   const int d = 768, K = 10;
   std::vector<float> g((size_t)n * d), q((size_t)Q * d);
   std::mt19937 rng(7);
@@ -40,8 +40,9 @@ int main(int argc, char** argv) {
     long long t[16];
     hipMemcpyFromSymbol(t, HIP_SYMBOL(g_sel_trace), sizeof(t));
     if (it < 2) continue;
-    printf("Q=%d mode=%d run %d: groups collected %lld, total %.2f us |", Q, mode, it, t[6], (t[5] - t[0]) * 0.01);
+    printf("n=%lld Q=%d mode=%d run %d: groups collected %lld, total %.2f us |", (long long)n, Q, mode, it, t[6], (t[5] - t[0]) * 0.01);
     for (int p = 0; p < 5; ++p) printf(" %s %.2f |", names[p], (t[p + 1] - t[p]) * 0.01);
+    printf(" [E: fill %.2f, loads+math (block 0, wave 0) %.2f]", (t[8] - t[3]) * 0.01, (t[9] - t[8]) * 0.01);
     printf("\n");
   }
   mmr_index_destroy(ix);
