@@ -33,6 +33,12 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
 
 // two f32 -> packed bf16x2 (RNE) in one v_cvt_pk_bf16_f32
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+// Pins a loaded value as used on every path: without it hipcc sinks a load whose value is later
+// masked into the branch that consumes it, and then waits on each such load before issuing the next.
+template <class T>
+__device__ __forceinline__ void pin(T& v) {
+  asm volatile("" : "+v"(v));
+}
 __device__ __forceinline__ uint32_t pack2bf(float a, float b) {
   const bf16x2_t v = {(__bf16)a, (__bf16)b};
   return __builtin_bit_cast(uint32_t, v);

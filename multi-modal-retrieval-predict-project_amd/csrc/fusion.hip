@@ -362,18 +362,30 @@ __global__ __launch_bounds__(256) void ln_rows(const TI* __restrict__ x, int64_t
     else return bf2f(((const uint16_t*)p)[i]);
   };
   const float av = a ? *a : 1.f;
-  float v[16];
-  float s = 0.f;
+  // all loads unconditional and issued before any use (index clamped, value masked): a "load if
+  // ch < c" branch makes hipcc wait for each load before the next — 16-32 serial round trips
+  float v[16], rv[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int ch = lane + 64 * i;
-    v[i] = 0.f;
-    if (ch < c) {
-      float t = av * ld(x, row * ldx + ch);
-      if (r) t += ld(r, row * ldr + ch);
-      v[i] = t;
-      s += t;
+    v[i] = ld(x, row * ldx + (ch < c ? ch : c - 1));
+  }
+  if (r) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int ch = lane + 64 * i;
+      rv[i] = ld(r, row * ldr + (ch < c ? ch : c - 1));
     }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) rv[i] = 0.f;
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const float t = av * v[i] + rv[i];
+    v[i] = lane + 64 * i < c ? t : 0.f;
+    s += v[i];
   }
   const float mean = mmr::wave_sum(s) / c;
   float ss = 0.f;
@@ -382,12 +394,28 @@ __global__ __launch_bounds__(256) void ln_rows(const TI* __restrict__ x, int64_t
     if (lane + 64 * i < c) ss += (v[i] - mean) * (v[i] - mean);
   const float rstd = rsqrtf(mmr::wave_sum(ss) / c + eps);
   const float pv = ps ? *ps : 1.f;
+  float gv[16], bv[16], pp[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int ch = lane + 64 * i, chc = ch < c ? ch : c - 1;
+    gv[i] = g[chc];
+    bv[i] = b[chc];
+  }
+  if (post) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int ch = lane + 64 * i;
+      pp[i] = pv * post[row * ldp + (ch < c ? ch : c - 1)];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) pp[i] = 0.f;
+  }
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int ch = lane + 64 * i;
+    const float t = (v[i] - mean) * rstd * gv[i] + bv[i] + pp[i];
     if (ch < c) {
-      float t = (v[i] - mean) * rstd * g[ch] + b[ch];
-      if (post) t += pv * post[row * ldp + ch];
       if constexpr (sizeof(TO) == 4) ((float*)y)[row * ldy + ch] = t;
       else ((uint16_t*)y)[row * ldy + ch] = f2bf(t);
     }

@@ -19,6 +19,7 @@ using mmr::f2bf;
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef short bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void load8(const uint16_t* p, float* v) {
   bf16x8 x = *(const bf16x8*)p;
@@ -51,25 +52,50 @@ __global__ __launch_bounds__(256) void layernorm_bf16(const uint16_t* __restrict
   const uint16_t* xr = x + (ok ? row : 0) * c;
   const int nch = c / 8;
   const float av = alpha ? *alpha : 1.f;  // learned scale of x (PreFusionEnhancer alpha, fusion.py:34)
+  // every load unconditional (chunk index clamped, value masked): a "load if in range" branch makes
+  // hipcc wait for each chunk's load before issuing the next — NC (x2 with ADD) serial round trips
+  bf16x8 xa[NC], ra[NC];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int ch = sub + i * LPR;
+    const int chc = ch < nch ? ch : nch - 1;
+    xa[i] = *(const bf16x8*)(xr + chc * 8);
+    if (ADD) ra[i] = *(const bf16x8*)(r + (ok ? row : 0) * c + chc * 8);
+  }
+  f32x4 ga[NC][2], ba[NC][2];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int ch = sub + i * LPR;
+    const int chc = ch < nch ? ch : nch - 1;
+    ga[i][0] = *(const f32x4*)(g + chc * 8);
+    ga[i][1] = *(const f32x4*)(g + chc * 8 + 4);
+    ba[i][0] = *(const f32x4*)(b + chc * 8);
+    ba[i][1] = *(const f32x4*)(b + chc * 8 + 4);
+  }
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    mmr::pin(xa[i]);
+    if (ADD) mmr::pin(ra[i]);
+  }
   float v[NC][8];
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < NC; ++i) {
     const int ch = sub + i * LPR;
-    if (ok && ch < nch) {
-      load8(xr + ch * 8, v[i]);
-      if (alpha) {
+    const bool in = ok && ch < nch;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[i][j] *= av;
-      }
-      if (ADD) {  // post-LN residual: LN(x + r), the sum kept in f32
-        float w[8];
-        load8(r + (ok ? row : 0) * c + ch * 8, w);
+    for (int j = 0; j < 8; ++j) v[i][j] = bf2f((uint16_t)xa[i][j]);
+    if (ADD) {  // post-LN residual: LN(x + r), the sum kept in f32
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[i][j] += w[j];
-      }
+      for (int j = 0; j < 8; ++j) v[i][j] = fmaf(v[i][j], av, bf2f((uint16_t)ra[i][j]));
+    } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += v[i][j];
+      for (int j = 0; j < 8; ++j) v[i][j] *= av;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[i][j] = in ? v[i][j] : 0.f;
+      s += v[i][j];
     }
   }
 #pragma unroll
@@ -90,15 +116,16 @@ __global__ __launch_bounds__(256) void layernorm_bf16(const uint16_t* __restrict
 #pragma unroll
   for (int i = 0; i < NC; ++i) {
     const int ch = sub + i * LPR;
-    if (ok && ch < nch) {
-      const float4 g0 = *(const float4*)(g + ch * 8), g1 = *(const float4*)(g + ch * 8 + 4);
-      const float4 b0 = *(const float4*)(b + ch * 8), b1 = *(const float4*)(b + ch * 8 + 4);
-      const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
-      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    mmr::pin(ga[i][0]);
+    mmr::pin(ga[i][1]);
+    mmr::pin(ba[i][0]);
+    mmr::pin(ba[i][1]);
+    const f32x4 g0 = ga[i][0], g1 = ga[i][1], b0 = ba[i][0], b1 = ba[i][1];
+    const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[i][j] = (v[i][j] - mean) * rstd * gg[j] + bb[j];
-      store8(y + row * c + ch * 8, v[i]);
-    }
+    for (int j = 0; j < 8; ++j) v[i][j] = (v[i][j] - mean) * rstd * gg[j] + bb[j];
+    if (ok && ch < nch) store8(y + row * c + ch * 8, v[i]);
   }
 }
 
@@ -406,15 +433,35 @@ __global__ __launch_bounds__(256) void patch_merge_ln(const uint16_t* __restrict
   if (c4 <= 2048) {
     // the 4c-wide merged row in registers (<= 4 chunks of 8 per lane), every load issued at once:
     // one memory round trip instead of three passes that each wait on their loads
+    // (loads unconditional — chunk clamped, value masked: a "load if k < 4c" branch makes hipcc
+    // wait for each load before issuing the next)
+    bf16x8 xa[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int k = lane * 8 + 512 * it;
+      xa[it] = *(const bf16x8*)src(k < c4 ? k : c4 - 8);
+    }
+    f32x4 ga[4][2], ba[4][2];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int k = lane * 8 + 512 * it, kc = k < c4 ? k : c4 - 8;
+      ga[it][0] = *(const f32x4*)(g + kc);
+      ga[it][1] = *(const f32x4*)(g + kc + 4);
+      ba[it][0] = *(const f32x4*)(b + kc);
+      ba[it][1] = *(const f32x4*)(b + kc + 4);
+    }
+#pragma unroll
+    for (int it = 0; it < 4; ++it) mmr::pin(xa[it]);
     float v[4][8];
     float s = 0.f;
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int k = lane * 8 + 512 * it;
-      if (k < c4) {
-        load8(src(k), v[it]);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) s += v[it][e];
+      for (int e = 0; e < 8; ++e) {
+        v[it][e] = bf2f((uint16_t)xa[it][e]);
+        v[it][e] = k < c4 ? v[it][e] : 0.f;
+        s += v[it][e];
       }
     }
     const float mean = mmr::wave_sum(s) / c4;
@@ -429,11 +476,16 @@ __global__ __launch_bounds__(256) void patch_merge_ln(const uint16_t* __restrict
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int k = lane * 8 + 512 * it;
-      if (k < c4) {
+      mmr::pin(ga[it][0]);
+      mmr::pin(ga[it][1]);
+      mmr::pin(ba[it][0]);
+      mmr::pin(ba[it][1]);
+      const f32x4 g0 = ga[it][0], g1 = ga[it][1], b0 = ba[it][0], b1 = ba[it][1];
+      const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[it][e] = (v[it][e] - mean) * rstd * g[k + e] + b[k + e];
-        store8(y + o * c4 + k, v[it]);
-      }
+      for (int e = 0; e < 8; ++e) v[it][e] = (v[it][e] - mean) * rstd * gg[e] + bb[e];
+      if (k < c4) store8(y + o * c4 + k, v[it]);
     }
     return;
   }
@@ -479,19 +531,26 @@ __global__ __launch_bounds__(64 * SH_WAVES) void swin_head(const uint16_t* __res
   const int bi = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int per = c / 64;
-  float acc1[SH_MAXPL], acc2[SH_MAXPL];
+  float acc1[SH_MAXPL], acc2[SH_MAXPL], gk[SH_MAXPL], bk[SH_MAXPL];
+  // every load unconditional (index clamped, value masked; a "load if e < per" branch makes hipcc wait
+  // for each load before the next), the LN parameters loaded once for all tokens
 #pragma unroll
-  for (int e = 0; e < SH_MAXPL; ++e) acc1[e] = acc2[e] = 0.f;
+  for (int e = 0; e < SH_MAXPL; ++e) {
+    acc1[e] = acc2[e] = 0.f;
+    const int k = lane + 64 * (e < per ? e : per - 1);
+    gk[e] = g[k];
+    bk[e] = b[k];
+  }
   for (int tk = wave; tk < t; tk += SH_WAVES) {
     const uint16_t* xr = x + ((int64_t)bi * t + tk) * c;
     float v[SH_MAXPL];
     float s = 0.f;
 #pragma unroll
-    for (int e = 0; e < SH_MAXPL; ++e)
-      if (e < per) {
-        v[e] = bf2f(xr[lane + 64 * e]);
-        s += v[e];
-      }
+    for (int e = 0; e < SH_MAXPL; ++e) {
+      const float xv = bf2f(xr[lane + 64 * (e < per ? e : per - 1)]);
+      v[e] = e < per ? xv : 0.f;
+      s += v[e];
+    }
     float mean = mmr::wave_sum(s) / c, ss = 0.f;
 #pragma unroll
     for (int e = 0; e < SH_MAXPL; ++e)
@@ -501,8 +560,7 @@ __global__ __launch_bounds__(64 * SH_WAVES) void swin_head(const uint16_t* __res
 #pragma unroll
     for (int e = 0; e < SH_MAXPL; ++e)
       if (e < per) {
-        const int k = lane + 64 * e;
-        v[e] = (v[e] - mean) * rstd * g[k] + b[k];  // once-normed token (forward_features output)
+        v[e] = (v[e] - mean) * rstd * gk[e] + bk[e];  // once-normed token (forward_features output)
         acc1[e] += v[e];
         s += v[e];
       }
@@ -516,7 +574,7 @@ __global__ __launch_bounds__(64 * SH_WAVES) void swin_head(const uint16_t* __res
     for (int e = 0; e < SH_MAXPL; ++e)
       if (e < per) {
         const int k = lane + 64 * e;
-        const float p2 = (v[e] - mean) * rstd * g[k] + b[k];  // swin_norm applied again
+        const float p2 = (v[e] - mean) * rstd * gk[e] + bk[e];  // swin_norm applied again
         acc2[e] += p2;
         if (patches) patches[((int64_t)bi * t + tk) * c + k] = p2;
       }
