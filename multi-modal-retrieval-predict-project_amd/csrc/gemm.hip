@@ -214,9 +214,22 @@ __device__ __forceinline__ void big_epilogue(f32x4 (&acc)[MT][NT], uint16_t* dsm
         const int c = it * 64 + lane;
         const int64_t m = m0 + wm * MT * 16 + hh * ROWS + c / CPR;
         const int n = n0 + wn * NT * 16 + (c % CPR) * 8;
-        if (c >= ROWS * CPR) continue;
-        rres[hh][it] = (m < M && n < N) ? *(const bf16x8*)(R + m * N + n) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+        // unconditional (clamped; out-of-range values are never stored): a "load or zero" makes hipcc
+        // wait for each residual load before issuing the next
+        const int64_t mc = m < M ? m : M - 1;
+        const int nc = n < N ? n : N - 8;
+        rres[hh][it] = *(const bf16x8*)(R + mc * N + nc);
       }
+#pragma unroll
+    for (int hh = 0; hh < HALVES; ++hh)
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) mmr::pin(rres[hh][it]);
+  }
+  f32x4 bvs[NT];  // bias of the wave's columns, all loads issued at once
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int n = n0 + wn * NT * 16 + j * 16 + fq * 4;
+    bvs[j] = HAS_BIAS ? *(const f32x4*)(bias + (n < N ? n : N - 4)) : (f32x4){0.f, 0.f, 0.f, 0.f};
   }
   if constexpr (SYNC) __syncthreads();
   uint16_t* et = dsm + wave * ROWS * EPI_LD;
@@ -226,10 +239,8 @@ __device__ __forceinline__ void big_epilogue(f32x4 (&acc)[MT][NT], uint16_t* dsm
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       const int nl = j * 16 + fq * 4;
-      const int n = n0 + wn * NT * 16 + nl;
-      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (HAS_BIAS && n < N) bv = *(const float4*)(bias + n);
-      const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
+      const f32x4 bv = bvs[j];
+      const float bb[4] = {bv[0], bv[1], bv[2], bv[3]};
 #pragma unroll
       for (int i4 = 0; i4 < MPH; ++i4) {
         float v[4];
@@ -246,14 +257,23 @@ __device__ __forceinline__ void big_epilogue(f32x4 (&acc)[MT][NT], uint16_t* dsm
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_wave_barrier();
+    // all LDS reads of the round first (unconditional; a read under the store's range test makes
+    // hipcc wait for each one before the next), then the guarded stores
+    bf16x8 vv[NIT];
 #pragma unroll
-    for (int it = 0; it < (ROWS * CPR + 63) / 64; ++it) {
+    for (int it = 0; it < NIT; ++it) {
+      const int c = it * 64 + lane;
+      const int rl = c / CPR < ROWS ? c / CPR : ROWS - 1, cc = (c % CPR) * 8;
+      vv[it] = *(const bf16x8*)(et + rl * EPI_LD + cc);
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
       const int c = it * 64 + lane;
       const int rl = c / CPR, cc = (c % CPR) * 8;
       const int64_t m = m0 + wm * MT * 16 + hh * ROWS + rl;
       const int n = n0 + wn * NT * 16 + cc;
       if (c >= ROWS * CPR || m >= M || n >= N) continue;
-      bf16x8 v = *(const bf16x8*)(et + rl * EPI_LD + cc);
+      bf16x8 v = vv[it];
       if (HAS_RES) {
         const bf16x8 rr = rres[HAS_RES ? hh : 0][HAS_RES ? it : 0];
         uint32_t o[4];
@@ -427,6 +447,336 @@ __global__ __launch_bounds__(512, 2 * OCC) void gemm_bf16_tn_big(const uint16_t*
   big_epilogue<MT, NT, ACT, HAS_BIAS, HAS_RES>(acc, dsm, bias, R, Y, M, N, m0, n0, wm, wn, wave, lane);
 }
 
+
+// ---------------------------------------------------------------- 8-phase persistent 256 x 64NT GEMM
+// cdna_hip_programming.md §5 "256² 8-phase template" (T1-T5), re-derived for nn.Linear operands and
+// made persistent: 8 waves = 2 (M) x 4 (N), wave tile 128 x 16NT (NT = 4: 256 x 256, NT = 3:
+// 256 x 192), BK = 64, two LDS K-tile buffers E / O (even / odd K-tile), each [A 256 x 64 | B 64NT x
+// 64] bf16, source-swizzled glds pieces (one wave instruction = 8 rows x 128 B; piece j of an
+// operand = its rows 64j..64j+63).
+// A K-tile is 4 phases; phase q computes one quadrant of the wave tile (m-half x n-half, both
+// k-steps) from fragments read in the phase's load segment:
+//   q0: read A[mh0], B[nh0] -> MFMA (mh0, nh0)      q1: read B[nh1] -> MFMA (mh0, nh1)
+//   q2: read A[mh1] -> MFMA (mh1, nh1)              q3: -> MFMA (mh1, nh0)
+// Each phase = load segment | s_barrier | MFMA segment | s_barrier; waves 4-7 (m-group 1) run one
+// barrier behind waves 0-3, so on every SIMD one wave's MFMA segment overlaps its partner's
+// LDS-read / glds segment (MI355X_MICROARCH.md "Two waves per SIMD").
+// glds schedule by segment s = 0..15 of an iteration (2 K-tiles; s = 2p load, 2p+1 MFMA segment
+// of phase p), each region re-staged only after every reader retired it (a barrier after the later
+// group's lgkmcnt):  E.A0 s2, E.A2 s3, E.B0 s5, E.B1+E.A1 s6, E.B2+E.A3 s7, E.B3 s8, and the same
+// + 8 for O.  Waits: vmcnt(5) at the end of s6 (O complete before group 0 reads it at s8) and s14
+// (E before s16): 5 younger pieces stay in flight across each wait.
+// Persistent: one workgroup per CU walks its XCD's tiles (consecutive tiles share the X panel in
+// that XCD's L2).  The K-tile stream runs on across tiles — the last iteration of a tile loads the
+// next tile's K-tiles 0 and 1 — so there is no per-tile prologue burst; the epilogue (bias / GELU /
+// residual in f32 -> bf16 -> 16-B row stores) stages through a per-wave LDS area outside E / O
+// while those loads are in flight, and the first wait of the next tile counts its stores out
+// (vmcnt(5 + NSTORE)) instead of draining them.  M % 256 == 0 (launcher): every store is issued, so
+// the count is exact.
+// LDS store the compiler does not track: hipcc waits vmcnt(0) before a ds_write that may alias an
+// in-flight LDS-DMA, which would drain the next tile's operand loads at the start of every epilogue
+__device__ __forceinline__ void ds_write_b64_untracked(const void* p, uint32_t lo, uint32_t hi) {
+  const uint32_t a = (uint32_t)(uintptr_t)p;
+  const unsigned long long d = ((unsigned long long)hi << 32) | lo;
+  asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(d) : "memory");
+}
+
+template <int NT>
+struct P8 {
+  static constexpr int TBN = 64 * NT;
+  static constexpr int RM = NT == 3 ? 2 : 1;           // m-tiles per epilogue round
+  static constexpr int ELD = 16 * NT + 8;              // bf16 row stride of the epilogue area
+  static constexpr int CPL = 16 * RM * 2 * NT / 64;    // 16-B chunks per lane per round
+  static constexpr int NSTORE = (8 / RM) * CPL;        // global stores per wave per tile
+  static constexpr size_t BUF_B = (size_t)(256 + TBN) * 64 * 2;
+  static constexpr size_t EPI_B = 8ull * 16 * RM * ELD * 2;
+  static constexpr size_t LDS_B = 2 * BUF_B + EPI_B + 2 * TBN * 4;
+};
+
+template <int NT, int ACT, bool HAS_BIAS, bool HAS_RES>
+__global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restrict__ X,
+                                                       const uint16_t* __restrict__ W,
+                                                       const float* __restrict__ bias,
+                                                       const uint16_t* __restrict__ R,
+                                                       uint16_t* __restrict__ Y, int64_t M, int N,
+                                                       int K, int tiles_m, int tiles_n) {
+#if defined(__HIP_DEVICE_COMPILE__)  // buffer-descriptor builtins exist in the device pass only
+  using C = P8<NT>;
+  constexpr int KB = 64, TBN = C::TBN;
+  constexpr int TA = 256 * KB, BUF = (256 + TBN) * KB;  // bf16 elements: A part, whole buffer
+  constexpr int NH0 = NT / 2;                           // n-tiles in n-half 0
+  static_assert(C::NSTORE + 5 <= 63, "vmcnt range");
+  extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
+
+  const int ntiles = tiles_m * tiles_n;
+  const int per = gridDim.x / 8, xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
+  const int lo = (int)((int64_t)ntiles * xcd / 8), hi = (int)((int64_t)ntiles * (xcd + 1) / 8);
+  int t = lo + slot;
+  if (t >= hi) return;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably uniform: SGPR LDS bases
+  const int wr = wave >> 2, wc = wave & 3;  // m-group (stagger group), n position
+  const int fr = lane & 15, fq = lane >> 4;
+  uint16_t* et = dsm + 2 * BUF + wave * 16 * C::RM * C::ELD;         // this wave's epilogue area
+  float* lbias = (float*)(dsm + 2 * BUF + 8 * 16 * C::RM * C::ELD);  // [2][TBN] f32, by tile parity
+  // bias of a tile -> LDS by one LDS-DMA from wave 0: the first tile's in the prologue, each next
+  // tile's at the end of wave 0's epilogue (the other parity; no registers live across the loop)
+  auto bias_dma = [&](int tile, int par) {
+    if (HAS_BIAS && wave == 0 && lane < TBN / 4)
+      __builtin_amdgcn_global_load_lds((const void*)(bias + (tile % tiles_n) * TBN + lane * 4),
+                                       (lds_ptr_t)(lbias + par * TBN), 16, 0, 0);
+  };
+
+  // glds: piece j of an operand stages LDS rows 64j + 8 wave + lane/8, physical chunk lane%8 <-
+  // logical chunk swz(row, lane%8); per-lane byte offsets are tile-independent, a tile contributes
+  // uniform bases only
+  const int prow = lane >> 3, pch = lane & 7;
+  uint32_t offA[4], offB[NT];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = 64 * j + 8 * wave + prow;
+    offA[j] = (uint32_t)((row * K + swz(row, pch) * 8) * 2);
+  }
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int row = 64 * j + 8 * wave + prow;
+    offB[j] = (uint32_t)((row * K + swz(row, pch) * 8) * 2);
+  }
+  const int nk = K / KB;  // even (K % 128 == 0, launcher)
+  // operand panels as buffer descriptors (uniform, SGPRs): a piece is buffer_load ... lds with the
+  // per-lane offset in voffset and the K-tile offset in soffset — no per-piece address registers
+  auto xbase = [&](int tile) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(X + (int64_t)(tile / tiles_n) * 256 * K), 0, 0x7FFFFFFF, 0x00020000);
+  };
+  auto wbase = [&](int tile) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(W + (int64_t)(tile % tiles_n) * TBN * K), 0, 0x7FFFFFFF, 0x00020000);
+  };
+  auto gA = [&](__amdgpu_buffer_rsrc_t xb, int buf, int j, int kt) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(xb, (lds_ptr_t)(dsm + buf * BUF + (64 * j + 8 * wave) * KB), 16, offA[j],
+                                             kt * (KB * 2), 0, 0);
+  };
+  auto gB = [&](__amdgpu_buffer_rsrc_t wb, int buf, int j, int kt) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wb, (lds_ptr_t)(dsm + buf * BUF + TA + (64 * j + 8 * wave) * KB), 16, offB[j],
+                                             kt * (KB * 2), 0, 0);
+  };
+  // fragment reads: the swizzle of row 16i + fr is a function of fr only, so every A (B) fragment
+  // address is one of two per-lane bases (k-step 0 / 1: logical chunk fq or 4 + fq) plus an
+  // immediate offset (buffer, tile) — 4 + 4 address registers instead of one per fragment
+  const int xs = fq ^ ((fr >> 1) & 7);
+  const uint16_t* pa[2][2];
+  const uint16_t* pb[2][2];
+#pragma unroll
+  for (int bf = 0; bf < 2; ++bf)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      pa[bf][ks] = dsm + bf * BUF + (wr * 128 + fr) * KB + (xs ^ (4 * ks)) * 8;
+      pb[bf][ks] = dsm + bf * BUF + TA + (wc * 16 * NT + fr) * KB + (xs ^ (4 * ks)) * 8;
+    }
+  auto rdA = [&](int buf, int ks, int i) { return *(const bf16x8*)(pa[buf][ks] + i * 16 * KB); };
+  auto rdB = [&](int buf, int ks, int j) { return *(const bf16x8*)(pb[buf][ks] + j * 16 * KB); };
+  auto barrier = [] {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // prologue: K-tile 0 -> E, K-tile 1 -> O of the first tile
+  bias_dma(t, 0);
+  {
+    const auto xb = xbase(t);
+    const auto wb = wbase(t);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) gA(xb, 0, j, 0);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) gB(wb, 0, j, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) gA(xb, 1, j, 1);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) gB(wb, 1, j, 1);
+  }
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(4 + NT));
+  barrier();
+  if (wr == 1) barrier();  // stagger: m-group 1 runs one barrier behind
+
+  bool first = true;
+  int par = 0;
+  bf16x8 fa[4][2], fb0[NH0][2], fb1[NT - NH0][2];
+  while (true) {
+    const int tnext = t + per;
+    const bool has_next = tnext < hi;
+    const auto xc = xbase(t);
+    const auto wcb = wbase(t);
+    const auto xn = xbase(has_next ? tnext : t);
+    const auto wn = wbase(has_next ? tnext : t);
+    const int n0 = (t % tiles_n) * TBN;
+    const int64_t m0 = (int64_t)(t / tiles_n) * 256;
+
+    f32x4 acc[8][NT];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    for (int it = 0; it < nk / 2; ++it) {
+      const bool last_it = it + 1 == nk / 2;
+      const bool loads = !last_it || has_next;  // this iteration stages two more K-tiles
+      const auto xl = last_it ? xn : xc;  // their tile: this one, or the next at the end
+      const auto wl = last_it ? wn : wcb;
+      const int ke = last_it ? 0 : 2 * it + 2, ko = ke + 1;
+#pragma unroll
+      for (int p = 0; p < 8; ++p) {
+        const int buf = p >> 2, q = p & 3;
+        // ---- load segment (s = 2p)
+        if (q == 0) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            fa[i][0] = rdA(buf, 0, i);
+            fa[i][1] = rdA(buf, 1, i);
+          }
+#pragma unroll
+          for (int j = 0; j < NH0; ++j) {
+            fb0[j][0] = rdB(buf, 0, j);
+            fb0[j][1] = rdB(buf, 1, j);
+          }
+        } else if (q == 1) {
+#pragma unroll
+          for (int j = 0; j < NT - NH0; ++j) {
+            fb1[j][0] = rdB(buf, 0, NH0 + j);
+            fb1[j][1] = rdB(buf, 1, NH0 + j);
+          }
+        } else if (q == 2) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            fa[i][0] = rdA(buf, 0, 4 + i);
+            fa[i][1] = rdA(buf, 1, 4 + i);
+          }
+        }
+        auto issue = [&](int sg) {
+          if (loads) {
+            if (sg == 2) gA(xl, 0, 0, ke);
+            if (sg == 3) gA(xl, 0, 2, ke);
+            if (sg == 5) gB(wl, 0, 0, ke);
+            if (sg == 6) { gB(wl, 0, 1, ke); gA(xl, 0, 1, ke); }
+            if (sg == 7) { gB(wl, 0, 2, ke); gA(xl, 0, 3, ke); }
+            if (sg == 8 && NT == 4) gB(wl, 0, 3, ke);
+            if (sg == 10) gA(xl, 1, 0, ko);
+            if (sg == 11) gA(xl, 1, 2, ko);
+            if (sg == 13) gB(wl, 1, 0, ko);
+            if (sg == 14) { gB(wl, 1, 1, ko); gA(xl, 1, 1, ko); }
+            if (sg == 15) { gB(wl, 1, 2, ko); gA(xl, 1, 3, ko); if (NT == 4) gB(wl, 1, 3, ko); }
+          }
+        };
+        issue(2 * p);
+        if (p == 3) {  // end of s6: O complete (younger: E pieces, + last tile's stores at it 0)
+          if (!loads) __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+          else if (it == 0 && !first) __builtin_amdgcn_s_waitcnt(vmcnt_imm(5 + C::NSTORE));
+          else __builtin_amdgcn_s_waitcnt(vmcnt_imm(5));
+        } else if (p == 7) {  // end of s14: E complete (younger: 5 O pieces)
+          if (loads) __builtin_amdgcn_s_waitcnt(vmcnt_imm(5));
+          else __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+        }
+        barrier();
+        // ---- MFMA segment (s = 2p + 1)
+        __builtin_amdgcn_s_setprio(1);
+        const int mb = q < 2 ? 0 : 4;
+        if (q == 0 || q == 3) {
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              if (ks == 0 && i == 1) issue(2 * p + 1);
+#pragma unroll
+              for (int j = 0; j < NH0; ++j)
+                acc[mb + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][ks], fa[i][ks], acc[mb + i][j], 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              if (ks == 0 && i == 1) issue(2 * p + 1);
+#pragma unroll
+              for (int j = 0; j < NT - NH0; ++j)
+                acc[mb + i][NH0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][ks], fa[i][ks], acc[mb + i][NH0 + j], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_s_setprio(0);
+        barrier();
+      }
+    }
+
+    // ---- epilogue (per wave, no workgroup barrier): C^T tiles (operands swapped) — lane has row
+    // 16i + fr, columns 16j + 4fq + 0..3 — act(acc + bias) (+ residual) in f32 -> bf16 in the wave's
+    // LDS area, RM m-tiles at a time -> 16-B row chunks -> Y
+    // lane-derived addresses recomputed here from an opaque copy of the lane id, so hipcc does not
+    // keep them live (and spilled) across the main loop
+    int le = lane;
+    asm volatile("" : "+v"(le));
+    const int efr = le & 15, efq = le >> 4;
+    f32x4 bq[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+      bq[j] = HAS_BIAS ? *(const f32x4*)(lbias + par * TBN + wc * 16 * NT + j * 16 + efq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    uint2 rq[HAS_RES ? 8 : 1][HAS_RES ? NT : 1];
+    if constexpr (HAS_RES) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          rq[i][j] = *(const uint2*)(R + (m0 + wr * 128 + i * 16 + efr) * N + n0 + wc * 16 * NT + j * 16 + efq * 4);
+    }
+#pragma unroll
+    for (int rd = 0; rd < 8 / C::RM; ++rd) {
+#pragma unroll
+      for (int ii = 0; ii < C::RM; ++ii) {
+        const int i = rd * C::RM + ii;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          float v[4];
+#pragma unroll
+          for (int rg = 0; rg < 4; ++rg) {
+            v[rg] = acc[i][j][rg] + bq[j][rg];
+            if (ACT == 1) v[rg] = mmr::gelu_fast(v[rg]);
+          }
+          if constexpr (HAS_RES) {
+            const uint2 rv = rq[i][j];
+            v[0] += __uint_as_float(rv.x << 16);
+            v[1] += __uint_as_float(rv.x & 0xFFFF0000u);
+            v[2] += __uint_as_float(rv.y << 16);
+            v[3] += __uint_as_float(rv.y & 0xFFFF0000u);
+          }
+          ds_write_b64_untracked(et + (ii * 16 + efr) * C::ELD + j * 16 + efq * 4, mmr::pack2bf(v[0], v[1]), mmr::pack2bf(v[2], v[3]));
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      __builtin_amdgcn_wave_barrier();
+      bf16x8 ov[C::CPL];
+#pragma unroll
+      for (int c = 0; c < C::CPL; ++c) {
+        const int idx = c * 64 + le;
+        ov[c] = *(const bf16x8*)(et + (idx / (2 * NT)) * C::ELD + (idx % (2 * NT)) * 8);
+      }
+#pragma unroll
+      for (int c = 0; c < C::CPL; ++c) {
+        const int idx = c * 64 + le;
+        const int64_t m = m0 + wr * 128 + rd * 16 * C::RM + idx / (2 * NT);
+        const int n = n0 + wc * 16 * NT + (idx % (2 * NT)) * 8;
+        *(bf16x8*)(Y + m * N + n) = ov[c];
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (!has_next) break;
+    par ^= 1;
+    bias_dma(tnext, par);
+    t = tnext;
+    first = false;
+  }
+  if (wr == 0) barrier();  // balance the stagger
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+#endif
+}
 
 // ---------------------------------------------------------------- 4-wave persistent large-tile GEMM
 // One wave per SIMD with a 128 x 16NT wave tile (NT = 8: 256 x 256 workgroup tile; NT = 6:
@@ -652,9 +1002,9 @@ int cu_count() {
 // tile when w4 does not apply (0 off -> 128x128; 1 256x256 KB64 x2; 2 256x256 KB32 x4;
 // 3 256x128 KB64 x3; 4 / 5 256x128 KB32 x2 / x3; 6 256x192 KB64 x2 — N = 768 / 2304 / 3072 at
 // M = 32768 give 512 / 1536 / 2048 tiles, whole rounds of 256 CUs where 256x256 leaves 1.5 / 4.5).
-constexpr int kVariants = 9;
-constexpr int kVarW4[kVariants] = {1, 2, 0, 0, 0, 0, 0, 0, 0};
-constexpr int kVarCfg[kVariants] = {1, 1, 1, 2, 3, 4, 5, 6, 0};
+constexpr int kVariants = 11;
+constexpr int kVarW4[kVariants] = {1, 2, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+constexpr int kVarCfg[kVariants] = {1, 1, 1, 2, 3, 4, 5, 6, 0, 7, 8};
 
 template <int ACT, bool HB, bool HR>
 void launch(const uint16_t* x, const uint16_t* w, const float* b, const uint16_t* r, uint16_t* y,
@@ -676,6 +1026,19 @@ void launch(const uint16_t* x, const uint16_t* w, const float* b, const uint16_t
     if (n % 192 == 0) {
       const int tm = (int)t256, tn = n / 192;
       gemm_bf16_tn_w4<6, ACT, HB, HR><<<dim3(std::min<int64_t>(grid, (int64_t)tm * tn)), dim3(256), w4_lds_bytes<6>(), st>>>(x, w, b, r, y, m, n, k, tm, tn);
+      return;
+    }
+  }
+  if (cfg >= 7 && k % 128 == 0 && m % 256 == 0) {  // persistent 8-phase: 7 -> 256x256, 8 -> 256x192
+    const int grid = std::max(8, cu_count() / 8 * 8);
+    if (cfg == 7 && n % 256 == 0) {
+      const int tm = (int)t256, tn = n / 256;
+      gemm_bf16_tn_p8<4, ACT, HB, HR><<<dim3(std::max<int64_t>(8, std::min<int64_t>(grid, (int64_t)tm * tn) / 8 * 8)), dim3(512), P8<4>::LDS_B, st>>>(x, w, b, r, y, m, n, k, tm, tn);
+      return;
+    }
+    if (cfg == 8 && n % 192 == 0) {
+      const int tm = (int)t256, tn = n / 192;
+      gemm_bf16_tn_p8<3, ACT, HB, HR><<<dim3(std::max<int64_t>(8, std::min<int64_t>(grid, (int64_t)tm * tn) / 8 * 8)), dim3(512), P8<3>::LDS_B, st>>>(x, w, b, r, y, m, n, k, tm, tn);
       return;
     }
   }
