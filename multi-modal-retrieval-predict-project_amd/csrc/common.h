@@ -71,6 +71,26 @@ __device__ __forceinline__ float gelu_fast(float v) {
   return v * __builtin_amdgcn_rcpf(1.0f + e);
 }
 
+// gelu_fast on two values with packed f32 math (v_pk_fma / v_pk_mul / v_pk_add: half the VALU
+// issues of two scalar calls); same operations in the same order, so bitwise equal to gelu_fast.
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2_t gelu_fast2(f32x2_t v) {
+  const f32x2_t x2 = v * v;
+  f32x2_t p = __builtin_elementwise_fma((f32x2_t)3.275317185739523e-06f, x2, (f32x2_t)-7.756018138382363e-05f);
+  p = __builtin_elementwise_fma(p, x2, (f32x2_t)-0.00016997469037563395f);
+  p = __builtin_elementwise_fma(p, x2, (f32x2_t)0.07280746695679054f);
+  p = __builtin_elementwise_fma(p, x2, (f32x2_t)1.5957042563586181f);
+  const f32x2_t y = ((f32x2_t)-1.4426950408889634f * v) * p;
+  f32x2_t e;
+  e.x = __builtin_amdgcn_exp2f(y.x);
+  e.y = __builtin_amdgcn_exp2f(y.y);
+  const f32x2_t d = e + 1.0f;
+  f32x2_t r;
+  r.x = __builtin_amdgcn_rcpf(d.x);
+  r.y = __builtin_amdgcn_rcpf(d.y);
+  return v * r;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

@@ -735,9 +735,11 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
         for (int j = 0; j < NT; ++j) {
           float v[4];
 #pragma unroll
-          for (int rg = 0; rg < 4; ++rg) {
-            v[rg] = acc[i][j][rg] + bq[j][rg];
-            if (ACT == 1) v[rg] = mmr::gelu_fast(v[rg]);
+          for (int rg = 0; rg < 4; rg += 2) {
+            mmr::f32x2_t u = {acc[i][j][rg] + bq[j][rg], acc[i][j][rg + 1] + bq[j][rg + 1]};
+            if (ACT == 1) u = mmr::gelu_fast2(u);
+            v[rg] = u.x;
+            v[rg + 1] = u.y;
           }
           if constexpr (HAS_RES) {
             const uint2 rv = rq[i][j];

@@ -6,7 +6,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 # variant index -> (MMR_GEMM_W4, MMR_GEMM_BIG), the launcher's kVarW4 / kVarCfg tables (gemm.hip)
-VARIANTS = [(1, 1), (2, 1), (0, 1), (0, 2), (0, 3), (0, 4), (0, 5), (0, 6), (0, 0)]
+VARIANTS = [(1, 1), (2, 1), (0, 1), (0, 2), (0, 3), (0, 4), (0, 5), (0, 6), (0, 0), (0, 7), (0, 8)]
 M, N, K, act, v = (int(x) for x in sys.argv[1:6])
 n_launch = int(sys.argv[6]) if len(sys.argv) > 6 else 5
 os.environ["MMR_GEMM_W4"], os.environ["MMR_GEMM_BIG"] = (str(c) for c in VARIANTS[v])
