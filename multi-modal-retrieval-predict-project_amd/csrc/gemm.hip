@@ -29,6 +29,7 @@ namespace {
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int BM = 128, BN = 128, BK = 64;
 constexpr int TILE = BM * BK;          // bf16 elements per operand per stage (16 KiB)
@@ -481,29 +482,52 @@ __device__ __forceinline__ void ds_write_b64_untracked(const void* p, uint32_t l
   asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(d) : "memory");
 }
 
-template <int NT>
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+// v_mfma_scale_f32_16x16x128_f8f6f4, e4m3 x e4m3; scale bytes selected by (compile-time) opsel
+__device__ __forceinline__ f32x4 mx_mfma(i32x8 a, i32x8 b, f32x4 c, uint32_t sa, int ja, uint32_t sb, int jb) {
+#define MX_CASE(A, B) \
+  if (ja == A && jb == B) return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, A, (int)sa, B, (int)sb);
+  MX_CASE(0, 0) MX_CASE(0, 1) MX_CASE(0, 2) MX_CASE(0, 3) MX_CASE(1, 0) MX_CASE(1, 1) MX_CASE(1, 2) MX_CASE(1, 3)
+  MX_CASE(2, 0) MX_CASE(2, 1) MX_CASE(2, 2) MX_CASE(2, 3) MX_CASE(3, 0) MX_CASE(3, 1) MX_CASE(3, 2) MX_CASE(3, 3)
+#undef MX_CASE
+  return c;
+}
+
+template <int NT, bool FP8 = false>
 struct P8 {
   static constexpr int TBN = 64 * NT;
+  static constexpr int SC = FP8 ? 1024 : 0;            // uint16 elements of per-K-tile scales (2 KB)
   static constexpr int RM = NT == 3 ? 2 : 1;           // m-tiles per epilogue round
   static constexpr int ELD = 16 * NT + 8;              // bf16 row stride of the epilogue area
   static constexpr int CPL = 16 * RM * 2 * NT / 64;    // 16-B chunks per lane per round
   static constexpr int NSTORE = (8 / RM) * CPL;        // global stores per wave per tile
-  static constexpr size_t BUF_B = (size_t)(256 + TBN) * 64 * 2;
+  static constexpr size_t BUF_B = (size_t)(256 + TBN) * 64 * 2 + SC * 2;
   static constexpr size_t EPI_B = 8ull * 16 * RM * ELD * 2;
   static constexpr size_t LDS_B = 2 * BUF_B + EPI_B + 2 * TBN * 4;
 };
 
-template <int NT, int ACT, bool HAS_BIAS, bool HAS_RES>
+// FP8 = true: the MX-fp8 form (OCP e4m3 operands, one E8M0 scale per 32 consecutive k of a row;
+// gfx950 v_mfma_scale_f32_16x16x128_f8f6f4).  A K-tile is then 128 k = the same 128-byte LDS rows,
+// one MFMA per (m-tile, n-tile) instead of two; X / W are byte matrices with row stride K, the
+// scales (XS, WS) are pre-arranged by mmr_quantize_mxfp8 in the per-lane order of the LDS scale
+// image (1 KB per operand panel and K-tile), staged by one more LDS-DMA each.  Fragment map
+// (tools/mfma_fp8_probe.hip, exact on integer data): lane (r = l%16, g = l/16) holds k = 16g..16g+15
+// and 64+16g..64+16g+15 of row r — the two 16-byte chunks the bf16 form reads as k-steps 0 / 1 —
+// and supplies the scale of row r, k-block g.
+template <int NT, int ACT, bool HAS_BIAS, bool HAS_RES, bool FP8 = false>
 __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restrict__ X,
                                                        const uint16_t* __restrict__ W,
                                                        const float* __restrict__ bias,
                                                        const uint16_t* __restrict__ R,
                                                        uint16_t* __restrict__ Y, int64_t M, int N,
-                                                       int K, int tiles_m, int tiles_n) {
+                                                       int K, int tiles_m, int tiles_n,
+                                                       const uint8_t* __restrict__ XS = nullptr,
+                                                       const uint8_t* __restrict__ WS = nullptr) {
 #if defined(__HIP_DEVICE_COMPILE__)  // buffer-descriptor builtins exist in the device pass only
-  using C = P8<NT>;
-  constexpr int KB = 64, TBN = C::TBN;
-  constexpr int TA = 256 * KB, BUF = (256 + TBN) * KB;  // bf16 elements: A part, whole buffer
+  using C = P8<NT, FP8>;
+  constexpr int KB = 64, TBN = C::TBN;                  // KB: 128-byte LDS rows (64 bf16 / 128 fp8)
+  constexpr int TA = 256 * KB, BUF = (256 + TBN) * KB + C::SC;  // uint16 elements: A part, buffer
+  constexpr int ESZ = FP8 ? 1 : 2;                      // operand element bytes
   constexpr int NH0 = NT / 2;                           // n-tiles in n-half 0
   static_assert(C::NSTORE + 5 <= 63, "vmcnt range");
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
@@ -536,21 +560,35 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int row = 64 * j + 8 * wave + prow;
-    offA[j] = (uint32_t)((row * K + swz(row, pch) * 8) * 2);
+    offA[j] = (uint32_t)(row * K * ESZ + swz(row, pch) * 16);
   }
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     const int row = 64 * j + 8 * wave + prow;
-    offB[j] = (uint32_t)((row * K + swz(row, pch) * 8) * 2);
+    offB[j] = (uint32_t)(row * K * ESZ + swz(row, pch) * 16);
   }
-  const int nk = K / KB;  // even (K % 128 == 0, launcher)
+  const int nk = K * ESZ / 128;  // 128-byte K-tiles; even (launcher)
   // operand panels as buffer descriptors (uniform, SGPRs): a piece is buffer_load ... lds with the
   // per-lane offset in voffset and the K-tile offset in soffset — no per-piece address registers
   auto xbase = [&](int tile) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(X + (int64_t)(tile / tiles_n) * 256 * K), 0, 0x7FFFFFFF, 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)X + (int64_t)(tile / tiles_n) * 256 * K * ESZ), 0, 0x7FFFFFFF, 0x00020000);
   };
   auto wbase = [&](int tile) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(W + (int64_t)(tile % tiles_n) * TBN * K), 0, 0x7FFFFFFF, 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)W + (int64_t)(tile % tiles_n) * TBN * K * ESZ), 0, 0x7FFFFFFF, 0x00020000);
+  };
+  // MX scales: one 1-KB piece per operand panel and K-tile (wave 0: X's, wave 1: W's); a wave issues
+  // it with its first piece of that K-tile, so every count-based wait below still covers it
+  const auto xsr = __builtin_amdgcn_make_buffer_rsrc((void*)XS, 0, 0x7FFFFFFF, 0x00020000);
+  const auto wsr = __builtin_amdgcn_make_buffer_rsrc((void*)WS, 0, 0x7FFFFFFF, 0x00020000);
+  auto gS = [&](int tile, int buf, int kt) {
+    if constexpr (FP8) {
+      if (wave == 0)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xsr, (lds_ptr_t)(dsm + buf * BUF + (256 + TBN) * KB), 16, lane * 16,
+                                                 ((tile / tiles_n) * nk + kt) * 1024, 0, 0);
+      else if (wave == 1)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wsr, (lds_ptr_t)(dsm + buf * BUF + (256 + TBN) * KB + 512), 16, lane * 16,
+                                                 ((tile % tiles_n) * nk + kt) * 1024, 0, 0);
+    }
   };
   auto gA = [&](__amdgpu_buffer_rsrc_t xb, int buf, int j, int kt) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(xb, (lds_ptr_t)(dsm + buf * BUF + (64 * j + 8 * wave) * KB), 16, offA[j],
@@ -575,6 +613,35 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
     }
   auto rdA = [&](int buf, int ks, int i) { return *(const bf16x8*)(pa[buf][ks] + i * 16 * KB); };
   auto rdB = [&](int buf, int ks, int j) { return *(const bf16x8*)(pb[buf][ks] + j * 16 * KB); };
+  bf16x8 fa[4][2], fb0[NH0][2], fb1[NT - NH0][2];
+  i32x8 fa8[4], fb08[NH0], fb18[NT - NH0];  // FP8: the two 16-byte chunks of a fragment, contiguous
+  auto ldA = [&](int buf, int i, int mt) {
+    if constexpr (FP8) {
+      fa8[i] = __builtin_shufflevector(__builtin_bit_cast(i32x4_t, rdA(buf, 0, mt)),
+                                       __builtin_bit_cast(i32x4_t, rdA(buf, 1, mt)), 0, 1, 2, 3, 4, 5, 6, 7);
+    } else {
+      fa[i][0] = rdA(buf, 0, mt);
+      fa[i][1] = rdA(buf, 1, mt);
+    }
+  };
+  auto ldB0 = [&](int buf, int j) {
+    if constexpr (FP8) {
+      fb08[j] = __builtin_shufflevector(__builtin_bit_cast(i32x4_t, rdB(buf, 0, j)),
+                                       __builtin_bit_cast(i32x4_t, rdB(buf, 1, j)), 0, 1, 2, 3, 4, 5, 6, 7);
+    } else {
+      fb0[j][0] = rdB(buf, 0, j);
+      fb0[j][1] = rdB(buf, 1, j);
+    }
+  };
+  auto ldB1 = [&](int buf, int j) {
+    if constexpr (FP8) {
+      fb18[j] = __builtin_shufflevector(__builtin_bit_cast(i32x4_t, rdB(buf, 0, NH0 + j)),
+                                       __builtin_bit_cast(i32x4_t, rdB(buf, 1, NH0 + j)), 0, 1, 2, 3, 4, 5, 6, 7);
+    } else {
+      fb1[j][0] = rdB(buf, 0, NH0 + j);
+      fb1[j][1] = rdB(buf, 1, NH0 + j);
+    }
+  };
   auto barrier = [] {
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -583,6 +650,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
 
   // prologue: K-tile 0 -> E, K-tile 1 -> O of the first tile
   bias_dma(t, 0);
+  gS(t, 0, 0);
+  gS(t, 1, 1);
   {
     const auto xb = xbase(t);
     const auto wb = wbase(t);
@@ -601,7 +670,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
 
   bool first = true;
   int par = 0;
-  bf16x8 fa[4][2], fb0[NH0][2], fb1[NT - NH0][2];
+  uint32_t sca[2] = {0u, 0u}, scb = 0u;  // FP8: this K-tile's E8M0 scales (m-tile i: byte i of sca; n-tile j: byte j of scb)
   while (true) {
     const int tnext = t + per;
     const bool has_next = tnext < hi;
@@ -629,39 +698,34 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
         const int buf = p >> 2, q = p & 3;
         // ---- load segment (s = 2p)
         if (q == 0) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            fa[i][0] = rdA(buf, 0, i);
-            fa[i][1] = rdA(buf, 1, i);
+          if constexpr (FP8) {
+            const uint8_t* sb = (const uint8_t*)(dsm + buf * BUF + (256 + TBN) * KB);
+            const uint2 sa2 = *(const uint2*)(sb + ((wr * 4 + fq) * 16 + fr) * 8);
+            sca[0] = sa2.x;
+            sca[1] = sa2.y;
+            scb = *(const uint32_t*)(sb + 1024 + ((wc * 4 + fq) * 16 + fr) * 4);
           }
 #pragma unroll
-          for (int j = 0; j < NH0; ++j) {
-            fb0[j][0] = rdB(buf, 0, j);
-            fb0[j][1] = rdB(buf, 1, j);
-          }
+          for (int i = 0; i < 4; ++i) ldA(buf, i, i);
+#pragma unroll
+          for (int j = 0; j < NH0; ++j) ldB0(buf, j);
         } else if (q == 1) {
 #pragma unroll
-          for (int j = 0; j < NT - NH0; ++j) {
-            fb1[j][0] = rdB(buf, 0, NH0 + j);
-            fb1[j][1] = rdB(buf, 1, NH0 + j);
-          }
+          for (int j = 0; j < NT - NH0; ++j) ldB1(buf, j);
         } else if (q == 2) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            fa[i][0] = rdA(buf, 0, 4 + i);
-            fa[i][1] = rdA(buf, 1, 4 + i);
-          }
+          for (int i = 0; i < 4; ++i) ldA(buf, i, 4 + i);
         }
         auto issue = [&](int sg) {
           if (loads) {
             if (sg == 2) gA(xl, 0, 0, ke);
-            if (sg == 3) gA(xl, 0, 2, ke);
+            if (sg == 3) { gS(last_it ? tnext : t, 0, ke); gA(xl, 0, 2, ke); }
             if (sg == 5) gB(wl, 0, 0, ke);
             if (sg == 6) { gB(wl, 0, 1, ke); gA(xl, 0, 1, ke); }
             if (sg == 7) { gB(wl, 0, 2, ke); gA(xl, 0, 3, ke); }
             if (sg == 8 && NT == 4) gB(wl, 0, 3, ke);
             if (sg == 10) gA(xl, 1, 0, ko);
-            if (sg == 11) gA(xl, 1, 2, ko);
+            if (sg == 11) { gS(last_it ? tnext : t, 1, ko); gA(xl, 1, 2, ko); }
             if (sg == 13) gB(wl, 1, 0, ko);
             if (sg == 14) { gB(wl, 1, 1, ko); gA(xl, 1, 1, ko); }
             if (sg == 15) { gB(wl, 1, 2, ko); gA(xl, 1, 3, ko); if (NT == 4) gB(wl, 1, 3, ko); }
@@ -680,7 +744,24 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
         // ---- MFMA segment (s = 2p + 1)
         __builtin_amdgcn_s_setprio(1);
         const int mb = q < 2 ? 0 : 4;
-        if (q == 0 || q == 3) {
+        if constexpr (FP8) {
+          // one 16x16x128 MX MFMA per (m-tile, n-tile): W fragment (src0, its scale) x X fragment
+          // (src1) -> C^T like the bf16 form; opsel picks the tile's scale byte
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (i == 1) issue(2 * p + 1);
+            const int mi = mb + i;
+            if (q == 0 || q == 3) {
+#pragma unroll
+              for (int j = 0; j < NH0; ++j)
+                acc[mi][j] = mx_mfma(fb08[j], fa8[i], acc[mi][j], scb, j, sca[mi >> 2], mi & 3);
+            } else {
+#pragma unroll
+              for (int j = 0; j < NT - NH0; ++j)
+                acc[mi][NH0 + j] = mx_mfma(fb18[j], fa8[i], acc[mi][NH0 + j], scb, NH0 + j, sca[mi >> 2], mi & 3);
+            }
+          }
+        } else if (q == 0 || q == 3) {
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -700,6 +781,16 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
               for (int j = 0; j < NT - NH0; ++j)
                 acc[mb + i][NH0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][ks], fa[i][ks], acc[mb + i][NH0 + j], 0, 0, 0);
             }
+        }
+        // FP8: the cluster's results are pinned before the barrier — machine sinking otherwise moves
+        // the scaled MFMAs into later blocks (toward their next use) and keeps several phases of
+        // fragments live (256 VGPRs + spills)
+        if constexpr (FP8) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+              if ((q == 0 || q == 3) == (j < NH0)) mmr::pin(acc[mb + i][j]);
         }
         __builtin_amdgcn_s_setprio(0);
         barrier();
@@ -988,6 +1079,61 @@ __global__ __launch_bounds__(256) void gemm_bf16_tn_w4(const uint16_t* __restric
   __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));  // no LDS-DMA may land after the workgroup retires
 }
 
+// ---------------------------------------------------------------- MX-fp8 quantizer
+// bf16 [rows][k] -> OCP e4m3 bytes [rows][kp] (zero-padded to kp) + one E8M0 scale per 32 consecutive
+// k of a row: scale 2^e with the smallest e such that amax <= 448 * 2^e (exact from amax's bits, no
+// clipping), q = round-to-nearest-even(x * 2^-e) (v_cvt_pk_fp8_f32).  The scales are written in
+// the order the GEMM's per-lane LDS scale image wants (1 KB per operand panel and 128-k K-tile):
+//   LAYOUT 0 (X, panels of 256 rows): [panel][kt][wr 2][fq 4][fr 16][i 8], row = 128 wr + 16 i + fr
+//   LAYOUT 1 (W, panels of 192 rows): [panel][kt][wc 4][fq 4][fr 16][j 4], row = 48 wc + 16 j + fr
+// (fq = the 32-block within the K-tile).  One thread per 8 values, 4 threads per block.
+template <int LAYOUT>
+__global__ __launch_bounds__(256) void quantize_mxfp8(const uint16_t* __restrict__ x, int64_t rows, int k,
+                                                      int kp, uint8_t* __restrict__ q, uint8_t* __restrict__ sc) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c8n = kp / 8;
+  const int64_t row = t / c8n;
+  const int k0 = (int)(t % c8n) * 8;
+  const bool ok = row < rows;
+  const int64_t rc = ok ? row : rows - 1;
+  const int kc = k0 < k ? k0 : k - 8;
+  const bf16x8 raw = *(const bf16x8*)(x + rc * k + kc);  // unconditional (clamped), masked below
+  float v[8];
+  float amax = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    v[e] = k0 < k ? mmr::bf2f((uint16_t)raw[e]) : 0.f;
+    amax = fmaxf(amax, fabsf(v[e]));
+  }
+  amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+  amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+  const uint32_t ab = __float_as_uint(amax);
+  int ex = (int)((ab >> 23) & 255) - 127 - 8 + ((ab & 0x7FFFFF) > 0x600000 ? 1 : 0);
+  ex = ex < -127 ? -127 : (ex > 126 ? 126 : ex);
+  const float inv = __uint_as_float((uint32_t)(127 - ex) << 23);  // 2^-ex, exact
+  uint32_t lo = 0, hi = 0;
+  lo = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[0] * inv, v[1] * inv, (int)lo, false);
+  lo = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[2] * inv, v[3] * inv, (int)lo, true);
+  hi = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[4] * inv, v[5] * inv, (int)hi, false);
+  hi = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[6] * inv, v[7] * inv, (int)hi, true);
+  if (!ok) return;
+  *(uint2*)(q + row * kp + k0) = make_uint2(lo, hi);
+  if ((k0 & 31) == 0) {
+    const int blk = k0 / 32, kt = blk / 4, fq = blk % 4;
+    int64_t off;
+    if (LAYOUT == 0) {
+      const int64_t P = row / 256;
+      const int rr = (int)(row % 256), wr = rr / 128, i = (rr % 128) / 16, fr = rr % 16;
+      off = (P * (kp / 128) + kt) * 1024 + ((wr * 4 + fq) * 16 + fr) * 8 + i;
+    } else {
+      const int64_t P = row / 192;
+      const int rr = (int)(row % 192), wc = rr / 48, j = (rr % 48) / 16, fr = rr % 16;
+      off = (P * (kp / 128) + kt) * 1024 + ((wc * 4 + fq) * 16 + fr) * 4 + j;
+    }
+    sc[off] = (uint8_t)(ex + 127);
+  }
+}
+
 int cu_count() {
   static int n = [] {
     int dev = 0, v = 0;
@@ -1192,6 +1338,57 @@ extern "C" mmr_status mmr_linear_bf16(const uint16_t* x, const uint16_t* w, cons
     const int v = tuned_variant(m, n, k, act, hb, hr, x, residual, y, st, run);
     run(kVarW4[v], kVarCfg[v]);
   }
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+extern "C" mmr_status mmr_quantize_mxfp8(const uint16_t* x, int64_t rows, int32_t k, int32_t kp, int32_t layout,
+                                         uint8_t* q, uint8_t* scales, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && q && scales, "mmr_quantize_mxfp8: NULL pointer");
+  MMR_REQUIRE(layout == 0 || layout == 1, "mmr_quantize_mxfp8: layout=%d (0: X panels of 256 rows, 1: W panels of 192)", layout);
+  MMR_REQUIRE(rows > 0 && rows % (layout == 0 ? 256 : 192) == 0, "mmr_quantize_mxfp8: rows=%lld must be a multiple of %d",
+              (long long)rows, layout == 0 ? 256 : 192);
+  MMR_REQUIRE(k > 0 && k % 8 == 0 && kp >= k && kp % 256 == 0, "mmr_quantize_mxfp8: k=%d kp=%d (k %% 8 == 0, kp >= k, kp %% 256 == 0)", k, kp);
+  const int64_t threads = rows * (kp / 8);
+  hipStream_t st = mmr::as_stream(stream);
+  if (layout == 0)
+    quantize_mxfp8<0><<<dim3((unsigned)mmr::ceil_div(threads, 256)), dim3(256), 0, st>>>(x, rows, k, kp, q, scales);
+  else
+    quantize_mxfp8<1><<<dim3((unsigned)mmr::ceil_div(threads, 256)), dim3(256), 0, st>>>(x, rows, k, kp, q, scales);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+extern "C" mmr_status mmr_linear_mxfp8(const uint8_t* xq, const uint8_t* xs, const uint8_t* wq, const uint8_t* ws,
+                                       const float* bias, const uint16_t* residual, uint16_t* y, int64_t m, int32_t n,
+                                       int32_t kp, int32_t act, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(xq && xs && wq && ws && y, "mmr_linear_mxfp8: NULL pointer");
+  MMR_REQUIRE(m > 0 && m % 256 == 0, "mmr_linear_mxfp8: m=%lld must be a positive multiple of 256", (long long)m);
+  MMR_REQUIRE(n > 0 && n % 192 == 0, "mmr_linear_mxfp8: n=%d must be a positive multiple of 192", n);
+  MMR_REQUIRE(kp > 0 && kp % 256 == 0, "mmr_linear_mxfp8: kp=%d must be a positive multiple of 256", kp);
+  MMR_REQUIRE(act == 0 || act == 1, "mmr_linear_mxfp8: act=%d", act);
+  hipStream_t st = mmr::as_stream(stream);
+  const int tm = (int)(m / 256), tn = n / 192;
+  const int grid = (int)std::max<int64_t>(8, std::min<int64_t>(std::max(8, cu_count() / 8 * 8), (int64_t)tm * tn) / 8 * 8);
+  const bool hb = bias != nullptr, hr = residual != nullptr;
+  const uint16_t* X = (const uint16_t*)xq;
+  const uint16_t* W = (const uint16_t*)wq;
+#define MX_LAUNCH(A, B, R) \
+  gemm_bf16_tn_p8<3, A, B, R, true><<<dim3(grid), dim3(512), P8<3, true>::LDS_B, st>>>(X, W, bias, residual, y, m, n, kp, tm, tn, xs, ws)
+  if (act == 0) {
+    if (hb && hr) MX_LAUNCH(0, true, true);
+    else if (hb) MX_LAUNCH(0, true, false);
+    else if (hr) MX_LAUNCH(0, false, true);
+    else MX_LAUNCH(0, false, false);
+  } else {
+    if (hb && hr) MX_LAUNCH(1, true, true);
+    else if (hb) MX_LAUNCH(1, true, false);
+    else if (hr) MX_LAUNCH(1, false, true);
+    else MX_LAUNCH(1, false, false);
+  }
+#undef MX_LAUNCH
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }

@@ -31,6 +31,46 @@ def linear(x, w, bias=None, residual=None, act=0, out=None):
     return y
 
 
+class MXFP8:
+    """An MX-fp8 operand: e4m3 bytes q [rows][kp] + E8M0 scales in the GEMM's image order (see
+    mmr_quantize_mxfp8), k the unpadded inner size, layout 0 (activations) / 1 (weights)."""
+    __slots__ = ("q", "s", "k", "layout")
+
+    def __init__(self, q, s, k, layout):
+        self.q, self.s, self.k, self.layout = q, s, k, layout
+
+    @property
+    def kp(self):
+        return self.q.shape[1]
+
+
+def quantize_mxfp8(x, layout=0, kp=None):
+    """bf16 (..., k) -> MXFP8 (rows = prod of leading dims; rows % 256 == 0 for layout 0, % 192 for 1)."""
+    _lib.require_gpu(x)
+    k = x.shape[-1]
+    rows = x.numel() // k
+    kp = kp or -(-k // 256) * 256
+    q = torch.empty((rows, kp), dtype=torch.uint8, device=x.device)
+    pr = 256 if layout == 0 else 192
+    nsc = (rows // pr) * (kp // 128) * 1024 if rows % pr == 0 else 0
+    s = torch.zeros((max(nsc, 1),), dtype=torch.uint8, device=x.device)
+    _chk(_L().mmr_quantize_mxfp8(_lib.ptr(x), rows, k, kp, layout, _lib.ptr(q), _lib.ptr(s), _s(x)),
+         "mmr_quantize_mxfp8")
+    return MXFP8(q, s, k, layout)
+
+
+def linear_mxfp8(x8, w8, bias=None, residual=None, act=0, out=None, lead=None):
+    """act(deq(x8) @ deq(w8).T + bias) (+ residual) -> bf16 (rows, N) (or lead + (N,))."""
+    _lib.require_gpu(x8.q)
+    assert x8.layout == 0 and w8.layout == 1 and x8.kp == w8.kp, "operand layouts / padded K disagree"
+    M, N = x8.q.shape[0], w8.q.shape[0]
+    shape = (lead if lead is not None else (M,)) + (N,)
+    y = out if out is not None else torch.empty(shape, dtype=torch.bfloat16, device=x8.q.device)
+    _chk(_L().mmr_linear_mxfp8(_lib.ptr(x8.q), _lib.ptr(x8.s), _lib.ptr(w8.q), _lib.ptr(w8.s), _lib.ptr(bias),
+                               _lib.ptr(residual), _lib.ptr(y), M, N, x8.kp, act, _s(x8.q)), "mmr_linear_mxfp8")
+    return y
+
+
 def layernorm(x, g, b, eps, out=None):
     _lib.require_gpu(x)
     c = x.shape[-1]

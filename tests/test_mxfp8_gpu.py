@@ -1,0 +1,89 @@
+"""GPU: MX-fp8 quantiser and block-scaled GEMM (the fp8 tower linears of BASELINE.json config 5)
+against the numpy restatement in oracle/mxfp8.py.
+
+Quantiser: bit-exact — every e4m3 value and every E8M0 scale byte (read back through the image-order
+offsets) equals the oracle's, including zero blocks, zero-padded K and both scale layouts.
+GEMM: the products of e4m3 x e4m3 x 2^(ea+eb) are exact in f32, so the only differences from an f64
+GEMM of the dequantised operands are the f32 accumulation order and the bf16 output rounding:
+tolerance |y - ref| <= 2^-8 |ref| + 1e-3 * max|ref| (bf16 half-ulp plus accumulation slack)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mmr_amd import ops
+from oracle import mxfp8 as mx
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _bf16_input(rows, k, seed, zero_block=True):
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal((rows, k)).astype(np.float32)
+    x *= np.exp(rng.uniform(-6, 6, (rows, 1))).astype(np.float32)   # per-row magnitudes over 5 decades
+    if zero_block:
+        x[3, 32:64] = 0.0
+    t = torch.from_numpy(x).to(torch.bfloat16)
+    return t, t.float().numpy()
+
+
+def _decode(x8, rows, layout):
+    q = mx.e4m3_decode(x8.q.cpu().numpy())
+    off = mx.scale_offsets(rows, x8.kp, layout)
+    e = x8.s.cpu().numpy()[off].astype(np.int32) - 127
+    return q, e
+
+
+@pytest.mark.parametrize("rows,k,layout", [(256, 768, 0), (512, 384, 0), (384, 768, 1), (192, 3072, 1)])
+def test_quantize_bit_exact(rows, k, layout):
+    xt, xf = _bf16_input(rows, k, 11 + rows + k)
+    x8 = ops.quantize_mxfp8(xt.to(DEV), layout=layout)
+    torch.cuda.synchronize()
+    q, e = _decode(x8, rows, layout)
+    qo, eo = mx.quantize(xf, x8.kp)
+    np.testing.assert_array_equal(e, eo)
+    np.testing.assert_array_equal(q, qo)
+    assert x8.kp >= k and np.all(q[:, k:] == 0)
+
+
+def _ref(x8, w8, rows, n, bias, res, act):
+    qx, ex = _decode(x8, rows, 0)
+    qw, ew = _decode(w8, n, 1)
+    y = mx.dequantize(qx, ex) @ mx.dequantize(qw, ew).T
+    if bias is not None:
+        y = y + bias.cpu().numpy().astype(np.float64)[None, :]
+    if act:
+        y = F.gelu(torch.from_numpy(y)).numpy()
+    if res is not None:
+        y = y + res.float().cpu().numpy()
+    return y
+
+
+@pytest.mark.parametrize("M,N,K,act,res", [(256, 192, 768, 0, False), (512, 384, 384, 1, False),
+                                           (1024, 576, 768, 0, True), (8192, 2304, 768, 0, False),
+                                           (4096, 768, 3072, 0, True), (2048, 3072, 768, 1, False)])
+def test_linear_mxfp8_matches_dequantised_gemm(M, N, K, act, res):
+    xt, _ = _bf16_input(M, K, 7 + M)
+    wt, _ = _bf16_input(N, K, 8 + N, zero_block=False)
+    x8 = ops.quantize_mxfp8(xt.to(DEV), layout=0)
+    w8 = ops.quantize_mxfp8((wt * 0.05).to(DEV), layout=1)
+    g = torch.Generator().manual_seed(M + N)
+    bias = torch.randn(N, generator=g).to(DEV)
+    r = (torch.randn(M, N, generator=g) * 3).to(torch.bfloat16).to(DEV) if res else None
+    y = ops.linear_mxfp8(x8, w8, bias, r, act=act)
+    torch.cuda.synchronize()
+    ref = _ref(x8, w8, M, N, bias, r, act)
+    d = np.abs(y.float().cpu().numpy() - ref)
+    tol = 2.0 ** -8 * np.abs(ref) + 1e-3 * np.abs(ref).max()
+    assert np.all(d <= tol), f"max excess {np.max(d - tol)}"
+
+
+def test_linear_mxfp8_rejects_bad_shapes():
+    x8 = ops.quantize_mxfp8(torch.zeros(256, 768, dtype=torch.bfloat16, device=DEV), layout=0)
+    w8 = ops.quantize_mxfp8(torch.zeros(200, 768, dtype=torch.bfloat16, device=DEV)[:192], layout=1)
+    with pytest.raises(Exception):
+        ops.quantize_mxfp8(torch.zeros(100, 768, dtype=torch.bfloat16, device=DEV), layout=0)
+    bad = ops.MXFP8(w8.q[:100], w8.s, 768, 1)
+    with pytest.raises(Exception):
+        ops.linear_mxfp8(x8, bad)

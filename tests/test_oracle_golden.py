@@ -139,3 +139,21 @@ def test_package_imports_without_gpu():
     assert hasattr(mmr_amd, "make_retrieval_engine")
     with pytest.raises(ValueError):
         mmr_amd.make_retrieval_engine("x.npy", "x.json", method="nope")
+
+
+def test_mxfp8_oracle_rounding_matches_torch_float8():
+    """The MX-fp8 oracle's e4m3 round-to-nearest-even and byte decode (oracle/mxfp8.py) equal torch's
+    own float8_e4m3fn conversion on 200k values over 6 decades, and all 256 byte codes."""
+    import torch
+    from oracle import mxfp8 as mx
+    rng = np.random.default_rng(0)
+    v = np.clip((rng.standard_normal(200_000) * rng.choice([1e-3, 1.0, 30.0, 200.0], 200_000)).astype(np.float32),
+                -448, 448)
+    np.testing.assert_array_equal(mx.e4m3_round(v), torch.from_numpy(v).to(torch.float8_e4m3fn).float().numpy())
+    b = np.arange(256, dtype=np.uint8)
+    np.testing.assert_array_equal(mx.e4m3_decode(b), torch.from_numpy(b).view(torch.float8_e4m3fn).float().numpy())
+    # block exponents: amax exactly 448 * 2^e -> e; one ulp above -> e + 1; zero block -> -127
+    x = np.zeros((3, 32), np.float32)
+    x[0, 5] = 448.0 * 4
+    x[1, 7] = np.nextafter(np.float32(448.0 * 4), np.float32(1e9))
+    np.testing.assert_array_equal(mx.block_exponents(x)[:, 0], [2, 3, -127])
