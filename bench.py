@@ -1,7 +1,7 @@
 """Benchmark of the hot path (BASELINE.json metric: query embeddings/sec + cosine-pairs/sec,
 100k x 768 gallery).
 
-python bench.py --gpus N --steps K --warmup W [--mode full|knn] [--preset cfg2|cfg3|cfg4]
+python bench.py --gpus N --steps K --warmup W [--mode full|knn] [--preset cfg2|cfg3|cfg4|cfg5]
   full (default): one step = Swin-T tower on B synthetic 224x224 images + ClinicalBERT-geometry
         tower on B synthetic 128-token reports (bf16) -> joint-embedding head (default: the
         reference's default model_type "multimodal", 5 fusion layers x 8 heads) -> exact cosine
@@ -10,7 +10,11 @@ python bench.py --gpus N --steps K --warmup W [--mode full|knn] [--preset cfg2|c
         image: image tower + image head only; both: both single-modality heads (2B embeddings).
   knn:  one step = exact cosine top-K of B resident queries over the gallery (kNN leg only).
 Presets (BASELINE.json configs): cfg2 = the defaults; cfg3 = --model-type text --batch 1024
-  --gallery 1000000 --k 50; cfg4 = cfg2 with 1M gallery rows per GPU (8M at --gpus 8).
+  --gallery 1000000 --k 50; cfg4 = cfg2 with 1M gallery rows per GPU (8M at --gpus 8); cfg5 =
+  --tower-dtype fp8 --batch 2048 --dim 1024 --gallery 1000000 --rerank: MX-fp8 linears in all BERT
+  layers and Swin stages 3-4, joint_dim 1024, top-10 per query over 1M x 1024 rows per GPU, then the
+  fused KG / label rerank (mmr_index_rerank, reranker.py:240-333) of those 10 candidates (batch 2048 is
+  per GPU: weak scaling like the other presets; --rerank runs at --gpus 1 only).
 N>1: `python bench.py --gpus N` starts N ranks itself (torch.distributed.run, one process per GPU,
 RCCL) unless it already runs under a launcher (WORLD_SIZE set, which must equal --gpus).  The
 gallery is row-sharded (--gallery rows per rank: weak scaling), every rank runs its own query batch
@@ -33,7 +37,9 @@ PRESETS = {
     "cfg2": {},
     "cfg3": {"model_type": "text", "batch": 1024, "gallery": 1_000_000, "k": 50},
     "cfg4": {"gallery": 1_000_000},
+    "cfg5": {"batch": 2048, "gallery": 1_000_000, "dim": 1024, "k": 10, "tower_dtype": "fp8", "rerank": True},
 }
+RERANK_DK = 128  # synthetic KG embedding width of the rerank tables
 
 
 def parse(argv=None):
@@ -44,13 +50,18 @@ def parse(argv=None):
     p.add_argument("--mode", choices=["full", "knn"], default="full")
     p.add_argument("--preset", choices=sorted(PRESETS), default="cfg2",
                    help="BASELINE.json config: cfg2 (default), cfg3 (text-only B=1024, 1M x 768, top-50), "
-                        "cfg4 (1M rows per GPU); explicit flags override the preset")
+                        "cfg4 (1M rows per GPU), cfg5 (fp8 towers, B=2048, 1M x 1024, rerank); explicit flags "
+                        "override the preset")
+    p.add_argument("--tower-dtype", choices=["bf16", "fp8"], default=None,
+                   help="tower linears: bf16 (configs 2-4) or MX-fp8 (config 5)")
+    p.add_argument("--rerank", action="store_true", default=None,
+                   help="fused KG / label rerank of each query's top-K candidates inside the step")
     p.add_argument("--batch", type=int, default=None)
     p.add_argument("--knn-mode", choices=["x3", "f16"], default="f16",
                    help="gallery scan: f16 (fp16 unit-row copy, default) or x3 (bf16 split GEMM; skinny f32 "
                         "stream for Q <= 32); both exact (f64 re-rank from the f32 rows)")
     p.add_argument("--gallery", type=int, default=None, help="gallery rows per GPU")
-    p.add_argument("--dim", type=int, default=768)
+    p.add_argument("--dim", type=int, default=None)
     p.add_argument("--k", type=int, default=None)
     p.add_argument("--model-type", choices=["multimodal", "text", "image", "both"], default=None,
                    help="joint-embedding head: multimodal (reference default, model.py:137; 5 fusion layers, "
@@ -58,7 +69,8 @@ def parse(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-queries", type=int, default=0)
     a = p.parse_args(argv)
-    pre = dict({"batch": 256, "gallery": 100_000, "k": 10, "model_type": "multimodal"}, **PRESETS[a.preset])
+    pre = dict({"batch": 256, "gallery": 100_000, "k": 10, "model_type": "multimodal", "dim": 768,
+                "tower_dtype": "bf16", "rerank": False}, **PRESETS[a.preset])
     for key, v in pre.items():
         if getattr(a, key) is None:
             setattr(a, key, v)
@@ -111,6 +123,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
         sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}: refusing to report a mismatched run")
+    if a.rerank and world > 1:
+        sys.exit("bench.py: --rerank needs the candidates' gallery rows on the reranking GPU; run it at --gpus 1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
@@ -138,7 +152,7 @@ def main():
     if a.mode == "full":
         from mmr_amd.model import build_bench_model
         mt = "text" if a.model_type == "both" else a.model_type
-        model = build_bench_model(device=dev, joint_dim=d, model_type=mt)
+        model = build_bench_model(device=dev, joint_dim=d, model_type=mt, tower_dtype=a.tower_dtype)
         if a.model_type != "text":
             imgs = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(B, synthetic.SEED + rank))).to(dev)
         if a.model_type != "image":
@@ -146,6 +160,21 @@ def main():
             ids, mask = torch.from_numpy(ids_np).to(dev), torch.from_numpy(mask_np).to(dev)
     else:
         qbatch = torch.from_numpy(synthetic.gauss_gallery(B, d, synthetic.SEED + 1 + rank)).to(dev)
+
+    rr = None
+    if a.rerank:
+        # synthetic rerank tables (reranker.py:88-129 loads them from the KG directory / labels CSV):
+        # 1-3 of 43 labels per row as uint64 bitsets, RERANK_DK-wide KG vectors
+        gen = torch.Generator(device=dev).manual_seed(synthetic.SEED + 31)
+        nqr = B * (2 if a.model_type == "both" else 1)
+
+        def bits(rows):
+            lab = torch.randint(0, synthetic.NUM_LABELS, (rows, 3), generator=gen, device=dev)
+            keep = torch.rand((rows, 3), generator=gen, device=dev) < torch.tensor([1.0, 0.5, 0.3], device=dev)
+            return ((torch.ones_like(lab) << lab) * keep).sum(1)
+        rr = {"g_lab": bits(n), "q_lab": bits(nqr),
+              "g_kg": torch.randn((n, RERANK_DK), generator=gen, device=dev),
+              "q_kg": torch.randn((nqr, RERANK_DK), generator=gen, device=dev)}
 
     stream = torch.cuda.current_stream(dev)
     ev_pairs = []
@@ -169,6 +198,8 @@ def main():
             e1.record(stream)
             ev_pairs.append((e0, e1))
         torch.maximum(st_max, st.max(), out=st_max)  # checked after the timed region (no sync here)
+        if rr is not None:  # fused rerank of the K candidates (world 1: local = global row ids)
+            i = index.rerank(allq, i, rr["q_lab"], rr["g_lab"], rr["q_kg"], rr["g_kg"], K, want_components=False)[0]
         if world > 1:
             gi = torch.empty((world * i.shape[0], K), dtype=i.dtype, device=dev)
             gs = torch.empty((world * s64.shape[0], K), dtype=s64.dtype, device=dev)
@@ -267,11 +298,14 @@ def main():
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": elapsed / a.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": ("bf16 towers / " if a.mode == "full" else "") + (
+            "dtype": (("MX-fp8 (e4m3 + E8M0/32) tower linears, bf16 elsewhere / " if a.tower_dtype == "fp8"
+                       else "bf16 towers / ") if a.mode == "full" else "") + (
                 "f32 gallery, fp16 unit-row scan copy, exact f64 re-rank" if a.knn_mode == "f16"
                 else "f32 gallery, bf16x3 scan, exact f64 re-rank"),
             "data": "synthetic (seeded N(0,1) gallery; random-init weights)",
-            "config": {"workload": ("%s: %s, B=%d, top-%d over %dx%d f32 per GPU" % (a.preset, workload, B, K, n, d))
+            "config": {"workload": ("%s: %s%s, B=%d, top-%d over %dx%d f32 per GPU%s" % (
+                a.preset, workload, " (MX-fp8 BERT + Swin stage 3-4 linears)" if a.tower_dtype == "fp8" else "", B, K, n, d,
+                " + fused KG/label rerank of the %d candidates" % K if a.rerank else ""))
                        if a.mode == "full" else ("%s kNN only: Q=%d, top-%d over %dx%d f32 per GPU" % (a.preset, B, K, n, d)),
                        "global_batch": world * B, "gallery_rows": world * n, "dim": d, "k": K,
                        "parallelism": f"gallery row-shard x{world} + tower DP x{world}" if world > 1 else "single"},
@@ -322,6 +356,8 @@ def roofline(a, n, d, K, Qs, ms_search, ms_small, q_small, gemm_ms, B):
         "frac": small_bytes / (ms_small / 1e3) / peak_hbm,
         "kernel": "whole search call: prep + %s scan + knn_select_t (events on the launch stream)"
                   % ("knn_scan_f16_gmax<1>" if a.knn_mode == "f16" else "knn_scan_f32_gmax<1>")}
+    fp8 = getattr(a, "tower_dtype", "bf16") == "fp8"
+    peak_gemm = 5.0e15 if fp8 else peak_bf16  # dense MX-fp8 / bf16 MFMA peaks (MI355X_MICROARCH.md)
     if gemm_ms:
         M = B * 128
         shapes = {"qkv": (M, 2304, 768), "o": (M, 768, 768), "ffn1": (M, 3072, 768), "ffn2": (M, 768, 3072)}
@@ -330,13 +366,15 @@ def roofline(a, n, d, K, Qs, ms_search, ms_small, q_small, gemm_ms, B):
             m_, n_, k_ = shapes[name]
             fl = 2.0 * m_ * n_ * k_
             fam[name] = {"shape_mnk": [m_, n_, k_], "ms_per_launch": ms, "tflops": fl / (ms / 1e3) / 1e12,
-                         "frac": fl / (ms / 1e3) / peak_bf16}
+                         "frac": fl / (ms / 1e3) / peak_gemm}
         ms_ffn1 = gemm_ms["ffn1"]
         fl = 2.0 * M * 3072 * 768
-        roof = {"bound": "mfma", "achieved": fl / (ms_ffn1 / 1e3) / 1e12, "peak": peak_bf16 / 1e12,
+        roof = {"bound": "mfma", "achieved": fl / (ms_ffn1 / 1e3) / 1e12, "peak": peak_gemm / 1e12,
                 "unit": "TFLOP/s", "traffic": None,
-                "kernel": ("BERT FFN1 GEMM + GELU (M=%d, N=3072, K=768; tuned variant), timed per launch with HIP "
-                           "events in a towers-in-sequence pass after the timed region" % M),
+                "kernel": (("BERT FFN1 MX-fp8 GEMM + GELU incl. its activation quantiser (M=%d, N=3072, K=768; "
+                            "gemm_bf16_tn_p8<3, FP8>), " if fp8 else
+                            "BERT FFN1 GEMM + GELU (M=%d, N=3072, K=768; tuned variant), ") % M
+                           + "timed per launch with HIP events in a towers-in-sequence pass after the timed region"),
                 "ms_per_launch": ms_ffn1, "flops_per_launch": fl, "bert_gemms": fam, "knn": knn_roof}
     elif a.mode == "full":
         roof = dict(knn_roof, bound=knn_roof["bound"], unit="GB/s", achieved=knn_roof["achieved_gbs"],
@@ -354,7 +392,9 @@ def roofline(a, n, d, K, Qs, ms_search, ms_small, q_small, gemm_ms, B):
     # HBM traffic per launch from the committed PMC pass (tools/pmc_traffic.py; FETCH_SIZE x2 per the
     # gfx950 correction + WRITE_SIZE), for the same kernels at the same shapes
     tr = pmc_traffic()
-    if gemm_ms:
+    if gemm_ms and fp8:
+        roof["variant"] = "mxfp8"
+    elif gemm_ms:
         from mmr_amd import _lib
         var = int(_lib.lib().mmr_linear_bf16_variant(B * 128, 3072, 768, 1, 1, 0))
         roof["variant"] = var
@@ -486,7 +526,7 @@ def recall_vs_cpu(index, q_gpu, emb_cpu, G, K):
     return {"recall_at_k": float(np.mean(inter)), "k": K, "queries": int(len(ci)),
             "exact_list_match": float(np.mean([np.array_equal(gi[r], ci[r]) for r in range(len(ci))])),
             "min_embedding_cosine": float(cos.min()),
-            "note": "GPU bf16 towers + GPU exact kNN vs fp32 oracle towers + sklearn-path kNN, same inputs"}
+            "note": "GPU towers (bf16, or MX-fp8 linears at --tower-dtype fp8) + GPU exact kNN vs fp32 oracle towers + sklearn-path kNN, same inputs"}
 
 
 if __name__ == "__main__":

@@ -32,18 +32,24 @@ def _sub(sd, prefix):
 
 class Backbones:
     def __init__(self, img_backbone="swin", swin_state=None, bert_state=None, swin_cfg=None, bert_cfg=None,
-                 device="cuda", pretrained=False, seed=2709):
+                 device="cuda", pretrained=False, seed=2709, tower_dtype="bf16"):
+        """tower_dtype "bf16" (config 2) or "fp8" (config 5: MX-fp8 linears in all BERT layers and
+        Swin stages 3-4)."""
+        if tower_dtype not in ("bf16", "fp8"):
+            raise ValueError(f"tower_dtype {tower_dtype!r}: bf16 or fp8")
+        self.tower_dtype = tower_dtype
         if img_backbone != "swin":
             raise ValueError(f"image backbone {img_backbone!r} is outside the accelerated path (swin only)")
         self.img_backbone = img_backbone
         self.device = torch.device(device)
         swin_cfg = dict(SWIN_T, **(swin_cfg or {}))
         bert_cfg = dict(BERT_BASE, **(bert_cfg or {}))
+        fp8 = tower_dtype == "fp8"
         self.vision = SwinTower(swin_state if swin_state is not None else init_swin_state(swin_cfg, seed),
-                                swin_cfg, self.device)
+                                swin_cfg, self.device, fp8_stages=(2, 3) if fp8 else ())
         self.swin = self.vision
         self.bert = BertTower(bert_state if bert_state is not None else init_bert_state(bert_cfg, seed + 1),
-                              bert_cfg, self.device)
+                              bert_cfg, self.device, fp8=fp8)
         self.img_dim = self.vision.num_features
         self.txt_dim = self.bert.hidden
 
@@ -80,12 +86,13 @@ class Backbones:
 class MultiModalRetrievalModel:
     def __init__(self, joint_dim=256, num_heads=4, model_type="multimodal", use_shared_ffn=False,
                  use_cls_only=False, backbones=None, head_state=None, device="cuda", retriever=None,
-                 swin_cfg=None, bert_cfg=None, seed=2709):
+                 swin_cfg=None, bert_cfg=None, seed=2709, tower_dtype="bf16"):
         if model_type not in ("multimodal", "image", "text"):
             raise ValueError(f"Unknown model_type {model_type!r}")
         self.model_type = model_type
         self.device = torch.device(device)
-        self.backbones = backbones or Backbones(swin_cfg=swin_cfg, bert_cfg=bert_cfg, device=device, seed=seed)
+        self.backbones = backbones or Backbones(swin_cfg=swin_cfg, bert_cfg=bert_cfg, device=device, seed=seed,
+                                                tower_dtype=tower_dtype)
         self.joint_dim = joint_dim
         self.use_shared_ffn = use_shared_ffn
         self.use_cls_only = use_cls_only
@@ -265,11 +272,12 @@ def init_fusion_state(img_dim, txt_dim, joint_dim, num_heads=8, num_fusion_layer
 
 
 def build_bench_model(device="cuda", joint_dim=768, seed=2709, model_type="multimodal", num_heads=8,
-                      num_fusion_layers=5):
+                      num_fusion_layers=5, tower_dtype="bf16"):
     """Swin-Tiny + ClinicalBERT-base geometry, random init (no checkpoints offline); multimodal head
-    with configs/config.yaml's num_heads 8 / num_fusion_layers 5 at joint_dim 768."""
+    with configs/config.yaml's num_heads 8 / num_fusion_layers 5 at joint_dim 768 (config 5: 1024,
+    tower_dtype "fp8")."""
     hs = init_head_state(768, 768, joint_dim, seed + 2)
     if model_type == "multimodal":
         hs.update(init_fusion_state(768, 768, joint_dim, num_heads, num_fusion_layers, seed + 3))
     return MultiModalRetrievalModel(joint_dim=joint_dim, num_heads=num_heads, model_type=model_type,
-                                    head_state=hs, device=device, seed=seed)
+                                    head_state=hs, device=device, seed=seed, tower_dtype=tower_dtype)

@@ -35,11 +35,30 @@ def _f(t, dev):
     return t.detach().to(device=dev, dtype=torch.float32).contiguous()
 
 
-class SwinTower:
-    """timm SwinTransformer.forward_features semantics (see oracle/towers.py for the restatement)."""
+def _w8(w):
+    """nn.Linear weight (bf16, device) -> its MX-fp8 operand (quantised once, at load)."""
+    return ops.quantize_mxfp8(w, layout=1)
 
-    def __init__(self, sd, cfg=SWIN_T, device="cuda", fused_mlp=True, fused_attn=True):
+
+def _lin(x, w, b=None, residual=None, act=0, w8=None):
+    """nn.Linear through the bf16 GEMM, or through the MX-fp8 GEMM when the layer holds w8: the
+    activation is quantised per 32-block (mmr_quantize_mxfp8) and the block-scaled MFMA GEMM
+    applies bias / GELU / residual in f32 (BASELINE config 5's fp8 towers)."""
+    if w8 is None:
+        return ops.linear(x, w, b, residual=residual, act=act)
+    K = x.shape[-1]
+    x8 = ops.quantize_mxfp8(x.reshape(-1, K), layout=0, kp=w8.kp)
+    return ops.linear_mxfp8(x8, w8, b, residual, act=act, lead=tuple(x.shape[:-1]))
+
+
+class SwinTower:
+    """timm SwinTransformer.forward_features semantics (see oracle/towers.py for the restatement).
+    fp8_stages: stages whose linears (qkv, proj, fc1, fc2 and the incoming PatchMerging reduction)
+    run as MX-fp8 GEMMs (config 5 uses (2, 3); the batch must make B * tokens a multiple of 256)."""
+
+    def __init__(self, sd, cfg=SWIN_T, device="cuda", fused_mlp=True, fused_attn=True, fp8_stages=()):
         self.cfg = dict(SWIN_T, **cfg)
+        self.fp8_stages = tuple(fp8_stages)
         self.fused_mlp = fused_mlp
         self.fused_attn = fused_attn
         dev = torch.device(device)
@@ -61,6 +80,7 @@ class SwinTower:
                 p = f"layers.{i}.downsample."
                 st["ds_g"], st["ds_b"] = _f(sd[p + "norm.weight"], dev), _f(sd[p + "norm.bias"], dev)
                 st["ds_w"] = _bf(sd[p + "reduction.weight"], dev)
+                st["ds_w8"] = _w8(st["ds_w"]) if i in self.fp8_stages else None
             ws = min(ws0, res)
             for j in range(depth):
                 p = f"layers.{i}.blocks.{j}."
@@ -77,9 +97,12 @@ class SwinTower:
                     "fc2_w": _bf(sd[p + "mlp.fc2.weight"], dev), "fc2_b": _f(sd[p + "mlp.fc2.bias"], dev),
                 })
                 bk = st["blocks"][-1]
-                bk["mlp_pack"] = ops.swin_mlp_pack(bk["fc1_w"], bk["fc2_w"]) if self.fused_mlp else None
+                fp8 = i in self.fp8_stages
+                for n in ("qkv", "proj", "fc1", "fc2"):
+                    bk[n + "_w8"] = _w8(bk[n + "_w"]) if fp8 else None
+                bk["mlp_pack"] = ops.swin_mlp_pack(bk["fc1_w"], bk["fc2_w"]) if self.fused_mlp and not fp8 else None
                 bk["attn_pack"] = None
-                if self.fused_attn and E * 2 ** i == 96 and self.cfg["num_heads"][i] == 3 and ws == 7:
+                if self.fused_attn and not fp8 and E * 2 ** i == 96 and self.cfg["num_heads"][i] == 3 and ws == 7:
                     bk["attn_pack"] = ops.swin_attn_block_pack(bk["qkv_w"], bk["qkv_b"], bk["proj_w"], bk["proj_b"],
                                                                bk["n1g"], bk["n1b"])
             self.stages.append(st)
@@ -98,7 +121,7 @@ class SwinTower:
         ws0 = cfg["window_size"]
         for i, st in enumerate(self.stages):
             if i > 0:
-                x = ops.linear(ops.patch_merge_ln(x, st["ds_g"], st["ds_b"], 1e-5), st["ds_w"])
+                x = _lin(ops.patch_merge_ln(x, st["ds_g"], st["ds_b"], 1e-5), st["ds_w"], w8=st["ds_w8"])
             H = x.shape[1]
             C = x.shape[-1]
             heads = cfg["num_heads"][i]
@@ -108,15 +131,15 @@ class SwinTower:
                     x = ops.swin_attn_block(x, bk["attn_pack"], bk["bias"], ws, bk["shift"], 1e-5)
                 else:
                     h = ops.layernorm(x, bk["n1g"], bk["n1b"], 1e-5)
-                    qkv = ops.linear(h, bk["qkv_w"], bk["qkv_b"])
+                    qkv = _lin(h, bk["qkv_w"], bk["qkv_b"], w8=bk["qkv_w8"])
                     a = ops.swin_window_attention(qkv, bk["bias"], H, heads, ws, bk["shift"])
-                    x = ops.linear(a, bk["proj_w"], bk["proj_b"], residual=x)
+                    x = _lin(a, bk["proj_w"], bk["proj_b"], residual=x, w8=bk["proj_w8"])
                 if bk["mlp_pack"] is not None:
                     x = ops.swin_mlp(x, bk["n2g"], bk["n2b"], bk["mlp_pack"], bk["fc1_b"], bk["fc2_b"], 1e-5)
                 else:
                     h = ops.layernorm(x, bk["n2g"], bk["n2b"], 1e-5)
-                    h = ops.linear(h, bk["fc1_w"], bk["fc1_b"], act=1)
-                    x = ops.linear(h, bk["fc2_w"], bk["fc2_b"], residual=x)
+                    h = _lin(h, bk["fc1_w"], bk["fc1_b"], act=1, w8=bk["fc1_w8"])
+                    x = _lin(h, bk["fc2_w"], bk["fc2_b"], residual=x, w8=bk["fc2_w8"])
             del C
         return x
 
@@ -127,10 +150,12 @@ class SwinTower:
 
 
 class BertTower:
-    """HF BertModel(input_ids, attention_mask).last_hidden_state semantics (eval)."""
+    """HF BertModel(input_ids, attention_mask).last_hidden_state semantics (eval).  fp8: the four
+    linears of every layer run as MX-fp8 GEMMs (config 5; B * L must be a multiple of 256)."""
 
-    def __init__(self, sd, cfg=BERT_BASE, device="cuda"):
+    def __init__(self, sd, cfg=BERT_BASE, device="cuda", fp8=False):
         self.cfg = dict(BERT_BASE, **cfg)
+        self.fp8 = fp8
         dev = torch.device(device)
         self.device = dev
         self.word = _f(sd["embeddings.word_embeddings.weight"], dev)
@@ -152,6 +177,9 @@ class BertTower:
                 "f_w": _bf(sd[p + "output.dense.weight"], dev), "f_b": _f(sd[p + "output.dense.bias"], dev),
                 "ln2_g": _f(sd[p + "output.LayerNorm.weight"], dev), "ln2_b": _f(sd[p + "output.LayerNorm.bias"], dev),
             })
+            ly = self.layers[-1]
+            for n in ("qkv", "o", "i", "f"):
+                ly[n + "_w8"] = _w8(ly[n + "_w"]) if fp8 else None
         self.hidden = self.word.shape[1]
         # optional dict name -> list of (start, end) torch.cuda.Event pairs around every launch of the
         # four GEMMs of a layer ("qkv", "o", "ffn1", "ffn2"): the bench's per-kernel roofline (events
@@ -174,22 +202,22 @@ class BertTower:
         h = ops.bert_embed(ids, self.word, self.pos, self.type0, self.eg, self.eb, 1e-12)
         ev = self.gemm_events
 
-        def gemm(name, x, w, b, act=0):
+        def gemm(name, x, w, b, act=0, w8=None):
             if ev is None:
-                return ops.linear(x, w, b, act=act)
+                return _lin(x, w, b, act=act, w8=w8)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            y = ops.linear(x, w, b, act=act)
+            y = _lin(x, w, b, act=act, w8=w8)
             e1.record()
             ev.setdefault(name, []).append((e0, e1))
             return y
         for ly in self.layers:
-            qkv = gemm("qkv", h, ly["qkv_w"], ly["qkv_b"])
+            qkv = gemm("qkv", h, ly["qkv_w"], ly["qkv_b"], w8=ly["qkv_w8"])
             ctx = ops.bert_attention(qkv, mask, heads, self.hidden // heads)
-            a = gemm("o", ctx, ly["o_w"], ly["o_b"])
+            a = gemm("o", ctx, ly["o_w"], ly["o_b"], w8=ly["o_w8"])
             h = ops.add_layernorm(a, h, ly["ln1_g"], ly["ln1_b"], 1e-12)
-            f = gemm("ffn1", h, ly["i_w"], ly["i_b"], act=1)
-            f = gemm("ffn2", f, ly["f_w"], ly["f_b"])
+            f = gemm("ffn1", h, ly["i_w"], ly["i_b"], act=1, w8=ly["i_w8"])
+            f = gemm("ffn2", f, ly["f_w"], ly["f_b"], w8=ly["f_w8"])
             h = ops.add_layernorm(f, h, ly["ln2_g"], ly["ln2_b"], 1e-12)
         return h
 

@@ -127,3 +127,32 @@ def test_e2e_full_size_batch_256(model_type):
     G, gl = synthetic.labelled_gallery(100_000, 768, 53)
     overlap, mg, mc, rb, _ = _compare(q_gpu, q_cpu, G, _labels(nq, 54), synthetic.labels_to_bits(gl))
     _assert_parity(overlap, mg, mc, rb, q_gpu, q_cpu, min_overlap=0.95)
+
+
+def test_e2e_fp8_towers_joint1024_batch_256():
+    """BASELINE config 5's tower path at the reference's joint_dim 1024 (configs/config.yaml:14):
+    MX-fp8 linears in every BERT layer and Swin stages 3-4 (tower_dtype "fp8"), multimodal head, B=256
+    through query_embeddings; 24 queries against the fp32 oracle, top-10 over a 100k x 1024 labelled
+    gallery.  fp8 tolerance: e4m3 keeps 3 mantissa bits, so the embeddings drift further than bf16's:
+    min embedding cosine >= 0.99 and mean top-10 overlap >= 0.8 (measured on MI355X: 0.998 / 0.89,
+    identical P@10), P@10 / R@10 within the overlap bound as above."""
+    from mmr_amd.model import build_bench_model
+    m = build_bench_model(device=DEV, joint_dim=1024, model_type="multimodal", tower_dtype="fp8")
+    B, nq = 256, 24
+    img = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(B, 61)))
+    ids, mask = (torch.from_numpy(a) for a in synthetic.reports(B, 128, 62))
+    m.query_embeddings(img.to(DEV), ids.to(DEV), mask.to(DEV))
+    q_gpu = m.query_embeddings(img.to(DEV), ids.to(DEV), mask.to(DEV))[:nq]
+    ssd, bsd = init_swin_state(SWIN_T, 2709), init_bert_state(BERT_BASE, 2710)
+    hsd = init_head_state(768, 768, 1024, 2711)
+    hsd.update(init_fusion_state(768, 768, 1024, 8, 5, 2712))
+    with torch.no_grad():
+        (g, p), t = otw.backbones_forward(img[:nq], ids[:nq], mask[:nq], ssd, bsd, SWIN_T, BERT_BASE)
+        q_cpu = otw.heads(g, p, t, hsd, "multimodal", mm_cfg={"num_heads": 8})["joint_emb"].numpy()
+    G, gl = synthetic.labelled_gallery(100_000, 1024, 63)
+    overlap, mg, mc, rb, _ = _compare(q_gpu, q_cpu, G, _labels(nq, 64), synthetic.labels_to_bits(gl))
+    a = q_gpu.float().cpu().numpy()
+    cos = np.sum(a * q_cpu, 1) / (np.linalg.norm(a, axis=1) * np.linalg.norm(q_cpu, axis=1))
+    print(json.dumps({"fp8_min_cosine": float(cos.min()), "fp8_mean_cosine": float(cos.mean())}))
+    assert cos.min() >= 0.99
+    _assert_parity(overlap, mg, mc, rb, q_gpu, q_cpu, min_overlap=0.8)
