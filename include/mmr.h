@@ -128,18 +128,19 @@ int32_t mmr_linear_bf16_variant(int64_t m, int32_t n, int32_t k, int32_t act, in
  * E8M0 scale per 32 consecutive k of a row: 2^e, the smallest e with amax <= 448 * 2^e (no clipping);
  * q = RNE(x * 2^-e).  The scale bytes are written in the GEMM's per-lane LDS image order:
  * layout 0 (activations, rows % 256 == 0): [rows/256][kp/128][2][4][16][8] (1 byte per row-block);
- * layout 1 (weights, rows % 192 == 0): [rows/192][kp/128][4][4][16][4] = rows/192 * kp/128 * 1024
- * bytes.  Replaces the bf16 operand of the Swin / BERT nn.Linear (fusion.py:198-199, 322-325) on the
+ * layouts 1 / 2 (weights, rows % 192 / 256 == 0, for 256 x 192 / 256 x 256 GEMM tiles):
+ * [rows/PR][kp/128][4][4][16][4] = rows/PR * kp/128 * 1024 bytes (PR = 192 / 256).  Replaces the bf16 operand of the Swin / BERT nn.Linear (fusion.py:198-199, 322-325) on the
  * fp8 tower path. */
 mmr_status mmr_quantize_mxfp8(const uint16_t* x, int64_t rows, int32_t k, int32_t kp, int32_t layout,
                               uint8_t* q, uint8_t* scales, void* stream);
 
 /* Y[m][n] = act(dequant(Xq) . dequant(Wq)^T + bias[n]) (+ R[m][n]) with gfx950 block-scaled MFMA
  * (v_mfma_scale_f32_16x16x128_f8f6f4, e4m3 x e4m3, f32 accumulation); Xq/xs from layout 0, Wq/ws
- * from layout 1 of mmr_quantize_mxfp8; Y, R bf16.  m % 256 == 0, n % 192 == 0, kp % 256 == 0. */
+ * from layout w_layout (1 or 2) of mmr_quantize_mxfp8; Y, R bf16.  m % 256 == 0, kp % 256 == 0,
+ * n % 192 == 0 (w_layout 1) or n % 256 == 0 (w_layout 2). */
 mmr_status mmr_linear_mxfp8(const uint8_t* xq, const uint8_t* xs, const uint8_t* wq, const uint8_t* ws,
-                            const float* bias, const uint16_t* residual, uint16_t* y, int64_t m,
-                            int32_t n, int32_t kp, int32_t act, void* stream);
+                            int32_t w_layout, const float* bias, const uint16_t* residual, uint16_t* y,
+                            int64_t m, int32_t n, int32_t kp, int32_t act, void* stream);
 
 /* Row LayerNorm over c channels (bf16 in/out, f32 math, gamma/beta f32). */
 mmr_status mmr_layernorm_bf16(const uint16_t* x, const float* gamma, const float* beta,

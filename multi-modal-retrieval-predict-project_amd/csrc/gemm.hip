@@ -526,7 +526,12 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
 #if defined(__HIP_DEVICE_COMPILE__)  // buffer-descriptor builtins exist in the device pass only
   using C = P8<NT, FP8>;
   constexpr int KB = 64, TBN = C::TBN;                  // KB: 128-byte LDS rows (64 bf16 / 128 fp8)
-  constexpr int TA = 256 * KB, BUF = (256 + TBN) * KB + C::SC;  // uint16 elements: A part, buffer
+  constexpr int TA = 256 * KB, TB = TBN * KB, BUF = TA + TB + C::SC;  // uint16 elements per K-tile buffer
+  // LDS image: [A_E | A_O | B_E | B_O | S_E | S_O] — the two buffers of an operand 32 KB apart, so one
+  // base register per (operand, k-step) reaches both through the ds_read immediate offset
+  auto aoff = [](int buf) { return buf * TA; };
+  auto boff = [](int buf) { return 2 * TA + buf * TB; };
+  auto soff = [](int buf) { return 2 * (TA + TB) + buf * C::SC; };
   constexpr int ESZ = FP8 ? 1 : 2;                      // operand element bytes
   constexpr int NH0 = NT / 2;                           // n-tiles in n-half 0
   static_assert(C::NSTORE + 5 <= 63, "vmcnt range");
@@ -555,18 +560,12 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   // glds: piece j of an operand stages LDS rows 64j + 8 wave + lane/8, physical chunk lane%8 <-
   // logical chunk swz(row, lane%8); per-lane byte offsets are tile-independent, a tile contributes
   // uniform bases only
+  // piece j's rows are 64 j + (piece 0's rows) and the swizzle depends on (row >> 1) & 7 only, so
+  // one per-lane offset serves every piece of an operand: 64 j rows go into the uniform soffset
   const int prow = lane >> 3, pch = lane & 7;
-  uint32_t offA[4], offB[NT];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int row = 64 * j + 8 * wave + prow;
-    offA[j] = (uint32_t)(row * K * ESZ + swz(row, pch) * 16);
-  }
-#pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    const int row = 64 * j + 8 * wave + prow;
-    offB[j] = (uint32_t)(row * K * ESZ + swz(row, pch) * 16);
-  }
+  const int row0 = 8 * wave + prow;
+  const uint32_t off0 = (uint32_t)(row0 * K * ESZ + swz(row0, pch) * 16);
+  const uint32_t pstride = (uint32_t)(64 * K * ESZ);  // bytes between consecutive pieces of an operand
   const int nk = K * ESZ / 128;  // 128-byte K-tiles; even (launcher)
   // operand panels as buffer descriptors (uniform, SGPRs): a piece is buffer_load ... lds with the
   // per-lane offset in voffset and the K-tile offset in soffset — no per-piece address registers
@@ -583,36 +582,34 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   auto gS = [&](int tile, int buf, int kt) {
     if constexpr (FP8) {
       if (wave == 0)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xsr, (lds_ptr_t)(dsm + buf * BUF + (256 + TBN) * KB), 16, lane * 16,
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xsr, (lds_ptr_t)(dsm + soff(buf)), 16, lane * 16,
                                                  ((tile / tiles_n) * nk + kt) * 1024, 0, 0);
       else if (wave == 1)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(wsr, (lds_ptr_t)(dsm + buf * BUF + (256 + TBN) * KB + 512), 16, lane * 16,
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wsr, (lds_ptr_t)(dsm + soff(buf) + 512), 16, lane * 16,
                                                  ((tile % tiles_n) * nk + kt) * 1024, 0, 0);
     }
   };
   auto gA = [&](__amdgpu_buffer_rsrc_t xb, int buf, int j, int kt) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(xb, (lds_ptr_t)(dsm + buf * BUF + (64 * j + 8 * wave) * KB), 16, offA[j],
-                                             kt * (KB * 2), 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(xb, (lds_ptr_t)(dsm + aoff(buf) + (64 * j + 8 * wave) * KB), 16, off0,
+                                             kt * (KB * 2) + j * pstride, 0, 0);
   };
   auto gB = [&](__amdgpu_buffer_rsrc_t wb, int buf, int j, int kt) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(wb, (lds_ptr_t)(dsm + buf * BUF + TA + (64 * j + 8 * wave) * KB), 16, offB[j],
-                                             kt * (KB * 2), 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wb, (lds_ptr_t)(dsm + boff(buf) + (64 * j + 8 * wave) * KB), 16, off0,
+                                             kt * (KB * 2) + j * pstride, 0, 0);
   };
   // fragment reads: the swizzle of row 16i + fr is a function of fr only, so every A (B) fragment
   // address is one of two per-lane bases (k-step 0 / 1: logical chunk fq or 4 + fq) plus an
   // immediate offset (buffer, tile) — 4 + 4 address registers instead of one per fragment
   const int xs = fq ^ ((fr >> 1) & 7);
-  const uint16_t* pa[2][2];
-  const uint16_t* pb[2][2];
+  const uint16_t* pa[2];
+  const uint16_t* pb[2];
 #pragma unroll
-  for (int bf = 0; bf < 2; ++bf)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      pa[bf][ks] = dsm + bf * BUF + (wr * 128 + fr) * KB + (xs ^ (4 * ks)) * 8;
-      pb[bf][ks] = dsm + bf * BUF + TA + (wc * 16 * NT + fr) * KB + (xs ^ (4 * ks)) * 8;
-    }
-  auto rdA = [&](int buf, int ks, int i) { return *(const bf16x8*)(pa[buf][ks] + i * 16 * KB); };
-  auto rdB = [&](int buf, int ks, int j) { return *(const bf16x8*)(pb[buf][ks] + j * 16 * KB); };
+  for (int ks = 0; ks < 2; ++ks) {
+    pa[ks] = dsm + (wr * 128 + fr) * KB + (xs ^ (4 * ks)) * 8;
+    pb[ks] = dsm + 2 * TA + (wc * 16 * NT + fr) * KB + (xs ^ (4 * ks)) * 8;
+  }
+  auto rdA = [&](int buf, int ks, int i) { return *(const bf16x8*)(pa[ks] + buf * TA + i * 16 * KB); };
+  auto rdB = [&](int buf, int ks, int j) { return *(const bf16x8*)(pb[ks] + buf * TB + j * 16 * KB); };
   bf16x8 fa[4][2], fb0[NH0][2], fb1[NT - NH0][2];
   i32x8 fa8[4], fb08[NH0], fb18[NT - NH0];  // FP8: the two 16-byte chunks of a fragment, contiguous
   auto ldA = [&](int buf, int i, int mt) {
@@ -699,7 +696,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
         // ---- load segment (s = 2p)
         if (q == 0) {
           if constexpr (FP8) {
-            const uint8_t* sb = (const uint8_t*)(dsm + buf * BUF + (256 + TBN) * KB);
+            const uint8_t* sb = (const uint8_t*)(dsm + soff(buf));
             const uint2 sa2 = *(const uint2*)(sb + ((wr * 4 + fq) * 16 + fr) * 8);
             sca[0] = sa2.x;
             sca[1] = sa2.y;
@@ -1086,38 +1083,41 @@ __global__ __launch_bounds__(256) void gemm_bf16_tn_w4(const uint16_t* __restric
 // the order the GEMM's per-lane LDS scale image wants (1 KB per operand panel and 128-k K-tile):
 //   LAYOUT 0 (X, panels of 256 rows): [panel][kt][wr 2][fq 4][fr 16][i 8], row = 128 wr + 16 i + fr
 //   LAYOUT 1 (W, panels of 192 rows): [panel][kt][wc 4][fq 4][fr 16][j 4], row = 48 wc + 16 j + fr
-// (fq = the 32-block within the K-tile).  One thread per 8 values, 4 threads per block.
+// (fq = the 32-block within the K-tile).
 template <int LAYOUT>
 __global__ __launch_bounds__(256) void quantize_mxfp8(const uint16_t* __restrict__ x, int64_t rows, int k,
                                                       int kp, uint8_t* __restrict__ q, uint8_t* __restrict__ sc) {
+  // one thread per 16 values (two 16-B bf16 loads, one 16-B fp8 store), 2 threads per 32-block
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int c8n = kp / 8;
-  const int64_t row = t / c8n;
-  const int k0 = (int)(t % c8n) * 8;
+  const int c16n = kp / 16;
+  const int64_t row = t / c16n;
+  const int k0 = (int)(t % c16n) * 16;
   const bool ok = row < rows;
   const int64_t rc = ok ? row : rows - 1;
-  const int kc = k0 < k ? k0 : k - 8;
-  const bf16x8 raw = *(const bf16x8*)(x + rc * k + kc);  // unconditional (clamped), masked below
-  float v[8];
+  const int ka = k0 < k ? k0 : k - 8, kb = k0 + 8 < k ? k0 + 8 : k - 8;
+  const bf16x8 r0 = *(const bf16x8*)(x + rc * k + ka);  // unconditional (clamped), masked below
+  const bf16x8 r1 = *(const bf16x8*)(x + rc * k + kb);
+  float v[16];
   float amax = 0.f;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    v[e] = k0 < k ? mmr::bf2f((uint16_t)raw[e]) : 0.f;
-    amax = fmaxf(amax, fabsf(v[e]));
+    v[e] = k0 < k ? mmr::bf2f((uint16_t)r0[e]) : 0.f;
+    v[8 + e] = k0 + 8 < k ? mmr::bf2f((uint16_t)r1[e]) : 0.f;
+    amax = fmaxf(amax, fmaxf(fabsf(v[e]), fabsf(v[8 + e])));
   }
   amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
-  amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
   const uint32_t ab = __float_as_uint(amax);
   int ex = (int)((ab >> 23) & 255) - 127 - 8 + ((ab & 0x7FFFFF) > 0x600000 ? 1 : 0);
   ex = ex < -127 ? -127 : (ex > 126 ? 126 : ex);
   const float inv = __uint_as_float((uint32_t)(127 - ex) << 23);  // 2^-ex, exact
-  uint32_t lo = 0, hi = 0;
-  lo = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[0] * inv, v[1] * inv, (int)lo, false);
-  lo = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[2] * inv, v[3] * inv, (int)lo, true);
-  hi = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[4] * inv, v[5] * inv, (int)hi, false);
-  hi = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[6] * inv, v[7] * inv, (int)hi, true);
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    w[i] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[4 * i] * inv, v[4 * i + 1] * inv, 0, false);
+    w[i] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[4 * i + 2] * inv, v[4 * i + 3] * inv, (int)w[i], true);
+  }
   if (!ok) return;
-  *(uint2*)(q + row * kp + k0) = make_uint2(lo, hi);
+  *(uint4*)(q + row * kp + k0) = make_uint4(w[0], w[1], w[2], w[3]);
   if ((k0 & 31) == 0) {
     const int blk = k0 / 32, kt = blk / 4, fq = blk % 4;
     int64_t off;
@@ -1125,9 +1125,10 @@ __global__ __launch_bounds__(256) void quantize_mxfp8(const uint16_t* __restrict
       const int64_t P = row / 256;
       const int rr = (int)(row % 256), wr = rr / 128, i = (rr % 128) / 16, fr = rr % 16;
       off = (P * (kp / 128) + kt) * 1024 + ((wr * 4 + fq) * 16 + fr) * 8 + i;
-    } else {
-      const int64_t P = row / 192;
-      const int rr = (int)(row % 192), wc = rr / 48, j = (rr % 48) / 16, fr = rr % 16;
+    } else {  // weights: panels of 64 NT rows (NT = 3 for layout 1, 4 for layout 2)
+      constexpr int PR = LAYOUT == 1 ? 192 : 256, WT = PR / 4;
+      const int64_t P = row / PR;
+      const int rr = (int)(row % PR), wc = rr / WT, j = (rr % WT) / 16, fr = rr % 16;
       off = (P * (kp / 128) + kt) * 1024 + ((wc * 4 + fq) * 16 + fr) * 4 + j;
     }
     sc[off] = (uint8_t)(ex + 127);
@@ -1346,37 +1347,46 @@ extern "C" mmr_status mmr_quantize_mxfp8(const uint16_t* x, int64_t rows, int32_
                                          uint8_t* q, uint8_t* scales, void* stream) {
   mmr::clear_error();
   MMR_REQUIRE(x && q && scales, "mmr_quantize_mxfp8: NULL pointer");
-  MMR_REQUIRE(layout == 0 || layout == 1, "mmr_quantize_mxfp8: layout=%d (0: X panels of 256 rows, 1: W panels of 192)", layout);
-  MMR_REQUIRE(rows > 0 && rows % (layout == 0 ? 256 : 192) == 0, "mmr_quantize_mxfp8: rows=%lld must be a multiple of %d",
-              (long long)rows, layout == 0 ? 256 : 192);
+  MMR_REQUIRE(layout >= 0 && layout <= 2, "mmr_quantize_mxfp8: layout=%d (0: X panels of 256 rows, 1 / 2: W panels of 192 / 256)", layout);
+  const int pr = layout == 1 ? 192 : 256;
+  MMR_REQUIRE(rows > 0 && rows % pr == 0, "mmr_quantize_mxfp8: rows=%lld must be a multiple of %d", (long long)rows, pr);
   MMR_REQUIRE(k > 0 && k % 8 == 0 && kp >= k && kp % 256 == 0, "mmr_quantize_mxfp8: k=%d kp=%d (k %% 8 == 0, kp >= k, kp %% 256 == 0)", k, kp);
-  const int64_t threads = rows * (kp / 8);
+  const int64_t threads = rows * (kp / 16);
   hipStream_t st = mmr::as_stream(stream);
-  if (layout == 0)
-    quantize_mxfp8<0><<<dim3((unsigned)mmr::ceil_div(threads, 256)), dim3(256), 0, st>>>(x, rows, k, kp, q, scales);
-  else
-    quantize_mxfp8<1><<<dim3((unsigned)mmr::ceil_div(threads, 256)), dim3(256), 0, st>>>(x, rows, k, kp, q, scales);
+  const dim3 grid((unsigned)mmr::ceil_div(threads, 256));
+  if (layout == 0) quantize_mxfp8<0><<<grid, dim3(256), 0, st>>>(x, rows, k, kp, q, scales);
+  else if (layout == 1) quantize_mxfp8<1><<<grid, dim3(256), 0, st>>>(x, rows, k, kp, q, scales);
+  else quantize_mxfp8<2><<<grid, dim3(256), 0, st>>>(x, rows, k, kp, q, scales);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }
 
 extern "C" mmr_status mmr_linear_mxfp8(const uint8_t* xq, const uint8_t* xs, const uint8_t* wq, const uint8_t* ws,
-                                       const float* bias, const uint16_t* residual, uint16_t* y, int64_t m, int32_t n,
-                                       int32_t kp, int32_t act, void* stream) {
+                                       int32_t w_layout, const float* bias, const uint16_t* residual, uint16_t* y,
+                                       int64_t m, int32_t n, int32_t kp, int32_t act, void* stream) {
   mmr::clear_error();
   MMR_REQUIRE(xq && xs && wq && ws && y, "mmr_linear_mxfp8: NULL pointer");
+  MMR_REQUIRE(w_layout == 1 || w_layout == 2, "mmr_linear_mxfp8: w_layout=%d (1: 192-row W panels, 2: 256-row)", w_layout);
+  const int tbn = w_layout == 1 ? 192 : 256;
   MMR_REQUIRE(m > 0 && m % 256 == 0, "mmr_linear_mxfp8: m=%lld must be a positive multiple of 256", (long long)m);
-  MMR_REQUIRE(n > 0 && n % 192 == 0, "mmr_linear_mxfp8: n=%d must be a positive multiple of 192", n);
+  MMR_REQUIRE(n > 0 && n % tbn == 0, "mmr_linear_mxfp8: n=%d must be a positive multiple of %d", n, tbn);
   MMR_REQUIRE(kp > 0 && kp % 256 == 0, "mmr_linear_mxfp8: kp=%d must be a positive multiple of 256", kp);
   MMR_REQUIRE(act == 0 || act == 1, "mmr_linear_mxfp8: act=%d", act);
   hipStream_t st = mmr::as_stream(stream);
-  const int tm = (int)(m / 256), tn = n / 192;
+  const int tm = (int)(m / 256), tn = n / tbn;
   const int grid = (int)std::max<int64_t>(8, std::min<int64_t>(std::max(8, cu_count() / 8 * 8), (int64_t)tm * tn) / 8 * 8);
   const bool hb = bias != nullptr, hr = residual != nullptr;
   const uint16_t* X = (const uint16_t*)xq;
   const uint16_t* W = (const uint16_t*)wq;
-#define MX_LAUNCH(A, B, R) \
-  gemm_bf16_tn_p8<3, A, B, R, true><<<dim3(grid), dim3(512), P8<3, true>::LDS_B, st>>>(X, W, bias, residual, y, m, n, kp, tm, tn, xs, ws)
+#define MX_LAUNCH(A, B, R)                                                                                         \
+  do {                                                                                                               \
+    if (w_layout == 1)                                                                                               \
+      gemm_bf16_tn_p8<3, A, B, R, true><<<dim3(grid), dim3(512), P8<3, true>::LDS_B, st>>>(X, W, bias, residual, y, m, \
+                                                                                          n, kp, tm, tn, xs, ws);    \
+    else                                                                                                             \
+      gemm_bf16_tn_p8<4, A, B, R, true><<<dim3(grid), dim3(512), P8<4, true>::LDS_B, st>>>(X, W, bias, residual, y, m, \
+                                                                                          n, kp, tm, tn, xs, ws);    \
+  } while (0)
   if (act == 0) {
     if (hb && hr) MX_LAUNCH(0, true, true);
     else if (hb) MX_LAUNCH(0, true, false);

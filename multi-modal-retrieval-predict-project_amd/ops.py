@@ -45,13 +45,14 @@ class MXFP8:
 
 
 def quantize_mxfp8(x, layout=0, kp=None):
-    """bf16 (..., k) -> MXFP8 (rows = prod of leading dims; rows % 256 == 0 for layout 0, % 192 for 1)."""
+    """bf16 (..., k) -> MXFP8 (rows = prod of leading dims; rows % 256 == 0 for layouts 0 / 2, % 192 for
+    layout 1).  Weights: layout 2 (256-row panels, 256 x 256 GEMM tiles) when N % 256 == 0, else 1."""
     _lib.require_gpu(x)
     k = x.shape[-1]
     rows = x.numel() // k
     kp = kp or -(-k // 256) * 256
     q = torch.empty((rows, kp), dtype=torch.uint8, device=x.device)
-    pr = 256 if layout == 0 else 192
+    pr = 192 if layout == 1 else 256
     nsc = (rows // pr) * (kp // 128) * 1024 if rows % pr == 0 else 0
     s = torch.zeros((max(nsc, 1),), dtype=torch.uint8, device=x.device)
     _chk(_L().mmr_quantize_mxfp8(_lib.ptr(x), rows, k, kp, layout, _lib.ptr(q), _lib.ptr(s), _s(x)),
@@ -62,11 +63,11 @@ def quantize_mxfp8(x, layout=0, kp=None):
 def linear_mxfp8(x8, w8, bias=None, residual=None, act=0, out=None, lead=None):
     """act(deq(x8) @ deq(w8).T + bias) (+ residual) -> bf16 (rows, N) (or lead + (N,))."""
     _lib.require_gpu(x8.q)
-    assert x8.layout == 0 and w8.layout == 1 and x8.kp == w8.kp, "operand layouts / padded K disagree"
+    assert x8.layout == 0 and w8.layout in (1, 2) and x8.kp == w8.kp, "operand layouts / padded K disagree"
     M, N = x8.q.shape[0], w8.q.shape[0]
     shape = (lead if lead is not None else (M,)) + (N,)
     y = out if out is not None else torch.empty(shape, dtype=torch.bfloat16, device=x8.q.device)
-    _chk(_L().mmr_linear_mxfp8(_lib.ptr(x8.q), _lib.ptr(x8.s), _lib.ptr(w8.q), _lib.ptr(w8.s), _lib.ptr(bias),
+    _chk(_L().mmr_linear_mxfp8(_lib.ptr(x8.q), _lib.ptr(x8.s), _lib.ptr(w8.q), _lib.ptr(w8.s), w8.layout, _lib.ptr(bias),
                                _lib.ptr(residual), _lib.ptr(y), M, N, x8.kp, act, _s(x8.q)), "mmr_linear_mxfp8")
     return y
 

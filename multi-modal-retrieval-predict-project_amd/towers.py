@@ -35,9 +35,11 @@ def _f(t, dev):
     return t.detach().to(device=dev, dtype=torch.float32).contiguous()
 
 
-def _w8(w):
-    """nn.Linear weight (bf16, device) -> its MX-fp8 operand (quantised once, at load)."""
-    return ops.quantize_mxfp8(w, layout=1)
+def _w8(w, plain=False):
+    """nn.Linear weight (bf16, device) -> its MX-fp8 operand (quantised once, at load).  plain: the
+    layer's GEMM has no GELU / residual epilogue, so it can take 256 x 256 tiles (weight panels of 256
+    rows, layout 2) when N % 256 == 0; the GELU / residual epilogues keep 256 x 192 (layout 1)."""
+    return ops.quantize_mxfp8(w, layout=2 if plain and w.shape[0] % 256 == 0 else 1)
 
 
 def _lin(x, w, b=None, residual=None, act=0, w8=None):
@@ -80,7 +82,7 @@ class SwinTower:
                 p = f"layers.{i}.downsample."
                 st["ds_g"], st["ds_b"] = _f(sd[p + "norm.weight"], dev), _f(sd[p + "norm.bias"], dev)
                 st["ds_w"] = _bf(sd[p + "reduction.weight"], dev)
-                st["ds_w8"] = _w8(st["ds_w"]) if i in self.fp8_stages else None
+                st["ds_w8"] = _w8(st["ds_w"], plain=True) if i in self.fp8_stages else None
             ws = min(ws0, res)
             for j in range(depth):
                 p = f"layers.{i}.blocks.{j}."
@@ -99,7 +101,7 @@ class SwinTower:
                 bk = st["blocks"][-1]
                 fp8 = i in self.fp8_stages
                 for n in ("qkv", "proj", "fc1", "fc2"):
-                    bk[n + "_w8"] = _w8(bk[n + "_w"]) if fp8 else None
+                    bk[n + "_w8"] = _w8(bk[n + "_w"], plain=n == "qkv") if fp8 else None
                 bk["mlp_pack"] = ops.swin_mlp_pack(bk["fc1_w"], bk["fc2_w"]) if self.fused_mlp and not fp8 else None
                 bk["attn_pack"] = None
                 if self.fused_attn and not fp8 and E * 2 ** i == 96 and self.cfg["num_heads"][i] == 3 and ws == 7:
@@ -179,7 +181,7 @@ class BertTower:
             })
             ly = self.layers[-1]
             for n in ("qkv", "o", "i", "f"):
-                ly[n + "_w8"] = _w8(ly[n + "_w"]) if fp8 else None
+                ly[n + "_w8"] = _w8(ly[n + "_w"], plain=n != "i") if fp8 else None
         self.hidden = self.word.shape[1]
         # optional dict name -> list of (start, end) torch.cuda.Event pairs around every launch of the
         # four GEMMs of a layer ("qkv", "o", "ffn1", "ffn2"): the bench's per-kernel roofline (events

@@ -10,7 +10,7 @@ quantize(x)      -> (q values as f32 on the e4m3 grid, scale exponents e) per ro
                     step 2^-9; |x * 2^-e| <= 448 so nothing saturates).
 dequantize       q * 2^e.
 scale_offsets    (row, block) -> byte offset of the scale in the GEMM's LDS-image order (layout 0:
-                 activations, panels of 256 rows; layout 1: weights, panels of 192 rows)."""
+                 activations, panels of 256 rows; layouts 1 / 2: weights, panels of 192 / 256 rows)."""
 import numpy as np
 
 
@@ -57,8 +57,10 @@ def scale_offsets(rows, kp, layout):
         P, rr = r // 256, r % 256
         wr, i, fr = rr // 128, (rr % 128) // 16, rr % 16
         return (P * (kp // 128) + kt) * 1024 + ((wr * 4 + fq) * 16 + fr) * 8 + i
-    P, rr = r // 192, r % 192
-    wc, j, fr = rr // 48, (rr % 48) // 16, rr % 16
+    pr = 192 if layout == 1 else 256          # weight panels: 256 x 192 (1) or 256 x 256 (2) GEMM tiles
+    wt = pr // 4
+    P, rr = r // pr, r % pr
+    wc, j, fr = rr // wt, (rr % wt) // 16, rr % 16
     return (P * (kp // 128) + kt) * 1024 + ((wc * 4 + fq) * 16 + fr) * 4 + j
 
 

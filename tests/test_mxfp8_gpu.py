@@ -35,7 +35,7 @@ def _decode(x8, rows, layout):
     return q, e
 
 
-@pytest.mark.parametrize("rows,k,layout", [(256, 768, 0), (512, 384, 0), (384, 768, 1), (192, 3072, 1)])
+@pytest.mark.parametrize("rows,k,layout", [(256, 768, 0), (512, 384, 0), (384, 768, 1), (192, 3072, 1), (512, 768, 2)])
 def test_quantize_bit_exact(rows, k, layout):
     xt, xf = _bf16_input(rows, k, 11 + rows + k)
     x8 = ops.quantize_mxfp8(xt.to(DEV), layout=layout)
@@ -49,7 +49,7 @@ def test_quantize_bit_exact(rows, k, layout):
 
 def _ref(x8, w8, rows, n, bias, res, act):
     qx, ex = _decode(x8, rows, 0)
-    qw, ew = _decode(w8, n, 1)
+    qw, ew = _decode(w8, n, w8.layout)
     y = mx.dequantize(qx, ex) @ mx.dequantize(qw, ew).T
     if bias is not None:
         y = y + bias.cpu().numpy().astype(np.float64)[None, :]
@@ -60,14 +60,17 @@ def _ref(x8, w8, rows, n, bias, res, act):
     return y
 
 
-@pytest.mark.parametrize("M,N,K,act,res", [(256, 192, 768, 0, False), (512, 384, 384, 1, False),
-                                           (1024, 576, 768, 0, True), (8192, 2304, 768, 0, False),
-                                           (4096, 768, 3072, 0, True), (2048, 3072, 768, 1, False)])
-def test_linear_mxfp8_matches_dequantised_gemm(M, N, K, act, res):
+@pytest.mark.parametrize("M,N,K,act,res,wl", [(256, 192, 768, 0, False, 1), (512, 384, 384, 1, False, 1),
+                                              (1024, 576, 768, 0, True, 1), (8192, 2304, 768, 0, False, 1),
+                                              (4096, 768, 3072, 0, True, 1), (2048, 3072, 768, 1, False, 1),
+                                              (256, 256, 768, 0, False, 2), (8192, 2304, 768, 0, False, 2),
+                                              (4096, 768, 3072, 0, False, 2), (1024, 512, 512, 1, True, 2)])
+def test_linear_mxfp8_matches_dequantised_gemm(M, N, K, act, res, wl):
+    """wl: weight layout 1 (256 x 192 tiles) or 2 (256 x 256 tiles)."""
     xt, _ = _bf16_input(M, K, 7 + M)
     wt, _ = _bf16_input(N, K, 8 + N, zero_block=False)
     x8 = ops.quantize_mxfp8(xt.to(DEV), layout=0)
-    w8 = ops.quantize_mxfp8((wt * 0.05).to(DEV), layout=1)
+    w8 = ops.quantize_mxfp8((wt * 0.05).to(DEV), layout=wl)
     g = torch.Generator().manual_seed(M + N)
     bias = torch.randn(N, generator=g).to(DEV)
     r = (torch.randn(M, N, generator=g) * 3).to(torch.bfloat16).to(DEV) if res else None

@@ -30,7 +30,7 @@ for M, N, K, act in SHAPES:
     x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
     w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16)
     b = torch.randn(N, device="cuda")
-    w8 = ops.quantize_mxfp8(w, layout=1)
+    w8 = ops.quantize_mxfp8(w, layout=2 if (N % 256 == 0 and not act) else 1)
     x8 = ops.quantize_mxfp8(x, layout=0)
     y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     t_bf = timeit(lambda: ops.linear(x, w, b, act=act, out=y))
