@@ -142,6 +142,13 @@ mmr_status mmr_linear_mxfp8(const uint8_t* xq, const uint8_t* xs, const uint8_t*
                             int32_t w_layout, const float* bias, const uint16_t* residual, uint16_t* y,
                             int64_t m, int32_t n, int32_t kp, int32_t act, void* stream);
 
+/* mmr_linear_mxfp8 (weights in layout 2, no residual) whose output is written directly as the next
+ * GEMM's MX-fp8 activation operand: yq [m][n] e4m3 + ys layout-0 scales (m/256 * n/128 * 1024 bytes),
+ * bit-identical to mmr_quantize_mxfp8 of the bf16 output (BERT FFN1 -> FFN2, Swin fc1 -> fc2). */
+mmr_status mmr_linear_mxfp8_q8(const uint8_t* xq, const uint8_t* xs, const uint8_t* wq, const uint8_t* ws,
+                               const float* bias, uint8_t* yq, uint8_t* ys, int64_t m, int32_t n,
+                               int32_t kp, int32_t act, void* stream);
+
 /* Row LayerNorm over c channels (bf16 in/out, f32 math, gamma/beta f32). */
 mmr_status mmr_layernorm_bf16(const uint16_t* x, const float* gamma, const float* beta,
                               uint16_t* y, int64_t rows, int32_t c, float eps, void* stream);

@@ -34,6 +34,7 @@ SIGNATURES = {
     "mmr_linear_bf16_variant": [c_i64, c_i32, c_i32, c_i32, c_i32, c_i32],
     "mmr_quantize_mxfp8": [c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp],
     "mmr_linear_mxfp8": [c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp],
+    "mmr_linear_mxfp8_q8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp],
     "mmr_layernorm_bf16": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp],
     "mmr_add_layernorm_bf16": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp],
     "mmr_scaled_add_layernorm_bf16": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp],

@@ -514,7 +514,11 @@ struct P8 {
 // (tools/mfma_fp8_probe.hip, exact on integer data): lane (r = l%16, g = l/16) holds k = 16g..16g+15
 // and 64+16g..64+16g+15 of row r — the two 16-byte chunks the bf16 form reads as k-steps 0 / 1 —
 // and supplies the scale of row r, k-block g.
-template <int NT, int ACT, bool HAS_BIAS, bool HAS_RES, bool FP8 = false>
+// OUT8 (FP8, NT = 4, no residual): the output is written as the NEXT GEMM's MX-fp8 activation
+// operand — e4m3 bytes [M][N] (Y reinterpreted) + E8M0 scales in the layout-0 image (YS) — instead of
+// bf16: each lane takes 16 values of one staged bf16 row, the 32-block max is one lane swap, so the
+// result is bit-identical to mmr_quantize_mxfp8 of the bf16 output (same per-round store count).
+template <int NT, int ACT, bool HAS_BIAS, bool HAS_RES, bool FP8 = false, bool OUT8 = false>
 __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restrict__ X,
                                                        const uint16_t* __restrict__ W,
                                                        const float* __restrict__ bias,
@@ -522,7 +526,9 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
                                                        uint16_t* __restrict__ Y, int64_t M, int N,
                                                        int K, int tiles_m, int tiles_n,
                                                        const uint8_t* __restrict__ XS = nullptr,
-                                                       const uint8_t* __restrict__ WS = nullptr) {
+                                                       const uint8_t* __restrict__ WS = nullptr,
+                                                       uint8_t* __restrict__ YS = nullptr) {
+  static_assert(!OUT8 || (FP8 && NT == 4 && !HAS_RES), "OUT8: MX-fp8 256x256 tiles without residual");
 #if defined(__HIP_DEVICE_COMPILE__)  // buffer-descriptor builtins exist in the device pass only
   using C = P8<NT, FP8>;
   constexpr int KB = 64, TBN = C::TBN;                  // KB: 128-byte LDS rows (64 bf16 / 128 fp8)
@@ -841,18 +847,51 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
       __builtin_amdgcn_wave_barrier();
-      bf16x8 ov[C::CPL];
+      if constexpr (OUT8) {
+        // lane: row le/4 of the round's 16 rows, columns 16 (le % 4) .. +15 of the wave's 64
+        const int rr = le >> 2, hb = le & 3;
+        const bf16x8 h0 = *(const bf16x8*)(et + rr * C::ELD + (2 * hb) * 8);
+        const bf16x8 h1 = *(const bf16x8*)(et + rr * C::ELD + (2 * hb + 1) * 8);
+        float v[16];
+        float amax = 0.f;
 #pragma unroll
-      for (int c = 0; c < C::CPL; ++c) {
-        const int idx = c * 64 + le;
-        ov[c] = *(const bf16x8*)(et + (idx / (2 * NT)) * C::ELD + (idx % (2 * NT)) * 8);
-      }
+        for (int e = 0; e < 8; ++e) {
+          v[e] = mmr::bf2f((uint16_t)h0[e]);
+          v[8 + e] = mmr::bf2f((uint16_t)h1[e]);
+          amax = fmaxf(amax, fmaxf(fabsf(v[e]), fabsf(v[8 + e])));
+        }
+        amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+        const uint32_t ab = __float_as_uint(amax);
+        int ex = (int)((ab >> 23) & 255) - 127 - 8 + ((ab & 0x7FFFFF) > 0x600000 ? 1 : 0);
+        ex = ex < -127 ? -127 : (ex > 126 ? 126 : ex);
+        const float inv = __uint_as_float((uint32_t)(127 - ex) << 23);
+        uint32_t w4[4];
 #pragma unroll
-      for (int c = 0; c < C::CPL; ++c) {
-        const int idx = c * 64 + le;
-        const int64_t m = m0 + wr * 128 + rd * 16 * C::RM + idx / (2 * NT);
-        const int n = n0 + wc * 16 * NT + (idx % (2 * NT)) * 8;
-        *(bf16x8*)(Y + m * N + n) = ov[c];
+        for (int i = 0; i < 4; ++i) {
+          w4[i] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[4 * i] * inv, v[4 * i + 1] * inv, 0, false);
+          w4[i] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[4 * i + 2] * inv, v[4 * i + 3] * inv, (int)w4[i], true);
+        }
+        const int64_t m = m0 + wr * 128 + rd * 16 + rr;
+        const int n = n0 + wc * 64 + hb * 16;
+        *(uint4*)((uint8_t*)Y + m * N + n) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        if ((hb & 1) == 0) {  // one scale byte per 32-block, layout-0 image: [m/256][n/128][wr][fq][fr][i]
+          const int fq = (n % 128) / 32;
+          YS[((m0 / 256) * (N / 128) + n / 128) * 1024 + ((wr * 4 + fq) * 16 + rr) * 8 + rd] = (uint8_t)(ex + 127);
+        }
+      } else {
+        bf16x8 ov[C::CPL];
+#pragma unroll
+        for (int c = 0; c < C::CPL; ++c) {
+          const int idx = c * 64 + le;
+          ov[c] = *(const bf16x8*)(et + (idx / (2 * NT)) * C::ELD + (idx % (2 * NT)) * 8);
+        }
+#pragma unroll
+        for (int c = 0; c < C::CPL; ++c) {
+          const int idx = c * 64 + le;
+          const int64_t m = m0 + wr * 128 + rd * 16 * C::RM + idx / (2 * NT);
+          const int n = n0 + wc * 16 * NT + (idx % (2 * NT)) * 8;
+          *(bf16x8*)(Y + m * N + n) = ov[c];
+        }
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_wave_barrier();
@@ -1399,6 +1438,33 @@ extern "C" mmr_status mmr_linear_mxfp8(const uint8_t* xq, const uint8_t* xs, con
     else MX_LAUNCH(1, false, false);
   }
 #undef MX_LAUNCH
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+extern "C" mmr_status mmr_linear_mxfp8_q8(const uint8_t* xq, const uint8_t* xs, const uint8_t* wq, const uint8_t* ws,
+                                         const float* bias, uint8_t* yq, uint8_t* ys, int64_t m, int32_t n,
+                                         int32_t kp, int32_t act, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(xq && xs && wq && ws && yq && ys, "mmr_linear_mxfp8_q8: NULL pointer");
+  MMR_REQUIRE(m > 0 && m % 256 == 0, "mmr_linear_mxfp8_q8: m=%lld must be a positive multiple of 256", (long long)m);
+  MMR_REQUIRE(n > 0 && n % 256 == 0, "mmr_linear_mxfp8_q8: n=%d must be a positive multiple of 256 (weights in layout 2)", n);
+  MMR_REQUIRE(kp > 0 && kp % 256 == 0, "mmr_linear_mxfp8_q8: kp=%d must be a positive multiple of 256", kp);
+  MMR_REQUIRE(act == 0 || act == 1, "mmr_linear_mxfp8_q8: act=%d", act);
+  hipStream_t st = mmr::as_stream(stream);
+  const int tm = (int)(m / 256), tn = n / 256;
+  const int grid = (int)std::max<int64_t>(8, std::min<int64_t>(std::max(8, cu_count() / 8 * 8), (int64_t)tm * tn) / 8 * 8);
+  const uint16_t* X = (const uint16_t*)xq;
+  const uint16_t* W = (const uint16_t*)wq;
+  uint16_t* Y = (uint16_t*)yq;
+  if (act == 0 && bias)
+    gemm_bf16_tn_p8<4, 0, true, false, true, true><<<dim3(grid), dim3(512), P8<4, true>::LDS_B, st>>>(X, W, bias, nullptr, Y, m, n, kp, tm, tn, xs, ws, ys);
+  else if (act == 0)
+    gemm_bf16_tn_p8<4, 0, false, false, true, true><<<dim3(grid), dim3(512), P8<4, true>::LDS_B, st>>>(X, W, bias, nullptr, Y, m, n, kp, tm, tn, xs, ws, ys);
+  else if (bias)
+    gemm_bf16_tn_p8<4, 1, true, false, true, true><<<dim3(grid), dim3(512), P8<4, true>::LDS_B, st>>>(X, W, bias, nullptr, Y, m, n, kp, tm, tn, xs, ws, ys);
+  else
+    gemm_bf16_tn_p8<4, 1, false, false, true, true><<<dim3(grid), dim3(512), P8<4, true>::LDS_B, st>>>(X, W, bias, nullptr, Y, m, n, kp, tm, tn, xs, ws, ys);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }

@@ -72,6 +72,19 @@ def linear_mxfp8(x8, w8, bias=None, residual=None, act=0, out=None, lead=None):
     return y
 
 
+def linear_mxfp8_q8(x8, w8, bias=None, act=0):
+    """act(deq(x8) @ deq(w8).T + bias) emitted as the next GEMM's MX-fp8 activation operand (== a
+    quantize_mxfp8 of the bf16 result, fused into the epilogue); w8 in layout 2, N % 256 == 0."""
+    _lib.require_gpu(x8.q)
+    assert x8.layout == 0 and w8.layout == 2 and x8.kp == w8.kp, "operand layouts / padded K disagree"
+    M, N = x8.q.shape[0], w8.q.shape[0]
+    q = torch.empty((M, N), dtype=torch.uint8, device=x8.q.device)
+    s = torch.empty(((M // 256) * (N // 128) * 1024,), dtype=torch.uint8, device=x8.q.device)
+    _chk(_L().mmr_linear_mxfp8_q8(_lib.ptr(x8.q), _lib.ptr(x8.s), _lib.ptr(w8.q), _lib.ptr(w8.s), _lib.ptr(bias),
+                                  _lib.ptr(q), _lib.ptr(s), M, N, x8.kp, act, _s(x8.q)), "mmr_linear_mxfp8_q8")
+    return MXFP8(q, s, N, 0)
+
+
 def layernorm(x, g, b, eps, out=None):
     _lib.require_gpu(x)
     c = x.shape[-1]

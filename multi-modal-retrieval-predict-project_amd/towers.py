@@ -37,9 +37,19 @@ def _f(t, dev):
 
 def _w8(w, plain=False):
     """nn.Linear weight (bf16, device) -> its MX-fp8 operand (quantised once, at load).  plain: the
-    layer's GEMM has no GELU / residual epilogue, so it can take 256 x 256 tiles (weight panels of 256
-    rows, layout 2) when N % 256 == 0; the GELU / residual epilogues keep 256 x 192 (layout 1)."""
+    layer's GEMM has no residual epilogue, so it takes 256 x 256 tiles (weight panels of 256 rows,
+    layout 2) when N % 256 == 0 (measured faster, GELU included: FFN1 1035 -> 1191 TF/s); residual
+    epilogues keep 256 x 192 (layout 1)."""
     return ops.quantize_mxfp8(w, layout=2 if plain and w.shape[0] % 256 == 0 else 1)
+
+
+def _mlp8(h, w1_8, b1, w2_8, b2, residual=None):
+    """fc1 (+ GELU) -> fc2 on the MX-fp8 path with fc1's epilogue emitting fc2's fp8 operand
+    (mmr_linear_mxfp8_q8): the hidden activation never exists in bf16."""
+    K = h.shape[-1]
+    x8 = ops.quantize_mxfp8(h.reshape(-1, K), layout=0, kp=w1_8.kp)
+    f8 = ops.linear_mxfp8_q8(x8, w1_8, b1, act=1)
+    return ops.linear_mxfp8(f8, w2_8, b2, residual, lead=tuple(h.shape[:-1]))
 
 
 def _lin(x, w, b=None, residual=None, act=0, w8=None):
@@ -101,7 +111,7 @@ class SwinTower:
                 bk = st["blocks"][-1]
                 fp8 = i in self.fp8_stages
                 for n in ("qkv", "proj", "fc1", "fc2"):
-                    bk[n + "_w8"] = _w8(bk[n + "_w"], plain=n == "qkv") if fp8 else None
+                    bk[n + "_w8"] = _w8(bk[n + "_w"], plain=n in ("qkv", "fc1")) if fp8 else None
                 bk["mlp_pack"] = ops.swin_mlp_pack(bk["fc1_w"], bk["fc2_w"]) if self.fused_mlp and not fp8 else None
                 bk["attn_pack"] = None
                 if self.fused_attn and not fp8 and E * 2 ** i == 96 and self.cfg["num_heads"][i] == 3 and ws == 7:
@@ -140,8 +150,11 @@ class SwinTower:
                     x = ops.swin_mlp(x, bk["n2g"], bk["n2b"], bk["mlp_pack"], bk["fc1_b"], bk["fc2_b"], 1e-5)
                 else:
                     h = ops.layernorm(x, bk["n2g"], bk["n2b"], 1e-5)
-                    h = _lin(h, bk["fc1_w"], bk["fc1_b"], act=1, w8=bk["fc1_w8"])
-                    x = _lin(h, bk["fc2_w"], bk["fc2_b"], residual=x, w8=bk["fc2_w8"])
+                    if bk["fc1_w8"] is not None and bk["fc1_w8"].layout == 2:
+                        x = _mlp8(h, bk["fc1_w8"], bk["fc1_b"], bk["fc2_w8"], bk["fc2_b"], residual=x)
+                    else:
+                        h = _lin(h, bk["fc1_w"], bk["fc1_b"], act=1, w8=bk["fc1_w8"])
+                        x = _lin(h, bk["fc2_w"], bk["fc2_b"], residual=x, w8=bk["fc2_w8"])
             del C
         return x
 
@@ -181,7 +194,7 @@ class BertTower:
             })
             ly = self.layers[-1]
             for n in ("qkv", "o", "i", "f"):
-                ly[n + "_w8"] = _w8(ly[n + "_w"], plain=n != "i") if fp8 else None
+                ly[n + "_w8"] = _w8(ly[n + "_w"], plain=True) if fp8 else None
         self.hidden = self.word.shape[1]
         # optional dict name -> list of (start, end) torch.cuda.Event pairs around every launch of the
         # four GEMMs of a layer ("qkv", "o", "ffn1", "ffn2"): the bench's per-kernel roofline (events
@@ -218,8 +231,11 @@ class BertTower:
             ctx = ops.bert_attention(qkv, mask, heads, self.hidden // heads)
             a = gemm("o", ctx, ly["o_w"], ly["o_b"], w8=ly["o_w8"])
             h = ops.add_layernorm(a, h, ly["ln1_g"], ly["ln1_b"], 1e-12)
-            f = gemm("ffn1", h, ly["i_w"], ly["i_b"], act=1, w8=ly["i_w8"])
-            f = gemm("ffn2", f, ly["f_w"], ly["f_b"], w8=ly["f_w8"])
+            if ly["i_w8"] is not None and ly["i_w8"].layout == 2 and ev is None:
+                f = _mlp8(h, ly["i_w8"], ly["i_b"], ly["f_w8"], ly["f_b"])  # FFN1 emits FFN2's fp8 operand
+            else:
+                f = gemm("ffn1", h, ly["i_w"], ly["i_b"], act=1, w8=ly["i_w8"])
+                f = gemm("ffn2", f, ly["f_w"], ly["f_b"], w8=ly["f_w8"])
             h = ops.add_layernorm(f, h, ly["ln2_g"], ly["ln2_b"], 1e-12)
         return h
 

@@ -90,3 +90,19 @@ def test_linear_mxfp8_rejects_bad_shapes():
     bad = ops.MXFP8(w8.q[:100], w8.s, 768, 1)
     with pytest.raises(Exception):
         ops.linear_mxfp8(x8, bad)
+
+
+@pytest.mark.parametrize("M,N,K,act", [(512, 3072, 768, 1), (1024, 1536, 512, 1), (256, 512, 768, 0)])
+def test_linear_mxfp8_q8_equals_quantised_bf16_output(M, N, K, act):
+    """The fused fp8-output epilogue (BERT FFN1 -> FFN2, Swin fc1 -> fc2) is bit-identical to
+    quantising the bf16 output of the same GEMM with mmr_quantize_mxfp8 (values and scale bytes)."""
+    xt, _ = _bf16_input(M, K, 3 + M)
+    wt, _ = _bf16_input(N, K, 4 + N, zero_block=False)
+    x8 = ops.quantize_mxfp8(xt.to(DEV), layout=0)
+    w8 = ops.quantize_mxfp8((wt * 0.05).to(DEV), layout=2)
+    bias = torch.randn(N, generator=torch.Generator().manual_seed(N)).to(DEV)
+    y8 = ops.linear_mxfp8_q8(x8, w8, bias, act=act)
+    ref8 = ops.quantize_mxfp8(ops.linear_mxfp8(x8, w8, bias, act=act), layout=0)
+    torch.cuda.synchronize()
+    assert torch.equal(y8.q, ref8.q)
+    assert torch.equal(y8.s, ref8.s)
