@@ -149,6 +149,14 @@ mmr_status mmr_linear_mxfp8_q8(const uint8_t* xq, const uint8_t* xs, const uint8
                                const float* bias, uint8_t* yq, uint8_t* ys, int64_t m, int32_t n,
                                int32_t kp, int32_t act, void* stream);
 
+/* LayerNorm(x (+ residual, may be NULL)) as mmr_layernorm_bf16 / mmr_add_layernorm_bf16, also
+ * emitting the row as an MX-fp8 activation operand (q8 [rows][c] e4m3 + layout-0 scales,
+ * rows % 256 == 0, c % 256 == 0), bit-identical to mmr_quantize_mxfp8 of y (the fp8 towers' QKV / FFN1
+ * inputs). */
+mmr_status mmr_layernorm_bf16_q8(const uint16_t* x, const uint16_t* residual, const float* gamma,
+                                 const float* beta, uint16_t* y, uint8_t* q8, uint8_t* q8_scales, int64_t rows,
+                                 int32_t c, float eps, void* stream);
+
 /* Row LayerNorm over c channels (bf16 in/out, f32 math, gamma/beta f32). */
 mmr_status mmr_layernorm_bf16(const uint16_t* x, const float* gamma, const float* beta,
                               uint16_t* y, int64_t rows, int32_t c, float eps, void* stream);

@@ -37,6 +37,7 @@ SIGNATURES = {
     "mmr_linear_mxfp8_q8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp],
     "mmr_layernorm_bf16": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp],
     "mmr_add_layernorm_bf16": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp],
+    "mmr_layernorm_bf16_q8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp],
     "mmr_scaled_add_layernorm_bf16": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp],
     "mmr_bert_embed": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp],
     "mmr_bert_attention": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp],

@@ -36,14 +36,20 @@ __device__ __forceinline__ void store8(uint16_t* p, const float* v) {
 // the row stays in registers (<= NC chunks of 8 per lane; NC sized to the launch so the register
 // file, and with it the occupancy, follows the row width): one read, one write, exact two-pass
 // (centred) variance like torch.
-template <int LPR, int NC, bool ADD>
+// Q8: also emit the row as the next GEMM's MX-fp8 activation operand (e4m3 q [rows][c] + E8M0
+// scales in the layout-0 image, see mmr_quantize_mxfp8) from the bf16-rounded outputs — bit-identical
+// to quantising y afterwards; a 32-block is 4 adjacent lanes' chunks (two lane swaps).
+template <int LPR, int NC, bool ADD, bool Q8 = false>
 __global__ __launch_bounds__(256) void layernorm_bf16(const uint16_t* __restrict__ x,
                                                       const uint16_t* __restrict__ r,
                                                       const float* __restrict__ g,
                                                       const float* __restrict__ b,
                                                       uint16_t* __restrict__ y, int64_t rows,
                                                       int c, float eps,
-                                                      const float* __restrict__ alpha = nullptr) {
+                                                      const float* __restrict__ alpha = nullptr,
+                                                      uint8_t* __restrict__ q8 = nullptr,
+                                                      uint8_t* __restrict__ q8s = nullptr) {
+  static_assert(!Q8 || LPR % 4 == 0, "Q8: a 32-block must be 4 lanes of one row");
   constexpr int RPW = 64 / LPR;
   const int lane = threadIdx.x & 63;
   const int sub = lane % LPR;
@@ -126,6 +132,33 @@ __global__ __launch_bounds__(256) void layernorm_bf16(const uint16_t* __restrict
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[i][j] = (v[i][j] - mean) * rstd * gg[j] + bb[j];
     if (ok && ch < nch) store8(y + row * c + ch * 8, v[i]);
+    if constexpr (Q8) {
+      float vb[8];
+      float amax = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        vb[j] = bf2f(f2bf(v[i][j]));  // the stored bf16 value
+        amax = fmaxf(amax, fabsf(vb[j]));
+      }
+      amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+      amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+      const uint32_t ab = __float_as_uint(amax);
+      int ex = (int)((ab >> 23) & 255) - 127 - 8 + ((ab & 0x7FFFFF) > 0x600000 ? 1 : 0);
+      ex = ex < -127 ? -127 : (ex > 126 ? 126 : ex);
+      const float inv = __uint_as_float((uint32_t)(127 - ex) << 23);
+      uint32_t w0 = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(vb[0] * inv, vb[1] * inv, 0, false);
+      w0 = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(vb[2] * inv, vb[3] * inv, (int)w0, true);
+      uint32_t w1 = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(vb[4] * inv, vb[5] * inv, 0, false);
+      w1 = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(vb[6] * inv, vb[7] * inv, (int)w1, true);
+      if (ok && ch < nch) {
+        *(uint2*)(q8 + row * c + ch * 8) = make_uint2(w0, w1);
+        if ((ch & 3) == 0) {
+          const int blk = ch / 4, kt = blk / 4, fq = blk % 4;
+          const int rr = (int)(row % 256), wr = rr / 128, ii = (rr % 128) / 16, fr = rr % 16;
+          q8s[((row / 256) * (c / 128) + kt) * 1024 + ((wr * 4 + fq) * 16 + fr) * 8 + ii] = (uint8_t)(ex + 127);
+        }
+      }
+    }
   }
 }
 
@@ -722,8 +755,11 @@ extern "C" {
 static mmr_status layernorm_launch(const uint16_t* x, const uint16_t* r, const float* gamma,
                                    const float* beta, uint16_t* y, int64_t rows, int32_t c,
                                    float eps, void* stream, const char* who,
-                                   const float* alpha = nullptr) {
+                                   const float* alpha = nullptr, uint8_t* q8 = nullptr,
+                                   uint8_t* q8s = nullptr) {
   MMR_REQUIRE(x && gamma && beta && y, "%s: NULL pointer", who);
+  MMR_REQUIRE(!q8 || (q8s && rows % 256 == 0 && c % 256 == 0),
+              "%s: the MX-fp8 output needs rows %% 256 == 0 and c %% 256 == 0 (rows=%lld c=%d)", who, (long long)rows, c);
   MMR_REQUIRE(c > 0 && c % 8 == 0 && rows >= 0, "%s: c=%d must be a positive multiple of 8", who, c);
   MMR_REQUIRE(c <= 4096, "%s: c=%d > 4096", who, c);
   if (rows == 0) return MMR_OK;
@@ -748,9 +784,13 @@ static mmr_status layernorm_launch(const uint16_t* x, const uint16_t* r, const f
   const int cpl = (nch + lpr - 1) / lpr;                   // chunks per lane
   const int64_t rows_per_block = 4 * (64 / lpr);
   const dim3 grid((unsigned)mmr::ceil_div(rows, rows_per_block));
-#define MMR_LN2(L, N)                                                                                \
-  (r ? layernorm_bf16<L, N, true><<<grid, 256, 0, st>>>(x, r, gamma, beta, y, rows, c, eps, alpha) \
-     : layernorm_bf16<L, N, false><<<grid, 256, 0, st>>>(x, r, gamma, beta, y, rows, c, eps, alpha))
+#define MMR_LN2(L, N)                                                                                          \
+  (q8 ? (r ? layernorm_bf16<L, N, true, true><<<grid, 256, 0, st>>>(x, r, gamma, beta, y, rows, c, eps, alpha, q8,  \
+                                                                    q8s)                                          \
+           : layernorm_bf16<L, N, false, true><<<grid, 256, 0, st>>>(x, r, gamma, beta, y, rows, c, eps, alpha, q8, \
+                                                                     q8s))                                        \
+      : (r ? layernorm_bf16<L, N, true><<<grid, 256, 0, st>>>(x, r, gamma, beta, y, rows, c, eps, alpha)          \
+           : layernorm_bf16<L, N, false><<<grid, 256, 0, st>>>(x, r, gamma, beta, y, rows, c, eps, alpha)))
 #define MMR_LN(L) (cpl <= 3 ? MMR_LN2(L, 3) : (cpl <= 6 ? MMR_LN2(L, 6) : MMR_LN2(L, 8)))
   if (lpr == 8) MMR_LN(8);
   else if (lpr == 16) MMR_LN(16);
@@ -774,6 +814,15 @@ mmr_status mmr_add_layernorm_bf16(const uint16_t* x, const uint16_t* residual, c
   mmr::clear_error();
   MMR_REQUIRE(residual, "mmr_add_layernorm_bf16: NULL residual");
   return layernorm_launch(x, residual, gamma, beta, y, rows, c, eps, stream, "mmr_add_layernorm_bf16");
+}
+
+mmr_status mmr_layernorm_bf16_q8(const uint16_t* x, const uint16_t* residual, const float* gamma,
+                                 const float* beta, uint16_t* y, uint8_t* q8, uint8_t* q8_scales, int64_t rows,
+                                 int32_t c, float eps, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(q8 && q8_scales, "mmr_layernorm_bf16_q8: NULL MX-fp8 output");
+  return layernorm_launch(x, residual, gamma, beta, y, rows, c, eps, stream, "mmr_layernorm_bf16_q8", nullptr, q8,
+                          q8_scales);
 }
 
 mmr_status mmr_scaled_add_layernorm_bf16(const uint16_t* x, const float* alpha, const uint16_t* residual,

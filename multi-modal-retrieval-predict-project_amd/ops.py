@@ -105,6 +105,20 @@ def add_layernorm(x, r, g, b, eps, out=None):
     return y
 
 
+def layernorm_q8(x, r, g, b, eps):
+    """LayerNorm(x (+ r)) -> (y bf16, its MX-fp8 activation operand) in one pass (rows % 256 == 0,
+    C % 256 == 0); r may be None."""
+    _lib.require_gpu(x)
+    c = x.shape[-1]
+    rows = x.numel() // c
+    y = torch.empty_like(x)
+    q = torch.empty((rows, c), dtype=torch.uint8, device=x.device)
+    s = torch.empty(((rows // 256) * (c // 128) * 1024,), dtype=torch.uint8, device=x.device)
+    _chk(_L().mmr_layernorm_bf16_q8(_lib.ptr(x), _lib.ptr(r), _lib.ptr(g), _lib.ptr(b), _lib.ptr(y), _lib.ptr(q),
+                                    _lib.ptr(s), rows, c, float(eps), _s(x)), "mmr_layernorm_bf16_q8")
+    return y, MXFP8(q, s, c, 0)
+
+
 def scaled_add_layernorm(x, alpha, r, g, b, eps, out=None):
     """LayerNorm(alpha * x + r), alpha a device scalar tensor (vectorised row kernel, bf16)."""
     _lib.require_gpu(x)

@@ -43,13 +43,20 @@ def _w8(w, plain=False):
     return ops.quantize_mxfp8(w, layout=2 if plain and w.shape[0] % 256 == 0 else 1)
 
 
-def _mlp8(h, w1_8, b1, w2_8, b2, residual=None):
+def _mlp8(h, w1_8, b1, w2_8, b2, residual=None, h8=None):
     """fc1 (+ GELU) -> fc2 on the MX-fp8 path with fc1's epilogue emitting fc2's fp8 operand
-    (mmr_linear_mxfp8_q8): the hidden activation never exists in bf16."""
+    (mmr_linear_mxfp8_q8): the hidden activation never exists in bf16.  h8: h's fp8 operand when
+    the producing LayerNorm already emitted it."""
     K = h.shape[-1]
-    x8 = ops.quantize_mxfp8(h.reshape(-1, K), layout=0, kp=w1_8.kp)
+    x8 = h8 if h8 is not None else ops.quantize_mxfp8(h.reshape(-1, K), layout=0, kp=w1_8.kp)
     f8 = ops.linear_mxfp8_q8(x8, w1_8, b1, act=1)
     return ops.linear_mxfp8(f8, w2_8, b2, residual, lead=tuple(h.shape[:-1]))
+
+
+def _ln8_ok(x, w8):
+    """The LayerNorm can emit the fp8 operand itself (rows and C multiples of 256, unpadded K)."""
+    C = x.shape[-1]
+    return w8 is not None and C % 256 == 0 and (x.numel() // C) % 256 == 0 and w8.kp == C
 
 
 def _lin(x, w, b=None, residual=None, act=0, w8=None):
@@ -141,6 +148,11 @@ class SwinTower:
             for j, bk in enumerate(st["blocks"]):
                 if bk["attn_pack"] is not None:
                     x = ops.swin_attn_block(x, bk["attn_pack"], bk["bias"], ws, bk["shift"], 1e-5)
+                elif _ln8_ok(x, bk["qkv_w8"]):  # fp8 stage, C % 256 == 0: the LN emits the QKV operand
+                    _, h8 = ops.layernorm_q8(x, None, bk["n1g"], bk["n1b"], 1e-5)
+                    qkv = ops.linear_mxfp8(h8, bk["qkv_w8"], bk["qkv_b"], lead=tuple(x.shape[:-1]))
+                    a = ops.swin_window_attention(qkv, bk["bias"], H, heads, ws, bk["shift"])
+                    x = _lin(a, bk["proj_w"], bk["proj_b"], residual=x, w8=bk["proj_w8"])
                 else:
                     h = ops.layernorm(x, bk["n1g"], bk["n1b"], 1e-5)
                     qkv = _lin(h, bk["qkv_w"], bk["qkv_b"], w8=bk["qkv_w8"])
@@ -148,6 +160,9 @@ class SwinTower:
                     x = _lin(a, bk["proj_w"], bk["proj_b"], residual=x, w8=bk["proj_w8"])
                 if bk["mlp_pack"] is not None:
                     x = ops.swin_mlp(x, bk["n2g"], bk["n2b"], bk["mlp_pack"], bk["fc1_b"], bk["fc2_b"], 1e-5)
+                elif _ln8_ok(x, bk["fc1_w8"]) and bk["fc1_w8"].layout == 2:
+                    h, h8 = ops.layernorm_q8(x, None, bk["n2g"], bk["n2b"], 1e-5)
+                    x = _mlp8(h, bk["fc1_w8"], bk["fc1_b"], bk["fc2_w8"], bk["fc2_b"], residual=x, h8=h8)
                 else:
                     h = ops.layernorm(x, bk["n2g"], bk["n2b"], 1e-5)
                     if bk["fc1_w8"] is not None and bk["fc1_w8"].layout == 2:
@@ -226,7 +241,20 @@ class BertTower:
             e1.record()
             ev.setdefault(name, []).append((e0, e1))
             return y
+        # fp8 fast path: every LayerNorm also emits the next GEMM's MX-fp8 operand, FFN1 emits FFN2's
+        fast8 = (self.fp8 and ev is None and all(_ln8_ok(h, ly["qkv_w8"]) and ly["i_w8"].layout == 2
+                                                  for ly in self.layers))
+        h8 = ops.quantize_mxfp8(h.reshape(-1, h.shape[-1]), layout=0) if fast8 else None
+        lead = tuple(h.shape[:-1])
         for ly in self.layers:
+            if fast8:
+                qkv = ops.linear_mxfp8(h8, ly["qkv_w8"], ly["qkv_b"], lead=lead)
+                ctx = ops.bert_attention(qkv, mask, heads, self.hidden // heads)
+                a = _lin(ctx, ly["o_w"], ly["o_b"], w8=ly["o_w8"])
+                h, h8 = ops.layernorm_q8(a, h, ly["ln1_g"], ly["ln1_b"], 1e-12)
+                f = _mlp8(h, ly["i_w8"], ly["i_b"], ly["f_w8"], ly["f_b"], h8=h8)
+                h, h8 = ops.layernorm_q8(f, h, ly["ln2_g"], ly["ln2_b"], 1e-12)
+                continue
             qkv = gemm("qkv", h, ly["qkv_w"], ly["qkv_b"], w8=ly["qkv_w8"])
             ctx = ops.bert_attention(qkv, mask, heads, self.hidden // heads)
             a = gemm("o", ctx, ly["o_w"], ly["o_b"], w8=ly["o_w8"])

@@ -106,3 +106,21 @@ def test_linear_mxfp8_q8_equals_quantised_bf16_output(M, N, K, act):
     torch.cuda.synchronize()
     assert torch.equal(y8.q, ref8.q)
     assert torch.equal(y8.s, ref8.s)
+
+
+@pytest.mark.parametrize("rows,c,add", [(512, 768, True), (256, 768, False), (256, 1536, True)])
+def test_layernorm_q8_equals_quantised_layernorm(rows, c, add):
+    """LayerNorm with the fused MX-fp8 output: y equals the plain LayerNorm bit for bit, and the fp8
+    operand equals mmr_quantize_mxfp8 of y (values and scale bytes)."""
+    xt, _ = _bf16_input(rows, c, 5 + rows)
+    rt, _ = _bf16_input(rows, c, 6 + rows)
+    g = torch.Generator().manual_seed(c)
+    gam, bet = (torch.randn(c, generator=g) * 0.5 + 1).to(DEV), (torch.randn(c, generator=g) * 0.1).to(DEV)
+    x, r = xt.to(DEV), (rt.to(DEV) if add else None)
+    y, y8 = ops.layernorm_q8(x, r, gam, bet, 1e-12)
+    ref = ops.add_layernorm(x, r, gam, bet, 1e-12) if add else ops.layernorm(x, gam, bet, 1e-12)
+    ref8 = ops.quantize_mxfp8(ref, layout=0)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+    assert torch.equal(y8.q, ref8.q)
+    assert torch.equal(y8.s, ref8.s)

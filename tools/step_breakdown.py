@@ -1,7 +1,9 @@
 """Per-op time breakdown of one bench step (multimodal default): wraps the mmr_amd.ops entry points
 with HIP events on the current stream and prints, per (op, shape), calls / total ms / TF/s for the
 GEMMs.  Diagnostic only.
-usage: python tools/step_breakdown.py [--model-type multimodal|text]"""
+usage: python tools/step_breakdown.py [--model-type multimodal|text] [--batch B] [--dim D] [--tower-dtype bf16|fp8]
+(MMR_TOWER_STREAMS=0 MMR_FUSION_STREAMS=0 for a sequential step: per-op events are exact only then)"""
+import argparse
 import collections
 import os
 import sys
@@ -13,11 +15,17 @@ import mmr_amd  # noqa: E402,F401
 from mmr_amd import ops, synthetic  # noqa: E402
 from mmr_amd.model import build_bench_model  # noqa: E402
 
-mt = sys.argv[2] if len(sys.argv) > 2 and sys.argv[1] == "--model-type" else "multimodal"
+ap = argparse.ArgumentParser()
+ap.add_argument("--model-type", default="multimodal")
+ap.add_argument("--batch", type=int, default=256)
+ap.add_argument("--dim", type=int, default=768)
+ap.add_argument("--tower-dtype", default="bf16")
+args = ap.parse_args()
+mt = args.model_type
 torch.cuda.set_device(0)
 dev = torch.device("cuda:0")
-model = build_bench_model(device=dev, joint_dim=768, model_type=mt)
-B = 256
+model = build_bench_model(device=dev, joint_dim=args.dim, model_type=mt, tower_dtype=args.tower_dtype)
+B = args.batch
 imgs = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(B, synthetic.SEED))).to(dev)
 ids_np, mask_np = synthetic.reports(B, 128, synthetic.SEED + 100)
 ids, mask = torch.from_numpy(ids_np).to(dev), torch.from_numpy(mask_np).to(dev)
@@ -26,7 +34,7 @@ rec = []
 names = ["linear", "layernorm", "add_layernorm", "scaled_add_layernorm", "bert_embed", "bert_attention",
          "swin_window_attention", "patch_im2col", "patch_merge_ln", "swin_head", "mean_tokens", "proj_head",
          "swin_mlp", "swin_attn_block", "linear_f32", "linear_f32_batched", "mha", "add_pos", "ln_rows",
-         "assemble_seq", "rows_to_f32"]
+         "assemble_seq", "rows_to_f32", "quantize_mxfp8", "linear_mxfp8", "linear_mxfp8_q8", "layernorm_q8"]
 
 
 def wrap(name, fn):
@@ -36,6 +44,12 @@ def wrap(name, fn):
         out = fn(*a, **k)
         e1.record()
         key = name
+        if name == "linear_mxfp8_q8":
+            key = (name, a[0].q.shape[0], a[1].q.shape[0], a[0].kp, k.get("act", 0), False)
+        elif name == "linear_mxfp8":
+            key = (name, a[0].q.shape[0], a[1].q.shape[0], a[0].kp, k.get("act", 0), (a[3] if len(a) > 3 else k.get("residual")) is not None)
+        elif name == "quantize_mxfp8":
+            key = (name, a[0].numel() // a[0].shape[-1], 0, a[0].shape[-1], 0, False)
         if name == "linear":
             x, wt = a[0], a[1]
             K = x.shape[-1]
@@ -64,8 +78,8 @@ tot = sum(v[1] for v in agg.values())
 print(f"total {tot:.3f} ms per step (sum of op times)")
 for key, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
     if isinstance(key, tuple):
-        _, M, N, K, act, res = key
+        nm, M, N, K, act, res = key
         tf = 2.0 * M * N * K * (c / 3) / (t * 1e-3) / 1e12
-        print(f"{t:8.3f} ms {c // 3:4d}x  linear M={M:7d} N={N:5d} K={K:5d} act={act} res={int(res)}  {tf:6.0f} TF/s")
+        print(f"{t:8.3f} ms {c // 3:4d}x  {nm:14s} M={M:7d} N={N:5d} K={K:5d} act={act} res={int(res)}  {tf:6.0f} TF/s")
     else:
         print(f"{t:8.3f} ms {c // 3:4d}x  {key}")
