@@ -239,6 +239,10 @@ def main():
     hev = []
     for _ in range(20):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        # a short device-side spin ahead of e0 keeps the stream busy while the host enqueues the
+        # call, so e0 -> e1 brackets the call's GPU work (prep / scan / select), not the host's
+        # enqueue latency (~60 us of Python + ctypes per call, more than the call's GPU time)
+        torch.cuda._sleep(1_000_000)
         e0.record(stream)
         _, _, st16 = index.search(q16, K, want_status=True)
         e1.record(stream)

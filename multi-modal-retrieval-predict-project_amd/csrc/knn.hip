@@ -448,13 +448,25 @@ __global__ __launch_bounds__(256, 2) void knn_scores_x3_gmax(const uint16_t* __r
 // Measured and dropped (MI355X, 100k x 768, 256 queries): splitting the query tiles over 2 or 4 waves
 // of one workgroup on the same 64-row block (more waves in flight, the block's gallery pieces re-read
 // from L2 by the sibling waves) — 4 waves x 4 tiles 102 us vs 68 us for one wave x 16 tiles.
-template <int QT, int KC, int WQ = 1>
+//
+// RAW (Q <= 32, d % 8 == 0, 16-B aligned rows): no query-prep launch — lane (h, r) reads k = 8h..8h+7 of
+// each 32-k piece of query row 16t + r straight from the caller's f32 rows (4 lanes = one 128-B line),
+// one chunk ahead like the gallery, and converts them to fp16 at the MFMA: the scores are q . g^ for
+// the UNNORMALISED query (|q| times the cosine; the order within a query is the same).  The selection
+// then uses the per-query margin 2 (|q| delta_rel + delta_abs) (argued at mmr_index_search), and takes
+// the exact path over every row if a component of q does not fit fp16.
+// Block maxima: besides the per-(query, unit) maxima, each (query, 64-row block) max goes to bmax —
+// the selection reads these 1/16-size rows first and touches unit maxima only inside blocks that can
+// hold a top-K row.
+template <int QT, int KC, int WQ = 1, bool RAW = false>
 __global__ __launch_bounds__(64 * WQ) void knn_scan_f16_gmax(const uint16_t* __restrict__ qh,
+                                                        const float* __restrict__ qraw, int64_t nq, int d,
                                                         const uint16_t* __restrict__ gh,
-                                                        float* __restrict__ gmax, int Dp, int64_t ldG,
-                                                        int64_t n) {
+                                                        float* __restrict__ gmax, float* __restrict__ bmax,
+                                                        int Dp, int64_t ldG, int64_t ldB, int64_t n) {
   typedef _Float16 h8 __attribute__((ext_vector_type(8)));
   constexpr int L = KC / 32;  // 1-KB pieces per tile per chunk
+  static_assert(!RAW || WQ == 1, "raw queries: one wave per block");
   const int lane = threadIdx.x & 63, wq = threadIdx.x >> 6;
   const int64_t blk = blockIdx.x;
   const int r = lane & 15, h = lane >> 4;
@@ -462,16 +474,46 @@ __global__ __launch_bounds__(64 * WQ) void knn_scan_f16_gmax(const uint16_t* __r
   const int64_t tileB = 16 * (int64_t)Dp;  // halfs per 16-row tile
   const uint16_t* pb = gh + g0 * Dp + 8 * lane;
   const uint16_t* pa = qh + (int64_t)wq * QT * tileB + 8 * lane;
+  // RAW query rows: clamped row pointer + row mask per query tile
+  constexpr int QR = RAW ? QT : 1;
+  const float* qrow[QR];
+  bool qok[QR];
+  if constexpr (RAW) {
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      const int64_t row = 16 * t + r;
+      qok[t] = row < nq;
+      qrow[t] = qraw + (qok[t] ? row : nq - 1) * (int64_t)d;
+    }
+  }
+  // raw: the 8 floats k0..k0+7 (k0 = chunk + 32e + 8h; d % 8 == 0, so a group is all in or all out)
+  auto qload = [&](int t, int k0, float4 (&x)[2]) {
+    const int kk = k0 < d ? k0 : d - 8;  // unconditional load, value masked at the conversion
+    x[0] = *(const float4*)(qrow[t] + kk);
+    x[1] = *(const float4*)(qrow[t] + kk + 4);
+  };
+  auto qcvt = [&](int t, int k0, const float4 (&x)[2]) -> h8 {
+    const bool ok = qok[t] && k0 < d;
+    h8 o;
+    o[0] = (_Float16)x[0].x; o[1] = (_Float16)x[0].y; o[2] = (_Float16)x[0].z; o[3] = (_Float16)x[0].w;
+    o[4] = (_Float16)x[1].x; o[5] = (_Float16)x[1].y; o[6] = (_Float16)x[1].z; o[7] = (_Float16)x[1].w;
+    return ok ? o : (h8){0, 0, 0, 0, 0, 0, 0, 0};
+  };
   f32x4 acc[QT][4];
 #pragma unroll
   for (int t = 0; t < QT; ++t)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[t][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  f32x4 b[4][L], a[QT][L];
+  constexpr int LA = RAW ? 1 : L, LR = RAW ? L : 1;
+  f32x4 b[4][L], a[QT][LA];
+  float4 ra[QT][LR][2];
 #pragma unroll
   for (int e = 0; e < L; ++e) {
 #pragma unroll
-    for (int t = 0; t < QT; ++t) a[t][e] = *(const f32x4*)(pa + t * tileB + 512 * e);
+    for (int t = 0; t < QT; ++t) {
+      if constexpr (RAW) qload(t, 32 * e + 8 * h, ra[t][e]);
+      else a[t][e] = *(const f32x4*)(pa + t * tileB + 512 * e);
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) b[j][e] = __builtin_nontemporal_load((const f32x4*)(pb + j * tileB + 512 * e));
   }
@@ -481,11 +523,15 @@ __global__ __launch_bounds__(64 * WQ) void knn_scan_f16_gmax(const uint16_t* __r
     // retires in issue order); the current ones were issued one iteration earlier.  Unconditional
     // (the last chunk re-reads itself): a branch would make the vmcnt at the join wait for them.
     const int kn = kc + KC < Dp ? kc + KC : kc;
-    f32x4 na[QT][L], nb[4][L];
+    f32x4 na[QT][LA], nb[4][L];
+    float4 nra[QT][LR][2];
 #pragma unroll
     for (int e = 0; e < L; ++e)
 #pragma unroll
-      for (int t = 0; t < QT; ++t) na[t][e] = *(const f32x4*)(pa + t * tileB + 16 * kn + 512 * e);
+      for (int t = 0; t < QT; ++t) {
+        if constexpr (RAW) qload(t, kn + 32 * e + 8 * h, nra[t][e]);
+        else na[t][e] = *(const f32x4*)(pa + t * tileB + 16 * kn + 512 * e);
+      }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -495,18 +541,28 @@ __global__ __launch_bounds__(64 * WQ) void knn_scan_f16_gmax(const uint16_t* __r
 #pragma unroll
     for (int e = 0; e < L; ++e)
 #pragma unroll
-      for (int t = 0; t < QT; ++t)
+      for (int t = 0; t < QT; ++t) {
+        h8 av;
+        if constexpr (RAW) av = qcvt(t, kc + 32 * e + 8 * h, ra[t][e]);
+        else av = __builtin_bit_cast(h8, a[t][e]);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a[t][e]),
-                                                             __builtin_bit_cast(h8, b[j][e]), acc[t][j], 0, 0, 0);
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, __builtin_bit_cast(h8, b[j][e]), acc[t][j], 0, 0, 0);
+      }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int e = 0; e < L; ++e) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) b[j][e] = nb[j][e];
 #pragma unroll
-      for (int t = 0; t < QT; ++t) a[t][e] = na[t][e];
+      for (int t = 0; t < QT; ++t) {
+        if constexpr (RAW) {
+          ra[t][e][0] = nra[t][e][0];
+          ra[t][e][1] = nra[t][e][1];
+        } else {
+          a[t][e] = na[t][e];
+        }
+      }
     }
   }
   const int64_t gcol = blk * 16 + r;
@@ -520,7 +576,13 @@ __global__ __launch_bounds__(64 * WQ) void knn_scan_f16_gmax(const uint16_t* __r
       float mx = -INFINITY;
 #pragma unroll
       for (int j = 0; j < 4; ++j) mx = fmaxf(mx, pad[j] ? -INFINITY : acc[t][j][rg]);
-      gmax[(int64_t)(16 * (wq * QT + t) + 4 * h + rg) * ldG + gcol] = mx;
+      const int64_t qrw = 16 * (wq * QT + t) + 4 * h + rg;
+      gmax[qrw * ldG + gcol] = mx;
+      // block max over the 16 lanes of this h (rows r of the block's 4 tiles)
+      float bm = mx;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) bm = fmaxf(bm, __shfl_xor(bm, o, 64));
+      if (r == 0) bmax[qrw * ldB + blk] = bm;
     }
 }
 
@@ -559,7 +621,7 @@ struct F16TileCfg {
   static constexpr int SLICE_B = P * 1024;
   static constexpr int STAGES = 163840 / SLICE_B > 8 ? 8 : 163840 / SLICE_B;
   static constexpr int AHEAD = STAGES - (PF ? 3 : 2);  // slices in flight beyond the one waited for
-  static constexpr int NST = MQ * MR / 4;        // epilogue stores per wave per tile
+  static constexpr int NST = 2 * (MQ * MR / 4);  // epilogue stores per wave per tile (unit + block maxima)
   static_assert(P % NW == 0 && MR % 4 == 0, "tile shape");
   static_assert(AHEAD >= 1 && PW * AHEAD + NST <= 63, "ring depth / vmcnt range");
 };
@@ -603,15 +665,18 @@ __device__ __forceinline__ f32x4 transpose4(const float (&v)[4], int h, int qc) 
 template <int WQ, int MQ, int WR, int MR, bool PF>
 __global__ __launch_bounds__(64 * WQ * WR) void knn_scan_f16_tile(const uint16_t* __restrict__ qh,
                                                                   const uint16_t* __restrict__ gh,
-                                                                  float* __restrict__ gmax, int Dp, int64_t ldG,
-                                                                  int64_t n, int64_t n_rt) {
+                                                                  float* __restrict__ gmax, float* __restrict__ bmax,
+                                                                  int Dp, int64_t ldG, int64_t ldB, int64_t n,
+                                                                  int64_t n_rt) {
   using C = F16TileCfg<WQ, MQ, WR, MR, PF>;
   typedef _Float16 h8 __attribute__((ext_vector_type(8)));
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];  // [STAGES][P][512] halfs
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave / WQ, wq = wave % WQ;
-  const int64_t lo = n_rt * blockIdx.x / gridDim.x, hi = n_rt * (blockIdx.x + 1) / gridDim.x;
+  // ranges of whole 64-row blocks (4 row tiles; n_rt % 4 == 0), so every block max is one lane group's
+  const int64_t nb4 = n_rt / 4;
+  const int64_t lo = 4 * (nb4 * blockIdx.x / gridDim.x), hi = 4 * (nb4 * (blockIdx.x + 1) / gridDim.x);
   if (lo >= hi) return;
   const int KP = Dp / 32;                          // k-pieces = slices per tile
   const int ntiles = (int)((hi - lo + C::RT - 1) / C::RT);
@@ -739,6 +804,11 @@ __global__ __launch_bounds__(64 * WQ * WR) void knn_scan_f16_tile(const uint16_t
           }
           const f32x4 o = transpose4(v, h, qc);
           if (rtb + h < hi) *(f32x4*)(orow + (rtb + h) * 4) = o;
+          // block max of rows 16 rtb .. +63 (rtb % 4 == 0): this lane's 4 units, then over h
+          float bm = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+          bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+          bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+          if (h == 0 && rtb < hi) bmax[(int64_t)(16 * (wq * MQ + t) + qc) * ldB + rtb / 4] = bm;
         }
       }
       stores_out = tile + 1 < ntiles;
@@ -974,8 +1044,11 @@ constexpr int kSlotCap = kMaxK + kCandCap;  // [0, kMaxK): carried top-K; [kMaxK
 __device__ long long g_sel_trace[16];
 #define SEL_MARK(i) \
   if (blockIdx.x == 0 && threadIdx.x == 0) g_sel_trace[i] = wall_clock64();
+#define SEL_VAL(i, v) \
+  if (blockIdx.x == 0 && threadIdx.x == 0) g_sel_trace[i] = (long long)(v);
 #else
 #define SEL_MARK(i)
+#define SEL_VAL(i, v)
 #endif
 
 template <int MODE>
@@ -985,12 +1058,16 @@ __device__ __forceinline__ int64_t unit_row(int64_t u, int m) {
   return 4 * u + m;
 }
 
+constexpr int kBlkCap = 1024;  // 64-row blocks collected by the coarse pass (more: the unit-level pass)
+
 template <int T>
 struct SelLds {
   float qrow[1024];  // raw query row (d <= 1024), first member: 16-B aligned
   uint32_t tmax[T];
   uint32_t hist[256];
   uint32_t bcast[4];
+  int cand_b[kBlkCap];   // coarse pass: collected blocks (also the compaction buffer of the tightening)
+  uint32_t ukey[kCandCap];  // keys of the collected units' values (tightening)
   int cand_u[kCandCap];
   double cand_d[kSlotCap];
   int rank_s[kSlotCap];
@@ -998,13 +1075,16 @@ struct SelLds {
   double tmp_d[kMaxK];
   int tmp_r[kMaxK];
   double qn;
+  float qmax;
 };
 
 // one 8-bit radix pass over the block's 1024 keys on the digit just below their common prefix
 // (from the block max / min): the smallest key of the digit bin holding the kth largest key — a
 // lower bound of it, resolved to 2^-8 of the keys' spread (a fixed top-down radix spends its first
 // passes on bits every key shares, with all 1024 LDS atomics on one bin)
-template <int T>
+// PASSES = 2: a second 8-bit pass inside the chosen bin (2^-16 of the spread) — needed when the keys
+// span several binary exponents (unnormalised RAW scores: one pass then resolves only to the exponent)
+template <int T, int PASSES = 1>
 __device__ uint32_t block_kth_lower(uint32_t key, int kth, uint32_t* hist, uint32_t* bcast) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   uint32_t mx = key, mn = key;
@@ -1044,14 +1124,36 @@ __device__ uint32_t block_kth_lower(uint32_t key, int kth, uint32_t* hist, uint3
   __syncthreads();
   pick_digit(hist, (uint32_t)kth, prefix, shift, bcast);
   __syncthreads();
-  const uint32_t r = bcast[0];
+  uint32_t r = bcast[0];
+  if (PASSES > 1 && shift >= 8) {
+    const uint32_t krem = bcast[1];
+    const int shift2 = shift - 8;
+    __syncthreads();
+    for (int i = tid; i < 256; i += T) hist[i] = 0;
+    __syncthreads();
+    if ((key >> shift) == (r >> shift)) atomicAdd(&hist[(key >> shift2) & 255u], 1u);
+    __syncthreads();
+    pick_digit(hist, krem, r, shift2, bcast);
+    __syncthreads();
+    r = bcast[0];
+  }
   __syncthreads();
   return r;
 }
 
-template <int MODE, int NC, int T>
+// COARSE (MODE 1 / 2, 16 units = one 64-row block): the scan also wrote per-(query, block) maxima
+// bvals; (A)-(C) run on those first — the K-th largest thread max over block maxima is a lower bound
+// b of t (each block max is a distinct row's score), and only blocks whose max clears b - 2 delta have
+// their 16 unit maxima read; when more units than 2K + 32 qualify, the K-th largest of THEIR values
+// (again a distinct-row bound, >= b) tightens the threshold before the re-score.
+// RAW: the scan scored the unnormalised query (knn_scan_f16_gmax<RAW>): the margin is per query,
+// two_delta * |q| + two_delta_abs, |q| computed first (wave 0, canonical order); a query with a
+// component outside fp16 range takes the exact every-row path; |q| = 0 scores every row 0 (rows
+// 0..K-1).
+template <int MODE, int NC, int T, bool COARSE = false, bool RAW = false>
 __global__ __launch_bounds__(T) void knn_select_t(
     const float* __restrict__ vals, int64_t ldV, int64_t nunits, int64_t n, int k, float two_delta,
+    const float* __restrict__ bvals, int64_t ldB, float two_delta_abs,
     const float* __restrict__ q_raw, int d, const double* __restrict__ qnorm64,
     const float* __restrict__ gal, int Dp, const double* __restrict__ gnorm64, int64_t idx_base,
     int64_t* __restrict__ out_idx, float* __restrict__ out_score, double* __restrict__ out_score64,
@@ -1088,38 +1190,109 @@ __global__ __launch_bounds__(T) void knn_select_t(
   const int64_t n4 = nunits >> 2;
   // the first kRegF4 float4 of each thread's strided slice stay in registers for (C): one HBM/L2
   // round trip for rows up to kRegF4 * 4 * 1024 = 32k units, all loads issued together
-  constexpr int kRegF4 = 8;
+  constexpr int kRegF4 = COARSE ? 1 : 8;
   float4 cache[kRegF4];
   float m = -INFINITY;
+  // COARSE: the block maxima (nunits / 16 per query; the first kRegB per thread kept for (C))
+  constexpr int kRegB = 4;
+  const int64_t nblk = nunits >> 4;
+  const float* brow = COARSE ? bvals + qi * ldB : nullptr;
+  float bc[kRegB];
+  if constexpr (COARSE) {
 #pragma unroll
-  for (int it = 0; it < kRegF4; ++it) {
-    // unconditional loads (clamped index, masked value): see knn_prep_queries
-    const int64_t i = tid + (int64_t)it * T;
-    const float4 v = ((const float4*)row)[i < n4 ? i : (n4 > 0 ? n4 - 1 : 0)];
-    cache[it] = i < n4 ? v : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
-  }
+    for (int it = 0; it < kRegB; ++it) {
+      const int64_t i = tid + (int64_t)it * T;
+      const float v = brow[i < nblk ? i : (nblk > 0 ? nblk - 1 : 0)];
+      bc[it] = i < nblk ? v : -INFINITY;
+    }
 #pragma unroll
-  for (int it = 0; it < kRegF4; ++it)
-    m = fmaxf(m, fmaxf(fmaxf(cache[it].x, cache[it].y), fmaxf(cache[it].z, cache[it].w)));
-  for (int64_t i = tid + (int64_t)kRegF4 * T; i < n4; i += T) {
-    const float4 v = ((const float4*)row)[i];
-    m = fmaxf(m, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+    for (int it = 0; it < kRegB; ++it) m = fmaxf(m, bc[it]);
+    for (int64_t i = tid + (int64_t)kRegB * T; i < nblk; i += T) m = fmaxf(m, brow[i]);
+  } else {
+#pragma unroll
+    for (int it = 0; it < kRegF4; ++it) {
+      // unconditional loads (clamped index, masked value): see knn_prep_queries
+      const int64_t i = tid + (int64_t)it * T;
+      const float4 v = ((const float4*)row)[i < n4 ? i : (n4 > 0 ? n4 - 1 : 0)];
+      cache[it] = i < n4 ? v : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    }
+#pragma unroll
+    for (int it = 0; it < kRegF4; ++it)
+      m = fmaxf(m, fmaxf(fmaxf(cache[it].x, cache[it].y), fmaxf(cache[it].z, cache[it].w)));
+    for (int64_t i = tid + (int64_t)kRegF4 * T; i < n4; i += T) {
+      const float4 v = ((const float4*)row)[i];
+      m = fmaxf(m, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+    }
+    for (int64_t i = (n4 << 2) + tid; i < nunits; i += T) m = fmaxf(m, row[i]);
   }
-  for (int64_t i = (n4 << 2) + tid; i < nunits; i += T) m = fmaxf(m, row[i]);
   if (tid == 0) {
     L.bcast[2] = 0;
     L.bcast[3] = 0;
   }
+  // |q| in f64 in the gallery norms' order (knn_prep_gallery: lane sums elements lane + 64c over c,
+  // then the xor tree), so a query equal to a gallery row scores exactly 1 whatever the scan path;
+  // RAW also needs max |q_k| (fp16 range of the scan's operand)
+  double qn = 0.0;
+  auto query_norm = [&]() {
+    if (wave == 0) {
+      double ss = 0.0;
+      float am = 0.f;
+      if constexpr (NC > 0) {
+        for (int e = lane; e < 1024; e += 64) {
+          const float x = L.qrow[e];
+          ss += (double)x * (double)x;
+          am = fmaxf(am, fabsf(x));
+        }
+      } else {
+        for (int e = lane; e < Dp; e += 64) {
+          const float x = e < d ? qr[e] : 0.f;
+          ss += (double)x * (double)x;
+          am = fmaxf(am, fabsf(x));
+        }
+      }
+      ss = mmr::wave_sum(ss);
+      if (RAW) am = mmr::wave_max(am);
+      if (lane == 0) {
+        L.qn = sqrt(ss);
+        L.qmax = am;
+      }
+    }
+  };
+  if (RAW) {
+    __syncthreads();  // qrow staged
+    query_norm();     // L.qn / L.qmax visible after block_kth_lower's first barrier
+  }
   SEL_MARK(1)
   // (B) lower bound of the K-th largest thread max, clamped to -inf's key (smaller keys are NaNs)
-  uint32_t bkey = block_kth_lower<T>(f2key(m), kk, L.hist, L.bcast);
+  uint32_t bkey = block_kth_lower<T, COARSE ? 2 : 1>(f2key(m), kk, L.hist, L.bcast);
   if (bkey < f2key(-INFINITY)) bkey = f2key(-INFINITY);
-  float thr = lower_threshold(key2f(bkey), two_delta);
+  float tdel = two_delta;
+  bool take_all = false;  // RAW, q outside fp16 range: every unit is a candidate (exact, slow)
+  if (RAW) {
+    const double qn0 = L.qn;
+    if (qn0 == 0.0) {
+      // s(q, g) = 0 for every row: rows 0 .. kk-1 (ties by lower index)
+      for (int r = tid; r < kk; r += T) {
+        oi[r] = (int64_t)r + idx_base;
+        if (os) os[r] = 0.f;
+        if (os64) os64[r] = 0.0;
+      }
+      return;
+    }
+    const double td = (double)two_delta * qn0 + (double)two_delta_abs;
+    tdel = (float)td;
+    if ((double)tdel < td) tdel = nextafterf(tdel, INFINITY);
+    take_all = !(L.qmax < 32768.f);
+  }
+  float thr = take_all ? -INFINITY : lower_threshold(key2f(bkey), tdel);
   SEL_MARK(2)
   auto take = [&](int64_t u, float v, float th) {
-    if (v >= th && v > -INFINITY) {
+    if (take_all || (v >= th && v > -INFINITY)) {
       const uint32_t p = atomicAdd(&L.bcast[2], 1u);
-      if (p < (uint32_t)UC) L.cand_u[p] = (int)u;
+      if (p < (uint32_t)UC) {
+        L.cand_u[p] = (int)u;
+        L.ukey[p] = f2key(v);
+      }
     }
   };
   // collect the units of [lo, hi) (float4-aligned lo) with value >= th into cand_u; returns the count
@@ -1150,24 +1323,6 @@ __global__ __launch_bounds__(T) void knn_select_t(
     __syncthreads();  // reset visible before any thread's next take()
     return c;
   };
-  // |q| in f64 in the gallery norms' order (knn_prep_gallery: lane sums elements lane + 64c over c,
-  // then the xor tree), so a query equal to a gallery row scores exactly 1 whatever the scan path
-  double qn = 0.0;
-  auto query_norm = [&]() {
-    if (wave == 0) {
-      double ss = 0.0;
-      if constexpr (NC > 0) {
-        for (int e = lane; e < 1024; e += 64) ss += (double)L.qrow[e] * (double)L.qrow[e];
-      } else {
-        for (int e = lane; e < Dp; e += 64) {
-          const double x = e < d ? (double)qr[e] : 0.0;
-          ss += x * x;
-        }
-      }
-      ss = mmr::wave_sum(ss);
-      if (lane == 0) L.qn = sqrt(ss);
-    }
-  };
   // (E) re-score the rows of cnt collected units in f64 into slots [kMaxK, ...)
   auto rescore = [&](int cnt) -> int {
     const int nslot = GS * cnt;
@@ -1182,7 +1337,9 @@ __global__ __launch_bounds__(T) void knn_select_t(
       // latency-bound: each wave issues the float4 loads of its RB rows (NC 256-float chunks each)
       // before reducing any of them, so up to 16*RB rows (48 at Dp = 768: a usual 11-unit candidate
       // set) take one round trip; the query row from LDS (lane owns elements 4(64c + lane) .. +3)
-      constexpr int RB = NC <= 2 ? 4 : NC == 3 ? 3 : 2;  // (a 256-thread variant with 8-12 rows per wave: 2x slower)
+      // (1024 threads; a 256-thread variant with 8-12 rows per wave: 2x slower); 512 threads: 8 rows at NC 3
+      // (64 rows, a usual 13-unit candidate set, in one round trip)
+      constexpr int RB = T >= 1024 ? (NC <= 2 ? 4 : NC == 3 ? 3 : 2) : (NC <= 2 ? 8 : NC == 3 ? 8 : 6);
       for (int s0 = wave * RB; s0 < nslot; s0 += (T / 64) * RB) {
         float4 gv[RB][NC];
         double gnr[RB];  // row norms loaded with the rows (not after the reduction: one round trip)
@@ -1282,10 +1439,76 @@ __global__ __launch_bounds__(T) void knn_select_t(
     __syncthreads();
     return kept;
   };
-  int cnt = collect(thr, true, 0, nunits);
-  query_norm();  // read after rescore's first barrier
+  int cnt;
+  bool coarse_ok = COARSE && !take_all;
+  if (COARSE && !take_all) {
+    // (C, coarse) blocks whose max clears thr, then their units
+    for (int it = 0; it < kRegB; ++it) {
+      const int64_t i = tid + (int64_t)it * T;
+      if (i < nblk && bc[it] >= thr && bc[it] > -INFINITY) {
+        const uint32_t p = atomicAdd(&L.bcast[3], 1u);
+        if (p < (uint32_t)kBlkCap) L.cand_b[p] = (int)i;
+      }
+    }
+    for (int64_t i = tid + (int64_t)kRegB * T; i < nblk; i += T) {
+      const float v = brow[i];
+      if (v >= thr && v > -INFINITY) {
+        const uint32_t p = atomicAdd(&L.bcast[3], 1u);
+        if (p < (uint32_t)kBlkCap) L.cand_b[p] = (int)i;
+      }
+    }
+    __syncthreads();
+    const int nb = (int)L.bcast[3];
+    SEL_VAL(10, nb)
+    __syncthreads();
+    if (tid == 0) L.bcast[3] = 0;
+    if (nb > kBlkCap) {
+      coarse_ok = false;
+      cnt = collect(thr, false, 0, nunits);
+    } else {
+      // one unit per thread-slot: all loads of a pass issued together
+      for (int s0 = 0; s0 < nb * 16; s0 += T) {
+        const int s = s0 + tid;
+        const int64_t u = (int64_t)L.cand_b[(s < nb * 16 ? s : 0) >> 4] * 16 + (s & 15);
+        const float v = row[u];
+        if (s < nb * 16) take(u, v, thr);
+      }
+      __syncthreads();
+      cnt = (int)L.bcast[2];
+      __syncthreads();
+      if (tid == 0) L.bcast[2] = 0;
+      __syncthreads();
+    }
+    SEL_VAL(11, cnt)
+    if (coarse_ok && cnt <= UC && cnt > 2 * kk + 32) {
+      // tighten: the exact K-th largest of the collected units' values (distinct rows: <= t)
+      const float t2 = key2f(block_select_kth(L.ukey, cnt, kk, L.hist, L.bcast, 4));
+      const float thr2 = lower_threshold(t2, tdel);
+      if (thr2 > thr) {
+        const uint32_t k2 = f2key(thr2);
+        for (int p = tid; p < cnt; p += T)
+          if (L.ukey[p] >= k2 && key2f(L.ukey[p]) > -INFINITY) {
+            const uint32_t o = atomicAdd(&L.bcast[2], 1u);
+            L.cand_b[o] = L.cand_u[p];  // cnt <= UC <= kBlkCap
+          }
+        __syncthreads();
+        cnt = (int)L.bcast[2];
+        for (int p = tid; p < cnt; p += T) L.cand_u[p] = L.cand_b[p];
+        thr = thr2;
+        __syncthreads();
+        if (tid == 0) L.bcast[2] = 0;
+        __syncthreads();
+      }
+    }
+  } else {
+    cnt = collect(thr, !COARSE, 0, nunits);
+  }
+  if (!RAW) query_norm();  // read after rescore's first barrier
+  SEL_VAL(12, cnt)
+  SEL_VAL(13, take_all)
+  SEL_VAL(14, __float_as_int(thr))
   SEL_MARK(3)
-  if (cnt > UC) {
+  if (cnt > UC && !take_all) {
     const float t = key2f(row_select_kth(row, nunits, kk, L.hist, L.bcast));
     thr = lower_threshold(t, two_delta);
     cnt = collect(thr, false, 0, nunits);
@@ -1508,6 +1731,8 @@ struct mmr_index {
   float* qn = nullptr;        // [rows][Dp] f32 (or fp16 / tile layouts, same bytes or fewer)
   double* qnorm64 = nullptr;  // [rows]
   float* vals = nullptr;      // scores (f32 mode) or per-(query, unit) maxima
+  int64_t ws_bvals = 0;       // floats in bvals
+  float* bvals = nullptr;     // mode f16: per-(query, 64-row block) maxima [256][Np/64]
   uint16_t* qs = nullptr;     // [rows][3Dp] bf16 split queries (x3 GEMM)
   int n_cu = 256;             // compute units of `device` (persistent grids)
   hipEvent_t ws_event = nullptr;
@@ -1545,7 +1770,7 @@ mmr_status grow(mmr_index* ix, T*& buf, int64_t& have, int64_t want, size_t elem
 // Workspace for a search of nq queries in the current mode (rows rounded to 256).
 mmr_status ensure_ws(mmr_index* ix, int64_t nq) {
   const int64_t cq = round_up(nq < chunk_queries(ix) ? nq : chunk_queries(ix), 256);
-  int64_t rows = cq, vals = 0, qs = 0;
+  int64_t rows = cq, vals = 0, qs = 0, bvals = 0;
   if (ix->mode == 0) {
     vals = cq * ix->Np;
   } else if (ix->mode == 1) {
@@ -1554,6 +1779,7 @@ mmr_status ensure_ws(mmr_index* ix, int64_t nq) {
   } else {
     rows = 256;
     vals = 256 * (ix->Np / 4);
+    bvals = 256 * (ix->Np / 64);
   }
   int64_t hq = ix->ws_qrows, hq2 = ix->ws_qrows;
   mmr_status s = grow(ix, ix->qn, hq, rows, sizeof(float) * ix->Dp);
@@ -1562,6 +1788,7 @@ mmr_status ensure_ws(mmr_index* ix, int64_t nq) {
   ix->ws_qrows = hq < hq2 ? hq : hq2;
   if ((s = grow(ix, ix->vals, ix->ws_vals, vals, sizeof(float))) != MMR_OK) return s;
   if (qs > 0 && (s = grow(ix, ix->qs, ix->ws_qsrows, qs, sizeof(uint16_t) * 3 * ix->Dp)) != MMR_OK) return s;
+  if (bvals > 0 && (s = grow(ix, ix->bvals, ix->ws_bvals, bvals, sizeof(float))) != MMR_OK) return s;
   return MMR_OK;
 }
 
@@ -1590,28 +1817,38 @@ struct DeviceGuard {
 
 // The LDS-staged fp16 tile scan for 33-256-query passes (MMR_KNN_F16_TILE=0: the one-wave stream
 // kernel instead, for A/B measurements).
+// The raw-query small-Q f16 scan (MMR_KNN_F16_RAW=0: prep launch + normalised scan, for A/B).
+bool raw_scan_enabled() {
+  const char* e = getenv("MMR_KNN_F16_RAW");
+  return !(e && atoi(e) == 0);
+}
+
 bool f16_tile_enabled() {
   const char* e = getenv("MMR_KNN_F16_TILE");
   return !(e && atoi(e) == 0);
 }
 
 template <int WQ, int MQ, int WR, int MR, bool PF>
-void launch_f16_tile(hipStream_t st, const mmr_index* ix, const uint16_t* qh, float* gm, int64_t ldG, int64_t n_rt) {
+void launch_f16_tile(hipStream_t st, const mmr_index* ix, const uint16_t* qh, float* gm, float* bm, int64_t ldG,
+                     int64_t ldB, int64_t n_rt) {
   using C = F16TileCfg<WQ, MQ, WR, MR, PF>;
   const size_t lds = (size_t)C::STAGES * C::SLICE_B;
   knn_scan_f16_tile<WQ, MQ, WR, MR, PF><<<dim3((unsigned)ix->n_cu), dim3(64 * C::NW), lds, st>>>(
-      qh, ix->gh, gm, ix->Dp, ldG, ix->n, n_rt);
+      qh, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, n_rt);
 }
 
-template <int MODE>
+// COARSE selections (block maxima first) run 512-thread workgroups, the unit-level ones 1024
+template <int MODE, bool COARSE = false, bool RAW = false>
 void launch_select(hipStream_t st, int64_t nq, const float* vals, int64_t ldV, int64_t nunits, const mmr_index* ix,
                    int k, float two_delta, const float* q_raw, const double* qnorm64, int64_t* oi, float* os,
-                   double* os64, int32_t* ost) {
-  const dim3 g((unsigned)nq), b(kSelThreads);
+                   double* os64, int32_t* ost, const float* bvals = nullptr, int64_t ldB = 0,
+                   float two_delta_abs = 0.f) {
+  constexpr int T = COARSE ? 512 : kSelThreads;
+  const dim3 g((unsigned)nq), b(T);
 #define MMR_SEL(NC)                                                                                              \
-  knn_select_t<MODE, NC, kSelThreads><<<g, b, 0, st>>>(vals, ldV, nunits, ix->n, k, two_delta, q_raw, ix->d,     \
-                                                       qnorm64, ix->gal, ix->Dp, ix->norm64, ix->idx_base, oi, os, \
-                                                       os64, ost)
+  knn_select_t<MODE, NC, T, COARSE, RAW><<<g, b, 0, st>>>(vals, ldV, nunits, ix->n, k, two_delta, bvals, ldB,    \
+                                                          two_delta_abs, q_raw, ix->d, qnorm64, ix->gal, ix->Dp,  \
+                                                          ix->norm64, ix->idx_base, oi, os, os64, ost)
   // NC = 256-float chunks of a row in the f64 re-score (0: d > 1024, strided loop)
   switch (ix->d > 1024 ? 0 : (int)ceil_div(ix->Dp, 256)) {
     case 1: MMR_SEL(1); break;
@@ -1720,6 +1957,7 @@ mmr_status mmr_index_destroy(mmr_index* ix) {
   if (ix->qn) (void)hipFree(ix->qn);
   if (ix->qnorm64) (void)hipFree(ix->qnorm64);
   if (ix->vals) (void)hipFree(ix->vals);
+  if (ix->bvals) (void)hipFree(ix->bvals);
   if (ix->ws_event) (void)hipEventDestroy(ix->ws_event);
   delete ix;
   return MMR_OK;
@@ -1771,6 +2009,14 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
   const float two_delta3 = 2.0f * ((float)(3 * ix->Dp + 16) * 5.9604645e-8f + 4.0f * 1.5258789e-5f);
   const float two_delta16 = 2.0f * (9.765625e-4f + 2.0f * sqrtf((float)ix->Dp) * 2.9802322e-8f +
                                     (float)(2 * ix->Dp + 64) * 5.9604645e-8f);
+  //  f16 RAW (knn_scan_f16_gmax<RAW>: fp16(q) . g^ for the unnormalised q): the same terms scaled by |q|
+  //      — fp16 rounding 2^-10 |q| (Cauchy-Schwarz over |q| |g^|), g^'s subnormal half-ulps
+  //      sum |q_k| 2^-25 <= sqrt(Dp) |q| 2^-25, f32 accumulation (2Dp + 64) 2^-24 |q| — plus q's own
+  //      subnormal half-ulps sum |g^_k| 2^-25 <= sqrt(Dp) 2^-25, independent of |q|:
+  //      delta = |q| two_delta16r / 2 + two_delta16a / 2 (the selection computes |q| first).
+  const float two_delta16r = 2.0f * (9.765625e-4f + sqrtf((float)ix->Dp) * 2.9802322e-8f +
+                                     (float)(2 * ix->Dp + 64) * 5.9604645e-8f);
+  const float two_delta16a = 2.0f * sqrtf((float)ix->Dp) * 2.9802322e-8f;
   const int64_t chunk = chunk_queries(ix);
   for (int64_t c0 = 0; c0 < nq; c0 += chunk) {
     const int64_t cq = nq - c0 < chunk ? nq - c0 : chunk;
@@ -1789,7 +2035,8 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
         const float* qp = qc + p0 * ix->d;
         const uint16_t* qh = (const uint16_t*)ix->qn;
         float* gm = ix->vals;
-        const int64_t ldG = ix->Np / 4;
+        float* bm = ix->bvals;
+        const int64_t ldG = ix->Np / 4, ldB = ix->Np / 64;
         if (pq > 32 && f16_tile_enabled()) {
           // 33-256 queries: the LDS-staged tile scan (64 / 128 / 256-query tiles), contiguous units
           const int wq = pq <= 64 ? 1 : pq <= 128 ? 2 : 4;
@@ -1801,43 +2048,63 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
           const char* ce = getenv("MMR_KNN_F16_CFG");  // tile shape (A/B measurements)
           const int cfg = ce ? atoi(ce) : 0;
           if (wq == 1) {
-            if (cfg == 1) launch_f16_tile<1, 4, 4, 4, true>(st, ix, qh, gm, ldG, n_rt);
-            else launch_f16_tile<1, 4, 4, 4, false>(st, ix, qh, gm, ldG, n_rt);
+            if (cfg == 1) launch_f16_tile<1, 4, 4, 4, true>(st, ix, qh, gm, bm, ldG, ldB, n_rt);
+            else launch_f16_tile<1, 4, 4, 4, false>(st, ix, qh, gm, bm, ldG, ldB, n_rt);
           } else if (wq == 2) {
-            if (cfg == 1) launch_f16_tile<1, 8, 4, 4, true>(st, ix, qh, gm, ldG, n_rt);
-            else launch_f16_tile<2, 4, 4, 4, false>(st, ix, qh, gm, ldG, n_rt);
+            if (cfg == 1) launch_f16_tile<1, 8, 4, 4, true>(st, ix, qh, gm, bm, ldG, ldB, n_rt);
+            else launch_f16_tile<2, 4, 4, 4, false>(st, ix, qh, gm, bm, ldG, ldB, n_rt);
           } else {
-            if (cfg == 1) launch_f16_tile<4, 4, 2, 8, true>(st, ix, qh, gm, ldG, n_rt);
-            else if (cfg == 2) launch_f16_tile<2, 8, 2, 8, true>(st, ix, qh, gm, ldG, n_rt);
-            else launch_f16_tile<4, 4, 2, 8, false>(st, ix, qh, gm, ldG, n_rt);
+            if (cfg == 1) launch_f16_tile<4, 4, 2, 8, true>(st, ix, qh, gm, bm, ldG, ldB, n_rt);
+            else if (cfg == 2) launch_f16_tile<2, 8, 2, 8, true>(st, ix, qh, gm, bm, ldG, ldB, n_rt);
+            else launch_f16_tile<4, 4, 2, 8, false>(st, ix, qh, gm, bm, ldG, ldB, n_rt);
           }
           MMR_LAUNCH_CHECK();
-          launch_select<2>(st, pq, gm, ldG, ldG, ix, k, two_delta16, qp, ix->qnorm64, oi + p0 * k,
-                           os ? os + p0 * k : nullptr, os64 ? os64 + p0 * k : nullptr, ost ? ost + p0 : nullptr);
+          launch_select<2, true>(st, pq, gm, ldG, ldG, ix, k, two_delta16, qp, ix->qnorm64, oi + p0 * k,
+                                 os ? os + p0 * k : nullptr, os64 ? os64 + p0 * k : nullptr, ost ? ost + p0 : nullptr,
+                                 bm, ldB);
+          MMR_LAUNCH_CHECK();
+          continue;
+        }
+        const dim3 grid((unsigned)(ix->Np / 64));
+        if (qt <= 2 && ix->d % 8 == 0 && ((uintptr_t)qp & 15) == 0 && raw_scan_enabled()) {
+          // <= 32 queries: the scan reads the caller's f32 rows itself (no prep launch), per-query margin
+          const int64_t nqp = pq;
+          if (qt == 1) {
+            if (ix->Dp % 128 == 0)
+              knn_scan_f16_gmax<1, 128, 1, true><<<grid, 64, 0, st>>>(nullptr, qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n);
+            else
+              knn_scan_f16_gmax<1, 64, 1, true><<<grid, 64, 0, st>>>(nullptr, qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n);
+          } else {
+            knn_scan_f16_gmax<2, 64, 1, true><<<grid, 64, 0, st>>>(nullptr, qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n);
+          }
+          MMR_LAUNCH_CHECK();
+          launch_select<1, true, true>(st, pq, gm, ldG, ldG, ix, k, two_delta16r, qp, ix->qnorm64, oi + p0 * k,
+                                       os ? os + p0 * k : nullptr, os64 ? os64 + p0 * k : nullptr,
+                                       ost ? ost + p0 : nullptr, bm, ldB, two_delta16a);
           MMR_LAUNCH_CHECK();
           continue;
         }
         knn_prep_queries<<<dim3((unsigned)ceil_div(Qp, 4)), dim3(256), 0, st>>>(
             qp, pq, ix->d, ix->qn, ix->Dp, Qp, ix->qnorm64, 2);
         MMR_LAUNCH_CHECK();
-        const dim3 grid((unsigned)(ix->Np / 64));
         switch (qt) {
           // KC must divide Dp (a multiple of 64): the 128-wide chunk only when Dp % 128 == 0
           case 1:
-            if (ix->Dp % 128 == 0) knn_scan_f16_gmax<1, 128><<<grid, 64, 0, st>>>(qh, ix->gh, gm, ix->Dp, ldG, ix->n);
-            else knn_scan_f16_gmax<1, 64><<<grid, 64, 0, st>>>(qh, ix->gh, gm, ix->Dp, ldG, ix->n);
+            if (ix->Dp % 128 == 0) knn_scan_f16_gmax<1, 128><<<grid, 64, 0, st>>>(qh, nullptr, 0, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n);
+            else knn_scan_f16_gmax<1, 64><<<grid, 64, 0, st>>>(qh, nullptr, 0, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n);
             break;
           case 2:
-            if (ix->Dp % 128 == 0) knn_scan_f16_gmax<2, 128><<<grid, 64, 0, st>>>(qh, ix->gh, gm, ix->Dp, ldG, ix->n);
-            else knn_scan_f16_gmax<2, 64><<<grid, 64, 0, st>>>(qh, ix->gh, gm, ix->Dp, ldG, ix->n);
+            if (ix->Dp % 128 == 0) knn_scan_f16_gmax<2, 128><<<grid, 64, 0, st>>>(qh, nullptr, 0, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n);
+            else knn_scan_f16_gmax<2, 64><<<grid, 64, 0, st>>>(qh, nullptr, 0, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n);
             break;
-          case 4: knn_scan_f16_gmax<4, 64><<<grid, 64, 0, st>>>(qh, ix->gh, gm, ix->Dp, ldG, ix->n); break;
-          case 8: knn_scan_f16_gmax<8, 64><<<grid, 64, 0, st>>>(qh, ix->gh, gm, ix->Dp, ldG, ix->n); break;
-          default: knn_scan_f16_gmax<16, 32><<<grid, 64, 0, st>>>(qh, ix->gh, gm, ix->Dp, ldG, ix->n); break;
+          case 4: knn_scan_f16_gmax<4, 64><<<grid, 64, 0, st>>>(qh, nullptr, 0, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n); break;
+          case 8: knn_scan_f16_gmax<8, 64><<<grid, 64, 0, st>>>(qh, nullptr, 0, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n); break;
+          default: knn_scan_f16_gmax<16, 32><<<grid, 64, 0, st>>>(qh, nullptr, 0, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n); break;
         }
         MMR_LAUNCH_CHECK();
-        launch_select<1>(st, pq, gm, ldG, ldG, ix, k, two_delta16, qp, ix->qnorm64, oi + p0 * k,
-                         os ? os + p0 * k : nullptr, os64 ? os64 + p0 * k : nullptr, ost ? ost + p0 : nullptr);
+        launch_select<1, true>(st, pq, gm, ldG, ldG, ix, k, two_delta16, qp, ix->qnorm64, oi + p0 * k,
+                               os ? os + p0 * k : nullptr, os64 ? os64 + p0 * k : nullptr, ost ? ost + p0 : nullptr,
+                               bm, ldB);
         MMR_LAUNCH_CHECK();
       }
     } else if (ix->mode == 1 && cq <= skinny_max_q()) {

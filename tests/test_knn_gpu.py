@@ -312,3 +312,58 @@ def test_knn_two_streams_share_one_index():
         for oa, ob in outs:
             assert torch.equal(oa, ra) and torch.equal(ob, rb)
         ix.close()
+
+
+def test_knn_f16_raw_query_range():
+    """Q <= 32 f16 searches score the caller's unnormalised rows in fp16 (no prep launch): a zero
+    query (every score 0 -> rows 0..K-1), tiny and large norms (per-query margin), a component beyond
+    fp16's safe range (the exact every-row path), and a query view that is not 16-B aligned (prep
+    path) all return the oracle's exact lists; the prep path agrees bit for bit."""
+    rng = np.random.default_rng(808)
+    G = rng.standard_normal((6000, 256), dtype=np.float32)
+    G[3000:3004] = G[17]
+    Qm = rng.standard_normal((12, 256), dtype=np.float32)
+    Qm[0] = 0.0
+    Qm[1] = G[17] * 1e-7             # |q| ~ 1.6e-6: fp16 subnormals, margin dominated by delta_abs
+    Qm[2] = G[17] * 3e3              # large but in range
+    Qm[3] = rng.standard_normal(256).astype(np.float32)
+    Qm[3, 5] = 5e4                   # beyond the fp16-safe range -> every-row path
+    Qm[4] = G[17] * 1e-3
+    gi, _ = _exact_check(G, Qm, 12, mode="f16")
+    assert gi[0].tolist() == list(range(12))
+    for r in (1, 2, 4):
+        assert gi[r, :5].tolist() == [17, 3000, 3001, 3002, 3003]
+    # unaligned view: 1 float in, same rows -> prep + normalised scan, same exact lists
+    buf = torch.from_numpy(np.concatenate([np.zeros(1, np.float32), Qm.ravel()])).cuda()
+    qv = buf[1:].view(12, 256)
+    ix = GalleryIndex(G, mode="f16")
+    i2, _, s2, st2 = ix.search(qv, 12, want_f64=True, want_status=True)
+    os.environ["MMR_KNN_F16_RAW"] = "0"
+    try:
+        i3, _, s3, _ = ix.search(torch.from_numpy(Qm).cuda(), 12, want_f64=True, want_status=True)
+    finally:
+        del os.environ["MMR_KNN_F16_RAW"]
+    torch.cuda.synchronize()
+    ix.close()
+    assert int(st2.max()) == 0
+    np.testing.assert_array_equal(i2.cpu().numpy(), gi)
+    np.testing.assert_array_equal(i3.cpu().numpy(), gi)
+    assert torch.equal(s2, s3)
+
+
+@pytest.mark.parametrize("Q", [5, 40, 256])
+@pytest.mark.parametrize("K", [10, 100])
+def test_knn_f16_coarse_select_clusters(Q, K):
+    """The f16 selection reads per-(query, 64-row block) maxima first: tight clusters put hundreds of
+    rows inside the margin (the tightening pass) and a run of near-duplicates inside one block (a
+    loose thread-max bound); lists stay exact."""
+    rng = np.random.default_rng(Q * 1000 + K)
+    G = rng.standard_normal((30_000, 128), dtype=np.float32)
+    c = rng.standard_normal(128).astype(np.float32)
+    G[4096:6096] = c + 0.05 * rng.standard_normal((2000, 128), dtype=np.float32)   # 2000-row cluster
+    G[20_000:20_064] = G[7] + 1e-4 * rng.standard_normal((64, 128), dtype=np.float32)  # one block
+    Qm = rng.standard_normal((Q, 128), dtype=np.float32)
+    Qm[0] = c
+    Qm[1] = G[7]
+    Qm[2] = -c
+    _exact_check(G, Qm, K, mode="f16")

@@ -38,11 +38,13 @@ int main(int argc, char** argv) {
     }
     hipDeviceSynchronize();
     long long t[16];
+    hipMemset(0, 0, 0);
     hipMemcpyFromSymbol(t, HIP_SYMBOL(g_sel_trace), sizeof(t));
     if (it < 2) continue;
     printf("n=%lld Q=%d mode=%d run %d: groups collected %lld, total %.2f us |", (long long)n, Q, mode, it, t[6], (t[5] - t[0]) * 0.01);
     for (int p = 0; p < 5; ++p) printf(" %s %.2f |", names[p], (t[p + 1] - t[p]) * 0.01);
     printf(" [E: fill %.2f, loads+math (block 0, wave 0) %.2f]", (t[8] - t[3]) * 0.01, (t[9] - t[8]) * 0.01);
+    printf(" [coarse: blocks %lld, units %lld, final %lld, take_all %lld, thr %g]", t[10], t[11], t[12], t[13], __builtin_bit_cast(float, (int)t[14]));
     printf("\n");
   }
   mmr_index_destroy(ix);
