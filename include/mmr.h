@@ -73,7 +73,10 @@ mmr_status mmr_index_set_mode(mmr_index* index, int32_t mode);
  * selection kernel, exactly, never truncated (a non-zero value would flag an inexact list).
  * Asynchronous on `stream`.  Threading: calls on one index may come from several host threads and
  * several streams; the index's workspace follows the stream (a search on a new stream first waits
- * for the previous search's last use), so concurrent searches serialise on the device but never race. */
+ * for the previous search's last use), so concurrent searches serialise on the device but never race.
+ * The hand-over event is recorded on the previous search's stream at the switch (not after every
+ * search: a per-search event record cost 3-5 us of device time), so that stream must still exist
+ * when a search on another stream, or a workspace growth, follows. */
 mmr_status mmr_index_search(mmr_index* index, const float* q, int64_t nq, int32_t k,
                             int64_t* out_idx, float* out_score, double* out_score64,
                             int32_t* out_status, void* stream);

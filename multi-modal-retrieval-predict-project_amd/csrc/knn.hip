@@ -586,6 +586,101 @@ __global__ __launch_bounds__(64 * WQ) void knn_scan_f16_gmax(const uint16_t* __r
     }
 }
 
+// LQ (Q <= 32, raw queries, d % 8 == 0): the knn_scan_f16_gmax<RAW> stream with the query operand
+// converted ONCE per workgroup into LDS (tile32h fp16 pieces, the MFMA operand layout) instead of once
+// per 64-row block from the caller's f32 rows in L2: a block then moves its 96 KB of gallery and no
+// query bytes through the CU's load path (RAW: + 48 KB of f32 queries per block at QT = 1).
+// Persistent: workgroup w owns the 64-row blocks [nblk*w/G, nblk*(w+1)/G) (one workgroup per CU),
+// its NWV waves take them round-robin; same unit / block maxima as knn_scan_f16_gmax<RAW>.
+template <int QT, int KC, int NWV>
+__global__ __launch_bounds__(64 * NWV) void knn_scan_f16_lq(const float* __restrict__ qraw, int64_t nq, int d,
+                                                          const uint16_t* __restrict__ gh,
+                                                          float* __restrict__ gmax, float* __restrict__ bmax,
+                                                          int Dp, int64_t ldG, int64_t ldB, int64_t n, int64_t nblk) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  constexpr int L = KC / 32;  // 1-KB pieces per tile per chunk
+  extern __shared__ __attribute__((aligned(16))) uint16_t qs[];  // [QT][Dp/32][512] halfs
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int KP = Dp / 32;
+  // (1) queries -> fp16 tile32h in LDS: one (row, 8-k group) per item, 16-B store; rows >= nq and
+  //     k >= d are zero (unconditional clamped loads, masked at the conversion)
+  const int groups = QT * 16 * (Dp / 8);
+  for (int gi = tid; gi < groups; gi += 64 * NWV) {
+    const int row = gi / (Dp / 8), k0 = (gi % (Dp / 8)) * 8;
+    const bool ok = row < nq && k0 < d;
+    const float* src = qraw + (int64_t)(row < nq ? row : nq - 1) * d + (k0 < d ? k0 : d - 8);
+    const float4 x0 = *(const float4*)src, x1 = *(const float4*)(src + 4);
+    h8 o;
+    o[0] = (_Float16)x0.x; o[1] = (_Float16)x0.y; o[2] = (_Float16)x0.z; o[3] = (_Float16)x0.w;
+    o[4] = (_Float16)x1.x; o[5] = (_Float16)x1.y; o[6] = (_Float16)x1.z; o[7] = (_Float16)x1.w;
+    *(h8*)(qs + tile32h_index(row, k0, Dp)) = ok ? o : (h8){0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  __syncthreads();
+  const int r = lane & 15, h = lane >> 4;
+  const int64_t tileB = 16 * (int64_t)Dp;  // halfs per 16-row tile
+  const int64_t b_lo = nblk * blockIdx.x / gridDim.x, b_hi = nblk * (blockIdx.x + 1) / gridDim.x;
+  const char* qbase = (const char*)qs + lane * 16;
+  for (int64_t blk = b_lo + wave; blk < b_hi; blk += NWV) {
+    const int64_t g0 = blk * 64;
+    const uint16_t* pb = gh + g0 * Dp + 8 * lane;
+    f32x4 acc[QT][4];
+#pragma unroll
+    for (int t = 0; t < QT; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[t][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    f32x4 b[4][L];
+#pragma unroll
+    for (int e = 0; e < L; ++e)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j][e] = __builtin_nontemporal_load((const f32x4*)(pb + j * tileB + 512 * e));
+#pragma unroll 1
+    for (int kc = 0; kc < Dp; kc += KC) {
+      // the next chunk's gallery pieces are issued before this chunk's MFMAs (the last re-reads itself)
+      const int kn = kc + KC < Dp ? kc + KC : kc;
+      f32x4 nb[4][L];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < L; ++e)
+          nb[j][e] = __builtin_nontemporal_load((const f32x4*)(pb + j * tileB + 16 * kn + 512 * e));
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int e = 0; e < L; ++e)
+#pragma unroll
+        for (int t = 0; t < QT; ++t) {
+          const h8 av = *(const h8*)(qbase + ((int64_t)t * KP + kc / 32 + e) * 1024);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, __builtin_bit_cast(h8, b[j][e]), acc[t][j], 0, 0, 0);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int e = 0; e < L; ++e)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j][e] = nb[j][e];
+    }
+    const int64_t gcol = blk * 16 + r;
+    bool pad[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pad[j] = g0 + 16 * j + r >= n;
+#pragma unroll
+    for (int t = 0; t < QT; ++t)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        float mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mx = fmaxf(mx, pad[j] ? -INFINITY : acc[t][j][rg]);
+        const int64_t qrw = 16 * t + 4 * h + rg;
+        gmax[qrw * ldG + gcol] = mx;
+        float bm = mx;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) bm = fmaxf(bm, __shfl_xor(bm, o, 64));
+        if (r == 0) bmax[qrw * ldB + blk] = bm;
+      }
+  }
+}
+
 // ------------------------------------------------------------------ fp16 tile scan (mode f16, Q > 32)
 // The same fp16 product as knn_scan_f16_gmax, as an LDS-staged MFMA GEMM for query passes of 64-256
 // queries.  Workgroup tile: RT = WR*MR gallery row tiles (16 rows each) x QT = WQ*MQ query tiles, one
@@ -1058,7 +1153,10 @@ __device__ __forceinline__ int64_t unit_row(int64_t u, int m) {
   return 4 * u + m;
 }
 
-constexpr int kBlkCap = 1024;  // 64-row blocks collected by the coarse pass (more: the unit-level pass)
+constexpr int kBlkCap = 1024;
+// A/B switch of the select's first bound (MMR_KNN_TOP4=0: the 2-pass radix), set by mmr_index_create
+__constant__ int g_top4_bound = 1;
+__device__ __forceinline__ bool top4_bound_enabled() { return g_top4_bound != 0; }  // 64-row blocks collected by the coarse pass (more: the unit-level pass)
 
 template <int T>
 struct SelLds {
@@ -1137,6 +1235,43 @@ __device__ uint32_t block_kth_lower(uint32_t key, int kth, uint32_t* hist, uint3
     __syncthreads();
     r = bcast[0];
   }
+  __syncthreads();
+  return r;
+}
+
+// Lower bound of the kth largest of the block's keys (kth <= 4 * waves) without a radix pass: each
+// wave's 4 largest keys (4 distinct threads: lanes removed one at a time), then the kth largest of
+// those 4 * T/64 values — kth values from distinct threads, so kth distinct rows score at least it.
+// Usually the kth largest overall (a wave holds > 4 of the top keys rarely); ~0.4 us against the
+// 2-pass radix's ~2.7 (select phase clock, Q = 16).
+template <int T>
+__device__ uint32_t block_kth_lower_top4(uint32_t key, int kth, uint32_t* vals, uint32_t* bcast) {
+  constexpr int NV = 4 * (T / 64);
+  static_assert(NV <= 64, "one wave ranks the candidates");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t v = key;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint32_t mx = v;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+    const uint64_t hit = __ballot(v == mx);
+    if (lane == (int)__builtin_ctzll(hit)) v = 0u;  // key 0 sorts below every float key
+    if (lane == 0) vals[wave * 4 + j] = mx;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const uint32_t mine = lane < NV ? vals[lane] : 0u;
+    int rank = 0;  // values ahead of mine (larger, or equal at a lower position)
+#pragma unroll 8
+    for (int j = 0; j < NV; ++j) {
+      const uint32_t o = vals[j];
+      rank += (o > mine) || (o == mine && j < lane);
+    }
+    if (lane < NV && rank == kth - 1) bcast[0] = mine;
+  }
+  __syncthreads();
+  const uint32_t r = bcast[0];
   __syncthreads();
   return r;
 }
@@ -1264,7 +1399,9 @@ __global__ __launch_bounds__(T) void knn_select_t(
   }
   SEL_MARK(1)
   // (B) lower bound of the K-th largest thread max, clamped to -inf's key (smaller keys are NaNs)
-  uint32_t bkey = block_kth_lower<T, COARSE ? 2 : 1>(f2key(m), kk, L.hist, L.bcast);
+  uint32_t bkey = COARSE && kk <= 4 * (T / 64) && top4_bound_enabled()
+                      ? block_kth_lower_top4<T>(f2key(m), kk, L.tmax, L.bcast)
+                      : block_kth_lower<T, COARSE ? 2 : 1>(f2key(m), kk, L.hist, L.bcast);
   if (bkey < f2key(-INFINITY)) bkey = f2key(-INFINITY);
   float tdel = two_delta;
   bool take_all = false;  // RAW, q outside fp16 range: every unit is a candidate (exact, slow)
@@ -1721,9 +1858,11 @@ struct mmr_index {
   uint16_t* gh = nullptr;     // [Np][Dp] fp16 unit rows in the tile32h layout (mode f16; built on first use)
   int mode = 1;               // 0: f32 MFMA scores, 1: bf16x3 split scores, 2: fp16 unit-row scan
   // Workspace: one set per index, sized by what the mode needs (grown on demand).  `mu` serialises
-  // the enqueue of searches; across streams the workspace follows the stream: a search records
-  // ws_event after its last use, and a search on another stream first waits for that event, so two
-  // streams never race on it (and a realloc waits for the last user).
+  // the enqueue of searches; across streams the workspace follows the stream: a search on another
+  // stream records ws_event on ws_stream (the last user's) and waits for it, so two streams never race
+  // on it (and a realloc waits for the last user the same way).  Recorded at the switch, not after
+  // every search: an event record per search cost 3-5 us of device time (16-query search 50.3 ->
+  // 47.2 us back to back).
   std::mutex mu;
   int64_t ws_qrows = 0;       // query rows in qn / qnorm64
   int64_t ws_vals = 0;        // floats in vals
@@ -1753,11 +1892,24 @@ int64_t chunk_queries(const mmr_index* ix) {
   return c < 256 ? 256 : c;
 }
 
+// A/B: record ws_event after every search (MMR_KNN_EAGER_EVENT=1) instead of at a stream switch /
+// workspace growth, on the stream that ran the last search
+bool eager_ws_event() {
+  static const bool v = [] {
+    const char* e = getenv("MMR_KNN_EAGER_EVENT");
+    return e && atoi(e) == 1;
+  }();
+  return v;
+}
+
 template <class T>
 mmr_status grow(mmr_index* ix, T*& buf, int64_t& have, int64_t want, size_t elem_bytes) {
   if (want <= have) return MMR_OK;
   if (buf) {
-    if (ix->ws_used) (void)hipEventSynchronize(ix->ws_event);  // the last search has released it
+    if (ix->ws_used) {  // the last search has released it
+      if (!eager_ws_event()) (void)hipEventRecord(ix->ws_event, ix->ws_stream);
+      (void)hipEventSynchronize(ix->ws_event);
+    }
     (void)hipFree(buf);
   }
   buf = nullptr;
@@ -1823,6 +1975,12 @@ bool raw_scan_enabled() {
   return !(e && atoi(e) == 0);
 }
 
+// The LDS-query persistent small-Q scan (MMR_KNN_F16_LQ=0: the one-wave-per-block RAW stream, for A/B).
+bool lq_scan_enabled() {
+  const char* e = getenv("MMR_KNN_F16_LQ");
+  return !(e && atoi(e) == 0);
+}
+
 bool f16_tile_enabled() {
   const char* e = getenv("MMR_KNN_F16_TILE");
   return !(e && atoi(e) == 0);
@@ -1879,6 +2037,10 @@ mmr_status mmr_index_create(const void* gallery, int64_t n, int32_t d, mmr_dtype
     return MMR_ERR_UNSUPPORTED;
   }
   DeviceGuard g(device);
+  if (const char* e = getenv("MMR_KNN_TOP4"); e && atoi(e) == 0) {  // A/B: the radix first bound
+    const int zero = 0;
+    MMR_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_top4_bound), &zero, sizeof(int)));
+  }
   mmr_index* ix = new mmr_index();
   ix->device = device;
   ix->n = n;
@@ -1993,7 +2155,10 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
   std::lock_guard<std::mutex> lk(ix->mu);
   hipStream_t st = mmr::as_stream(stream);
   // the workspace follows the stream: wait for the previous search if it ran on another stream
-  if (ix->ws_used && ix->ws_stream != st) MMR_CHECK_HIP(hipStreamWaitEvent(st, ix->ws_event, 0));
+  if (ix->ws_used && ix->ws_stream != st) {
+    if (!eager_ws_event()) MMR_CHECK_HIP(hipEventRecord(ix->ws_event, ix->ws_stream));
+    MMR_CHECK_HIP(hipStreamWaitEvent(st, ix->ws_event, 0));
+  }
   mmr_status s = ensure_ws(ix, nq);
   if (s != MMR_OK) return s;
   // |s_approx - s64| <= delta; threshold margin 2*delta.
@@ -2069,7 +2234,19 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
         if (qt <= 2 && ix->d % 8 == 0 && ((uintptr_t)qp & 15) == 0 && raw_scan_enabled()) {
           // <= 32 queries: the scan reads the caller's f32 rows itself (no prep launch), per-query margin
           const int64_t nqp = pq;
-          if (qt == 1) {
+          if (lq_scan_enabled() && ix->Dp <= 1024) {
+            const size_t lds = (size_t)qt * 16 * ix->Dp * 2;
+            const int64_t nblk = ix->Np / 64;
+            const dim3 g2((unsigned)ix->n_cu);
+            if (qt == 1) {
+              if (ix->Dp % 128 == 0)
+                knn_scan_f16_lq<1, 128, 8><<<g2, 512, lds, st>>>(qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, nblk);
+              else
+                knn_scan_f16_lq<1, 64, 8><<<g2, 512, lds, st>>>(qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, nblk);
+            } else {
+              knn_scan_f16_lq<2, 64, 8><<<g2, 512, lds, st>>>(qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, nblk);
+            }
+          } else if (qt == 1) {
             if (ix->Dp % 128 == 0)
               knn_scan_f16_gmax<1, 128, 1, true><<<grid, 64, 0, st>>>(nullptr, qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n);
             else
@@ -2161,7 +2338,7 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
       MMR_LAUNCH_CHECK();
     }
   }
-  MMR_CHECK_HIP(hipEventRecord(ix->ws_event, st));
+  if (eager_ws_event()) MMR_CHECK_HIP(hipEventRecord(ix->ws_event, st));
   ix->ws_stream = st;
   ix->ws_used = true;
   return MMR_OK;
