@@ -493,14 +493,15 @@ __device__ __forceinline__ f32x4 mx_mfma(i32x8 a, i32x8 b, f32x4 c, uint32_t sa,
   return c;
 }
 
-template <int NT, bool FP8 = false>
+template <int NT, bool FP8 = false, bool KNN = false>
 struct P8 {
   static constexpr int TBN = 64 * NT;
   static constexpr int SC = FP8 ? 1024 : 0;            // uint16 elements of per-K-tile scales (2 KB)
   static constexpr int RM = NT == 3 ? 2 : 1;           // m-tiles per epilogue round
   static constexpr int ELD = 16 * NT + 8;              // bf16 row stride of the epilogue area
   static constexpr int CPL = 16 * RM * 2 * NT / 64;    // 16-B chunks per lane per round
-  static constexpr int NSTORE = (8 / RM) * CPL;        // global stores per wave per tile
+  // global stores per wave per tile (KNN: 8 m-tiles x (4 unit-max + 1 block-max) stores)
+  static constexpr int NSTORE = KNN ? 40 : (8 / RM) * CPL;
   static constexpr size_t BUF_B = (size_t)(256 + TBN) * 64 * 2 + SC * 2;
   static constexpr size_t EPI_B = 8ull * 16 * RM * ELD * 2;
   static constexpr size_t LDS_B = 2 * BUF_B + EPI_B + 2 * TBN * 4;
@@ -518,7 +519,13 @@ struct P8 {
 // operand — e4m3 bytes [M][N] (Y reinterpreted) + E8M0 scales in the layout-0 image (YS) — instead of
 // bf16: each lane takes 16 values of one staged bf16 row, the 32-block max is one lane swap, so the
 // result is bit-identical to mmr_quantize_mxfp8 of the bf16 output (same per-round store count).
-template <int NT, int ACT, bool HAS_BIAS, bool HAS_RES, bool FP8 = false, bool OUT8 = false>
+// KNN (NT = 4, no bias / residual / act): the fp16 cosine scan of knn.hip (mmr::knn_scan_p8) — X =
+// the <= 256 fp16 unit queries [256][K], W = the fp16 unit gallery rows [tiles_n * 256][K], fp16 MFMA
+// (v_mfma_f32_16x16x32_f16: exact products, f32 accumulate).  The C^T layout gives a lane 4
+// CONSECUTIVE gallery rows of one query, so the epilogue stores their max — the 4-row unit maxima of
+// knn_select_t<2> — GM[q][unit] (ldG) and each wave column's 64-row block max BM[q][block] (ldB),
+// rows >= nval as -inf, instead of the tile.
+template <int NT, int ACT, bool HAS_BIAS, bool HAS_RES, bool FP8 = false, bool OUT8 = false, bool KNN = false>
 __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restrict__ X,
                                                        const uint16_t* __restrict__ W,
                                                        const float* __restrict__ bias,
@@ -527,10 +534,13 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
                                                        int K, int tiles_m, int tiles_n,
                                                        const uint8_t* __restrict__ XS = nullptr,
                                                        const uint8_t* __restrict__ WS = nullptr,
-                                                       uint8_t* __restrict__ YS = nullptr) {
+                                                       uint8_t* __restrict__ YS = nullptr,
+                                                       float* __restrict__ GM = nullptr, float* __restrict__ BM = nullptr,
+                                                       int64_t ldG = 0, int64_t ldB = 0, int64_t nval = 0) {
   static_assert(!OUT8 || (FP8 && NT == 4 && !HAS_RES), "OUT8: MX-fp8 256x256 tiles without residual");
+  static_assert(!KNN || (NT == 4 && !FP8 && !HAS_BIAS && !HAS_RES && ACT == 0), "KNN: plain 256x256 fp16 tiles");
 #if defined(__HIP_DEVICE_COMPILE__)  // buffer-descriptor builtins exist in the device pass only
-  using C = P8<NT, FP8>;
+  using C = P8<NT, FP8, KNN>;
   constexpr int KB = 64, TBN = C::TBN;                  // KB: 128-byte LDS rows (64 bf16 / 128 fp8)
   constexpr int TA = 256 * KB, TB = TBN * KB, BUF = TA + TB + C::SC;  // uint16 elements per K-tile buffer
   // LDS image: [A_E | A_O | B_E | B_O | S_E | S_O] — the two buffers of an operand 32 KB apart, so one
@@ -649,6 +659,13 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+  };
+  typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+  auto mfma16 = [](bf16x8 a, bf16x8 b, f32x4 c) {
+    if constexpr (KNN)
+      return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, a), __builtin_bit_cast(h8_t, b), c, 0, 0, 0);
+    else
+      return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
   };
 
   // prologue: K-tile 0 -> E, K-tile 1 -> O of the first tile
@@ -772,7 +789,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
               if (ks == 0 && i == 1) issue(2 * p + 1);
 #pragma unroll
               for (int j = 0; j < NH0; ++j)
-                acc[mb + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][ks], fa[i][ks], acc[mb + i][j], 0, 0, 0);
+                acc[mb + i][j] = mfma16(fb0[j][ks], fa[i][ks], acc[mb + i][j]);
             }
         } else {
 #pragma unroll
@@ -782,7 +799,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
               if (ks == 0 && i == 1) issue(2 * p + 1);
 #pragma unroll
               for (int j = 0; j < NT - NH0; ++j)
-                acc[mb + i][NH0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][ks], fa[i][ks], acc[mb + i][NH0 + j], 0, 0, 0);
+                acc[mb + i][NH0 + j] = mfma16(fb1[j][ks], fa[i][ks], acc[mb + i][NH0 + j]);
             }
         }
         // FP8: the cluster's results are pinned before the barrier — machine sinking otherwise moves
@@ -808,6 +825,33 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
     int le = lane;
     asm volatile("" : "+v"(le));
     const int efr = le & 15, efq = le >> 4;
+    if constexpr (KNN) {
+      // lane: query m0 + wr 128 + 16 i + efr; gallery rows n0 + wc 64 + 16 j + 4 efq .. +3 = unit
+      // (n0 + wc 64) / 4 + 4 j + efq; the wave column's 64 rows = one block.  Every store issued
+      // (NSTORE exact for the next tile's counted wait)
+      const int64_t r0 = n0 + wc * 64;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int64_t q = m0 + wr * 128 + i * 16 + efr;
+        float bmx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int64_t rj = r0 + 16 * j + 4 * efq;
+          float mx = -INFINITY;
+#pragma unroll
+          for (int rg = 0; rg < 4; ++rg) mx = fmaxf(mx, rj + rg < nval ? acc[i][j][rg] : -INFINITY);
+          GM[q * ldG + r0 / 4 + 4 * j + efq] = mx;
+          bmx = fmaxf(bmx, mx);
+        }
+        bmx = fmaxf(bmx, __shfl_xor(bmx, 16, 64));
+        bmx = fmaxf(bmx, __shfl_xor(bmx, 32, 64));
+        if (efq == 0) BM[q * ldB + r0 / 64] = bmx;
+      }
+      if (!has_next) break;
+      t = tnext;
+      first = false;
+      continue;
+    }
     f32x4 bq[NT];
 #pragma unroll
     for (int j = 0; j < NT; ++j)
@@ -1468,3 +1512,18 @@ extern "C" mmr_status mmr_linear_mxfp8_q8(const uint8_t* xq, const uint8_t* xs, 
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }
+
+namespace mmr {
+// The fp16 kNN scan on the persistent 8-phase GEMM (gemm_bf16_tn_p8<KNN>): qh [256][K] fp16 unit
+// queries (zero rows past the pass), gh [tiles_n * 256][K] fp16 unit gallery rows (zero rows past
+// nval); writes unit maxima gm [256][ldG] (ldG >= tiles_n * 64) and block maxima bm [256][ldB].
+// K % 128 == 0 (the caller checks).
+hipError_t knn_scan_p8(const uint16_t* qh, const uint16_t* gh, int K, int tiles_n, int64_t nval, float* gm,
+                       int64_t ldG, float* bm, int64_t ldB, hipStream_t st) {
+  const int grid = std::max(8, std::min(cu_count(), tiles_n) / 8 * 8);
+  gemm_bf16_tn_p8<4, 0, false, false, false, false, true><<<dim3(grid), dim3(512), P8<4>::LDS_B, st>>>(
+      qh, gh, nullptr, nullptr, nullptr, 256, tiles_n * 256, K, 1, tiles_n, nullptr, nullptr, nullptr, gm, bm, ldG,
+      ldB, nval);
+  return hipGetLastError();
+}
+}  // namespace mmr

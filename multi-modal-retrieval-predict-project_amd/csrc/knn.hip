@@ -42,6 +42,11 @@
 
 #include "common.h"
 
+namespace mmr {
+hipError_t knn_scan_p8(const uint16_t* qh, const uint16_t* gh, int K, int tiles_n, int64_t nval, float* gm,
+                       int64_t ldG, float* bm, int64_t ldB, hipStream_t st);  // gemm.hip
+}
+
 namespace {
 
 using mmr::ceil_div;
@@ -113,13 +118,14 @@ __global__ __launch_bounds__(256) void knn_prep_queries(const float* __restrict_
   int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   int lane = threadIdx.x & 63;
   if (row >= Qp) return;
-  // tiled: 0 row-major f32, 1 tile16 f32, 2 tile32h fp16 (qn reinterpreted as halfs)
+  // tiled: 0 row-major f32, 1 tile16 f32, 2 tile32h fp16, 3 row-major fp16 (qn reinterpreted as halfs;
+  // 3 needs Dp <= 1024)
   auto put = [&](int k, float v) {
     if (tiled == 2) ((_Float16*)qn)[tile32h_index(row, k, Dp)] = (_Float16)v;
     else if (tiled == 1) qn[tile16_index(row, k, Dp)] = v;
     else qn[row * Dp + k] = v;
   };
-  if (tiled == 2 && Dp <= 1024) {
+  if ((tiled == 2 || tiled == 3) && Dp <= 1024) {
     // fp16 tile32h: lane owns the 8-half groups g = lane + 64j (j < 2) of the row — 16-B stores
     // (one (row, 8-half) run is contiguous in tile32h) instead of 2-B scatters; loads unconditional
     typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -145,7 +151,7 @@ __global__ __launch_bounds__(256) void knn_prep_queries(const float* __restrict_
       h8 o;
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = (_Float16)(v[j][e] * inv);
-      *(h8*)((_Float16*)qn + tile32h_index(row, k0, Dp)) = o;
+      *(h8*)((_Float16*)qn + (tiled == 2 ? tile32h_index(row, k0, Dp) : row * (int64_t)Dp + k0)) = o;
     }
     if (lane == 0) qnorm64[row] = row < nq ? nrm : 0.0;
     return;
@@ -328,6 +334,24 @@ __global__ __launch_bounds__(256) void knn_tile_gallery_f16(const float* __restr
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] = (_Float16)(src[e] * ig);
   ((h8*)gh)[i] = v;
+}
+
+// row-major fp16 unit rows [total8 / (Dp/8)][Dp] (rows >= Np zero): the p8 scan's gallery operand
+__global__ __launch_bounds__(256) void knn_rows_f16(const float* __restrict__ gal, const float* __restrict__ inv_g,
+                                                    int64_t Np, int Dp, int64_t total8, uint16_t* __restrict__ ghr) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // 16-B unit index in ghr
+  if (i >= total8) return;
+  const int64_t row = i / (Dp >> 3);
+  const int c8 = (int)(i % (Dp >> 3));
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  h8 v = (h8){0, 0, 0, 0, 0, 0, 0, 0};
+  if (row < Np) {
+    const float ig = inv_g[row];
+    const float* src = gal + row * Dp + c8 * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (_Float16)(src[e] * ig);
+  }
+  ((h8*)ghr)[i] = v;
 }
 
 __device__ __forceinline__ int xswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
@@ -1856,6 +1880,8 @@ struct mmr_index {
   uint16_t* gs = nullptr;     // [Np][2Dp] bf16 hi/lo split (mode x3)
   float* gt = nullptr;        // [Np][Dp] f32 in the tile16 layout (skinny scan)
   uint16_t* gh = nullptr;     // [Np][Dp] fp16 unit rows in the tile32h layout (mode f16; built on first use)
+  uint16_t* ghr = nullptr;    // [Np256][Dp] fp16 unit rows, row-major, zero rows past n (mode f16, p8 scan)
+  int64_t Np256 = 0;          // rows of ghr (a multiple of 256)
   int mode = 1;               // 0: f32 MFMA scores, 1: bf16x3 split scores, 2: fp16 unit-row scan
   // Workspace: one set per index, sized by what the mode needs (grown on demand).  `mu` serialises
   // the enqueue of searches; across streams the workspace follows the stream: a search on another
@@ -1930,8 +1956,9 @@ mmr_status ensure_ws(mmr_index* ix, int64_t nq) {
     qs = cq;
   } else {
     rows = 256;
-    vals = 256 * (ix->Np / 4);
-    bvals = 256 * (ix->Np / 64);
+    const int64_t nr = ix->Np256 > ix->Np ? ix->Np256 : ix->Np;  // the p8 scan writes whole 256-row tiles
+    vals = 256 * (nr / 4);
+    bvals = 256 * (nr / 64);
   }
   int64_t hq = ix->ws_qrows, hq2 = ix->ws_qrows;
   mmr_status s = grow(ix, ix->qn, hq, rows, sizeof(float) * ix->Dp);
@@ -1978,6 +2005,12 @@ bool raw_scan_enabled() {
 // The LDS-query persistent small-Q scan (MMR_KNN_F16_LQ=0: the one-wave-per-block RAW stream, for A/B).
 bool lq_scan_enabled() {
   const char* e = getenv("MMR_KNN_F16_LQ");
+  return !(e && atoi(e) == 0);
+}
+
+// The p8 GEMM scan for 33-256-query f16 passes (MMR_KNN_P8=0: the LDS-ring tile scan, for A/B).
+bool p8_scan_enabled() {
+  const char* e = getenv("MMR_KNN_P8");
   return !(e && atoi(e) == 0);
 }
 
@@ -2115,6 +2148,7 @@ mmr_status mmr_index_destroy(mmr_index* ix) {
   if (ix->gs) (void)hipFree(ix->gs);
   if (ix->gt) (void)hipFree(ix->gt);
   if (ix->gh) (void)hipFree(ix->gh);
+  if (ix->ghr) (void)hipFree(ix->ghr);
   if (ix->qs) (void)hipFree(ix->qs);
   if (ix->qn) (void)hipFree(ix->qn);
   if (ix->qnorm64) (void)hipFree(ix->qnorm64);
@@ -2202,6 +2236,19 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
         float* gm = ix->vals;
         float* bm = ix->bvals;
         const int64_t ldG = ix->Np / 4, ldB = ix->Np / 64;
+        if (pq > 32 && ix->ghr != nullptr && p8_scan_enabled()) {
+          // 33-256 queries: the persistent 8-phase GEMM (gemm.hip) with the unit-max epilogue —
+          // one 256-query M tile x 256-row gallery tiles, row-major fp16 operands
+          knn_prep_queries<<<dim3(64), dim3(256), 0, st>>>(qp, pq, ix->d, ix->qn, ix->Dp, 256, ix->qnorm64, 3);
+          MMR_LAUNCH_CHECK();
+          const int64_t ldG8 = ix->Np256 / 4, ldB8 = ix->Np256 / 64;
+          MMR_CHECK_HIP(mmr::knn_scan_p8(qh, ix->ghr, ix->Dp, (int)(ix->Np256 / 256), ix->n, gm, ldG8, bm, ldB8, st));
+          launch_select<2, true>(st, pq, gm, ldG8, ldG8, ix, k, two_delta16, qp, ix->qnorm64, oi + p0 * k,
+                                 os ? os + p0 * k : nullptr, os64 ? os64 + p0 * k : nullptr, ost ? ost + p0 : nullptr,
+                                 bm, ldB8);
+          MMR_LAUNCH_CHECK();
+          continue;
+        }
         if (pq > 32 && f16_tile_enabled()) {
           // 33-256 queries: the LDS-staged tile scan (64 / 128 / 256-query tiles), contiguous units
           const int wq = pq <= 64 ? 1 : pq <= 128 ? 2 : 4;
@@ -2424,6 +2471,27 @@ mmr_status mmr_index_set_mode(mmr_index* ix, int32_t mode) {
       mmr::set_error("mmr_index_set_mode: fp16 copy kernel failed: %s", hipGetErrorString(e));
       return MMR_ERR_HIP;
     }
+  }
+  if (mode == 2 && ix->ghr == nullptr && ix->Dp % 128 == 0 && ix->Dp <= 1024) {
+    // row-major fp16 unit rows for the p8 scan of 33-256-query passes (whole 256-row tiles)
+    DeviceGuard g(ix->device);
+    const int64_t np256 = round_up(ix->Np, 256);
+    hipError_t e = hipMalloc(&ix->ghr, sizeof(uint16_t) * np256 * ix->Dp);
+    if (e != hipSuccess) {
+      ix->ghr = nullptr;
+      mmr::set_error("mmr_index_set_mode: hipMalloc(fp16 row copy) failed: %s", hipGetErrorString(e));
+      return MMR_ERR_OOM;
+    }
+    const int64_t total8 = np256 * ix->Dp / 8;
+    knn_rows_f16<<<dim3((unsigned)ceil_div(total8, 256)), dim3(256)>>>(ix->gal, ix->inv_norm, ix->Np, ix->Dp,
+                                                                     total8, ix->ghr);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+      mmr::set_error("mmr_index_set_mode: fp16 row copy kernel failed: %s", hipGetErrorString(e));
+      return MMR_ERR_HIP;
+    }
+    ix->Np256 = np256;
   }
   ix->mode = mode;
   return MMR_OK;
