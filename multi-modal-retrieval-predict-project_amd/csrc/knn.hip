@@ -1558,19 +1558,47 @@ __global__ __launch_bounds__(T) void knn_select_t(
     SEL_MARK(9)
     return nslot;
   };
-  // (F) rank the carried rows [0, carry) with the re-scored slots [kMaxK, +nslot): the m^2 (slot,
-  // other) comparisons spread over all threads, ranks counted in LDS; `direct` writes the first kk
-  // to the outputs, else they become the new carried top-K in [0, kk)
+  // (F) rank the carried rows [0, carry) with the re-scored slots [kMaxK, +nslot): a thread per slot
+  // counts the slots ahead of it (score desc, row asc) in a register, every thread reading the same
+  // other slot at each step (LDS broadcast); `direct` writes the first kk to the outputs, else they
+  // become the new carried top-K in [0, kk).  (A first version spread the m^2 pairs over all threads
+  // with an LDS atomic per pair: consecutive threads hit the same counter, 45 us at m = 272 —
+  // K = 50 over 1M rows; a one-read-per-step loop then paid the LDS latency per step, 21 us.)
   auto rank = [&](int carry, int nslot, bool direct) -> int {
     const int mtot = carry + nslot;
     auto slot = [&](int u) { return u < carry ? u : kMaxK + u - carry; };
-    for (int u = tid; u < mtot; u += T) L.rank_s[slot(u)] = 0;
-    __syncthreads();
-    const int npair = mtot * mtot;
-    for (int p = tid; p < npair; p += T) {
-      const int a = slot(p / mtot), b = slot(p % mtot);
-      const double sa = L.cand_d[a], sb = L.cand_d[b];
-      if ((sb > sa) || (sb == sa && L.row_s[b] < L.row_s[a])) atomicAdd(&L.rank_s[a], 1);
+    // G threads per slot (a power of two, G * mtot <= T, G <= 64: one wave's lanes), each counting a
+    // contiguous share of the others, summed by lane swaps
+    int G = 1;
+    while (G < 64 && 2 * G * mtot <= T) G *= 2;
+    const int per = (mtot + G - 1) / G;
+    const int rounds = (mtot * G + T - 1) / T;  // block-uniform
+    for (int rd = 0; rd < rounds; ++rd) {
+      const int w = rd * T + tid, u = w / G, g = w % G;
+      const int a = slot(u < mtot ? u : 0);
+      const double sa = L.cand_d[a];
+      const int ra = L.row_s[a];
+      const int v0 = g * per, v1 = v0 + per < mtot ? v0 + per : mtot;
+      int rk = 0, v = v0;
+      for (; v + 8 <= v1; v += 8) {  // 8 independent LDS reads in flight per step
+        double sb[8];
+        int rb[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int b = slot(v + e);
+          sb[e] = L.cand_d[b];
+          rb[e] = L.row_s[b];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) rk += (sb[e] > sa) || (sb[e] == sa && rb[e] < ra);
+      }
+      for (; v < v1; ++v) {
+        const int b = slot(v);
+        const double sb = L.cand_d[b];
+        rk += (sb > sa) || (sb == sa && L.row_s[b] < ra);
+      }
+      for (int o = 1; o < G; o <<= 1) rk += __shfl_xor(rk, o, 64);
+      if (u < mtot && g == 0) L.rank_s[a] = rk;
     }
     __syncthreads();
     for (int u = tid; u < mtot; u += T) {
@@ -1608,21 +1636,50 @@ __global__ __launch_bounds__(T) void knn_select_t(
       const int64_t i = tid + (int64_t)it * T;
       if (i < nblk && bc[it] >= thr && bc[it] > -INFINITY) {
         const uint32_t p = atomicAdd(&L.bcast[3], 1u);
-        if (p < (uint32_t)kBlkCap) L.cand_b[p] = (int)i;
+        if (p < (uint32_t)kBlkCap) {
+          L.cand_b[p] = (int)i;
+          L.ukey[p] = f2key(bc[it]);
+        }
       }
     }
     for (int64_t i = tid + (int64_t)kRegB * T; i < nblk; i += T) {
       const float v = brow[i];
       if (v >= thr && v > -INFINITY) {
         const uint32_t p = atomicAdd(&L.bcast[3], 1u);
-        if (p < (uint32_t)kBlkCap) L.cand_b[p] = (int)i;
+        if (p < (uint32_t)kBlkCap) {
+          L.cand_b[p] = (int)i;
+          L.ukey[p] = f2key(v);
+        }
       }
     }
     __syncthreads();
-    const int nb = (int)L.bcast[3];
+    int nb = (int)L.bcast[3];
     SEL_VAL(10, nb)
     __syncthreads();
     if (tid == 0) L.bcast[3] = 0;
+    if (nb <= kBlkCap && nb > 2 * kk + 32) {
+      // block-level tightening (large K: the first bound comes from thread maxima, each over ~nblk/T
+      // blocks, and admits many blocks — K = 50 over 1M rows: ~100 blocks, ~1700 units, past the unit
+      // buffer, which sent every query through the all-units path): the exact kth largest of the
+      // collected blocks' maxima is again a distinct-row bound (>= thr), and only blocks clearing
+      // it - 2 delta keep their units
+      const float t2 = key2f(block_select_kth(L.ukey, nb, kk, L.hist, L.bcast, 4));
+      const float thr2 = lower_threshold(t2, tdel);
+      if (thr2 > thr) {
+        const uint32_t k2 = f2key(thr2);
+        __syncthreads();
+        for (int p = tid; p < nb; p += T)  // compacted into cand_u (nb <= kBlkCap <= kCandCap), then back
+          if (L.ukey[p] >= k2) L.cand_u[atomicAdd(&L.bcast[3], 1u)] = L.cand_b[p];
+        __syncthreads();
+        const int nb2 = (int)L.bcast[3];
+        for (int p = tid; p < nb2; p += T) L.cand_b[p] = L.cand_u[p];
+        __syncthreads();
+        if (tid == 0) L.bcast[3] = 0;
+        nb = nb2;
+        thr = thr2;
+        __syncthreads();
+      }
+    }
     if (nb > kBlkCap) {
       coarse_ok = false;
       cnt = collect(thr, false, 0, nunits);

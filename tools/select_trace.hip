@@ -2,7 +2,7 @@
 // standalone binary, runs searches over a 100k x 768 Gaussian gallery and prints per-phase times.
 // build: hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -I include tools/select_trace.hip \
 //          multi-modal-retrieval-predict-project_amd/csrc/capi.cpp -o tools/select_trace.bin
-// run:   tools/select_trace.bin [Q] [mode]
+// run:   tools/select_trace.bin [Q] [mode] [n] [K] [d]
 #define MMR_SELECT_TRACE
 #include "../multi-modal-retrieval-predict-project_amd/csrc/knn.hip"
 
@@ -11,7 +11,7 @@
 int main(int argc, char** argv) {
   const int Q = argc > 1 ? atoi(argv[1]) : 16, mode = argc > 2 ? atoi(argv[2]) : 2;
   const int64_t n = argc > 3 ? atoll(argv[3]) : 100000;
-  const int d = 768, K = 10;
+  const int K = argc > 4 ? atoi(argv[4]) : 10, d = argc > 5 ? atoi(argv[5]) : 768;
   std::vector<float> g((size_t)n * d), q((size_t)Q * d);
   std::mt19937 rng(7);
   std::normal_distribution<float> nd;
