@@ -105,6 +105,19 @@ __device__ __forceinline__ float gelu_t(float v) {
   else return mmr::gelu_erf(v);
 }
 
+// bias + GELU of two hidden values -> packed bf16 pair; FAST on packed f32 math (v_pk_add / v_pk_fma
+// / v_pk_mul: half the VALU issues — the kernel is VALU-bound on GELU), bitwise equal to the scalar
+// gelu_fast (same operations in the same order)
+template <bool FAST>
+__device__ __forceinline__ uint32_t gelu_pack(float a0, float a1, float b0, float b1) {
+  if constexpr (FAST) {
+    const mmr::f32x2_t u = mmr::gelu_fast2((mmr::f32x2_t){a0, a1} + (mmr::f32x2_t){b0, b1});
+    return mmr::pack2bf(u.x, u.y);
+  } else {
+    return mmr::pack2bf(gelu_t<FAST>(a0 + b0), gelu_t<FAST>(a1 + b1));
+  }
+}
+
 template <int C, int NW, int HC, int R, bool FAST>
 __global__ __launch_bounds__(64 * NW) void swin_mlp(const uint16_t* __restrict__ x,
                                                          const float* __restrict__ lng,
@@ -216,8 +229,8 @@ __global__ __launch_bounds__(64 * NW) void swin_mlp(const uint16_t* __restrict__
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const f32x4 bb = *(const f32x4*)(Pb1 + HC * ch + 32 * t + 8 * i + 4 * h);
-        hp[2 * i] = mmr::pack2bf(gelu_t<FAST>(a1[4 * i] + bb[0]), gelu_t<FAST>(a1[4 * i + 1] + bb[1]));
-        hp[2 * i + 1] = mmr::pack2bf(gelu_t<FAST>(a1[4 * i + 2] + bb[2]), gelu_t<FAST>(a1[4 * i + 3] + bb[3]));
+        hp[2 * i] = gelu_pack<FAST>(a1[4 * i], a1[4 * i + 1], bb[0], bb[1]);
+        hp[2 * i + 1] = gelu_pack<FAST>(a1[4 * i + 2], a1[4 * i + 3], bb[2], bb[3]);
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {  // k-step over hidden 32t + 16 s2 .. +15
@@ -388,8 +401,8 @@ __global__ __launch_bounds__(64 * NW) void swin_mlp_res(const uint16_t* __restri
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const f32x4 bb = *(const f32x4*)(Pb1 + 32 * t + 8 * i + 4 * h);
-        hp[2 * i] = mmr::pack2bf(gelu_t<FAST>(a1[4 * i] + bb[0]), gelu_t<FAST>(a1[4 * i + 1] + bb[1]));
-        hp[2 * i + 1] = mmr::pack2bf(gelu_t<FAST>(a1[4 * i + 2] + bb[2]), gelu_t<FAST>(a1[4 * i + 3] + bb[3]));
+        hp[2 * i] = gelu_pack<FAST>(a1[4 * i], a1[4 * i + 1], bb[0], bb[1]);
+        hp[2 * i + 1] = gelu_pack<FAST>(a1[4 * i + 2], a1[4 * i + 3], bb[2], bb[3]);
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
