@@ -367,3 +367,21 @@ def test_knn_f16_coarse_select_clusters(Q, K):
     Qm[1] = G[7]
     Qm[2] = -c
     _exact_check(G, Qm, K, mode="f16")
+
+
+@pytest.mark.parametrize("Q", [3, 64])
+@pytest.mark.parametrize("K", [10, 50])
+def test_knn_f16_scattered_cluster_block_tightening(Q, K):
+    """A cluster scattered over many 64-row blocks: more than 2K + 32 blocks clear the first
+    (thread-max) bound, so the selection tightens it with the exact K-th largest of the collected
+    blocks' maxima before reading their unit maxima (knn_select_t COARSE); lists stay exact."""
+    rng = np.random.default_rng(7000 + Q * 10 + K)
+    N, D = 60_000, 256
+    G = rng.standard_normal((N, D), dtype=np.float32)
+    c = rng.standard_normal(D).astype(np.float32)
+    rows = rng.choice(N // 64, size=800, replace=False) * 64 + rng.integers(0, 64, size=800)
+    G[rows] = c + 0.08 * rng.standard_normal((800, D), dtype=np.float32)
+    Qm = rng.standard_normal((Q, D), dtype=np.float32)
+    Qm[0] = c
+    Qm[1] = c + 0.01 * rng.standard_normal(D).astype(np.float32)
+    _exact_check(G, Qm, K, mode="f16")
