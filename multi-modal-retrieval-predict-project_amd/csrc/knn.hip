@@ -2065,7 +2065,7 @@ bool lq_scan_enabled() {
   return !(e && atoi(e) == 0);
 }
 
-// The p8 GEMM scan for 33-256-query f16 passes (MMR_KNN_P8=0: the LDS-ring tile scan, for A/B).
+// The p8 GEMM scan for 129-256-query f16 passes (MMR_KNN_P8=0: the LDS-ring tile scan, for A/B).
 bool p8_scan_enabled() {
   const char* e = getenv("MMR_KNN_P8");
   return !(e && atoi(e) == 0);
@@ -2293,9 +2293,11 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
         float* gm = ix->vals;
         float* bm = ix->bvals;
         const int64_t ldG = ix->Np / 4, ldB = ix->Np / 64;
-        if (pq > 32 && ix->ghr != nullptr && p8_scan_enabled()) {
-          // 33-256 queries: the persistent 8-phase GEMM (gemm.hip) with the unit-max epilogue —
-          // one 256-query M tile x 256-row gallery tiles, row-major fp16 operands
+        if (pq > 128 && ix->ghr != nullptr && p8_scan_enabled()) {
+          // 129-256 queries: the persistent 8-phase GEMM (gemm.hip) with the unit-max epilogue —
+          // one 256-query M tile x 256-row gallery tiles, row-major fp16 operands.  (It computes
+          // all 256 query rows; at 100k x 768 it beats the LDS-ring tile scan from Q ~ 160:
+          // Q = 64 / 128 / 192 / 256: 81 / 83 / 86 / 88 us vs 62 / 69 / 96 / 100.)
           knn_prep_queries<<<dim3(64), dim3(256), 0, st>>>(qp, pq, ix->d, ix->qn, ix->Dp, 256, ix->qnorm64, 3);
           MMR_LAUNCH_CHECK();
           const int64_t ldG8 = ix->Np256 / 4, ldB8 = ix->Np256 / 64;
