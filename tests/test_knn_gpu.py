@@ -385,3 +385,14 @@ def test_knn_f16_scattered_cluster_block_tightening(Q, K):
     Qm[0] = c
     Qm[1] = c + 0.01 * rng.standard_normal(D).astype(np.float32)
     _exact_check(G, Qm, K, mode="f16")
+
+
+@pytest.mark.parametrize("N", [1, 100, 255, 256, 257, 513])
+@pytest.mark.parametrize("Q", [129, 256])
+def test_knn_f16_p8_small_galleries(N, Q):
+    """129-256-query f16 passes on the 8-phase GEMM scan with fewer gallery tiles than workgroups
+    (one 256-row tile, or a few: most XCD slots idle) and padded rows inside the last tile."""
+    rng = np.random.default_rng(N * 7 + Q)
+    G = rng.standard_normal((N, 128), dtype=np.float32)
+    Qm = rng.standard_normal((Q, 128), dtype=np.float32)
+    _exact_check(G, Qm, 10, mode="f16")
