@@ -522,8 +522,9 @@ struct P8 {
 // KNN (NT = 4, no bias / residual / act): the fp16 cosine scan of knn.hip (mmr::knn_scan_p8) — X =
 // the <= 256 fp16 unit queries [256][K], W = the fp16 unit gallery rows [tiles_n * 256][K], fp16 MFMA
 // (v_mfma_f32_16x16x32_f16: exact products, f32 accumulate).  The C^T layout gives a lane 4
-// CONSECUTIVE gallery rows of one query, so the epilogue stores their max — the 4-row unit maxima of
-// knn_select_t<2> — GM[q][unit] (ldG) and each wave column's 64-row block max BM[q][block] (ldB),
+// CONSECUTIVE gallery rows of one query, so the epilogue stores the maxima of its two row pairs —
+// the 2-row unit maxima of knn_select_t<3> — GM[q][unit] (ldG) and each wave column's 64-row block
+// max BM[q][block] (ldB),
 // rows >= nval as -inf, instead of the tile.
 template <int NT, int ACT, bool HAS_BIAS, bool HAS_RES, bool FP8 = false, bool OUT8 = false, bool KNN = false>
 __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restrict__ X,
@@ -826,9 +827,9 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
     asm volatile("" : "+v"(le));
     const int efr = le & 15, efq = le >> 4;
     if constexpr (KNN) {
-      // lane: query m0 + wr 128 + 16 i + efr; gallery rows n0 + wc 64 + 16 j + 4 efq .. +3 = unit
-      // (n0 + wc 64) / 4 + 4 j + efq; the wave column's 64 rows = one block.  Every store issued
-      // (NSTORE exact for the next tile's counted wait)
+      // lane: query m0 + wr 128 + 16 i + efr; gallery rows rj .. rj + 3 (rj = n0 + wc 64 + 16 j +
+      // 4 efq) = the 2-row units rj / 2 and rj / 2 + 1 (one 8-B store); the wave column's 64 rows =
+      // one block.  Every store issued (NSTORE exact for the next tile's counted wait)
       const int64_t r0 = n0 + wc * 64;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -837,11 +838,12 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int64_t rj = r0 + 16 * j + 4 * efq;
-          float mx = -INFINITY;
+          float a[4];
 #pragma unroll
-          for (int rg = 0; rg < 4; ++rg) mx = fmaxf(mx, rj + rg < nval ? acc[i][j][rg] : -INFINITY);
-          GM[q * ldG + r0 / 4 + 4 * j + efq] = mx;
-          bmx = fmaxf(bmx, mx);
+          for (int rg = 0; rg < 4; ++rg) a[rg] = rj + rg < nval ? acc[i][j][rg] : -INFINITY;
+          const float2 u2 = make_float2(fmaxf(a[0], a[1]), fmaxf(a[2], a[3]));
+          *(float2*)(GM + q * ldG + rj / 2) = u2;
+          bmx = fmaxf(bmx, fmaxf(u2.x, u2.y));
         }
         bmx = fmaxf(bmx, __shfl_xor(bmx, 16, 64));
         bmx = fmaxf(bmx, __shfl_xor(bmx, 32, 64));
@@ -1516,7 +1518,7 @@ extern "C" mmr_status mmr_linear_mxfp8_q8(const uint8_t* xq, const uint8_t* xs, 
 namespace mmr {
 // The fp16 kNN scan on the persistent 8-phase GEMM (gemm_bf16_tn_p8<KNN>): qh [256][K] fp16 unit
 // queries (zero rows past the pass), gh [tiles_n * 256][K] fp16 unit gallery rows (zero rows past
-// nval); writes unit maxima gm [256][ldG] (ldG >= tiles_n * 64) and block maxima bm [256][ldB].
+// nval); writes 2-row unit maxima gm [256][ldG] (ldG >= tiles_n * 128) and block maxima bm [256][ldB].
 // K % 128 == 0 (the caller checks).
 hipError_t knn_scan_p8(const uint16_t* qh, const uint16_t* gh, int K, int tiles_n, int64_t nval, float* gm,
                        int64_t ldG, float* bm, int64_t ldB, hipStream_t st) {

@@ -1147,7 +1147,8 @@ __device__ __forceinline__ float lower_threshold(float t, float two_delta) {
 // Units (what one value covers): MODE 0 = one gallery row (f32-mode score matrix, knn_scores);
 // MODE 1 = a strided 4-row group {(u>>4)*64 + (u&15) + 16m : m < 4} (the gmax of knn_scores_x3_gmax /
 // knn_scan_f32_gmax / knn_scan_f16_gmax: one lane's 4 rows of a 64-row block); MODE 2 = 4 consecutive
-// rows {4u + m} (knn_scan_f16_tile).  A unit's value is >= the approximate score of each of its rows.
+// rows {4u + m} (knn_scan_f16_tile); MODE 3 = 2 consecutive rows {2u + m} (the 8-phase GEMM scan,
+// gemm_bf16_tn_p8<KNN>: half the rows to re-score per candidate unit).  A unit's value is >= the approximate score of each of its rows.
 // (A) per-thread max over a strided slice; (B) b = a lower bound of the K-th largest unit value (each
 // unit value is a distinct row's score, so b <= t, the K-th largest approximate row score); (C)
 // collect every unit with value >= b - 2 delta: a true top-K row j has s(j) >= t - 2 delta >= b - 2
@@ -1174,6 +1175,7 @@ template <int MODE>
 __device__ __forceinline__ int64_t unit_row(int64_t u, int m) {
   if (MODE == 0) return u;
   if (MODE == 1) return (u >> 4) * 64 + (u & 15) + 16 * m;
+  if (MODE == 3) return 2 * u + m;
   return 4 * u + m;
 }
 
@@ -1300,7 +1302,7 @@ __device__ uint32_t block_kth_lower_top4(uint32_t key, int kth, uint32_t* vals, 
   return r;
 }
 
-// COARSE (MODE 1 / 2, 16 units = one 64-row block): the scan also wrote per-(query, block) maxima
+// COARSE (MODE 1 / 2: 16 units = one 64-row block; MODE 3: 32): the scan also wrote per-(query, block) maxima
 // bvals; (A)-(C) run on those first — the K-th largest thread max over block maxima is a lower bound
 // b of t (each block max is a distinct row's score), and only blocks whose max clears b - 2 delta have
 // their 16 unit maxima read; when more units than 2K + 32 qualify, the K-th largest of THEIR values
@@ -1317,7 +1319,8 @@ __global__ __launch_bounds__(T) void knn_select_t(
     const float* __restrict__ gal, int Dp, const double* __restrict__ gnorm64, int64_t idx_base,
     int64_t* __restrict__ out_idx, float* __restrict__ out_score, double* __restrict__ out_score64,
     int32_t* __restrict__ status) {
-  constexpr int GS = MODE == 0 ? 1 : 4;      // rows per unit
+  constexpr int GS = MODE == 0 ? 1 : MODE == 3 ? 2 : 4;  // rows per unit
+  constexpr int UPB = 64 / GS;               // units per 64-row block (COARSE)
   constexpr int UC = kCandCap / GS;          // units per batch
   __shared__ __attribute__((aligned(16))) SelLds<T> L;
 
@@ -1354,7 +1357,7 @@ __global__ __launch_bounds__(T) void knn_select_t(
   float m = -INFINITY;
   // COARSE: the block maxima (nunits / 16 per query; the first kRegB per thread kept for (C))
   constexpr int kRegB = 4;
-  const int64_t nblk = nunits >> 4;
+  const int64_t nblk = nunits / UPB;
   const float* brow = COARSE ? bvals + qi * ldB : nullptr;
   float bc[kRegB];
   if constexpr (COARSE) {
@@ -1685,11 +1688,11 @@ __global__ __launch_bounds__(T) void knn_select_t(
       cnt = collect(thr, false, 0, nunits);
     } else {
       // one unit per thread-slot: all loads of a pass issued together
-      for (int s0 = 0; s0 < nb * 16; s0 += T) {
+      for (int s0 = 0; s0 < nb * UPB; s0 += T) {
         const int s = s0 + tid;
-        const int64_t u = (int64_t)L.cand_b[(s < nb * 16 ? s : 0) >> 4] * 16 + (s & 15);
+        const int64_t u = (int64_t)L.cand_b[(s < nb * UPB ? s : 0) / UPB] * UPB + (s % UPB);
         const float v = row[u];
-        if (s < nb * 16) take(u, v, thr);
+        if (s < nb * UPB) take(u, v, thr);
       }
       __syncthreads();
       cnt = (int)L.bcast[2];
@@ -2014,7 +2017,7 @@ mmr_status ensure_ws(mmr_index* ix, int64_t nq) {
   } else {
     rows = 256;
     const int64_t nr = ix->Np256 > ix->Np ? ix->Np256 : ix->Np;  // the p8 scan writes whole 256-row tiles
-    vals = 256 * (nr / 4);
+    vals = 256 * (ix->Np256 > 0 ? nr / 2 : nr / 4);  // p8: 2-row unit maxima
     bvals = 256 * (nr / 64);
   }
   int64_t hq = ix->ws_qrows, hq2 = ix->ws_qrows;
@@ -2300,9 +2303,9 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
           // Q = 64 / 128 / 192 / 256: 81 / 83 / 86 / 88 us vs 62 / 69 / 96 / 100.)
           knn_prep_queries<<<dim3(64), dim3(256), 0, st>>>(qp, pq, ix->d, ix->qn, ix->Dp, 256, ix->qnorm64, 3);
           MMR_LAUNCH_CHECK();
-          const int64_t ldG8 = ix->Np256 / 4, ldB8 = ix->Np256 / 64;
+          const int64_t ldG8 = ix->Np256 / 2, ldB8 = ix->Np256 / 64;  // 2-row units
           MMR_CHECK_HIP(mmr::knn_scan_p8(qh, ix->ghr, ix->Dp, (int)(ix->Np256 / 256), ix->n, gm, ldG8, bm, ldB8, st));
-          launch_select<2, true>(st, pq, gm, ldG8, ldG8, ix, k, two_delta16, qp, ix->qnorm64, oi + p0 * k,
+          launch_select<3, true>(st, pq, gm, ldG8, ldG8, ix, k, two_delta16, qp, ix->qnorm64, oi + p0 * k,
                                  os ? os + p0 * k : nullptr, os64 ? os64 + p0 * k : nullptr, ost ? ost + p0 : nullptr,
                                  bm, ldB8);
           MMR_LAUNCH_CHECK();
