@@ -493,7 +493,7 @@ __device__ __forceinline__ f32x4 mx_mfma(i32x8 a, i32x8 b, f32x4 c, uint32_t sa,
   return c;
 }
 
-template <int NT, bool FP8 = false, bool KNN = false>
+template <int NT, bool FP8 = false, int KNN = 0>
 struct P8 {
   static constexpr int TBN = 64 * NT;
   static constexpr int SC = FP8 ? 1024 : 0;            // uint16 elements of per-K-tile scales (2 KB)
@@ -522,11 +522,11 @@ struct P8 {
 // KNN (NT = 4, no bias / residual / act): the fp16 cosine scan of knn.hip (mmr::knn_scan_p8) — X =
 // the <= 256 fp16 unit queries [256][K], W = the fp16 unit gallery rows [tiles_n * 256][K], fp16 MFMA
 // (v_mfma_f32_16x16x32_f16: exact products, f32 accumulate).  The C^T layout gives a lane 4
-// CONSECUTIVE gallery rows of one query, so the epilogue stores the maxima of its two row pairs —
-// the 2-row unit maxima of knn_select_t<3> — GM[q][unit] (ldG) and each wave column's 64-row block
-// max BM[q][block] (ldB),
+// CONSECUTIVE gallery rows of one query, so the epilogue stores the maxima of its two row pairs
+// (KNN = 2: knn_select_t<3>'s 2-row units, one 8-B store) or of all four (KNN = 4: knn_select_t<2>'s
+// 4-row units) — GM[q][unit] (ldG) — and each wave column's 64-row block max BM[q][block] (ldB),
 // rows >= nval as -inf, instead of the tile.
-template <int NT, int ACT, bool HAS_BIAS, bool HAS_RES, bool FP8 = false, bool OUT8 = false, bool KNN = false>
+template <int NT, int ACT, bool HAS_BIAS, bool HAS_RES, bool FP8 = false, bool OUT8 = false, int KNN = 0>
 __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restrict__ X,
                                                        const uint16_t* __restrict__ W,
                                                        const float* __restrict__ bias,
@@ -539,7 +539,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
                                                        float* __restrict__ GM = nullptr, float* __restrict__ BM = nullptr,
                                                        int64_t ldG = 0, int64_t ldB = 0, int64_t nval = 0) {
   static_assert(!OUT8 || (FP8 && NT == 4 && !HAS_RES), "OUT8: MX-fp8 256x256 tiles without residual");
-  static_assert(!KNN || (NT == 4 && !FP8 && !HAS_BIAS && !HAS_RES && ACT == 0), "KNN: plain 256x256 fp16 tiles");
+  static_assert(KNN == 0 || ((KNN == 2 || KNN == 4) && NT == 4 && !FP8 && !HAS_BIAS && !HAS_RES && ACT == 0),
+                "KNN (rows per unit 2 / 4): plain 256x256 fp16 tiles");
 #if defined(__HIP_DEVICE_COMPILE__)  // buffer-descriptor builtins exist in the device pass only
   using C = P8<NT, FP8, KNN>;
   constexpr int KB = 64, TBN = C::TBN;                  // KB: 128-byte LDS rows (64 bf16 / 128 fp8)
@@ -842,7 +843,11 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
 #pragma unroll
           for (int rg = 0; rg < 4; ++rg) a[rg] = rj + rg < nval ? acc[i][j][rg] : -INFINITY;
           const float2 u2 = make_float2(fmaxf(a[0], a[1]), fmaxf(a[2], a[3]));
-          *(float2*)(GM + q * ldG + rj / 2) = u2;
+          if constexpr (KNN == 2) {
+            *(float2*)(GM + q * ldG + rj / 2) = u2;
+          } else {
+            GM[q * ldG + rj / 4] = fmaxf(u2.x, u2.y);
+          }
           bmx = fmaxf(bmx, fmaxf(u2.x, u2.y));
         }
         bmx = fmaxf(bmx, __shfl_xor(bmx, 16, 64));
@@ -1518,14 +1523,20 @@ extern "C" mmr_status mmr_linear_mxfp8_q8(const uint8_t* xq, const uint8_t* xs, 
 namespace mmr {
 // The fp16 kNN scan on the persistent 8-phase GEMM (gemm_bf16_tn_p8<KNN>): qh [256][K] fp16 unit
 // queries (zero rows past the pass), gh [tiles_n * 256][K] fp16 unit gallery rows (zero rows past
-// nval); writes 2-row unit maxima gm [256][ldG] (ldG >= tiles_n * 128) and block maxima bm [256][ldB].
+// nval); writes unit maxima of unit_rows (2 or 4) consecutive rows gm [256][ldG] (ldG >= tiles_n *
+// 256 / unit_rows) and block maxima bm [256][ldB].
 // K % 128 == 0 (the caller checks).
 hipError_t knn_scan_p8(const uint16_t* qh, const uint16_t* gh, int K, int tiles_n, int64_t nval, float* gm,
-                       int64_t ldG, float* bm, int64_t ldB, hipStream_t st) {
+                       int64_t ldG, float* bm, int64_t ldB, int unit_rows, hipStream_t st) {
   const int grid = std::max(8, std::min(cu_count(), tiles_n) / 8 * 8);
-  gemm_bf16_tn_p8<4, 0, false, false, false, false, true><<<dim3(grid), dim3(512), P8<4>::LDS_B, st>>>(
-      qh, gh, nullptr, nullptr, nullptr, 256, tiles_n * 256, K, 1, tiles_n, nullptr, nullptr, nullptr, gm, bm, ldG,
-      ldB, nval);
+  if (unit_rows == 2)
+    gemm_bf16_tn_p8<4, 0, false, false, false, false, 2><<<dim3(grid), dim3(512), P8<4>::LDS_B, st>>>(
+        qh, gh, nullptr, nullptr, nullptr, 256, tiles_n * 256, K, 1, tiles_n, nullptr, nullptr, nullptr, gm, bm, ldG,
+        ldB, nval);
+  else
+    gemm_bf16_tn_p8<4, 0, false, false, false, false, 4><<<dim3(grid), dim3(512), P8<4>::LDS_B, st>>>(
+        qh, gh, nullptr, nullptr, nullptr, 256, tiles_n * 256, K, 1, tiles_n, nullptr, nullptr, nullptr, gm, bm, ldG,
+        ldB, nval);
   return hipGetLastError();
 }
 }  // namespace mmr

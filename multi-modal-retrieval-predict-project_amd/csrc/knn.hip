@@ -44,7 +44,7 @@
 
 namespace mmr {
 hipError_t knn_scan_p8(const uint16_t* qh, const uint16_t* gh, int K, int tiles_n, int64_t nval, float* gm,
-                       int64_t ldG, float* bm, int64_t ldB, hipStream_t st);  // gemm.hip
+                       int64_t ldG, float* bm, int64_t ldB, int unit_rows, hipStream_t st);  // gemm.hip
 }
 
 namespace {
@@ -2303,11 +2303,22 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
           // Q = 64 / 128 / 192 / 256: 81 / 83 / 86 / 88 us vs 62 / 69 / 96 / 100.)
           knn_prep_queries<<<dim3(64), dim3(256), 0, st>>>(qp, pq, ix->d, ix->qn, ix->Dp, 256, ix->qnorm64, 3);
           MMR_LAUNCH_CHECK();
-          const int64_t ldG8 = ix->Np256 / 2, ldB8 = ix->Np256 / 64;  // 2-row units
-          MMR_CHECK_HIP(mmr::knn_scan_p8(qh, ix->ghr, ix->Dp, (int)(ix->Np256 / 256), ix->n, gm, ldG8, bm, ldB8, st));
-          launch_select<3, true>(st, pq, gm, ldG8, ldG8, ix, k, two_delta16, qp, ix->qnorm64, oi + p0 * k,
-                                 os ? os + p0 * k : nullptr, os64 ? os64 + p0 * k : nullptr, ost ? ost + p0 : nullptr,
-                                 bm, ldB8);
+          // unit size: 2 rows halves the rows the select re-scores per candidate unit, 4 rows halves
+          // the unit maxima the scan writes (512 vs 256 MB per pass at 1M rows): 2 for small
+          // galleries or large K (cfg2 100k / K 10: select 22 -> 16 us; cfg3 1M / K 50: 104 -> 65 us for
+          // +30 us of scan), 4 for large galleries at small K (cfg5 1M / K 10: +37 us scan, -9 select)
+          const bool u2 = ix->n <= (int64_t(1) << 18) || k >= 32;
+          const int64_t ldG8 = ix->Np256 / (u2 ? 2 : 4), ldB8 = ix->Np256 / 64;
+          MMR_CHECK_HIP(mmr::knn_scan_p8(qh, ix->ghr, ix->Dp, (int)(ix->Np256 / 256), ix->n, gm, ldG8, bm, ldB8,
+                                         u2 ? 2 : 4, st));
+          if (u2)
+            launch_select<3, true>(st, pq, gm, ldG8, ldG8, ix, k, two_delta16, qp, ix->qnorm64, oi + p0 * k,
+                                   os ? os + p0 * k : nullptr, os64 ? os64 + p0 * k : nullptr, ost ? ost + p0 : nullptr,
+                                   bm, ldB8);
+          else
+            launch_select<2, true>(st, pq, gm, ldG8, ldG8, ix, k, two_delta16, qp, ix->qnorm64, oi + p0 * k,
+                                   os ? os + p0 * k : nullptr, os64 ? os64 + p0 * k : nullptr, ost ? ost + p0 : nullptr,
+                                   bm, ldB8);
           MMR_LAUNCH_CHECK();
           continue;
         }

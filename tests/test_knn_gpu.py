@@ -396,3 +396,16 @@ def test_knn_f16_p8_small_galleries(N, Q):
     G = rng.standard_normal((N, 128), dtype=np.float32)
     Qm = rng.standard_normal((Q, 128), dtype=np.float32)
     _exact_check(G, Qm, 10, mode="f16")
+
+
+def test_knn_f16_p8_four_row_units():
+    """Galleries above 2^18 rows at K < 32: the 8-phase GEMM scan writes 4-row unit maxima
+    (knn_select_t<2>) instead of 2-row ones; exact vs the oracle, with a duplicate run and the
+    padded last tile."""
+    rng = np.random.default_rng(4444)
+    G = rng.standard_normal((300_001, 128), dtype=np.float32)
+    G[200_000:200_006] = G[11]
+    Qm = rng.standard_normal((200, 128), dtype=np.float32)
+    Qm[0] = G[11]
+    gi, _ = _exact_check(G, Qm, 10, mode="f16")
+    assert gi[0, :7].tolist() == [11] + list(range(200_000, 200_006))
