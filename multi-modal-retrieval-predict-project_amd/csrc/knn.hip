@@ -658,17 +658,7 @@ __global__ __launch_bounds__(64 * NWV) void knn_scan_f16_lq(const float* __restr
     for (int e = 0; e < L; ++e)
 #pragma unroll
       for (int j = 0; j < 4; ++j) b[j][e] = __builtin_nontemporal_load((const f32x4*)(pb + j * tileB + 512 * e));
-#pragma unroll 1
-    for (int kc = 0; kc < Dp; kc += KC) {
-      // the next chunk's gallery pieces are issued before this chunk's MFMAs (the last re-reads itself)
-      const int kn = kc + KC < Dp ? kc + KC : kc;
-      f32x4 nb[4][L];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int e = 0; e < L; ++e)
-          nb[j][e] = __builtin_nontemporal_load((const f32x4*)(pb + j * tileB + 16 * kn + 512 * e));
-      __builtin_amdgcn_sched_barrier(0);
+    auto mma = [&](int kc) {
 #pragma unroll
       for (int e = 0; e < L; ++e)
 #pragma unroll
@@ -678,12 +668,27 @@ __global__ __launch_bounds__(64 * NWV) void knn_scan_f16_lq(const float* __restr
           for (int j = 0; j < 4; ++j)
             acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, __builtin_bit_cast(h8, b[j][e]), acc[t][j], 0, 0, 0);
         }
+    };
+    // the next chunk's gallery pieces are issued before this chunk's MFMAs; the last chunk is peeled
+    // (no loads: an unconditional re-read of itself cost ~1/7 more load instructions at Dp = 768)
+    int kc = 0;
+#pragma unroll 1
+    for (; kc + KC < Dp; kc += KC) {
+      f32x4 nb[4][L];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < L; ++e)
+          nb[j][e] = __builtin_nontemporal_load((const f32x4*)(pb + j * tileB + 16 * (kc + KC) + 512 * e));
+      __builtin_amdgcn_sched_barrier(0);
+      mma(kc);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int e = 0; e < L; ++e)
 #pragma unroll
         for (int j = 0; j < 4; ++j) b[j][e] = nb[j][e];
     }
+    mma(kc);
     const int64_t gcol = blk * 16 + r;
     bool pad[4];
 #pragma unroll
