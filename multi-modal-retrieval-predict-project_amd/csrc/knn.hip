@@ -541,12 +541,26 @@ __global__ __launch_bounds__(64 * WQ) void knn_scan_f16_gmax(const uint16_t* __r
 #pragma unroll
     for (int j = 0; j < 4; ++j) b[j][e] = __builtin_nontemporal_load((const f32x4*)(pb + j * tileB + 512 * e));
   }
+  auto mma = [&](int kc) {
+#pragma unroll
+    for (int e = 0; e < L; ++e)
+#pragma unroll
+      for (int t = 0; t < QT; ++t) {
+        h8 av;
+        if constexpr (RAW) av = qcvt(t, kc + 32 * e + 8 * h, ra[t][e]);
+        else av = __builtin_bit_cast(h8, a[t][e]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, __builtin_bit_cast(h8, b[j][e]), acc[t][j], 0, 0, 0);
+      }
+  };
+  // both operands of the NEXT chunk are issued before this chunk's MFMAs (queries first: vmcnt
+  // retires in issue order); the current ones were issued one iteration earlier.  The last chunk is
+  // peeled (no loads: an unconditional re-read of itself cost ~1/7 more load instructions at Dp = 768).
+  int kc = 0;
 #pragma unroll 1
-  for (int kc = 0; kc < Dp; kc += KC) {
-    // both operands of the NEXT chunk are issued before this chunk's MFMAs (queries first: vmcnt
-    // retires in issue order); the current ones were issued one iteration earlier.  Unconditional
-    // (the last chunk re-reads itself): a branch would make the vmcnt at the join wait for them.
-    const int kn = kc + KC < Dp ? kc + KC : kc;
+  for (; kc + KC < Dp; kc += KC) {
+    const int kn = kc + KC;
     f32x4 na[QT][LA], nb[4][L];
     float4 nra[QT][LR][2];
 #pragma unroll
@@ -562,17 +576,7 @@ __global__ __launch_bounds__(64 * WQ) void knn_scan_f16_gmax(const uint16_t* __r
       for (int e = 0; e < L; ++e)
         nb[j][e] = __builtin_nontemporal_load((const f32x4*)(pb + j * tileB + 16 * kn + 512 * e));
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int e = 0; e < L; ++e)
-#pragma unroll
-      for (int t = 0; t < QT; ++t) {
-        h8 av;
-        if constexpr (RAW) av = qcvt(t, kc + 32 * e + 8 * h, ra[t][e]);
-        else av = __builtin_bit_cast(h8, a[t][e]);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, __builtin_bit_cast(h8, b[j][e]), acc[t][j], 0, 0, 0);
-      }
+    mma(kc);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int e = 0; e < L; ++e) {
@@ -589,6 +593,7 @@ __global__ __launch_bounds__(64 * WQ) void knn_scan_f16_gmax(const uint16_t* __r
       }
     }
   }
+  mma(kc);
   const int64_t gcol = blk * 16 + r;
   bool pad[4];
 #pragma unroll
@@ -993,24 +998,15 @@ __global__ __launch_bounds__(64) void knn_scan_f32_gmax(const float* __restrict_
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int e = 0; e < L; ++e) b[j][e] = __builtin_nontemporal_load((const f32x4*)(pb + j * tileB + 256 * e));
-  for (int kc = 0; kc < Dp; kc += KC) {
-    // queries first: vmcnt retires loads in issue order, so loads issued after the next chunk's
-    // gallery loads would make the MFMAs below wait for that chunk too
-    f32x4 a[QT][L];
+  // queries first: vmcnt retires loads in issue order, so loads issued after the next chunk's
+  // gallery loads would make the MFMAs below wait for that chunk too
+  auto qload = [&](int kc, f32x4 (&a)[QT][L]) {
 #pragma unroll
     for (int t = 0; t < QT; ++t)
 #pragma unroll
       for (int e = 0; e < L; ++e) a[t][e] = *(const f32x4*)(pa + t * tileB + 16 * kc + 256 * e);
-    // unconditional (the last chunk re-reads itself, an L2 hit): a branch here would make the
-    // compiler's vmcnt at the join wait for these loads before the MFMAs
-    f32x4 nb[4][L];
-    const int kn = kc + KC < Dp ? kc + KC : kc;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int e = 0; e < L; ++e)
-        nb[j][e] = __builtin_nontemporal_load((const f32x4*)(pb + j * tileB + 16 * kn + 256 * e));
-    __builtin_amdgcn_sched_barrier(0);  // keep the whole next chunk issued ahead of the MFMAs
+  };
+  auto mma = [&](const f32x4 (&a)[QT][L]) {
 #pragma unroll
     for (int e = 0; e < L; ++e) {
 #pragma unroll
@@ -1026,11 +1022,31 @@ __global__ __launch_bounds__(64) void knn_scan_f32_gmax(const float* __restrict_
         }
       }
     }
+  };
+  // the next chunk's gallery pieces are issued ahead of this chunk's MFMAs; the last chunk is peeled
+  // (no gallery loads: an unconditional re-read of itself cost extra load instructions per chunk)
+  int kc = 0;
+  for (; kc + KC < Dp; kc += KC) {
+    f32x4 a[QT][L];
+    qload(kc, a);
+    f32x4 nb[4][L];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < L; ++e)
+        nb[j][e] = __builtin_nontemporal_load((const f32x4*)(pb + j * tileB + 16 * (kc + KC) + 256 * e));
+    __builtin_amdgcn_sched_barrier(0);  // keep the whole next chunk issued ahead of the MFMAs
+    mma(a);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int e = 0; e < L; ++e) b[j][e] = nb[j][e];
+  }
+  {
+    f32x4 a[QT][L];
+    qload(kc, a);
+    mma(a);
   }
   // C[i][c]: c = lane&15 (gallery row r of tile j), i = 4h + reg (query of tile t)
   float ig[4];
