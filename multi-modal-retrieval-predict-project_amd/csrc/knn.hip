@@ -1309,10 +1309,11 @@ __device__ uint32_t block_kth_lower_top4(uint32_t key, int kth, uint32_t* vals, 
   __syncthreads();
   if (tid < 64) {
     const uint32_t mine = lane < NV ? vals[lane] : 0u;
-    int rank = 0;  // values ahead of mine (larger, or equal at a lower position)
-#pragma unroll 8
+    int rank = 0;  // values ahead of mine (larger, or equal at a lower position); the others' values
+                   // by lane swaps (a loop of LDS reads paid the LDS latency per step, ~1.3 us)
+#pragma unroll
     for (int j = 0; j < NV; ++j) {
-      const uint32_t o = vals[j];
+      const uint32_t o = (uint32_t)__shfl((int)mine, j, 64);
       rank += (o > mine) || (o == mine && j < lane);
     }
     if (lane < NV && rank == kth - 1) bcast[0] = mine;
