@@ -625,13 +625,33 @@ template <int QT, int KC, int NWV>
 __global__ __launch_bounds__(64 * NWV) void knn_scan_f16_lq(const float* __restrict__ qraw, int64_t nq, int d,
                                                           const uint16_t* __restrict__ gh,
                                                           float* __restrict__ gmax, float* __restrict__ bmax,
-                                                          int Dp, int64_t ldG, int64_t ldB, int64_t n, int64_t nblk) {
+                                                          int Dp, int64_t ldG, int64_t ldB, int64_t n, int64_t nblk,
+                                                          double* __restrict__ qpre) {
   typedef _Float16 h8 __attribute__((ext_vector_type(8)));
   constexpr int L = KC / 32;  // 1-KB pieces per tile per chunk
   extern __shared__ __attribute__((aligned(16))) uint16_t qs[];  // [QT][Dp/32][512] halfs
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int KP = Dp / 32;
+  if (blockIdx.x == 0) {
+    // |q| (f64, the select's canonical order: lane sums elements lane + 64c, c < 16, then the xor
+    // tree — bit-identical to knn_select_t's own query_norm) and max |q_k| per query, for the select
+    for (int row = wave; row < nq; row += NWV) {
+      double ss = 0.0;
+      float am = 0.f;
+      for (int e = lane; e < 1024; e += 64) {
+        const float x = e < d ? qraw[(int64_t)row * d + e] : 0.f;
+        ss += (double)x * (double)x;
+        am = fmaxf(am, fabsf(x));
+      }
+      ss = mmr::wave_sum(ss);
+      am = mmr::wave_max(am);
+      if (lane == 0) {
+        qpre[2 * row] = sqrt(ss);
+        qpre[2 * row + 1] = (double)am;
+      }
+    }
+  }
   // (1) queries -> fp16 tile32h in LDS: one (row, 8-k group) per item, 16-B store; rows >= nq and
   //     k >= d are zero (unconditional clamped loads, masked at the conversion)
   const int groups = QT * 16 * (Dp / 8);
@@ -1340,7 +1360,7 @@ __global__ __launch_bounds__(T) void knn_select_t(
     const float* __restrict__ q_raw, int d, const double* __restrict__ qnorm64,
     const float* __restrict__ gal, int Dp, const double* __restrict__ gnorm64, int64_t idx_base,
     int64_t* __restrict__ out_idx, float* __restrict__ out_score, double* __restrict__ out_score64,
-    int32_t* __restrict__ status) {
+    int32_t* __restrict__ status, const double* __restrict__ qpre = nullptr) {
   constexpr int GS = MODE == 0 ? 1 : MODE == 3 ? 2 : 4;  // rows per unit
   constexpr int UPB = 64 / GS;               // units per 64-row block (COARSE)
   constexpr int UC = kCandCap / GS;          // units per batch
@@ -1443,8 +1463,16 @@ __global__ __launch_bounds__(T) void knn_select_t(
     }
   };
   if (RAW) {
-    __syncthreads();  // qrow staged
-    query_norm();     // L.qn / L.qmax visible after block_kth_lower's first barrier
+    if (qpre != nullptr) {  // computed by the scan (knn_scan_f16_lq), same order and bits
+      if (tid == 0) {
+        L.qn = qpre[2 * qi];
+        L.qmax = (float)qpre[2 * qi + 1];
+      }
+    } else {
+      __syncthreads();  // qrow staged
+      query_norm();
+    }
+    // L.qn / L.qmax visible after the first bound's first barrier
   }
   SEL_MARK(1)
   // (B) lower bound of the K-th largest thread max, clamped to -inf's key (smaller keys are NaNs)
@@ -2115,13 +2143,13 @@ template <int MODE, bool COARSE = false, bool RAW = false>
 void launch_select(hipStream_t st, int64_t nq, const float* vals, int64_t ldV, int64_t nunits, const mmr_index* ix,
                    int k, float two_delta, const float* q_raw, const double* qnorm64, int64_t* oi, float* os,
                    double* os64, int32_t* ost, const float* bvals = nullptr, int64_t ldB = 0,
-                   float two_delta_abs = 0.f) {
+                   float two_delta_abs = 0.f, const double* qpre = nullptr) {
   constexpr int T = COARSE ? 512 : kSelThreads;
   const dim3 g((unsigned)nq), b(T);
 #define MMR_SEL(NC)                                                                                              \
   knn_select_t<MODE, NC, T, COARSE, RAW><<<g, b, 0, st>>>(vals, ldV, nunits, ix->n, k, two_delta, bvals, ldB,    \
                                                           two_delta_abs, q_raw, ix->d, qnorm64, ix->gal, ix->Dp,  \
-                                                          ix->norm64, ix->idx_base, oi, os, os64, ost)
+                                                          ix->norm64, ix->idx_base, oi, os, os64, ost, qpre)
   // NC = 256-float chunks of a row in the f64 re-score (0: d > 1024, strided loop)
   switch (ix->d > 1024 ? 0 : (int)ceil_div(ix->Dp, 256)) {
     case 1: MMR_SEL(1); break;
@@ -2376,17 +2404,18 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
         if (qt <= 2 && ix->d % 8 == 0 && ((uintptr_t)qp & 15) == 0 && raw_scan_enabled()) {
           // <= 32 queries: the scan reads the caller's f32 rows itself (no prep launch), per-query margin
           const int64_t nqp = pq;
-          if (lq_scan_enabled() && ix->Dp <= 1024) {
+          const bool lq = lq_scan_enabled();
+          if (lq && ix->Dp <= 1024) {
             const size_t lds = (size_t)qt * 16 * ix->Dp * 2;
             const int64_t nblk = ix->Np / 64;
             const dim3 g2((unsigned)ix->n_cu);
             if (qt == 1) {
               if (ix->Dp % 128 == 0)
-                knn_scan_f16_lq<1, 128, 8><<<g2, 512, lds, st>>>(qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, nblk);
+                knn_scan_f16_lq<1, 128, 8><<<g2, 512, lds, st>>>(qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, nblk, ix->qnorm64);
               else
-                knn_scan_f16_lq<1, 64, 8><<<g2, 512, lds, st>>>(qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, nblk);
+                knn_scan_f16_lq<1, 64, 8><<<g2, 512, lds, st>>>(qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, nblk, ix->qnorm64);
             } else {
-              knn_scan_f16_lq<2, 64, 8><<<g2, 512, lds, st>>>(qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, nblk);
+              knn_scan_f16_lq<2, 64, 8><<<g2, 512, lds, st>>>(qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, nblk, ix->qnorm64);
             }
           } else if (qt == 1) {
             if (ix->Dp % 128 == 0)
@@ -2399,7 +2428,8 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
           MMR_LAUNCH_CHECK();
           launch_select<1, true, true>(st, pq, gm, ldG, ldG, ix, k, two_delta16r, qp, ix->qnorm64, oi + p0 * k,
                                        os ? os + p0 * k : nullptr, os64 ? os64 + p0 * k : nullptr,
-                                       ost ? ost + p0 : nullptr, bm, ldB, two_delta16a);
+                                       ost ? ost + p0 : nullptr, bm, ldB, two_delta16a,
+                                       lq && ix->Dp <= 1024 ? ix->qnorm64 : nullptr);
           MMR_LAUNCH_CHECK();
           continue;
         }
