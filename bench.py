@@ -13,8 +13,11 @@ Presets (BASELINE.json configs): cfg2 = the defaults; cfg3 = --model-type text -
   --gallery 1000000 --k 50; cfg4 = cfg2 with 1M gallery rows per GPU (8M at --gpus 8); cfg5 =
   --tower-dtype fp8 --batch 2048 --dim 1024 --gallery 1000000 --rerank: MX-fp8 linears in all BERT
   layers and Swin stages 3-4, joint_dim 1024, top-10 per query over 1M x 1024 rows per GPU, then the
-  fused KG / label rerank (mmr_index_rerank, reranker.py:240-333) of those 10 candidates (batch 2048 is
-  per GPU: weak scaling like the other presets; --rerank runs at --gpus 1 only).
+  KG / label rerank (reranker.py:240-333) of those 10 candidates (batch 2048 is per GPU: weak scaling
+  like the other presets).  World 1: one fused kernel (mmr_index_rerank).  World > 1: each shard
+  computes its candidates' raw components (mmr_index_rerank_components), they ride with the score /
+  index lists through the all-gather and the merge (mmr_merge_topk_payload), and the min-max / mix /
+  rank runs on the merged list (mmr_rerank_mix) — the same result as one index.
 N>1: `python bench.py --gpus N` starts N ranks itself (torch.distributed.run, one process per GPU,
 RCCL) unless it already runs under a launcher (WORLD_SIZE set, which must equal --gpus).  The
 gallery is row-sharded (--gallery rows per rank: weak scaling), every rank runs its own query batch
@@ -68,6 +71,8 @@ def parse(argv=None):
                         "8 heads), text / image (one tower + its head), both (both single-modality heads)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-queries", type=int, default=0)
+    p.add_argument("--parity-queries", type=int, default=64,
+                   help="queries re-embedded by the fp32 oracle for recall / P@10 vs the CPU path")
     a = p.parse_args(argv)
     pre = dict({"batch": 256, "gallery": 100_000, "k": 10, "model_type": "multimodal", "dim": 768,
                 "tower_dtype": "bf16", "rerank": False}, **PRESETS[a.preset])
@@ -123,8 +128,6 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
         sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}: refusing to report a mismatched run")
-    if a.rerank and world > 1:
-        sys.exit("bench.py: --rerank needs the candidates' gallery rows on the reranking GPU; run it at --gpus 1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
@@ -139,7 +142,7 @@ def main():
 
     import mmr_amd  # noqa: F401
     from mmr_amd import synthetic
-    from mmr_amd.retrieval import GalleryIndex, check_status, merge_topk
+    from mmr_amd.retrieval import GalleryIndex, check_status, merge_topk, rerank_mix
 
     # gallery shard: rows [rank*n, (rank+1)*n) of a virtual (world*n, d) N(0,1) gallery
     n, d, K, B = a.gallery, a.dim, a.k, a.batch
@@ -164,17 +167,19 @@ def main():
     rr = None
     if a.rerank:
         # synthetic rerank tables (reranker.py:88-129 loads them from the KG directory / labels CSV):
-        # 1-3 of 43 labels per row as uint64 bitsets, RERANK_DK-wide KG vectors
-        gen = torch.Generator(device=dev).manual_seed(synthetic.SEED + 31)
+        # 1-3 of 43 labels per row as uint64 bitsets, RERANK_DK-wide KG vectors.  Query tables cover
+        # all world * nqr queries in all-gather order (same seed on every rank), gallery tables this
+        # rank's shard rows
         nqr = B * (2 if a.model_type == "both" else 1)
 
-        def bits(rows):
+        def bits(rows, gen):
             lab = torch.randint(0, synthetic.NUM_LABELS, (rows, 3), generator=gen, device=dev)
             keep = torch.rand((rows, 3), generator=gen, device=dev) < torch.tensor([1.0, 0.5, 0.3], device=dev)
             return ((torch.ones_like(lab) << lab) * keep).sum(1)
-        rr = {"g_lab": bits(n), "q_lab": bits(nqr),
-              "g_kg": torch.randn((n, RERANK_DK), generator=gen, device=dev),
-              "q_kg": torch.randn((nqr, RERANK_DK), generator=gen, device=dev)}
+        gq = torch.Generator(device=dev).manual_seed(synthetic.SEED + 31)
+        gg = torch.Generator(device=dev).manual_seed(synthetic.SEED + 32 + rank)
+        rr = {"q_lab": bits(world * nqr, gq), "q_kg": torch.randn((world * nqr, RERANK_DK), generator=gq, device=dev),
+              "g_lab": bits(n, gg), "g_kg": torch.randn((n, RERANK_DK), generator=gg, device=dev)}
 
     stream = torch.cuda.current_stream(dev)
     ev_pairs = []
@@ -198,14 +203,23 @@ def main():
             e1.record(stream)
             ev_pairs.append((e0, e1))
         torch.maximum(st_max, st.max(), out=st_max)  # checked after the timed region (no sync here)
-        if rr is not None:  # fused rerank of the K candidates (world 1: local = global row ids)
+        if rr is not None and world == 1:  # fused rerank of the K candidates (local = global row ids)
             i = index.rerank(allq, i, rr["q_lab"], rr["g_lab"], rr["q_kg"], rr["g_kg"], K, want_components=False)[0]
         if world > 1:
+            nq = q.shape[0]
             gi = torch.empty((world * i.shape[0], K), dtype=i.dtype, device=dev)
             gs = torch.empty((world * s64.shape[0], K), dtype=s64.dtype, device=dev)
             dist.all_gather_into_tensor(gi, i)
             dist.all_gather_into_tensor(gs, s64)
-            i, s, _ = merge_topk(gs.view(world, -1, K), gi.view(world, -1, K), K)
+            if rr is None:  # merge this rank's queries only
+                i, s, _ = merge_topk(gs.view(world, -1, K), gi.view(world, -1, K), K, q0=rank * nq, nq=nq)
+            else:  # sharded rerank: shard-local raw components ride through the merge
+                comp = index.rerank_components(allq, i, rr["q_lab"], rr["g_lab"], rr["q_kg"], rr["g_kg"])
+                gc = torch.empty((world * comp.shape[0], K, 3), dtype=comp.dtype, device=dev)
+                dist.all_gather_into_tensor(gc, comp)
+                mi, s, _, mc = merge_topk(gs.view(world, -1, K), gi.view(world, -1, K), K,
+                                          payload=gc.view(world, -1, K, 3), q0=rank * nq, nq=nq)
+                i = rerank_mix(mi, mc, K, want_components=False)[0]
         return q, i, s
 
     for _ in range(a.warmup):
@@ -250,6 +264,23 @@ def main():
     torch.cuda.synchronize(dev)
     check_status(st16)
     lat_small = sum(e0.elapsed_time(e1) for e0, e1 in hev) / len(hev)
+    # the same single search with the Infinity Cache (256 MB MALL) flushed first: a 512 MB write
+    # between searches evicts the gallery copy, so the search streams it from HBM (the back-to-back
+    # figure below re-reads a copy that fits the MALL when n*d*2 < 256 MB)
+    flush = torch.empty((512 << 20) // 4, dtype=torch.float32, device=dev)
+    hev = []
+    for _ in range(10):
+        flush.zero_()
+        torch.cuda._sleep(1_000_000)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        _, _, st16 = index.search(q16, K, want_status=True)
+        e1.record(stream)
+        hev.append((e0, e1))
+    torch.cuda.synchronize(dev)
+    check_status(st16)
+    lat_cold = sum(e0.elapsed_time(e1) for e0, e1 in hev) / len(hev)
+    del flush
     # serving throughput: NB back-to-back 16-query searches between ONE event pair, all enqueued
     # behind a device spin longer than their host enqueue time (so the GPU never waits on the host);
     # every search does its full work (own outputs, status checked)
@@ -292,16 +323,21 @@ def main():
     q_per_s = world * nq_step * a.steps / elapsed
     pairs_per_s = (world * nq_step) * (world * n) * a.steps / elapsed
     Qs = world * nq_step
-    roof, knn_roof = roofline(a, n, d, K, Qs, ms_search, ms_small, q16.shape[0], gemm_ms, B, lat_small)
+    roof, knn_roof = roofline(a, n, d, K, Qs, ms_search, ms_small, q16.shape[0], gemm_ms, B, lat_small, lat_cold)
 
-    cpu = cpu_knn = recall = None
+    cpu = cpu_knn = recall = p10 = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         if model is None:
             cpu = cpu_baseline_knn(a, G, qbatch.cpu().numpy())
         else:
             cpu, emb_cpu = cpu_baseline_full(a, G, imgs, ids, mask)
             cpu_knn = cpu_baseline_knn(a, G, q_last[:64].cpu().numpy())
-            recall = recall_vs_cpu(index, q_last[:emb_cpu.shape[0]], emb_cpu, G, K)
+            nq_par = min(a.parity_queries, q_last.shape[0] if a.model_type != "both" else B)
+            emb_par = oracle_embeddings(a, imgs, ids, mask, nq_par)
+            q_par = q_last[:nq_par] if a.model_type != "both" else torch.cat([q_last[:nq_par], q_last[B:B + nq_par]])
+            recall = recall_vs_cpu(index, q_par, emb_par, G, K)
+            p10 = precision_vs_cpu(q_par, emb_par, d, a.knn_mode)
+            del emb_cpu
 
     if rank == 0:
         workload = {
@@ -332,6 +368,7 @@ def main():
             "knn_status_ok": True,
             "recall_at_10_vs_cpu": recall["recall_at_k"] if recall else None,
             "recall_vs_cpu": recall,
+            "p_at_10": p10,
             "cpu_baseline": cpu,
             "cpu_baseline_knn": cpu_knn,
         }
@@ -340,7 +377,7 @@ def main():
         dist.destroy_process_group()
 
 
-def roofline(a, n, d, K, Qs, ms_search, ms_small, q_small, gemm_ms, B, lat_small=None):
+def roofline(a, n, d, K, Qs, ms_search, ms_small, q_small, gemm_ms, B, lat_small=None, lat_cold=None):
     """Roofline object of the dominant kernel (full: the BERT FFN1 GEMM, with the other BERT GEMM
     families beside it; knn: the search call) + the kNN search's own roofline."""
     # kNN search: algorithmic flops 2*Q*N*D; bytes = the scanned gallery copy once + norms + queries +
@@ -374,9 +411,14 @@ def roofline(a, n, d, K, Qs, ms_search, ms_small, q_small, gemm_ms, B, lat_small
         "achieved_gbs": small_bytes / (ms_small / 1e3) / 1e9,
         "frac": small_bytes / (ms_small / 1e3) / peak_hbm,
         "timing": "20 back-to-back whole search calls between one event pair on the launch stream "
-                  "(serving throughput; queued behind a device spin so the host enqueue is hidden)",
+                  "(serving throughput; queued behind a device spin so the host enqueue is hidden); the "
+                  "scanned copy (%d MB) %s the 256 MB Infinity Cache, so these re-reads may be partly "
+                  "MALL-served: latency_ms_single_cold flushes it (512 MB write) before each search"
+                  % (n * d * gbytes >> 20, "fits" if n * d * gbytes < (256 << 20) else "exceeds"),
         "latency_ms_single": lat_small,
         "latency_frac_single": (small_bytes / (lat_small / 1e3) / peak_hbm) if lat_small else None,
+        "latency_ms_single_cold": lat_cold,
+        "latency_frac_single_cold": (small_bytes / (lat_cold / 1e3) / peak_hbm) if lat_cold else None,
         "kernel": "whole search call: %s scan + knn_select_t"
                   % ("knn_scan_f16_gmax<1, RAW> (no prep launch)" if a.knn_mode == "f16"
                      else "prep + knn_scan_f32_gmax<1>")}
@@ -395,8 +437,10 @@ def roofline(a, n, d, K, Qs, ms_search, ms_small, q_small, gemm_ms, B, lat_small
         fl = 2.0 * M * 3072 * 768
         roof = {"bound": "mfma", "achieved": fl / (ms_ffn1 / 1e3) / 1e12, "peak": peak_gemm / 1e12,
                 "unit": "TFLOP/s", "traffic": None,
-                "kernel": (("BERT FFN1 MX-fp8 GEMM + GELU incl. its activation quantiser (M=%d, N=3072, K=768; "
-                            "gemm_bf16_tn_p8<3, FP8>), " if fp8 else
+                "kernel": (("BERT FFN1 MX-fp8 GEMM + GELU (M=%d, N=3072, K=768; gemm_bf16_tn_p8<4, FP8>, bf16 "
+                            "output) + its activation quantiser launch: the per-GEMM timing pass runs the "
+                            "UNFUSED form (in the timed steps FFN1 emits FFN2's fp8 operand directly, "
+                            "mmr_linear_mxfp8_q8), " if fp8 else
                             "BERT FFN1 GEMM + GELU (M=%d, N=3072, K=768; tuned variant), ") % M
                            + "timed per launch with HIP events in a towers-in-sequence pass after the timed region"),
                 "ms_per_launch": ms_ffn1, "flops_per_launch": fl, "bert_gemms": fam, "knn": knn_roof}
@@ -534,6 +578,43 @@ def cpu_baseline_full(a, G, imgs, ids, mask):
                        f"CPU: {cpu_model()}"}, res["q"])
 
 
+def oracle_embeddings(a, imgs, ids, mask, nq):
+    """fp32 oracle (the reference's CPU path restated, oracle/towers.py) joint embeddings of the
+    first nq of the bench's own inputs (both: [image heads; text heads])."""
+    import torch
+    from mmr_amd.model import init_fusion_state, init_head_state
+    from mmr_amd.towers import BERT_BASE, SWIN_T, init_bert_state, init_swin_state
+    from oracle import towers as otw
+    _cores()
+    ssd, bsd = init_swin_state(SWIN_T, 2709), init_bert_state(BERT_BASE, 2710)
+    hsd = init_head_state(768, 768, a.dim, 2711)
+    if a.model_type == "multimodal":
+        hsd.update(init_fusion_state(768, 768, a.dim, 8, 5, 2712))
+    img = imgs[:nq].cpu() if imgs is not None else None
+    ii = ids[:nq].cpu() if ids is not None else None
+    mm = mask[:nq].cpu() if mask is not None else None
+    out = []
+    with torch.no_grad():
+        for c0 in range(0, nq, 16):  # bounded host memory per chunk
+            sl = slice(c0, min(nq, c0 + 16))
+            if a.model_type == "text":
+                t = otw.bert_forward(ii[sl], mm[sl], bsd, BERT_BASE["num_hidden_layers"], BERT_BASE["num_attention_heads"])
+                q = otw.heads(None, None, t, hsd, "text")["joint_emb"]
+            elif a.model_type == "image":
+                g, p = otw.swin_image(img[sl], ssd, SWIN_T)
+                q = otw.heads(g, p, None, hsd, "image")["joint_emb"]
+            else:
+                (g, p), t = otw.backbones_forward(img[sl], ii[sl], mm[sl], ssd, bsd, SWIN_T, BERT_BASE)
+                if a.model_type == "multimodal":
+                    q = otw.heads(g, p, t, hsd, "multimodal", mm_cfg={"num_heads": 8})["joint_emb"]
+                else:
+                    q = (otw.heads(g, p, t, hsd, "image")["joint_emb"], otw.heads(g, p, t, hsd, "text")["joint_emb"])
+            out.append(q)
+    if a.model_type == "both":
+        return torch.cat([torch.cat([o[0] for o in out]), torch.cat([o[1] for o in out])]).numpy()
+    return torch.cat(out).numpy()
+
+
 def recall_vs_cpu(index, q_gpu, emb_cpu, G, K):
     """Recall@K of the GPU path against the reference CPU path on the same inputs: top-K of the GPU
     (bf16-tower) embeddings through the GPU index vs top-K of the fp32 oracle embeddings through the
@@ -550,7 +631,45 @@ def recall_vs_cpu(index, q_gpu, emb_cpu, G, K):
     return {"recall_at_k": float(np.mean(inter)), "k": K, "queries": int(len(ci)),
             "exact_list_match": float(np.mean([np.array_equal(gi[r], ci[r]) for r in range(len(ci))])),
             "min_embedding_cosine": float(cos.min()),
-            "note": "GPU towers (bf16, or MX-fp8 linears at --tower-dtype fp8) + GPU exact kNN vs fp32 oracle towers + sklearn-path kNN, same inputs"}
+            "note": "GPU towers (bf16, or MX-fp8 linears at --tower-dtype fp8) + GPU exact kNN vs fp32 oracle towers + "
+                    "sklearn-path kNN, same inputs, over the bench's N(0,1) gallery"}
+
+
+def precision_vs_cpu(q_gpu, emb_cpu, d, knn_mode, K=10, n_gallery=100_000):
+    """BASELINE.md §3 "identical Precision@10": the GPU path (GPU towers + GPU exact kNN) and the
+    reference CPU path restated (fp32 oracle towers + sklearn-path ranking, retrieval_overlap.py:84-90)
+    on the same queries over a LABELLED synthetic gallery (43 labels, 1-3 per row, row = sum of
+    label centres + noise; relevance = shares >= 1 label, contructGT.py:69-81), P@10 with the
+    reference's precision_at_k (retrieval_metrics.py:4-11) and R@10 / MRR per
+    retrieval_overlap.py:84-115 / retrieval_eval.py:146-171."""
+    import numpy as np
+    from mmr_amd import metrics, synthetic
+    from mmr_amd.retrieval import GalleryIndex
+    from oracle import knn as oknn
+    G, gl = synthetic.labelled_gallery(n_gallery, d, synthetic.SEED + 53)
+    gbits = synthetic.labels_to_bits(gl)
+    rng = np.random.default_rng(synthetic.SEED + 54)
+    nq = q_gpu.shape[0]
+    ql = np.zeros((nq, synthetic.NUM_LABELS), np.uint8)
+    for r in range(nq):
+        ql[r, rng.choice(synthetic.NUM_LABELS, size=int(rng.integers(1, 4)), replace=False)] = 1
+    qbits = synthetic.labels_to_bits(ql)
+    ix = GalleryIndex(G, mode=knn_mode)
+    gi = ix.search(q_gpu.contiguous(), K)[0].cpu().numpy()
+    ix.close()
+    ci, _ = oknn.sklearn_topk(emb_cpu, G, K)
+
+    def pr(idx):
+        rel = [[str(j) for j in np.nonzero(gbits & qbits[q])[0]] for q in range(nq)]
+        p = float(np.mean([metrics.precision_at_k([str(j) for j in idx[q]], rel[q], K) for q in range(nq)]))
+        mrr, _, rec = metrics.ranking_metrics(idx, qbits, gbits, K)
+        return p, float(rec), float(mrr)
+    pg, rg, mg = pr(gi)
+    pc, rc, mc = pr(ci)
+    return {"queries": int(nq), "gallery": f"labelled {n_gallery}x{d}", "k": K,
+            "p_at_10_gpu": pg, "p_at_10_cpu": pc, "r_at_10_gpu": rg, "r_at_10_cpu": rc,
+            "mrr_gpu": mg, "mrr_cpu": mc, "identical_p_at_10": pg == pc, "identical_r_at_10": rg == rc,
+            "top10_overlap": float(np.mean([len(set(gi[r]) & set(ci[r])) / K for r in range(nq)]))}
 
 
 if __name__ == "__main__":

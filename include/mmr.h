@@ -53,6 +53,11 @@ mmr_status mmr_index_create(const void* gallery, int64_t n, int32_t d, mmr_dtype
                             int gallery_is_host, int64_t idx_base, int device, mmr_index** out);
 mmr_status mmr_index_destroy(mmr_index* index);
 mmr_status mmr_index_info(const mmr_index* index, int64_t* n, int32_t* d, int64_t* idx_base);
+/* Device bytes the index holds: gallery_bytes = f32 rows + norms + the scan copies of the current
+ * mode (x3: bf16 hi/lo split + tile16 f32, 12 B per element; f16: fp16 tile32h + row-major fp16,
+ * 4 B per element; f32: none — copies of other modes are freed at a mode switch);
+ * workspace_bytes = the query / per-unit-maxima workspace.  Either pointer may be NULL. */
+mmr_status mmr_index_device_bytes(const mmr_index* index, int64_t* gallery_bytes, int64_t* workspace_bytes);
 /* Pre-allocate the workspace for up to `max_q` queries in the CURRENT scan mode so that later
  * searches allocate nothing (required before capturing a search into a HIP graph). */
 mmr_status mmr_index_reserve(mmr_index* index, int64_t max_q);
@@ -112,6 +117,32 @@ mmr_status mmr_index_rerank(const mmr_index* index, const float* q_emb, int64_t 
 mmr_status mmr_merge_topk(const double* scores, const int64_t* idx, int32_t n_lists, int64_t nq,
                           int32_t k_in, int32_t k_out, int64_t* out_idx, float* out_score,
                           double* out_score64, void* stream);
+/* mmr_merge_topk over queries [q0, q0 + nq) of lists laid out [n_lists][nq_total][k_in] (a rank
+ * merges only its own queries after the all-gather), with an optional f64 payload of
+ * payload_width (<= 16) values per entry, [n_lists][nq_total][k_in][width], carried into
+ * out_payload [nq][k_out][width] (zeros for empty slots).  payload and out_payload are both NULL or
+ * both set.  The sharded rerank's per-candidate components ride here (reranker.py:240-333 needs
+ * them over the MERGED candidate list). */
+mmr_status mmr_merge_topk_payload(const double* scores, const int64_t* idx, const double* payload,
+                                  int32_t payload_width, int32_t n_lists, int64_t nq_total, int64_t q0,
+                                  int64_t nq, int32_t k_in, int32_t k_out, int64_t* out_idx, float* out_score,
+                                  double* out_score64, double* out_payload, void* stream);
+
+/* Sharded KG / label rerank (Reranker.rerank, src/Retrieval/reranker.py:240-333, over a row-sharded
+ * gallery).  Shard side: mmr_index_rerank_components writes, for each of this shard's candidates
+ * cand (nq, kc) (global indices into this index, -1 = empty), the three RAW components
+ * out_comp (nq, kc, 3) f64 = {emb cosine, label Jaccard, KG cosine} — the same f64 arithmetic as
+ * mmr_index_rerank (zeros for an empty slot).  They travel with the (score, index) lists through
+ * the all-gather and mmr_merge_topk_payload; mmr_rerank_mix then min-max scales them over the
+ * merged list, mixes alpha/beta/gamma and ranks exactly as mmr_index_rerank does, so a sharded
+ * rerank returns bit-identical results to the single-index one.  Arguments as mmr_index_rerank. */
+mmr_status mmr_index_rerank_components(const mmr_index* index, const float* q_emb, int64_t nq,
+                                       const int64_t* cand, int32_t kc, const uint64_t* q_labels,
+                                       const uint64_t* g_labels, const float* q_kg, const float* g_kg,
+                                       int32_t dk, double* out_comp, void* stream);
+mmr_status mmr_rerank_mix(const int64_t* cand, const double* comp, int64_t nq, int32_t kc, double alpha,
+                          double beta, double gamma, int32_t topk, int64_t* out_idx, double* out_final,
+                          double* out_emb, double* out_lab, double* out_kg, void* stream);
 
 /* ---------------------------------------------------------------- tower ops (bf16 = uint16) */
 /* Y[m][n] = act(X[m][k] . W[n][k]^T + bias[n]) (+ R[m][n]); X, W, R, Y bf16; bias f32 or NULL;

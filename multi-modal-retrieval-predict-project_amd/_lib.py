@@ -24,12 +24,18 @@ SIGNATURES = {
     "mmr_index_destroy": [c_vp],
     "mmr_index_info": [c_vp, ctypes.POINTER(c_i64), ctypes.POINTER(c_i32), ctypes.POINTER(c_i64)],
     "mmr_index_reserve": [c_vp, c_i64],
+    "mmr_index_device_bytes": [c_vp, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)],
     "mmr_index_set_mode": [c_vp, c_i32],
     "mmr_index_search": [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
     "mmr_index_link_graph": [c_vp, ctypes.c_double, c_i32, c_i64, c_i64, c_vp, c_vp, c_vp],
     "mmr_index_rerank": [c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, ctypes.c_double,
                          ctypes.c_double, ctypes.c_double, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "mmr_merge_topk": [c_vp, c_vp, c_i32, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp],
+    "mmr_merge_topk_payload": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp,
+                               c_vp, c_vp],
+    "mmr_index_rerank_components": [c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp],
+    "mmr_rerank_mix": [c_vp, c_vp, c_i64, c_i32, ctypes.c_double, ctypes.c_double, ctypes.c_double, c_i32, c_vp, c_vp,
+                       c_vp, c_vp, c_vp, c_vp],
     "mmr_linear_bf16": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp],
     "mmr_linear_bf16_variant": [c_i64, c_i32, c_i32, c_i32, c_i32, c_i32],
     "mmr_quantize_mxfp8": [c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp],

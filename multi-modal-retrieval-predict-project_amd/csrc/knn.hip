@@ -1814,20 +1814,25 @@ __global__ __launch_bounds__(T) void knn_select_t(
 }
 
 // ------------------------------------------------------------------ shard merge
+// Lists [n_lists][nq_total][k_in]; workgroup qi merges query q0 + qi.  Optional payload
+// pay [n_lists][nq_total][k_in][P] f64 rides with each entry into out_pay [nq][k_out][P] (the
+// sharded rerank's per-candidate components, computed on the shard that owns the row).
 __global__ __launch_bounds__(256) void knn_merge(const double* __restrict__ scores,
                                                  const int64_t* __restrict__ idx, int n_lists,
-                                                 int64_t nq, int k_in, int k_out,
+                                                 int64_t nq_total, int64_t q0, int k_in, int k_out,
                                                  int64_t* __restrict__ out_idx,
                                                  float* __restrict__ out_score,
-                                                 double* __restrict__ out_score64) {
+                                                 double* __restrict__ out_score64,
+                                                 const double* __restrict__ pay, int P,
+                                                 double* __restrict__ out_pay) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* cs = (double*)smem;
   int64_t* ci = (int64_t*)(smem + sizeof(double) * n_lists * k_in);
   const int64_t qi = blockIdx.x;
   const int m = n_lists * k_in;
+  auto src = [&](int c) { return ((int64_t)(c / k_in) * nq_total + q0 + qi) * k_in + c % k_in; };
   for (int c = threadIdx.x; c < m; c += blockDim.x) {
-    const int l = c / k_in, e = c % k_in;
-    const int64_t off = ((int64_t)l * nq + qi) * k_in + e;
+    const int64_t off = src(c);
     cs[c] = scores[off];
     ci[c] = idx[off];
   }
@@ -1849,12 +1854,16 @@ __global__ __launch_bounds__(256) void knn_merge(const double* __restrict__ scor
       out_idx[qi * k_out + rank] = ic;
       if (out_score) out_score[qi * k_out + rank] = (float)sc;
       if (out_score64) out_score64[qi * k_out + rank] = sc;
+      if (out_pay)
+        for (int p = 0; p < P; ++p) out_pay[(qi * k_out + rank) * P + p] = pay[src(c) * P + p];
     }
   }
   for (int r = nvalid + threadIdx.x; r < k_out; r += blockDim.x) {
     out_idx[qi * k_out + r] = -1;
     if (out_score) out_score[qi * k_out + r] = -INFINITY;
     if (out_score64) out_score64[qi * k_out + r] = -INFINITY;
+    if (out_pay)
+      for (int p = 0; p < P; ++p) out_pay[(qi * k_out + r) * P + p] = 0.0;
   }
 }
 
@@ -1907,15 +1916,17 @@ __device__ __forceinline__ double minmax_lane(double x, bool valid) {
   return (hi - lo == 0.0) ? 0.0 : (x - lo) / (hi - lo);
 }
 
-__global__ __launch_bounds__(64) void knn_rerank(
-    const float* __restrict__ qe, int d, const float* __restrict__ gal, int Dp,
-    const double* __restrict__ gnorm64, int64_t n, int64_t idx_base, const int64_t* __restrict__ cand,
-    int kc, const uint64_t* __restrict__ qlab, const uint64_t* __restrict__ glab,
-    const float* __restrict__ qkg, const float* __restrict__ gkg, int dk, double wa, double wb,
-    double wg, int topk, int64_t* __restrict__ out_idx, double* __restrict__ out_final,
-    double* __restrict__ out_emb, double* __restrict__ out_lab, double* __restrict__ out_kg) {
-  const int64_t qi = blockIdx.x;
-  const int lane = threadIdx.x;
+// The three raw components of candidate `lane` of query qi (lane < kc): e = emb cosine, lab =
+// label Jaccard, kg = KG cosine; my = its local row (-1: empty or not in this index).  One wave.
+struct RerankRaw {
+  double e, lab, kg;
+  int64_t my;
+};
+__device__ RerankRaw rerank_raw(const float* __restrict__ qe, int d, const float* __restrict__ gal, int Dp,
+                                const double* __restrict__ gnorm64, int64_t n, int64_t idx_base,
+                                const int64_t* __restrict__ cand, int kc, const uint64_t* __restrict__ qlab,
+                                const uint64_t* __restrict__ glab, const float* __restrict__ qkg,
+                                const float* __restrict__ gkg, int dk, int64_t qi, int lane) {
   const int64_t* cq = cand + qi * kc;
   const float* qr = qe + qi * (int64_t)d;
   const float* qk = qkg + qi * (int64_t)dk;
@@ -1923,8 +1934,7 @@ __global__ __launch_bounds__(64) void knn_rerank(
   for (int t = lane; t < d; t += 64) qq += (double)qr[t] * (double)qr[t];
   for (int t = lane; t < dk; t += 64) kk += (double)qk[t] * (double)qk[t];
   const double qn = sqrt(mmr::wave_sum(qq)), qkn = sqrt(mmr::wave_sum(kk));
-  double e = 0.0, kgs = 0.0;
-  int64_t my = -1;
+  RerankRaw r = {0.0, 0.0, 0.0, -1};
   for (int c = 0; c < kc; ++c) {  // wave-cooperative dot products, candidate c lands on lane c
     const int64_t g = cq[c] - idx_base;
     const bool ok = cq[c] >= 0 && g >= 0 && g < n;
@@ -1942,20 +1952,26 @@ __global__ __launch_bounds__(64) void knn_rerank(
     dkg = mmr::wave_sum(dkg);
     gk = mmr::wave_sum(gk);
     if (lane == c && ok) {
-      my = g;
+      r.my = g;
       const double gn = gnorm64[g];
-      e = (qn > 0.0 && gn > 0.0) ? de / (qn * gn) : 0.0;
+      r.e = (qn > 0.0 && gn > 0.0) ? de / (qn * gn) : 0.0;
       const double gkn = sqrt(gk);
-      kgs = (qkn > 0.0 && gkn > 0.0) ? dkg / (qkn * gkn) : 0.0;
+      r.kg = (qkn > 0.0 && gkn > 0.0) ? dkg / (qkn * gkn) : 0.0;
     }
   }
-  const bool valid = lane < kc && my >= 0;
-  double lab = 0.0;
-  if (valid) {
-    const uint64_t a = qlab[qi], b = glab[my];
+  if (lane < kc && r.my >= 0) {
+    const uint64_t a = qlab[qi], b = glab[r.my];
     const int u = __popcll(a | b);
-    lab = u == 0 ? 0.0 : (double)__popcll(a & b) / (double)u;
+    r.lab = u == 0 ? 0.0 : (double)__popcll(a & b) / (double)u;
   }
+  return r;
+}
+
+// min-max over the valid lanes, mix, rank (final desc, equal finals: later candidate first), write
+__device__ void rerank_mix_out(double e, double lab, double kgs, bool valid, int64_t gidx, double wa, double wb,
+                               double wg, int topk, int64_t qi, int lane, int64_t* __restrict__ out_idx,
+                               double* __restrict__ out_final, double* __restrict__ out_emb,
+                               double* __restrict__ out_lab, double* __restrict__ out_kg) {
   const double en = minmax_lane(e, valid), ln = minmax_lane(lab, valid), kn = minmax_lane(kgs, valid);
   const double f = wa * en + wb * ln + wg * kn;
   int rank = 0;
@@ -1966,7 +1982,7 @@ __global__ __launch_bounds__(64) void knn_rerank(
   }
   if (valid && rank < topk) {
     const int64_t o = qi * topk + rank;
-    out_idx[o] = my + idx_base;
+    out_idx[o] = gidx;
     if (out_final) out_final[o] = f;
     if (out_emb) out_emb[o] = en;
     if (out_lab) out_lab[o] = ln;
@@ -1975,6 +1991,53 @@ __global__ __launch_bounds__(64) void knn_rerank(
   int nvalid = 0;
   for (int j = 0; j < 64; ++j) nvalid += __shfl((int)valid, j, 64);
   for (int r = nvalid + lane; r < topk; r += 64) out_idx[qi * topk + r] = -1;
+}
+
+__global__ __launch_bounds__(64) void knn_rerank(
+    const float* __restrict__ qe, int d, const float* __restrict__ gal, int Dp,
+    const double* __restrict__ gnorm64, int64_t n, int64_t idx_base, const int64_t* __restrict__ cand,
+    int kc, const uint64_t* __restrict__ qlab, const uint64_t* __restrict__ glab,
+    const float* __restrict__ qkg, const float* __restrict__ gkg, int dk, double wa, double wb,
+    double wg, int topk, int64_t* __restrict__ out_idx, double* __restrict__ out_final,
+    double* __restrict__ out_emb, double* __restrict__ out_lab, double* __restrict__ out_kg) {
+  const int64_t qi = blockIdx.x;
+  const int lane = threadIdx.x;
+  const RerankRaw r = rerank_raw(qe, d, gal, Dp, gnorm64, n, idx_base, cand, kc, qlab, glab, qkg, gkg, dk, qi, lane);
+  rerank_mix_out(r.e, r.lab, r.kg, lane < kc && r.my >= 0, r.my + idx_base, wa, wb, wg, topk, qi, lane, out_idx,
+                 out_final, out_emb, out_lab, out_kg);
+}
+
+// Sharded rerank, shard side: the raw components of this shard's candidates -> comp [nq][kc][3]
+// (zeros for an empty slot).
+__global__ __launch_bounds__(64) void knn_rerank_comp(
+    const float* __restrict__ qe, int d, const float* __restrict__ gal, int Dp,
+    const double* __restrict__ gnorm64, int64_t n, int64_t idx_base, const int64_t* __restrict__ cand,
+    int kc, const uint64_t* __restrict__ qlab, const uint64_t* __restrict__ glab,
+    const float* __restrict__ qkg, const float* __restrict__ gkg, int dk, double* __restrict__ comp) {
+  const int64_t qi = blockIdx.x;
+  const int lane = threadIdx.x;
+  const RerankRaw r = rerank_raw(qe, d, gal, Dp, gnorm64, n, idx_base, cand, kc, qlab, glab, qkg, gkg, dk, qi, lane);
+  if (lane < kc) {
+    double* o = comp + (qi * kc + lane) * 3;
+    o[0] = r.e;
+    o[1] = r.lab;
+    o[2] = r.kg;
+  }
+}
+
+// Sharded rerank, after the merge: cand (global indices, -1 empty) + their merged components.
+__global__ __launch_bounds__(64) void knn_rerank_mix(const int64_t* __restrict__ cand, const double* __restrict__ comp,
+                                                     int kc, double wa, double wb, double wg, int topk,
+                                                     int64_t* __restrict__ out_idx, double* __restrict__ out_final,
+                                                     double* __restrict__ out_emb, double* __restrict__ out_lab,
+                                                     double* __restrict__ out_kg) {
+  const int64_t qi = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int64_t g = lane < kc ? cand[qi * kc + lane] : -1;
+  const bool valid = g >= 0;
+  const double* c = comp + (qi * kc + (lane < kc ? lane : 0)) * 3;
+  rerank_mix_out(valid ? c[0] : 0.0, valid ? c[1] : 0.0, valid ? c[2] : 0.0, valid, g, wa, wb, wg, topk, qi, lane,
+                 out_idx, out_final, out_emb, out_lab, out_kg);
 }
 
 }  // namespace
@@ -2161,6 +2224,54 @@ void launch_select(hipStream_t st, int64_t nq, const float* vals, int64_t ldV, i
 #undef MMR_SEL
 }
 
+// Mode-specific scan copies, built when a mode first needs them (mmr_index_set_mode / the first
+// search): x3 = the bf16 hi/lo split [Np][2Dp] + the tile16 f32 copy of the skinny scan (12 B per
+// element); f16 = the tile32h fp16 unit rows + (Dp % 128 == 0, Dp <= 1024) the row-major fp16 copy
+// of the p8 scan (4 B per element).  A switch to f16 / f32 frees the x3 copies (an fp16 gallery
+// index holds f32 rows + fp16 copies only); a switch away from f16 frees the fp16 copies.
+mmr_status build_x3_copies(mmr_index* ix) {
+  if (ix->gs != nullptr && ix->gt != nullptr) return MMR_OK;
+  DeviceGuard g(ix->device);
+  hipError_t e;
+  if ((ix->gs == nullptr && (e = hipMalloc(&ix->gs, sizeof(uint16_t) * ix->Np * 2 * ix->Dp)) != hipSuccess) ||
+      (ix->gt == nullptr && (e = hipMalloc(&ix->gt, sizeof(float) * ix->Np * ix->Dp)) != hipSuccess)) {
+    mmr::set_error("mmr_index: hipMalloc(x3 scan copies) failed: %s", hipGetErrorString(e));
+    return MMR_ERR_OOM;
+  }
+  const int64_t total = ix->Np * ix->Dp;
+  knn_split_gallery<<<dim3((unsigned)ceil_div(total, 256)), dim3(256)>>>(ix->gal, ix->Dp, total, ix->gs);
+  e = hipGetLastError();
+  if (e == hipSuccess) {
+    const int64_t total4 = total / 4;
+    knn_tile_gallery<<<dim3((unsigned)ceil_div(total4, 256)), dim3(256)>>>(ix->gal, ix->Dp, total4, ix->gt);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    mmr::set_error("mmr_index: x3 scan copy kernels failed: %s", hipGetErrorString(e));
+    return MMR_ERR_HIP;
+  }
+  return MMR_OK;
+}
+
+void free_copies(mmr_index* ix, bool x3, bool f16) {
+  DeviceGuard g(ix->device);
+  if (x3 || f16) (void)hipDeviceSynchronize();  // no search still reads them
+  if (x3) {
+    if (ix->gs) (void)hipFree(ix->gs);
+    if (ix->gt) (void)hipFree(ix->gt);
+    ix->gs = nullptr;
+    ix->gt = nullptr;
+  }
+  if (f16) {
+    if (ix->gh) (void)hipFree(ix->gh);
+    if (ix->ghr) (void)hipFree(ix->ghr);
+    ix->gh = nullptr;
+    ix->ghr = nullptr;
+    ix->Np256 = 0;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -2205,9 +2316,7 @@ mmr_status mmr_index_create(const void* gallery, int64_t n, int32_t d, mmr_dtype
   }
   if ((e = hipMalloc(&ix->gal, sizeof(float) * ix->Np * ix->Dp)) != hipSuccess ||
       (e = hipMalloc(&ix->inv_norm, sizeof(float) * ix->Np)) != hipSuccess ||
-      (e = hipMalloc(&ix->norm64, sizeof(double) * ix->Np)) != hipSuccess ||
-      (e = hipMalloc(&ix->gs, sizeof(uint16_t) * ix->Np * 2 * ix->Dp)) != hipSuccess ||
-      (e = hipMalloc(&ix->gt, sizeof(float) * ix->Np * ix->Dp)) != hipSuccess) {
+      (e = hipMalloc(&ix->norm64, sizeof(double) * ix->Np)) != hipSuccess) {
     mmr::set_error("mmr_index_create: hipMalloc failed: %s", hipGetErrorString(e));
     return fail(MMR_ERR_OOM);
   }
@@ -2229,16 +2338,6 @@ mmr_status mmr_index_create(const void* gallery, int64_t n, int32_t d, mmr_dtype
   knn_prep_gallery<<<dim3((unsigned)ceil_div(ix->Np, 4)), dim3(256)>>>(
       raw, n, d, ix->gal, ix->Dp, ix->Np, ix->inv_norm, ix->norm64);
   e = hipGetLastError();
-  if (e == hipSuccess) {
-    const int64_t total = ix->Np * ix->Dp;
-    knn_split_gallery<<<dim3((unsigned)ceil_div(total, 256)), dim3(256)>>>(ix->gal, ix->Dp, total, ix->gs);
-    e = hipGetLastError();
-  }
-  if (e == hipSuccess) {
-    const int64_t total4 = ix->Np * ix->Dp / 4;
-    knn_tile_gallery<<<dim3((unsigned)ceil_div(total4, 256)), dim3(256)>>>(ix->gal, ix->Dp, total4, ix->gt);
-    e = hipGetLastError();
-  }
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (raw) (void)hipFree(raw);
   if (e != hipSuccess) {
@@ -2266,6 +2365,21 @@ mmr_status mmr_index_destroy(mmr_index* ix) {
   if (ix->bvals) (void)hipFree(ix->bvals);
   if (ix->ws_event) (void)hipEventDestroy(ix->ws_event);
   delete ix;
+  return MMR_OK;
+}
+
+mmr_status mmr_index_device_bytes(const mmr_index* ix, int64_t* gallery_bytes, int64_t* workspace_bytes) {
+  mmr::clear_error();
+  MMR_REQUIRE(ix != nullptr, "mmr_index_device_bytes: index is NULL");
+  const int64_t e = ix->Np * ix->Dp;
+  int64_t gb = e * 4 + ix->Np * (4 + 8);
+  if (ix->gs) gb += e * 2 * 2;
+  if (ix->gt) gb += e * 4;
+  if (ix->gh) gb += e * 2;
+  if (ix->ghr) gb += ix->Np256 * ix->Dp * 2;
+  const int64_t wb = ix->ws_qrows * (ix->Dp * 4 + 8) + ix->ws_vals * 4 + ix->ws_bvals * 4 + ix->ws_qsrows * 3 * ix->Dp * 2;
+  if (gallery_bytes) *gallery_bytes = gb;
+  if (workspace_bytes) *workspace_bytes = wb;
   return MMR_OK;
 }
 
@@ -2305,6 +2419,7 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
   }
   mmr_status s = ensure_ws(ix, nq);
   if (s != MMR_OK) return s;
+  if (ix->mode == 1 && (s = build_x3_copies(ix)) != MMR_OK) return s;  // default mode, first search
   // |s_approx - s64| <= delta; threshold margin 2*delta.
   //  f32 (knn_scores, knn_scan_f32_gmax): (Dp + 16) 2^-24 — f32 products accumulated in f32 over Dp
   //      terms of a unit query against g/|g| (|sum| <= 1), plus the normalisations;
@@ -2579,6 +2694,12 @@ mmr_status mmr_index_set_mode(mmr_index* ix, int32_t mode) {
   mmr::clear_error();
   MMR_REQUIRE(ix != nullptr && mode >= 0 && mode <= 2, "mmr_index_set_mode: bad arguments");
   std::lock_guard<std::mutex> lk(ix->mu);
+  if (mode == ix->mode && (mode != 1 || ix->gs != nullptr) && (mode != 2 || ix->gh != nullptr)) return MMR_OK;
+  free_copies(ix, mode != 1, mode != 2);
+  if (mode == 1) {
+    mmr_status s = build_x3_copies(ix);
+    if (s != MMR_OK) return s;
+  }
   if (mode == 2 && ix->gh == nullptr) {
     DeviceGuard g(ix->device);
     hipError_t e = hipMalloc(&ix->gh, sizeof(uint16_t) * ix->Np * ix->Dp);
@@ -2625,14 +2746,60 @@ mmr_status mmr_index_set_mode(mmr_index* ix, int32_t mode) {
 mmr_status mmr_merge_topk(const double* scores, const int64_t* idx, int32_t n_lists, int64_t nq,
                           int32_t k_in, int32_t k_out, int64_t* out_idx, float* out_score,
                           double* out_score64, void* stream) {
+  return mmr_merge_topk_payload(scores, idx, nullptr, 0, n_lists, nq, 0, nq, k_in, k_out, out_idx, out_score,
+                                out_score64, nullptr, stream);
+}
+
+mmr_status mmr_merge_topk_payload(const double* scores, const int64_t* idx, const double* payload,
+                                  int32_t payload_width, int32_t n_lists, int64_t nq_total, int64_t q0, int64_t nq,
+                                  int32_t k_in, int32_t k_out, int64_t* out_idx, float* out_score,
+                                  double* out_score64, double* out_payload, void* stream) {
   mmr::clear_error();
-  MMR_REQUIRE(n_lists >= 1 && k_in >= 1 && k_out >= 1 && nq >= 0, "mmr_merge_topk: bad sizes");
+  MMR_REQUIRE(n_lists >= 1 && k_in >= 1 && k_out >= 1 && nq >= 0 && q0 >= 0 && q0 + nq <= nq_total,
+              "mmr_merge_topk: bad sizes");
   MMR_REQUIRE((int64_t)n_lists * k_in <= 4096, "mmr_merge_topk: n_lists*k_in > 4096");
+  MMR_REQUIRE(payload_width >= 0 && payload_width <= 16 && ((payload == nullptr) == (out_payload == nullptr)) &&
+                  (payload == nullptr || payload_width > 0),
+              "mmr_merge_topk_payload: payload / out_payload / width disagree");
   if (nq == 0) return MMR_OK;
   MMR_REQUIRE(scores && idx && out_idx, "mmr_merge_topk: NULL pointer");
   const size_t lds = (sizeof(double) + sizeof(int64_t)) * (size_t)n_lists * k_in;
   knn_merge<<<dim3((unsigned)nq), dim3(256), lds, mmr::as_stream(stream)>>>(
-      scores, idx, n_lists, nq, k_in, k_out, out_idx, out_score, out_score64);
+      scores, idx, n_lists, nq_total, q0, k_in, k_out, out_idx, out_score, out_score64, payload, payload_width,
+      out_payload);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_index_rerank_components(const mmr_index* ix, const float* q_emb, int64_t nq, const int64_t* cand,
+                                       int32_t kc, const uint64_t* q_labels, const uint64_t* g_labels,
+                                       const float* q_kg, const float* g_kg, int32_t dk, double* out_comp,
+                                       void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(ix != nullptr, "mmr_index_rerank_components: index is NULL");
+  MMR_REQUIRE(kc >= 1 && kc <= 64 && dk >= 1 && nq >= 0, "mmr_index_rerank_components: kc=%d (1..64), dk=%d", kc,
+              dk);
+  if (nq == 0) return MMR_OK;
+  MMR_REQUIRE(q_emb && cand && q_labels && g_labels && q_kg && g_kg && out_comp,
+              "mmr_index_rerank_components: NULL pointer");
+  DeviceGuard g(ix->device);
+  knn_rerank_comp<<<dim3((unsigned)nq), dim3(64), 0, mmr::as_stream(stream)>>>(
+      q_emb, ix->d, ix->gal, ix->Dp, ix->norm64, ix->n, ix->idx_base, cand, kc, q_labels, g_labels, q_kg, g_kg, dk,
+      out_comp);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_rerank_mix(const int64_t* cand, const double* comp, int64_t nq, int32_t kc, double alpha,
+                          double beta, double gamma, int32_t topk, int64_t* out_idx, double* out_final,
+                          double* out_emb, double* out_lab, double* out_kg, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(kc >= 1 && kc <= 64 && topk >= 1 && topk <= kc && nq >= 0, "mmr_rerank_mix: kc=%d (1..64), topk=%d",
+              kc, topk);
+  if (nq == 0) return MMR_OK;
+  MMR_REQUIRE(cand && comp && out_idx, "mmr_rerank_mix: NULL pointer");
+  knn_rerank_mix<<<dim3((unsigned)nq), dim3(64), 0, mmr::as_stream(stream)>>>(
+      cand, comp, kc, alpha, beta, gamma, topk, out_idx, out_final, out_emb, out_lab, out_kg);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }

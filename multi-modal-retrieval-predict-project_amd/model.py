@@ -17,41 +17,164 @@ MultiModalRetrievalModel.forward(...) -> {"joint_emb", "img_emb", "txt_emb", "lo
     (model.py:375-459) on libmmr kernels (mmr_amd/fusion.py); the classifier (logits) is
     classification, out of scope -> None; attention maps (return_attention) are not produced.
 """
+import json
 import os
+from pathlib import Path
 
 import torch
 
 from . import ops
 from .fusion import FusionStack
-from .towers import BERT_BASE, SWIN_T, BertTower, SwinTower, init_bert_state, init_swin_state
+from .towers import BERT_BASE, SWIN_T, SWIN_ARCHS, BertTower, SwinTower, init_bert_state, init_swin_state
 
 
 def _sub(sd, prefix):
     return {k[len(prefix):]: v for k, v in sd.items() if k.startswith(prefix)}
 
 
+def _load_tensors(path):
+    """A weights file as a state dict, executing nothing from it: .safetensors via safetensors,
+    anything else via torch.load(..., weights_only=True) (a dict, or {"state_dict" / "model": dict})."""
+    path = str(path)
+    if path.endswith(".safetensors"):
+        from safetensors.torch import load_file
+        return load_file(path, device="cpu")
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    for key in ("state_dict", "model"):
+        if isinstance(sd, dict) and key in sd and isinstance(sd[key], dict):
+            sd = sd[key]
+    return sd
+
+
+def swin_cfg_from_state(sd, base=None):
+    """timm Swin geometry read off a timm-keyed state dict (embed dim, depths, heads per stage,
+    window), so a checkpoint of any Swin size builds the matching tower."""
+    cfg = dict(base or SWIN_T)
+    if "patch_embed.proj.weight" not in sd:
+        return cfg
+    cfg["embed_dim"] = int(sd["patch_embed.proj.weight"].shape[0])
+    depths, heads = [], []
+    i = 0
+    while any(k.startswith(f"layers.{i}.") for k in sd):
+        j = 0
+        while f"layers.{i}.blocks.{j}.norm1.weight" in sd:
+            j += 1
+        depths.append(j)
+        heads.append(int(sd[f"layers.{i}.blocks.0.attn.relative_position_bias_table"].shape[1]))
+        i += 1
+    if depths:
+        cfg["depths"], cfg["num_heads"] = depths, heads
+        t = int(sd["layers.0.blocks.0.attn.relative_position_bias_table"].shape[0])
+        cfg["window_size"] = (int(round(t ** 0.5)) + 1) // 2
+    return cfg
+
+
+def bert_cfg_from_state(sd, user=None):
+    """BERT geometry read off an HF BertModel state dict (user keys override nothing the weights
+    fix); heads are not visible in the weights: the user's / config.json's num_attention_heads,
+    else hidden / 64 (every BERT-family checkpoint of the reference; Bio_ClinicalBERT: 12)."""
+    user = dict(user or {})
+    cfg = dict(BERT_BASE, **user)
+    if "embeddings.word_embeddings.weight" not in sd:
+        return cfg
+    v, h = sd["embeddings.word_embeddings.weight"].shape
+    n = 0
+    while f"encoder.layer.{n}.attention.self.query.weight" in sd:
+        n += 1
+    cfg.update(vocab_size=int(v), hidden_size=int(h), num_hidden_layers=n,
+               intermediate_size=int(sd["encoder.layer.0.intermediate.dense.weight"].shape[0]),
+               max_position_embeddings=int(sd["embeddings.position_embeddings.weight"].shape[0]),
+               type_vocab_size=int(sd["embeddings.token_type_embeddings.weight"].shape[0]))
+    cfg["num_attention_heads"] = int(user.get("num_attention_heads", max(1, int(h) // 64)))
+    return cfg
+
+
+def load_bert_dir(local_dir):
+    """Helpers/model_utils.py:11-55 local branch (AutoModel.from_pretrained(local_dir)) without
+    transformers: config.json for the geometry + model.safetensors / pytorch_model.bin weights
+    (a "bert." prefix of BertFor* checkpoints is stripped).  Nothing is downloaded."""
+    d = Path(local_dir)
+    cfg = {}
+    if (d / "config.json").exists():
+        c = json.loads((d / "config.json").read_text())
+        cfg = {k: c[k] for k in ("vocab_size", "hidden_size", "num_hidden_layers", "num_attention_heads",
+                                 "intermediate_size", "max_position_embeddings", "type_vocab_size") if k in c}
+    for name in ("model.safetensors", "pytorch_model.bin"):
+        if (d / name).exists():
+            sd = _load_tensors(d / name)
+            if any(k.startswith("bert.") for k in sd):
+                sd = _sub(sd, "bert.")
+            return sd, cfg
+    raise FileNotFoundError(f"no model.safetensors / pytorch_model.bin in {d}")
+
+
 class Backbones:
-    def __init__(self, img_backbone="swin", swin_state=None, bert_state=None, swin_cfg=None, bert_cfg=None,
-                 device="cuda", pretrained=False, seed=2709, tower_dtype="bf16"):
-        """tower_dtype "bf16" (config 2) or "fp8" (config 5: MX-fp8 linears in all BERT layers and
-        Swin stages 3-4)."""
+    """src/Model/fusion.py:37-332 Backbones (Swin + ClinicalBERT branches) on libmmr kernels.
+
+    Reference arguments (fusion.py:42-53), same names and order: img_backbone ('swin' only — the
+    CNN / MedCLIP branches are outside the accelerated path), swin_model_name (a timm Swin name:
+    its geometry, SWIN_ARCHS), cnn_model_name (accepted, unused), bert_model_name,
+    swin_checkpoint_path (timm-keyed weights, .safetensors or a torch state dict), bert_local_dir
+    (an HF save_pretrained directory, Helpers/model_utils.py:11-55), pretrained, img_dim, txt_dim.
+    There is no hub access: pretrained=True needs swin_checkpoint_path / bert_local_dir (or the
+    explicit states below); pretrained=False builds seeded random weights (the benchmark).
+    The reference collapses patch_embed.proj.weight to one input channel before loading
+    (fusion.py:92-96), which cannot load into its in_chans=3 model (it falls back to a download,
+    :101-107); here a 3-channel weight loads as is and a 1-channel weight w is expanded to w/3 per
+    channel (the same response on the grey-replicated inputs, tensorDICOM.py:150).
+    Extras (keyword-only): swin_state / bert_state (state dicts), swin_cfg / bert_cfg (geometry
+    overrides), device, seed, tower_dtype ("bf16" configs 1-4, "fp8" config 5: MX-fp8 linears in
+    every BERT layer and Swin stages 3-4)."""
+
+    def __init__(self, img_backbone="swin", swin_model_name="swin_base_patch4_window7_224", cnn_model_name="resnet50",
+                 bert_model_name="emilyalsentzer/Bio_ClinicalBERT", swin_checkpoint_path=None, bert_local_dir=None,
+                 pretrained=True, img_dim=None, txt_dim=None, *, swin_state=None, bert_state=None, swin_cfg=None,
+                 bert_cfg=None, device="cuda", seed=2709, tower_dtype="bf16"):
         if tower_dtype not in ("bf16", "fp8"):
             raise ValueError(f"tower_dtype {tower_dtype!r}: bf16 or fp8")
         self.tower_dtype = tower_dtype
         if img_backbone != "swin":
             raise ValueError(f"image backbone {img_backbone!r} is outside the accelerated path (swin only)")
         self.img_backbone = img_backbone
+        self.swin_model_name, self.bert_model_name = swin_model_name, bert_model_name
         self.device = torch.device(device)
-        swin_cfg = dict(SWIN_T, **(swin_cfg or {}))
-        bert_cfg = dict(BERT_BASE, **(bert_cfg or {}))
+        arch = SWIN_ARCHS.get(swin_model_name)
+        if swin_state is None and swin_checkpoint_path and (pretrained or not Path(str(swin_checkpoint_path)).exists()):
+            if not Path(str(swin_checkpoint_path)).exists():
+                raise FileNotFoundError(f"Swin checkpoint not found at {swin_checkpoint_path} (no hub access here)")
+            swin_state = _load_tensors(swin_checkpoint_path)
+        if swin_state is not None:
+            w = swin_state.get("patch_embed.proj.weight")
+            if w is not None and w.shape[1] == 1:
+                swin_state = dict(swin_state, **{"patch_embed.proj.weight": w.expand(-1, 3, -1, -1) / 3.0})
+            swin_cfg = dict(swin_cfg_from_state(swin_state, arch), **(swin_cfg or {}))
+        else:
+            if pretrained and swin_cfg is None:
+                raise ValueError(f"pretrained Swin {swin_model_name!r} needs swin_checkpoint_path (no hub access)")
+            if swin_cfg is None and arch is None:
+                raise ValueError(f"unknown Swin name {swin_model_name!r}: pass swin_cfg (known: {sorted(SWIN_ARCHS)})")
+            swin_cfg = dict(arch or SWIN_T, **(swin_cfg or {}))
+            swin_state = init_swin_state(swin_cfg, seed)
+        if bert_state is None and bert_local_dir:
+            bert_state, dir_cfg = load_bert_dir(bert_local_dir)
+            bert_cfg = dict(dir_cfg, **(bert_cfg or {}))
+        if bert_state is not None:
+            bert_cfg = bert_cfg_from_state(bert_state, bert_cfg)
+        else:
+            if pretrained and bert_cfg is None:
+                raise ValueError(f"pretrained {bert_model_name!r} needs bert_local_dir (no hub access)")
+            bert_cfg = dict(BERT_BASE, **(bert_cfg or {}))
+            bert_state = init_bert_state(bert_cfg, seed + 1)
         fp8 = tower_dtype == "fp8"
-        self.vision = SwinTower(swin_state if swin_state is not None else init_swin_state(swin_cfg, seed),
-                                swin_cfg, self.device, fp8_stages=(2, 3) if fp8 else ())
+        self.swin_cfg, self.bert_cfg = swin_cfg, bert_cfg
+        self.vision = SwinTower(swin_state, swin_cfg, self.device, fp8_stages=(2, 3) if fp8 else ())
         self.swin = self.vision
-        self.bert = BertTower(bert_state if bert_state is not None else init_bert_state(bert_cfg, seed + 1),
-                              bert_cfg, self.device, fp8=fp8)
-        self.img_dim = self.vision.num_features
-        self.txt_dim = self.bert.hidden
+        self.bert = BertTower(bert_state, bert_cfg, self.device, fp8=fp8)
+        self.img_dim = self.vision.num_features if img_dim is None else img_dim
+        self.txt_dim = self.bert.hidden if txt_dim is None else txt_dim
+        if self.img_dim != self.vision.num_features or self.txt_dim != self.bert.hidden:
+            raise ValueError(f"img_dim/txt_dim {self.img_dim}/{self.txt_dim} differ from the towers' "
+                             f"{self.vision.num_features}/{self.bert.hidden}")
 
     # fast path: bf16 hidden states + fused pooling, no f32 copies of the full token grids
     def encode_image(self, image, want_patches=True):
@@ -84,26 +207,71 @@ class Backbones:
 
 
 class MultiModalRetrievalModel:
-    def __init__(self, joint_dim=256, num_heads=4, model_type="multimodal", use_shared_ffn=False,
-                 use_cls_only=False, backbones=None, head_state=None, device="cuda", retriever=None,
-                 swin_cfg=None, bert_cfg=None, seed=2709, tower_dtype="bf16"):
+    """src/Model/model.py:114-328 MultiModalRetrievalModel (inference) on libmmr kernels.
+
+    Reference arguments (model.py:116-137), same names, order and defaults: joint_dim, num_heads,
+    num_classes (the classifier is classification, out of scope: accepted, logits None),
+    num_fusion_layers, fusion_type ("cross" only, as in the reference), img_backbone, swin_name,
+    cnn_name, bert_name, img_dim, txt_dim, swin_ckpt_path, bert_local_dir, pretrained,
+    checkpoint_path (a state dict of the whole reference model, loaded with torch.load(...,
+    weights_only=True) as model.py:282-287 loads it — tower and head weights; geometry read off
+    it), device (a GPU: there is no CPU path; default "cuda"), training (False: like the
+    reference, weights must come from checkpoint_path — or head_state / backbones below — else
+    ValueError, model.py:288-289), use_shared_ffn, use_cls_only, model_type, retriever (with
+    training=False and no retriever: a DLS engine over $MMR_EMBEDDINGS_DIR/val_joint_embeddings.npy
+    + val_ids.json when that directory is set, as model.py:294-312 does over EMBEDDINGS_DIR).
+    Extras (keyword-only): backbones (a built Backbones), head_state (head / fusion weights under
+    the reference's keys), swin_cfg / bert_cfg, seed, tower_dtype."""
+
+    def __init__(self, joint_dim=256, num_heads=4, num_classes=22, num_fusion_layers=3, fusion_type="cross",
+                 img_backbone="swin", swin_name="swin_base_patch4_window7_224", cnn_name="resnet50",
+                 bert_name="emilyalsentzer/Bio_ClinicalBERT", img_dim=None, txt_dim=None, swin_ckpt_path=None,
+                 bert_local_dir=None, pretrained=True, checkpoint_path=None, device="cuda", training=False,
+                 use_shared_ffn=True, use_cls_only=False, model_type="multimodal", retriever=None, *,
+                 backbones=None, head_state=None, swin_cfg=None, bert_cfg=None, seed=2709, tower_dtype="bf16"):
         if model_type not in ("multimodal", "image", "text"):
             raise ValueError(f"Unknown model_type {model_type!r}")
+        if fusion_type != "cross":
+            raise ValueError(f"Unknown fusion_type {fusion_type!r}")
         self.model_type = model_type
         self.device = torch.device(device)
-        self.backbones = backbones or Backbones(swin_cfg=swin_cfg, bert_cfg=bert_cfg, device=device, seed=seed,
-                                                tower_dtype=tower_dtype)
+        sd = None
+        if checkpoint_path:
+            sd = _load_tensors(checkpoint_path)
+            if any(k.startswith("module.") for k in sd):  # DataParallel-saved
+                sd = _sub(sd, "module.")
+        elif not training and head_state is None:
+            raise ValueError("checkpoint_path must be provided for inference")
+        if backbones is None:
+            if sd is not None:
+                backbones = Backbones(img_backbone, swin_name, cnn_name, bert_name, None, None, False, img_dim, txt_dim,
+                                      swin_state=_sub(sd, "backbones.vision."), bert_state=_sub(sd, "backbones.bert."),
+                                      swin_cfg=swin_cfg, bert_cfg=bert_cfg, device=device, seed=seed,
+                                      tower_dtype=tower_dtype)
+            else:
+                backbones = Backbones(img_backbone, swin_name, cnn_name, bert_name, swin_ckpt_path, bert_local_dir,
+                                      pretrained and (swin_ckpt_path is not None or bert_local_dir is not None),
+                                      img_dim, txt_dim, swin_cfg=swin_cfg, bert_cfg=bert_cfg, device=device, seed=seed,
+                                      tower_dtype=tower_dtype)
+        self.backbones = backbones
         self.joint_dim = joint_dim
+        self.num_classes = num_classes
         self.use_shared_ffn = use_shared_ffn
         self.use_cls_only = use_cls_only
         self.retriever = retriever
         self._side = None
         self._warm = False
-        hs = head_state if head_state is not None else init_head_state(self.backbones.img_dim,
-                                                                       self.backbones.txt_dim, joint_dim, seed + 2)
+        hs = head_state if head_state is not None else sd
+        if hs is None:  # training=True without a checkpoint: seeded random init (the reference's fresh model)
+            hs = init_head_state(self.backbones.img_dim, self.backbones.txt_dim, joint_dim, seed + 2)
+            if model_type == "multimodal":
+                hs.update(init_fusion_state(self.backbones.img_dim, self.backbones.txt_dim, joint_dim, num_heads,
+                                            num_fusion_layers, seed + 3, use_shared_ffn=use_shared_ffn))
         f = lambda k: hs[k].detach().to(self.device, torch.float32).contiguous()  # noqa: E731
         self.img_proj = (f("img_proj.weight"), f("img_proj.bias"))
         self.txt_proj = (f("txt_proj.weight"), f("txt_proj.bias"))
+        if self.img_proj[0].shape[0] != joint_dim:
+            raise ValueError(f"joint_dim {joint_dim} does not match the weights' {self.img_proj[0].shape[0]}")
         pre = "shared_ffn." if use_shared_ffn else "ffn.0."
         self.ffn = (f(pre + "linear1.weight"), f(pre + "linear1.bias"), f(pre + "linear2.weight"), f(pre + "linear2.bias"))
         self.num_heads = num_heads
@@ -113,17 +281,29 @@ class MultiModalRetrievalModel:
                 raise ValueError("model_type='multimodal' with use_cls_only fails in the reference (model.py:428)")
             if not any(k.startswith("fusion_layers.") for k in hs):
                 raise ValueError("head_state has no fusion_layers.* weights for model_type='multimodal'")
+            nfl = len({k.split(".")[1] for k in hs if k.startswith("fusion_layers.")})
+            if nfl != num_fusion_layers and (checkpoint_path or head_state is not None):
+                num_fusion_layers = nfl  # the weights decide (a checkpoint of another depth)
             self.fusion = FusionStack(hs, num_heads, device=self.device, use_shared_ffn=use_shared_ffn)
+        self.num_fusion_layers = num_fusion_layers
+        if self.retriever is None and not training and os.environ.get("MMR_EMBEDDINGS_DIR"):
+            from .retrieval import make_retrieval_engine
+            d = Path(os.environ["MMR_EMBEDDINGS_DIR"])
+            fp, ip = d / "val_joint_embeddings.npy", d / "val_ids.json"
+            if not fp.exists() or not ip.exists():
+                raise FileNotFoundError(f"Expected embeddings at {fp} and IDs at {ip}")
+            self.retriever = make_retrieval_engine(str(fp), str(ip), method="dls", link_threshold=0.5, max_links=10)
 
     @classmethod
-    def from_reference_state_dict(cls, sd, swin_cfg, bert_cfg, joint_dim, model_type="text", device="cuda",
-                                  use_shared_ffn=False, num_heads=4):
-        """Build from a reference checkpoint state dict (model.py:282-287 layout)."""
+    def from_reference_state_dict(cls, sd, swin_cfg=None, bert_cfg=None, joint_dim=None, model_type="text",
+                                  device="cuda", use_shared_ffn=False, num_heads=4, tower_dtype="bf16"):
+        """Build from a reference model state dict (the model.py:282-287 layout) already in memory."""
         vis = _sub(sd, "backbones.vision.")
-        bb = Backbones(swin_state=vis, bert_state=_sub(sd, "backbones.bert."), swin_cfg=swin_cfg,
-                       bert_cfg=bert_cfg, device=device)
-        return cls(joint_dim=joint_dim, num_heads=num_heads, model_type=model_type, backbones=bb, head_state=sd,
-                   device=device, use_shared_ffn=use_shared_ffn)
+        bb = Backbones(pretrained=False, swin_state=vis, bert_state=_sub(sd, "backbones.bert."), swin_cfg=swin_cfg,
+                       bert_cfg=bert_cfg, device=device, tower_dtype=tower_dtype)
+        jd = joint_dim or int(sd["img_proj.weight"].shape[0])
+        return cls(joint_dim=jd, num_heads=num_heads, model_type=model_type, backbones=bb, head_state=sd,
+                   device=device, use_shared_ffn=use_shared_ffn, training=True)
 
     def set_retriever(self, retriever):
         self.retriever = retriever
@@ -279,5 +459,8 @@ def build_bench_model(device="cuda", joint_dim=768, seed=2709, model_type="multi
     hs = init_head_state(768, 768, joint_dim, seed + 2)
     if model_type == "multimodal":
         hs.update(init_fusion_state(768, 768, joint_dim, num_heads, num_fusion_layers, seed + 3))
-    return MultiModalRetrievalModel(joint_dim=joint_dim, num_heads=num_heads, model_type=model_type,
-                                    head_state=hs, device=device, seed=seed, tower_dtype=tower_dtype)
+    bb = Backbones("swin", "swin_tiny_patch4_window7_224", pretrained=False, device=device, seed=seed,
+                   tower_dtype=tower_dtype)
+    return MultiModalRetrievalModel(joint_dim=joint_dim, num_heads=num_heads, num_fusion_layers=num_fusion_layers,
+                                    model_type=model_type, backbones=bb, head_state=hs, device=device, seed=seed,
+                                    use_shared_ffn=False, training=True, tower_dtype=tower_dtype)

@@ -9,12 +9,18 @@ Each rank owns rows [start_r, end_r) of the gallery (balanced split).  A search:
      bound (30 KB at Q=256, K=10): one collective per query batch, no data-path exchange,
   4. deterministic k-way merge: score desc, then global index asc — so the sharded result is
      bit-identical to the single-device result (ranking on the same f64 scores).
+Sharded rerank (BASELINE config 5's KG-rerank head at world > 1; Reranker.rerank,
+src/Retrieval/reranker.py:240-333, min-max scales each component over the FINAL candidate list, so
+it must run after the merge): each shard computes its candidates' raw {emb cosine, label Jaccard, KG
+cosine} where the rows and tables live (mmr_index_rerank_components), the components ride with the
+(score, index) lists through the same all-gather and the merge (mmr_merge_topk_payload), and the
+min-max / mix / rank runs on the merged list (mmr_rerank_mix) — bit-identical to one index.
 """
 import numpy as np
 import torch
 import torch.distributed as dist
 
-from .retrieval import GalleryIndex, RetrievalEngine, check_status, merge_topk
+from .retrieval import GalleryIndex, RetrievalEngine, check_status, merge_topk, rerank_mix
 
 
 def shard_bounds(n, world):
@@ -28,26 +34,65 @@ def shard_bounds(n, world):
     return out
 
 
-def merge_topk_host(scores64, idx, k_out):
-    """Same merge as the HIP kernel (mmr_merge_topk) for host-resident lists [L][B][k_in]
-    (a CPU coordinator, or the gloo test path): score desc, index asc, idx -1 = empty."""
+def merge_topk_host(scores64, idx, k_out, payload=None):
+    """Same merge as the HIP kernel (mmr_merge_topk[_payload]) for host-resident lists [L][B][k_in]
+    (a CPU coordinator, or the gloo test path): score desc, index asc, idx -1 = empty; payload
+    [L][B][k_in][P] rides with each entry (4th output (B, k_out, P), zeros for empty slots)."""
     L_, B, k_in = idx.shape
+    src = torch.arange(L_ * k_in).view(1, -1).expand(B, -1)
     s = scores64.permute(1, 0, 2).reshape(B, L_ * k_in).to(torch.float64)
     i = idx.permute(1, 0, 2).reshape(B, L_ * k_in).to(torch.int64)
     valid = i >= 0
     s = torch.where(valid, s, torch.full_like(s, -float("inf")))
     ikey = torch.where(valid, i, torch.full_like(i, torch.iinfo(torch.int64).max))
     o1 = torch.argsort(ikey, dim=1, stable=True)
-    s1, i1 = torch.gather(s, 1, o1), torch.gather(ikey, 1, o1)
+    s1, i1, src1 = torch.gather(s, 1, o1), torch.gather(ikey, 1, o1), torch.gather(src, 1, o1)
     o2 = torch.argsort(s1, dim=1, descending=True, stable=True)
     s2, i2 = torch.gather(s1, 1, o2)[:, :k_out], torch.gather(i1, 1, o2)[:, :k_out]
+    src2 = torch.gather(src1, 1, o2)[:, :k_out]
     bad = i2 == torch.iinfo(torch.int64).max
     i2 = torch.where(bad, torch.full_like(i2, -1), i2)
     if s2.shape[1] < k_out:  # fewer candidates than k_out in total
         pad = k_out - s2.shape[1]
         s2 = torch.cat([s2, torch.full((B, pad), -float("inf"), dtype=s2.dtype)], 1)
         i2 = torch.cat([i2, torch.full((B, pad), -1, dtype=i2.dtype)], 1)
-    return i2, s2.to(torch.float32), s2
+        src2 = torch.cat([src2, torch.zeros((B, pad), dtype=src2.dtype)], 1)
+    if payload is None:
+        return i2, s2.to(torch.float32), s2
+    P = payload.shape[-1]
+    pf = payload.permute(1, 0, 2, 3).reshape(B, L_ * k_in, P).to(torch.float64)
+    pay = torch.gather(pf, 1, src2.unsqueeze(-1).expand(-1, -1, P))
+    pay = torch.where((i2 >= 0).unsqueeze(-1), pay, torch.zeros_like(pay))
+    return i2, s2.to(torch.float32), s2, pay
+
+
+def rerank_mix_host(cand, comp, topk, alpha=0.6, beta=0.25, gamma=0.15):
+    """Host form of mmr_rerank_mix (the gloo / CPU-coordinator path): per query, min-max scale each
+    raw component over the valid candidates (constant -> 0, reranker.py:151-159), final =
+    alpha e + beta l + gamma k, rank by final desc with equal finals -> later candidate first
+    (np.argsort(final)[::-1]); -> (idx (nq, topk) int64, -1 padded; final, emb_n, lab_n, kg_n f64)."""
+    cand = cand.to(torch.int64)
+    comp = comp.to(torch.float64)
+    nq, kc = cand.shape
+    out = [torch.full((nq, topk), -1, dtype=torch.int64)] + [torch.zeros((nq, topk), dtype=torch.float64)
+                                                            for _ in range(4)]
+    for qi in range(nq):
+        valid = [c for c in range(kc) if int(cand[qi, c]) >= 0]
+        if not valid:
+            continue
+        scaled = []
+        for p in range(3):
+            x = [float(comp[qi, c, p]) for c in valid]
+            lo, hi = min(x), max(x)
+            scaled.append([0.0 if hi - lo == 0 else (v - lo) / (hi - lo) for v in x])
+        fin = [alpha * scaled[0][j] + beta * scaled[1][j] + gamma * scaled[2][j] for j in range(len(valid))]
+        order = sorted(range(len(valid)), key=lambda j: (-fin[j], -j))[:topk]
+        for r, j in enumerate(order):
+            out[0][qi, r] = cand[qi, valid[j]]
+            out[1][qi, r] = fin[j]
+            for p in range(3):
+                out[2 + p][qi, r] = scaled[p][j]
+    return tuple(out)
 
 
 class ShardedIndex:
@@ -61,7 +106,7 @@ class ShardedIndex:
     exact list."""
 
     def __init__(self, gallery_rows, n_total, start, group=None, device=None, local_search=None, mode="x3",
-                 fallback_search=None):
+                 fallback_search=None, local_components=None):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -74,6 +119,7 @@ class ShardedIndex:
                 fallback_search = self._index_search_x3
         self.local_search = local_search
         self.fallback_search = fallback_search
+        self.local_components = local_components  # (q, cand) -> (nq, kc, 3) raw rerank components
         self.reruns = 0  # queries re-run through fallback_search (diagnostic)
 
     def _index_search(self, q, k):
@@ -81,21 +127,19 @@ class ShardedIndex:
         return i, s64, st
 
     def _index_search_x3(self, q, k):
-        mode = self.index.mode
-        self.index.set_mode("x3")
-        try:
-            i, _, s64, st = self.index.search(q, k, want_f64=True, want_status=True)
-        finally:
-            self.index.set_mode(mode)
+        # per-call mode override: the switch and the search hold the index's lock together
+        i, _, s64, st = self.index.search(q, k, want_f64=True, want_status=True, mode="x3")
         check_status(st)
         return i, s64
 
     @classmethod
     def from_full(cls, gallery, group=None, device=None, local_search=None, mode="x3", fallback_search=None):
+        """gallery may be a memmap: only this rank's rows are read (and converted to f32)."""
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
         s, e = shard_bounds(len(gallery), world)[rank]
-        rows = gallery[s:e]
+        rows = np.ascontiguousarray(gallery[s:e], dtype=np.float32) if not isinstance(gallery, torch.Tensor) \
+            else gallery[s:e]
         return cls(rows, len(gallery), s, group=group, device=device, local_search=local_search, mode=mode,
                    fallback_search=fallback_search)
 
@@ -135,17 +179,54 @@ class ShardedIndex:
         sl = slice(self.rank * b, (self.rank + 1) * b)
         return mi[sl], ms[sl], m64[sl]
 
+    def _components(self, q, cand, tables):
+        """Raw rerank components of this shard's candidates (nq, kc, 3) f64."""
+        if self.local_components is not None:
+            return self.local_components(q, cand)
+        q_lab, g_lab, q_kg, g_kg = tables
+        return self.index.rerank_components(q, cand, q_lab, g_lab, q_kg, g_kg)
+
+    def search_rerank(self, q_local, k, tables=None, topk=None, alpha=0.6, beta=0.25, gamma=0.15):
+        """Collective exact top-k + the KG / label rerank of those k candidates (config 5 at world >
+        1).  tables = (q_labels for ALL world*b queries in all-gather order, this shard's g_labels,
+        q_kg for all queries, this shard's g_kg) as device tensors (GPU path), or None when
+        `local_components` was injected.  Returns this rank's (idx (b, topk), final, emb_n, lab_n,
+        kg_n) — bit-identical to GalleryIndex.rerank of the single-index top-k."""
+        b = q_local.shape[0]
+        topk = k if topk is None else topk
+        allq = torch.empty((self.world * b,) + tuple(q_local.shape[1:]), dtype=q_local.dtype,
+                           device=q_local.device)
+        dist.all_gather_into_tensor(allq, q_local.contiguous(), group=self.group)
+        i, s64 = self._local(allq, k)
+        comp = self._components(allq, i, tables).to(s64.device)
+        W = self.world
+        gi = torch.empty((W * i.shape[0],) + tuple(i.shape[1:]), dtype=i.dtype, device=i.device)
+        gs = torch.empty((W * s64.shape[0],) + tuple(s64.shape[1:]), dtype=s64.dtype, device=s64.device)
+        gc = torch.empty((W * comp.shape[0],) + tuple(comp.shape[1:]), dtype=comp.dtype, device=comp.device)
+        dist.all_gather_into_tensor(gi, i.contiguous(), group=self.group)
+        dist.all_gather_into_tensor(gs, s64.contiguous(), group=self.group)
+        dist.all_gather_into_tensor(gc, comp.contiguous(), group=self.group)
+        gi, gs, gc = gi.view((W,) + tuple(i.shape)), gs.view((W,) + tuple(s64.shape)), gc.view((W,) + tuple(comp.shape))
+        if gi.is_cuda:
+            mi, _, _, mc = merge_topk(gs, gi, k, payload=gc, q0=self.rank * b, nq=b)
+            return rerank_mix(mi, mc, topk, alpha, beta, gamma)
+        sl = slice(self.rank * b, (self.rank + 1) * b)
+        mi, _, _, mc = merge_topk_host(gs[:, sl], gi[:, sl], k, payload=gc[:, sl])
+        return rerank_mix_host(mi, mc, topk, alpha, beta, gamma)
+
 
 class ShardedRetrievalEngine(RetrievalEngine):
     """make_retrieval_engine(method="mi355x_sharded"): every rank mmaps the .npy, keeps its row
     shard on its GPU; retrieve()/search() are collective calls (all ranks, same batch size).
     dtype "fp32" scans the bf16x3 split copy, "fp16" the fp16 unit-row copy (BASELINE cfg5's fp16
-    gallery); both rank exactly (f64 re-score from the f32 rows), so results are identical."""
+    gallery); both rank exactly (f64 re-score from the f32 rows), so results are identical.
+    Host memory: `embs` stays the memmap (no whole-gallery f32 copy per rank, unlike the ABC's
+    astype), so a rank's resident host bytes are its shard's, read once into its GPU."""
 
     def __init__(self, features_path=None, ids_path=None, dtype="fp32", embs=None, ids=None, group=None):
         if embs is None:
             embs = np.load(features_path, mmap_mode="r")
-        super().__init__(features_path, ids_path, embs=embs, ids=ids)
+        super().__init__(features_path, ids_path, embs=embs, ids=ids, lazy=True)
         if dtype not in ("fp32", "fp16"):
             raise ValueError(f"gallery dtype {dtype!r} (fp32 | fp16)")
         self.sharded = ShardedIndex.from_full(self.embs, group=group, device=torch.cuda.current_device(),

@@ -12,6 +12,7 @@ make_retrieval_engine      retrieval.py:273-304  (string switch; unknown method 
 import abc
 import ctypes
 import json
+import threading
 from typing import List, Optional, Tuple
 
 import numpy as np
@@ -23,10 +24,16 @@ from . import _lib
 class RetrievalEngine(abc.ABC):
     """Loads embeddings once; id -> index map; abstract retrieve (retrieval.py:18-50)."""
 
-    def __init__(self, features_path: Optional[str], ids_path: Optional[str], embs=None, ids=None):
+    def __init__(self, features_path: Optional[str], ids_path: Optional[str], embs=None, ids=None,
+                 lazy: bool = False):
+        """lazy: keep `embs` as given (e.g. an np.load(..., mmap_mode="r") memmap of any float dtype)
+        instead of materialising a float32 copy — the sharded engine converts only its rows."""
         if embs is None:
             embs = np.load(features_path)
-        self.embs = np.ascontiguousarray(np.asarray(embs).astype("float32"))  # (N, D)
+        if lazy:
+            self.embs = embs if isinstance(embs, np.ndarray) else np.asarray(embs)
+        else:
+            self.embs = np.ascontiguousarray(np.asarray(embs).astype("float32"))  # (N, D)
         if ids is None:
             with open(ids_path, "r") as f:
                 ids = json.load(f)
@@ -43,7 +50,8 @@ class RetrievalEngine(abc.ABC):
         rows = []
         for _id in ids:
             idx = self.id2idx.get(str(_id), None)
-            rows.append(np.zeros(self.embs.shape[1], dtype=self.embs.dtype) if idx is None else self.embs[idx])
+            rows.append(np.zeros(self.embs.shape[1], dtype=np.float32) if idx is None
+                        else np.asarray(self.embs[idx], dtype=np.float32))
         return np.vstack(rows)
 
 
@@ -90,18 +98,42 @@ class GalleryIndex:
         _lib.check(L.mmr_index_set_mode(h, self.MODES[mode]), "mmr_index_set_mode")
         self.mode = mode
         self.n, self.d, self.idx_base = int(n), int(d), int(idx_base)
+        # held across a set_mode / search / set_mode sequence (per-call mode override) and by every
+        # search, so no search of another host thread runs in a temporarily switched mode
+        self._lock = threading.RLock()
 
     def set_mode(self, mode: str):
         if mode not in self.MODES:
             raise ValueError(f"scan mode {mode!r} (x3 | f32 | f16)")
-        _lib.check(_lib.lib().mmr_index_set_mode(self._h, self.MODES[mode]), "mmr_index_set_mode")
-        self.mode = mode
+        with self._lock:
+            _lib.check(_lib.lib().mmr_index_set_mode(self._h, self.MODES[mode]), "mmr_index_set_mode")
+            self.mode = mode
+
+    def device_bytes(self):
+        """(gallery bytes, workspace bytes) this index holds on its GPU (mmr_index_device_bytes)."""
+        g, w = ctypes.c_int64(), ctypes.c_int64()
+        _lib.check(_lib.lib().mmr_index_device_bytes(self._h, ctypes.byref(g), ctypes.byref(w)),
+                   "mmr_index_device_bytes")
+        return int(g.value), int(w.value)
 
     def reserve(self, max_q: int):
         _lib.check(_lib.lib().mmr_index_reserve(self._h, int(max_q)), "mmr_index_reserve")
 
-    def search(self, q: torch.Tensor, k: int, want_f64: bool = False, want_status: bool = False):
-        """q (B, D) f32 device tensor -> (idx int64 (B,k), score f32 (B,k)[, score64][, status])."""
+    def search(self, q: torch.Tensor, k: int, want_f64: bool = False, want_status: bool = False, mode=None):
+        """q (B, D) f32 device tensor -> (idx int64 (B,k), score f32 (B,k)[, score64][, status]).
+        mode: run this one search in another scan mode (the index's mode is restored after)."""
+        if mode is not None and mode != self.mode:
+            with self._lock:
+                prev = self.mode
+                self.set_mode(mode)
+                try:
+                    return self.search(q, k, want_f64, want_status)
+                finally:
+                    self.set_mode(prev)
+        with self._lock:
+            return self._search(q, k, want_f64, want_status)
+
+    def _search(self, q, k, want_f64, want_status):
         _lib.require_gpu(q)
         if q.dim() != 2 or q.shape[1] != self.d:
             raise ValueError(f"query shape {tuple(q.shape)} does not match gallery dim {self.d}")
@@ -153,6 +185,18 @@ class GalleryIndex:
             _lib.ptr(out_i), *(_lib.ptr(o) for o in outs), _lib.stream_ptr(dev)), "mmr_index_rerank")
         return (out_i, *outs)
 
+    def rerank_components(self, q_emb, cand, q_labels, g_labels, q_kg, g_kg):
+        """Shard side of the sharded rerank (mmr_index_rerank_components): the raw {emb cosine, label
+        Jaccard, KG cosine} of this shard's candidates cand (nq, kc) -> (nq, kc, 3) f64 device."""
+        q_emb = q_emb.to(torch.float32).contiguous()
+        nq, kc = cand.shape
+        comp = torch.empty((nq, kc, 3), dtype=torch.float64, device=cand.device)
+        _lib.check(_lib.lib().mmr_index_rerank_components(
+            self._h, _lib.ptr(q_emb), nq, _lib.ptr(cand.contiguous()), kc, _lib.ptr(q_labels), _lib.ptr(g_labels),
+            _lib.ptr(q_kg), _lib.ptr(g_kg), q_kg.shape[1], _lib.ptr(comp), _lib.stream_ptr(cand.device)),
+            "mmr_index_rerank_components")
+        return comp
+
     def close(self):
         h, self._h = getattr(self, "_h", None), None
         if h:
@@ -173,18 +217,40 @@ def check_status(st: torch.Tensor):
                            f"{int((st != 0).sum().item())} queries")
 
 
-def merge_topk(scores64: torch.Tensor, idx: torch.Tensor, k_out: int):
-    """[L][B][k_in] f64 scores + int64 idx (-1 = empty) -> global top-k_out (idx, f32, f64) on device."""
+def merge_topk(scores64: torch.Tensor, idx: torch.Tensor, k_out: int, payload=None, q0: int = 0, nq=None):
+    """[L][B][k_in] f64 scores + int64 idx (-1 = empty) -> global top-k_out (idx, f32, f64) on device
+    for queries [q0, q0 + nq) (default: all B).  payload [L][B][k_in][P] f64 (optional) rides with
+    each entry: then a 4th output (nq, k_out, P) is returned."""
     _lib.require_gpu(scores64)
     L_, B, k_in = idx.shape
+    nq = B - q0 if nq is None else nq
     dev = idx.device
-    oi = torch.empty((B, k_out), dtype=torch.int64, device=dev)
-    os_ = torch.empty((B, k_out), dtype=torch.float32, device=dev)
-    o64 = torch.empty((B, k_out), dtype=torch.float64, device=dev)
-    _lib.check(_lib.lib().mmr_merge_topk(_lib.ptr(scores64.contiguous()), _lib.ptr(idx.contiguous()), L_, B,
-                                         k_in, k_out, _lib.ptr(oi), _lib.ptr(os_), _lib.ptr(o64),
-                                         _lib.stream_ptr(dev)), "mmr_merge_topk")
-    return oi, os_, o64
+    oi = torch.empty((nq, k_out), dtype=torch.int64, device=dev)
+    os_ = torch.empty((nq, k_out), dtype=torch.float32, device=dev)
+    o64 = torch.empty((nq, k_out), dtype=torch.float64, device=dev)
+    P = 0 if payload is None else payload.shape[-1]
+    op = None if payload is None else torch.empty((nq, k_out, P), dtype=torch.float64, device=dev)
+    _lib.check(_lib.lib().mmr_merge_topk_payload(
+        _lib.ptr(scores64.contiguous()), _lib.ptr(idx.contiguous()),
+        _lib.ptr(None if payload is None else payload.contiguous()), P, L_, B, q0, nq, k_in, k_out, _lib.ptr(oi),
+        _lib.ptr(os_), _lib.ptr(o64), _lib.ptr(op), _lib.stream_ptr(dev)), "mmr_merge_topk_payload")
+    return (oi, os_, o64) if payload is None else (oi, os_, o64, op)
+
+
+def rerank_mix(cand: torch.Tensor, comp: torch.Tensor, topk: int, alpha=0.6, beta=0.25, gamma=0.15,
+               want_components=True):
+    """After the shard merge (mmr_rerank_mix): cand (nq, kc) global indices (-1 = empty) + their raw
+    components (nq, kc, 3) -> (idx (nq, topk), final, emb_n, lab_n, kg_n (nq, topk) f64 or None),
+    bit-identical to GalleryIndex.rerank on one index holding the whole gallery."""
+    _lib.require_gpu(cand)
+    nq, kc = cand.shape
+    dev = cand.device
+    out_i = torch.empty((nq, topk), dtype=torch.int64, device=dev)
+    outs = [torch.empty((nq, topk), dtype=torch.float64, device=dev) if want_components else None for _ in range(4)]
+    _lib.check(_lib.lib().mmr_rerank_mix(_lib.ptr(cand.contiguous()), _lib.ptr(comp.contiguous()), nq, kc,
+                                         float(alpha), float(beta), float(gamma), int(topk), _lib.ptr(out_i),
+                                         *(_lib.ptr(o) for o in outs), _lib.stream_ptr(dev)), "mmr_rerank_mix")
+    return (out_i, *outs)
 
 
 class MI355XRetrievalEngine(RetrievalEngine):
@@ -368,10 +434,11 @@ class DLSRetrievalEngine(MI355XRetrievalEngine):
         return ids, scores
 
 
-def make_retrieval_engine(features_path: str, ids_path: str, method: str = "mi355x", **kwargs) -> RetrievalEngine:
-    """Factory (retrieval.py:273-304). method: "mi355x" (aliases "exact", "brute") -> exact GPU
-    engine; "mi355x_sharded" -> row-sharded over torch.distributed ranks; "dls" -> DenseLinkSearch
-    with the GPU-built link graph (link_threshold, max_links, fdb_path, name as in the reference)."""
+def make_retrieval_engine(features_path: str, ids_path: str, method: str = "dls", **kwargs) -> RetrievalEngine:
+    """Factory (retrieval.py:273-304; default method "dls" as there). method: "dls" ->
+    DenseLinkSearch with the GPU-built link graph (link_threshold, max_links, fdb_path, name as in
+    the reference); "mi355x" (aliases "exact", "brute") -> exact GPU engine; "mi355x_sharded" ->
+    row-sharded over torch.distributed ranks."""
     method = method.lower()
     if method in ("mi355x", "exact", "brute", "bruteforce"):
         return MI355XRetrievalEngine(features_path, ids_path, device=kwargs.get("device"),

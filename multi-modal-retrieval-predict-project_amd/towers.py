@@ -23,6 +23,14 @@ from . import ops
 
 SWIN_T = dict(embed_dim=96, depths=[2, 2, 6, 2], num_heads=[3, 6, 12, 24], window_size=7, img_size=224,
               patch=4, in_chans=3)
+# timm Swin names -> geometry (timm swin_transformer.py model defs); the reference's default is
+# swin_base_patch4_window7_224 (fusion.py:45, model.py:124), the north star's Swin-Tiny
+SWIN_ARCHS = {
+    "swin_tiny_patch4_window7_224": SWIN_T,
+    "swin_small_patch4_window7_224": dict(SWIN_T, depths=[2, 2, 18, 2]),
+    "swin_base_patch4_window7_224": dict(SWIN_T, embed_dim=128, depths=[2, 2, 18, 2], num_heads=[4, 8, 16, 32]),
+    "swin_large_patch4_window7_224": dict(SWIN_T, embed_dim=192, depths=[2, 2, 18, 2], num_heads=[6, 12, 24, 48]),
+}
 BERT_BASE = dict(vocab_size=28996, hidden_size=768, num_hidden_layers=12, num_attention_heads=12,
                  intermediate_size=3072, max_position_embeddings=512, type_vocab_size=2)
 
@@ -43,14 +51,33 @@ def _w8(w, plain=False):
     return ops.quantize_mxfp8(w, layout=2 if plain and w.shape[0] % 256 == 0 else 1)
 
 
+def _pad_rows(t2, rows_p):
+    """2-D rows zero-padded to rows_p (the MX-fp8 operands and GEMM tiles take 256-row multiples:
+    a batch of any size — B = 1 serving, a ragged last batch — runs the same fp8 arithmetic on its
+    real rows; the padded rows are discarded)."""
+    if t2 is None or t2.shape[0] == rows_p:
+        return t2
+    out = torch.zeros((rows_p,) + tuple(t2.shape[1:]), dtype=t2.dtype, device=t2.device)
+    out[:t2.shape[0]] = t2
+    return out
+
+
+def _rows256(x):
+    rows = x.numel() // x.shape[-1]
+    return rows, -(-rows // 256) * 256
+
+
 def _mlp8(h, w1_8, b1, w2_8, b2, residual=None, h8=None):
     """fc1 (+ GELU) -> fc2 on the MX-fp8 path with fc1's epilogue emitting fc2's fp8 operand
     (mmr_linear_mxfp8_q8): the hidden activation never exists in bf16.  h8: h's fp8 operand when
-    the producing LayerNorm already emitted it."""
+    the producing LayerNorm already emitted it (rows a multiple of 256)."""
     K = h.shape[-1]
-    x8 = h8 if h8 is not None else ops.quantize_mxfp8(h.reshape(-1, K), layout=0, kp=w1_8.kp)
+    rows, rp = _rows256(h)
+    x8 = h8 if h8 is not None else ops.quantize_mxfp8(_pad_rows(h.reshape(-1, K), rp), layout=0, kp=w1_8.kp)
     f8 = ops.linear_mxfp8_q8(x8, w1_8, b1, act=1)
-    return ops.linear_mxfp8(f8, w2_8, b2, residual, lead=tuple(h.shape[:-1]))
+    r = None if residual is None else _pad_rows(residual.reshape(rows, -1), rp)
+    y = ops.linear_mxfp8(f8, w2_8, b2, r)
+    return (y if rp == rows else y[:rows]).reshape(tuple(h.shape[:-1]) + (y.shape[-1],))
 
 
 def _ln8_ok(x, w8):
@@ -62,12 +89,18 @@ def _ln8_ok(x, w8):
 def _lin(x, w, b=None, residual=None, act=0, w8=None):
     """nn.Linear through the bf16 GEMM, or through the MX-fp8 GEMM when the layer holds w8: the
     activation is quantised per 32-block (mmr_quantize_mxfp8) and the block-scaled MFMA GEMM
-    applies bias / GELU / residual in f32 (BASELINE config 5's fp8 towers)."""
+    applies bias / GELU / residual in f32 (BASELINE config 5's fp8 towers).  Rows are zero-padded
+    to a multiple of 256 when needed (_pad_rows)."""
     if w8 is None:
         return ops.linear(x, w, b, residual=residual, act=act)
     K = x.shape[-1]
-    x8 = ops.quantize_mxfp8(x.reshape(-1, K), layout=0, kp=w8.kp)
-    return ops.linear_mxfp8(x8, w8, b, residual, act=act, lead=tuple(x.shape[:-1]))
+    rows, rp = _rows256(x)
+    x8 = ops.quantize_mxfp8(_pad_rows(x.reshape(-1, K), rp), layout=0, kp=w8.kp)
+    r = None if residual is None else _pad_rows(residual.reshape(rows, -1), rp)
+    if rp == rows:
+        return ops.linear_mxfp8(x8, w8, b, r, act=act, lead=tuple(x.shape[:-1]))
+    y = ops.linear_mxfp8(x8, w8, b, r, act=act)
+    return y[:rows].reshape(tuple(x.shape[:-1]) + (y.shape[-1],))
 
 
 class SwinTower:

@@ -158,3 +158,77 @@ def test_dls_cache_path_naming(tmp_path, monkeypatch):
     assert (tmp_path / "fdb").is_dir()
     monkeypatch.delenv("MMR_FEATURE_DB_DIR")
     assert cp(None) is None
+
+
+def _rerank_fixture(N, D, Q, DK):
+    rng = np.random.default_rng(91)
+    G, _ = synthetic.labelled_gallery(N, D, 92)
+    G[4] = G[N - 2]                        # duplicate across shards
+    glab = [set(rng.choice(12, size=int(rng.integers(0, 4)), replace=False).tolist()) for _ in range(N)]
+    qlab = [set(rng.choice(12, size=int(rng.integers(1, 3)), replace=False).tolist()) for _ in range(Q)]
+    return G, glab, qlab, rng.standard_normal((N, DK)), rng.standard_normal((Q, DK))
+
+
+def _worker_rerank(rank, world, port, N, D, b, K, DK, out_q):
+    """Sharded rerank (config 5 at world > 1): the shard computes its candidates' raw components,
+    they ride through the all-gather and the host payload merge, the mix runs on the merged list."""
+    from oracle import dls as odls
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        G, glab, qlab, gkg, qkg = _rerank_fixture(N, D, world * b, DK)
+        Q, _ = synthetic.labelled_gallery(world * b, D, 93)
+        s, e = shard_bounds(N, world)[rank]
+
+        def local(q, k):
+            i, sc = oknn.exact_topk(q.numpy(), G[s:e], k)
+            return torch.from_numpy(np.where(i >= 0, i + s, -1).astype(np.int64)), torch.from_numpy(sc)
+
+        def comps(q, cand):
+            out = np.zeros(tuple(cand.shape) + (3,))
+            for qi in range(cand.shape[0]):
+                for c in range(cand.shape[1]):
+                    g = int(cand[qi, c])
+                    if g >= 0:
+                        assert s <= g < e  # a shard only scores its own rows
+                        out[qi, c] = (odls._cos(q[qi].numpy().astype(np.float64), G[g].astype(np.float64)),
+                                      odls._jac(qlab[qi], glab[g]), odls._cos(qkg[qi], gkg[g]))
+            return torch.from_numpy(out)
+
+        sh = ShardedIndex(G[s:e], N, s, local_search=local, local_components=comps)
+        out = sh.search_rerank(torch.from_numpy(Q[rank * b:(rank + 1) * b]), K, topk=K - 2)
+        out_q.put((rank,) + tuple(t.numpy() for t in out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_rerank_world2_equals_single_list_rerank():
+    """gloo world 2: the sharded rerank's (order, final, components) equal oracle/dls.rerank
+    (reranker.py:240-333) over the single-device exact top-K list of every query."""
+    from oracle import dls as odls
+    world, N, D, b, K, DK = 2, 1501, 48, 6, 10, 16
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_rerank, args=(r, world, port, N, D, b, K, DK, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    G, glab, qlab, gkg, qkg = _rerank_fixture(N, D, world * b, DK)
+    Q, _ = synthetic.labelled_gallery(world * b, D, 93)
+    ei, _ = oknn.exact_topk(Q, G, K)
+    for rank, oi, fi, e, lab, kg in res:
+        for r in range(b):
+            qi = rank * b + r
+            cand = ei[qi]
+            order, final, re_, rl, rk = odls.rerank(Q[qi].astype(np.float64), G[cand], qlab[qi],
+                                                    [glab[j] for j in cand], qkg[qi], gkg[cand], topk=K - 2)
+            assert oi[r].tolist() == cand[order].tolist()
+            np.testing.assert_allclose(fi[r], final, rtol=0, atol=1e-12)
+            np.testing.assert_allclose(e[r], re_, rtol=0, atol=1e-12)
+            np.testing.assert_allclose(lab[r], rl, rtol=0, atol=1e-12)
+            np.testing.assert_allclose(kg[r], rk, rtol=0, atol=1e-12)

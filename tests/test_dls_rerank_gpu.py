@@ -182,7 +182,8 @@ def test_build_gallery_files(tmp_path):
     scfg = dict(SWIN_T, embed_dim=32, depths=[2, 2, 2, 2], num_heads=[1, 2, 4, 8])
     bcfg = dict(BERT_BASE, vocab_size=1000, hidden_size=128, num_hidden_layers=2, num_attention_heads=2,
                 intermediate_size=512)
-    m = MultiModalRetrievalModel(joint_dim=64, model_type="text", swin_cfg=scfg, bert_cfg=bcfg, device="cuda")
+    m = MultiModalRetrievalModel(joint_dim=64, model_type="text", swin_cfg=scfg, bert_cfg=bcfg, device="cuda",
+                                 training=True, pretrained=False)
     batches = []
     for b in range(3):
         img = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(4, 50 + b)))

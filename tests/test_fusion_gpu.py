@@ -138,7 +138,7 @@ def test_full_size_multimodal_vs_oracle():
     hs.update(init_fusion_state(768, 768, 768, 8, 5, 8))
     bb = Backbones(swin_state=ssd, bert_state=bsd, device=DEV)
     m = MultiModalRetrievalModel(joint_dim=768, num_heads=8, model_type="multimodal", backbones=bb,
-                                 head_state=hs, device=DEV)
+                                 head_state=hs, device=DEV, use_shared_ffn=False)
     img = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(2, 9)))
     ids, mask = (torch.from_numpy(a) for a in synthetic.reports(2, 128, 10))
     o = m(img.to(DEV), ids.to(DEV), mask.to(DEV))
@@ -178,7 +178,7 @@ def test_full_size_multimodal_joint_dim_1024_batch_256_vs_oracle():
     hs.update(init_fusion_state(768, 768, 1024, 8, 5, 18))
     bb = Backbones(swin_state=ssd, bert_state=bsd, device=DEV)
     m = MultiModalRetrievalModel(joint_dim=1024, num_heads=8, model_type="multimodal", backbones=bb,
-                                 head_state=hs, device=DEV)
+                                 head_state=hs, device=DEV, use_shared_ffn=False)
     img = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(256, 19)))
     ids, mask = (torch.from_numpy(a) for a in synthetic.reports(256, 128, 20))
     q = m.query_embeddings(img.to(DEV), ids.to(DEV), mask.to(DEV))      # first call: towers in sequence

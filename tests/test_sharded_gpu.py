@@ -17,23 +17,25 @@ from mmr_amd.retrieval import GalleryIndex
 
 pytestmark = pytest.mark.gpu
 
-N, D, B, K = 30_011, 384, 24, 16
+SMALL = (30_011, 384, 24, 16)
+CFG4 = (2_000_000, 768, 128, 10)   # BASELINE cfg4's per-GPU shard (1M rows) at world 2
 
 
-def _gallery():
+def _gallery(N, D):
     G = synthetic.gauss_gallery(N, D, 501)
     G[17] = G[N - 5]          # exact duplicate across the two shards: tie broken by global index
     G[40] = 0.0
     return G
 
 
-def _worker(rank, world, port, mode, out_q):
+def _worker(rank, world, port, mode, shape, out_q):
+    N, D, B, K = shape
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
-        G = _gallery()
+        G = _gallery(N, D)
         Q = synthetic.gauss_gallery(world * B, D, 502)
         Q[0] = G[17]
         s, e = shard_bounds(N, world)[rank]
@@ -51,8 +53,11 @@ def _worker(rank, world, port, mode, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["f16", "x3"])
-def test_sharded_gallery_index_world2_equals_single_device(mode):
+@pytest.mark.parametrize("mode,shape", [("f16", SMALL), ("x3", SMALL), ("f16", CFG4)])
+def test_sharded_gallery_index_world2_equals_single_device(mode, shape):
+    """Two ranks, each holding half the gallery (cfg4 case: 2 x 1M x 768, 128 queries per rank,
+    top-10 on the 4-row-unit path), merged = one index over the whole gallery, bit for bit."""
+    N, D, B, K = shape
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -60,14 +65,14 @@ def test_sharded_gallery_index_world2_equals_single_device(mode):
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, shape, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=180) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    G = _gallery()
+    G = _gallery(N, D)
     Q = synthetic.gauss_gallery(world * B, D, 502)
     Q[0] = G[17]
     ix = GalleryIndex(G, mode=mode)
@@ -79,3 +84,81 @@ def test_sharded_gallery_index_world2_equals_single_device(mode):
         assert reruns == 0
         np.testing.assert_array_equal(mi, si[rank * B:(rank + 1) * B])
         np.testing.assert_array_equal(m64, s64[rank * B:(rank + 1) * B])
+
+
+def _worker_rerank(rank, world, port, out_q):
+    """Sharded rerank over gloo with the real per-rank GalleryIndex: components computed on the
+    owning shard, lists + components all-gathered (staged to host), host merge + host mix."""
+    N, D, B, K, DK = 20_011, 256, 16, 12, 64
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        G, gb, qb, gk, qk = _rerank_data(N, D, world * B, DK)
+        Q = synthetic.gauss_gallery(world * B, D, 512)
+        s, e = shard_bounds(N, world)[rank]
+        ix = GalleryIndex(G[s:e], device=0, idx_base=s, mode="f16")
+        dev = torch.device("cuda:0")
+
+        def local(q, k):
+            i, _, s64, st = ix.search(q.cuda(), k, want_f64=True, want_status=True)
+            return i.cpu(), s64.cpu(), st.cpu()
+
+        def comps(q, cand):
+            return ix.rerank_components(q.cuda(), cand.cuda(), _t(qb, dev), _t(gb[s:e], dev), _t(qk, dev),
+                                        _t(gk[s:e], dev)).cpu()
+
+        sh = ShardedIndex(G[s:e], N, s, local_search=local, local_components=comps)
+        out = sh.search_rerank(torch.from_numpy(Q[rank * B:(rank + 1) * B]), K)
+        out_q.put((rank,) + tuple(t.numpy() for t in out))
+        ix.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def _t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int64) if a.dtype == np.uint64 else a).to(dev)
+
+
+def _rerank_data(N, D, Q, DK):
+    rng = np.random.default_rng(511)
+    G = synthetic.gauss_gallery(N, D, 511)
+    G[3] = G[N - 7]
+    gb = rng.integers(0, 1 << 20, size=N).astype(np.uint64)
+    qb = rng.integers(0, 1 << 20, size=Q).astype(np.uint64)
+    return G, gb, qb, rng.standard_normal((N, DK), dtype=np.float32), rng.standard_normal((Q, DK), dtype=np.float32)
+
+
+def test_sharded_rerank_world2_matches_single_index():
+    """config 5's rerank at world > 1: (idx, final, emb_n, lab_n, kg_n) of the sharded path equal the
+    single-index fused rerank (mmr_index_rerank) — order exactly, scores within f64 contraction
+    rounding (the host mix vs the device's fused multiply-adds)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = [ctx.Process(target=_worker_rerank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    N, D, B, K, DK = 20_011, 256, 16, 12, 64
+    G, gb, qb, gk, qk = _rerank_data(N, D, world * B, DK)
+    Q = synthetic.gauss_gallery(world * B, D, 512)
+    dev = torch.device("cuda:0")
+    ix = GalleryIndex(G, mode="f16")
+    qd = torch.from_numpy(Q).cuda()
+    i = ix.search(qd, K)[0]
+    ref = [t.cpu().numpy() for t in ix.rerank(qd, i, _t(qb, dev), _t(gb, dev), _t(qk, dev), _t(gk, dev), K)]
+    ix.close()
+    for rank, *got in res:
+        sl = slice(rank * B, (rank + 1) * B)
+        np.testing.assert_array_equal(got[0], ref[0][sl])
+        for a, b in zip(got[1:], ref[1:]):
+            np.testing.assert_allclose(a, b[sl], rtol=0, atol=1e-12)

@@ -259,7 +259,7 @@ def test_mini_towers_match_reference_golden():
     _check_emb(t, torch.from_numpy(f["txt_feats"]))
     for mt in ("text", "image", "multimodal"):
         m = MultiModalRetrievalModel(joint_dim=cfg["joint_dim"], num_heads=cfg["num_heads"], model_type=mt,
-                                     backbones=bb, head_state=head, device=DEV)
+                                     backbones=bb, head_state=head, device=DEV, use_shared_ffn=False)
         o = m(image, ids, mask)
         _check_emb(o["joint_emb"], torch.from_numpy(f[f"{mt}_joint_emb"]))
         _check_emb(o["img_emb"], torch.from_numpy(f[f"{mt}_img_emb"]))
@@ -278,3 +278,30 @@ def test_full_size_towers_vs_oracle():
     _check_emb(g, rg)
     _check_emb(p, rp)
     _check_emb(t, rt)
+
+
+def test_checkpoint_path_reference_layout(tmp_path):
+    """The reference's inference constructor path (model.py:116-137 arguments; checkpoint loaded as
+    model.py:282-287 does, here with torch.load(..., weights_only=True)): the golden mini model's
+    weights re-keyed into the reference state-dict layout (backbones.vision.* timm keys,
+    backbones.bert.* HF keys, head keys) and saved; MultiModalRetrievalModel(checkpoint_path=...)
+    reads the tower geometry off the weights and reproduces the golden outputs of all three heads.
+    Without a checkpoint (training=False) it raises like the reference."""
+    from test_boundary_cpu import _reference_layout_state
+    sd, cfg = _reference_layout_state()
+    p = tmp_path / "model_best.pt"
+    torch.save(sd, p)
+    f = np.load(os.path.join(GOLDEN, "towers_mini.npz"), allow_pickle=False)
+    image = torch.from_numpy(synthetic.image_from_u8(f["img_u8"])).to(DEV)
+    ids = torch.from_numpy(f["input_ids"]).to(DEV)
+    mask = torch.from_numpy(f["attention_mask"]).to(DEV)
+    for mt in ("text", "image", "multimodal"):
+        m = MultiModalRetrievalModel(joint_dim=cfg["joint_dim"], num_heads=cfg["num_heads"], num_classes=43,
+                                     num_fusion_layers=2, checkpoint_path=str(p), device=DEV, use_shared_ffn=False,
+                                     model_type=mt)
+        o = m(image, ids, mask)
+        _check_emb(o["joint_emb"], torch.from_numpy(f[f"{mt}_joint_emb"]))
+        _check_emb(o["img_emb"], torch.from_numpy(f[f"{mt}_img_emb"]))
+        _check_emb(o["txt_emb"], torch.from_numpy(f[f"{mt}_txt_emb"]))
+    with pytest.raises(ValueError, match="checkpoint_path must be provided"):
+        MultiModalRetrievalModel(joint_dim=64, device=DEV)

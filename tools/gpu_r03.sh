@@ -1,0 +1,36 @@
+#!/bin/bash
+# Round-3 GPU pass.  usage (via gpurun): bash tools/gpu_r03.sh <tag> [steps...]
+# Each GPU step has its own time limit; the first failing step ends the script.
+set -e -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+TAG=${1:-r03}; shift || true
+STEPS=${@:-tests smoke bench}
+OUT=gpurun_out/$TAG; mkdir -p $OUT
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 1050 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -40 $OUT/tests.log; exit 1; }
+      tail -3 $OUT/tests.log ;;
+    testsx)  # a subset: TESTS env = pytest node ids / -k expression file list
+      timeout -k 10 1050 python -u -m pytest $TESTS -m gpu -v --timeout 300 --timeout-method thread > $OUT/testsx.log 2>&1 || { tail -40 $OUT/testsx.log; exit 1; }
+      tail -3 $OUT/testsx.log ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1
+      tail -1 $OUT/smoke.log ;;
+    bench)
+      timeout -k 10 400 python -u bench.py > $OUT/bench_full.json 2> $OUT/bench_full.err
+      cat $OUT/bench_full.json ;;
+    benchknn)
+      timeout -k 10 300 python -u bench.py --mode knn > $OUT/bench_knn.json 2> $OUT/bench_knn.err
+      cat $OUT/bench_knn.json ;;
+    presets)
+      timeout -k 10 400 python -u bench.py --preset cfg3 --steps 5 --warmup 2 > $OUT/bench_cfg3.json 2> $OUT/bench_cfg3.err
+      timeout -k 10 500 python -u bench.py --preset cfg5 --steps 5 --warmup 2 > $OUT/bench_cfg5.json 2> $OUT/bench_cfg5.err
+      echo presets ok ;;
+    prof)
+      MMR_TOWER_STREAMS=0 MMR_FUSION_STREAMS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o full \
+        -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof_full.log 2>&1
+      echo prof ok ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
