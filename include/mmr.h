@@ -54,7 +54,7 @@ mmr_status mmr_index_create(const void* gallery, int64_t n, int32_t d, mmr_dtype
 mmr_status mmr_index_destroy(mmr_index* index);
 mmr_status mmr_index_info(const mmr_index* index, int64_t* n, int32_t* d, int64_t* idx_base);
 /* Device bytes the index holds: gallery_bytes = f32 rows + norms + the scan copies of the current
- * mode (x3: bf16 hi/lo split + tile16 f32, 12 B per element; f16: fp16 tile32h + row-major fp16,
+ * mode (x3: bf16 hi/lo split + tile16 f32, 8 B per element; f16: fp16 tile32h + row-major fp16,
  * 4 B per element; f32: none — copies of other modes are freed at a mode switch);
  * workspace_bytes = the query / per-unit-maxima workspace.  Either pointer may be NULL. */
 mmr_status mmr_index_device_bytes(const mmr_index* index, int64_t* gallery_bytes, int64_t* workspace_bytes);

@@ -537,7 +537,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
                                                        const uint8_t* __restrict__ WS = nullptr,
                                                        uint8_t* __restrict__ YS = nullptr,
                                                        float* __restrict__ GM = nullptr, float* __restrict__ BM = nullptr,
-                                                       int64_t ldG = 0, int64_t ldB = 0, int64_t nval = 0) {
+                                                       int64_t ldG = 0, int64_t ldB = 0, int64_t nval = 0,
+                                                       int nck = 0) {
   static_assert(!OUT8 || (FP8 && NT == 4 && !HAS_RES), "OUT8: MX-fp8 256x256 tiles without residual");
   static_assert(KNN == 0 || ((KNN == 2 || KNN == 4) && NT == 4 && !FP8 && !HAS_BIAS && !HAS_RES && ACT == 0),
                 "KNN (rows per unit 2 / 4): plain 256x256 fp16 tiles");
@@ -557,9 +558,26 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
 
   const int ntiles = tiles_m * tiles_n;
   const int per = gridDim.x / 8, xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
-  const int lo = (int)((int64_t)ntiles * xcd / 8), hi = (int)((int64_t)ntiles * (xcd + 1) / 8);
+  // Tile order.  nck = 0: the XCD's share is a contiguous run of the row-major (m, n) tile grid
+  // (the 32 concurrent tiles of an XCD span ~32 / tiles_n X panels and every W panel).  nck > 0:
+  // the XCD owns whole X panels [plo, phi) and walks them in n-chunks of nck W panels — every panel
+  // of the chunk, then the next chunk — so a chunk of W (nck x 256 x K) stays in the XCD's L2 while
+  // its X panels stream past once per chunk (W fetched once per XCD instead of once per round).
+  const int plo = (int)((int64_t)tiles_m * xcd / 8), phi = (int)((int64_t)tiles_m * (xcd + 1) / 8);
+  const int lo = nck > 0 ? plo * tiles_n : (int)((int64_t)ntiles * xcd / 8);
+  const int hi = nck > 0 ? phi * tiles_n : (int)((int64_t)ntiles * (xcd + 1) / 8);
   int t = lo + slot;
   if (t >= hi) return;
+  auto mof = [&](int tile) -> int {
+    if (nck <= 0) return tile / tiles_n;
+    const int u = tile - lo, P = phi - plo, k = u / (P * nck), w = min(nck, tiles_n - k * nck);
+    return plo + (u - k * P * nck) / w;
+  };
+  auto nof = [&](int tile) -> int {
+    if (nck <= 0) return tile % tiles_n;
+    const int u = tile - lo, P = phi - plo, k = u / (P * nck), w = min(nck, tiles_n - k * nck);
+    return k * nck + (u - k * P * nck) % w;
+  };
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably uniform: SGPR LDS bases
@@ -571,7 +589,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   // tile's at the end of wave 0's epilogue (the other parity; no registers live across the loop)
   auto bias_dma = [&](int tile, int par) {
     if (HAS_BIAS && wave == 0 && lane < TBN / 4)
-      __builtin_amdgcn_global_load_lds((const void*)(bias + (tile % tiles_n) * TBN + lane * 4),
+      __builtin_amdgcn_global_load_lds((const void*)(bias + nof(tile) * TBN + lane * 4),
                                        (lds_ptr_t)(lbias + par * TBN), 16, 0, 0);
   };
 
@@ -588,10 +606,10 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   // operand panels as buffer descriptors (uniform, SGPRs): a piece is buffer_load ... lds with the
   // per-lane offset in voffset and the K-tile offset in soffset — no per-piece address registers
   auto xbase = [&](int tile) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)X + (int64_t)(tile / tiles_n) * 256 * K * ESZ), 0, 0x7FFFFFFF, 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)X + (int64_t)mof(tile) * 256 * K * ESZ), 0, 0x7FFFFFFF, 0x00020000);
   };
   auto wbase = [&](int tile) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)W + (int64_t)(tile % tiles_n) * TBN * K * ESZ), 0, 0x7FFFFFFF, 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)W + (int64_t)nof(tile) * TBN * K * ESZ), 0, 0x7FFFFFFF, 0x00020000);
   };
   // MX scales: one 1-KB piece per operand panel and K-tile (wave 0: X's, wave 1: W's); a wave issues
   // it with its first piece of that K-tile, so every count-based wait below still covers it
@@ -601,10 +619,10 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
     if constexpr (FP8) {
       if (wave == 0)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(xsr, (lds_ptr_t)(dsm + soff(buf)), 16, lane * 16,
-                                                 ((tile / tiles_n) * nk + kt) * 1024, 0, 0);
+                                                 (mof(tile) * nk + kt) * 1024, 0, 0);
       else if (wave == 1)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(wsr, (lds_ptr_t)(dsm + soff(buf) + 512), 16, lane * 16,
-                                                 ((tile % tiles_n) * nk + kt) * 1024, 0, 0);
+                                                 (nof(tile) * nk + kt) * 1024, 0, 0);
     }
   };
   auto gA = [&](__amdgpu_buffer_rsrc_t xb, int buf, int j, int kt) {
@@ -700,8 +718,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
     const auto wcb = wbase(t);
     const auto xn = xbase(has_next ? tnext : t);
     const auto wn = wbase(has_next ? tnext : t);
-    const int n0 = (t % tiles_n) * TBN;
-    const int64_t m0 = (int64_t)(t / tiles_n) * 256;
+    const int n0 = nof(t) * TBN;
+    const int64_t m0 = (int64_t)mof(t) * 256;
 
     f32x4 acc[8][NT];
 #pragma unroll
@@ -1245,6 +1263,20 @@ constexpr int kVariants = 11;
 constexpr int kVarW4[kVariants] = {1, 2, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 constexpr int kVarCfg[kVariants] = {1, 1, 1, 2, 3, 4, 5, 6, 0, 7, 8};
 
+// n-chunk width of the 8-phase GEMM's tile order (see gemm_bf16_tn_p8): MMR_P8_NCK=c selects
+// n-chunks of c W panels per XCD, default 0 = the row-major order.  The chunked order cuts the
+// modelled L2-miss bytes of FFN1 / QKV by ~2x (W fetched once per XCD instead of once per round of
+// 32 concurrent tiles) but measured 1-6 % SLOWER on every BERT shape (profiles/r03_gemm_tile_order_ab.txt):
+// those misses are served by the 256 MB MALL and the kernel is not bound by them.
+int p8_nck(int tm, int tn, int k, int tbn) {
+  (void)tm;
+  (void)tn;
+  (void)k;
+  (void)tbn;
+  if (const char* e = getenv("MMR_P8_NCK")) return atoi(e);
+  return 0;
+}
+
 template <int ACT, bool HB, bool HR>
 void launch(const uint16_t* x, const uint16_t* w, const float* b, const uint16_t* r, uint16_t* y,
             int64_t m, int n, int k, hipStream_t st, int w4, int cfg) {
@@ -1272,12 +1304,14 @@ void launch(const uint16_t* x, const uint16_t* w, const float* b, const uint16_t
     const int grid = std::max(8, cu_count() / 8 * 8);
     if (cfg == 7 && n % 256 == 0) {
       const int tm = (int)t256, tn = n / 256;
-      gemm_bf16_tn_p8<4, ACT, HB, HR><<<dim3(std::max<int64_t>(8, std::min<int64_t>(grid, (int64_t)tm * tn) / 8 * 8)), dim3(512), P8<4>::LDS_B, st>>>(x, w, b, r, y, m, n, k, tm, tn);
+      gemm_bf16_tn_p8<4, ACT, HB, HR><<<dim3(std::max<int64_t>(8, std::min<int64_t>(grid, (int64_t)tm * tn) / 8 * 8)), dim3(512), P8<4>::LDS_B, st>>>(
+          x, w, b, r, y, m, n, k, tm, tn, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, p8_nck(tm, tn, k, 256));
       return;
     }
     if (cfg == 8 && n % 192 == 0) {
       const int tm = (int)t256, tn = n / 192;
-      gemm_bf16_tn_p8<3, ACT, HB, HR><<<dim3(std::max<int64_t>(8, std::min<int64_t>(grid, (int64_t)tm * tn) / 8 * 8)), dim3(512), P8<3>::LDS_B, st>>>(x, w, b, r, y, m, n, k, tm, tn);
+      gemm_bf16_tn_p8<3, ACT, HB, HR><<<dim3(std::max<int64_t>(8, std::min<int64_t>(grid, (int64_t)tm * tn) / 8 * 8)), dim3(512), P8<3>::LDS_B, st>>>(
+          x, w, b, r, y, m, n, k, tm, tn, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, p8_nck(tm, tn, k, 192));
       return;
     }
   }

@@ -2225,7 +2225,7 @@ void launch_select(hipStream_t st, int64_t nq, const float* vals, int64_t ldV, i
 }
 
 // Mode-specific scan copies, built when a mode first needs them (mmr_index_set_mode / the first
-// search): x3 = the bf16 hi/lo split [Np][2Dp] + the tile16 f32 copy of the skinny scan (12 B per
+// search): x3 = the bf16 hi/lo split [Np][2Dp] + the tile16 f32 copy of the skinny scan (8 B per
 // element); f16 = the tile32h fp16 unit rows + (Dp % 128 == 0, Dp <= 1024) the row-major fp16 copy
 // of the p8 scan (4 B per element).  A switch to f16 / f32 frees the x3 copies (an fp16 gallery
 // index holds f32 rows + fp16 copies only); a switch away from f16 frees the fp16 copies.

@@ -223,8 +223,8 @@ def test_cfg3_text_tower_batch_1024_vs_oracle():
 
 def test_index_device_bytes_per_mode():
     """Scan copies exist only in the mode that reads them: f32 rows + norms always; x3 adds the bf16
-    split + tile16 copies (12 B per element); f16 the two fp16 copies (4 B per element) and frees the
-    x3 ones — a 1M x 1024 fp16-gallery index holds f32 rows + fp16 copies only."""
+    hi/lo split + tile16 f32 copies (8 B per element); f16 the two fp16 copies (4 B per element) and
+    frees the x3 ones — a 1M x 1024 fp16-gallery index holds f32 rows + fp16 copies only."""
     N, D = 1_000_000, 1024
     G = synthetic.gauss_gallery(N, D, synthetic.SEED + 60)
     base = N * D * 4 + N * 12
@@ -233,7 +233,7 @@ def test_index_device_bytes_per_mode():
     assert base + N * D * 4 <= g16 <= base + N * D * 4 + 512 * D * 4 + 512 * 12
     ix.set_mode("x3")
     g3, _ = ix.device_bytes()
-    assert base + N * D * 12 <= g3 <= base + N * D * 12 + 512 * D * 16
+    assert base + N * D * 8 <= g3 <= base + N * D * 8 + 512 * D * 12
     ix.set_mode("f32")
     g32, _ = ix.device_bytes()
     assert g32 <= base + 512 * D * 4 + 512 * 12
