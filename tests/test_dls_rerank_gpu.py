@@ -197,7 +197,7 @@ def test_build_gallery_files(tmp_path):
     me, mi = merge_galleries(tmp_path)
     assert me.shape == (16, 64) and mi == ids + ids[:4]
     eng = mmr_amd.make_retrieval_engine(str(tmp_path / "trainval_joint_embeddings.npy"),
-                                        str(tmp_path / "trainval_ids.json"))
+                                        str(tmp_path / "trainval_ids.json"), method="mi355x")
     r_ids, r_sc = eng.retrieve(me[3], K=2)
     assert r_ids == [ids[3], ids[3]] and abs(r_sc[0] - 1.0) < 1e-6  # row 3 and its duplicate row 15
     eng.close()
