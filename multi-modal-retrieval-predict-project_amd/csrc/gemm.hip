@@ -500,8 +500,11 @@ struct P8 {
   static constexpr int RM = NT == 3 ? 2 : 1;           // m-tiles per epilogue round
   static constexpr int ELD = 16 * NT + 8;              // bf16 row stride of the epilogue area
   static constexpr int CPL = 16 * RM * 2 * NT / 64;    // 16-B chunks per lane per round
-  // global stores per wave per tile (KNN: 8 m-tiles x (4 unit-max + 1 block-max) stores)
-  static constexpr int NSTORE = KNN ? 40 : (8 / RM) * CPL;
+  // global stores per wave per tile (KNN: 8 m-tiles x (4 unit-max + 1 block-max) stores; the LDS-
+  // staged epilogue (OUT8, MMR_P8_EPI=0): 8 / RM rounds x CPL 16-B chunks; the permlane epilogue:
+  // one 16-B store per (m-tile, n-tile pair) — NT = 3 stores its odd tile as a pair with itself)
+  static constexpr int NSTORE_LDS = KNN ? 40 : (8 / RM) * CPL;
+  static constexpr int NSTORE_PL = 8 * ((NT + 1) / 2);
   static constexpr size_t BUF_B = (size_t)(256 + TBN) * 64 * 2 + SC * 2;
   static constexpr size_t EPI_B = 8ull * 16 * RM * ELD * 2;
   static constexpr size_t LDS_B = 2 * BUF_B + EPI_B + 2 * TBN * 4;
@@ -538,7 +541,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
                                                        uint8_t* __restrict__ YS = nullptr,
                                                        float* __restrict__ GM = nullptr, float* __restrict__ BM = nullptr,
                                                        int64_t ldG = 0, int64_t ldB = 0, int64_t nval = 0,
-                                                       int nck = 0) {
+                                                       int nck = 0, int epi_mode = -1) {
   static_assert(!OUT8 || (FP8 && NT == 4 && !HAS_RES), "OUT8: MX-fp8 256x256 tiles without residual");
   static_assert(KNN == 0 || ((KNN == 2 || KNN == 4) && NT == 4 && !FP8 && !HAS_BIAS && !HAS_RES && ACT == 0),
                 "KNN (rows per unit 2 / 4): plain 256x256 fp16 tiles");
@@ -553,7 +556,14 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   auto soff = [](int buf) { return 2 * (TA + TB) + buf * C::SC; };
   constexpr int ESZ = FP8 ? 1 : 2;                      // operand element bytes
   constexpr int NH0 = NT / 2;                           // n-tiles in n-half 0
-  static_assert(C::NSTORE + 5 <= 63, "vmcnt range");
+  static_assert(C::NSTORE_LDS + 5 <= 63 && C::NSTORE_PL + 5 <= 63, "vmcnt range");
+  // Epilogue: permlane row chunks straight from registers (no LDS round trips) or the per-wave LDS
+  // staging.  epi_mode -1 (default) = permlane for GELU epilogues only: measured (random operands,
+  // profiles/r03_gemm_epilogue_ab.txt) FFN1 + GELU 925 -> 1015 TF, Swin fc1 + GELU +8 %, but the
+  // plain / residual epilogues 3-7 % slower than the LDS path (QKV 1041 vs 947 TF at 256 x 192);
+  // 0 / 1 force LDS / permlane (MMR_P8_EPI, A/B).  OUT8 / KNN always use their own epilogues.
+  const bool epi_pl = !OUT8 && !KNN && (epi_mode < 0 ? ACT == 1 : epi_mode != 0);
+  const int nstore = epi_pl ? C::NSTORE_PL : C::NSTORE_LDS;
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
 
   const int ntiles = tiles_m * tiles_n;
@@ -774,7 +784,10 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
         issue(2 * p);
         if (p == 3) {  // end of s6: O complete (younger: E pieces, + last tile's stores at it 0)
           if (!loads) __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
-          else if (it == 0 && !first) __builtin_amdgcn_s_waitcnt(vmcnt_imm(5 + C::NSTORE));
+          else if (it == 0 && !first) {
+            if (nstore == C::NSTORE_PL) __builtin_amdgcn_s_waitcnt(vmcnt_imm(5 + C::NSTORE_PL));
+            else __builtin_amdgcn_s_waitcnt(vmcnt_imm(5 + C::NSTORE_LDS));
+          }
           else __builtin_amdgcn_s_waitcnt(vmcnt_imm(5));
         } else if (p == 7) {  // end of s14: E complete (younger: 5 O pieces)
           if (loads) __builtin_amdgcn_s_waitcnt(vmcnt_imm(5));
@@ -889,8 +902,49 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
         for (int j = 0; j < NT; ++j)
           rq[i][j] = *(const uint2*)(R + (m0 + wr * 128 + i * 16 + efr) * N + n0 + wc * 16 * NT + j * 16 + efq * 4);
     }
+    if (epi_pl) {
+      // C^T fragment -> 16-B row chunks in registers: for an n-tile pair (j, j + 1) one
+      // v_permlane16_swap per dword hands lane group fq = 1 (3) the pair's tile-(j+1) columns
+      // 0-3 (8-11) of fq = 0 (2) and takes back tile j's columns 4-7 (12-15), so every lane holds
+      // 8 consecutive columns of its row: fq 0 -> tile j cols 0-7, fq 1 -> tile j+1 cols 0-7,
+      // fq 2 -> tile j cols 8-15, fq 3 -> tile j+1 cols 8-15 (an odd last tile pairs with itself:
+      // lanes fq 0/1 and 2/3 then write the same bytes).  One dwordx4 store per pair and m-tile.
 #pragma unroll
-    for (int rd = 0; rd < 8 / C::RM; ++rd) {
+      for (int i = 0; i < 8; ++i) {
+        const int64_t row = m0 + wr * 128 + i * 16 + efr;
+#pragma unroll
+        for (int j = 0; j < NT; j += 2) {
+          const int j2 = j + 1 < NT ? j + 1 : j;
+          uint2 pk[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int jj = h ? j2 : j;
+            float v[4];
+#pragma unroll
+            for (int rg = 0; rg < 4; rg += 2) {
+              mmr::f32x2_t u = {acc[i][jj][rg] + bq[jj][rg], acc[i][jj][rg + 1] + bq[jj][rg + 1]};
+              if (ACT == 1) u = mmr::gelu_fast2(u);
+              v[rg] = u.x;
+              v[rg + 1] = u.y;
+            }
+            if constexpr (HAS_RES) {
+              const uint2 rv = rq[i][jj];
+              v[0] += __uint_as_float(rv.x << 16);
+              v[1] += __uint_as_float(rv.x & 0xFFFF0000u);
+              v[2] += __uint_as_float(rv.y << 16);
+              v[3] += __uint_as_float(rv.y & 0xFFFF0000u);
+            }
+            pk[h] = make_uint2(mmr::pack2bf(v[0], v[1]), mmr::pack2bf(v[2], v[3]));
+          }
+          const auto sx = __builtin_amdgcn_permlane16_swap(pk[0].x, pk[1].x, false, false);
+          const auto sy = __builtin_amdgcn_permlane16_swap(pk[0].y, pk[1].y, false, false);
+          const int col = n0 + wc * 16 * NT + 16 * j + (j2 != j && (efq & 1) ? 16 : 0) + (efq >> 1) * 8;
+          *(uint4*)(Y + row * N + col) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+        }
+      }
+    }
+#pragma unroll
+    for (int rd = 0; rd < (epi_pl ? 0 : 8 / C::RM); ++rd) {
 #pragma unroll
       for (int ii = 0; ii < C::RM; ++ii) {
         const int i = rd * C::RM + ii;
@@ -1277,6 +1331,13 @@ int p8_nck(int tm, int tn, int k, int tbn) {
   return 0;
 }
 
+// Epilogue of the 8-phase GEMM (see gemm_bf16_tn_p8): -1 = by epilogue kind (default), 0 = the
+// per-wave LDS staging, 1 = permlane row chunks from registers (A/B: MMR_P8_EPI).
+int p8_epi() {
+  const char* e = getenv("MMR_P8_EPI");
+  return e ? atoi(e) : -1;
+}
+
 template <int ACT, bool HB, bool HR>
 void launch(const uint16_t* x, const uint16_t* w, const float* b, const uint16_t* r, uint16_t* y,
             int64_t m, int n, int k, hipStream_t st, int w4, int cfg) {
@@ -1305,13 +1366,15 @@ void launch(const uint16_t* x, const uint16_t* w, const float* b, const uint16_t
     if (cfg == 7 && n % 256 == 0) {
       const int tm = (int)t256, tn = n / 256;
       gemm_bf16_tn_p8<4, ACT, HB, HR><<<dim3(std::max<int64_t>(8, std::min<int64_t>(grid, (int64_t)tm * tn) / 8 * 8)), dim3(512), P8<4>::LDS_B, st>>>(
-          x, w, b, r, y, m, n, k, tm, tn, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, p8_nck(tm, tn, k, 256));
+          x, w, b, r, y, m, n, k, tm, tn, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, p8_nck(tm, tn, k, 256),
+          p8_epi());
       return;
     }
     if (cfg == 8 && n % 192 == 0) {
       const int tm = (int)t256, tn = n / 192;
       gemm_bf16_tn_p8<3, ACT, HB, HR><<<dim3(std::max<int64_t>(8, std::min<int64_t>(grid, (int64_t)tm * tn) / 8 * 8)), dim3(512), P8<3>::LDS_B, st>>>(
-          x, w, b, r, y, m, n, k, tm, tn, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, p8_nck(tm, tn, k, 192));
+          x, w, b, r, y, m, n, k, tm, tn, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, p8_nck(tm, tn, k, 192),
+          p8_epi());
       return;
     }
   }

@@ -31,6 +31,8 @@ for s in $STEPS; do
       MMR_TOWER_STREAMS=0 MMR_FUSION_STREAMS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o full \
         -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof_full.log 2>&1
       echo prof ok ;;
+    epi)
+      timeout -k 10 300 python -u tools/gemm_ab.py --env MMR_P8_EPI --values 0,1 > $OUT/gemm_epi.txt 2>&1; cat $OUT/gemm_epi.txt ;;
     nck)
       timeout -k 10 300 python -u tools/gemm_nck.py > $OUT/gemm_nck.txt 2>&1; cat $OUT/gemm_nck.txt ;;
     *) echo "unknown step $s"; exit 2 ;;
