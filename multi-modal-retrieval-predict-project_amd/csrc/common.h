@@ -72,15 +72,17 @@ __device__ __forceinline__ float gelu_fast(float v) {
 }
 
 // gelu_fast on two values with packed f32 math (v_pk_fma / v_pk_mul / v_pk_add: half the VALU
-// issues of two scalar calls); same operations in the same order, so bitwise equal to gelu_fast.
+// issues of two scalar calls), with -log2(e) folded into P's coefficients (one v_pk_mul fewer;
+// equal to gelu_fast up to f32 rounding of the folded constants).
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2_t gelu_fast2(f32x2_t v) {
+  constexpr float L2E = -1.4426950408889634f;
   const f32x2_t x2 = v * v;
-  f32x2_t p = __builtin_elementwise_fma((f32x2_t)3.275317185739523e-06f, x2, (f32x2_t)-7.756018138382363e-05f);
-  p = __builtin_elementwise_fma(p, x2, (f32x2_t)-0.00016997469037563395f);
-  p = __builtin_elementwise_fma(p, x2, (f32x2_t)0.07280746695679054f);
-  p = __builtin_elementwise_fma(p, x2, (f32x2_t)1.5957042563586181f);
-  const f32x2_t y = ((f32x2_t)-1.4426950408889634f * v) * p;
+  f32x2_t p = __builtin_elementwise_fma((f32x2_t)(3.275317185739523e-06f * L2E), x2, (f32x2_t)(-7.756018138382363e-05f * L2E));
+  p = __builtin_elementwise_fma(p, x2, (f32x2_t)(-0.00016997469037563395f * L2E));
+  p = __builtin_elementwise_fma(p, x2, (f32x2_t)(0.07280746695679054f * L2E));
+  p = __builtin_elementwise_fma(p, x2, (f32x2_t)(1.5957042563586181f * L2E));
+  const f32x2_t y = v * p;
   f32x2_t e;
   e.x = __builtin_amdgcn_exp2f(y.x);
   e.y = __builtin_amdgcn_exp2f(y.y);

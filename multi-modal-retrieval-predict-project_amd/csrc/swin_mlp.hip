@@ -106,8 +106,7 @@ __device__ __forceinline__ float gelu_t(float v) {
 }
 
 // bias + GELU of two hidden values -> packed bf16 pair; FAST on packed f32 math (v_pk_add / v_pk_fma
-// / v_pk_mul: half the VALU issues — the kernel is VALU-bound on GELU), bitwise equal to the scalar
-// gelu_fast (same operations in the same order)
+// / v_pk_mul: half the VALU issues — the kernel is VALU-bound on GELU)
 template <bool FAST>
 __device__ __forceinline__ uint32_t gelu_pack(float a0, float a1, float b0, float b1) {
   if constexpr (FAST) {
@@ -115,6 +114,17 @@ __device__ __forceinline__ uint32_t gelu_pack(float a0, float a1, float b0, floa
     return mmr::pack2bf(u.x, u.y);
   } else {
     return mmr::pack2bf(gelu_t<FAST>(a0 + b0), gelu_t<FAST>(a1 + b1));
+  }
+}
+
+// GELU of two hidden values whose bias is already in the accumulator -> packed bf16 pair
+template <bool FAST>
+__device__ __forceinline__ uint32_t gelu_pack2(float a0, float a1) {
+  if constexpr (FAST) {
+    const mmr::f32x2_t u = mmr::gelu_fast2((mmr::f32x2_t){a0, a1});
+    return mmr::pack2bf(u.x, u.y);
+  } else {
+    return mmr::pack2bf(gelu_t<FAST>(a0), gelu_t<FAST>(a1));
   }
 }
 
@@ -215,9 +225,13 @@ __global__ __launch_bounds__(64 * NW) void swin_mlp(const uint16_t* __restrict__
     const unsigned char* W2s = W1s + G::W1B;
 #pragma unroll
     for (int t = 0; t < G::NT; ++t) {  // 32 hidden units per step
-      f32x16 a1;
+      f32x16 a1;  // starts at fc1's bias (lane: hidden HC*ch + 32t + 8i + 4h + rr)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) a1[e] = 0.f;
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 bb = *(const f32x4*)(Pb1 + HC * ch + 32 * t + 8 * i + 4 * h);
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) a1[4 * i + rr] = bb[rr];
+      }
       const int row = 32 * t + r;
 #pragma unroll
       for (int ks = 0; ks < G::KS1; ++ks) {
@@ -228,9 +242,8 @@ __global__ __launch_bounds__(64 * NW) void swin_mlp(const uint16_t* __restrict__
       uint32_t hp[8];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const f32x4 bb = *(const f32x4*)(Pb1 + HC * ch + 32 * t + 8 * i + 4 * h);
-        hp[2 * i] = gelu_pack<FAST>(a1[4 * i], a1[4 * i + 1], bb[0], bb[1]);
-        hp[2 * i + 1] = gelu_pack<FAST>(a1[4 * i + 2], a1[4 * i + 3], bb[2], bb[3]);
+        hp[2 * i] = gelu_pack2<FAST>(a1[4 * i], a1[4 * i + 1]);
+        hp[2 * i + 1] = gelu_pack2<FAST>(a1[4 * i + 2], a1[4 * i + 3]);
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {  // k-step over hidden 32t + 16 s2 .. +15
@@ -269,7 +282,7 @@ __global__ __launch_bounds__(64 * NW) void swin_mlp(const uint16_t* __restrict__
 // Resident-weight variant (C = 96: W1 + W2 = 147 KiB fit in one CU's LDS).  One workgroup per CU,
 // persistent: each wave walks 32-token tiles on its own (no barrier after the one-time weight
 // load), prefetching the next tile's x into registers while it computes the current one.
-template <int C, int NW, bool FAST, bool XRES>
+template <int C, int NW, bool FAST, bool XRES, bool PF = true>
 __global__ __launch_bounds__(64 * NW) void swin_mlp_res(const uint16_t* __restrict__ x,
                                                         const float* __restrict__ lng,
                                                         const float* __restrict__ lnb,
@@ -311,7 +324,7 @@ __global__ __launch_bounds__(64 * NW) void swin_mlp_res(const uint16_t* __restri
       dst[ks] = ok ? *(const bf16x8*)(xr + 16 * ks + 8 * h) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
   };
   bf16x8 xn[G::KS1];
-  load_x(tile, xn);
+  if constexpr (PF) load_x(tile, xn);
   __builtin_amdgcn_s_waitcnt(vmcnt_n(0));
   __builtin_amdgcn_s_waitcnt(0xC07F);
   asm volatile("" ::: "memory");
@@ -322,9 +335,13 @@ __global__ __launch_bounds__(64 * NW) void swin_mlp_res(const uint16_t* __restri
     asm volatile("" ::: "memory");  // keep the LN/bias parameter reads in the loop (LICM would pin
                                     // ~100 VGPRs of them across it)
     bf16x8 xr[G::KS1], xb[G::KS1];
+    if constexpr (PF) {
 #pragma unroll
-    for (int ks = 0; ks < G::KS1; ++ks) xr[ks] = xn[ks];
-    load_x(tile + stride, xn);  // next tile's x in flight during this one
+      for (int ks = 0; ks < G::KS1; ++ks) xr[ks] = xn[ks];
+      load_x(tile + stride, xn);  // next tile's x in flight during this one
+    } else {
+      load_x(tile, xr);  // (3 waves per SIMD hide the latency instead of a prefetch register set)
+    }
     const int64_t tok = tile * 32 + r;
 
     // LayerNorm (row split over the lane pair h = 0, 1) -> fc1 B operand
@@ -386,10 +403,48 @@ __global__ __launch_bounds__(64 * NW) void swin_mlp_res(const uint16_t* __restri
           f[s2 * G::NU + u] = *(const bf16x8*)(W2s + (c * G::U2 + unit_swz<G::U2>(c, q)) * 16);
         }
     };
-    bf16x8 w1f[G::KS1], w2f[2 * G::NU];
-    rd_w1(0, w1f);
+    if constexpr (!PF) {
+      // 3 waves per SIMD (register budget 168): fragments read just in time, no prefetch
+      // register sets — the co-resident waves hide the LDS latency
 #pragma unroll 1
-    for (int t = 0; t < 4 * C / 32; ++t) {  // 32 hidden units per step
+      for (int t = 0; t < 4 * C / 32; ++t) {
+        f32x16 a1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const f32x4 bb = *(const f32x4*)(Pb1 + 32 * t + 8 * i + 4 * h);
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) a1[4 * i + rr] = bb[rr];
+        }
+        {
+          bf16x8 w1f[G::KS1];
+          rd_w1(t, w1f);
+#pragma unroll
+          for (int ks = 0; ks < G::KS1; ++ks) a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1f[ks], xb[ks], a1, 0, 0, 0);
+        }
+        uint32_t hp[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          hp[2 * i] = gelu_pack2<FAST>(a1[4 * i], a1[4 * i + 1]);
+          hp[2 * i + 1] = gelu_pack2<FAST>(a1[4 * i + 2], a1[4 * i + 3]);
+        }
+        const unsigned char* W2s = smem + (t >> 1) * G::CHUNK_B + G::W1B;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 hf = __builtin_bit_cast(bf16x8, make_uint4(hp[4 * s2], hp[4 * s2 + 1], hp[4 * s2 + 2],
+                                                                  hp[4 * s2 + 3]));
+#pragma unroll
+          for (int u = 0; u < G::NU; ++u) {
+            const int c = 32 * u + r, q = 2 * (2 * (t & 1) + s2) + h;
+            const bf16x8 w = *(const bf16x8*)(W2s + (c * G::U2 + unit_swz<G::U2>(c, q)) * 16);
+            acc2[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w, hf, acc2[u], 0, 0, 0);
+          }
+        }
+      }
+    }
+    bf16x8 w1f[G::KS1], w2f[2 * G::NU];
+    if constexpr (PF) rd_w1(0, w1f);
+#pragma unroll 1
+    for (int t = 0; t < (PF ? 4 * C / 32 : 0); ++t) {  // 32 hidden units per step
       f32x16 a1;
 #pragma unroll
       for (int e = 0; e < 16; ++e) a1[e] = 0.f;
@@ -444,14 +499,14 @@ int cu_count() {
   return n;
 }
 
-template <int C, int NW, bool FAST, bool XRES>
+template <int C, int NW, bool FAST, bool XRES, bool PF = true>
 mmr_status launch_res(const uint16_t* x, const float* g, const float* b, const uint16_t* pack,
                       const float* b1, const float* b2, uint16_t* y, int64_t T, float eps,
                       hipStream_t st) {
   using G = MlpGeo<C, NW, 64, 2>;
   const int64_t wave_tiles = (T + 31) / 32;
   const int64_t grid = std::min<int64_t>(cu_count(), (wave_tiles + NW - 1) / NW);
-  swin_mlp_res<C, NW, FAST, XRES><<<dim3((unsigned)grid), 64 * NW, G::NCH * G::CHUNK_B + 7 * C * 4, st>>>(
+  swin_mlp_res<C, NW, FAST, XRES, PF><<<dim3((unsigned)grid), 64 * NW, G::NCH * G::CHUNK_B + 7 * C * 4, st>>>(
       x, g, b, pack, b1, b2, y, T, eps);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
@@ -505,7 +560,13 @@ mmr_status mmr_swin_mlp(const uint16_t* x, const float* ln_g, const float* ln_b,
   MMR_REQUIRE(x != y, "mmr_swin_mlp: in-place not supported");
   if (tokens == 0) return MMR_OK;
   hipStream_t st = mmr::as_stream(stream);
-  if (c == 96) return launch_res<96, 8, true, true>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
+  if (c == 96) {
+    // MMR_SWIN_MLP_CFG=1 (A/B): 12 waves (3 per SIMD) without the x prefetch / residual registers
+    const char* e = getenv("MMR_SWIN_MLP_CFG");
+    if (e && atoi(e) == 1) return launch_res<96, 12, true, false, false>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
+    if (e && atoi(e) == 2) return launch_res<96, 8, true, false, false>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
+    return launch_res<96, 8, true, true>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
+  }
   if (c == 192) return launch_stream<192, 8, 64, 3, true>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
   mmr::set_error("mmr_swin_mlp: C=%d not built (96, 192)", c);
   return MMR_ERR_UNSUPPORTED;

@@ -33,6 +33,8 @@ for s in $STEPS; do
       echo prof ok ;;
     epi)
       timeout -k 10 300 python -u tools/gemm_ab.py --env MMR_P8_EPI --values 0,1 > $OUT/gemm_epi.txt 2>&1; cat $OUT/gemm_epi.txt ;;
+    mlp)
+      timeout -k 10 300 python -u tools/mlp_ab.py 0,1,2 > $OUT/mlp_ab.txt 2>&1; cat $OUT/mlp_ab.txt ;;
     nck)
       timeout -k 10 300 python -u tools/gemm_nck.py > $OUT/gemm_nck.txt 2>&1; cat $OUT/gemm_nck.txt ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -1,0 +1,53 @@
+"""A/B of the fused Swin MLP variants (MMR_SWIN_MLP_CFG for C = 96) at the Swin-T stage-1 shape
+(B=256: 802,816 tokens), interleaved rounds in one process, each output checked against a torch
+fp32 reference of LN -> fc1 -> GELU(erf) -> fc2 + residual.  Diagnostic."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from mmr_amd import ops  # noqa: E402
+
+
+def timeit(fn, it=20):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(it):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / it * 1e3
+
+
+def main():
+    cfgs = (sys.argv[1] if len(sys.argv) > 1 else "0,1,2").split(",")
+    for C, T in ((96, 256 * 3136), (192, 256 * 784)):
+        g = torch.Generator(device="cuda").manual_seed(C)
+        x = torch.randn(T, C, device="cuda", generator=g).to(torch.bfloat16)
+        lg = 1 + 0.1 * torch.randn(C, device="cuda", generator=g)
+        lb = 0.1 * torch.randn(C, device="cuda", generator=g)
+        w1 = (0.05 * torch.randn(4 * C, C, device="cuda", generator=g)).to(torch.bfloat16)
+        w2 = (0.05 * torch.randn(C, 4 * C, device="cuda", generator=g)).to(torch.bfloat16)
+        b1 = 0.1 * torch.randn(4 * C, device="cuda", generator=g)
+        b2 = 0.1 * torch.randn(C, device="cuda", generator=g)
+        pack = ops.swin_mlp_pack(w1, w2)
+        n = 4096
+        h = F.layer_norm(x[:n].float(), (C,), lg, lb, 1e-5)
+        ref = x[:n].float() + F.linear(F.gelu(F.linear(h, w1.float(), b1)), w2.float(), b2)
+        res = {}
+        for _ in range(3):
+            for c in cfgs:
+                os.environ["MMR_SWIN_MLP_CFG"] = c
+                y = ops.swin_mlp(x, lg, lb, pack, b1, b2, 1e-5)
+                err = (y[:n].float() - ref).abs().max().item() / ref.abs().max().item()
+                assert err < 2e-2, (C, c, err)
+                res.setdefault(c, []).append(timeit(lambda: ops.swin_mlp(x, lg, lb, pack, b1, b2, 1e-5)))
+        print(f"C={C} T={T}: " + "  ".join(f"cfg{c} {min(v):.1f}us" for c, v in res.items()), flush=True)
+
+
+if __name__ == "__main__":
+    main()
