@@ -106,12 +106,22 @@ class ShardedIndex:
     exact list."""
 
     def __init__(self, gallery_rows, n_total, start, group=None, device=None, local_search=None, mode="x3",
-                 fallback_search=None, local_components=None):
+                 fallback_search=None, local_components=None, index=None, status_out=None):
+        """index: an existing GalleryIndex of this rank's rows (instead of building one from
+        gallery_rows).  status_out: a device int32 scalar that accumulates the max per-query
+        search status without a host sync (a benchmark loop checks it once afterwards; the
+        selection kernel resolves every overflow in-kernel, so the re-run path is a guard) —
+        with it, flagged queries are not re-run here."""
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.n_total, self.start = int(n_total), int(start)
-        self.index = None
+        self.index = index
+        self.status_out = status_out
+        if local_search is None and index is not None:
+            local_search = self._index_search
+            if fallback_search is None:
+                fallback_search = self._index_search_x3
         if local_search is None:
             self.index = GalleryIndex(gallery_rows, device=device, idx_base=start, mode=mode)
             local_search = self._index_search
@@ -147,6 +157,10 @@ class ShardedIndex:
         out = self.local_search(q, k)
         i, s64 = out[0], out[1]
         st = out[2] if len(out) > 2 else None
+        if st is not None and self.status_out is not None:
+            if st.numel():
+                torch.maximum(self.status_out, st.max().to(self.status_out.dtype), out=self.status_out)
+            return i, s64
         if st is not None and st.numel() and int(st.max().item()) != 0:
             if self.fallback_search is None:
                 check_status(st)
@@ -172,12 +186,10 @@ class ShardedIndex:
         dist.all_gather_into_tensor(gs, s64.contiguous(), group=self.group)
         gi = gi.view(self.world, i.shape[0], i.shape[1])
         gs = gs.view(self.world, s64.shape[0], s64.shape[1])
-        if gi.is_cuda:
-            mi, ms, m64 = merge_topk(gs, gi, k)
-        else:
-            mi, ms, m64 = merge_topk_host(gs, gi, k)
+        if gi.is_cuda:  # merge this rank's queries only
+            return merge_topk(gs, gi, k, q0=self.rank * b, nq=b)
         sl = slice(self.rank * b, (self.rank + 1) * b)
-        return mi[sl], ms[sl], m64[sl]
+        return merge_topk_host(gs[:, sl], gi[:, sl], k)
 
     def _components(self, q, cand, tables):
         """Raw rerank components of this shard's candidates (nq, kc, 3) f64."""
