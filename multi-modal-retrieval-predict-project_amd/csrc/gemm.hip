@@ -540,8 +540,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
                                                        const uint8_t* __restrict__ WS = nullptr,
                                                        uint8_t* __restrict__ YS = nullptr,
                                                        float* __restrict__ GM = nullptr, float* __restrict__ BM = nullptr,
-                                                       int64_t ldG = 0, int64_t ldB = 0, int64_t nval = 0,
-                                                       int nck = 0, int epi_mode = -1) {
+                                                       int64_t ldG = 0, int64_t ldB = 0, int64_t nval = 0) {
   static_assert(!OUT8 || (FP8 && NT == 4 && !HAS_RES), "OUT8: MX-fp8 256x256 tiles without residual");
   static_assert(KNN == 0 || ((KNN == 2 || KNN == 4) && NT == 4 && !FP8 && !HAS_BIAS && !HAS_RES && ACT == 0),
                 "KNN (rows per unit 2 / 4): plain 256x256 fp16 tiles");
@@ -557,37 +556,27 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   constexpr int ESZ = FP8 ? 1 : 2;                      // operand element bytes
   constexpr int NH0 = NT / 2;                           // n-tiles in n-half 0
   static_assert(C::NSTORE_LDS + 5 <= 63 && C::NSTORE_PL + 5 <= 63, "vmcnt range");
-  // Epilogue: permlane row chunks straight from registers (no LDS round trips) or the per-wave LDS
-  // staging.  epi_mode -1 (default) = permlane for GELU epilogues only: measured (random operands,
-  // profiles/r03_gemm_epilogue_ab.txt) FFN1 + GELU 925 -> 1015 TF, Swin fc1 + GELU +8 %, but the
-  // plain / residual epilogues 3-7 % slower than the LDS path (QKV 1041 vs 947 TF at 256 x 192);
-  // 0 / 1 force LDS / permlane (MMR_P8_EPI, A/B).  OUT8 / KNN always use their own epilogues.
-  const bool epi_pl = !OUT8 && !KNN && (epi_mode < 0 ? ACT == 1 : epi_mode != 0);
-  const int nstore = epi_pl ? C::NSTORE_PL : C::NSTORE_LDS;
+  // Epilogue: permlane row chunks straight from registers (no LDS round trips) for GELU epilogues,
+  // the per-wave LDS staging otherwise: measured (random operands, profiles/r03_gemm_epilogue_ab.txt)
+  // FFN1 + GELU 925 -> 1015 TF and Swin fc1 + GELU +8 % with permlane, but the plain / residual
+  // epilogues 3-7 % slower than with the LDS path (QKV 1041 vs 947 TF at 256 x 192: its 16 rows x
+  // 64 B stores are twice the L2 write requests of the LDS path's 8 rows x 128 B).  OUT8 / KNN keep
+  // their own epilogues.
+  constexpr bool epi_pl = !OUT8 && !KNN && ACT == 1;
+  constexpr int nstore = epi_pl ? C::NSTORE_PL : C::NSTORE_LDS;
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
 
   const int ntiles = tiles_m * tiles_n;
   const int per = gridDim.x / 8, xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
-  // Tile order.  nck = 0: the XCD's share is a contiguous run of the row-major (m, n) tile grid
-  // (the 32 concurrent tiles of an XCD span ~32 / tiles_n X panels and every W panel).  nck > 0:
-  // the XCD owns whole X panels [plo, phi) and walks them in n-chunks of nck W panels — every panel
-  // of the chunk, then the next chunk — so a chunk of W (nck x 256 x K) stays in the XCD's L2 while
-  // its X panels stream past once per chunk (W fetched once per XCD instead of once per round).
-  const int plo = (int)((int64_t)tiles_m * xcd / 8), phi = (int)((int64_t)tiles_m * (xcd + 1) / 8);
-  const int lo = nck > 0 ? plo * tiles_n : (int)((int64_t)ntiles * xcd / 8);
-  const int hi = nck > 0 ? phi * tiles_n : (int)((int64_t)ntiles * (xcd + 1) / 8);
+  // Tile order: the XCD's share is a contiguous run of the row-major (m, n) tile grid (the 32
+  // concurrent tiles of an XCD share X panels; W panels are re-read from the MALL once per round of
+  // concurrent tiles).  An n-chunked order that keeps a slice of W resident in the XCD's L2 (W read
+  // once per XCD) measured 1-6 % slower on every BERT shape (profiles/r03_gemm_tile_order_ab.txt).
+  const int lo = (int)((int64_t)ntiles * xcd / 8), hi = (int)((int64_t)ntiles * (xcd + 1) / 8);
   int t = lo + slot;
   if (t >= hi) return;
-  auto mof = [&](int tile) -> int {
-    if (nck <= 0) return tile / tiles_n;
-    const int u = tile - lo, P = phi - plo, k = u / (P * nck), w = min(nck, tiles_n - k * nck);
-    return plo + (u - k * P * nck) / w;
-  };
-  auto nof = [&](int tile) -> int {
-    if (nck <= 0) return tile % tiles_n;
-    const int u = tile - lo, P = phi - plo, k = u / (P * nck), w = min(nck, tiles_n - k * nck);
-    return k * nck + (u - k * P * nck) % w;
-  };
+  auto mof = [&](int tile) -> int { return tile / tiles_n; };
+  auto nof = [&](int tile) -> int { return tile % tiles_n; };
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably uniform: SGPR LDS bases
@@ -784,10 +773,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
         issue(2 * p);
         if (p == 3) {  // end of s6: O complete (younger: E pieces, + last tile's stores at it 0)
           if (!loads) __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
-          else if (it == 0 && !first) {
-            if (nstore == C::NSTORE_PL) __builtin_amdgcn_s_waitcnt(vmcnt_imm(5 + C::NSTORE_PL));
-            else __builtin_amdgcn_s_waitcnt(vmcnt_imm(5 + C::NSTORE_LDS));
-          }
+          else if (it == 0 && !first) __builtin_amdgcn_s_waitcnt(vmcnt_imm(5 + nstore));
           else __builtin_amdgcn_s_waitcnt(vmcnt_imm(5));
         } else if (p == 7) {  // end of s14: E complete (younger: 5 O pieces)
           if (loads) __builtin_amdgcn_s_waitcnt(vmcnt_imm(5));
@@ -902,7 +888,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
         for (int j = 0; j < NT; ++j)
           rq[i][j] = *(const uint2*)(R + (m0 + wr * 128 + i * 16 + efr) * N + n0 + wc * 16 * NT + j * 16 + efq * 4);
     }
-    if (epi_pl) {
+    if constexpr (epi_pl) {
       // C^T fragment -> 16-B row chunks in registers: for an n-tile pair (j, j + 1) one
       // v_permlane16_swap per dword hands lane group fq = 1 (3) the pair's tile-(j+1) columns
       // 0-3 (8-11) of fq = 0 (2) and takes back tile j's columns 4-7 (12-15), so every lane holds
@@ -944,7 +930,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
       }
     }
 #pragma unroll
-    for (int rd = 0; rd < (epi_pl ? 0 : 8 / C::RM); ++rd) {
+    for (int rd = 0; rd < (epi_pl ? 0 : 8 / C::RM); ++rd) {  // LDS-staged rounds
 #pragma unroll
       for (int ii = 0; ii < C::RM; ++ii) {
         const int i = rd * C::RM + ii;
@@ -1317,27 +1303,6 @@ constexpr int kVariants = 11;
 constexpr int kVarW4[kVariants] = {1, 2, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 constexpr int kVarCfg[kVariants] = {1, 1, 1, 2, 3, 4, 5, 6, 0, 7, 8};
 
-// n-chunk width of the 8-phase GEMM's tile order (see gemm_bf16_tn_p8): MMR_P8_NCK=c selects
-// n-chunks of c W panels per XCD, default 0 = the row-major order.  The chunked order cuts the
-// modelled L2-miss bytes of FFN1 / QKV by ~2x (W fetched once per XCD instead of once per round of
-// 32 concurrent tiles) but measured 1-6 % SLOWER on every BERT shape (profiles/r03_gemm_tile_order_ab.txt):
-// those misses are served by the 256 MB MALL and the kernel is not bound by them.
-int p8_nck(int tm, int tn, int k, int tbn) {
-  (void)tm;
-  (void)tn;
-  (void)k;
-  (void)tbn;
-  if (const char* e = getenv("MMR_P8_NCK")) return atoi(e);
-  return 0;
-}
-
-// Epilogue of the 8-phase GEMM (see gemm_bf16_tn_p8): -1 = by epilogue kind (default), 0 = the
-// per-wave LDS staging, 1 = permlane row chunks from registers (A/B: MMR_P8_EPI).
-int p8_epi() {
-  const char* e = getenv("MMR_P8_EPI");
-  return e ? atoi(e) : -1;
-}
-
 template <int ACT, bool HB, bool HR>
 void launch(const uint16_t* x, const uint16_t* w, const float* b, const uint16_t* r, uint16_t* y,
             int64_t m, int n, int k, hipStream_t st, int w4, int cfg) {
@@ -1366,15 +1331,13 @@ void launch(const uint16_t* x, const uint16_t* w, const float* b, const uint16_t
     if (cfg == 7 && n % 256 == 0) {
       const int tm = (int)t256, tn = n / 256;
       gemm_bf16_tn_p8<4, ACT, HB, HR><<<dim3(std::max<int64_t>(8, std::min<int64_t>(grid, (int64_t)tm * tn) / 8 * 8)), dim3(512), P8<4>::LDS_B, st>>>(
-          x, w, b, r, y, m, n, k, tm, tn, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, p8_nck(tm, tn, k, 256),
-          p8_epi());
+          x, w, b, r, y, m, n, k, tm, tn);
       return;
     }
     if (cfg == 8 && n % 192 == 0) {
       const int tm = (int)t256, tn = n / 192;
       gemm_bf16_tn_p8<3, ACT, HB, HR><<<dim3(std::max<int64_t>(8, std::min<int64_t>(grid, (int64_t)tm * tn) / 8 * 8)), dim3(512), P8<3>::LDS_B, st>>>(
-          x, w, b, r, y, m, n, k, tm, tn, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, p8_nck(tm, tn, k, 192),
-          p8_epi());
+          x, w, b, r, y, m, n, k, tm, tn);
       return;
     }
   }

@@ -30,11 +30,21 @@ for s in $STEPS; do
     prof)
       MMR_TOWER_STREAMS=0 MMR_FUSION_STREAMS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o full \
         -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof_full.log 2>&1
-      echo prof ok ;;
+      f=$(find $OUT/prof -name "*kernel_stats.csv" | head -1); python tools/prof_csv_summary.py "$f" > $OUT/prof_summary.txt 2>&1 || cp "$f" $OUT/prof_summary.txt
+      head -45 $OUT/prof_summary.txt ;;
     epi)
       timeout -k 10 300 python -u tools/gemm_ab.py --env MMR_P8_EPI --values 0,1 > $OUT/gemm_epi.txt 2>&1; cat $OUT/gemm_epi.txt ;;
     mlp)
       timeout -k 10 300 python -u tools/mlp_ab.py 0,1,2 > $OUT/mlp_ab.txt 2>&1; cat $OUT/mlp_ab.txt ;;
+    abr02)  # same-box A/B of the cfg2 step: this tree's libmmr vs round 2's (tools/ab/libmmr_r02.so)
+      for i in 1 2; do
+        for lib in new old; do
+          if [ $lib = old ]; then export MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/libmmr_r02.so; else unset MMR_LIBMMR; fi
+          timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 30 > $OUT/ab_${lib}_$i.json 2> $OUT/ab_${lib}_$i.err
+          python -c "import json;d=json.load(open('$OUT/ab_${lib}_$i.json'));print('$lib',round(d['ms_per_step'],3),{k:round(v['ms_per_launch']*1e3,1) for k,v in d['roofline']['bert_gemms'].items()})"
+        done
+      done
+      unset MMR_LIBMMR ;;
     nck)
       timeout -k 10 300 python -u tools/gemm_nck.py > $OUT/gemm_nck.txt 2>&1; cat $OUT/gemm_nck.txt ;;
     *) echo "unknown step $s"; exit 2 ;;
