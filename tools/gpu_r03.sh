@@ -45,6 +45,11 @@ for s in $STEPS; do
         done
       done
       unset MMR_LIBMMR ;;
+    prof5)
+      MMR_TOWER_STREAMS=0 MMR_FUSION_STREAMS=0 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof5 -o cfg5 \
+        -- python3 bench.py --preset cfg5 --steps 4 --warmup 2 --no-cpu-baseline > $OUT/prof5.log 2>&1
+      f=$(find $OUT/prof5 -name "*kernel_stats.csv" | head -1); python tools/prof_csv_summary.py "$f" > $OUT/prof5_summary.txt 2>&1 || cp "$f" $OUT/prof5_summary.txt
+      head -45 $OUT/prof5_summary.txt ;;
     nck)
       timeout -k 10 300 python -u tools/gemm_nck.py > $OUT/gemm_nck.txt 2>&1; cat $OUT/gemm_nck.txt ;;
     *) echo "unknown step $s"; exit 2 ;;
