@@ -614,14 +614,16 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   // it with its first piece of that K-tile, so every count-based wait below still covers it
   const auto xsr = __builtin_amdgcn_make_buffer_rsrc((void*)XS, 0, 0x7FFFFFFF, 0x00020000);
   const auto wsr = __builtin_amdgcn_make_buffer_rsrc((void*)WS, 0, 0x7FFFFFFF, 0x00020000);
-  auto gS = [&](int tile, int buf, int kt) {
+  // a tile's scale-panel base (K-tile 0) in bytes, for wave 0 (X's) / wave 1 (W's) / others (unused);
+  // computed once per tile: in the K loop the tile's division would be re-done per K-tile (SALU)
+  auto sbase = [&](int tile) -> int {
+    return FP8 ? (wave == 0 ? mof(tile) : nof(tile)) * nk * 1024 : 0;
+  };
+  auto gS = [&](int sb, int buf, int kt) {
     if constexpr (FP8) {
-      if (wave == 0)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xsr, (lds_ptr_t)(dsm + soff(buf)), 16, lane * 16,
-                                                 (mof(tile) * nk + kt) * 1024, 0, 0);
-      else if (wave == 1)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(wsr, (lds_ptr_t)(dsm + soff(buf) + 512), 16, lane * 16,
-                                                 (nof(tile) * nk + kt) * 1024, 0, 0);
+      if (wave < 2)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wave == 0 ? xsr : wsr, (lds_ptr_t)(dsm + soff(buf) + wave * 512), 16,
+                                                 lane * 16, sb + kt * 1024, 0, 0);
     }
   };
   auto gA = [&](__amdgpu_buffer_rsrc_t xb, int buf, int j, int kt) {
@@ -689,8 +691,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
 
   // prologue: K-tile 0 -> E, K-tile 1 -> O of the first tile
   bias_dma(t, 0);
-  gS(t, 0, 0);
-  gS(t, 1, 1);
+  gS(sbase(t), 0, 0);
+  gS(sbase(t), 1, 1);
   {
     const auto xb = xbase(t);
     const auto wb = wbase(t);
@@ -719,6 +721,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
     const auto wn = wbase(has_next ? tnext : t);
     const int n0 = nof(t) * TBN;
     const int64_t m0 = (int64_t)mof(t) * 256;
+    const int sbc = sbase(t), sbn = sbase(has_next ? tnext : t);
 
     f32x4 acc[8][NT];
 #pragma unroll
@@ -758,13 +761,13 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
         auto issue = [&](int sg) {
           if (loads) {
             if (sg == 2) gA(xl, 0, 0, ke);
-            if (sg == 3) { gS(last_it ? tnext : t, 0, ke); gA(xl, 0, 2, ke); }
+            if (sg == 3) { gS(last_it ? sbn : sbc, 0, ke); gA(xl, 0, 2, ke); }
             if (sg == 5) gB(wl, 0, 0, ke);
             if (sg == 6) { gB(wl, 0, 1, ke); gA(xl, 0, 1, ke); }
             if (sg == 7) { gB(wl, 0, 2, ke); gA(xl, 0, 3, ke); }
             if (sg == 8 && NT == 4) gB(wl, 0, 3, ke);
             if (sg == 10) gA(xl, 1, 0, ko);
-            if (sg == 11) { gS(last_it ? tnext : t, 1, ko); gA(xl, 1, 2, ko); }
+            if (sg == 11) { gS(last_it ? sbn : sbc, 1, ko); gA(xl, 1, 2, ko); }
             if (sg == 13) gB(wl, 1, 0, ko);
             if (sg == 14) { gB(wl, 1, 1, ko); gA(xl, 1, 1, ko); }
             if (sg == 15) { gB(wl, 1, 2, ko); gA(xl, 1, 3, ko); if (NT == 4) gB(wl, 1, 3, ko); }

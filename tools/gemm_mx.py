@@ -38,5 +38,5 @@ for M, N, K, act in SHAPES:
     t_q = timeit(lambda: ops.quantize_mxfp8(x, layout=0))
     fl = 2.0 * M * N * K
     print(f"M={M:6d} N={N:5d} K={K:5d} act={act} | bf16 {t_bf:7.1f}us {fl / t_bf / 1e6:5.0f}TF | mxfp8 {t_mx:7.1f}us "
-          f"{fl / t_mx / 1e6:5.0f}TF | quantise x {t_q:6.1f}us ({M * K * 3 / t_q / 1e6:5.0f} GB/s)", flush=True)
+          f"{fl / t_mx / 1e6:5.0f}TF | quantise x {t_q:6.1f}us ({M * K * 3 / t_q / 1e6:5.2f} TB/s)", flush=True)
     del x, w, x8, w8, y

@@ -50,6 +50,18 @@ for s in $STEPS; do
         -- python3 bench.py --preset cfg5 --steps 4 --warmup 2 --no-cpu-baseline > $OUT/prof5.log 2>&1
       f=$(find $OUT/prof5 -name "*kernel_stats.csv" | head -1); python tools/prof_csv_summary.py "$f" > $OUT/prof5_summary.txt 2>&1 || cp "$f" $OUT/prof5_summary.txt
       head -45 $OUT/prof5_summary.txt ;;
+    mxab)  # same-box A/B of the MX-fp8 / bf16 GEMMs: this tree's libmmr vs tools/ab/libmmr_head.so
+      for i in 1 2; do
+        for lib in new old; do
+          if [ $lib = old ]; then export MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/libmmr_head.so; else unset MMR_LIBMMR; fi
+          echo "== $lib $i" >> $OUT/mxab.txt
+          timeout -k 10 300 python -u tools/gemm_mx.py >> $OUT/mxab.txt 2>&1
+        done
+      done
+      unset MMR_LIBMMR; cat $OUT/mxab.txt ;;
+    clk)  # effective clock per GEMM kernel (GRBM_GUI_ACTIVE / 8 / duration), bf16 vs MX-fp8
+      timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $OUT/clk -o clk -- python3 tools/clock_probe.py > $OUT/clk.log 2>&1
+      f=$(find $OUT/clk -name "*counter_collection.csv" | head -1); python tools/clock_summary.py "$f" > $OUT/clk.txt 2>&1; cat $OUT/clk.txt ;;
     nck)
       timeout -k 10 300 python -u tools/gemm_nck.py > $OUT/gemm_nck.txt 2>&1; cat $OUT/gemm_nck.txt ;;
     *) echo "unknown step $s"; exit 2 ;;
