@@ -507,8 +507,21 @@ struct P8 {
   static constexpr int NSTORE_PL = 8 * ((NT + 1) / 2);
   static constexpr size_t BUF_B = (size_t)(256 + TBN) * 64 * 2 + SC * 2;
   static constexpr size_t EPI_B = 8ull * 16 * RM * ELD * 2;
-  static constexpr size_t LDS_B = 2 * BUF_B + EPI_B + 2 * TBN * 4;
+#ifdef MMR_P8_STAMPS
+  static constexpr size_t STAMP_B = 8 * 8 * 4 * 8;  // diagnostic build: [wave][tile < 8][4] u64 clocks
+#else
+  static constexpr size_t STAMP_B = 0;
+#endif
+  static constexpr size_t LDS_B = 2 * BUF_B + EPI_B + 2 * TBN * 4 + STAMP_B;
 };
+
+#ifdef MMR_P8_STAMPS
+// Diagnostic build only (tools/p8_stamps.py): per workgroup, wave and tile (first 8 tiles) the shader
+// clock at the tile's start, at the end of its K loop and at the end of its epilogue, plus the
+// 100 MHz real-time clock at the tile start — buffered in LDS (no vmcnt traffic in the loop),
+// written out at the kernel's end.
+__device__ unsigned long long p8_stamps[1024 * 8 * 8 * 4];
+#endif
 
 // FP8 = true: the MX-fp8 form (OCP e4m3 operands, one E8M0 scale per 32 consecutive k of a row;
 // gfx950 v_mfma_scale_f32_16x16x128_f8f6f4).  A K-tile is then 128 k = the same 128-byte LDS rows,
@@ -711,6 +724,16 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
 
   bool first = true;
   int par = 0;
+#ifdef MMR_P8_STAMPS
+  unsigned long long* lst = (unsigned long long*)((char*)dsm + C::LDS_B - C::STAMP_B);
+  int tcount = 0;
+  auto stamp = [&](int k) {
+    const unsigned long long v = k == 3 ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();
+    if (lane == 0 && tcount < 8) lst[(wave * 8 + tcount) * 4 + k] = v;
+  };
+#else
+  auto stamp = [](int) {};
+#endif
   uint32_t sca[2] = {0u, 0u}, scb = 0u;  // FP8: this K-tile's E8M0 scales (m-tile i: byte i of sca; n-tile j: byte j of scb)
   while (true) {
     const int tnext = t + per;
@@ -722,6 +745,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
     const int n0 = nof(t) * TBN;
     const int64_t m0 = (int64_t)mof(t) * 256;
     const int sbc = sbase(t), sbn = sbase(has_next ? tnext : t);
+    stamp(3);
+    stamp(0);
 
     f32x4 acc[8][NT];
 #pragma unroll
@@ -741,11 +766,16 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
         // ---- load segment (s = 2p)
         if (q == 0) {
           if constexpr (FP8) {
+            // native vector types on purpose: a HIP uint2 (struct) LDS read carries no TBAA, and hipcc
+            // then waits vmcnt(0) for every in-flight LDS-DMA before it (drained the K-tile prefetch
+            // at every K-tile: fp8 phases ran ~30 % longer than bf16's)
+            typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+            typedef uint32_t u32x1_t __attribute__((ext_vector_type(1)));
             const uint8_t* sb = (const uint8_t*)(dsm + soff(buf));
-            const uint2 sa2 = *(const uint2*)(sb + ((wr * 4 + fq) * 16 + fr) * 8);
-            sca[0] = sa2.x;
-            sca[1] = sa2.y;
-            scb = *(const uint32_t*)(sb + 1024 + ((wc * 4 + fq) * 16 + fr) * 4);
+            const u32x2_t sa2 = *(const u32x2_t*)(sb + ((wr * 4 + fq) * 16 + fr) * 8);
+            sca[0] = sa2[0];
+            sca[1] = sa2[1];
+            scb = (*(const u32x1_t*)(sb + 1024 + ((wc * 4 + fq) * 16 + fr) * 4))[0];
           }
 #pragma unroll
           for (int i = 0; i < 4; ++i) ldA(buf, i, i);
@@ -839,6 +869,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
       }
     }
 
+    stamp(1);
     // ---- epilogue (per wave, no workgroup barrier): C^T tiles (operands swapped) — lane has row
     // 16i + fr, columns 16j + 4fq + 0..3 — act(acc + bias) (+ residual) in f32 -> bf16 in the wave's
     // LDS area, RM m-tiles at a time -> 16-B row chunks -> Y
@@ -1008,6 +1039,10 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_wave_barrier();
     }
+    stamp(2);
+#ifdef MMR_P8_STAMPS
+    ++tcount;
+#endif
     if (!has_next) break;
     par ^= 1;
     bias_dma(tnext, par);
@@ -1016,6 +1051,11 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   }
   if (wr == 0) barrier();  // balance the stagger
   __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+#ifdef MMR_P8_STAMPS
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __syncthreads();
+  if (blockIdx.x < 1024 && tid < 8 * 8 * 4) p8_stamps[blockIdx.x * 256 + tid] = lst[tid];
+#endif
 #endif
 }
 
@@ -1447,6 +1487,12 @@ int tuned_variant(int64_t m, int n, int k, int act, bool hb, bool hr, const void
 }
 
 }  // namespace
+
+#ifdef MMR_P8_STAMPS
+extern "C" int mmr_diag_p8_stamps(unsigned long long* out, int64_t n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(p8_stamps), (size_t)std::min<int64_t>(n, 1024 * 256) * 8) == hipSuccess ? 0 : 1;
+}
+#endif
 
 extern "C" int32_t mmr_linear_bf16_variant(int64_t m, int32_t n, int32_t k, int32_t act, int32_t has_bias,
                                            int32_t has_residual) {

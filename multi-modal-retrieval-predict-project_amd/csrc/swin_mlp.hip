@@ -489,6 +489,201 @@ __global__ __launch_bounds__(64 * NW) void swin_mlp_res(const uint16_t* __restri
   }
 }
 
+// Software-pipelined resident variant (C = 96): iteration t runs fc1 of hidden block t+1 and fc2 of
+// block t-1 (12 MFMAs) beside the bias'd GELU of block t (VALU) — three mutually independent
+// streams in one basic block, so the matrix pipe works under the GELU instead of waiting for it
+// (the forms above serialise fc1 -> GELU -> fc2 inside a wave and rely on other waves to fill the
+// gaps).  2 waves per SIMD (<= 256 VGPRs: two fc1 accumulators, both packed hidden sets, the fc2
+// accumulators, the LN'd x of this tile and the next tile's x; the residual is re-read from L2).
+template <int C, int NW, bool FAST>
+__global__ __launch_bounds__(64 * NW) void swin_mlp_sp(const uint16_t* __restrict__ x,
+                                                       const float* __restrict__ lng,
+                                                       const float* __restrict__ lnb,
+                                                       const uint16_t* __restrict__ pack,
+                                                       const float* __restrict__ b1,
+                                                       const float* __restrict__ b2,
+                                                       uint16_t* __restrict__ y, int64_t T, float eps) {
+  using G = MlpGeo<C, NW, 64, 2>;
+  constexpr int WB = G::NCH * G::CHUNK_B;
+  constexpr int PWW = WB / 1024 / NW;
+  constexpr int NB = 4 * C / 32;  // 32-wide hidden blocks
+  static_assert(WB % (1024 * NW) == 0, "weights must split evenly over the waves");
+  static_assert(NB >= 3, "pipeline depth");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* Pg = (float*)(smem + WB);
+  const float* Pb = Pg + C;
+  const float* Pb1 = Pg + 2 * C;
+  const float* Pb2 = Pg + 6 * C;
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t ntile = (T + 31) / 32, stride = (int64_t)gridDim.x * NW;
+  int64_t tile = (int64_t)blockIdx.x * NW + wave;
+
+  for (int i = threadIdx.x; i < 7 * C; i += 64 * NW)
+    Pg[i] = i < C ? lng[i] : (i < 2 * C ? lnb[i - C] : (i < 6 * C ? b1[i - 2 * C] : b2[i - 6 * C]));
+#pragma unroll
+  for (int p = 0; p < PWW; ++p) {
+    const int piece = wave * PWW + p;
+    __builtin_amdgcn_global_load_lds((const void*)((const unsigned char*)pack + piece * 1024 + lane * 16),
+                                     (lds_ptr_t)(smem + piece * 1024), 16, 0, 0);
+  }
+  auto load_x = [&](int64_t tl, bf16x8* dst) {
+    const int64_t tk = tl * 32 + r;
+    const bool ok = tl < ntile && tk < T;
+    const uint16_t* xr = x + (ok ? tk : 0) * C;
+#pragma unroll
+    for (int ks = 0; ks < G::KS1; ++ks) {
+      const bf16x8 v = *(const bf16x8*)(xr + 16 * ks + 8 * h);  // clamped row: unconditional load
+      dst[ks] = ok ? v : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  };
+  bf16x8 xn[G::KS1];
+  load_x(tile, xn);
+  __builtin_amdgcn_s_waitcnt(vmcnt_n(0));
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  // fc1 of hidden block t (bias in the accumulator): lane holds hidden 32t + 8i + 4h + rr of token r
+  auto fc1 = [&](int t, const bf16x8* xb) {
+    f32x16 a;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f32x4 bb = *(const f32x4*)(Pb1 + 32 * t + 8 * i + 4 * h);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) a[4 * i + rr] = bb[rr];
+    }
+    const unsigned char* W1s = smem + (t >> 1) * G::CHUNK_B;
+    const int row = 32 * (t & 1) + r;
+    bf16x8 w[G::KS1];
+#pragma unroll
+    for (int ks = 0; ks < G::KS1; ++ks)
+      w[ks] = *(const bf16x8*)(W1s + (row * G::U1 + unit_swz<G::U1>(row, 2 * ks + h)) * 16);
+#pragma unroll
+    for (int ks = 0; ks < G::KS1; ++ks) a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[ks], xb[ks], a, 0, 0, 0);
+    return a;
+  };
+  auto gelu = [&](const f32x16& a, uint32_t* hp) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      hp[2 * i] = gelu_pack2<FAST>(a[4 * i], a[4 * i + 1]);
+      hp[2 * i + 1] = gelu_pack2<FAST>(a[4 * i + 2], a[4 * i + 3]);
+    }
+  };
+  auto fc2 = [&](int t, const uint32_t* hp, f32x16* acc2) {
+    const unsigned char* W2s = smem + (t >> 1) * G::CHUNK_B + G::W1B;
+    bf16x8 w[2 * G::NU];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int u = 0; u < G::NU; ++u) {
+        const int c = 32 * u + r, q = 2 * (2 * (t & 1) + s2) + h;
+        w[s2 * G::NU + u] = *(const bf16x8*)(W2s + (c * G::U2 + unit_swz<G::U2>(c, q)) * 16);
+      }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 hf = __builtin_bit_cast(bf16x8, make_uint4(hp[4 * s2], hp[4 * s2 + 1], hp[4 * s2 + 2], hp[4 * s2 + 3]));
+#pragma unroll
+      for (int u = 0; u < G::NU; ++u)
+        acc2[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[s2 * G::NU + u], hf, acc2[u], 0, 0, 0);
+    }
+  };
+
+  for (; tile < ntile; tile += stride) {
+    asm volatile("" ::: "memory");  // keep the parameter reads in the loop (LICM would pin them)
+    bf16x8 xr[G::KS1], xb[G::KS1];
+#pragma unroll
+    for (int ks = 0; ks < G::KS1; ++ks) xr[ks] = xn[ks];
+    load_x(tile + stride, xn);  // next tile's x in flight during this one
+    const int64_t tok = tile * 32 + r;
+
+    // LayerNorm (row split over the lane pair h = 0, 1) -> fc1 B operand
+    {
+      float s = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += mmr::bf2f((uint16_t)xr[ks][j]);
+      s += __shfl_xor(s, 32, 64);
+      const float mean = s * (1.0f / C);
+      float ss = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = mmr::bf2f((uint16_t)xr[ks][j]) - mean;
+          ss += d * d;
+        }
+      ss += __shfl_xor(ss, 32, 64);
+      const float rstd = rsqrtf(ss * (1.0f / C) + eps);
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks) {
+        const int k0 = 16 * ks + 8 * h;
+        const f32x4 g0 = *(const f32x4*)(Pg + k0), g1 = *(const f32x4*)(Pg + k0 + 4);
+        const f32x4 c0 = *(const f32x4*)(Pb + k0), c1 = *(const f32x4*)(Pb + k0 + 4);
+        const float gg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+        const float cc[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (mmr::bf2f((uint16_t)xr[ks][j]) - mean) * rstd * gg[j] + cc[j];
+        xb[ks] = __builtin_bit_cast(bf16x8, make_uint4(mmr::pack2bf(v[0], v[1]), mmr::pack2bf(v[2], v[3]),
+                                                       mmr::pack2bf(v[4], v[5]), mmr::pack2bf(v[6], v[7])));
+      }
+    }
+
+    f32x16 acc2[G::NU];
+#pragma unroll
+    for (int u = 0; u < G::NU; ++u)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc2[u][e] = 0.f;
+
+    // pipeline: a1 = fc1(t) ready at the top of iteration t; hp = GELU(t - 1) packed
+    f32x16 a1 = fc1(0, xb);
+    uint32_t hp[8];
+    {
+      const f32x16 an = fc1(1, xb);
+      gelu(a1, hp);
+      a1 = an;
+    }
+#pragma unroll 1
+    for (int t = 1; t < NB - 1; ++t) {
+      const f32x16 an = fc1(t + 1, xb);
+      uint32_t hn[8];
+      gelu(a1, hn);
+      fc2(t - 1, hp, acc2);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) hp[e] = hn[e];
+      a1 = an;
+    }
+    {
+      uint32_t hn[8];
+      gelu(a1, hn);
+      fc2(NB - 2, hp, acc2);
+      fc2(NB - 1, hn, acc2);
+    }
+
+    // y = x + b2 + fc2: lane half h holds channels 32u + 16 half + 8h + 0..7 (w2_channel order)
+    if (tok < T) {
+#pragma unroll
+      for (int u = 0; u < G::NU; ++u)
+#pragma unroll
+        for (int hf2 = 0; hf2 < 2; ++hf2) {
+          const int c0 = 32 * u + 16 * hf2 + 8 * h;
+          const f32x4 bl = *(const f32x4*)(Pb2 + c0), bh = *(const f32x4*)(Pb2 + c0 + 4);
+          const bf16x8 xv = *(const bf16x8*)(x + tok * C + c0);  // residual re-read (L2): no registers held
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            v[j] = acc2[u][8 * hf2 + j] + (j < 4 ? bl[j] : bh[j - 4]) + mmr::bf2f((uint16_t)xv[j]);
+          *(uint4*)(y + tok * C + c0) = make_uint4(mmr::pack2bf(v[0], v[1]), mmr::pack2bf(v[2], v[3]),
+                                                   mmr::pack2bf(v[4], v[5]), mmr::pack2bf(v[6], v[7]));
+        }
+    }
+  }
+}
+
 int cu_count() {
   static int n = [] {
     int dev = 0, v = 0;
@@ -507,6 +702,18 @@ mmr_status launch_res(const uint16_t* x, const float* g, const float* b, const u
   const int64_t wave_tiles = (T + 31) / 32;
   const int64_t grid = std::min<int64_t>(cu_count(), (wave_tiles + NW - 1) / NW);
   swin_mlp_res<C, NW, FAST, XRES, PF><<<dim3((unsigned)grid), 64 * NW, G::NCH * G::CHUNK_B + 7 * C * 4, st>>>(
+      x, g, b, pack, b1, b2, y, T, eps);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+template <int C, int NW, bool FAST>
+mmr_status launch_sp(const uint16_t* x, const float* g, const float* b, const uint16_t* pack,
+                     const float* b1, const float* b2, uint16_t* y, int64_t T, float eps, hipStream_t st) {
+  using G = MlpGeo<C, NW, 64, 2>;
+  const int64_t wave_tiles = (T + 31) / 32;
+  const int64_t grid = std::min<int64_t>(cu_count(), (wave_tiles + NW - 1) / NW);
+  swin_mlp_sp<C, NW, FAST><<<dim3((unsigned)grid), 64 * NW, G::NCH * G::CHUNK_B + 7 * C * 4, st>>>(
       x, g, b, pack, b1, b2, y, T, eps);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
@@ -567,6 +774,7 @@ mmr_status mmr_swin_mlp(const uint16_t* x, const float* ln_g, const float* ln_b,
     const char* e = getenv("MMR_SWIN_MLP_CFG");
     if (e && atoi(e) == 0) return launch_res<96, 8, true, true>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
     if (e && atoi(e) == 2) return launch_res<96, 8, true, false, false>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
+    if (e && atoi(e) == 3) return launch_sp<96, 8, true>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
     return launch_res<96, 12, true, false, false>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
   }
   if (c == 192) return launch_stream<192, 8, 64, 3, true>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);

@@ -35,7 +35,7 @@ for s in $STEPS; do
     epi)
       timeout -k 10 300 python -u tools/gemm_ab.py --env MMR_P8_EPI --values 0,1 > $OUT/gemm_epi.txt 2>&1; cat $OUT/gemm_epi.txt ;;
     mlp)
-      timeout -k 10 300 python -u tools/mlp_ab.py 0,1,2 > $OUT/mlp_ab.txt 2>&1; cat $OUT/mlp_ab.txt ;;
+      timeout -k 10 300 python -u tools/mlp_ab.py ${MLP_CFGS:-0,1,2} > $OUT/mlp_ab.txt 2>&1; cat $OUT/mlp_ab.txt ;;
     abr02)  # same-box A/B of the cfg2 step: this tree's libmmr vs round 2's (tools/ab/libmmr_r02.so)
       for i in 1 2; do
         for lib in new old; do
@@ -62,6 +62,10 @@ for s in $STEPS; do
     clk)  # effective clock per GEMM kernel (GRBM_GUI_ACTIVE / 8 / duration), bf16 vs MX-fp8
       timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $OUT/clk -o clk -- python3 tools/clock_probe.py > $OUT/clk.log 2>&1
       f=$(find $OUT/clk -name "*counter_collection.csv" | head -1); python tools/clock_summary.py "$f" > $OUT/clk.txt 2>&1; cat $OUT/clk.txt ;;
+    ksweep)
+      timeout -k 10 300 python -u tools/gemm_ksweep.py > $OUT/ksweep.txt 2>&1; cat $OUT/ksweep.txt ;;
+    stamps)  # per-tile breakdown of the 8-phase GEMM (diagnostic stamp build)
+      MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/libmmr_stamps.so timeout -k 10 300 python -u tools/p8_stamps.py > $OUT/stamps.txt 2>&1; cat $OUT/stamps.txt ;;
     nck)
       timeout -k 10 300 python -u tools/gemm_nck.py > $OUT/gemm_nck.txt 2>&1; cat $OUT/gemm_nck.txt ;;
     *) echo "unknown step $s"; exit 2 ;;

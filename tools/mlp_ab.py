@@ -39,12 +39,19 @@ def main():
         h = F.layer_norm(x[:n].float(), (C,), lg, lb, 1e-5)
         ref = x[:n].float() + F.linear(F.gelu(F.linear(h, w1.float(), b1)), w2.float(), b2)
         res = {}
+        first = None
         for _ in range(3):
             for c in cfgs:
                 os.environ["MMR_SWIN_MLP_CFG"] = c
                 y = ops.swin_mlp(x, lg, lb, pack, b1, b2, 1e-5)
                 err = (y[:n].float() - ref).abs().max().item() / ref.abs().max().item()
                 assert err < 2e-2, (C, c, err)
+                if first is None:
+                    first = y.clone()
+                elif _ == 0:  # whole output vs the first variant's (bitwise where the op order matches)
+                    d = (y.float() - first.float()).abs().max().item()
+                    print(f"  C={C} cfg{c} vs cfg{cfgs[0]}: max|diff| {d:.3g}, bitwise equal {torch.equal(y, first)}",
+                          flush=True)
                 res.setdefault(c, []).append(timeit(lambda: ops.swin_mlp(x, lg, lb, pack, b1, b2, 1e-5)))
         print(f"C={C} T={T}: " + "  ".join(f"cfg{c} {min(v):.1f}us" for c, v in res.items()), flush=True)
 
