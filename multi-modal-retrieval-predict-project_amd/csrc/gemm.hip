@@ -493,6 +493,27 @@ __device__ __forceinline__ f32x4 mx_mfma(i32x8 a, i32x8 b, f32x4 c, uint32_t sa,
   return c;
 }
 
+// 16-B output store of the 8-phase GEMM epilogue; nt: non-temporal (streamed past L2).  The launchers
+// set it for outputs larger than the 256 MB MALL written as whole 128-B lines (the LDS-staged and
+// OUT8 epilogues): the output then no longer evicts the X / W panels the concurrent tiles re-read
+// (random operands, M = 262144: fp8 QKV 1551 -> 1940 TF, O 1537 -> 1849, Swin qkv +29 %; bf16 QKV
+// +4 %).  The permlane epilogue writes 64-B half lines and stays write-back (non-temporal: bf16 FFN1
+// -10 %), as do outputs the next kernel may find in the MALL.  profiles/r03_p8_nt_store_ab.txt.
+__device__ __forceinline__ void st16(void* p, uint4 v, bool nt) {
+  typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+  if (nt) __builtin_nontemporal_store(__builtin_bit_cast(u32x4_t, v), (u32x4_t*)p);
+  else *(uint4*)p = v;
+}
+
+// the launchers' choice (MMR_P8_NT=0 / 1 forces it, A/B)
+inline int p8_nt(int64_t m, int64_t n, int64_t esz) {
+  static const int force = [] {
+    const char* e = getenv("MMR_P8_NT");
+    return e ? atoi(e) : -1;
+  }();
+  return force >= 0 ? force : (m * n * esz > (int64_t)256 << 20 ? 1 : 0);
+}
+
 template <int NT, bool FP8 = false, int KNN = 0>
 struct P8 {
   static constexpr int TBN = 64 * NT;
@@ -553,7 +574,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
                                                        const uint8_t* __restrict__ WS = nullptr,
                                                        uint8_t* __restrict__ YS = nullptr,
                                                        float* __restrict__ GM = nullptr, float* __restrict__ BM = nullptr,
-                                                       int64_t ldG = 0, int64_t ldB = 0, int64_t nval = 0) {
+                                                       int64_t ldG = 0, int64_t ldB = 0, int64_t nval = 0,
+                                                       int ntst = 0) {
   static_assert(!OUT8 || (FP8 && NT == 4 && !HAS_RES), "OUT8: MX-fp8 256x256 tiles without residual");
   static_assert(KNN == 0 || ((KNN == 2 || KNN == 4) && NT == 4 && !FP8 && !HAS_BIAS && !HAS_RES && ACT == 0),
                 "KNN (rows per unit 2 / 4): plain 256x256 fp16 tiles");
@@ -576,7 +598,12 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   // 64 B stores are twice the L2 write requests of the LDS path's 8 rows x 128 B).  OUT8 / KNN keep
   // their own epilogues.
   constexpr bool epi_pl = !OUT8 && !KNN && ACT == 1;
-  constexpr int nstore = epi_pl ? C::NSTORE_PL : C::NSTORE_LDS;
+#ifdef MMR_P8_NOSTORE
+  constexpr bool skip_st = !KNN && !OUT8;  // diagnostic build: bf16 outputs computed, not stored
+#else
+  constexpr bool skip_st = false;
+#endif
+  constexpr int nstore = skip_st ? 0 : (epi_pl ? C::NSTORE_PL : C::NSTORE_LDS);
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
 
   const int ntiles = tiles_m * tiles_n;
@@ -959,7 +986,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
           const auto sx = __builtin_amdgcn_permlane16_swap(pk[0].x, pk[1].x, false, false);
           const auto sy = __builtin_amdgcn_permlane16_swap(pk[0].y, pk[1].y, false, false);
           const int col = n0 + wc * 16 * NT + 16 * j + (j2 != j && (efq & 1) ? 16 : 0) + (efq >> 1) * 8;
-          *(uint4*)(Y + row * N + col) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+          if (!skip_st) st16(Y + row * N + col, make_uint4(sx[0], sy[0], sx[1], sy[1]), false);
+          else asm volatile("" ::"v"(sx[0]), "v"(sy[0]), "v"(sx[1]), "v"(sy[1]));
         }
       }
     }
@@ -1016,7 +1044,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
         }
         const int64_t m = m0 + wr * 128 + rd * 16 + rr;
         const int n = n0 + wc * 64 + hb * 16;
-        *(uint4*)((uint8_t*)Y + m * N + n) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        st16((uint8_t*)Y + m * N + n, make_uint4(w4[0], w4[1], w4[2], w4[3]), ntst != 0);
         if ((hb & 1) == 0) {  // one scale byte per 32-block, layout-0 image: [m/256][n/128][wr][fq][fr][i]
           const int fq = (n % 128) / 32;
           YS[((m0 / 256) * (N / 128) + n / 128) * 1024 + ((wr * 4 + fq) * 16 + rr) * 8 + rd] = (uint8_t)(ex + 127);
@@ -1033,7 +1061,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
           const int idx = c * 64 + le;
           const int64_t m = m0 + wr * 128 + rd * 16 * C::RM + idx / (2 * NT);
           const int n = n0 + wc * 16 * NT + (idx % (2 * NT)) * 8;
-          *(bf16x8*)(Y + m * N + n) = ov[c];
+          if (!skip_st) st16(Y + m * N + n, __builtin_bit_cast(uint4, ov[c]), ntst != 0);
+          else asm volatile("" ::"v"(ov[c]));
         }
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -1374,13 +1403,13 @@ void launch(const uint16_t* x, const uint16_t* w, const float* b, const uint16_t
     if (cfg == 7 && n % 256 == 0) {
       const int tm = (int)t256, tn = n / 256;
       gemm_bf16_tn_p8<4, ACT, HB, HR><<<dim3(std::max<int64_t>(8, std::min<int64_t>(grid, (int64_t)tm * tn) / 8 * 8)), dim3(512), P8<4>::LDS_B, st>>>(
-          x, w, b, r, y, m, n, k, tm, tn);
+          x, w, b, r, y, m, n, k, tm, tn, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, p8_nt(m, n, 2));
       return;
     }
     if (cfg == 8 && n % 192 == 0) {
       const int tm = (int)t256, tn = n / 192;
       gemm_bf16_tn_p8<3, ACT, HB, HR><<<dim3(std::max<int64_t>(8, std::min<int64_t>(grid, (int64_t)tm * tn) / 8 * 8)), dim3(512), P8<3>::LDS_B, st>>>(
-          x, w, b, r, y, m, n, k, tm, tn);
+          x, w, b, r, y, m, n, k, tm, tn, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, p8_nt(m, n, 2));
       return;
     }
   }
@@ -1577,14 +1606,15 @@ extern "C" mmr_status mmr_linear_mxfp8(const uint8_t* xq, const uint8_t* xs, con
   const bool hb = bias != nullptr, hr = residual != nullptr;
   const uint16_t* X = (const uint16_t*)xq;
   const uint16_t* W = (const uint16_t*)wq;
+  const int nts = p8_nt(m, n, 2);
 #define MX_LAUNCH(A, B, R)                                                                                         \
   do {                                                                                                               \
     if (w_layout == 1)                                                                                               \
       gemm_bf16_tn_p8<3, A, B, R, true><<<dim3(grid), dim3(512), P8<3, true>::LDS_B, st>>>(X, W, bias, residual, y, m, \
-                                                                                          n, kp, tm, tn, xs, ws);    \
+                                                                                          n, kp, tm, tn, xs, ws, nullptr, nullptr, nullptr, 0, 0, 0, nts); \
     else                                                                                                             \
       gemm_bf16_tn_p8<4, A, B, R, true><<<dim3(grid), dim3(512), P8<4, true>::LDS_B, st>>>(X, W, bias, residual, y, m, \
-                                                                                          n, kp, tm, tn, xs, ws);    \
+                                                                                          n, kp, tm, tn, xs, ws, nullptr, nullptr, nullptr, 0, 0, 0, nts); \
   } while (0)
   if (act == 0) {
     if (hb && hr) MX_LAUNCH(0, true, true);
@@ -1618,13 +1648,13 @@ extern "C" mmr_status mmr_linear_mxfp8_q8(const uint8_t* xq, const uint8_t* xs, 
   const uint16_t* W = (const uint16_t*)wq;
   uint16_t* Y = (uint16_t*)yq;
   if (act == 0 && bias)
-    gemm_bf16_tn_p8<4, 0, true, false, true, true><<<dim3(grid), dim3(512), P8<4, true>::LDS_B, st>>>(X, W, bias, nullptr, Y, m, n, kp, tm, tn, xs, ws, ys);
+    gemm_bf16_tn_p8<4, 0, true, false, true, true><<<dim3(grid), dim3(512), P8<4, true>::LDS_B, st>>>(X, W, bias, nullptr, Y, m, n, kp, tm, tn, xs, ws, ys, nullptr, nullptr, 0, 0, 0, p8_nt(m, n, 1));
   else if (act == 0)
-    gemm_bf16_tn_p8<4, 0, false, false, true, true><<<dim3(grid), dim3(512), P8<4, true>::LDS_B, st>>>(X, W, bias, nullptr, Y, m, n, kp, tm, tn, xs, ws, ys);
+    gemm_bf16_tn_p8<4, 0, false, false, true, true><<<dim3(grid), dim3(512), P8<4, true>::LDS_B, st>>>(X, W, bias, nullptr, Y, m, n, kp, tm, tn, xs, ws, ys, nullptr, nullptr, 0, 0, 0, p8_nt(m, n, 1));
   else if (bias)
-    gemm_bf16_tn_p8<4, 1, true, false, true, true><<<dim3(grid), dim3(512), P8<4, true>::LDS_B, st>>>(X, W, bias, nullptr, Y, m, n, kp, tm, tn, xs, ws, ys);
+    gemm_bf16_tn_p8<4, 1, true, false, true, true><<<dim3(grid), dim3(512), P8<4, true>::LDS_B, st>>>(X, W, bias, nullptr, Y, m, n, kp, tm, tn, xs, ws, ys, nullptr, nullptr, 0, 0, 0, p8_nt(m, n, 1));
   else
-    gemm_bf16_tn_p8<4, 1, false, false, true, true><<<dim3(grid), dim3(512), P8<4, true>::LDS_B, st>>>(X, W, bias, nullptr, Y, m, n, kp, tm, tn, xs, ws, ys);
+    gemm_bf16_tn_p8<4, 1, false, false, true, true><<<dim3(grid), dim3(512), P8<4, true>::LDS_B, st>>>(X, W, bias, nullptr, Y, m, n, kp, tm, tn, xs, ws, ys, nullptr, nullptr, 0, 0, 0, p8_nt(m, n, 1));
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }

@@ -768,14 +768,16 @@ mmr_status mmr_swin_mlp(const uint16_t* x, const float* ln_g, const float* ln_b,
   if (tokens == 0) return MMR_OK;
   hipStream_t st = mmr::as_stream(stream);
   if (c == 96) {
-    // default: 12 waves (3 per SIMD, 148 VGPRs) reading fragments just in time, no x prefetch /
-    // residual registers — 216 -> 210 us at B = 256 over the 8-wave prefetching form (MMR_SWIN_MLP_CFG=0;
-    // =2: 8 waves without prefetch, 222 us) (profiles/r03_swin_mlp_ab.txt)
+    // default (MMR_SWIN_MLP_CFG=3): the software-pipelined form, 2 waves per SIMD — 215 -> 199 us at
+    // B = 256, bitwise equal (profiles/r03_swin_mlp_sp_ab.txt); =1: 12 waves (3 per SIMD) reading
+    // fragments just in time; =0: the 8-wave prefetching form; =2: 8 waves without prefetch
+    // (profiles/r03_swin_mlp_ab.txt)
     const char* e = getenv("MMR_SWIN_MLP_CFG");
-    if (e && atoi(e) == 0) return launch_res<96, 8, true, true>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
-    if (e && atoi(e) == 2) return launch_res<96, 8, true, false, false>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
-    if (e && atoi(e) == 3) return launch_sp<96, 8, true>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
-    return launch_res<96, 12, true, false, false>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
+    const int cfg = e ? atoi(e) : 3;
+    if (cfg == 0) return launch_res<96, 8, true, true>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
+    if (cfg == 1) return launch_res<96, 12, true, false, false>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
+    if (cfg == 2) return launch_res<96, 8, true, false, false>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
+    return launch_sp<96, 8, true>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
   }
   if (c == 192) return launch_stream<192, 8, 64, 3, true>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
   mmr::set_error("mmr_swin_mlp: C=%d not built (96, 192)", c);

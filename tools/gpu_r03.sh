@@ -36,10 +36,10 @@ for s in $STEPS; do
       timeout -k 10 300 python -u tools/gemm_ab.py --env MMR_P8_EPI --values 0,1 > $OUT/gemm_epi.txt 2>&1; cat $OUT/gemm_epi.txt ;;
     mlp)
       timeout -k 10 300 python -u tools/mlp_ab.py ${MLP_CFGS:-0,1,2} > $OUT/mlp_ab.txt 2>&1; cat $OUT/mlp_ab.txt ;;
-    abr02)  # same-box A/B of the cfg2 step: this tree's libmmr vs round 2's (tools/ab/libmmr_r02.so)
+    abr02)  # same-box A/B of the cfg2 step: this tree's libmmr vs tools/ab/${ABLIB:-libmmr_r02.so} (round 2's)
       for i in 1 2; do
         for lib in new old; do
-          if [ $lib = old ]; then export MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/libmmr_r02.so; else unset MMR_LIBMMR; fi
+          if [ $lib = old ]; then export MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/${ABLIB:-libmmr_r02.so}; else unset MMR_LIBMMR; fi
           timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 30 > $OUT/ab_${lib}_$i.json 2> $OUT/ab_${lib}_$i.err
           python -c "import json;d=json.load(open('$OUT/ab_${lib}_$i.json'));print('$lib',round(d['ms_per_step'],3),{k:round(v['ms_per_launch']*1e3,1) for k,v in d['roofline']['bert_gemms'].items()})"
         done
@@ -50,10 +50,10 @@ for s in $STEPS; do
         -- python3 bench.py --preset cfg5 --steps 4 --warmup 2 --no-cpu-baseline > $OUT/prof5.log 2>&1
       f=$(find $OUT/prof5 -name "*kernel_stats.csv" | head -1); python tools/prof_csv_summary.py "$f" > $OUT/prof5_summary.txt 2>&1 || cp "$f" $OUT/prof5_summary.txt
       head -45 $OUT/prof5_summary.txt ;;
-    mxab)  # same-box A/B of the MX-fp8 / bf16 GEMMs: this tree's libmmr vs tools/ab/libmmr_head.so
+    mxab)  # same-box A/B of the MX-fp8 / bf16 GEMMs: this tree's libmmr vs tools/ab/${ABLIB:-libmmr_head.so}
       for i in 1 2; do
         for lib in new old; do
-          if [ $lib = old ]; then export MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/libmmr_head.so; else unset MMR_LIBMMR; fi
+          if [ $lib = old ]; then export MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/${ABLIB:-libmmr_head.so}; else unset MMR_LIBMMR; fi
           echo "== $lib $i" >> $OUT/mxab.txt
           timeout -k 10 300 python -u tools/gemm_mx.py >> $OUT/mxab.txt 2>&1
         done
@@ -65,7 +65,9 @@ for s in $STEPS; do
     ksweep)
       timeout -k 10 300 python -u tools/gemm_ksweep.py > $OUT/ksweep.txt 2>&1; cat $OUT/ksweep.txt ;;
     stamps)  # per-tile breakdown of the 8-phase GEMM (diagnostic stamp build)
-      MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/libmmr_stamps.so timeout -k 10 300 python -u tools/p8_stamps.py > $OUT/stamps.txt 2>&1; cat $OUT/stamps.txt ;;
+      MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/libmmr_stamps.so timeout -k 10 300 python -u tools/p8_stamps.py > $OUT/stamps.txt 2>&1; cat $OUT/stamps.txt
+      if [ -f tools/ab/libmmr_nostore.so ]; then echo "== no stores" >> $OUT/stamps.txt
+        MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/libmmr_nostore.so timeout -k 10 300 python -u tools/p8_stamps.py >> $OUT/stamps.txt 2>&1; cat $OUT/stamps.txt; fi ;;
     nck)
       timeout -k 10 300 python -u tools/gemm_nck.py > $OUT/gemm_nck.txt 2>&1; cat $OUT/gemm_nck.txt ;;
     *) echo "unknown step $s"; exit 2 ;;
