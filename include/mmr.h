@@ -209,6 +209,14 @@ mmr_status mmr_scaled_add_layernorm_bf16(const uint16_t* x, const float* alpha, 
                                          const float* gamma, const float* beta, uint16_t* y, int64_t rows,
                                          int32_t c, float eps, void* stream);
 
+/* mmr_scaled_add_layernorm_bf16 that also writes y as the next GEMM's MX-fp8 activation operand
+ * (q8 [rows][c] e4m3 + q8_scales in the layout-0 image, bit-identical to mmr_quantize_mxfp8 of y):
+ * the fusion stack's enhanced tokens feeding the folded cross projections (config 5, fp8 towers).
+ * rows % 256 == 0, c % 256 == 0. */
+mmr_status mmr_scaled_add_layernorm_bf16_q8(const uint16_t* x, const float* alpha, const uint16_t* residual,
+                                            const float* gamma, const float* beta, uint16_t* y, uint8_t* q8,
+                                            uint8_t* q8_scales, int64_t rows, int32_t c, float eps, void* stream);
+
 /* BERT embeddings (HF BertEmbeddings): LN(word[id] + pos[l] + type[0]) -> bf16 (b*l, c). */
 mmr_status mmr_bert_embed(const int64_t* ids, const float* word, const float* pos,
                           const float* type0, const float* gamma, const float* beta, uint16_t* y,
@@ -325,6 +333,12 @@ mmr_status mmr_mha(const uint16_t* q, int64_t ldq, const uint16_t* k, int64_t ld
  * (PreFusionEnhancer.pos_embed fusion.py:32). c % 8 == 0. */
 mmr_status mmr_add_pos_bf16(const void* x, int32_t x_is_f32, const float* pos, uint16_t* y, int64_t rows,
                             int32_t l, int32_t c, void* stream);
+
+/* mmr_add_pos_bf16 that also writes y as the next GEMM's MX-fp8 activation operand (as
+ * mmr_scaled_add_layernorm_bf16_q8): the enhancer input x + pos feeding its in_proj GEMM (config 5).
+ * rows % 256 == 0, c % 256 == 0. */
+mmr_status mmr_add_pos_bf16_q8(const void* x, int32_t x_is_f32, const float* pos, uint16_t* y, uint8_t* q8,
+                               uint8_t* q8_scales, int64_t rows, int32_t l, int32_t c, void* stream);
 
 /* y = LayerNorm(alpha*x + residual) (+ post_scale*post), per row of c <= 1024 channels.
  * alpha / post_scale are DEVICE f32 scalars (learned parameters) or NULL (= 1); residual / post

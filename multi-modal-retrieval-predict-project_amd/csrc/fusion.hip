@@ -300,9 +300,13 @@ __global__ __launch_bounds__(256, DT == 1 ? 4 : (DT <= 3 ? 3 : 2)) void mha_smal
 // ------------------------------------------------------------------ x + positional table -> bf16
 // y[b][t][c] = x[b][t][c] + pos[t][c] (PreFusionEnhancer.pos_embed fusion.py:32, PositionalEncoding
 // model.py:99-107); x f32 or bf16, pos f32 [>= l][c], 8 channels per thread.
-template <typename TX>
+// Q8: also the row as the next GEMM's MX-fp8 activation operand (mmr::q8_chunk8; c % 256 == 0, so a
+// row's chunks fill whole 4-lane groups and a group never straddles the grid's ragged end).
+template <typename TX, bool Q8 = false>
 __global__ __launch_bounds__(256) void add_pos_bf16(const TX* __restrict__ x, const float* __restrict__ pos,
-                                                    uint16_t* __restrict__ y, int64_t rows, int l, int c) {
+                                                    uint16_t* __restrict__ y, int64_t rows, int l, int c,
+                                                    uint8_t* __restrict__ q8 = nullptr,
+                                                    uint8_t* __restrict__ q8s = nullptr) {
   const int nch = c / 8;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= rows * nch) return;
@@ -334,6 +338,12 @@ __global__ __launch_bounds__(256) void add_pos_bf16(const TX* __restrict__ x, co
   v[4] += p1.x; v[5] += p1.y; v[6] += p1.z; v[7] += p1.w;
   *(uint4*)(y + row * c + ch * 8) = make_uint4(mmr::pack2bf(v[0], v[1]), mmr::pack2bf(v[2], v[3]),
                                                mmr::pack2bf(v[4], v[5]), mmr::pack2bf(v[6], v[7]));
+  if constexpr (Q8) {
+    float vb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vb[j] = mmr::bf2f(mmr::f2bf(v[j]));  // the stored bf16 value
+    mmr::q8_chunk8(vb, row, ch, c, q8, q8s, true);
+  }
 }
 
 // ------------------------------------------------------------------ scaled-residual LayerNorm
@@ -568,6 +578,22 @@ mmr_status mmr_add_pos_bf16(const void* x, int32_t x_is_f32, const float* pos, u
   hipStream_t st = mmr::as_stream(stream);
   if (x_is_f32) add_pos_bf16<float><<<grid, 256, 0, st>>>((const float*)x, pos, y, rows, l, c);
   else add_pos_bf16<uint16_t><<<grid, 256, 0, st>>>((const uint16_t*)x, pos, y, rows, l, c);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_add_pos_bf16_q8(const void* x, int32_t x_is_f32, const float* pos, uint16_t* y, uint8_t* q8,
+                               uint8_t* q8_scales, int64_t rows, int32_t l, int32_t c, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && pos && y && q8 && q8_scales && l > 0 && rows >= 0, "mmr_add_pos_bf16_q8: bad arguments");
+  MMR_REQUIRE(rows % 256 == 0 && c > 0 && c % 256 == 0,
+              "mmr_add_pos_bf16_q8: the MX-fp8 output needs rows %% 256 == 0 and c %% 256 == 0 (rows=%lld c=%d)",
+              (long long)rows, c);
+  if (rows == 0) return MMR_OK;
+  const dim3 grid((unsigned)mmr::ceil_div(rows * (c / 8), 256));
+  hipStream_t st = mmr::as_stream(stream);
+  if (x_is_f32) add_pos_bf16<float, true><<<grid, 256, 0, st>>>((const float*)x, pos, y, rows, l, c, q8, q8_scales);
+  else add_pos_bf16<uint16_t, true><<<grid, 256, 0, st>>>((const uint16_t*)x, pos, y, rows, l, c, q8, q8_scales);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }

@@ -134,30 +134,9 @@ __global__ __launch_bounds__(256) void layernorm_bf16(const uint16_t* __restrict
     if (ok && ch < nch) store8(y + row * c + ch * 8, v[i]);
     if constexpr (Q8) {
       float vb[8];
-      float amax = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        vb[j] = bf2f(f2bf(v[i][j]));  // the stored bf16 value
-        amax = fmaxf(amax, fabsf(vb[j]));
-      }
-      amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
-      amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
-      const uint32_t ab = __float_as_uint(amax);
-      int ex = (int)((ab >> 23) & 255) - 127 - 8 + ((ab & 0x7FFFFF) > 0x600000 ? 1 : 0);
-      ex = ex < -127 ? -127 : (ex > 126 ? 126 : ex);
-      const float inv = __uint_as_float((uint32_t)(127 - ex) << 23);
-      uint32_t w0 = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(vb[0] * inv, vb[1] * inv, 0, false);
-      w0 = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(vb[2] * inv, vb[3] * inv, (int)w0, true);
-      uint32_t w1 = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(vb[4] * inv, vb[5] * inv, 0, false);
-      w1 = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(vb[6] * inv, vb[7] * inv, (int)w1, true);
-      if (ok && ch < nch) {
-        *(uint2*)(q8 + row * c + ch * 8) = make_uint2(w0, w1);
-        if ((ch & 3) == 0) {
-          const int blk = ch / 4, kt = blk / 4, fq = blk % 4;
-          const int rr = (int)(row % 256), wr = rr / 128, ii = (rr % 128) / 16, fr = rr % 16;
-          q8s[((row / 256) * (c / 128) + kt) * 1024 + ((wr * 4 + fq) * 16 + fr) * 8 + ii] = (uint8_t)(ex + 127);
-        }
-      }
+      for (int j = 0; j < 8; ++j) vb[j] = bf2f(f2bf(v[i][j]));  // the stored bf16 value
+      mmr::q8_chunk8(vb, row, ch, c, q8, q8s, ok && ch < nch);
     }
   }
 }
@@ -831,6 +810,15 @@ mmr_status mmr_scaled_add_layernorm_bf16(const uint16_t* x, const float* alpha, 
   mmr::clear_error();
   return layernorm_launch(x, residual, gamma, beta, y, rows, c, eps, stream, "mmr_scaled_add_layernorm_bf16",
                           alpha);
+}
+
+mmr_status mmr_scaled_add_layernorm_bf16_q8(const uint16_t* x, const float* alpha, const uint16_t* residual,
+                                            const float* gamma, const float* beta, uint16_t* y, uint8_t* q8,
+                                            uint8_t* q8_scales, int64_t rows, int32_t c, float eps, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(q8 && q8_scales, "mmr_scaled_add_layernorm_bf16_q8: NULL MX-fp8 output");
+  return layernorm_launch(x, residual, gamma, beta, y, rows, c, eps, stream, "mmr_scaled_add_layernorm_bf16_q8",
+                          alpha, q8, q8_scales);
 }
 
 mmr_status mmr_bert_embed(const int64_t* ids, const float* word, const float* pos,

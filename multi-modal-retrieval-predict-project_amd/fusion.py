@@ -22,6 +22,11 @@ Every fusion layer reads the SAME backbone features (img_global, img_patches, tx
   joint chain      f32 (B, D): norm1 / alpha residual, norm2 -> FFN, adapter (exact f32 MFMA linears)
 
 bf16 activations / f32 accumulation for the token-level work, f32 for every per-query vector.
+tower_dtype="fp8" (BASELINE config 5): the token-level GEMMs fed by an enhancer's input or output —
+each enhancer's in_proj and the folded text / patch cross projections + img_patch_proj, 72 % of the
+stack's token FLOPs — run on the MX-fp8 GEMM; their activation operands come out of the producing
+add-pos / LayerNorm kernels (no quantise pass).  Batches whose token rows are not a 256 multiple
+keep bf16 there.
 """
 import math
 import os
@@ -45,10 +50,15 @@ def _fold(w_in, b_in, w, b):
     return w_in @ w, w_in @ b + b_in
 
 
+def _w8(w):
+    """bf16 weight -> MX-fp8 operand for a plain bias GEMM (256 x 256 tiles when N % 256 == 0)."""
+    return ops.quantize_mxfp8(w, layout=2 if w.shape[0] % 256 == 0 else 1)
+
+
 class _Enhancer:
     """PreFusionEnhancer weights (fusion.py:20-35)."""
 
-    def __init__(self, sd, p, heads, dev):
+    def __init__(self, sd, p, heads, dev, fp8=False):
         C = sd[p + "self_attn.in_proj_weight"].shape[1]
         self.C, self.heads, self.dh = C, heads, C // heads
         self.pos = _f(sd[p + "pos_embed"][0], dev)                       # [max_len][C]
@@ -56,25 +66,36 @@ class _Enhancer:
         self.w_o, self.b_o = _bf(sd[p + "self_attn.out_proj.weight"], dev), _f(sd[p + "self_attn.out_proj.bias"], dev)
         self.alpha = _f(sd[p + "alpha"].reshape(1), dev)
         self.g, self.b = _f(sd[p + "norm1.weight"], dev), _f(sd[p + "norm1.bias"], dev)
+        self.w_in8 = _w8(self.w_in) if fp8 and C % 256 == 0 else None
 
-    def __call__(self, x, B, L, eps):
-        """x (B*L, C) f32 or bf16 -> LN(alpha*(x + pos) + MHA(x + pos)) bf16 (B*L, C)."""
-        X = ops.add_pos(x, self.pos, L)
-        qkv = ops.linear(X, self.w_in, self.b_in)
+    def fp8_ok(self, rows):
+        return self.w_in8 is not None and rows % 256 == 0
+
+    def __call__(self, x, B, L, eps, q8=False):
+        """x (B*L, C) f32 or bf16 -> LN(alpha*(x + pos) + MHA(x + pos)) bf16 (B*L, C); q8 (fp8 path):
+        (y, its MX-fp8 operand)."""
+        if self.fp8_ok(B * L):
+            X, X8 = ops.add_pos(x, self.pos, L, q8=True)
+            qkv = ops.linear_mxfp8(X8, self.w_in8, self.b_in)
+        else:
+            X = ops.add_pos(x, self.pos, L)
+            qkv = ops.linear(X, self.w_in, self.b_in)
         a = torch.empty_like(X)
         C = self.C
         ops.mha(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], B, L, L, self.heads, self.dh,
                 1.0 / math.sqrt(self.dh), out=a)
         x2 = ops.linear(a, self.w_o, self.b_o)
-        return ops.scaled_add_layernorm(X, self.alpha, x2, self.g, self.b, eps)
+        return ops.scaled_add_layernorm(X, self.alpha, x2, self.g, self.b, eps, q8=q8)
 
 
 class FusionStack:
     """The multimodal head: num_fusion_layers x CrossModalFusion + combiner (model.py:375-459)."""
 
-    def __init__(self, sd, num_heads, device="cuda", use_shared_ffn=False, eps=1e-5):
+    def __init__(self, sd, num_heads, device="cuda", use_shared_ffn=False, eps=1e-5, tower_dtype="bf16"):
         dev = torch.device(device)
         self.device, self.heads, self.eps = dev, num_heads, eps
+        fp8 = tower_dtype == "fp8"
+        self.fp8 = fp8
         n = 1 + max(int(k.split(".")[1]) for k in sd if k.startswith("fusion_layers."))
         self.layers = []
         D = sd["self_attn.in_proj_weight"].shape[1]
@@ -82,8 +103,8 @@ class FusionStack:
         for i in range(n):
             p = f"fusion_layers.{i}."
             g = lambda k: sd[p + k]  # noqa: E731
-            L = {"txt": _Enhancer(sd, p + "txt_self_attn.", num_heads, dev),
-                 "patch": _Enhancer(sd, p + "img_patch_self_attn.", num_heads, dev)}
+            L = {"txt": _Enhancer(sd, p + "txt_self_attn.", num_heads, dev, fp8),
+                 "patch": _Enhancer(sd, p + "img_patch_self_attn.", num_heads, dev, fp8)}
             # global enhancer: softmax over ONE key is 1 -> x2 = Wo (Wv x + bv) + bo; with x = G + pos0
             # and the LN input alpha*x + x2 = alpha*G + (Wov G + Wov pos0 + bov + alpha*pos0)
             pg = "img_global_self_attn."
@@ -112,6 +133,9 @@ class FusionStack:
             L["p_w"] = _bf(torch.cat([ki[0], vi[0], qi[0]]), dev)
             L["p_b"] = _f(torch.cat([ki[1], vi[1], qi[1]]), dev)
             L["pp_w"], L["pp_b"] = _bf(g("img_patch_proj.weight"), dev), _f(g("img_patch_proj.bias"), dev)
+            if fp8:
+                for k in ("t_w", "p_w", "pp_w"):
+                    L[k + "8"] = _w8(L[k])
             L["o1_w"], L["o1_b"] = _f(g("attn_txt2img.out_proj.weight"), dev), _f(g("attn_txt2img.out_proj.bias"), dev)
             L["o2_wb"] = _bf(g("attn_img2txt.out_proj.weight"), dev)
             L["o2_w"], L["o2_b"] = _f(g("attn_img2txt.out_proj.weight"), dev), _f(g("attn_img2txt.out_proj.bias"), dev)
@@ -189,9 +213,14 @@ class FusionStack:
             side.wait_stream(main)
         with torch.cuda.stream(side):
             for L in self.layers:
-                Pe = L["patch"](P, B, Np, eps)                         # (B*Np, Ci) bf16
-                pq.append(ops.linear(Pe, L["p_w"], L["p_b"]))          # (B*Np, 3D): k_t2i | v_t2i | q_i2t
-                pp.append(ops.linear(Pe, L["pp_w"], L["pp_b"]))        # img_patch_proj
+                if L["patch"].fp8_ok(B * Np):  # MX-fp8 (config 5): the LayerNorm emits the operand
+                    Pe, Pe8 = L["patch"](P, B, Np, eps, q8=True)
+                    pq.append(ops.linear_mxfp8(Pe8, L["p_w8"], L["p_b"]))
+                    pp.append(ops.linear_mxfp8(Pe8, L["pp_w8"], L["pp_b"]))
+                else:
+                    Pe = L["patch"](P, B, Np, eps)                         # (B*Np, Ci) bf16
+                    pq.append(ops.linear(Pe, L["p_w"], L["p_b"]))          # (B*Np, 3D): k_t2i | v_t2i | q_i2t
+                    pp.append(ops.linear(Pe, L["pp_w"], L["pp_b"]))        # img_patch_proj
                 if two:
                     e = torch.cuda.Event()
                     e.record(side)
@@ -206,12 +235,19 @@ class FusionStack:
             else:
                 Lt = txt_feats.shape[1]
                 T = txt_feats.to(torch.bfloat16).contiguous().view(B * Lt, -1)
-            Te = L["txt"](T, B, Lt, eps)                               # (B*Lt, Ct) bf16
+            t8 = L["txt"].fp8_ok(B * Lt)
+            if t8:
+                Te, Te8 = L["txt"](T, B, Lt, eps, q8=True)
+            else:
+                Te = L["txt"](T, B, Lt, eps)                           # (B*Lt, Ct) bf16
             Ct = Te.shape[1]
             if cls is None:
                 cls = torch.empty((nl, B, Ct), dtype=torch.float32, device=dev)
             ops.rows_to_f32(Te, B, Ct, Lt * Ct, out=cls[i])            # CLS rows (fusion.py:447)
-            TQ = ops.linear(Te, L["t_w"], L["t_b"])                    # (B*Lt, 3D): q_t2i | k_i2t | v_i2t
+            if t8:
+                TQ = ops.linear_mxfp8(Te8, L["t_w8"], L["t_b"])
+            else:
+                TQ = ops.linear(Te, L["t_w"], L["t_b"])                # (B*Lt, 3D): q_t2i | k_i2t | v_i2t
             if two:
                 main.wait_event(ev[i])
             PQ, PP = pq[i], pp[i]

@@ -284,7 +284,8 @@ class MultiModalRetrievalModel:
             nfl = len({k.split(".")[1] for k in hs if k.startswith("fusion_layers.")})
             if nfl != num_fusion_layers and (checkpoint_path or head_state is not None):
                 num_fusion_layers = nfl  # the weights decide (a checkpoint of another depth)
-            self.fusion = FusionStack(hs, num_heads, device=self.device, use_shared_ffn=use_shared_ffn)
+            self.fusion = FusionStack(hs, num_heads, device=self.device, use_shared_ffn=use_shared_ffn,
+                                      tower_dtype=getattr(self.backbones, "tower_dtype", tower_dtype))
         self.num_fusion_layers = num_fusion_layers
         if self.retriever is None and not training and os.environ.get("MMR_EMBEDDINGS_DIR"):
             from .retrieval import make_retrieval_engine

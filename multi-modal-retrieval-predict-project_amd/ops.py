@@ -119,15 +119,28 @@ def layernorm_q8(x, r, g, b, eps):
     return y, MXFP8(q, s, c, 0)
 
 
-def scaled_add_layernorm(x, alpha, r, g, b, eps, out=None):
-    """LayerNorm(alpha * x + r), alpha a device scalar tensor (vectorised row kernel, bf16)."""
+def _q8_out(rows, c, dev):
+    return (torch.empty((rows, c), dtype=torch.uint8, device=dev),
+            torch.empty(((rows // 256) * (c // 128) * 1024,), dtype=torch.uint8, device=dev))
+
+
+def scaled_add_layernorm(x, alpha, r, g, b, eps, out=None, q8=False):
+    """LayerNorm(alpha * x + r), alpha a device scalar tensor (vectorised row kernel, bf16).  q8: also
+    the result's MX-fp8 activation operand, returned as (y, MXFP8) (rows % 256 == 0, C % 256 == 0)."""
     _lib.require_gpu(x)
     c = x.shape[-1]
     if r is not None:
         assert r.shape == x.shape
     y = out if out is not None else torch.empty_like(x)
+    rows = x.numel() // c
+    if q8:
+        q, s = _q8_out(rows, c, x.device)
+        _chk(_L().mmr_scaled_add_layernorm_bf16_q8(_lib.ptr(x), _lib.ptr(alpha), _lib.ptr(r), _lib.ptr(g),
+                                                   _lib.ptr(b), _lib.ptr(y), _lib.ptr(q), _lib.ptr(s), rows, c,
+                                                   float(eps), _s(x)), "mmr_scaled_add_layernorm_bf16_q8")
+        return y, MXFP8(q, s, c, 0)
     _chk(_L().mmr_scaled_add_layernorm_bf16(_lib.ptr(x), _lib.ptr(alpha), _lib.ptr(r), _lib.ptr(g), _lib.ptr(b),
-                                            _lib.ptr(y), x.numel() // c, c, float(eps), _s(x)),
+                                            _lib.ptr(y), rows, c, float(eps), _s(x)),
          "mmr_scaled_add_layernorm_bf16")
     return y
 
@@ -235,13 +248,20 @@ def mha(q, k, v, b, lq, lk, heads, dh, scale, out=None, mean_out=None):
     return out, mean_out
 
 
-def add_pos(x, pos, l):
-    """bf16 (rows, c) = x + pos[row % l] for x (..., c) f32 or bf16 contiguous, pos f32 [>= l][c]."""
+def add_pos(x, pos, l, q8=False):
+    """bf16 (rows, c) = x + pos[row % l] for x (..., c) f32 or bf16 contiguous, pos f32 [>= l][c].
+    q8: also its MX-fp8 activation operand, returned as (y, MXFP8) (rows % 256 == 0, C % 256 == 0)."""
     _lib.require_gpu(x)
     c = x.shape[-1]
+    rows = x.numel() // c
     y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    if q8:
+        q, s = _q8_out(rows, c, x.device)
+        _chk(_L().mmr_add_pos_bf16_q8(_lib.ptr(x), int(x.dtype == torch.float32), _lib.ptr(pos), _lib.ptr(y),
+                                      _lib.ptr(q), _lib.ptr(s), rows, l, c, _s(x)), "mmr_add_pos_bf16_q8")
+        return y, MXFP8(q, s, c, 0)
     _chk(_L().mmr_add_pos_bf16(_lib.ptr(x), int(x.dtype == torch.float32), _lib.ptr(pos), _lib.ptr(y),
-                               x.numel() // c, l, c, _s(x)), "mmr_add_pos_bf16")
+                               rows, l, c, _s(x)), "mmr_add_pos_bf16")
     return y
 
 

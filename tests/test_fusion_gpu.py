@@ -4,7 +4,9 @@ the reference by tests/golden/towers_mini.npz in test_oracle_golden.py).
 
 Tolerances: attention core (bf16 q/k/v, bf16 P) max|err| <= 2e-2 * max|ref|; exact-f32 kernels
 (linear_f32, ln_rows f32) 1e-5; end-to-end multimodal joint embeddings cosine >= 0.999 per row and
-max|err| <= 4e-2 * max|ref| (bf16 token activations through the stack)."""
+max|err| <= 4e-2 * max|ref| (bf16 token activations through the stack).  MX-fp8 stack (config 5:
+e4m3 operands of the enhancer in_proj and cross-projection GEMMs): cosine >= 0.995 per row,
+max|err| <= 1e-1 * max|ref| — e4m3 keeps 3 mantissa bits per operand element."""
 import math
 
 import pytest
@@ -190,3 +192,30 @@ def test_full_size_multimodal_joint_dim_1024_batch_256_vs_oracle():
         (rg, rp), rt = otw.backbones_forward(img[rows], ids[rows], mask[rows], ssd, bsd, SWIN_T, BERT_BASE)
         ref = otw.heads(rg, rp, rt, hs, "multimodal", mm_cfg={"num_heads": 8})["joint_emb"]
     _check_emb(q[rows], ref)
+
+
+def test_fusion_stack_fp8_vs_oracle():
+    """tower_dtype="fp8": the enhancer in_proj and folded cross-projection GEMMs on MX-fp8 operands
+    emitted by the add-pos / LayerNorm kernels.  B=256 so both the text (B*128) and the patch
+    (B*49) token rows are 256 multiples (both sides take the fp8 path); 8 rows vs the oracle."""
+    g = torch.Generator().manual_seed(13)
+    B, Lt, Np, C, D = 256, 128, 49, 768, 1024
+    hs = init_head_state(C, C, D, 25)
+    hs.update(init_fusion_state(C, C, D, 8, 2, 26))
+    G = torch.randn(B, C, generator=g)
+    P = torch.randn(B, Np, C, generator=g)
+    T = bf(torch.randn(B, Lt, C, generator=g)).float()
+    from mmr_amd.fusion import FusionStack
+    fs8 = FusionStack(hs, 8, device=DEV, tower_dtype="fp8")
+    assert all(L["txt"].fp8_ok(B * Lt) and L["patch"].fp8_ok(B * Np) for L in fs8.layers)
+    got8 = fs8.forward(G.to(DEV), P.to(DEV), T.to(DEV))
+    got = FusionStack(hs, 8, device=DEV).forward(G.to(DEV), P.to(DEV), T.to(DEV))
+    rows = [0, 1, 63, 100, 128, 200, 254, 255]
+    with torch.no_grad():
+        ref = otw.multimodal(G[rows], P[rows], T[rows], hs, num_heads=8)
+    _check_emb(got[rows], ref)
+    got8 = got8.detach().float().cpu()[rows]
+    cos = F.cosine_similarity(got8, ref.float(), dim=1)
+    assert cos.min().item() >= 0.995, cos
+    assert rel_err(got8, ref) <= 1e-1
+    assert not torch.equal(got8, got.detach().float().cpu()[rows])  # the fp8 path really ran

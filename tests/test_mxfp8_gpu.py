@@ -124,3 +124,35 @@ def test_layernorm_q8_equals_quantised_layernorm(rows, c, add):
     assert torch.equal(y, ref)
     assert torch.equal(y8.q, ref8.q)
     assert torch.equal(y8.s, ref8.s)
+
+
+@pytest.mark.parametrize("rows,c,l,f32in", [(512, 768, 128, False), (256, 768, 49, True), (768, 1024, 51, False)])
+def test_add_pos_q8_and_scaled_ln_q8_equal_quantised_outputs(rows, c, l, f32in):
+    """The fusion stack's fp8 operand producers (config 5): x + pos and LayerNorm(alpha*x + r) with the
+    fused MX-fp8 output — y equal to the plain kernels bit for bit, the operand equal to
+    mmr_quantize_mxfp8 of y (values and scale bytes)."""
+    xt, _ = _bf16_input(rows, c, 31 + rows)
+    rt, _ = _bf16_input(rows, c, 32 + rows)
+    g = torch.Generator().manual_seed(c + l)
+    pos = (torch.randn(max(l, 64), c, generator=g) * 0.2).to(DEV)
+    x = xt.to(DEV).float() if f32in else xt.to(DEV)
+    y, y8 = ops.add_pos(x, pos, l, q8=True)
+    ref = ops.add_pos(x, pos, l)
+    ref8 = ops.quantize_mxfp8(ref, layout=0)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref) and torch.equal(y8.q, ref8.q) and torch.equal(y8.s, ref8.s)
+    gam, bet = (torch.randn(c, generator=g) * 0.5 + 1).to(DEV), (torch.randn(c, generator=g) * 0.1).to(DEV)
+    alpha = torch.tensor([0.7], device=DEV)
+    r = rt.to(DEV)
+    z, z8 = ops.scaled_add_layernorm(ref, alpha, r, gam, bet, 1e-5, q8=True)
+    zr = ops.scaled_add_layernorm(ref, alpha, r, gam, bet, 1e-5)
+    zr8 = ops.quantize_mxfp8(zr, layout=0)
+    torch.cuda.synchronize()
+    assert torch.equal(z, zr) and torch.equal(z8.q, zr8.q) and torch.equal(z8.s, zr8.s)
+
+
+def test_q8_producers_reject_ragged_rows():
+    x = torch.zeros(100, 768, dtype=torch.bfloat16, device=DEV)
+    pos = torch.zeros(128, 768, device=DEV)
+    with pytest.raises(Exception, match="mmr_add_pos_bf16_q8"):
+        ops.add_pos(x, pos, 50, q8=True)
