@@ -190,48 +190,48 @@ __global__ __launch_bounds__(256) void swin_attn_block(const uint16_t* __restric
       }
     }
 
-    f32x16 acc[3][2];  // proj output^T per (32-channel tile u, token tile)
-#pragma unroll
-    for (int u = 0; u < 3; ++u)
-#pragma unroll
-      for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[u][t2][e] = 0.f;
+    // every head's O^T (bf16 fragments) is kept and the proj runs after the head loop, one token tile
+    // at a time: 48 registers of packed O instead of 96 of proj accumulators live across the heads
+    bf16x8 ost[AH][2][2];
 
     auto wrow = [&](const uint16_t* W, int row, int ks) {  // A/B fragment: weight row, k-step ks
       return *(const bf16x8*)(W + row * AC + 8 * u12(row, 2 * ks + h));
     };
 
-#pragma unroll 1
+#pragma unroll
     for (int hd = 0; hd < AH; ++hd) {
       const float* bt = bias + ((int64_t)type * AH + hd) * 4096;  // dense rel-pos + mask, L2-resident
       // K^T (C^T: lane (token r, half h) holds dh = 8i + 4h + rr) and V (swapped: lane (dh r,
       // half h) holds tokens 8i + 4h + rr) of both token tiles, packed into MFMA fragments
       bf16x8 kf[2][2], vf[2][2];
+      // biases start the accumulators (no VALU pass over the MFMA results)
+      f32x16 kb, vb;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 bkk = *(const f32x4*)(Pqb + AC + hd * ADH + 8 * i + 4 * h);
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) kb[4 * i + rr] = bkk[rr];
+      }
+      {
+        const float bv = Pqb[2 * AC + hd * ADH + r];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) vb[e] = bv;
+      }
 #pragma unroll
       for (int t2 = 0; t2 < 2; ++t2) {
-        f32x16 ak = {0};
+        f32x16 ak = kb;
 #pragma unroll
         for (int ks = 0; ks < AC / 16; ++ks)
           ak = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wrow(Wqkv, AC + hd * ADH + r, ks), hB[t2][ks], ak, 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const f32x4 bkk = *(const f32x4*)(Pqb + AC + hd * ADH + 8 * i + 4 * h);
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) ak[4 * i + rr] += bkk[rr];
-        }
         kf[t2][0] = pack_frag(ak, 0);
         kf[t2][1] = pack_frag(ak, 1);
       }
 #pragma unroll
       for (int t2 = 0; t2 < 2; ++t2) {
-        f32x16 av = {0};
+        f32x16 av = vb;
 #pragma unroll
         for (int ks = 0; ks < AC / 16; ++ks)
           av = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hB[t2][ks], wrow(Wqkv, 2 * AC + hd * ADH + r, ks), av, 0, 0, 0);
-        const float bv = Pqb[2 * AC + hd * ADH + r];
-#pragma unroll
-        for (int e = 0; e < 16; ++e) av[e] += bv;
         vf[t2][0] = pack_frag(av, 0);
         vf[t2][1] = pack_frag(av, 1);
       }
@@ -247,43 +247,46 @@ __global__ __launch_bounds__(256) void swin_attn_block(const uint16_t* __restric
         if (hd == AH - 1 && qt == 1 && win + stride < total) gather(win + stride, buf ^ 1);  // after the last bias loads
         bf16x8 qf[2];
         {
-          f32x16 aq = {0};
-#pragma unroll
-          for (int ks = 0; ks < AC / 16; ++ks)
-            aq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wrow(Wqkv, hd * ADH + r, ks), hB[qt][ks], aq, 0, 0, 0);
+          // q = (Wq x + bq) * scale before the bf16 rounding (timm scales q before q @ k^T), bias in
+          // the accumulator
+          f32x16 aq;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const f32x4 bqq = *(const f32x4*)(Pqb + hd * ADH + 8 * i + 4 * h);
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) aq[4 * i + rr] += bqq[rr];
+            for (int rr = 0; rr < 4; ++rr) aq[4 * i + rr] = bqq[rr];
           }
+#pragma unroll
+          for (int ks = 0; ks < AC / 16; ++ks)
+            aq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wrow(Wqkv, hd * ADH + r, ks), hB[qt][ks], aq, 0, 0, 0);
+#pragma unroll
+          for (int e = 0; e < 16; ++e) aq[e] *= scale;
           qf[0] = pack_frag(aq, 0);
           qf[1] = pack_frag(aq, 1);
         }
-        // S^T[key][query] = K Q^T, scaled, biased; softmax over the 64 keys of query r
+        // S^T[key][query] = K (scale Q)^T + bias (the rel-pos / mask rows start the accumulator);
+        // softmax over the 64 keys of query r
         f32x16 s[2];
         float mx = -FLT_MAX;
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
-          s[kt] = (f32x16){0};
-#pragma unroll
-          for (int k2 = 0; k2 < 2; ++k2) s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kt][k2], qf[k2], s[kt], 0, 0, 0);
 #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-              const float v = s[kt][4 * i + rr] * scale + bq[kt][i][rr];
-              s[kt][4 * i + rr] = v;
-              mx = fmaxf(mx, v);
-            }
+            for (int rr = 0; rr < 4; ++rr) s[kt][4 * i + rr] = bq[kt][i][rr];
+#pragma unroll
+          for (int k2 = 0; k2 < 2; ++k2) s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kt][k2], qf[k2], s[kt], 0, 0, 0);
+#pragma unroll
+          for (int e = 0; e < 16; ++e) mx = fmaxf(mx, s[kt][e]);
         }
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mxl = mx * 1.4426950408889634f;  // exp(s - mx) = exp2(s log2e - mx log2e): one fma
         float sum = 0.f;
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
-            const float p = __builtin_amdgcn_exp2f((s[kt][e] - mx) * 1.4426950408889634f);
+            const float p = __builtin_amdgcn_exp2f(fmaf(s[kt][e], 1.4426950408889634f, -mxl));
             s[kt][e] = p;
             sum += p;
           }
@@ -297,19 +300,34 @@ __global__ __launch_bounds__(256) void swin_attn_block(const uint16_t* __restric
         const float inv = __builtin_amdgcn_rcpf(sum);
 #pragma unroll
         for (int e = 0; e < 16; ++e) o[e] *= inv;
-        // proj: out^T[c][query] += Wproj[c][hd*32 + dh] O^T[dh][query]
-        const bf16x8 ob0 = pack_frag(o, 0), ob1 = pack_frag(o, 1);
-#pragma unroll
-        for (int u = 0; u < 3; ++u) {
-          acc[u][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wrow(Wproj, 32 * u + r, 2 * hd), ob0, acc[u][qt], 0, 0, 0);
-          acc[u][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wrow(Wproj, 32 * u + r, 2 * hd + 1), ob1, acc[u][qt], 0, 0, 0);
-        }
+        ost[hd][qt][0] = pack_frag(o, 0);
+        ost[hd][qt][1] = pack_frag(o, 1);
       }
     }
 
-    // ---- y = x + proj_b + out: lane half h holds channels 32u + 16 hf + 8h + 0..7 of token r
+    // ---- proj: out^T[c][query] = Wproj[c][hd*32 + dh] O^T[dh][query] (+ proj_b in the accumulator);
+    // y = x + out: lane half h holds channels 32u + 16 hf + 8h + 0..7 of token r
 #pragma unroll
     for (int t2 = 0; t2 < 2; ++t2) {
+      f32x16 acc[3];
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          const int c0 = 32 * u + 16 * hf + 8 * h;
+          const f32x4 b0 = *(const f32x4*)(Ppb + c0), b1 = *(const f32x4*)(Ppb + c0 + 4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[u][8 * hf + j] = b0[j];
+            acc[u][8 * hf + 4 + j] = b1[j];
+          }
+        }
+#pragma unroll
+        for (int hd = 0; hd < AH; ++hd) {
+          acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wrow(Wproj, 32 * u + r, 2 * hd), ost[hd][t2][0], acc[u], 0, 0, 0);
+          acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wrow(Wproj, 32 * u + r, 2 * hd + 1), ost[hd][t2][1], acc[u], 0, 0, 0);
+        }
+      }
       const int t = t2 * 32 + r;
       if (t >= ATOK) continue;
       uint16_t* yr = y + tok_row(win, t) * AC;
@@ -319,11 +337,9 @@ __global__ __launch_bounds__(256) void swin_attn_block(const uint16_t* __restric
         for (int hf = 0; hf < 2; ++hf) {
           const int c0 = 32 * u + 16 * hf + 8 * h;
           const bf16x8 xv = *(const bf16x8*)(xs + (t * 12 + u12(t, c0 >> 3)) * 16);
-          const f32x4 b0 = *(const f32x4*)(Ppb + c0), b1 = *(const f32x4*)(Ppb + c0 + 4);
           float v[8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j)
-            v[j] = acc[u][t2][8 * hf + j] + (j < 4 ? b0[j] : b1[j - 4]) + mmr::bf2f((uint16_t)xv[j]);
+          for (int j = 0; j < 8; ++j) v[j] = acc[u][8 * hf + j] + mmr::bf2f((uint16_t)xv[j]);
           *(uint4*)(yr + c0) = make_uint4(mmr::pack2bf(v[0], v[1]), mmr::pack2bf(v[2], v[3]),
                                           mmr::pack2bf(v[4], v[5]), mmr::pack2bf(v[6], v[7]));
         }

@@ -68,6 +68,11 @@ for s in $STEPS; do
       MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/libmmr_stamps.so timeout -k 10 300 python -u tools/p8_stamps.py > $OUT/stamps.txt 2>&1; cat $OUT/stamps.txt
       if [ -f tools/ab/libmmr_nostore.so ]; then echo "== no stores" >> $OUT/stamps.txt
         MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/libmmr_nostore.so timeout -k 10 300 python -u tools/p8_stamps.py >> $OUT/stamps.txt 2>&1; cat $OUT/stamps.txt; fi ;;
+    attnab)  # fused Swin attention block: this tree vs tools/ab/${ABLIB:-libmmr_head.so}
+      for i in 1 2; do
+        timeout -k 10 120 python -u tools/attn_ab.py >> $OUT/attn_ab.txt 2>&1
+        MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/${ABLIB:-libmmr_head.so} timeout -k 10 120 python -u tools/attn_ab.py >> $OUT/attn_ab.txt 2>&1
+      done; grep -v amdgpu.ids $OUT/attn_ab.txt ;;
     nck)
       timeout -k 10 300 python -u tools/gemm_nck.py > $OUT/gemm_nck.txt 2>&1; cat $OUT/gemm_nck.txt ;;
     *) echo "unknown step $s"; exit 2 ;;
