@@ -228,6 +228,13 @@ mmr_status mmr_bert_embed(const int64_t* ids, const float* word, const float* po
 mmr_status mmr_bert_attention(const uint16_t* qkv, const int64_t* mask01, uint16_t* ctx,
                               int32_t b, int32_t l, int32_t h, int32_t dh, void* stream);
 
+/* mmr_bert_attention that writes the context as the O-proj GEMM's MX-fp8 activation operand (q8
+ * (b*l, h*dh) e4m3 + q8_scales in the layout-0 image, bit-identical to mmr_quantize_mxfp8 of ctx);
+ * ctx may be NULL (no bf16 copy).  Config 5's fp8 BERT: no quantise pass between attention and
+ * O-proj.  dh % 32 == 0, (b*l) % 256 == 0, (h*dh) % 256 == 0. */
+mmr_status mmr_bert_attention_q8(const uint16_t* qkv, const int64_t* mask01, uint16_t* ctx, uint8_t* q8,
+                                 uint8_t* q8_scales, int32_t b, int32_t l, int32_t h, int32_t dh, void* stream);
+
 /* Swin (shifted-)window attention core (timm WindowAttention + cyclic shift, eval):
  * qkv bf16 (b*hw*hw, 3*c) in natural token order; the kernel applies roll(-shift), window
  * partition, q*dh^-0.5, k^T, + the dense bias from mmr_swin_attn_bias, softmax, v, window reverse

@@ -111,6 +111,24 @@ __device__ __forceinline__ T wave_max(T v) {
 // result is bit-identical to mmr_quantize_mxfp8 of the bf16 output.  A 32-block is 4 ADJACENT
 // lanes' chunks (ch % 4 = lane % 4; every lane of the group calls it); its E8M0 scale goes to the
 // layout-0 image [row/256][c/128][wr][fq][fr][ii] (see mmr_quantize_mxfp8).  valid masks the stores.
+// E8M0 exponent of a 32-block from its max |value| (mmr_quantize_mxfp8's rule) and the e4m3 packing
+__device__ __forceinline__ int q8_exp(float amax) {
+  const uint32_t ab = __float_as_uint(amax);
+  const int ex = (int)((ab >> 23) & 255) - 127 - 8 + ((ab & 0x7FFFFF) > 0x600000 ? 1 : 0);
+  return ex < -127 ? -127 : (ex > 126 ? 126 : ex);
+}
+__device__ __forceinline__ float q8_inv(int ex) { return __uint_as_float((uint32_t)(127 - ex) << 23); }
+__device__ __forceinline__ uint32_t q8_pack4(const float* v, float inv) {
+  const uint32_t w = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[0] * inv, v[1] * inv, 0, false);
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[2] * inv, v[3] * inv, (int)w, true);
+}
+// byte offset of (row, 32-block of column col) in the layout-0 scale image of a c-column operand
+__device__ __forceinline__ int64_t q8_soff(int64_t row, int col, int c) {
+  const int kt = col / 128, fq = (col % 128) / 32;
+  const int rr = (int)(row % 256), wr = rr / 128, ii = (rr % 128) / 16, fr = rr % 16;
+  return ((row / 256) * (c / 128) + kt) * 1024 + ((wr * 4 + fq) * 16 + fr) * 8 + ii;
+}
+
 __device__ __forceinline__ void q8_chunk8(const float* vb, int64_t row, int ch, int c, uint8_t* q8,
                                           uint8_t* q8s, bool valid) {
   float amax = 0.f;
@@ -118,21 +136,12 @@ __device__ __forceinline__ void q8_chunk8(const float* vb, int64_t row, int ch, 
   for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(vb[j]));
   amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
   amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
-  const uint32_t ab = __float_as_uint(amax);
-  int ex = (int)((ab >> 23) & 255) - 127 - 8 + ((ab & 0x7FFFFF) > 0x600000 ? 1 : 0);
-  ex = ex < -127 ? -127 : (ex > 126 ? 126 : ex);
-  const float inv = __uint_as_float((uint32_t)(127 - ex) << 23);
-  uint32_t w0 = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(vb[0] * inv, vb[1] * inv, 0, false);
-  w0 = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(vb[2] * inv, vb[3] * inv, (int)w0, true);
-  uint32_t w1 = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(vb[4] * inv, vb[5] * inv, 0, false);
-  w1 = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(vb[6] * inv, vb[7] * inv, (int)w1, true);
+  const int ex = q8_exp(amax);
+  const float inv = q8_inv(ex);
+  const uint32_t w0 = q8_pack4(vb, inv), w1 = q8_pack4(vb + 4, inv);
   if (valid) {
     *(uint2*)(q8 + row * c + ch * 8) = make_uint2(w0, w1);
-    if ((ch & 3) == 0) {
-      const int blk = ch / 4, kt = blk / 4, fq = blk % 4;
-      const int rr = (int)(row % 256), wr = rr / 128, ii = (rr % 128) / 16, fr = rr % 16;
-      q8s[((row / 256) * (c / 128) + kt) * 1024 + ((wr * 4 + fq) * 16 + fr) * 8 + ii] = (uint8_t)(ex + 127);
-    }
+    if ((ch & 3) == 0) q8s[q8_soff(row, ch * 8, c)] = (uint8_t)(ex + 127);
   }
 }
 

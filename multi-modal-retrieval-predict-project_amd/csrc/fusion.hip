@@ -48,7 +48,9 @@ __global__ __launch_bounds__(256, DT == 1 ? 4 : (DT <= 3 ? 3 : 2)) void mha_smal
                                                  uint16_t* __restrict__ out, int64_t ldo,
                                                  float* __restrict__ mean_out,
                                                  const int64_t* __restrict__ kmask, int lq, int lk,
-                                                 int heads, int dh, float scale) {
+                                                 int heads, int dh, float scale,
+                                                 uint8_t* __restrict__ q8 = nullptr,
+                                                 uint8_t* __restrict__ q8s = nullptr) {
   constexpr int DHP = DT * 32;
   constexpr int KS = DHP / 16;
   constexpr int KROW = DHP + 8;       // padded K row (elements): 16-B skew between consecutive keys
@@ -241,7 +243,7 @@ __global__ __launch_bounds__(256, DT == 1 ? 4 : (DT <= 3 ? 3 : 2)) void mha_smal
   __syncthreads();
   if (active) {
     const float inv = 1.0f / (l_run + __shfl_xor(l_run, 32, 64));
-    if (out != nullptr) {
+    if (out != nullptr || q8 != nullptr) {
       uint16_t* st = (uint16_t*)red;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt)
@@ -256,11 +258,43 @@ __global__ __launch_bounds__(256, DT == 1 ? 4 : (DT <= 3 ? 3 : 2)) void mha_smal
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes landed
       __builtin_amdgcn_wave_barrier();
       const int nc4 = dh / 4;
-      for (int c = lane; c < 32 * nc4; c += 64) {
-        const int row = c / nc4, ch = c % nc4;
-        if (q0 + row < lq)
-          *(bf16x4*)(out + ((int64_t)bi * lq + q0 + row) * ldo + hh * dh + ch * 4) =
-              *(const bf16x4*)(st + row * OROW + ch * 4);
+      if (out != nullptr)
+        for (int c = lane; c < 32 * nc4; c += 64) {
+          const int row = c / nc4, ch = c % nc4;
+          if (q0 + row < lq)
+            *(bf16x4*)(out + ((int64_t)bi * lq + q0 + row) * ldo + hh * dh + ch * 4) =
+                *(const bf16x4*)(st + row * OROW + ch * 4);
+        }
+      if (q8 != nullptr) {
+        // the context as the O-proj GEMM's MX-fp8 operand (bit-identical to quantising the bf16
+        // rows): lane = (query row, 32-channel block of this head), 32 values from the staged tile
+        const int nb = dh / 32, c = heads * dh;
+        for (int pr = lane; pr < 32 * nb; pr += 64) {
+          const int row = pr / nb, blk = pr % nb;
+          const int64_t grow = (int64_t)bi * lq + q0 + row;
+          float v[32];
+          float amax = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const bf16x4 u = *(const bf16x4*)(st + row * OROW + blk * 32 + 4 * j);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[4 * j + e] = mmr::bf2f((uint16_t)u[e]);
+              amax = fmaxf(amax, fabsf(v[4 * j + e]));
+            }
+          }
+          const int ex = mmr::q8_exp(amax);
+          const float iv = mmr::q8_inv(ex);
+          uint32_t w[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) w[j] = mmr::q8_pack4(v + 4 * j, iv);
+          if (q0 + row < lq) {
+            uint8_t* dst = q8 + grow * c + hh * dh + blk * 32;
+            *(uint4*)dst = make_uint4(w[0], w[1], w[2], w[3]);
+            *(uint4*)(dst + 16) = make_uint4(w[4], w[5], w[6], w[7]);
+            q8s[mmr::q8_soff(grow, hh * dh + blk * 32, c)] = (uint8_t)(ex + 127);
+          }
+        }
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_wave_barrier();
@@ -501,8 +535,10 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 mmr_status launch_mha(const char* who, const uint16_t* q, int64_t ldq, const uint16_t* k, int64_t ldk,
                       const uint16_t* v, int64_t ldv, uint16_t* out, int64_t ldo, float* mean_out,
                       const int64_t* kmask, int32_t b, int32_t lq, int32_t lk, int32_t heads, int32_t dh,
-                      float scale, void* stream) {
-  MMR_REQUIRE(q && k && v && (out || mean_out), "%s: NULL pointer", who);
+                      float scale, void* stream, uint8_t* q8 = nullptr, uint8_t* q8s = nullptr) {
+  MMR_REQUIRE(q && k && v && (out || mean_out || q8), "%s: NULL pointer", who);
+  MMR_REQUIRE(!q8 || (q8s && dh % 32 == 0 && ((int64_t)b * lq) % 256 == 0 && ((int64_t)heads * dh) % 256 == 0),
+              "%s: the MX-fp8 output needs head_dim %% 32 == 0, b*lq %% 256 == 0 and heads*dh %% 256 == 0", who);
   MMR_REQUIRE(b >= 0 && lq > 0 && lk > 0 && heads > 0, "%s: bad shape b=%d lq=%d lk=%d heads=%d", who, b, lq, lk,
               heads);
   MMR_REQUIRE(dh > 0 && dh % 8 == 0 && dh <= 192, "%s: head_dim %d must be a multiple of 8 <= 192", who, dh);
@@ -526,10 +562,10 @@ mmr_status launch_mha(const char* who, const uint16_t* q, int64_t ldq, const uin
   do {                                                                                                         \
     if (kmask)                                                                                                 \
       mha_small<D, true><<<grid, blk, lds, st>>>(q, ldq, k, ldk, v, ldv, out, ldo, mean_out, kmask, lq, lk,    \
-                                                 heads, dh, scale);                                            \
+                                                 heads, dh, scale, q8, q8s);                                   \
     else                                                                                                       \
       mha_small<D, false><<<grid, blk, lds, st>>>(q, ldq, k, ldk, v, ldv, out, ldo, mean_out, nullptr, lq, lk, \
-                                                  heads, dh, scale);                                           \
+                                                  heads, dh, scale, q8, q8s);                                  \
   } while (0)
   switch (dt) {
     case 1: MMR_MHA(1); break;
@@ -567,6 +603,16 @@ mmr_status mmr_bert_attention(const uint16_t* qkv, const int64_t* mask01, uint16
   const int64_t C = (int64_t)h * dh;
   return launch_mha("mmr_bert_attention", qkv, 3 * C, qkv + C, 3 * C, qkv + 2 * C, 3 * C, ctx, C, nullptr, mask01,
                     b, l, l, h, dh, 1.0f / sqrtf((float)dh), stream);
+}
+
+mmr_status mmr_bert_attention_q8(const uint16_t* qkv, const int64_t* mask01, uint16_t* ctx, uint8_t* q8,
+                                 uint8_t* q8_scales, int32_t b, int32_t l, int32_t h, int32_t dh, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(qkv && mask01 && q8 && q8_scales, "mmr_bert_attention_q8: NULL pointer");
+  MMR_REQUIRE(h > 0 && dh > 0, "mmr_bert_attention_q8: bad shape h=%d dh=%d", h, dh);
+  const int64_t C = (int64_t)h * dh;
+  return launch_mha("mmr_bert_attention_q8", qkv, 3 * C, qkv + C, 3 * C, qkv + 2 * C, 3 * C, ctx, C, nullptr, mask01,
+                    b, l, l, h, dh, 1.0f / sqrtf((float)dh), stream, q8, q8_scales);
 }
 
 mmr_status mmr_add_pos_bf16(const void* x, int32_t x_is_f32, const float* pos, uint16_t* y, int64_t rows,

@@ -155,9 +155,17 @@ def bert_embed(ids, word, pos, type0, g, b, eps):
     return y
 
 
-def bert_attention(qkv, mask, heads, dh=64):
+def bert_attention(qkv, mask, heads, dh=64, q8=False, bf16=True):
+    """ctx (B, L, C) bf16; q8: the context as an MX-fp8 activation operand too, returned as
+    (ctx or None, MXFP8) — bf16=False skips the bf16 copy ((B*L) % 256 == 0, C % 256 == 0)."""
     B, L, C3 = qkv.shape
-    ctx = torch.empty((B, L, C3 // 3), dtype=torch.bfloat16, device=qkv.device)
+    ctx = torch.empty((B, L, C3 // 3), dtype=torch.bfloat16, device=qkv.device) if (bf16 or not q8) else None
+    if q8:
+        C = C3 // 3
+        q, s = _q8_out(B * L, C, qkv.device)
+        _chk(_L().mmr_bert_attention_q8(_lib.ptr(qkv), _lib.ptr(mask), _lib.ptr(ctx), _lib.ptr(q), _lib.ptr(s), B, L,
+                                        heads, dh, _s(qkv)), "mmr_bert_attention_q8")
+        return ctx, MXFP8(q, s, C, 0)
     _chk(_L().mmr_bert_attention(_lib.ptr(qkv), _lib.ptr(mask), _lib.ptr(ctx), B, L, heads, dh, _s(qkv)),
          "mmr_bert_attention")
     return ctx

@@ -282,8 +282,13 @@ class BertTower:
         for ly in self.layers:
             if fast8:
                 qkv = ops.linear_mxfp8(h8, ly["qkv_w8"], ly["qkv_b"], lead=lead)
-                ctx = ops.bert_attention(qkv, mask, heads, self.hidden // heads)
-                a = _lin(ctx, ly["o_w"], ly["o_b"], w8=ly["o_w8"])
+                dh = self.hidden // heads
+                if dh % 32 == 0 and ly["o_w8"].kp == self.hidden:  # the attention emits O-proj's operand
+                    _, c8 = ops.bert_attention(qkv, mask, heads, dh, q8=True, bf16=False)
+                    a = ops.linear_mxfp8(c8, ly["o_w8"], ly["o_b"], lead=lead)
+                else:
+                    ctx = ops.bert_attention(qkv, mask, heads, dh)
+                    a = _lin(ctx, ly["o_w"], ly["o_b"], w8=ly["o_w8"])
                 h, h8 = ops.layernorm_q8(a, h, ly["ln1_g"], ly["ln1_b"], 1e-12)
                 f = _mlp8(h, ly["i_w8"], ly["i_b"], ly["f_w8"], ly["f_b"], h8=h8)
                 h, h8 = ops.layernorm_q8(f, h, ly["ln2_g"], ly["ln2_b"], 1e-12)

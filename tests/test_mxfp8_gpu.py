@@ -156,3 +156,24 @@ def test_q8_producers_reject_ragged_rows():
     pos = torch.zeros(128, 768, device=DEV)
     with pytest.raises(Exception, match="mmr_add_pos_bf16_q8"):
         ops.add_pos(x, pos, 50, q8=True)
+
+
+@pytest.mark.parametrize("B,L,heads,dh", [(2, 128, 12, 64), (4, 64, 8, 96)])
+def test_bert_attention_q8_equals_quantised_context(B, L, heads, dh):
+    """The attention kernel's fused MX-fp8 context (config 5's O-proj operand): the bf16 context equals
+    the plain kernel's bit for bit and the operand equals mmr_quantize_mxfp8 of it; bf16=False
+    writes the same operand without the bf16 copy."""
+    g = torch.Generator().manual_seed(B * L + dh)
+    C = heads * dh
+    qkv = (torch.randn(B, L, 3 * C, generator=g) * 2).to(torch.bfloat16).to(DEV)
+    mask = torch.ones(B, L, dtype=torch.int64)
+    mask[0, L // 2:] = 0
+    mask = mask.to(DEV)
+    ref = ops.bert_attention(qkv, mask, heads, dh)
+    ctx, c8 = ops.bert_attention(qkv, mask, heads, dh, q8=True)
+    _, c8b = ops.bert_attention(qkv, mask, heads, dh, q8=True, bf16=False)
+    ref8 = ops.quantize_mxfp8(ref.view(B * L, C), layout=0)
+    torch.cuda.synchronize()
+    assert torch.equal(ctx, ref)
+    for x8 in (c8, c8b):
+        assert torch.equal(x8.q, ref8.q) and torch.equal(x8.s, ref8.s)
