@@ -66,4 +66,7 @@ for M, N, K, act in [(262144, 2304, 768, 0), (262144, 3072, 768, 1), (262144, 76
     w8 = ops.quantize_mxfp8(w, layout=2 if (N % 256 == 0 and not act) else 1)
     x8 = ops.quantize_mxfp8(x, layout=0)
     report(f"fp8  M={M} N={N} K={K} act={act}", lambda: ops.linear_mxfp8(x8, w8, b, act=act, out=y), 256)
+    if N % 256 == 0:
+        w8b = ops.quantize_mxfp8(w, layout=2)
+        report(f"fp8 q8-out M={M} N={N} K={K} act={act}", lambda: ops.linear_mxfp8_q8(x8, w8b, b, act=act), 256)
     del x, w, x8, w8, y
