@@ -598,12 +598,16 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   // 64 B stores are twice the L2 write requests of the LDS path's 8 rows x 128 B).  OUT8 / KNN keep
   // their own epilogues.
   constexpr bool epi_pl = !OUT8 && !KNN && ACT == 1;
+  // OUT8 + GELU in registers (the permlane row chunks, a 32-column block = the 4 lanes fq = 0..3 of
+  // one row, quantised after two lane swaps) measured slower than the LDS-staged OUT8 rounds: FFN1
+  // 1060 -> 1197 us at M = 262144 (8-B stores, 32-B row segments; profiles/r03_out8_permlane_ab.txt)
+  constexpr bool epi_pl8 = false;
 #ifdef MMR_P8_NOSTORE
   constexpr bool skip_st = !KNN && !OUT8;  // diagnostic build: bf16 outputs computed, not stored
 #else
   constexpr bool skip_st = false;
 #endif
-  constexpr int nstore = skip_st ? 0 : (epi_pl ? C::NSTORE_PL : C::NSTORE_LDS);
+  constexpr int nstore = skip_st ? 0 : (epi_pl ? C::NSTORE_PL : (epi_pl8 ? 2 * C::NSTORE_PL : C::NSTORE_LDS));
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
 
   const int ntiles = tiles_m * tiles_n;
@@ -991,8 +995,53 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
         }
       }
     }
+    if constexpr (epi_pl8) {
+      // lane: row m0 + wr 128 + 16 i + efr; after the swap, 8 consecutive columns of the n-tile pair
+      // (j, j + 1) = one quarter of the pair's 32-column block (the quarter index is efq)
 #pragma unroll
-    for (int rd = 0; rd < (epi_pl ? 0 : 8 / C::RM); ++rd) {  // LDS-staged rounds
+      for (int i = 0; i < 8; ++i) {
+        const int64_t row = m0 + wr * 128 + i * 16 + efr;
+#pragma unroll
+        for (int j = 0; j < NT; j += 2) {
+          uint2 pk[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int jj = j + h;
+            float v[4];
+#pragma unroll
+            for (int rg = 0; rg < 4; rg += 2) {
+              mmr::f32x2_t u = {acc[i][jj][rg] + bq[jj][rg], acc[i][jj][rg + 1] + bq[jj][rg + 1]};
+              u = mmr::gelu_fast2(u);
+              v[rg] = u.x;
+              v[rg + 1] = u.y;
+            }
+            pk[h] = make_uint2(mmr::pack2bf(v[0], v[1]), mmr::pack2bf(v[2], v[3]));
+          }
+          const auto sx = __builtin_amdgcn_permlane16_swap(pk[0].x, pk[1].x, false, false);
+          const auto sy = __builtin_amdgcn_permlane16_swap(pk[0].y, pk[1].y, false, false);
+          const uint32_t d4[4] = {sx[0], sy[0], sx[1], sy[1]};  // 8 bf16 columns, in order
+          float vb[8];
+          float amax = 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            vb[2 * e] = __uint_as_float(d4[e] << 16);
+            vb[2 * e + 1] = __uint_as_float(d4[e] & 0xFFFF0000u);
+            amax = fmaxf(amax, fmaxf(fabsf(vb[2 * e]), fabsf(vb[2 * e + 1])));
+          }
+          amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
+          amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+          const int ex = mmr::q8_exp(amax);
+          const float iv = mmr::q8_inv(ex);
+          const int col = n0 + wc * 16 * NT + 16 * j + ((efq & 1) ? 16 : 0) + (efq >> 1) * 8;
+          if (!skip_st) {
+            *(uint2*)((uint8_t*)Y + row * N + col) = make_uint2(mmr::q8_pack4(vb, iv), mmr::q8_pack4(vb + 4, iv));
+            if (efq == 0) YS[mmr::q8_soff(row, col, N)] = (uint8_t)(ex + 127);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int rd = 0; rd < ((epi_pl || epi_pl8) ? 0 : 8 / C::RM); ++rd) {  // LDS-staged rounds
 #pragma unroll
       for (int ii = 0; ii < C::RM; ++ii) {
         const int i = rd * C::RM + ii;

@@ -36,7 +36,12 @@ for M, N, K, act in SHAPES:
     t_bf = timeit(lambda: ops.linear(x, w, b, act=act, out=y))
     t_mx = timeit(lambda: ops.linear_mxfp8(x8, w8, b, act=act, out=y))
     t_q = timeit(lambda: ops.quantize_mxfp8(x, layout=0))
+    t_q8 = None
+    if N % 256 == 0:
+        w8b = ops.quantize_mxfp8(w, layout=2)
+        t_q8 = timeit(lambda: ops.linear_mxfp8_q8(x8, w8b, b, act=act))
     fl = 2.0 * M * N * K
     print(f"M={M:6d} N={N:5d} K={K:5d} act={act} | bf16 {t_bf:7.1f}us {fl / t_bf / 1e6:5.0f}TF | mxfp8 {t_mx:7.1f}us "
-          f"{fl / t_mx / 1e6:5.0f}TF | quantise x {t_q:6.1f}us ({M * K * 3 / t_q / 1e6:5.2f} TB/s)", flush=True)
+          f"{fl / t_mx / 1e6:5.0f}TF | quantise x {t_q:6.1f}us ({M * K * 3 / t_q / 1e6:5.2f} TB/s)"
+          + (f" | q8-out {t_q8:7.1f}us {fl / t_q8 / 1e6:5.0f}TF" if t_q8 else ""), flush=True)
     del x, w, x8, w8, y
