@@ -71,6 +71,19 @@ __device__ __forceinline__ float gelu_fast(float v) {
   return v * __builtin_amdgcn_rcpf(1.0f + e);
 }
 
+// gelu_fast with -log2(e) folded into P (bitwise equal to one lane of gelu_fast2): for code where
+// the GELU runs beside MFMAs, which packed f32 math slows (MI355X_MICROARCH.md, filler prices)
+__device__ __forceinline__ float gelu_fast1(float v) {
+  constexpr float L2E = -1.4426950408889634f;
+  const float x2 = v * v;
+  float p = fmaf(3.275317185739523e-06f * L2E, x2, -7.756018138382363e-05f * L2E);
+  p = fmaf(p, x2, -0.00016997469037563395f * L2E);
+  p = fmaf(p, x2, 0.07280746695679054f * L2E);
+  p = fmaf(p, x2, 1.5957042563586181f * L2E);
+  const float e = __builtin_amdgcn_exp2f(v * p);
+  return v * __builtin_amdgcn_rcpf(e + 1.0f);
+}
+
 // gelu_fast on two values with packed f32 math (v_pk_fma / v_pk_mul / v_pk_add: half the VALU
 // issues of two scalar calls), with -log2(e) folded into P's coefficients (one v_pk_mul fewer;
 // equal to gelu_fast up to f32 rounding of the folded constants).

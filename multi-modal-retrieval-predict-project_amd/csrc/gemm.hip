@@ -524,6 +524,9 @@ struct P8 {
   // global stores per wave per tile (KNN: 8 m-tiles x (4 unit-max + 1 block-max) stores; the LDS-
   // staged epilogue (OUT8, MMR_P8_EPI=0): 8 / RM rounds x CPL 16-B chunks; the permlane epilogue:
   // one 16-B store per (m-tile, n-tile pair) — NT = 3 stores its odd tile as a pair with itself)
+  // (KNN: staging the 2-row unit maxima through LDS into 64-B row segments — 24 stores instead of
+  // 40 — measured 59.3 -> 61.7 us at Q=256 x 100k: the round trips cost more than the store path
+  // saves; without any unit-maxima stores the scan runs 46 us, profiles/r03_knn_unit_store_ab.txt)
   static constexpr int NSTORE_LDS = KNN ? 40 : (8 / RM) * CPL;
   static constexpr int NSTORE_PL = 8 * ((NT + 1) / 2);
   static constexpr size_t BUF_B = (size_t)(256 + TBN) * 64 * 2 + SC * 2;
@@ -604,10 +607,13 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   constexpr bool epi_pl8 = false;
 #ifdef MMR_P8_NOSTORE
   constexpr bool skip_st = !KNN && !OUT8;  // diagnostic build: bf16 outputs computed, not stored
+  constexpr bool skip_gm = KNN != 0;       // ... and the kNN unit maxima (block maxima still stored)
 #else
   constexpr bool skip_st = false;
+  constexpr bool skip_gm = false;
 #endif
-  constexpr int nstore = skip_st ? 0 : (epi_pl ? C::NSTORE_PL : (epi_pl8 ? 2 * C::NSTORE_PL : C::NSTORE_LDS));
+  constexpr int nstore = skip_st ? 0
+                                 : (skip_gm ? 8 : (epi_pl ? C::NSTORE_PL : (epi_pl8 ? 2 * C::NSTORE_PL : C::NSTORE_LDS)));
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
 
   const int ntiles = tiles_m * tiles_n;
@@ -925,7 +931,9 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
 #pragma unroll
           for (int rg = 0; rg < 4; ++rg) a[rg] = rj + rg < nval ? acc[i][j][rg] : -INFINITY;
           const float2 u2 = make_float2(fmaxf(a[0], a[1]), fmaxf(a[2], a[3]));
-          if constexpr (KNN == 2) {
+          if constexpr (skip_gm) {
+            asm volatile("" ::"v"(u2.x), "v"(u2.y));
+          } else if constexpr (KNN == 2) {
             *(float2*)(GM + q * ldG + rj / 2) = u2;
           } else {
             GM[q * ldG + rj / 4] = fmaxf(u2.x, u2.y);

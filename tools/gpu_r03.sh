@@ -73,6 +73,12 @@ for s in $STEPS; do
         timeout -k 10 120 python -u tools/attn_ab.py >> $OUT/attn_ab.txt 2>&1
         MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/${ABLIB:-libmmr_head.so} timeout -k 10 120 python -u tools/attn_ab.py >> $OUT/attn_ab.txt 2>&1
       done; grep -v amdgpu.ids $OUT/attn_ab.txt ;;
+    knnprof)  # kNN search (bench --mode knn) kernel stats: this tree vs tools/ab/${ABLIB:-libmmr_nostore.so}
+      for lib in new old; do
+        if [ $lib = old ]; then export MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/${ABLIB:-libmmr_nostore.so}; else unset MMR_LIBMMR; fi
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/knn_$lib -o k -- python3 bench.py --mode knn --no-cpu-baseline > $OUT/knn_$lib.log 2>&1 || true
+        f=$(find $OUT/knn_$lib -name "*kernel_stats.csv" | head -1); echo "== $lib"; python tools/prof_csv_summary.py "$f" | head -8
+      done; unset MMR_LIBMMR ;;
     nck)
       timeout -k 10 300 python -u tools/gemm_nck.py > $OUT/gemm_nck.txt 2>&1; cat $OUT/gemm_nck.txt ;;
     *) echo "unknown step $s"; exit 2 ;;
