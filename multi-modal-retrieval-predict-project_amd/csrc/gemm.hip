@@ -1552,19 +1552,27 @@ int tuned_variant(int64_t m, int n, int k, int act, bool hb, bool hr, const void
     (void)hipEventDestroy(e0);
     return 0;
   }
+  // two interleaved passes, the faster of each variant's two timings: one 3-launch timing picked a
+  // 13 % slower variant for the BERT QKV shape on some runs (clock / cache state of the moment)
+  float vbest[kVariants];
+  for (int v = 0; v < kVariants; ++v) vbest[v] = 1e30f;
+  for (int pass = 0; pass < 2; ++pass)
+    for (int v = 0; v < kVariants; ++v) {
+      run(kVarW4[v], kVarCfg[v]);
+      (void)hipEventRecord(e0, st);
+      for (int rep = 0; rep < 3; ++rep) run(kVarW4[v], kVarCfg[v]);
+      (void)hipEventRecord(e1, st);
+      float ms = 1e30f;
+      if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess)
+        vbest[v] = std::min(vbest[v], ms);
+    }
   float best = 1e30f;
   int bv = 0;
-  for (int v = 0; v < kVariants; ++v) {
-    run(kVarW4[v], kVarCfg[v]);
-    (void)hipEventRecord(e0, st);
-    for (int rep = 0; rep < 3; ++rep) run(kVarW4[v], kVarCfg[v]);
-    (void)hipEventRecord(e1, st);
-    float ms = 1e30f;
-    if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms < best) {
-      best = ms;
+  for (int v = 0; v < kVariants; ++v)
+    if (vbest[v] < best) {
+      best = vbest[v];
       bv = v;
     }
-  }
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   std::lock_guard<std::mutex> lk(g_tune_mu);

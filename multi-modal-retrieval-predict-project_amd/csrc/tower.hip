@@ -250,124 +250,139 @@ __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __r
                                                              uint16_t* __restrict__ out,
                                                              int64_t units, int H, int C,
                                                              int heads, int ws, int shift) {
-  __shared__ __attribute__((aligned(16))) uint16_t vt_all[4][SW_DH][64 + 4];
-  __shared__ int tok_all[4][64];
+  // round 3: every global load of a wave (Q / K fragments, V rows, the bias rows of both query
+  // tiles) is issued up front from clamped token indices (padded lanes read a real token and are
+  // masked by the bias / the store guard): the previous form's "token valid ? load : 0" gathers
+  // compiled into branches with a vmcnt(0) each (7 serial memory round trips per wave).  V goes to
+  // LDS row-major with 16-B writes and comes back as the V^T fragment by ds_read_b64_tr_b16 (was 32
+  // 2-byte transposing writes per lane); no workgroup barrier (each wave owns its LDS slice).
+  constexpr int VROW = 48;  // halfs per V row: tr-read rows land on disjoint banks
+  __shared__ __attribute__((aligned(16))) uint16_t vs_all[4][64 * VROW];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t unit = (int64_t)blockIdx.x * 4 + wave;
-  const bool active = unit < units;
+  if (unit >= units) return;
   const int nwin1 = H / ws;
-  const int64_t u = active ? unit : 0;
-  // unit order (image, head, window): the 4 waves of a block share one head, so its dense bias
-  // tile (16 KiB per window type) is re-read from L1/L2 instead of once per unit from farther out
-  const int nwin = nwin1 * nwin1;
-  const int win = (int)(u % nwin);
-  const int64_t bh = u / nwin;
-  const int hh = (int)(bh % heads);
-  const int64_t bi = bh / heads;
+  // unit = (image, window, head pair): a wave reads whole 128-B lines of Q / K / V (two heads x 32
+  // dims; the second head's loads hit the lines the first head's brought in) and writes whole
+  // output lines — with one head per wave the two halves of every line were fetched by waves of
+  // different workgroups, i.e. usually by different XCDs (2x the HBM / MALL reads)
+  const int nwin = nwin1 * nwin1, npair = (heads + 1) / 2;
+  const int hp = (int)(unit % npair);
+  const int64_t bw = unit / npair;
+  const int win = (int)(bw % nwin);
+  const int64_t bi = bw / nwin;
   const int wy = win / nwin1, wx = win % nwin1;
   const int N = ws * ws;
   const int type = shift > 0 ? ((wy == nwin1 - 1) ? 2 : 0) + ((wx == nwin1 - 1) ? 1 : 0) : 0;
-  const float* bt = bias + ((int64_t)type * heads + hh) * 4096;
-  uint16_t(*vt)[64 + 4] = vt_all[wave];
-  int* tok = tok_all[wave];
+  uint16_t* vs = vs_all[wave];
+  // window-local token of this lane (rolled coordinates; lanes >= N take token 0 of the window)
+  int tl;
   {
-    const int i = lane;
-    int t = -1;
-    if (i < N) {
-      const int hr = wy * ws + i / ws, wr = wx * ws + i % ws;
-      const int h0 = (hr + shift) % H, w0 = (wr + shift) % H;
-      t = (int)(bi * H * H + h0 * H + w0);
-    }
-    tok[i] = t;
+    const int i = lane < N ? lane : 0;
+    const int hr = wy * ws + i / ws, wr = wx * ws + i % ws;
+    const int h0 = (hr + shift) % H, w0 = (wr + shift) % H;
+    tl = (int)(bi * H * H + h0 * H + w0);
   }
-  __builtin_amdgcn_wave_barrier();
-  for (int c = lane; c < 256; c += 64) {
-    const int key = c >> 2, ch = c & 3;
-    const int t = tok[key];
-    bf16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (active && t >= 0) v = *(const bf16x8*)(qkv + (int64_t)t * 3 * C + 2 * C + hh * SW_DH + ch * 8);
+#pragma unroll 1
+  for (int h2 = 0; h2 < 2; ++h2) {
+    const int hh = 2 * hp + h2;
+    if (hh >= heads) break;
+    const float* bt = bias + ((int64_t)type * heads + hh) * 4096;
+    asm volatile("" ::: "memory");  // the previous head's V reads stay before this head's V writes
+    const int r = lane & 31, hf = lane >> 5;
+    const uint16_t* hb = qkv + hh * SW_DH;
+    const uint32_t rs = 3u * (uint32_t)C;  // element offsets fit 32 bits (launcher)
+    bf16x8 qf[2][2], kf[2][2], vr[4];
+    float4 bb[2][2][4];  // bias rows of this lane's two queries: [qt][kt][g4] (keys kt 32 + 8 g4 + 4 hf ..)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) vt[ch * 8 + j][key] = (uint16_t)v[j];
-  }
-  __syncthreads();
-  if (!active) return;
+    for (int it = 0; it < 4; ++it)  // V rows: lane (key 16 it + lane / 4, 16-B chunk lane % 4)
+      vr[it] = *(const bf16x8*)(hb + (uint32_t)__shfl(tl, 16 * it + (lane >> 2), 64) * rs + 2 * C + (lane & 3) * 8);
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {
+      const uint16_t* row = hb + (uint32_t)__shfl(tl, t2 * 32 + r, 64) * rs;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        qf[t2][ks] = *(const bf16x8*)(row + ks * 16 + 8 * hf);
+        kf[t2][ks] = *(const bf16x8*)(row + C + ks * 16 + 8 * hf);
+      }
+    }
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) bb[qt][kt][g4] = *(const float4*)(bt + (qt * 32 + r) * 64 + kt * 32 + 8 * g4 + 4 * hf);
+    __builtin_amdgcn_sched_barrier(0);  // every load above in flight before the first use
+#pragma unroll
+    for (int it = 0; it < 4; ++it) *(bf16x8*)(vs + (16 * it + (lane >> 2)) * VROW + (lane & 3) * 8) = vr[it];
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's V rows are in LDS
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
 
-  const int r = lane & 31, hf = lane >> 5;
-  const float scale = 0.17677669529663687f;  // 32^-0.5
-  bf16x8 qf[2][2], kf[2][2];
+    constexpr float L2E = 1.4426950408889634f;
+    const float scale = 0.17677669529663687f;  // 32^-0.5
+    const int grp = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
 #pragma unroll
-  for (int t2 = 0; t2 < 2; ++t2) {
-    const int tq = tok[t2 * 32 + r];
+    for (int qt = 0; qt < 2; ++qt) {
+      const int qi = qt * 32 + r;  // this lane's query (local index)
+      f32x16 s[2];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-      qf[t2][ks] = tq >= 0 ? *(const bf16x8*)(qkv + (int64_t)tq * 3 * C + hh * SW_DH + ks * 16 + 8 * hf) : z;
-      kf[t2][ks] = tq >= 0 ? *(const bf16x8*)(qkv + (int64_t)tq * 3 * C + C + hh * SW_DH + ks * 16 + 8 * hf) : z;
-    }
-  }
+      for (int kt = 0; kt < 2; ++kt) {
+        s[kt] = (f32x16){0};
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int qi = qt * 32 + r;  // this lane's query (local index)
-    f32x16 s[2];
+        for (int ks = 0; ks < 2; ++ks)
+          s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kt][ks], qf[qt][ks], s[kt], 0, 0, 0);
+      }
+      float mloc = -FLT_MAX;
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      s[kt] = (f32x16){0};
+      for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kt][ks], qf[qt][ks], s[kt], 0, 0, 0);
-    }
-    const float* brow = bt + qi * 64;
-    float mloc = -FLT_MAX;
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const float bv[4] = {bb[qt][kt][g4].x, bb[qt][kt][g4].y, bb[qt][kt][g4].z, bb[qt][kt][g4].w};
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const float4 bb = *(const float4*)(brow + kt * 32 + 8 * g4 + 4 * hf);
-        const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float v = s[kt][4 * g4 + e] * scale + bv[e];
-          s[kt][4 * g4 + e] = v;
-          mloc = fmaxf(mloc, v);
+          for (int e = 0; e < 4; ++e) {
+            const float v = fmaf(s[kt][4 * g4 + e], scale, bv[e]);
+            s[kt][4 * g4 + e] = v;
+            mloc = fmaxf(mloc, v);
+          }
         }
-      }
-    }
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-    float psum = 0.f;
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      const float ml = mloc * L2E;
+      float psum = 0.f;
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+      for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int rg = 0; rg < 16; ++rg) {
-        const float p = __expf(s[kt][rg] - mloc);
-        s[kt][rg] = p;
-        psum += p;
-      }
-    }
-    psum += __shfl_xor(psum, 32, 64);
-    f32x16 o = {0};
+        for (int rg = 0; rg < 16; ++rg) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[kt][rg], L2E, -ml));
+          s[kt][rg] = p;
+          psum += p;
+        }
+      psum += __shfl_xor(psum, 32, 64);
+      // O^T = V^T . P^T; the V^T fragment (lane: dim r, keys kbase..+3 and kbase+8..+11 in P^T's
+      // register order) by two ds_read_b64_tr_b16 from the key-major V image
+      f32x16 o = {0};
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+      for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int sidx = 0; sidx < 2; ++sidx) {
-        bf16x8 pf;
+        for (int sidx = 0; sidx < 2; ++sidx) {
+          const bf16x8 pf = __builtin_bit_cast(
+              bf16x8, make_uint4(mmr::pack2bf(s[kt][8 * sidx], s[kt][8 * sidx + 1]), mmr::pack2bf(s[kt][8 * sidx + 2], s[kt][8 * sidx + 3]),
+                                 mmr::pack2bf(s[kt][8 * sidx + 4], s[kt][8 * sidx + 5]), mmr::pack2bf(s[kt][8 * sidx + 6], s[kt][8 * sidx + 7])));
+          const int r0 = kt * 32 + 16 * sidx + 4 * (grp >> 1);
+          const uint16_t* va = vs + (r0 + tq) * VROW + (grp & 1) * 16 + 4 * tp;
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4*)va);
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4*)(va + 8 * VROW));
+          const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o, 0, 0, 0);
+        }
+      const int tqi = __shfl(tl, qi, 64);
+      if (qi < N) {
+        const float inv = 1.0f / psum;
+        uint16_t* orow = out + (int64_t)tqi * C + hh * SW_DH;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) pf[j] = (short)f2bf(s[kt][8 * sidx + j]);
-        const int kbase = kt * 32 + 16 * sidx + 4 * hf;
-        const bf16x4 lo = *(const bf16x4*)(&vt[r][kbase]);
-        const bf16x4 hi = *(const bf16x4*)(&vt[r][kbase + 8]);
-        const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o, 0, 0, 0);
-      }
-    }
-    if (qi < N) {
-      const float inv = 1.0f / psum;
-      uint16_t* orow = out + (int64_t)tok[qi] * C + hh * SW_DH;
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        bf16x4 w;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = (short)f2bf(o[4 * g4 + j] * inv);
-        *(bf16x4*)(orow + 8 * g4 + 4 * hf) = w;
+        for (int g4 = 0; g4 < 4; ++g4)
+          *(uint2*)(orow + 8 * g4 + 4 * hf) = make_uint2(mmr::pack2bf(o[4 * g4] * inv, o[4 * g4 + 1] * inv),
+                                                         mmr::pack2bf(o[4 * g4 + 2] * inv, o[4 * g4 + 3] * inv));
       }
     }
   }
@@ -858,7 +873,9 @@ mmr_status mmr_swin_window_attention(const uint16_t* qkv, const float* bias, uin
   MMR_REQUIRE(ws > 0 && ws * ws <= 64 && hw % ws == 0, "mmr_swin_window_attention: window %d / resolution %d", ws, hw);
   MMR_REQUIRE(shift >= 0 && shift < ws, "mmr_swin_window_attention: shift %d", shift);
   if (b == 0) return MMR_OK;
-  const int64_t units = (int64_t)b * (hw / ws) * (hw / ws) * heads;
+  MMR_REQUIRE((int64_t)b * hw * hw * 3 * c < ((int64_t)1 << 32), "mmr_swin_window_attention: %lld qkv elements (32-bit offsets)",
+              (long long)b * hw * hw * 3 * c);
+  const int64_t units = (int64_t)b * (hw / ws) * (hw / ws) * ((heads + 1) / 2);
   swin_window_attention<<<dim3((unsigned)mmr::ceil_div(units, 4)), 256, 0, mmr::as_stream(stream)>>>(
       qkv, bias, out, units, hw, c, heads, ws, shift);
   MMR_LAUNCH_CHECK();

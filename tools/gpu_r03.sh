@@ -79,6 +79,18 @@ for s in $STEPS; do
         timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/knn_$lib -o k -- python3 bench.py --mode knn --no-cpu-baseline > $OUT/knn_$lib.log 2>&1 || true
         f=$(find $OUT/knn_$lib -name "*kernel_stats.csv" | head -1); echo "== $lib"; python tools/prof_csv_summary.py "$f" | head -8
       done; unset MMR_LIBMMR ;;
+    libab)  # same-box A/B of the tuned bf16 GEMM on the cfg2 shapes: this tree vs tools/ab/${ABLIB:-libmmr_nostore.so}
+      for i in 1 2; do
+        timeout -k 10 200 python -u tools/lib_ab.py new >> $OUT/libab.txt 2>&1
+        MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/${ABLIB:-libmmr_nostore.so} timeout -k 10 200 python -u tools/lib_ab.py ${ABLIB:-nostore} >> $OUT/libab.txt 2>&1
+      done; grep -v amdgpu.ids $OUT/libab.txt | tr '|' '\n' ;;
+    swa)  # Swin window attention: this tree vs tools/ab/${ABLIB:-libmmr_head.so}
+      for i in 1 2; do
+        timeout -k 10 120 python -u tools/swa_bench.py new >> $OUT/swa.txt 2>&1
+        MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/${ABLIB:-libmmr_head.so} timeout -k 10 120 python -u tools/swa_bench.py old >> $OUT/swa.txt 2>&1
+      done; grep -v amdgpu.ids $OUT/swa.txt ;;
+    breakdown)  # per-(op, shape) times of one sequential cfg2 step
+      MMR_TOWER_STREAMS=0 MMR_FUSION_STREAMS=0 timeout -k 10 300 python -u tools/step_breakdown.py > $OUT/breakdown.txt 2>&1; grep -v amdgpu.ids $OUT/breakdown.txt | head -70 ;;
     nck)
       timeout -k 10 300 python -u tools/gemm_nck.py > $OUT/gemm_nck.txt 2>&1; cat $OUT/gemm_nck.txt ;;
     *) echo "unknown step $s"; exit 2 ;;
