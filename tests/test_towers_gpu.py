@@ -56,6 +56,38 @@ def test_linear_bf16(M, N, K, act, bias, res):
     assert rel_err(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize("cfg", [7, 8])
+@pytest.mark.parametrize("M,N,K,act,bias,res", [(32768, 1152, 128, 0, True, False), (32768, 1152, 384, 0, True, True),
+                                                (65536, 768, 768, 0, False, True), (32768, 2304, 256, 0, False, False),
+                                                (16384, 768, 3072, 0, True, True), (32768, 1536, 384, 1, True, False)])
+def test_linear_bf16_p8_persistent(monkeypatch, cfg, M, N, K, act, bias, res):
+    """The persistent 8-phase GEMM pinned (MMR_GEMM_BIG=7: 256x256 tiles, 8: 256x192) on shapes with
+    2-4 tiles per workgroup and K = 128 ... 3072 (1 ... 12 K iterations per tile: the K stream runs
+    on across tile boundaries), every epilogue; vs torch fp32 of the same bf16 operands (tolerance
+    1e-2 * max|ref|: bf16 output rounding)."""
+    if N % (256 if cfg == 7 else 192):
+        pytest.skip("tile width")
+    monkeypatch.setenv("MMR_GEMM_W4", "0")
+    monkeypatch.setenv("MMR_GEMM_BIG", str(cfg))
+    g = torch.Generator(device=DEV).manual_seed(M + N + K + cfg)
+    x = torch.randn(M, K, generator=g, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, generator=g, device=DEV) * 0.05).to(torch.bfloat16)
+    b = torch.randn(N, generator=g, device=DEV) if bias else None
+    r = torch.randn(M, N, generator=g, device=DEV).to(torch.bfloat16) if res else None
+    ref = x.float() @ w.float().T
+    if b is not None:
+        ref = ref + b
+    if act == 1:
+        ref = F.gelu(ref)
+    if r is not None:
+        ref = ref + r.float()
+    y = ops.linear(x, w, b, r, act=act)
+    torch.cuda.synchronize()
+    assert rel_err(y, ref) < 1e-2
+    # every row block written
+    assert ((y.float() - ref).abs().amax(dim=1) <= 2e-2 * ref.abs().max()).all()
+
+
 @pytest.mark.parametrize("T,C", [(1000, 96), (3136 * 4 + 17, 96), (64, 192), (784 * 8 + 5, 192), (1, 96)])
 def test_swin_mlp_fused(T, C):
     """mmr_swin_mlp == x + fc2(GELU(fc1(LN(x)))) (fusion.py:198-199 via timm Mlp), ragged token counts;
