@@ -172,10 +172,14 @@ class FusionStack:
         self.ln_img_all = tuple(torch.stack([L["ln_img"][k] for L in Ls]).contiguous() for k in (0, 1))
         self.ln_txt_all = tuple(torch.stack([L["ln_txt"][k] for L in Ls]).contiguous() for k in (0, 1))
 
-    def _side_stream(self):
+    def _side_stream(self, main):
+        # one side stream per calling stream (pipelined callers keep their batches independent)
         if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(self.device)
-        return self._side
+            self._side = {}
+        side = self._side.get(main.cuda_stream)
+        if side is None:
+            side = self._side[main.cuda_stream] = torch.cuda.Stream(self.device)
+        return side
 
     def forward(self, img_global, img_patches, txt_feats):
         """img_global (B, Ci) f32, img_patches (B, Np, Ci) f32, txt_feats (B, L, Ct) bf16/f32 or None
@@ -207,7 +211,7 @@ class FusionStack:
         two = getattr(self, "_warm", False) and os.environ.get("MMR_FUSION_STREAMS", "1") != "0"
         self._warm = True
         main = torch.cuda.current_stream(dev)
-        side = self._side_stream() if two else main
+        side = self._side_stream(main) if two else main
         pq, pp, ev = [], [], []
         if two:
             side.wait_stream(main)

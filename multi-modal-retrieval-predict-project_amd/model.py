@@ -367,9 +367,13 @@ class MultiModalRetrievalModel:
             return (self.backbones.encode_image(image, want_patches=want_patches),
                     self.backbones.encode_text(input_ids, attention_mask))
         main = torch.cuda.current_stream(self.device)
+        # one side stream per calling stream: callers that pipeline batches over several streams
+        # (bench.py --pipeline) keep their batches independent
         if self._side is None:
-            self._side = torch.cuda.Stream(self.device)
-        side = self._side
+            self._side = {}
+        side = self._side.get(main.cuda_stream)
+        if side is None:
+            side = self._side[main.cuda_stream] = torch.cuda.Stream(self.device)
         side.wait_stream(main)                        # the image batch is ready
         with torch.cuda.stream(side):
             img = self.backbones.encode_image(image, want_patches=want_patches)
