@@ -157,6 +157,17 @@ mmr_status mmr_linear_bf16(const uint16_t* x, const uint16_t* w, const float* bi
 int32_t mmr_linear_bf16_variant(int64_t m, int32_t n, int32_t k, int32_t act, int32_t has_bias,
                                 int32_t has_residual);
 
+/* Resident-weight streaming linear for the short-K, narrow tower linears (Swin patch embed, stage-2
+ * qkv / proj, PatchMerging 1->2; timm nn.Linear, reference fusion.py:198-199):
+ * y = x @ W^T + bias (+ residual), K in {64, 192, 384}.  W is kept in LDS for the whole launch, as
+ * mmr_linear_rw_parts(n, k) parts of N / P channels, from an image built once by
+ * mmr_linear_rw_pack (n * k bf16 elements, caller-allocated).  mmr_linear_rw_parts returns 0 for
+ * shapes it does not take (then use mmr_linear_bf16). */
+int32_t mmr_linear_rw_parts(int32_t n, int32_t k);
+mmr_status mmr_linear_rw_pack(const uint16_t* w, int32_t n, int32_t k, uint16_t* img, void* stream);
+mmr_status mmr_linear_rw(const uint16_t* x, const uint16_t* img, const float* bias, const uint16_t* residual,
+                         uint16_t* y, int64_t m, int32_t n, int32_t k, void* stream);
+
 /* ---------------------------------------------------------------- MX-fp8 linears (config 5) */
 /* Quantise bf16 x [rows][k] to OCP e4m3 q [rows][kp] (zero-padded, kp >= k, kp % 256 == 0) with one
  * E8M0 scale per 32 consecutive k of a row: 2^e, the smallest e with amax <= 448 * 2^e (no clipping);

@@ -31,6 +31,38 @@ def linear(x, w, bias=None, residual=None, act=0, out=None):
     return y
 
 
+class RWPack:
+    """A weight image for mmr_linear_rw (resident-weight streaming linear): W (N, K) bf16 re-laid for
+    LDS; `None` from rw_pack when the shape is not one the kernel takes."""
+    __slots__ = ("img", "n", "k")
+
+    def __init__(self, img, n, k):
+        self.img, self.n, self.k = img, n, k
+
+
+def rw_pack(w):
+    """bf16 W (N, K) -> RWPack, or None (K not in {64, 192, 384} or W too large for LDS parts)."""
+    _lib.require_gpu(w)
+    n, k = w.shape
+    if _L().mmr_linear_rw_parts(n, k) <= 0:
+        return None
+    img = torch.empty((n, k), dtype=torch.bfloat16, device=w.device)
+    _chk(_L().mmr_linear_rw_pack(_lib.ptr(w.contiguous()), n, k, _lib.ptr(img), _s(w)), "mmr_linear_rw_pack")
+    return RWPack(img, n, k)
+
+
+def linear_rw(x, pack, bias=None, residual=None, out=None):
+    """x @ W^T + bias (+ residual) on the resident-weight streaming kernel; x (..., K) bf16."""
+    _lib.require_gpu(x)
+    K = x.shape[-1]
+    assert K == pack.k
+    M = x.numel() // K
+    y = out if out is not None else torch.empty(x.shape[:-1] + (pack.n,), dtype=torch.bfloat16, device=x.device)
+    _chk(_L().mmr_linear_rw(_lib.ptr(x), _lib.ptr(pack.img), _lib.ptr(bias), _lib.ptr(residual), _lib.ptr(y), M,
+                            pack.n, K, _s(x)), "mmr_linear_rw")
+    return y
+
+
 class MXFP8:
     """An MX-fp8 operand: e4m3 bytes q [rows][kp] + E8M0 scales in the GEMM's image order (see
     mmr_quantize_mxfp8), k the unpadded inner size, layout 0 (activations) / 1 (weights)."""

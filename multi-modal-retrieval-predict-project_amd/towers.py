@@ -51,6 +51,12 @@ def _w8(w, plain=False):
     return ops.quantize_mxfp8(w, layout=2 if plain and w.shape[0] % 256 == 0 else 1)
 
 
+def _rw(w):
+    """Resident-weight streaming image for the short-K linears (K = 64 / 192: patch embed, stage-2
+    qkv / proj; tools/rw_bench.py: 1.1-1.4x the tuned GEMM there, slower at K = 384), else None."""
+    return ops.rw_pack(w) if w.shape[1] in (64, 192) else None
+
+
 def _pad_rows(t2, rows_p):
     """2-D rows zero-padded to rows_p (the MX-fp8 operands and GEMM tiles take 256-row multiples:
     a batch of any size — B = 1 serving, a ragged last batch — runs the same fp8 arithmetic on its
@@ -120,6 +126,7 @@ class SwinTower:
         wp = torch.zeros((E, 64), dtype=torch.float32)
         wp[:, :w.shape[1]] = w
         self.pe_w, self.pe_b = _bf(wp, dev), _f(sd["patch_embed.proj.bias"], dev)
+        self.pe_rw = _rw(self.pe_w)
         self.pe_g, self.pe_beta = _f(sd["patch_embed.norm.weight"], dev), _f(sd["patch_embed.norm.bias"], dev)
         self.stages = []
         res = self.cfg["img_size"] // self.cfg["patch"]
@@ -152,6 +159,8 @@ class SwinTower:
                 fp8 = i in self.fp8_stages
                 for n in ("qkv", "proj", "fc1", "fc2"):
                     bk[n + "_w8"] = _w8(bk[n + "_w"], plain=n in ("qkv", "fc1")) if fp8 else None
+                for n in ("qkv", "proj"):  # short-K linears (stage 2): resident-weight streaming kernel
+                    bk[n + "_rw"] = _rw(bk[n + "_w"]) if not fp8 else None
                 bk["mlp_pack"] = ops.swin_mlp_pack(bk["fc1_w"], bk["fc2_w"]) if self.fused_mlp and not fp8 else None
                 bk["attn_pack"] = None
                 if self.fused_attn and not fp8 and E * 2 ** i == 96 and self.cfg["num_heads"][i] == 3 and ws == 7:
@@ -168,7 +177,8 @@ class SwinTower:
         B = image.shape[0]
         g = cfg["img_size"] // cfg["patch"]
         cols = ops.patch_im2col(image, cfg["patch"])
-        x = ops.linear(cols, self.pe_w, self.pe_b)                   # (B, g*g, E)
+        x = (ops.linear_rw(cols, self.pe_rw, self.pe_b) if self.pe_rw is not None
+             else ops.linear(cols, self.pe_w, self.pe_b))                 # (B, g*g, E)
         x = ops.layernorm(x, self.pe_g, self.pe_beta, 1e-5).view(B, g, g, -1)
         ws0 = cfg["window_size"]
         for i, st in enumerate(self.stages):
@@ -188,9 +198,11 @@ class SwinTower:
                     x = _lin(a, bk["proj_w"], bk["proj_b"], residual=x, w8=bk["proj_w8"])
                 else:
                     h = ops.layernorm(x, bk["n1g"], bk["n1b"], 1e-5)
-                    qkv = _lin(h, bk["qkv_w"], bk["qkv_b"], w8=bk["qkv_w8"])
+                    qkv = (ops.linear_rw(h, bk["qkv_rw"], bk["qkv_b"]) if bk["qkv_rw"] is not None
+                           else _lin(h, bk["qkv_w"], bk["qkv_b"], w8=bk["qkv_w8"]))
                     a = ops.swin_window_attention(qkv, bk["bias"], H, heads, ws, bk["shift"])
-                    x = _lin(a, bk["proj_w"], bk["proj_b"], residual=x, w8=bk["proj_w8"])
+                    x = (ops.linear_rw(a, bk["proj_rw"], bk["proj_b"], residual=x) if bk["proj_rw"] is not None
+                         else _lin(a, bk["proj_w"], bk["proj_b"], residual=x, w8=bk["proj_w8"]))
                 if bk["mlp_pack"] is not None:
                     x = ops.swin_mlp(x, bk["n2g"], bk["n2b"], bk["mlp_pack"], bk["fc1_b"], bk["fc2_b"], 1e-5)
                 elif _ln8_ok(x, bk["fc1_w8"]) and bk["fc1_w8"].layout == 2:

@@ -88,6 +88,38 @@ def test_linear_bf16_p8_persistent(monkeypatch, cfg, M, N, K, act, bias, res):
     assert ((y.float() - ref).abs().amax(dim=1) <= 2e-2 * ref.abs().max()).all()
 
 
+@pytest.mark.parametrize("M,N,K,bias,res", [(3136 * 4 + 17, 96, 64, True, False), (784 * 8 + 5, 576, 192, True, False),
+                                            (784 * 8 + 5, 192, 192, True, True), (784 * 2, 192, 384, False, False),
+                                            (1000, 384, 384, True, True), (31, 576, 192, True, True),
+                                            (500, 32, 64, True, False), (300, 160, 192, False, True)])
+def test_linear_rw(M, N, K, bias, res):
+    """mmr_linear_rw (resident-weight streaming linear: Swin patch embed / stage-2 qkv, proj /
+    PatchMerging 1->2 shapes, N split into LDS-sized parts, ragged token counts) vs torch fp32 of the
+    same bf16 operands (tolerance 1e-2 * max|ref|) and vs mmr_linear_bf16."""
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) * K ** -0.5
+    b = torch.randn(N, generator=g) if bias else None
+    r = torch.randn(M, N, generator=g) if res else None
+    ref = bf(x).float() @ bf(w).float().T
+    if b is not None:
+        ref = ref + b
+    if r is not None:
+        ref = ref + bf(r).float()
+    pk = ops.rw_pack(bf(w).to(DEV))
+    assert pk is not None
+    args = (b.to(DEV) if b is not None else None, bf(r).to(DEV) if r is not None else None)
+    y = ops.linear_rw(bf(x).to(DEV), pk, *args)
+    assert rel_err(y, ref) < 1e-2
+    y2 = ops.linear(bf(x).to(DEV), bf(w).to(DEV), *args)
+    assert rel_err(y, y2) < 1e-2
+
+
+def test_linear_rw_rejects():
+    assert ops.rw_pack(bf(torch.randn(96, 96)).to(DEV)) is None       # K = 96
+    assert ops.rw_pack(bf(torch.randn(3072, 768)).to(DEV)) is None    # K = 768
+
+
 @pytest.mark.parametrize("T,C", [(1000, 96), (3136 * 4 + 17, 96), (64, 192), (784 * 8 + 5, 192), (1, 96)])
 def test_swin_mlp_fused(T, C):
     """mmr_swin_mlp == x + fc2(GELU(fc1(LN(x)))) (fusion.py:198-199 via timm Mlp), ragged token counts;

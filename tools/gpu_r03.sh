@@ -94,6 +94,8 @@ for s in $STEPS; do
         timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 30 --pipeline $pp ${BENCHARGS:-} > $OUT/pipe_${pp}_$i.json 2> $OUT/pipe_${pp}_$i.err
         python -c "import json;d=json.load(open('$OUT/pipe_${pp}_$i.json'));print('pipeline $pp', round(d['ms_per_step'],3), round(d['value']), round(d['roofline']['knn']['ms_per_launch']*1e3,1))"
       done; done ;;
+    rw)
+      timeout -k 10 200 python -u tools/rw_bench.py > $OUT/rw.txt 2>&1; grep -v amdgpu.ids $OUT/rw.txt ;;
     breakdown)  # per-(op, shape) times of one sequential cfg2 step
       MMR_TOWER_STREAMS=0 MMR_FUSION_STREAMS=0 timeout -k 10 300 python -u tools/step_breakdown.py > $OUT/breakdown.txt 2>&1; grep -v amdgpu.ids $OUT/breakdown.txt | head -70 ;;
     nck)

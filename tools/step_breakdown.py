@@ -34,7 +34,8 @@ rec = []
 names = ["linear", "layernorm", "add_layernorm", "scaled_add_layernorm", "bert_embed", "bert_attention",
          "swin_window_attention", "patch_im2col", "patch_merge_ln", "swin_head", "mean_tokens", "proj_head",
          "swin_mlp", "swin_attn_block", "linear_f32", "linear_f32_batched", "mha", "add_pos", "ln_rows",
-         "assemble_seq", "rows_to_f32", "quantize_mxfp8", "linear_mxfp8", "linear_mxfp8_q8", "layernorm_q8"]
+         "assemble_seq", "rows_to_f32", "quantize_mxfp8", "linear_mxfp8", "linear_mxfp8_q8", "layernorm_q8",
+         "linear_rw"]
 
 
 def wrap(name, fn):
@@ -50,6 +51,10 @@ def wrap(name, fn):
             key = (name, a[0].q.shape[0], a[1].q.shape[0], a[0].kp, k.get("act", 0), (a[3] if len(a) > 3 else k.get("residual")) is not None)
         elif name == "quantize_mxfp8":
             key = (name, a[0].numel() // a[0].shape[-1], 0, a[0].shape[-1], 0, False)
+        if name == "linear_rw":
+            x, pk = a[0], a[1]
+            res = (k.get("residual") if "residual" in k else (a[3] if len(a) > 3 else None)) is not None
+            key = (name, x.numel() // pk.k, pk.n, pk.k, 0, res)
         if name == "linear":
             x, wt = a[0], a[1]
             K = x.shape[-1]
