@@ -511,7 +511,9 @@ inline int p8_nt(int64_t m, int64_t n, int64_t esz) {
     const char* e = getenv("MMR_P8_NT");
     return e ? atoi(e) : -1;
   }();
-  return force >= 0 ? force : (m * n * esz > (int64_t)256 << 20 ? 1 : 0);
+  // 128 MB: the cfg2 BERT / fusion QKV outputs (151 MB) stream too (QKV 121 -> 118.5 us, step
+  // 15.58 -> 15.51 ms same box, profiles/r03_s4_nt_store_step.txt); the 50 MB O / FFN2 outputs measured equal
+  return force >= 0 ? force : (m * n * esz > (int64_t)128 << 20 ? 1 : 0);
 }
 
 template <int NT, bool FP8 = false, int KNN = 0>

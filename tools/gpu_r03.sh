@@ -89,10 +89,10 @@ for s in $STEPS; do
         timeout -k 10 120 python -u tools/swa_bench.py new >> $OUT/swa.txt 2>&1
         MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/${ABLIB:-libmmr_head.so} timeout -k 10 120 python -u tools/swa_bench.py old >> $OUT/swa.txt 2>&1
       done; grep -v amdgpu.ids $OUT/swa.txt ;;
-    pipeab)  # cfg2 step: stream-lane pipelining depth ${PIPES:-1 2 3}, same box
-      for i in 1 2; do for pp in ${PIPES:-1 2 3}; do
-        timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 30 --pipeline $pp ${BENCHARGS:-} > $OUT/pipe_${pp}_$i.json 2> $OUT/pipe_${pp}_$i.err
-        python -c "import json;d=json.load(open('$OUT/pipe_${pp}_$i.json'));print('pipeline $pp', round(d['ms_per_step'],3), round(d['value']), round(d['roofline']['knn']['ms_per_launch']*1e3,1))"
+    envab)  # cfg2 step with env setting A / B (ENVA / ENVB, e.g. "MMR_P8_NT=1"), same box
+      for i in 1 2; do for e in "${ENVA:-X=0}" "${ENVB:-X=1}"; do
+        env $e timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 30 ${BENCHARGS:-} > $OUT/envab.json 2> $OUT/envab.err
+        python -c "import json;d=json.load(open('$OUT/envab.json'));print('$e', round(d['ms_per_step'],3), round(d['value']), {k:round(v['ms_per_launch']*1e3,1) for k,v in d['roofline']['bert_gemms'].items()})"
       done; done ;;
     rw)
       timeout -k 10 200 python -u tools/rw_bench.py > $OUT/rw.txt 2>&1; grep -v amdgpu.ids $OUT/rw.txt ;;
