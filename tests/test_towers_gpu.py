@@ -268,6 +268,21 @@ def test_patch_im2col_and_merge():
     assert rel_err(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize("B,H,C", [(2, 28, 96), (3, 14, 192), (1, 14, 384), (1, 2, 96), (5, 6, 192)])
+def test_patch_merge_ln_geometries(B, H, C):
+    """PatchMerging gather + LN (timm: x0..x3 = x[0::2,0::2], x[1::2,0::2], x[0::2,1::2], x[1::2,1::2]
+    concatenated, LayerNorm(4C)) for the grouped-lane forms (4C = 384 / 768) and the generic one,
+    incl. output row counts that leave a partial wave."""
+    g0 = torch.Generator().manual_seed(B * H + C)
+    x = torch.randn(B, H, H, C, generator=g0)
+    g, b = torch.randn(4 * C, generator=g0), torch.randn(4 * C, generator=g0)
+    xx = bf(x).float()
+    h2 = H // 2
+    ref = F.layer_norm(xx.reshape(B, h2, 2, h2, 2, C).permute(0, 1, 3, 4, 2, 5).flatten(3), (4 * C,), g, b, 1e-5)
+    y = ops.patch_merge_ln(bf(x).to(DEV), g.to(DEV), b.to(DEV), 1e-5)
+    assert rel_err(y, ref) < 1e-2
+
+
 def test_swin_head_and_means():
     x = torch.randn(3, 49, 768) * 2
     g, b = torch.rand(768) + 0.5, torch.randn(768) * 0.1

@@ -94,6 +94,15 @@ for s in $STEPS; do
         env $e timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 30 ${BENCHARGS:-} > $OUT/envab.json 2> $OUT/envab.err
         python -c "import json;d=json.load(open('$OUT/envab.json'));print('$e', round(d['ms_per_step'],3), round(d['value']), {k:round(v['ms_per_launch']*1e3,1) for k,v in d['roofline']['bert_gemms'].items()})"
       done; done ;;
+    mlpab)  # fused Swin MLP: this tree vs tools/ab/${ABLIB}
+      for i in 1 2; do
+        timeout -k 10 120 python -u tools/mlp_bench.py >> $OUT/mlpab_new.txt 2>&1
+        MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/${ABLIB} timeout -k 10 120 python -u tools/mlp_bench.py >> $OUT/mlpab_old.txt 2>&1
+      done; echo new; grep -v amdgpu.ids $OUT/mlpab_new.txt; echo $ABLIB; grep -v amdgpu.ids $OUT/mlpab_old.txt ;;
+    trace)  # kernel trace of sequential cfg2 steps; launch list of step 4 (TRACEFLT filters names)
+      MMR_TOWER_STREAMS=0 MMR_FUSION_STREAMS=0 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace -o tr \
+        -- python3 bench.py --steps 6 --warmup 2 --no-cpu-baseline > $OUT/trace.log 2>&1
+      f=$(find $OUT/trace -name "*kernel_trace.csv" | head -1); python tools/step_list.py "$f" 4 "${TRACEFLT:-}" > $OUT/step_list.txt; cat $OUT/step_list.txt | tail -${TRACEN:-60} ;;
     rw)
       timeout -k 10 200 python -u tools/rw_bench.py > $OUT/rw.txt 2>&1; grep -v amdgpu.ids $OUT/rw.txt ;;
     breakdown)  # per-(op, shape) times of one sequential cfg2 step
