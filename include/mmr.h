@@ -168,6 +168,17 @@ mmr_status mmr_linear_rw_pack(const uint16_t* w, int32_t n, int32_t k, uint16_t*
 mmr_status mmr_linear_rw(const uint16_t* x, const uint16_t* img, const float* bias, const uint16_t* residual,
                          uint16_t* y, int64_t m, int32_t n, int32_t k, void* stream);
 
+/* Per-query f32 linears on bf16x3 MFMA (the multimodal head's per-vector chain, reference model.py:375-459):
+ * y = act(x @ W^T + bias) (+ residual), x / y / residual f32 rows (strides ldx / ldy / ldr), W given as its
+ * bf16 split W_hi = bf16(W), W_lo = bf16(W - W_hi) ([cout][cin] each); x is split the same way in
+ * registers and each product summed as hi*hi + hi*lo + lo*hi in f32 (~2^-17 relative per product).
+ * nbatch independent problems at element strides bsx / bsw / bsb / bsr / bsy (nbatch = 1: one linear).
+ * cin % 128 == 0, cout % 32 == 0; residual may alias y. */
+mmr_status mmr_linear_x3(const float* x, int64_t ldx, int64_t bsx, const uint16_t* w_hi, const uint16_t* w_lo,
+                         int64_t bsw, const float* bias, int64_t bsb, const float* residual, int64_t ldr, int64_t bsr,
+                         float* y, int64_t ldy, int64_t bsy, int32_t nbatch, int32_t b, int32_t cin, int32_t cout,
+                         int32_t act, void* stream);
+
 /* ---------------------------------------------------------------- MX-fp8 linears (config 5) */
 /* Quantise bf16 x [rows][k] to OCP e4m3 q [rows][kp] (zero-padded, kp >= k, kp % 256 == 0) with one
  * E8M0 scale per 32 consecutive k of a row: 2^e, the smallest e with amax <= 448 * 2^e (no clipping);

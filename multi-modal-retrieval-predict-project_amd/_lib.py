@@ -41,6 +41,8 @@ SIGNATURES = {
     "mmr_linear_rw_parts": [c_i32, c_i32],
     "mmr_linear_rw_pack": [c_vp, c_i32, c_i32, c_vp, c_vp],
     "mmr_linear_rw": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp],
+    "mmr_linear_x3": [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,
+                      c_i32, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_quantize_mxfp8": [c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp],
     "mmr_linear_mxfp8": [c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp],
     "mmr_linear_mxfp8_q8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp],

@@ -19,9 +19,11 @@ Every fusion layer reads the SAME backbone features (img_global, img_patches, tx
                    affine out_proj, so mha emits the mean directly (no B*L x D out_proj GEMM)
   fused sequence   [ln_img(.); img_patch_proj(P) + out_proj(img2txt); ln_txt(.)] + pe  ->  QKV GEMM
                    -> mha with mean output -> one f32 out_proj row per batch (model.py:431 mean)
-  joint chain      f32 (B, D): norm1 / alpha residual, norm2 -> FFN, adapter (exact f32 MFMA linears)
+  joint chain      f32 (B, D): norm1 / alpha residual, norm2 -> FFN, adapter (f32 vectors, linears on
+                   bf16x3 MFMA: ops.linear_x3, ~2^-17 relative per product)
 
-bf16 activations / f32 accumulation for the token-level work, f32 for every per-query vector.
+bf16 activations / f32 accumulation for the token-level work, f32 for every per-query vector (its
+linears on bf16x3 MFMA).
 tower_dtype="fp8" (BASELINE config 5): the token-level GEMMs fed by an enhancer's input or output —
 each enhancer's in_proj and the folded text / patch cross projections + img_patch_proj, 72 % of the
 stack's token FLOPs — run on the MX-fp8 GEMM; their activation operands come out of the producing
@@ -169,6 +171,15 @@ class FusionStack:
         self.o2_w_all, self.o2_b_all = st("o2_w"), st("o2_b")
         self.gp_w_all, self.gp_b_all = st("gp_w"), st("gp_b")
         self.tp_w_all, self.tp_b_all = st("tp_w"), st("tp_b")
+        # bf16x3 splits of every per-query weight (ops.linear_x3: 1/5 of the f32 MFMA time)
+        X3 = ops.X3W
+        self.g_w_x3 = X3(self.g_w_all)
+        self.o1_x3, self.o2_x3, self.gp_x3, self.tp_x3 = (X3(self.o1_w_all), X3(self.o2_w_all), X3(self.gp_w_all),
+                                                          X3(self.tp_w_all))
+        self.s_ow_x3 = X3(self.s_ow)
+        for L in Ls:
+            L["ffn_x3"] = (X3(L["ffn"][0]), X3(L["ffn"][2]))
+            L["ad_x3"] = (X3(L["ad"][0]), X3(L["ad"][2]))
         self.ln_img_all = tuple(torch.stack([L["ln_img"][k] for L in Ls]).contiguous() for k in (0, 1))
         self.ln_txt_all = tuple(torch.stack([L["ln_txt"][k] for L in Ls]).contiguous() for k in (0, 1))
 
@@ -261,20 +272,20 @@ class FusionStack:
             ops.linear(a2, L["o2_wb"], L["o2_b"], residual=PP, out=PF[i])  # patches_fused (fusion.py:437)
         del pq, pp
         # phase 2: per-query vectors of all layers
-        Ge = ops.linear_f32(G, self.g_w_all, self.g_b_all)             # (B, nl*Ci), layer-minor
+        Ge = ops.linear_x3(G, self.g_w_x3, self.g_b_all)               # (B, nl*Ci), layer-minor
         Ge = ops.ln_rows(Ge.view(B * nl, Ci), *self.g_ln_all, eps, groups=nl).view(B, nl * Ci)
-        t2i = ops.linear_f32_batched(m1, self.o1_w_all, self.o1_b_all, nl, B)          # mean_L att_txt2img
-        x1 = ops.linear_f32_batched(Ge, self.gp_w_all, self.gp_b_all, nl, B, residual=t2i, ldx=nl * Ci, bsx=Ci)
+        t2i = ops.linear_x3_batched(m1, self.o1_x3, self.o1_b_all, nl, B)              # mean_L att_txt2img
+        x1 = ops.linear_x3_batched(Ge, self.gp_x3, self.gp_b_all, nl, B, residual=t2i, ldx=nl * Ci, bsx=Ci)
         x1 = ops.ln_rows(x1.view(nl * B, D), *self.ln_img_all, eps, groups=nl, group_div=B)
-        i2t = ops.linear_f32_batched(m2, self.o2_w_all, self.o2_b_all, nl, B)          # mean_Np att_img2txt
-        x2 = ops.linear_f32_batched(cls, self.tp_w_all, self.tp_b_all, nl, B, residual=i2t)
+        i2t = ops.linear_x3_batched(m2, self.o2_x3, self.o2_b_all, nl, B)              # mean_Np att_img2txt
+        x2 = ops.linear_x3_batched(cls, self.tp_x3, self.tp_b_all, nl, B, residual=i2t)
         x2 = ops.ln_rows(x2.view(nl * B, D), *self.ln_txt_all, eps, groups=nl, group_div=B)
         # phase 3: the shared combiner self-attention over every layer's fused sequence
         S = ops.assemble_seq(x1, PF.view(nl * B * Np, D), x2, self.pe, Np).view(nl * B * (Np + 2), D)
         SQ = ops.linear(S, self.s_w, self.s_b)
         m3 = torch.empty((nl * B, D), dtype=torch.float32, device=dev)
         ops.mha(SQ[:, :D], SQ[:, D:2 * D], SQ[:, 2 * D:], nl * B, Np + 2, Np + 2, h, dh, sc, mean_out=m3)
-        fused = ops.linear_f32(m3, self.s_ow, self.s_ob).view(nl, B, D)  # mean of self_attn output
+        fused = ops.linear_x3(m3, self.s_ow_x3, self.s_ob).view(nl, B, D)  # mean of self_attn output
         # phase 4: the joint chain
         joint = None
         for i, L in enumerate(self.layers):
@@ -283,9 +294,11 @@ class FusionStack:
             else:  # norm1(joint) + alpha * fused  (StochasticDepth in eval = plain residual)
                 x = ops.ln_rows(joint, *L["n1"], eps, post=fused[i], post_scale=self.alpha)
             xf = ops.ln_rows(x, *L["n2"], eps)
-            w1, b1, w2, b2 = L["ffn"]
-            ops.linear_f32(ops.linear_f32(xf, w1, b1, act=1), w2, b2, residual=x, out=x)
-            a1, c1, a2, c2 = L["ad"]
-            ops.linear_f32(ops.linear_f32(x, a1, c1, act=1), a2, c2, residual=x, out=x)
+            _, b1, _, b2 = L["ffn"]
+            w1, w2 = L["ffn_x3"]
+            ops.linear_x3(ops.linear_x3(xf, w1, b1, act=1), w2, b2, residual=x, out=x)
+            _, c1, _, c2 = L["ad"]
+            a1, a2 = L["ad_x3"]
+            ops.linear_x3(ops.linear_x3(x, a1, c1, act=1), a2, c2, residual=x, out=x)
             joint = x
         return joint.contiguous()

@@ -279,6 +279,61 @@ def linear_f32(x, w, bias=None, residual=None, act=0, out=None):
     return y
 
 
+class X3W:
+    """A per-query linear weight for linear_x3: the f32 weight (kept for the exact-f32 fallback) and its
+    bf16 split hi = bf16(w), lo = bf16(w - hi); (..., cout, cin)."""
+    __slots__ = ("w", "hi", "lo")
+
+    def __init__(self, w):
+        self.w = w.contiguous()
+        self.hi = self.w.to(torch.bfloat16)
+        self.lo = (self.w - self.hi.float()).to(torch.bfloat16)
+
+
+def _x3_ok(cin, cout):
+    return cin % 128 == 0 and cout % 32 == 0
+
+
+def linear_x3(x, wx, bias=None, residual=None, act=0, out=None):
+    """act(x @ w.T + bias) (+ residual) on bf16x3 MFMA (mmr_linear_x3; ~2^-17 relative per product);
+    x (B, cin) f32 rows (unit column stride), residual may be `out`.  Shapes the kernel does not take
+    (cin % 128, cout % 32) run linear_f32."""
+    cout, cin = wx.w.shape
+    if not _x3_ok(cin, cout):
+        return linear_f32(x, wx.w, bias, residual=residual, act=act, out=out)
+    _lib.require_gpu(x)
+    assert x.dim() == 2 and x.stride(1) == 1
+    B = x.shape[0]
+    y = out if out is not None else torch.empty((B, cout), dtype=torch.float32, device=x.device)
+    ldr = residual.stride(0) if residual is not None else 0
+    _chk(_L().mmr_linear_x3(_lib.ptr(x), x.stride(0), 0, _lib.ptr(wx.hi), _lib.ptr(wx.lo), 0, _lib.ptr(bias), 0,
+                            _lib.ptr(residual), ldr, 0, _lib.ptr(y), y.stride(0), 0, 1, B, cin, cout, act, _s(x)),
+         "mmr_linear_x3")
+    return y
+
+
+def linear_x3_batched(x, wx, bias, nbatch, b, residual=None, act=0, out=None, ldx=None, bsx=None, ldy=None,
+                      bsy=None, ldr=None, bsr=None):
+    """linear_f32_batched on bf16x3 MFMA: wx.w (nbatch, cout, cin); same stride conventions."""
+    cout, cin = wx.w.shape[1], wx.w.shape[2]
+    if not _x3_ok(cin, cout):
+        return linear_f32_batched(x, wx.w, bias, nbatch, b, residual=residual, act=act, out=out, ldx=ldx, bsx=bsx,
+                                  ldy=ldy, bsy=bsy, ldr=ldr, bsr=bsr)
+    _lib.require_gpu(x)
+    ldx = cin if ldx is None else ldx
+    bsx = b * ldx if bsx is None else bsx
+    y = out if out is not None else torch.empty((nbatch, b, cout), dtype=torch.float32, device=x.device)
+    ldy = cout if ldy is None else ldy
+    bsy = b * ldy if bsy is None else bsy
+    if residual is not None:
+        ldr = cout if ldr is None else ldr
+        bsr = b * ldr if bsr is None else bsr
+    _chk(_L().mmr_linear_x3(_lib.ptr(x), ldx, bsx, _lib.ptr(wx.hi), _lib.ptr(wx.lo), cout * cin, _lib.ptr(bias),
+                            cout if bias is not None else 0, _lib.ptr(residual), ldr or 0, bsr or 0, _lib.ptr(y), ldy,
+                            bsy, nbatch, b, cin, cout, act, _s(x)), "mmr_linear_x3")
+    return y
+
+
 def mha(q, k, v, b, lq, lk, heads, dh, scale, out=None, mean_out=None):
     """Attention core over strided row views: q (b*lq, >=heads*dh) etc. (unit column stride)."""
     _lib.require_gpu(q)

@@ -62,6 +62,47 @@ def test_mha_strided_and_mean(B, lq, lk, heads, dh):
         assert rel_err(mean2, mean.cpu()) < 1e-5
 
 
+@pytest.mark.parametrize("B,cin,cout,act,bias,res", [(256, 768, 1536, 1, True, False), (256, 1536, 768, 0, True, True),
+                                                  (256, 768, 384, 1, True, False), (256, 384, 768, 0, True, True),
+                                                  (1280, 768, 768, 0, True, False), (7, 1024, 2048, 1, False, False)])
+def test_linear_x3(B, cin, cout, act, bias, res):
+    """mmr_linear_x3 (bf16x3 MFMA: hi*hi + hi*lo + lo*hi of the bf16 splits, f32 accumulation) vs an f64
+    reference: within 2e-5 * max|ref| (f32 linear_f32: 1e-5), ragged row counts, residual in place."""
+    g = torch.Generator().manual_seed(B + cin + cout)
+    x = torch.randn(B, cin, generator=g)
+    w = torch.randn(cout, cin, generator=g) * cin ** -0.5
+    b = torch.randn(cout, generator=g) if bias else None
+    r = torch.randn(B, cout, generator=g) if res else None
+    ref = x.double() @ w.double().T
+    if b is not None:
+        ref = ref + b.double()
+    if act == 1:
+        ref = torch.nn.functional.gelu(ref)
+    if r is not None:
+        ref = ref + r.double()
+    y = r.to(DEV) if r is not None else None
+    out = ops.linear_x3(x.to(DEV), ops.X3W(w.to(DEV)), b.to(DEV) if b is not None else None, residual=y, act=act,
+                        out=y)
+    err = (out.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-5, err
+
+
+def test_linear_x3_batched_strided():
+    """The batched form over strided row views (the fusion head's phase-2 layout: x rows of nl*C with
+    per-problem column offsets, residual per problem) == per-problem linear_f32 within 2e-5."""
+    g = torch.Generator().manual_seed(5)
+    nl, B, C, D = 5, 64, 768, 768
+    G = torch.randn(B, nl * C, generator=g).to(DEV)
+    w = (torch.randn(nl, D, C, generator=g) * C ** -0.5).to(DEV)
+    b = torch.randn(nl, D, generator=g).to(DEV)
+    r = torch.randn(nl, B, D, generator=g).to(DEV)
+    y = ops.linear_x3_batched(G, ops.X3W(w), b, nl, B, residual=r, ldx=nl * C, bsx=C)
+    for i in range(nl):
+        ref = ops.linear_f32(G[:, i * C:(i + 1) * C], w[i], b[i], residual=r[i])
+        err = (y[i] - ref).abs().max().item() / ref.abs().max().item()
+        assert err < 2e-5, (i, err)
+
+
 def test_linear_f32_strided_residual_inplace():
     g = torch.Generator().manual_seed(5)
     x = torch.randn(70, 200, generator=g)
