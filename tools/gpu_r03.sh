@@ -106,7 +106,7 @@ for s in $STEPS; do
     rw)
       timeout -k 10 200 python -u tools/rw_bench.py > $OUT/rw.txt 2>&1; grep -v amdgpu.ids $OUT/rw.txt ;;
     breakdown)  # per-(op, shape) times of one sequential cfg2 step
-      MMR_TOWER_STREAMS=0 MMR_FUSION_STREAMS=0 timeout -k 10 300 python -u tools/step_breakdown.py > $OUT/breakdown.txt 2>&1; grep -v amdgpu.ids $OUT/breakdown.txt | head -70 ;;
+      MMR_TOWER_STREAMS=0 MMR_FUSION_STREAMS=0 timeout -k 10 300 python -u tools/step_breakdown.py ${BDARGS:-} > $OUT/breakdown.txt 2>&1; grep -v amdgpu.ids $OUT/breakdown.txt | head -70 ;;
     nck)
       timeout -k 10 300 python -u tools/gemm_nck.py > $OUT/gemm_nck.txt 2>&1; cat $OUT/gemm_nck.txt ;;
     *) echo "unknown step $s"; exit 2 ;;
