@@ -249,7 +249,7 @@ __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __r
                                                              const float* __restrict__ bias,
                                                              uint16_t* __restrict__ out,
                                                              int64_t units, int H, int C,
-                                                             int heads, int ws, int shift) {
+                                                             int heads, int ws, int shift, int hpw) {
   // round 3: every global load of a wave (Q / K fragments, V rows, the bias rows of both query
   // tiles) is issued up front from clamped token indices (padded lanes read a real token and are
   // masked by the bias / the store guard): the previous form's "token valid ? load : 0" gathers
@@ -262,11 +262,11 @@ __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __r
   const int64_t unit = (int64_t)blockIdx.x * 4 + wave;
   if (unit >= units) return;
   const int nwin1 = H / ws;
-  // unit = (image, window, head pair): a wave reads whole 128-B lines of Q / K / V (two heads x 32
+  // unit = (image, window, head group of hpw): with hpw = 2 a wave reads whole 128-B lines of Q / K / V (two heads x 32
   // dims; the second head's loads hit the lines the first head's brought in) and writes whole
   // output lines — with one head per wave the two halves of every line were fetched by waves of
   // different workgroups, i.e. usually by different XCDs (2x the HBM / MALL reads)
-  const int nwin = nwin1 * nwin1, npair = (heads + 1) / 2;
+  const int nwin = nwin1 * nwin1, npair = (heads + hpw - 1) / hpw;
   const int hp = (int)(unit % npair);
   const int64_t bw = unit / npair;
   const int win = (int)(bw % nwin);
@@ -284,8 +284,8 @@ __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __r
     tl = (int)(bi * H * H + h0 * H + w0);
   }
 #pragma unroll 1
-  for (int h2 = 0; h2 < 2; ++h2) {
-    const int hh = 2 * hp + h2;
+  for (int h2 = 0; h2 < hpw; ++h2) {
+    const int hh = hpw * hp + h2;
     if (hh >= heads) break;
     const float* bt = bias + ((int64_t)type * heads + hh) * 4096;
     asm volatile("" ::: "memory");  // the previous head's V reads stay before this head's V writes
@@ -937,9 +937,13 @@ mmr_status mmr_swin_window_attention(const uint16_t* qkv, const float* bias, uin
   if (b == 0) return MMR_OK;
   MMR_REQUIRE((int64_t)b * hw * hw * 3 * c < ((int64_t)1 << 32), "mmr_swin_window_attention: %lld qkv elements (32-bit offsets)",
               (long long)b * hw * hw * 3 * c);
-  const int64_t units = (int64_t)b * (hw / ws) * (hw / ws) * ((heads + 1) / 2);
+  // head pairs per wave where single-head waves would be plentiful (stage 2: 24576 single units),
+  // one head per wave otherwise (stage 4, 6144 single units: 27 vs 31 us with pairs)
+  const int64_t single = (int64_t)b * (hw / ws) * (hw / ws) * heads;
+  const int hpw = single >= 16384 ? 2 : 1;
+  const int64_t units = (int64_t)b * (hw / ws) * (hw / ws) * ((heads + hpw - 1) / hpw);
   swin_window_attention<<<dim3((unsigned)mmr::ceil_div(units, 4)), 256, 0, mmr::as_stream(stream)>>>(
-      qkv, bias, out, units, hw, c, heads, ws, shift);
+      qkv, bias, out, units, hw, c, heads, ws, shift, hpw);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }
