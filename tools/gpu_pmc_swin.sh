@@ -10,7 +10,7 @@ P2="GRBM_GUI_ACTIVE GRBM_COUNT SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_MISC SQ_INSTS
 i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d $OUT/p$i -o p -- python3 tools/mlp_bench.py > $OUT/p$i.log 2>&1 || { echo "FAIL pass $i"; tail -5 $OUT/p$i.log; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d $OUT/p$i -o p -- python3 ${PMC_PY:-tools/mlp_bench.py} > $OUT/p$i.log 2>&1 || { echo "FAIL pass $i"; tail -5 $OUT/p$i.log; exit 1; }
   f=$(find $OUT/p$i -name "*counter_collection.csv" | head -1)
   for k in ${PMC_KERNELS:-swin_mlp_res<96 swin_mlp<192}; do echo "== pass $i $k"; python3 tools/pmc_summary.py $f "$k"; done
 done
