@@ -103,6 +103,14 @@ for s in $STEPS; do
       MMR_TOWER_STREAMS=0 MMR_FUSION_STREAMS=0 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace -o tr \
         -- python3 bench.py --steps 6 --warmup 2 --no-cpu-baseline > $OUT/trace.log 2>&1
       f=$(find $OUT/trace -name "*kernel_trace.csv" | head -1); python tools/step_list.py "$f" 4 "${TRACEFLT:-}" > $OUT/step_list.txt; cat $OUT/step_list.txt | tail -${TRACEN:-60} ;;
+    attab)  # attention cores (tools/mha_bench.py + tools/attn_ab.py): this tree vs tools/ab/${ABLIB:-libmmr_prev.so}
+      for i in 1 2; do
+        echo "== new $i" >> $OUT/attab.txt; timeout -k 10 120 python -u tools/mha_bench.py >> $OUT/attab.txt 2>&1
+        timeout -k 10 120 python -u tools/attn_ab.py >> $OUT/attab.txt 2>&1
+        echo "== old $i" >> $OUT/attab.txt
+        MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/${ABLIB:-libmmr_prev.so} timeout -k 10 120 python -u tools/mha_bench.py >> $OUT/attab.txt 2>&1
+        MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/${ABLIB:-libmmr_prev.so} timeout -k 10 120 python -u tools/attn_ab.py >> $OUT/attab.txt 2>&1
+      done; grep -v amdgpu.ids $OUT/attab.txt ;;
     rw)
       timeout -k 10 200 python -u tools/rw_bench.py > $OUT/rw.txt 2>&1; grep -v amdgpu.ids $OUT/rw.txt ;;
     breakdown)  # per-(op, shape) times of one sequential cfg2 step
