@@ -357,6 +357,12 @@ mmr_status mmr_linear_f32_batched(const float* x, int64_t ldx, int64_t bsx, cons
 mmr_status mmr_mha(const uint16_t* q, int64_t ldq, const uint16_t* k, int64_t ldk, const uint16_t* v,
                    int64_t ldv, uint16_t* out, int64_t ldo, float* mean_out, int32_t b, int32_t lq,
                    int32_t lk, int32_t heads, int32_t dh, float scale, void* stream);
+/* mmr_mha emitting its output (also) as the next GEMM's MX-fp8 activation operand: e4m3 q8
+ * [b*lq][heads*dh] + E8M0 scales in the layout-0 image of mmr_quantize_mxfp8 (bit-identical to
+ * quantising the bf16 rows); out may be NULL.  head_dim % 32 == 0, b*lq % 256 == 0, heads*dh % 256 == 0. */
+mmr_status mmr_mha_q8(const uint16_t* q, int64_t ldq, const uint16_t* k, int64_t ldk, const uint16_t* v, int64_t ldv,
+                      uint16_t* out, int64_t ldo, float* mean_out, uint8_t* q8, uint8_t* q8_scales, int32_t b,
+                      int32_t lq, int32_t lk, int32_t heads, int32_t dh, float scale, void* stream);
 
 /* y = x + pos[row % l] -> bf16 (rows, c); x f32 (x_is_f32) or bf16; pos f32 [>= l][c]
  * (PreFusionEnhancer.pos_embed fusion.py:32). c % 8 == 0. */

@@ -70,6 +70,8 @@ SIGNATURES = {
     "mmr_linear_f32": [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_mha": [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_f32,
                 c_vp],
+    "mmr_mha_q8": [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32,
+                   c_i32, c_f32, c_vp],
     "mmr_add_pos_bf16": [c_vp, c_i32, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp],
     "mmr_add_pos_bf16_q8": [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp],
     "mmr_ln_rows": [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_i32, c_f32,

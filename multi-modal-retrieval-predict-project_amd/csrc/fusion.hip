@@ -605,6 +605,19 @@ mmr_status mmr_bert_attention(const uint16_t* qkv, const int64_t* mask01, uint16
                     b, l, l, h, dh, 1.0f / sqrtf((float)dh), stream);
 }
 
+// mmr_mha with the output as the next GEMM's MX-fp8 activation operand as well (or instead: out may
+// be NULL): e4m3 [b*lq][heads*dh] + E8M0 scales in the layout-0 image, bit-identical to
+// mmr_quantize_mxfp8 of the bf16 rows (the fusion head's enhancer / cross-attention out-projections
+// on the fp8 path)
+mmr_status mmr_mha_q8(const uint16_t* q, int64_t ldq, const uint16_t* k, int64_t ldk, const uint16_t* v, int64_t ldv,
+                      uint16_t* out, int64_t ldo, float* mean_out, uint8_t* q8, uint8_t* q8_scales, int32_t b,
+                      int32_t lq, int32_t lk, int32_t heads, int32_t dh, float scale, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(q8 && q8_scales, "mmr_mha_q8: NULL pointer");
+  return launch_mha("mmr_mha_q8", q, ldq, k, ldk, v, ldv, out, ldo, mean_out, nullptr, b, lq, lk, heads, dh, scale,
+                    stream, q8, q8_scales);
+}
+
 mmr_status mmr_bert_attention_q8(const uint16_t* qkv, const int64_t* mask01, uint16_t* ctx, uint8_t* q8,
                                  uint8_t* q8_scales, int32_t b, int32_t l, int32_t h, int32_t dh, void* stream) {
   mmr::clear_error();

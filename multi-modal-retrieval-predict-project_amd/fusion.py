@@ -24,11 +24,11 @@ Every fusion layer reads the SAME backbone features (img_global, img_patches, tx
 
 bf16 activations / f32 accumulation for the token-level work, f32 for every per-query vector (its
 linears on bf16x3 MFMA).
-tower_dtype="fp8" (BASELINE config 5): the token-level GEMMs fed by an enhancer's input or output —
-each enhancer's in_proj and the folded text / patch cross projections + img_patch_proj, 72 % of the
-stack's token FLOPs — run on the MX-fp8 GEMM; their activation operands come out of the producing
-add-pos / LayerNorm kernels (no quantise pass).  Batches whose token rows are not a 256 multiple
-keep bf16 there.
+tower_dtype="fp8" (BASELINE config 5): the token-level GEMMs — each enhancer's in_proj and out_proj,
+the folded text / patch cross projections + img_patch_proj, and the img2txt out-projection
+(patches_fused) — run on the MX-fp8 GEMM; their activation operands come out of the producing
+add-pos / attention / LayerNorm kernels (no quantise pass).  Batches whose token rows are not a 256
+multiple keep bf16 there.
 """
 import math
 import os
@@ -69,6 +69,7 @@ class _Enhancer:
         self.alpha = _f(sd[p + "alpha"].reshape(1), dev)
         self.g, self.b = _f(sd[p + "norm1.weight"], dev), _f(sd[p + "norm1.bias"], dev)
         self.w_in8 = _w8(self.w_in) if fp8 and C % 256 == 0 else None
+        self.w_o8 = _w8(self.w_o) if fp8 and C % 256 == 0 else None
 
     def fp8_ok(self, rows):
         return self.w_in8 is not None and rows % 256 == 0
@@ -76,17 +77,21 @@ class _Enhancer:
     def __call__(self, x, B, L, eps, q8=False):
         """x (B*L, C) f32 or bf16 -> LN(alpha*(x + pos) + MHA(x + pos)) bf16 (B*L, C); q8 (fp8 path):
         (y, its MX-fp8 operand)."""
+        C = self.C
         if self.fp8_ok(B * L):
+            # MX-fp8: the add-pos kernel emits the in_proj operand, the attention core the out_proj one
             X, X8 = ops.add_pos(x, self.pos, L, q8=True)
             qkv = ops.linear_mxfp8(X8, self.w_in8, self.b_in)
+            _, _, a8 = ops.mha(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], B, L, L, self.heads, self.dh,
+                               1.0 / math.sqrt(self.dh), q8=True)
+            x2 = ops.linear_mxfp8(a8, self.w_o8, self.b_o)
         else:
             X = ops.add_pos(x, self.pos, L)
             qkv = ops.linear(X, self.w_in, self.b_in)
-        a = torch.empty_like(X)
-        C = self.C
-        ops.mha(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], B, L, L, self.heads, self.dh,
-                1.0 / math.sqrt(self.dh), out=a)
-        x2 = ops.linear(a, self.w_o, self.b_o)
+            a = torch.empty_like(X)
+            ops.mha(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], B, L, L, self.heads, self.dh,
+                    1.0 / math.sqrt(self.dh), out=a)
+            x2 = ops.linear(a, self.w_o, self.b_o)
         return ops.scaled_add_layernorm(X, self.alpha, x2, self.g, self.b, eps, q8=q8)
 
 
@@ -135,11 +140,11 @@ class FusionStack:
             L["p_w"] = _bf(torch.cat([ki[0], vi[0], qi[0]]), dev)
             L["p_b"] = _f(torch.cat([ki[1], vi[1], qi[1]]), dev)
             L["pp_w"], L["pp_b"] = _bf(g("img_patch_proj.weight"), dev), _f(g("img_patch_proj.bias"), dev)
-            if fp8:
-                for k in ("t_w", "p_w", "pp_w"):
-                    L[k + "8"] = _w8(L[k])
             L["o1_w"], L["o1_b"] = _f(g("attn_txt2img.out_proj.weight"), dev), _f(g("attn_txt2img.out_proj.bias"), dev)
             L["o2_wb"] = _bf(g("attn_img2txt.out_proj.weight"), dev)
+            if fp8:
+                for k in ("t_w", "p_w", "pp_w", "o2_wb"):
+                    L[k + "8"] = _w8(L[k])
             L["o2_w"], L["o2_b"] = _f(g("attn_img2txt.out_proj.weight"), dev), _f(g("attn_img2txt.out_proj.bias"), dev)
             L["gp_w"], L["gp_b"] = _f(g("img_global_proj.weight"), dev), _f(g("img_global_proj.bias"), dev)
             L["tp_w"], L["tp_b"] = _f(g("txt_proj.weight"), dev), _f(g("txt_proj.bias"), dev)
@@ -267,9 +272,14 @@ class FusionStack:
                 main.wait_event(ev[i])
             PQ, PP = pq[i], pp[i]
             ops.mha(TQ[:, :D], PQ[:, :D], PQ[:, D:2 * D], B, Lt, Np, h, dh, sc, mean_out=m1[i])
-            a2 = torch.empty((B * Np, D), dtype=torch.bfloat16, device=dev)
-            ops.mha(PQ[:, 2 * D:], TQ[:, D:2 * D], TQ[:, 2 * D:], B, Np, Lt, h, dh, sc, out=a2, mean_out=m2[i])
-            ops.linear(a2, L["o2_wb"], L["o2_b"], residual=PP, out=PF[i])  # patches_fused (fusion.py:437)
+            if self.fp8 and (B * Np) % 256 == 0 and D % 256 == 0:  # the attention core emits the o2 operand
+                _, _, a28 = ops.mha(PQ[:, 2 * D:], TQ[:, D:2 * D], TQ[:, 2 * D:], B, Np, Lt, h, dh, sc, mean_out=m2[i],
+                                    q8=True)
+                ops.linear_mxfp8(a28, L["o2_wb8"], L["o2_b"], residual=PP, out=PF[i])  # patches_fused (fusion.py:437)
+            else:
+                a2 = torch.empty((B * Np, D), dtype=torch.bfloat16, device=dev)
+                ops.mha(PQ[:, 2 * D:], TQ[:, D:2 * D], TQ[:, 2 * D:], B, Np, Lt, h, dh, sc, out=a2, mean_out=m2[i])
+                ops.linear(a2, L["o2_wb"], L["o2_b"], residual=PP, out=PF[i])  # patches_fused (fusion.py:437)
         del pq, pp
         # phase 2: per-query vectors of all layers
         Ge = ops.linear_x3(G, self.g_w_x3, self.g_b_all)               # (B, nl*Ci), layer-minor

@@ -334,9 +334,17 @@ def linear_x3_batched(x, wx, bias, nbatch, b, residual=None, act=0, out=None, ld
     return y
 
 
-def mha(q, k, v, b, lq, lk, heads, dh, scale, out=None, mean_out=None):
-    """Attention core over strided row views: q (b*lq, >=heads*dh) etc. (unit column stride)."""
+def mha(q, k, v, b, lq, lk, heads, dh, scale, out=None, mean_out=None, q8=False):
+    """Attention core over strided row views: q (b*lq, >=heads*dh) etc. (unit column stride).  q8: the
+    output also as an MX-fp8 activation operand, returned as (out, mean_out, MXFP8)."""
     _lib.require_gpu(q)
+    if q8:
+        c = heads * dh
+        q8t, s8 = _q8_out(b * lq, c, q.device)
+        _chk(_L().mmr_mha_q8(_lib.ptr(q), q.stride(0), _lib.ptr(k), k.stride(0), _lib.ptr(v), v.stride(0),
+                             _lib.ptr(out), out.stride(0) if out is not None else 0, _lib.ptr(mean_out),
+                             _lib.ptr(q8t), _lib.ptr(s8), b, lq, lk, heads, dh, float(scale), _s(q)), "mmr_mha_q8")
+        return out, mean_out, MXFP8(q8t, s8, c, 0)
     _chk(_L().mmr_mha(_lib.ptr(q), q.stride(0), _lib.ptr(k), k.stride(0), _lib.ptr(v), v.stride(0),
                       _lib.ptr(out), out.stride(0) if out is not None else 0, _lib.ptr(mean_out), b, lq, lk,
                       heads, dh, float(scale), _s(q)), "mmr_mha")

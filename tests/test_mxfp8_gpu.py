@@ -177,3 +177,24 @@ def test_bert_attention_q8_equals_quantised_context(B, L, heads, dh):
     assert torch.equal(ctx, ref)
     for x8 in (c8, c8b):
         assert torch.equal(x8.q, ref8.q) and torch.equal(x8.s, ref8.s)
+
+
+@pytest.mark.parametrize("B,lq,lk,heads,dh", [(256, 49, 128, 8, 96), (4, 128, 128, 8, 128), (512, 49, 64, 8, 96)])
+def test_mha_q8_equals_quantised_output(B, lq, lk, heads, dh):
+    """mmr_mha_q8 (the fusion head's fp8 out-projection operands, strided Q / K / V views of packed
+    projections, ragged lq = 49 with the mean output beside it): the operand equals mmr_quantize_mxfp8 of
+    the plain kernel's bf16 output bit for bit, and the mean is unchanged."""
+    g = torch.Generator().manual_seed(B + lq + lk + dh)
+    C = heads * dh
+    qp = (torch.randn(B * lq, 3 * C, generator=g) * 2).to(torch.bfloat16).to(DEV)
+    kv = (torch.randn(B * lk, 3 * C, generator=g) * 2).to(torch.bfloat16).to(DEV)
+    sc = 1.0 / dh ** 0.5
+    out = torch.empty(B * lq, C, dtype=torch.bfloat16, device=DEV)
+    m_ref = torch.empty(B, C, device=DEV)
+    ops.mha(qp[:, 2 * C:], kv[:, C:2 * C], kv[:, 2 * C:], B, lq, lk, heads, dh, sc, out=out, mean_out=m_ref)
+    m8 = torch.empty(B, C, device=DEV)
+    _, _, a8 = ops.mha(qp[:, 2 * C:], kv[:, C:2 * C], kv[:, 2 * C:], B, lq, lk, heads, dh, sc, mean_out=m8, q8=True)
+    ref8 = ops.quantize_mxfp8(out, layout=0)
+    torch.cuda.synchronize()
+    assert torch.equal(a8.q, ref8.q) and torch.equal(a8.s, ref8.s)
+    assert torch.equal(m8, m_ref)
