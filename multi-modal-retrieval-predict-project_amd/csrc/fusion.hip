@@ -24,7 +24,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // softmax(q k^T * scale) v per (batch, head): the fusion's short sequences (text L <= 512,
 // 49 patches, 51-token fused sequence; no masks) and BERT self-attention (MASK: key-padding mask,
 // HF BertSelfAttention).  Block = (batch*head, chunk of 128 queries), one 32-query tile per wave;
-// keys stream through LDS in blocks of MHA_KB with an online softmax.  The swapped product
+// keys stream through LDS in blocks of kbs (64 / 128) with an online softmax.  The swapped product
 // S^T = K . Q^T on v_mfma_f32_32x32x16_bf16 puts the query on the lane, the softmax reductions
 // stay in registers, and P^T feeds the P.V MFMA as its B operand with no data movement (V^T read
 // in the matching key permutation).  head_dim is
@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256, DT == 1 ? 4 : (DT <= 3 ? 3 : 2)) void mha_smal
                                                  uint16_t* __restrict__ out, int64_t ldo,
                                                  float* __restrict__ mean_out,
                                                  const int64_t* __restrict__ kmask, int lq, int lk,
-                                                 int heads, int dh, float scale,
+                                                 int heads, int dh, float scale, int kbs,
                                                  uint8_t* __restrict__ q8 = nullptr,
                                                  uint8_t* __restrict__ q8s = nullptr) {
   constexpr int DHP = DT * 32;
@@ -61,13 +61,16 @@ __global__ __launch_bounds__(256, DT == 1 ? 4 : (DT <= 3 ? 3 : 2)) void mha_smal
   const int unit = mmr::xcd_contiguous(blockIdx.x, gridDim.x);
   const int bi = unit / heads, hh = unit % heads;
   const int lkp = (lk + 31) & ~31;
-  uint16_t* Ks = (uint16_t*)smem;            // [MHA_KB][KROW]
-  uint16_t* Vs = Ks + MHA_KB * KROW;         // [MHA_KB][VROW], natural (key-major) layout
+  // LDS sized to the launch (mha_lds_bytes): kbs keys per staged block (64 / 128), one epilogue
+  // area per wave — a 49-query / 51-key call then takes half the LDS of a 128 x 128 one, and with it
+  // twice the workgroups per CU
+  const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6, nwv = nthr >> 6;
+  uint16_t* Ks = (uint16_t*)smem;            // [kbs][KROW]
+  uint16_t* Vs = Ks + kbs * KROW;            // [kbs][VROW], natural (key-major) layout
   // [waves][DHP] per-wave partial means, after the larger of the K/V image and the epilogue area
-  constexpr int KV_BYTES = MHA_KB * (KROW + VROW) * 2, RED_BYTES = 4 * DHP * 33 * 4;
-  float* msum = (float*)(smem + (KV_BYTES > RED_BYTES ? KV_BYTES : RED_BYTES));
-  float* madd = msum + 4 * DHP;  // [MHA_KB] additive key mask of the current key block (kmask)
-  const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6;
+  const int kv_bytes = kbs * (KROW + VROW) * 2, red_bytes = nwv * DHP * 33 * 4;
+  float* msum = (float*)(smem + (kv_bytes > red_bytes ? kv_bytes : red_bytes));
+  float* madd = msum + nwv * DHP;  // [kbs] additive key mask of the current key block (kmask)
   const uint16_t* kbase = k + (int64_t)bi * lk * ldk + hh * dh;
   const uint16_t* vbase = v + (int64_t)bi * lk * ldv + hh * dh;
 
@@ -91,8 +94,8 @@ __global__ __launch_bounds__(256, DT == 1 ? 4 : (DT <= 3 ? 3 : 2)) void mha_smal
   for (int dt = 0; dt < DT; ++dt) o[dt] = (f32x16){0};
   float m_run = -FLT_MAX, l_run = 0.f;
   const float c2 = scale * 1.4426950408889634f;  // scale * log2(e)
-  for (int k0 = 0; k0 < lkp; k0 += MHA_KB) {
-    const int kn = min(MHA_KB, lkp - k0);   // keys staged this round (multiple of 32)
+  for (int k0 = 0; k0 < lkp; k0 += kbs) {
+    const int kn = min(kbs, lkp - k0);      // keys staged this round (multiple of 32)
     __syncthreads();                          // previous key block consumed
     // HBM -> LDS by global_load_lds (16 B per lane, lane-linear per wave instruction): LDS slot j of
     // the padded image is filled from whichever global chunk belongs there, so every load of the
@@ -550,11 +553,19 @@ mmr_status launch_mha(const char* who, const uint16_t* q, int64_t ldq, const uin
               "%s: operands must be 16-B aligned", who);
   if (b == 0) return MMR_OK;
   const int dt = (dh + 31) / 32;
-  const size_t kv_bytes = (size_t)MHA_KB * (dt * 32 + 8) * 2 + (size_t)MHA_KB * (dt * 32 + ((dt & 1) ? 0 : 16)) * 2;
+  const int nqt = (lq + 31) / 32, nchunk = (lq + 127) / 128, nwv = std::min(4, nqt);
+  // key block: all keys when lk <= 64; 64 for a 1-2-wave block (its LDS, and with it the workgroups
+  // per CU, is then set by the K/V image); else 128
+  int kbs = (lk <= 64 || nwv <= 2) ? 64 : MHA_KB;
+  if (const char* e = getenv("MMR_MHA_KB")) {  // A/B override (64 / 128)
+    const int v = atoi(e);
+    if (v == 64 || v == 128) kbs = v;
+  }
+  kbs = std::min(kbs, (lk + 31) & ~31);
+  const size_t kv_bytes = (size_t)kbs * (dt * 32 + 8) * 2 + (size_t)kbs * (dt * 32 + ((dt & 1) ? 0 : 16)) * 2;
   const size_t lds =
-      std::max(kv_bytes, (size_t)4 * dt * 32 * 33 * 4) + (size_t)4 * dt * 32 * 4 + (size_t)MHA_KB * 4;
-  const int nqt = (lq + 31) / 32, nchunk = (lq + 127) / 128;
-  const dim3 grid((unsigned)((int64_t)b * heads), (unsigned)nchunk), blk(64 * std::min(4, nqt));
+      std::max(kv_bytes, (size_t)nwv * dt * 32 * 33 * 4) + (size_t)nwv * dt * 32 * 4 + (size_t)kbs * 4;
+  const dim3 grid((unsigned)((int64_t)b * heads), (unsigned)nchunk), blk(64 * nwv);
   hipStream_t st = mmr::as_stream(stream);
   if (mean_out && nchunk > 1)  // query chunks accumulate their partial means
     MMR_CHECK_HIP(hipMemsetAsync(mean_out, 0, sizeof(float) * (size_t)b * heads * dh, st));
@@ -562,10 +573,10 @@ mmr_status launch_mha(const char* who, const uint16_t* q, int64_t ldq, const uin
   do {                                                                                                         \
     if (kmask)                                                                                                 \
       mha_small<D, true><<<grid, blk, lds, st>>>(q, ldq, k, ldk, v, ldv, out, ldo, mean_out, kmask, lq, lk,    \
-                                                 heads, dh, scale, q8, q8s);                                   \
+                                                 heads, dh, scale, kbs, q8, q8s);                                   \
     else                                                                                                       \
       mha_small<D, false><<<grid, blk, lds, st>>>(q, ldq, k, ldk, v, ldv, out, ldo, mean_out, nullptr, lq, lk, \
-                                                  heads, dh, scale, q8, q8s);                                  \
+                                                  heads, dh, scale, kbs, q8, q8s);                                  \
   } while (0)
   switch (dt) {
     case 1: MMR_MHA(1); break;

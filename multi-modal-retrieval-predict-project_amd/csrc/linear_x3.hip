@@ -9,8 +9,9 @@
 // Reference semantics: the fusion head's nn.Linear chain in fp32 (model.py:375-459, MultiHeadMLP
 // model.py:61-75, adapters :262-268); linear_f32 (tower.hip) stays the exact-f32 path.
 //
-// Geometry: one 32x32 output tile per 256-thread workgroup, the K range split over the 4 waves
-// (cin % 128 == 0), partial tiles summed in LDS in a fixed order (deterministic); every load of a
+// Geometry: one 32x32 output tile per workgroup of NW waves, the K range split over the waves
+// (cin % (32 NW) == 0; NW = 8 when the launch has too few tiles to fill the chip, which halves each
+// wave's serial K chain), partial tiles summed in LDS in a fixed order (deterministic); every load of a
 // 3-step chunk issued before its MFMAs; rows >= nb clamped (loaded, never stored).  blockIdx.y is the
 // problem index of the batched form (independent problems at fixed element strides).
 #include "common.h"
@@ -36,15 +37,15 @@ __device__ __forceinline__ void split8(const float4& p, const float4& q, bf16x8&
   lo = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
 }
 
-template <int ACT, bool BIAS, bool RES>
-__global__ __launch_bounds__(256) void linear_x3(const float* __restrict__ X, int64_t ldx,
+template <int ACT, bool BIAS, bool RES, int NW>
+__global__ __launch_bounds__(64 * NW) void linear_x3(const float* __restrict__ X, int64_t ldx,
                                                  const uint16_t* __restrict__ Wh,
                                                  const uint16_t* __restrict__ Wl,
                                                  const float* __restrict__ bias, const float* R,
                                                  int64_t ldr, float* Y, int64_t ldy, int nb, int cin,
                                                  int cout, int64_t bsx, int64_t bsw, int64_t bsb,
                                                  int64_t bsr, int64_t bsy) {
-  __shared__ float part[4][32][33];
+  __shared__ float part[NW][32][33];
   X += blockIdx.y * bsx;
   Wh += blockIdx.y * bsw;
   Wl += blockIdx.y * bsw;
@@ -65,7 +66,7 @@ __global__ __launch_bounds__(256) void linear_x3(const float* __restrict__ X, in
     wh[t] = Wh + (int64_t)(to * 32 + 16 * t + r) * cin + 8 * g;
     wl[t] = Wl + (int64_t)(to * 32 + 16 * t + r) * cin + 8 * g;
   }
-  const int kw = cin / 4, k0 = wave * kw, nsteps = kw / 32;
+  const int kw = cin / NW, k0 = wave * kw, nsteps = kw / 32;
   f32x4 acc[2][2];
 #pragma unroll
   for (int m = 0; m < 2; ++m)
@@ -111,10 +112,12 @@ __global__ __launch_bounds__(256) void linear_x3(const float* __restrict__ X, in
       for (int i = 0; i < 4; ++i) part[wave][16 * m + 4 * g + i][16 * n + r] = acc[m][n][i];
   __syncthreads();
 #pragma unroll
-  for (int e4 = 0; e4 < 4; ++e4) {
-    const int e = threadIdx.x + 256 * e4, row = e >> 5, col = e & 31;
+  for (int e4 = 0; e4 < 16 / NW; ++e4) {
+    const int e = threadIdx.x + 64 * NW * e4, row = e >> 5, col = e & 31;
     const int bb = tb * 32 + row, o = to * 32 + col;
-    float v = ((part[0][row][col] + part[1][row][col]) + part[2][row][col]) + part[3][row][col];
+    float v = part[0][row][col];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) v += part[w][row][col];
     if (bb >= nb) continue;
     if (BIAS) v += bias[o];
     if (ACT == 1) v = mmr::gelu_erf(v);
@@ -143,7 +146,18 @@ extern "C" mmr_status mmr_linear_x3(const float* x, int64_t ldx, int64_t bsx, co
   const dim3 grid((unsigned)(mmr::ceil_div(b, 32) * (cout / 32)), (unsigned)nbatch);
   hipStream_t st = mmr::as_stream(stream);
   const bool hb = bias != nullptr, hr = residual != nullptr;
-#define X3_L(A, B_, R_) linear_x3<A, B_, R_><<<grid, 256, 0, st>>>(x, ldx, w_hi, w_lo, bias, residual, ldr, y, ldy, b, cin, cout, bsx, bsw, bsb, bsr, bsy)
+  // 8 waves per tile when the launch has fewer than 2 tiles per CU (the joint chain at B = 256:
+  // 96-384 tiles) and the K range splits evenly into 8
+  int nw = (cin % 256 == 0 && (int64_t)grid.x * grid.y < 512) ? 8 : 4;
+  if (const char* e = getenv("MMR_X3_NW")) {  // A/B override (4 / 8)
+    const int v = atoi(e);
+    if (v == 4 || (v == 8 && cin % 256 == 0)) nw = v;
+  }
+#define X3_L(A, B_, R_)                                                                                          \
+  (nw == 8 ? linear_x3<A, B_, R_, 8><<<grid, 512, 0, st>>>(x, ldx, w_hi, w_lo, bias, residual, ldr, y, ldy, b, cin, \
+                                                         cout, bsx, bsw, bsb, bsr, bsy)                          \
+           : linear_x3<A, B_, R_, 4><<<grid, 256, 0, st>>>(x, ldx, w_hi, w_lo, bias, residual, ldr, y, ldy, b, cin, \
+                                                         cout, bsx, bsw, bsb, bsr, bsy))
   if (act == 1) {
     if (hb && hr) X3_L(1, true, true);
     else if (hb) X3_L(1, true, false);
