@@ -111,6 +111,12 @@ for s in $STEPS; do
         MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/${ABLIB:-libmmr_prev.so} timeout -k 10 120 python -u tools/mha_bench.py >> $OUT/attab.txt 2>&1
         MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/${ABLIB:-libmmr_prev.so} timeout -k 10 120 python -u tools/attn_ab.py >> $OUT/attab.txt 2>&1
       done; grep -v amdgpu.ids $OUT/attab.txt ;;
+    cfg5ab)  # cfg5 step: this tree vs tools/ab/${ABLIB:-libmmr_prev.so}, same box
+      for i in 1 2; do for L in new old; do
+        if [ $L = new ]; then E=X=0; else E=MMR_LIBMMR=tools/ab/${ABLIB:-libmmr_prev.so}; fi
+        env $E timeout -k 10 500 python -u bench.py --preset cfg5 --steps 5 --warmup 2 --no-cpu-baseline > $OUT/cfg5ab.json 2> $OUT/cfg5ab.err
+        python -c "import json;d=json.load(open('$OUT/cfg5ab.json'));print('$L', round(d['ms_per_step'],3), round(d['value']))"
+      done; done ;;
     rw)
       timeout -k 10 200 python -u tools/rw_bench.py > $OUT/rw.txt 2>&1; grep -v amdgpu.ids $OUT/rw.txt ;;
     breakdown)  # per-(op, shape) times of one sequential cfg2 step
