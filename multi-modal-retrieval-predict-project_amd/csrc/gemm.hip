@@ -627,8 +627,10 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   const int lo = (int)((int64_t)ntiles * xcd / 8), hi = (int)((int64_t)ntiles * (xcd + 1) / 8);
   int t = lo + slot;
   if (t >= hi) return;
-  auto mof = [&](int tile) -> int { return tile / tiles_n; };
-  auto nof = [&](int tile) -> int { return tile % tiles_n; };
+  // KNN: query tile fastest (tiles_m = 1 or 2), so the two query tiles of a gallery tile run at once
+  // on CUs of one XCD and the second reads the gallery panel from its L2
+  auto mof = [&](int tile) -> int { return KNN ? tile % tiles_m : tile / tiles_n; };
+  auto nof = [&](int tile) -> int { return KNN ? tile / tiles_m : tile % tiles_n; };
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably uniform: SGPR LDS bases
@@ -1727,22 +1729,22 @@ extern "C" mmr_status mmr_linear_mxfp8_q8(const uint8_t* xq, const uint8_t* xs, 
 }
 
 namespace mmr {
-// The fp16 kNN scan on the persistent 8-phase GEMM (gemm_bf16_tn_p8<KNN>): qh [256][K] fp16 unit
-// queries (zero rows past the pass), gh [tiles_n * 256][K] fp16 unit gallery rows (zero rows past
-// nval); writes unit maxima of unit_rows (2 or 4) consecutive rows gm [256][ldG] (ldG >= tiles_n *
-// 256 / unit_rows) and block maxima bm [256][ldB].
+// The fp16 kNN scan on the persistent 8-phase GEMM (gemm_bf16_tn_p8<KNN>): qh [256 tiles_m][K] fp16
+// unit queries (zero rows past the pass; tiles_m 1 or 2), gh [tiles_n * 256][K] fp16 unit gallery rows
+// (zero rows past nval); writes unit maxima of unit_rows (2 or 4) consecutive rows gm [256 tiles_m][ldG]
+// (ldG >= tiles_n * 256 / unit_rows) and block maxima bm [256 tiles_m][ldB].
 // K % 128 == 0 (the caller checks).
 hipError_t knn_scan_p8(const uint16_t* qh, const uint16_t* gh, int K, int tiles_n, int64_t nval, float* gm,
-                       int64_t ldG, float* bm, int64_t ldB, int unit_rows, hipStream_t st) {
-  const int grid = std::max(8, std::min(cu_count(), tiles_n) / 8 * 8);
+                       int64_t ldG, float* bm, int64_t ldB, int unit_rows, hipStream_t st, int tiles_m) {
+  const int grid = std::max(8, std::min(cu_count(), tiles_m * tiles_n) / 8 * 8);
   if (unit_rows == 2)
     gemm_bf16_tn_p8<4, 0, false, false, false, false, 2><<<dim3(grid), dim3(512), P8<4>::LDS_B, st>>>(
-        qh, gh, nullptr, nullptr, nullptr, 256, tiles_n * 256, K, 1, tiles_n, nullptr, nullptr, nullptr, gm, bm, ldG,
-        ldB, nval);
+        qh, gh, nullptr, nullptr, nullptr, 256 * tiles_m, tiles_n * 256, K, tiles_m, tiles_n, nullptr, nullptr, nullptr,
+        gm, bm, ldG, ldB, nval);
   else
     gemm_bf16_tn_p8<4, 0, false, false, false, false, 4><<<dim3(grid), dim3(512), P8<4>::LDS_B, st>>>(
-        qh, gh, nullptr, nullptr, nullptr, 256, tiles_n * 256, K, 1, tiles_n, nullptr, nullptr, nullptr, gm, bm, ldG,
-        ldB, nval);
+        qh, gh, nullptr, nullptr, nullptr, 256 * tiles_m, tiles_n * 256, K, tiles_m, tiles_n, nullptr, nullptr, nullptr,
+        gm, bm, ldG, ldB, nval);
   return hipGetLastError();
 }
 }  // namespace mmr

@@ -44,7 +44,8 @@
 
 namespace mmr {
 hipError_t knn_scan_p8(const uint16_t* qh, const uint16_t* gh, int K, int tiles_n, int64_t nval, float* gm,
-                       int64_t ldG, float* bm, int64_t ldB, int unit_rows, hipStream_t st);  // gemm.hip
+                       int64_t ldG, float* bm, int64_t ldB, int unit_rows, hipStream_t st,
+                       int tiles_m = 1);  // gemm.hip
 }
 
 namespace {
@@ -2128,10 +2129,12 @@ mmr_status ensure_ws(mmr_index* ix, int64_t nq) {
     vals = cq * (ix->Np / 4);
     qs = cq;
   } else {
-    rows = 256;
+    // passes of <= 256 queries; 512 with the p8 scan's 4-row units (same unit-maxima bytes as 256
+    // queries of 2-row units; the fp16 query rows of a 512 pass fit the 256 f32 rows of qn)
+    rows = 512;
     const int64_t nr = ix->Np256 > ix->Np ? ix->Np256 : ix->Np;  // the p8 scan writes whole 256-row tiles
     vals = 256 * (ix->Np256 > 0 ? nr / 2 : nr / 4);  // p8: 2-row unit maxima
-    bvals = 256 * (nr / 64);
+    bvals = 512 * (nr / 64);
   }
   int64_t hq = ix->ws_qrows, hq2 = ix->ws_qrows;
   mmr_status s = grow(ix, ix->qn, hq, rows, sizeof(float) * ix->Dp);
@@ -2182,6 +2185,15 @@ bool lq_scan_enabled() {
 }
 
 // The p8 GEMM scan for 129-256-query f16 passes (MMR_KNN_P8=0: the LDS-ring tile scan, for A/B).
+// A/B: 512-query passes of the 4-row-unit p8 scan (MMR_KNN_P8_PAIR=0: 256)
+bool p8_pair_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("MMR_KNN_P8_PAIR");
+    return !(e && atoi(e) == 0);
+  }();
+  return v;
+}
+
 bool p8_scan_enabled() {
   const char* e = getenv("MMR_KNN_P8");
   return !(e && atoi(e) == 0);
@@ -2450,9 +2462,14 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
     double* os64 = out_score64 ? out_score64 + c0 * k : nullptr;
     int32_t* ost = out_status ? out_status + c0 : nullptr;
     if (ix->mode == 2) {
-      // fp16 scan, passes of <= 256 queries (16 * QT, QT a power of two)
-      for (int64_t p0 = 0; p0 < cq; p0 += 256) {
-        const int64_t pq = cq - p0 < 256 ? cq - p0 : 256;
+      // fp16 scan, passes of <= 256 queries (16 * QT, QT a power of two), or <= 512 on the p8 scan with
+      // 4-row units: its two query tiles share every gallery tile read (cfg5: Q = 2048 over 1M rows
+      // reads the 2 GB fp16 gallery 4 times instead of 8)
+      const bool p8ok = ix->ghr != nullptr && p8_scan_enabled();
+      const bool u2 = ix->n <= (int64_t(1) << 18) || k >= 32;
+      const int64_t pass = (p8ok && !u2 && p8_pair_enabled()) ? 512 : 256;
+      for (int64_t p0 = 0; p0 < cq; p0 += pass) {
+        const int64_t pq = cq - p0 < pass ? cq - p0 : pass;
         int qt = 1;
         while (16 * qt < pq) qt *= 2;
         const int64_t Qp = 16 * qt;
@@ -2461,21 +2478,21 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
         float* gm = ix->vals;
         float* bm = ix->bvals;
         const int64_t ldG = ix->Np / 4, ldB = ix->Np / 64;
-        if (pq > 128 && ix->ghr != nullptr && p8_scan_enabled()) {
+        if (pq > 128 && p8ok) {
           // 129-256 queries: the persistent 8-phase GEMM (gemm.hip) with the unit-max epilogue —
           // one 256-query M tile x 256-row gallery tiles, row-major fp16 operands.  (It computes
           // all 256 query rows; at 100k x 768 it beats the LDS-ring tile scan from Q ~ 160:
           // Q = 64 / 128 / 192 / 256: 81 / 83 / 86 / 88 us vs 62 / 69 / 96 / 100.)
-          knn_prep_queries<<<dim3(64), dim3(256), 0, st>>>(qp, pq, ix->d, ix->qn, ix->Dp, 256, ix->qnorm64, 3);
+          const int tm = pq > 256 ? 2 : 1;  // query tiles of this pass
+          knn_prep_queries<<<dim3(64 * tm), dim3(256), 0, st>>>(qp, pq, ix->d, ix->qn, ix->Dp, 256 * tm, ix->qnorm64, 3);
           MMR_LAUNCH_CHECK();
           // unit size: 2 rows halves the rows the select re-scores per candidate unit, 4 rows halves
           // the unit maxima the scan writes (512 vs 256 MB per pass at 1M rows): 2 for small
           // galleries or large K (cfg2 100k / K 10: select 22 -> 16 us; cfg3 1M / K 50: 104 -> 65 us for
           // +30 us of scan), 4 for large galleries at small K (cfg5 1M / K 10: +37 us scan, -9 select)
-          const bool u2 = ix->n <= (int64_t(1) << 18) || k >= 32;
           const int64_t ldG8 = ix->Np256 / (u2 ? 2 : 4), ldB8 = ix->Np256 / 64;
           MMR_CHECK_HIP(mmr::knn_scan_p8(qh, ix->ghr, ix->Dp, (int)(ix->Np256 / 256), ix->n, gm, ldG8, bm, ldB8,
-                                         u2 ? 2 : 4, st));
+                                         u2 ? 2 : 4, st, tm));
           if (u2)
             launch_select<3, true>(st, pq, gm, ldG8, ldG8, ix, k, two_delta16, qp, ix->qnorm64, oi + p0 * k,
                                    os ? os + p0 * k : nullptr, os64 ? os64 + p0 * k : nullptr, ost ? ost + p0 : nullptr,

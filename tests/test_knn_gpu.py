@@ -398,14 +398,16 @@ def test_knn_f16_p8_small_galleries(N, Q):
     _exact_check(G, Qm, 10, mode="f16")
 
 
-def test_knn_f16_p8_four_row_units():
+@pytest.mark.parametrize("Q", [200, 300, 700])
+def test_knn_f16_p8_four_row_units(Q):
     """Galleries above 2^18 rows at K < 32: the 8-phase GEMM scan writes 4-row unit maxima
-    (knn_select_t<2>) instead of 2-row ones; exact vs the oracle, with a duplicate run and the
-    padded last tile."""
+    (knn_select_t<2>) instead of 2-row ones, in passes of up to 512 queries (two query tiles per
+    gallery tile: Q = 300 one padded pair, 700 a full pair + a 188-query pass); exact vs the oracle,
+    with a duplicate run and the padded last tile."""
     rng = np.random.default_rng(4444)
     G = rng.standard_normal((300_001, 128), dtype=np.float32)
     G[200_000:200_006] = G[11]
-    Qm = rng.standard_normal((200, 128), dtype=np.float32)
+    Qm = rng.standard_normal((Q, 128), dtype=np.float32)
     Qm[0] = G[11]
     gi, _ = _exact_check(G, Qm, 10, mode="f16")
     assert gi[0, :7].tolist() == [11] + list(range(200_000, 200_006))
