@@ -2129,11 +2129,11 @@ mmr_status ensure_ws(mmr_index* ix, int64_t nq) {
     vals = cq * (ix->Np / 4);
     qs = cq;
   } else {
-    // passes of <= 256 queries; 512 with the p8 scan's 4-row units (same unit-maxima bytes as 256
-    // queries of 2-row units; the fp16 query rows of a 512 pass fit the 256 f32 rows of qn)
+    // passes of <= 256 queries, or 512 on the p8 scan (the fp16 query rows of a 512 pass fit the 256
+    // f32 rows of qn)
     rows = 512;
     const int64_t nr = ix->Np256 > ix->Np ? ix->Np256 : ix->Np;  // the p8 scan writes whole 256-row tiles
-    vals = 256 * (ix->Np256 > 0 ? nr / 2 : nr / 4);  // p8: 2-row unit maxima
+    vals = ix->Np256 > 0 ? 512 * (nr / 2) : 256 * (nr / 4);  // p8: up to 512 queries of 2-row unit maxima
     bvals = 512 * (nr / 64);
   }
   int64_t hq = ix->ws_qrows, hq2 = ix->ws_qrows;
@@ -2185,7 +2185,7 @@ bool lq_scan_enabled() {
 }
 
 // The p8 GEMM scan for 129-256-query f16 passes (MMR_KNN_P8=0: the LDS-ring tile scan, for A/B).
-// A/B: 512-query passes of the 4-row-unit p8 scan (MMR_KNN_P8_PAIR=0: 256)
+// A/B: 512-query passes of the p8 scan (MMR_KNN_P8_PAIR=0: 256)
 bool p8_pair_enabled() {
   static const bool v = [] {
     const char* e = getenv("MMR_KNN_P8_PAIR");
@@ -2462,12 +2462,12 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
     double* os64 = out_score64 ? out_score64 + c0 * k : nullptr;
     int32_t* ost = out_status ? out_status + c0 : nullptr;
     if (ix->mode == 2) {
-      // fp16 scan, passes of <= 256 queries (16 * QT, QT a power of two), or <= 512 on the p8 scan with
-      // 4-row units: its two query tiles share every gallery tile read (cfg5: Q = 2048 over 1M rows
-      // reads the 2 GB fp16 gallery 4 times instead of 8)
+      // fp16 scan, passes of <= 256 queries (16 * QT, QT a power of two), or <= 512 on the p8 scan:
+      // its two query tiles share every gallery tile read (cfg5: Q = 2048 over 1M rows reads the 2 GB
+      // fp16 gallery 4 times instead of 8)
       const bool p8ok = ix->ghr != nullptr && p8_scan_enabled();
       const bool u2 = ix->n <= (int64_t(1) << 18) || k >= 32;
-      const int64_t pass = (p8ok && !u2 && p8_pair_enabled()) ? 512 : 256;
+      const int64_t pass = (p8ok && p8_pair_enabled()) ? 512 : 256;
       for (int64_t p0 = 0; p0 < cq; p0 += pass) {
         const int64_t pq = cq - p0 < pass ? cq - p0 : pass;
         int qt = 1;

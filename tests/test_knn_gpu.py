@@ -388,10 +388,11 @@ def test_knn_f16_scattered_cluster_block_tightening(Q, K):
 
 
 @pytest.mark.parametrize("N", [1, 100, 255, 256, 257, 513])
-@pytest.mark.parametrize("Q", [129, 256])
+@pytest.mark.parametrize("Q", [129, 256, 600])
 def test_knn_f16_p8_small_galleries(N, Q):
-    """129-256-query f16 passes on the 8-phase GEMM scan with fewer gallery tiles than workgroups
-    (one 256-row tile, or a few: most XCD slots idle) and padded rows inside the last tile."""
+    """129-512-query f16 passes on the 8-phase GEMM scan with fewer gallery tiles than workgroups
+    (one 256-row tile, or a few: most XCD slots idle) and padded rows inside the last tile; Q = 600:
+    a 512-query pass (two query tiles per gallery tile) + an 88-query tile-scan pass."""
     rng = np.random.default_rng(N * 7 + Q)
     G = rng.standard_normal((N, 128), dtype=np.float32)
     Qm = rng.standard_normal((Q, 128), dtype=np.float32)
