@@ -2129,12 +2129,12 @@ mmr_status ensure_ws(mmr_index* ix, int64_t nq) {
     vals = cq * (ix->Np / 4);
     qs = cq;
   } else {
-    // passes of <= 256 queries, or 512 on the p8 scan (the fp16 query rows of a 512 pass fit the 256
-    // f32 rows of qn)
-    rows = 512;
+    // passes of <= 256 queries, or on the p8 scan 512 (2-row units) / 1024 (4-row units): the same
+    // unit-maxima bytes; fp16 query rows of a pass take half the f32 rows of qn
+    rows = 1024;
     const int64_t nr = ix->Np256 > ix->Np ? ix->Np256 : ix->Np;  // the p8 scan writes whole 256-row tiles
     vals = ix->Np256 > 0 ? 512 * (nr / 2) : 256 * (nr / 4);  // p8: up to 512 queries of 2-row unit maxima
-    bvals = 512 * (nr / 64);
+    bvals = 1024 * (nr / 64);
   }
   int64_t hq = ix->ws_qrows, hq2 = ix->ws_qrows;
   mmr_status s = grow(ix, ix->qn, hq, rows, sizeof(float) * ix->Dp);
@@ -2185,7 +2185,16 @@ bool lq_scan_enabled() {
 }
 
 // The p8 GEMM scan for 129-256-query f16 passes (MMR_KNN_P8=0: the LDS-ring tile scan, for A/B).
-// A/B: 512-query passes of the p8 scan (MMR_KNN_P8_PAIR=0: 256)
+// query tiles per p8 pass with 4-row units (MMR_KNN_P8_TILES 2 / 4, default 4)
+int p8_pair_tiles() {
+  static const int v = [] {
+    const char* e = getenv("MMR_KNN_P8_TILES");
+    return (e && atoi(e) == 2) ? 2 : 4;
+  }();
+  return v;
+}
+
+// A/B: multi-query-tile passes of the p8 scan (MMR_KNN_P8_PAIR=0: 256)
 bool p8_pair_enabled() {
   static const bool v = [] {
     const char* e = getenv("MMR_KNN_P8_PAIR");
@@ -2462,12 +2471,12 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
     double* os64 = out_score64 ? out_score64 + c0 * k : nullptr;
     int32_t* ost = out_status ? out_status + c0 : nullptr;
     if (ix->mode == 2) {
-      // fp16 scan, passes of <= 256 queries (16 * QT, QT a power of two), or <= 512 on the p8 scan:
-      // its two query tiles share every gallery tile read (cfg5: Q = 2048 over 1M rows reads the 2 GB
-      // fp16 gallery 4 times instead of 8)
+      // fp16 scan, passes of <= 256 queries (16 * QT, QT a power of two), or on the p8 scan <= 512
+      // (2-row units) / 1024 (4-row units): its query tiles share every gallery tile read (cfg5: Q =
+      // 2048 over 1M rows reads the 2 GB fp16 gallery twice instead of 8 times)
       const bool p8ok = ix->ghr != nullptr && p8_scan_enabled();
       const bool u2 = ix->n <= (int64_t(1) << 18) || k >= 32;
-      const int64_t pass = (p8ok && p8_pair_enabled()) ? 512 : 256;
+      const int64_t pass = (p8ok && p8_pair_enabled()) ? 256 * (u2 ? 2 : p8_pair_tiles()) : 256;
       for (int64_t p0 = 0; p0 < cq; p0 += pass) {
         const int64_t pq = cq - p0 < pass ? cq - p0 : pass;
         int qt = 1;
@@ -2483,7 +2492,7 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
           // one 256-query M tile x 256-row gallery tiles, row-major fp16 operands.  (It computes
           // all 256 query rows; at 100k x 768 it beats the LDS-ring tile scan from Q ~ 160:
           // Q = 64 / 128 / 192 / 256: 81 / 83 / 86 / 88 us vs 62 / 69 / 96 / 100.)
-          const int tm = pq > 256 ? 2 : 1;  // query tiles of this pass
+          const int tm = (int)((pq + 255) / 256);  // query tiles of this pass
           knn_prep_queries<<<dim3(64 * tm), dim3(256), 0, st>>>(qp, pq, ix->d, ix->qn, ix->Dp, 256 * tm, ix->qnorm64, 3);
           MMR_LAUNCH_CHECK();
           // unit size: 2 rows halves the rows the select re-scores per candidate unit, 4 rows halves

@@ -402,8 +402,8 @@ def test_knn_f16_p8_small_galleries(N, Q):
 @pytest.mark.parametrize("Q", [200, 300, 700])
 def test_knn_f16_p8_four_row_units(Q):
     """Galleries above 2^18 rows at K < 32: the 8-phase GEMM scan writes 4-row unit maxima
-    (knn_select_t<2>) instead of 2-row ones, in passes of up to 512 queries (two query tiles per
-    gallery tile: Q = 300 one padded pair, 700 a full pair + a 188-query pass); exact vs the oracle,
+    (knn_select_t<2>) instead of 2-row ones, in passes of up to 1024 queries (query tiles sharing
+    each gallery tile: Q = 300 two tiles, the second padded; 700 three tiles); exact vs the oracle,
     with a duplicate run and the padded last tile."""
     rng = np.random.default_rng(4444)
     G = rng.standard_normal((300_001, 128), dtype=np.float32)
