@@ -391,6 +391,12 @@ mmr_status mmr_ln_rows(const void* x, int64_t ldx, const float* alpha, const voi
 mmr_status mmr_assemble_seq(const float* x1, const uint16_t* patches_fused, const float* x2, const float* pe,
                             uint16_t* seq, int32_t b, int32_t np, int32_t c, void* stream);
 
+/* mmr_assemble_seq written only as the combiner QKV GEMM's MX-fp8 activation operand (layout 0, as
+ * mmr_quantize_mxfp8 of the bf16 sequence, bit-identical); b*(np+2) and c multiples of 256.
+ * Replaces: the same cat + pos_encoder (reference src/Model/model.py:396-397) on the fp8 path. */
+mmr_status mmr_assemble_seq_q8(const float* x1, const uint16_t* patches_fused, const float* x2, const float* pe,
+                               uint8_t* q8, uint8_t* q8_scales, int32_t b, int32_t np, int32_t c, void* stream);
+
 /* y (b, c) f32 = x[i*ldx + 0..c) (bf16 rows, e.g. the CLS token of each sequence). */
 mmr_status mmr_rows_to_f32(const uint16_t* x, int64_t ldx, float* y, int32_t b, int32_t c, void* stream);
 

@@ -79,6 +79,7 @@ SIGNATURES = {
     "mmr_linear_f32_batched": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,
                                c_i32, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_assemble_seq": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
+    "mmr_assemble_seq_q8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
     "mmr_rows_to_f32": [c_vp, c_i64, c_vp, c_i32, c_i32, c_vp],
 }
 _RESTYPES = {"mmr_last_error": ctypes.c_char_p, "mmr_version": ctypes.c_int, "mmr_max_k": ctypes.c_int,

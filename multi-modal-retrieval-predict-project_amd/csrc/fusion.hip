@@ -491,9 +491,15 @@ __global__ __launch_bounds__(256) void assemble_seq(const float* __restrict__ x1
 
 // Same, 8 channels per thread (c % 8 == 0, fewer than 2^31 chunks): 16-B bf16 loads / stores, 32-bit
 // index math (the element-wise form spends its time in 64-bit divisions: 150 us at 1280 x 51 x 768).
+// Q8: the sequence written only as the combiner QKV GEMM's MX-fp8 operand (mmr::q8_chunk8 of the
+// bf16-rounded values: bit-identical to quantising the bf16 sequence; rows and c multiples of 256, so
+// a 4-lane group never straddles a row or the grid's ragged end).
+template <bool Q8 = false>
 __global__ __launch_bounds__(256) void assemble_seq8(const float* __restrict__ x1, const uint16_t* __restrict__ pf,
                                                      const float* __restrict__ x2, const float* __restrict__ pe,
-                                                     uint16_t* __restrict__ seq, int nb, int np, int c) {
+                                                     uint16_t* __restrict__ seq, int nb, int np, int c,
+                                                     uint8_t* __restrict__ q8 = nullptr,
+                                                     uint8_t* __restrict__ q8s = nullptr) {
   const uint32_t ls = (uint32_t)np + 2u, c8 = (uint32_t)c >> 3;
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   if (i >= (uint32_t)nb * ls * c8) return;
@@ -521,7 +527,18 @@ __global__ __launch_bounds__(256) void assemble_seq8(const float* __restrict__ x
   o.y = mmr::pack2bf(v[2] + pv[2], v[3] + pv[3]);
   o.z = mmr::pack2bf(v[4] + pv[4], v[5] + pv[5]);
   o.w = mmr::pack2bf(v[6] + pv[6], v[7] + pv[7]);
-  *(uint4*)(seq + (size_t)row * c + ch) = o;
+  if constexpr (Q8) {
+    const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+    float vb[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      vb[2 * e] = __uint_as_float(w[e] << 16);
+      vb[2 * e + 1] = __uint_as_float(w[e] & 0xFFFF0000u);
+    }
+    mmr::q8_chunk8(vb, (int64_t)row, (int)(ch >> 3), c, q8, q8s, true);
+  } else {
+    *(uint4*)(seq + (size_t)row * c + ch) = o;
+  }
 }
 
 // ------------------------------------------------------------------ strided bf16 -> f32 row gather
@@ -699,11 +716,28 @@ mmr_status mmr_assemble_seq(const float* x1, const uint16_t* patches_fused, cons
   const bool vec = c % 8 == 0 && n / 8 < (int64_t(1) << 31) && aligned16(x1) && aligned16(x2) && aligned16(pe) &&
                    aligned16(patches_fused) && aligned16(seq);
   if (vec)
-    assemble_seq8<<<dim3((unsigned)mmr::ceil_div(n / 8, 256)), 256, 0, mmr::as_stream(stream)>>>(
+    assemble_seq8<false><<<dim3((unsigned)mmr::ceil_div(n / 8, 256)), 256, 0, mmr::as_stream(stream)>>>(
         x1, patches_fused, x2, pe, seq, b, np, c);
   else
     assemble_seq<<<dim3((unsigned)mmr::ceil_div(n, 256)), 256, 0, mmr::as_stream(stream)>>>(x1, patches_fused, x2, pe,
                                                                                             seq, b, np, c);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_assemble_seq_q8(const float* x1, const uint16_t* patches_fused, const float* x2, const float* pe,
+                               uint8_t* q8, uint8_t* q8_scales, int32_t b, int32_t np, int32_t c, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x1 && patches_fused && x2 && pe && q8 && q8_scales && b >= 0 && np > 0 && c > 0,
+              "mmr_assemble_seq_q8: bad arguments");
+  const int64_t rows = (int64_t)b * (np + 2), n = rows * c;
+  MMR_REQUIRE(rows % 256 == 0 && c % 256 == 0 && n / 8 < (int64_t(1) << 31),
+              "mmr_assemble_seq_q8: needs b*(np+2) %% 256 == 0 and c %% 256 == 0 (rows=%lld c=%d)", (long long)rows, c);
+  MMR_REQUIRE(aligned16(x1) && aligned16(x2) && aligned16(pe) && aligned16(patches_fused),
+              "mmr_assemble_seq_q8: operands must be 16-B aligned");
+  if (b == 0) return MMR_OK;
+  assemble_seq8<true><<<dim3((unsigned)mmr::ceil_div(n / 8, 256)), 256, 0, mmr::as_stream(stream)>>>(
+      x1, patches_fused, x2, pe, nullptr, b, np, c, q8, q8_scales);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }

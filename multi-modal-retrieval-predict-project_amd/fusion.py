@@ -160,6 +160,9 @@ class FusionStack:
             L["ad"] = tuple(_f(sd[f"adapters.{i}.{k}"], dev) for k in ("0.weight", "0.bias", "2.weight", "2.bias"))
             self.layers.append(L)
         self.s_w, self.s_b = _bf(sd["self_attn.in_proj_weight"], dev), _f(sd["self_attn.in_proj_bias"], dev)
+        # combiner QKV on MX-fp8 (its operand written by the sequence assembly itself)
+        self.s_w8 = (_w8(self.s_w) if fp8 and D % 256 == 0 and os.environ.get("MMR_COMB_FP8", "1") != "0"
+                     else None)  # MMR_COMB_FP8=0: bf16 combiner QKV (A/B)
         self.s_ow, self.s_ob = _f(sd["self_attn.out_proj.weight"], dev), _f(sd["self_attn.out_proj.bias"], dev)
         self.pe = _f(sd["pos_encoder.pe"][0], dev)
         self.alpha = _f(sd["alpha"].reshape(1), dev)
@@ -291,8 +294,12 @@ class FusionStack:
         x2 = ops.linear_x3_batched(cls, self.tp_x3, self.tp_b_all, nl, B, residual=i2t)
         x2 = ops.ln_rows(x2.view(nl * B, D), *self.ln_txt_all, eps, groups=nl, group_div=B)
         # phase 3: the shared combiner self-attention over every layer's fused sequence
-        S = ops.assemble_seq(x1, PF.view(nl * B * Np, D), x2, self.pe, Np).view(nl * B * (Np + 2), D)
-        SQ = ops.linear(S, self.s_w, self.s_b)
+        if self.s_w8 is not None and (nl * B * (Np + 2)) % 256 == 0:
+            S8 = ops.assemble_seq(x1, PF.view(nl * B * Np, D), x2, self.pe, Np, q8=True)
+            SQ = ops.linear_mxfp8(S8, self.s_w8, self.s_b)
+        else:
+            S = ops.assemble_seq(x1, PF.view(nl * B * Np, D), x2, self.pe, Np).view(nl * B * (Np + 2), D)
+            SQ = ops.linear(S, self.s_w, self.s_b)
         m3 = torch.empty((nl * B, D), dtype=torch.float32, device=dev)
         ops.mha(SQ[:, :D], SQ[:, D:2 * D], SQ[:, 2 * D:], nl * B, Np + 2, Np + 2, h, dh, sc, mean_out=m3)
         fused = ops.linear_x3(m3, self.s_ow_x3, self.s_ob).view(nl, B, D)  # mean of self_attn output

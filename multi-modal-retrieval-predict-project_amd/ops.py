@@ -406,8 +406,14 @@ def linear_f32_batched(x, w, bias, nbatch, b, residual=None, act=0, out=None, ld
     return y
 
 
-def assemble_seq(x1, pf, x2, pe, np_):
+def assemble_seq(x1, pf, x2, pe, np_, q8=False):
+    """bf16 (B, np_+2, c) = [x1; pf; x2] + pe; q8: only its MX-fp8 operand (MXFP8 of B*(np_+2) rows)."""
     B, c = x1.shape
+    if q8:
+        q, s = _q8_out(B * (np_ + 2), c, x1.device)
+        _chk(_L().mmr_assemble_seq_q8(_lib.ptr(x1), _lib.ptr(pf), _lib.ptr(x2), _lib.ptr(pe), _lib.ptr(q), _lib.ptr(s),
+                                      B, np_, c, _s(x1)), "mmr_assemble_seq_q8")
+        return MXFP8(q, s, c, 0)
     seq = torch.empty((B, np_ + 2, c), dtype=torch.bfloat16, device=x1.device)
     _chk(_L().mmr_assemble_seq(_lib.ptr(x1), _lib.ptr(pf), _lib.ptr(x2), _lib.ptr(pe), _lib.ptr(seq), B, np_, c,
                                _s(x1)), "mmr_assemble_seq")

@@ -198,3 +198,19 @@ def test_mha_q8_equals_quantised_output(B, lq, lk, heads, dh):
     torch.cuda.synchronize()
     assert torch.equal(a8.q, ref8.q) and torch.equal(a8.s, ref8.s)
     assert torch.equal(m8, m_ref)
+
+
+@pytest.mark.parametrize("B,np_,c", [(256, 49, 256), (1280, 49, 1024)])
+def test_assemble_seq_q8_equals_quantised_sequence(B, np_, c):
+    """The combiner's fp8 QKV operand (config 5) written by the sequence assembly itself equals
+    mmr_quantize_mxfp8 of the bf16 sequence bit for bit (values and scale bytes); B*(np_+2) % 256 == 0."""
+    g = torch.Generator().manual_seed(B + c)
+    x1 = (torch.randn(B, c, generator=g) * 3).to(DEV)
+    x2 = (torch.randn(B, c, generator=g) * 0.5).to(DEV)
+    pf = (torch.randn(B * np_, c, generator=g) * 2).to(torch.bfloat16).to(DEV)
+    pe = (torch.randn(np_ + 2, c, generator=g) * 0.1).to(DEV)
+    seq = ops.assemble_seq(x1, pf, x2, pe, np_).view(B * (np_ + 2), c)
+    s8 = ops.assemble_seq(x1, pf, x2, pe, np_, q8=True)
+    ref8 = ops.quantize_mxfp8(seq, layout=0)
+    torch.cuda.synchronize()
+    assert torch.equal(s8.q, ref8.q) and torch.equal(s8.s, ref8.s)
