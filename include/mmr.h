@@ -213,6 +213,14 @@ mmr_status mmr_layernorm_bf16_q8(const uint16_t* x, const uint16_t* residual, co
                                  const float* beta, uint16_t* y, uint8_t* q8, uint8_t* q8_scales, int64_t rows,
                                  int32_t c, float eps, void* stream);
 
+/* mmr_layernorm_bf16_q8 with the operand's K padded to kp (kp % 256 == 0, kp >= c, c % 32 == 0; q8 is
+ * [rows][kp], the padding written as zero bytes with zero scale bytes, bit-identical to
+ * mmr_quantize_mxfp8(y, k=c, kp)), and y may be NULL when only the operand is consumed (the fp8 Swin
+ * stages: C = 384 -> kp 512 for stage 3, C = 768 for stage 4). */
+mmr_status mmr_layernorm_bf16_q8p(const uint16_t* x, const uint16_t* residual, const float* gamma,
+                                  const float* beta, uint16_t* y, uint8_t* q8, uint8_t* q8_scales, int64_t rows,
+                                  int32_t c, int32_t kp, float eps, void* stream);
+
 /* Row LayerNorm over c channels (bf16 in/out, f32 math, gamma/beta f32). */
 mmr_status mmr_layernorm_bf16(const uint16_t* x, const float* gamma, const float* beta,
                               uint16_t* y, int64_t rows, int32_t c, float eps, void* stream);
@@ -264,6 +272,13 @@ mmr_status mmr_bert_attention_q8(const uint16_t* qkv, const int64_t* mask01, uin
 mmr_status mmr_swin_window_attention(const uint16_t* qkv, const float* bias, uint16_t* out,
                                      int32_t b, int32_t hw, int32_t c, int32_t heads, int32_t ws,
                                      int32_t shift, void* stream);
+/* mmr_swin_window_attention writing its output as the proj GEMM's MX-fp8 activation operand (q8
+ * [b*hw*hw][kp] e4m3 + layout-0 scales, K padded to kp with zero bytes / zero scale bytes) instead of
+ * bf16 rows, bit-identical to mmr_quantize_mxfp8 of the bf16 output (the fp8 Swin stages 3-4; rows %
+ * 256 == 0, kp % 256 == 0, kp >= c). */
+mmr_status mmr_swin_window_attention_q8(const uint16_t* qkv, const float* bias, uint8_t* q8, uint8_t* q8_scales,
+                                        int32_t b, int32_t hw, int32_t c, int32_t kp, int32_t heads, int32_t ws,
+                                        int32_t shift, void* stream);
 /* Dense additive attention bias for one Swin block, built once at load: f32
  * [t][heads][64][64], t = 4 window types when shift > 0 (2*last-row + last-col), else 1:
  * relative_position_bias_table[(yi-yj+ws-1)*(2ws-1) + (xi-xj+ws-1)][head] (timm index), + -100

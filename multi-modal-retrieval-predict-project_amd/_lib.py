@@ -49,12 +49,14 @@ SIGNATURES = {
     "mmr_layernorm_bf16": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp],
     "mmr_add_layernorm_bf16": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp],
     "mmr_layernorm_bf16_q8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp],
+    "mmr_layernorm_bf16_q8p": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_f32, c_vp],
     "mmr_scaled_add_layernorm_bf16": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp],
     "mmr_scaled_add_layernorm_bf16_q8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp],
     "mmr_bert_embed": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp],
     "mmr_bert_attention": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_bert_attention_q8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_swin_window_attention": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp],
+    "mmr_swin_window_attention_q8": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_swin_attn_bias": [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_swin_attn_block_pack_bytes": [c_i32],
     "mmr_swin_attn_block_pack": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp],

@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256) void layernorm_bf16(const uint16_t* __restrict
                                                       int c, float eps,
                                                       const float* __restrict__ alpha = nullptr,
                                                       uint8_t* __restrict__ q8 = nullptr,
-                                                      uint8_t* __restrict__ q8s = nullptr) {
+                                                      uint8_t* __restrict__ q8s = nullptr, int kp = 0) {
   static_assert(!Q8 || LPR % 4 == 0, "Q8: a 32-block must be 4 lanes of one row");
   constexpr int RPW = 64 / LPR;
   const int lane = threadIdx.x & 63;
@@ -131,13 +131,22 @@ __global__ __launch_bounds__(256) void layernorm_bf16(const uint16_t* __restrict
     const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[i][j] = (v[i][j] - mean) * rstd * gg[j] + bb[j];
-    if (ok && ch < nch) store8(y + row * c + ch * 8, v[i]);
+    if (y && ok && ch < nch) store8(y + row * c + ch * 8, v[i]);
     if constexpr (Q8) {
       float vb[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) vb[j] = bf2f(f2bf(v[i][j]));  // the stored bf16 value
-      mmr::q8_chunk8(vb, row, ch, c, q8, q8s, ok && ch < nch);
+      mmr::q8_chunk8(vb, row, ch, kp, q8, q8s, ok && ch < nch);
     }
+  }
+  if constexpr (Q8) {
+    // K padded to kp (c = 384 -> 512: the stage-3 Swin linears): zero bytes and zero scale bytes for
+    // the padding blocks, as mmr_quantize_mxfp8 writes them (amax 0 -> E8M0 byte 0)
+    if (ok)
+      for (int pc = nch + sub; pc < kp / 8; pc += LPR) {
+        *(uint2*)(q8 + row * kp + pc * 8) = make_uint2(0u, 0u);
+        if ((pc & 3) == 0) q8s[mmr::q8_soff(row, pc * 8, kp)] = 0;
+      }
   }
 }
 
@@ -245,11 +254,18 @@ __global__ __launch_bounds__(256) void swin_attn_bias(const float* __restrict__ 
   bias[idx] = v;
 }
 
+// Q8: the output is written as the proj GEMM's MX-fp8 activation operand instead of bf16 rows (a
+// head's 32 dims are one 32-block: the lane pair (r, r + 32) holds them, one lane swap for the
+// amax), bit-identical to mmr_quantize_mxfp8(out, kp); the K padding C..kp is written by the last
+// head's waves (zero bytes, zero scale bytes).
+template <bool Q8 = false>
 __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __restrict__ qkv,
                                                              const float* __restrict__ bias,
                                                              uint16_t* __restrict__ out,
                                                              int64_t units, int H, int C,
-                                                             int heads, int ws, int shift, int hpw) {
+                                                             int heads, int ws, int shift, int hpw,
+                                                             uint8_t* __restrict__ q8 = nullptr,
+                                                             uint8_t* __restrict__ q8s = nullptr, int kp = 0) {
   // round 3: every global load of a wave (Q / K fragments, V rows, the bias rows of both query
   // tiles) is issued up front from clamped token indices (padded lanes read a real token and are
   // masked by the bias / the store guard): the previous form's "token valid ? load : 0" gathers
@@ -380,7 +396,29 @@ __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __r
           o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o, 0, 0, 0);
         }
       const int tqi = __shfl(tl, qi, 64);
-      if (qi < N) {
+      if constexpr (Q8) {
+        const float inv = 1.0f / psum;
+        float vb[16];
+        float amax = 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          vb[e] = bf2f(f2bf(o[e] * inv));  // the bf16 value the plain kernel stores
+          amax = fmaxf(amax, fabsf(vb[e]));
+        }
+        amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+        const int ex = mmr::q8_exp(amax);
+        const float qinv = mmr::q8_inv(ex);
+        if (qi < N) {
+          uint8_t* qrow = q8 + (int64_t)tqi * kp;
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4) *(uint32_t*)(qrow + hh * SW_DH + 8 * g4 + 4 * hf) = mmr::q8_pack4(vb + 4 * g4, qinv);
+          if (hf == 0) q8s[mmr::q8_soff(tqi, hh * SW_DH, kp)] = (uint8_t)(ex + 127);
+          if (hh == heads - 1) {
+            for (int off = C + 16 * hf; off < kp; off += 32) *(uint4*)(qrow + off) = make_uint4(0u, 0u, 0u, 0u);
+            for (int bk = C / 32 + hf; bk < kp / 32; bk += 2) q8s[mmr::q8_soff(tqi, bk * 32, kp)] = 0;
+          }
+        }
+      } else if (qi < N) {
         const float inv = 1.0f / psum;
         uint16_t* orow = out + (int64_t)tqi * C + hh * SW_DH;
 #pragma unroll
@@ -816,10 +854,12 @@ static mmr_status layernorm_launch(const uint16_t* x, const uint16_t* r, const f
                                    const float* beta, uint16_t* y, int64_t rows, int32_t c,
                                    float eps, void* stream, const char* who,
                                    const float* alpha = nullptr, uint8_t* q8 = nullptr,
-                                   uint8_t* q8s = nullptr) {
-  MMR_REQUIRE(x && gamma && beta && y, "%s: NULL pointer", who);
-  MMR_REQUIRE(!q8 || (q8s && rows % 256 == 0 && c % 256 == 0),
-              "%s: the MX-fp8 output needs rows %% 256 == 0 and c %% 256 == 0 (rows=%lld c=%d)", who, (long long)rows, c);
+                                   uint8_t* q8s = nullptr, int32_t kp = 0) {
+  if (!kp) kp = c;
+  MMR_REQUIRE(x && gamma && beta && (y || q8), "%s: NULL pointer", who);
+  MMR_REQUIRE(!q8 || (q8s && rows % 256 == 0 && c % 32 == 0 && kp % 256 == 0 && kp >= c),
+              "%s: the MX-fp8 output needs rows %% 256 == 0, c %% 32 == 0 and its padded K kp a multiple of 256 "
+              ">= c (rows=%lld c=%d kp=%d)", who, (long long)rows, c, kp);
   MMR_REQUIRE(c > 0 && c % 8 == 0 && rows >= 0, "%s: c=%d must be a positive multiple of 8", who, c);
   MMR_REQUIRE(c <= 4096, "%s: c=%d > 4096", who, c);
   if (rows == 0) return MMR_OK;
@@ -846,9 +886,9 @@ static mmr_status layernorm_launch(const uint16_t* x, const uint16_t* r, const f
   const dim3 grid((unsigned)mmr::ceil_div(rows, rows_per_block));
 #define MMR_LN2(L, N)                                                                                          \
   (q8 ? (r ? layernorm_bf16<L, N, true, true><<<grid, 256, 0, st>>>(x, r, gamma, beta, y, rows, c, eps, alpha, q8,  \
-                                                                    q8s)                                          \
+                                                                    q8s, kp)                                        \
            : layernorm_bf16<L, N, false, true><<<grid, 256, 0, st>>>(x, r, gamma, beta, y, rows, c, eps, alpha, q8, \
-                                                                     q8s))                                        \
+                                                                     q8s, kp))                                        \
       : (r ? layernorm_bf16<L, N, true><<<grid, 256, 0, st>>>(x, r, gamma, beta, y, rows, c, eps, alpha)          \
            : layernorm_bf16<L, N, false><<<grid, 256, 0, st>>>(x, r, gamma, beta, y, rows, c, eps, alpha)))
 #define MMR_LN(L) (cpl <= 3 ? MMR_LN2(L, 3) : (cpl <= 6 ? MMR_LN2(L, 6) : MMR_LN2(L, 8)))
@@ -883,6 +923,15 @@ mmr_status mmr_layernorm_bf16_q8(const uint16_t* x, const uint16_t* residual, co
   MMR_REQUIRE(q8 && q8_scales, "mmr_layernorm_bf16_q8: NULL MX-fp8 output");
   return layernorm_launch(x, residual, gamma, beta, y, rows, c, eps, stream, "mmr_layernorm_bf16_q8", nullptr, q8,
                           q8_scales);
+}
+
+mmr_status mmr_layernorm_bf16_q8p(const uint16_t* x, const uint16_t* residual, const float* gamma,
+                                  const float* beta, uint16_t* y, uint8_t* q8, uint8_t* q8_scales, int64_t rows,
+                                  int32_t c, int32_t kp, float eps, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(q8 && q8_scales, "mmr_layernorm_bf16_q8p: NULL MX-fp8 output");
+  return layernorm_launch(x, residual, gamma, beta, y, rows, c, eps, stream, "mmr_layernorm_bf16_q8p", nullptr, q8,
+                          q8_scales, kp);
 }
 
 mmr_status mmr_scaled_add_layernorm_bf16(const uint16_t* x, const float* alpha, const uint16_t* residual,
@@ -930,11 +979,13 @@ mmr_status mmr_swin_attn_bias(const float* relpos_table, float* bias, int32_t he
   return MMR_OK;
 }
 
-mmr_status mmr_swin_window_attention(const uint16_t* qkv, const float* bias, uint16_t* out,
-                                     int32_t b, int32_t hw, int32_t c, int32_t heads, int32_t ws,
-                                     int32_t shift, void* stream) {
-  mmr::clear_error();
-  MMR_REQUIRE(qkv && bias && out, "mmr_swin_window_attention: NULL pointer");
+static mmr_status swin_window_attention_launch(const uint16_t* qkv, const float* bias, uint16_t* out, uint8_t* q8,
+                                               uint8_t* q8s, int32_t b, int32_t hw, int32_t c, int32_t kp,
+                                               int32_t heads, int32_t ws, int32_t shift, void* stream) {
+  MMR_REQUIRE(qkv && bias && (out || (q8 && q8s)), "mmr_swin_window_attention: NULL pointer");
+  MMR_REQUIRE(!q8 || ((int64_t)b * hw * hw % 256 == 0 && kp % 256 == 0 && kp >= c),
+              "mmr_swin_window_attention_q8: rows %lld must be a multiple of 256 and kp=%d a multiple of 256 >= c=%d",
+              (long long)b * hw * hw, kp, c);
   MMR_REQUIRE(heads > 0 && c == heads * SW_DH, "mmr_swin_window_attention: c=%d heads=%d (head_dim 32 only)", c, heads);
   MMR_REQUIRE(ws > 0 && ws * ws <= 64 && hw % ws == 0, "mmr_swin_window_attention: window %d / resolution %d", ws, hw);
   MMR_REQUIRE(shift >= 0 && shift < ws, "mmr_swin_window_attention: shift %d", shift);
@@ -946,10 +997,30 @@ mmr_status mmr_swin_window_attention(const uint16_t* qkv, const float* bias, uin
   const int64_t single = (int64_t)b * (hw / ws) * (hw / ws) * heads;
   const int hpw = single >= 16384 ? 2 : 1;
   const int64_t units = (int64_t)b * (hw / ws) * (hw / ws) * ((heads + hpw - 1) / hpw);
-  swin_window_attention<<<dim3((unsigned)mmr::ceil_div(units, 4)), 256, 0, mmr::as_stream(stream)>>>(
-      qkv, bias, out, units, hw, c, heads, ws, shift, hpw);
+  if (q8)
+    swin_window_attention<true><<<dim3((unsigned)mmr::ceil_div(units, 4)), 256, 0, mmr::as_stream(stream)>>>(
+        qkv, bias, nullptr, units, hw, c, heads, ws, shift, hpw, q8, q8s, kp);
+  else
+    swin_window_attention<false><<<dim3((unsigned)mmr::ceil_div(units, 4)), 256, 0, mmr::as_stream(stream)>>>(
+        qkv, bias, out, units, hw, c, heads, ws, shift, hpw);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
+}
+
+mmr_status mmr_swin_window_attention(const uint16_t* qkv, const float* bias, uint16_t* out,
+                                     int32_t b, int32_t hw, int32_t c, int32_t heads, int32_t ws,
+                                     int32_t shift, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(out, "mmr_swin_window_attention: NULL output");
+  return swin_window_attention_launch(qkv, bias, out, nullptr, nullptr, b, hw, c, c, heads, ws, shift, stream);
+}
+
+mmr_status mmr_swin_window_attention_q8(const uint16_t* qkv, const float* bias, uint8_t* q8, uint8_t* q8_scales,
+                                        int32_t b, int32_t hw, int32_t c, int32_t kp, int32_t heads, int32_t ws,
+                                        int32_t shift, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(q8 && q8_scales, "mmr_swin_window_attention_q8: NULL MX-fp8 output");
+  return swin_window_attention_launch(qkv, bias, nullptr, q8, q8_scales, b, hw, c, kp, heads, ws, shift, stream);
 }
 
 mmr_status mmr_patch_im2col(const float* image, uint16_t* cols, int32_t b, int32_t cin,

@@ -137,17 +137,24 @@ def add_layernorm(x, r, g, b, eps, out=None):
     return y
 
 
-def layernorm_q8(x, r, g, b, eps):
+def layernorm_q8(x, r, g, b, eps, kp=None, want_y=True):
     """LayerNorm(x (+ r)) -> (y bf16, its MX-fp8 activation operand) in one pass (rows % 256 == 0,
-    C % 256 == 0); r may be None."""
+    C % 32 == 0); r may be None.  kp: the operand's padded K (a multiple of 256 >= C; default C, which
+    must then be a multiple of 256) — the padding is written as quantize_mxfp8 writes it.  want_y=False
+    skips the bf16 output (y is None) when only the operand is consumed."""
     _lib.require_gpu(x)
     c = x.shape[-1]
     rows = x.numel() // c
-    y = torch.empty_like(x)
-    q = torch.empty((rows, c), dtype=torch.uint8, device=x.device)
-    s = torch.empty(((rows // 256) * (c // 128) * 1024,), dtype=torch.uint8, device=x.device)
-    _chk(_L().mmr_layernorm_bf16_q8(_lib.ptr(x), _lib.ptr(r), _lib.ptr(g), _lib.ptr(b), _lib.ptr(y), _lib.ptr(q),
-                                    _lib.ptr(s), rows, c, float(eps), _s(x)), "mmr_layernorm_bf16_q8")
+    kp = kp or c
+    y = torch.empty_like(x) if want_y else None
+    q = torch.empty((rows, kp), dtype=torch.uint8, device=x.device)
+    s = torch.empty(((rows // 256) * (kp // 128) * 1024,), dtype=torch.uint8, device=x.device)
+    if kp == c and want_y:
+        _chk(_L().mmr_layernorm_bf16_q8(_lib.ptr(x), _lib.ptr(r), _lib.ptr(g), _lib.ptr(b), _lib.ptr(y), _lib.ptr(q),
+                                        _lib.ptr(s), rows, c, float(eps), _s(x)), "mmr_layernorm_bf16_q8")
+    else:
+        _chk(_L().mmr_layernorm_bf16_q8p(_lib.ptr(x), _lib.ptr(r), _lib.ptr(g), _lib.ptr(b), _lib.ptr(y), _lib.ptr(q),
+                                         _lib.ptr(s), rows, c, kp, float(eps), _s(x)), "mmr_layernorm_bf16_q8p")
     return y, MXFP8(q, s, c, 0)
 
 
@@ -219,6 +226,20 @@ def swin_window_attention(qkv, bias, hw, heads, ws, shift):
     _chk(_L().mmr_swin_window_attention(_lib.ptr(qkv), _lib.ptr(bias), _lib.ptr(out), B, hw, C, heads, ws,
                                         shift, _s(qkv)), "mmr_swin_window_attention")
     return out
+
+
+def swin_window_attention_q8(qkv, bias, hw, heads, ws, shift, kp=None):
+    """swin_window_attention emitting the proj GEMM's MX-fp8 operand (K padded to kp) instead of bf16
+    rows: == quantize_mxfp8(swin_window_attention(...), kp=kp), rows % 256 == 0."""
+    B = qkv.shape[0]
+    C = qkv.shape[-1] // 3
+    kp = kp or -(-C // 256) * 256
+    rows = qkv.numel() // qkv.shape[-1]
+    q = torch.empty((rows, kp), dtype=torch.uint8, device=qkv.device)
+    s = torch.empty(((rows // 256) * (kp // 128) * 1024,), dtype=torch.uint8, device=qkv.device)
+    _chk(_L().mmr_swin_window_attention_q8(_lib.ptr(qkv), _lib.ptr(bias), _lib.ptr(q), _lib.ptr(s), B, hw, C, kp,
+                                           heads, ws, shift, _s(qkv)), "mmr_swin_window_attention_q8")
+    return MXFP8(q, s, C, 0)
 
 
 def patch_im2col(img, patch=4):

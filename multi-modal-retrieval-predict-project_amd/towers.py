@@ -17,6 +17,8 @@ Per-block dataflow (all hand-written kernels, bf16 activations, f32 accumulation
                FFN1 GEMM(+bias, GELU) -> FFN2 GEMM(+bias) -> LN(+residual)   (post-LN residual
                adds ride in the LayerNorm kernel, so the GEMMs run the residual-free epilogue)
 """
+import os
+
 import torch
 
 from . import ops
@@ -86,10 +88,17 @@ def _mlp8(h, w1_8, b1, w2_8, b2, residual=None, h8=None):
     return (y if rp == rows else y[:rows]).reshape(tuple(h.shape[:-1]) + (y.shape[-1],))
 
 
+_LN8_PAD = os.environ.get("MMR_LN8_PAD", "1") != "0"
+_SWA_Q8 = os.environ.get("MMR_SWA_Q8", "1") != "0"  # A/B switch: window attention emits the proj operand
+
+
 def _ln8_ok(x, w8):
-    """The LayerNorm can emit the fp8 operand itself (rows and C multiples of 256, unpadded K)."""
+    """The LayerNorm can emit the fp8 operand itself: rows a multiple of 256, C of 32 (K padded to the
+    weight's kp, e.g. stage 3's C = 384 -> 512, is written by the LayerNorm too)."""
     C = x.shape[-1]
-    return w8 is not None and C % 256 == 0 and (x.numel() // C) % 256 == 0 and w8.kp == C
+    if not _LN8_PAD:  # A/B switch (MMR_LN8_PAD=0): unpadded C % 256 == 0 only, as before
+        return w8 is not None and C % 256 == 0 and (x.numel() // C) % 256 == 0 and w8.kp == C
+    return w8 is not None and C % 32 == 0 and (x.numel() // C) % 256 == 0 and w8.kp >= C
 
 
 def _lin(x, w, b=None, residual=None, act=0, w8=None):
@@ -191,11 +200,16 @@ class SwinTower:
             for j, bk in enumerate(st["blocks"]):
                 if bk["attn_pack"] is not None:
                     x = ops.swin_attn_block(x, bk["attn_pack"], bk["bias"], ws, bk["shift"], 1e-5)
-                elif _ln8_ok(x, bk["qkv_w8"]):  # fp8 stage, C % 256 == 0: the LN emits the QKV operand
-                    _, h8 = ops.layernorm_q8(x, None, bk["n1g"], bk["n1b"], 1e-5)
+                elif _ln8_ok(x, bk["qkv_w8"]):  # fp8 stage: the LN emits the QKV operand (no bf16 rows)
+                    _, h8 = ops.layernorm_q8(x, None, bk["n1g"], bk["n1b"], 1e-5, kp=bk["qkv_w8"].kp, want_y=False)
                     qkv = ops.linear_mxfp8(h8, bk["qkv_w8"], bk["qkv_b"], lead=tuple(x.shape[:-1]))
-                    a = ops.swin_window_attention(qkv, bk["bias"], H, heads, ws, bk["shift"])
-                    x = _lin(a, bk["proj_w"], bk["proj_b"], residual=x, w8=bk["proj_w8"])
+                    if _SWA_Q8:  # the attention core writes the proj operand (no bf16 rows, no quantise pass)
+                        a8 = ops.swin_window_attention_q8(qkv, bk["bias"], H, heads, ws, bk["shift"],
+                                                          kp=bk["proj_w8"].kp)
+                        x = ops.linear_mxfp8(a8, bk["proj_w8"], bk["proj_b"], x, lead=tuple(x.shape[:-1]))
+                    else:
+                        a = ops.swin_window_attention(qkv, bk["bias"], H, heads, ws, bk["shift"])
+                        x = _lin(a, bk["proj_w"], bk["proj_b"], residual=x, w8=bk["proj_w8"])
                 else:
                     h = ops.layernorm(x, bk["n1g"], bk["n1b"], 1e-5)
                     qkv = (ops.linear_rw(h, bk["qkv_rw"], bk["qkv_b"]) if bk["qkv_rw"] is not None
@@ -206,8 +220,8 @@ class SwinTower:
                 if bk["mlp_pack"] is not None:
                     x = ops.swin_mlp(x, bk["n2g"], bk["n2b"], bk["mlp_pack"], bk["fc1_b"], bk["fc2_b"], 1e-5)
                 elif _ln8_ok(x, bk["fc1_w8"]) and bk["fc1_w8"].layout == 2:
-                    h, h8 = ops.layernorm_q8(x, None, bk["n2g"], bk["n2b"], 1e-5)
-                    x = _mlp8(h, bk["fc1_w8"], bk["fc1_b"], bk["fc2_w8"], bk["fc2_b"], residual=x, h8=h8)
+                    _, h8 = ops.layernorm_q8(x, None, bk["n2g"], bk["n2b"], 1e-5, kp=bk["fc1_w8"].kp, want_y=False)
+                    x = _mlp8(x, bk["fc1_w8"], bk["fc1_b"], bk["fc2_w8"], bk["fc2_b"], residual=x, h8=h8)
                 else:
                     h = ops.layernorm(x, bk["n2g"], bk["n2b"], 1e-5)
                     if bk["fc1_w8"] is not None and bk["fc1_w8"].layout == 2:
@@ -287,8 +301,8 @@ class BertTower:
             ev.setdefault(name, []).append((e0, e1))
             return y
         # fp8 fast path: every LayerNorm also emits the next GEMM's MX-fp8 operand, FFN1 emits FFN2's
-        fast8 = (self.fp8 and ev is None and all(_ln8_ok(h, ly["qkv_w8"]) and ly["i_w8"].layout == 2
-                                                  for ly in self.layers))
+        fast8 = (self.fp8 and ev is None and all(_ln8_ok(h, ly["qkv_w8"]) and ly["qkv_w8"].kp == h.shape[-1]
+                                                  and ly["i_w8"].layout == 2 for ly in self.layers))
         h8 = ops.quantize_mxfp8(h.reshape(-1, h.shape[-1]), layout=0) if fast8 else None
         lead = tuple(h.shape[:-1])
         for ly in self.layers:

@@ -126,6 +126,28 @@ def test_layernorm_q8_equals_quantised_layernorm(rows, c, add):
     assert torch.equal(y8.s, ref8.s)
 
 
+@pytest.mark.parametrize("rows,c,kp,want_y", [(512, 384, 512, False), (256, 384, 512, True), (256, 96, 256, False),
+                                             (256, 768, 768, False)])
+def test_layernorm_q8_padded_k(rows, c, kp, want_y):
+    """The fp8 Swin stages' LayerNorm operand with K padded to the weight's kp (stage 3: C = 384 -> 512):
+    bytes and scale bytes equal mmr_quantize_mxfp8(LayerNorm(x), kp) including the zero padding; with
+    want_y=False no bf16 rows are written."""
+    xt, _ = _bf16_input(rows, c, 7 + rows + c)
+    g = torch.Generator().manual_seed(c + 1)
+    gam, bet = (torch.randn(c, generator=g) * 0.5 + 1).to(DEV), (torch.randn(c, generator=g) * 0.1).to(DEV)
+    x = xt.to(DEV)
+    y, y8 = ops.layernorm_q8(x, None, gam, bet, 1e-5, kp=kp, want_y=want_y)
+    ref = ops.layernorm(x, gam, bet, 1e-5)
+    ref8 = ops.quantize_mxfp8(ref, layout=0, kp=kp)
+    torch.cuda.synchronize()
+    assert (y is None) == (not want_y)
+    if want_y:
+        assert torch.equal(y, ref)
+    assert y8.kp == kp and y8.k == c
+    assert torch.equal(y8.q, ref8.q)
+    assert torch.equal(y8.s, ref8.s)
+
+
 @pytest.mark.parametrize("rows,c,l,f32in", [(512, 768, 128, False), (256, 768, 49, True), (768, 1024, 51, False)])
 def test_add_pos_q8_and_scaled_ln_q8_equal_quantised_outputs(rows, c, l, f32in):
     """The fusion stack's fp8 operand producers (config 5): x + pos and LayerNorm(alpha*x + r) with the

@@ -226,6 +226,24 @@ def test_swin_window_attention(H, heads, shift):
     assert rel_err(y, ref) < 2e-2
 
 
+@pytest.mark.parametrize("B,H,heads,shift,kp", [(128, 14, 12, 3, 512), (128, 14, 12, 0, 512), (256, 7, 24, 0, 768),
+                                                (256, 7, 24, 0, 1024)])
+def test_swin_window_attention_q8(B, H, heads, shift, kp):
+    """The fp8 stages' window attention writing the proj GEMM's MX-fp8 operand (stage 3: C = 384, K
+    padded to 512; stage 4: C = 768): bytes and scale bytes equal quantize_mxfp8 of the bf16 kernel's
+    output, the padding included."""
+    ws, C = 7, heads * 32
+    g = torch.Generator().manual_seed(B + H + heads + shift)
+    qkv = bf(torch.randn(B, H, H, 3 * C, generator=g)).to(DEV)
+    bias = ops.swin_attn_bias(torch.randn(169, heads, generator=g).to(DEV), heads, ws, H, shift)
+    a8 = ops.swin_window_attention_q8(qkv, bias, H, heads, ws, shift, kp=kp)
+    ref8 = ops.quantize_mxfp8(ops.swin_window_attention(qkv, bias, H, heads, ws, shift), layout=0, kp=kp)
+    torch.cuda.synchronize()
+    assert a8.kp == kp and a8.k == C
+    assert torch.equal(a8.q, ref8.q)
+    assert torch.equal(a8.s, ref8.s)
+
+
 @pytest.mark.parametrize("B,shift", [(2, 0), (2, 3), (5, 3)])
 def test_swin_attn_block_fused(B, shift):
     """mmr_swin_attn_block == oracle swin_attn_half (timm: x + proj(W-MSA(norm1(x))) with roll,

@@ -117,6 +117,14 @@ for s in $STEPS; do
         env $E timeout -k 10 500 python -u bench.py --preset cfg5 --steps 5 --warmup 2 --no-cpu-baseline > $OUT/cfg5ab.json 2> $OUT/cfg5ab.err
         python -c "import json;d=json.load(open('$OUT/cfg5ab.json'));print('$L', round(d['ms_per_step'],3), round(d['value']))"
       done; done ;;
+    cfg5env)  # cfg5 step, env A / B (ENVA / ENVB), same box
+      for i in 1 2; do for e in "${ENVA:-X=0}" "${ENVB:-X=1}"; do
+        env $e timeout -k 10 500 python -u bench.py --preset cfg5 --steps 5 --warmup 2 --no-cpu-baseline > $OUT/cfg5env.json 2> $OUT/cfg5env.err
+        python -c "import json;d=json.load(open('$OUT/cfg5env.json'));print('$e', round(d['ms_per_step'],3), round(d['value']))"
+      done; done ;;
+    pyt)  # a subset of the GPU tests (PYT = pytest selection)
+      timeout -k 10 400 python -u -m pytest ${PYT} -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pyt.log 2>&1 || { tail -30 $OUT/pyt.log; exit 1; }
+      tail -2 $OUT/pyt.log ;;
     knnab)  # kNN leg alone at KNNARGS (default cfg5: Q 2048 over 1M x 1024), env A / B (ENVA / ENVB)
       for i in 1 2; do for e in "${ENVA:-X=0}" "${ENVB:-X=1}"; do
         env $e timeout -k 10 300 python -u bench.py --mode knn ${KNNARGS:---preset cfg5 --batch 2048} --steps 10 --warmup 2 --no-cpu-baseline > $OUT/knnab.json 2> $OUT/knnab.err
