@@ -251,6 +251,12 @@ mmr_status mmr_scaled_add_layernorm_bf16_q8(const uint16_t* x, const float* alph
 mmr_status mmr_bert_embed(const int64_t* ids, const float* word, const float* pos,
                           const float* type0, const float* gamma, const float* beta, uint16_t* y,
                           int32_t b, int32_t l, int32_t c, float eps, void* stream);
+/* mmr_bert_embed also writing y as the first QKV GEMM's MX-fp8 activation operand (q8 [b*l][c] e4m3 +
+ * layout-0 scales), bit-identical to mmr_quantize_mxfp8 of y (the fp8 BERT tower; c % 256 == 0,
+ * c <= 1024, b*l % 256 == 0).  q8 / q8_scales NULL = mmr_bert_embed. */
+mmr_status mmr_bert_embed_q8(const int64_t* ids, const float* word, const float* pos, const float* type0,
+                             const float* gamma, const float* beta, uint16_t* y, uint8_t* q8, uint8_t* q8_scales,
+                             int32_t b, int32_t l, int32_t c, float eps, void* stream);
 
 /* BERT self-attention core (HF BertSelfAttention, eval): qkv bf16 (b*l, 3*h*dh) [q|k|v],
  * additive mask from mask01 (b, l) int64 (0 -> masked), softmax(q k^T / sqrt(dh)) v -> ctx bf16
@@ -322,6 +328,12 @@ mmr_status mmr_patch_im2col(const float* image, uint16_t* cols, int32_t b, int32
 mmr_status mmr_patch_merge_ln(const uint16_t* x, const float* gamma, const float* beta,
                               uint16_t* y, int32_t b, int32_t hw, int32_t c, float eps,
                               void* stream);
+/* mmr_patch_merge_ln also (y may be NULL: instead) writing the merged row as the reduction GEMM's
+ * MX-fp8 activation operand (q8 [rows][4c] e4m3 + layout-0 scales), bit-identical to
+ * mmr_quantize_mxfp8 of y (the fp8 Swin stages 3-4: 4c = 768 / 1536; rows % 256 == 0, 4c % 256 == 0). */
+mmr_status mmr_patch_merge_ln_q8(const uint16_t* x, const float* gamma, const float* beta, uint16_t* y,
+                                 uint8_t* q8, uint8_t* q8_scales, int32_t b, int32_t hw, int32_t c, float eps,
+                                 void* stream);
 
 /* Swin head (fusion.py:263-265 with swin_norm = swin.norm): x bf16 (b, t, c) = backbone tokens
  * BEFORE the final norm.  patches = LN(LN(x)) f32 (b,t,c), global = mean_t LN(x) f32 (b,c),

@@ -158,7 +158,10 @@ __global__ __launch_bounds__(256) void bert_embed(const int64_t* __restrict__ id
                                                   const float* __restrict__ g,
                                                   const float* __restrict__ b,
                                                   uint16_t* __restrict__ y, int64_t ntok, int l,
-                                                  int c, float eps) {
+                                                  int c, float eps, uint8_t* __restrict__ q8 = nullptr,
+                                                  uint8_t* __restrict__ q8s = nullptr) {
+  // q8 (c % 256 == 0, ntok % 256 == 0): also the first QKV GEMM's MX-fp8 operand, bit-identical to
+  // mmr_quantize_mxfp8 of y (a 32-block = 8 adjacent lanes' float4s)
   const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (tok >= ntok) return;
@@ -197,6 +200,17 @@ __global__ __launch_bounds__(256) void bert_embed(const int64_t* __restrict__ id
         o.x = mmr::pack2bf((v[j].x - mean) * rstd * gg.x + bb.x, (v[j].y - mean) * rstd * gg.y + bb.y);
         o.y = mmr::pack2bf((v[j].z - mean) * rstd * gg.z + bb.z, (v[j].w - mean) * rstd * gg.w + bb.w);
         *(uint2*)(y + tok * c + k) = o;
+        if (q8) {  // k < c is wave-uniform here (c % 256 == 0)
+          const float vb[4] = {__uint_as_float(o.x << 16), __uint_as_float(o.x & 0xFFFF0000u),
+                               __uint_as_float(o.y << 16), __uint_as_float(o.y & 0xFFFF0000u)};
+          float amax = fmaxf(fmaxf(fabsf(vb[0]), fabsf(vb[1])), fmaxf(fabsf(vb[2]), fabsf(vb[3])));
+          amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+          amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+          amax = fmaxf(amax, __shfl_xor(amax, 4, 64));
+          const int ex = mmr::q8_exp(amax);
+          *(uint32_t*)(q8 + tok * c + k) = mmr::q8_pack4(vb, mmr::q8_inv(ex));
+          if ((lane & 7) == 0) q8s[mmr::q8_soff(tok, k, c)] = (uint8_t)(ex + 127);
+        }
       }
     }
     return;
@@ -485,12 +499,17 @@ __global__ __launch_bounds__(256) void patch_im2col_p4c3(const float* __restrict
 // merged row, 3 16-B chunks per lane (chunk it of lane l: merged channels 8 (l + G it) .. +7, inside
 // one source token since c % 8 == 0), 64 / G rows per wave.  The one-row-per-wave form below left
 // 3/4 of the lanes on clamped duplicate loads at 4c = 384 (172 us for the 308 MB of stage 1 -> 2).
+// q8 (both forms, a runtime pointer so y is the same code either way): also / instead (y NULL) emit the merged row as the reduction GEMM's MX-fp8
+// operand (4c % 256 == 0, no K padding), bit-identical to mmr_quantize_mxfp8 of the bf16 row: a
+// 32-block is 4 adjacent lanes' chunks in both lane maps.
 template <int G>
 __global__ __launch_bounds__(256) void patch_merge_ln_g(const uint16_t* __restrict__ x,
                                                         const float* __restrict__ g,
                                                         const float* __restrict__ b,
                                                         uint16_t* __restrict__ y, int64_t nout,
-                                                        int hw, int c, float eps) {
+                                                        int hw, int c, float eps,
+                                                        uint8_t* __restrict__ q8 = nullptr,
+                                                        uint8_t* __restrict__ q8s = nullptr) {
   constexpr int C4 = 24 * G, RPW = 64 / G;
   const int lane = threadIdx.x & 63, lg = lane % G;
   const int64_t o0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / G;
@@ -530,15 +549,19 @@ __global__ __launch_bounds__(256) void patch_merge_ln_g(const uint16_t* __restri
 #pragma unroll
   for (int m = 1; m < G; m <<= 1) ss += __shfl_xor(ss, m, 64);
   const float rstd = rsqrtf(ss * (1.0f / C4) + eps);
-  if (o0 < nout) {
 #pragma unroll
-    for (int it = 0; it < 3; ++it) {
-      const f32x4 g0 = ga[it][0], g1 = ga[it][1], b0 = ba[it][0], b1 = ba[it][1];
-      const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
-      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+  for (int it = 0; it < 3; ++it) {
+    const f32x4 g0 = ga[it][0], g1 = ga[it][1], b0 = ba[it][0], b1 = ba[it][1];
+    const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[it][e] = (v[it][e] - mean) * rstd * gg[e] + bb[e];
-      store8(y + o0 * C4 + 8 * (lg + G * it), v[it]);
+    for (int e = 0; e < 8; ++e) v[it][e] = fmaf((v[it][e] - mean) * rstd, gg[e], bb[e]);  // explicit: same in both forms
+    if (y && o0 < nout) store8(y + o0 * C4 + 8 * (lg + G * it), v[it]);
+    if (q8) {  // wave-uniform
+      float vb[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) vb[e] = bf2f(f2bf(v[it][e]));
+      mmr::q8_chunk8(vb, o0, lg + G * it, C4, q8, q8s, o0 < nout);
     }
   }
 }
@@ -547,7 +570,9 @@ __global__ __launch_bounds__(256) void patch_merge_ln(const uint16_t* __restrict
                                                       const float* __restrict__ g,
                                                       const float* __restrict__ b,
                                                       uint16_t* __restrict__ y, int64_t nout,
-                                                      int hw, int c, float eps) {
+                                                      int hw, int c, float eps,
+                                                      uint8_t* __restrict__ q8 = nullptr,
+                                                      uint8_t* __restrict__ q8s = nullptr) {
   const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (o >= nout) return;
@@ -615,11 +640,18 @@ __global__ __launch_bounds__(256) void patch_merge_ln(const uint16_t* __restrict
       const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
       const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[it][e] = (v[it][e] - mean) * rstd * gg[e] + bb[e];
-      if (k < c4) store8(y + o * c4 + k, v[it]);
+      for (int e = 0; e < 8; ++e) v[it][e] = fmaf((v[it][e] - mean) * rstd, gg[e], bb[e]);
+      if (y && k < c4) store8(y + o * c4 + k, v[it]);
+      if (q8) {  // wave-uniform
+        float vb[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vb[e] = bf2f(f2bf(v[it][e]));
+        mmr::q8_chunk8(vb, o, lane + 64 * it, c4, q8, q8s, k < c4);
+      }
     }
     return;
   }
+  if (q8) return;  // the launcher keeps q8 to 4c <= 2048
   float s = 0.f;
   for (int k = lane * 8; k < c4; k += 512) {
     float v[8];
@@ -951,18 +983,27 @@ mmr_status mmr_scaled_add_layernorm_bf16_q8(const uint16_t* x, const float* alph
                           alpha, q8, q8_scales);
 }
 
-mmr_status mmr_bert_embed(const int64_t* ids, const float* word, const float* pos,
-                          const float* type0, const float* gamma, const float* beta, uint16_t* y,
-                          int32_t b, int32_t l, int32_t c, float eps, void* stream) {
+mmr_status mmr_bert_embed_q8(const int64_t* ids, const float* word, const float* pos, const float* type0,
+                             const float* gamma, const float* beta, uint16_t* y, uint8_t* q8, uint8_t* q8_scales,
+                             int32_t b, int32_t l, int32_t c, float eps, void* stream) {
   mmr::clear_error();
   MMR_REQUIRE(ids && word && pos && type0 && gamma && beta && y, "mmr_bert_embed: NULL pointer");
   MMR_REQUIRE(b >= 0 && l > 0 && c > 0, "mmr_bert_embed: bad shape");
   const int64_t ntok = (int64_t)b * l;
+  MMR_REQUIRE(!q8 || (q8_scales && c % 256 == 0 && c <= 1024 && ntok % 256 == 0),
+              "mmr_bert_embed_q8: needs c %% 256 == 0, c <= 1024 and b*l %% 256 == 0 (c=%d, b*l=%lld)", c,
+              (long long)ntok);
   if (ntok == 0) return MMR_OK;
   bert_embed<<<dim3((unsigned)mmr::ceil_div(ntok, 4)), 256, 0, mmr::as_stream(stream)>>>(
-      ids, word, pos, type0, gamma, beta, y, ntok, l, c, eps);
+      ids, word, pos, type0, gamma, beta, y, ntok, l, c, eps, q8, q8_scales);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
+}
+
+mmr_status mmr_bert_embed(const int64_t* ids, const float* word, const float* pos,
+                          const float* type0, const float* gamma, const float* beta, uint16_t* y,
+                          int32_t b, int32_t l, int32_t c, float eps, void* stream) {
+  return mmr_bert_embed_q8(ids, word, pos, type0, gamma, beta, y, nullptr, nullptr, b, l, c, eps, stream);
 }
 
 mmr_status mmr_swin_attn_bias(const float* relpos_table, float* bias, int32_t heads, int32_t ws,
@@ -1041,25 +1082,43 @@ mmr_status mmr_patch_im2col(const float* image, uint16_t* cols, int32_t b, int32
   return MMR_OK;
 }
 
+static mmr_status patch_merge_launch(const uint16_t* x, const float* gamma, const float* beta, uint16_t* y,
+                                     uint8_t* q8, uint8_t* q8s, int32_t b, int32_t hw, int32_t c, float eps,
+                                     void* stream) {
+  MMR_REQUIRE(x && gamma && beta && (y || q8), "mmr_patch_merge_ln: NULL pointer");
+  MMR_REQUIRE(hw % 2 == 0 && c % 8 == 0, "mmr_patch_merge_ln: hw=%d c=%d", hw, c);
+  const int64_t nout = (int64_t)b * (hw / 2) * (hw / 2);
+  MMR_REQUIRE(!q8 || (nout % 256 == 0 && (4 * c) % 256 == 0 && 4 * c <= 2048),
+              "mmr_patch_merge_ln_q8: needs merged rows %% 256 == 0 and 4c %% 256 == 0, 4c <= 2048 (rows=%lld c=%d)",
+              (long long)nout, c);
+  if (nout == 0) return MMR_OK;
+  hipStream_t st = mmr::as_stream(stream);
+  if (4 * c == 24 * 16)
+    patch_merge_ln_g<16><<<dim3((unsigned)mmr::ceil_div(nout, 16)), 256, 0, st>>>(x, gamma, beta, y, nout, hw, c, eps);
+  else if (4 * c == 24 * 32)
+    patch_merge_ln_g<32><<<dim3((unsigned)mmr::ceil_div(nout, 8)), 256, 0, st>>>(x, gamma, beta, y, nout, hw, c, eps,
+                                                                                  q8, q8s);
+  else
+    patch_merge_ln<<<dim3((unsigned)mmr::ceil_div(nout, 4)), 256, 0, st>>>(x, gamma, beta, y, nout, hw, c, eps, q8,
+                                                                            q8s);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
 mmr_status mmr_patch_merge_ln(const uint16_t* x, const float* gamma, const float* beta,
                               uint16_t* y, int32_t b, int32_t hw, int32_t c, float eps,
                               void* stream) {
   mmr::clear_error();
-  MMR_REQUIRE(x && gamma && beta && y, "mmr_patch_merge_ln: NULL pointer");
-  MMR_REQUIRE(hw % 2 == 0 && c % 8 == 0, "mmr_patch_merge_ln: hw=%d c=%d", hw, c);
-  const int64_t nout = (int64_t)b * (hw / 2) * (hw / 2);
-  if (nout == 0) return MMR_OK;
-  if (4 * c == 24 * 16)
-    patch_merge_ln_g<16><<<dim3((unsigned)mmr::ceil_div(nout, 16)), 256, 0, mmr::as_stream(stream)>>>(
-        x, gamma, beta, y, nout, hw, c, eps);
-  else if (4 * c == 24 * 32)
-    patch_merge_ln_g<32><<<dim3((unsigned)mmr::ceil_div(nout, 8)), 256, 0, mmr::as_stream(stream)>>>(
-        x, gamma, beta, y, nout, hw, c, eps);
-  else
-    patch_merge_ln<<<dim3((unsigned)mmr::ceil_div(nout, 4)), 256, 0, mmr::as_stream(stream)>>>(
-        x, gamma, beta, y, nout, hw, c, eps);
-  MMR_LAUNCH_CHECK();
-  return MMR_OK;
+  MMR_REQUIRE(y, "mmr_patch_merge_ln: NULL output");
+  return patch_merge_launch(x, gamma, beta, y, nullptr, nullptr, b, hw, c, eps, stream);
+}
+
+mmr_status mmr_patch_merge_ln_q8(const uint16_t* x, const float* gamma, const float* beta, uint16_t* y,
+                                 uint8_t* q8, uint8_t* q8_scales, int32_t b, int32_t hw, int32_t c, float eps,
+                                 void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(q8 && q8_scales, "mmr_patch_merge_ln_q8: NULL MX-fp8 output");
+  return patch_merge_launch(x, gamma, beta, y, q8, q8_scales, b, hw, c, eps, stream);
 }
 
 mmr_status mmr_swin_head(const uint16_t* x, const float* gamma, const float* beta, float* patches,

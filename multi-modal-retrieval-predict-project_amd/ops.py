@@ -194,6 +194,20 @@ def bert_embed(ids, word, pos, type0, g, b, eps):
     return y
 
 
+def bert_embed_q8(ids, word, pos, type0, g, b, eps):
+    """bert_embed also emitting the first QKV GEMM's MX-fp8 operand: (y, MXFP8) with the operand ==
+    quantize_mxfp8(y); B * L % 256 == 0, C % 256 == 0."""
+    _lib.require_gpu(ids)
+    B, L = ids.shape
+    C = word.shape[1]
+    y = torch.empty((B, L, C), dtype=torch.bfloat16, device=ids.device)
+    q, s = _q8_out(B * L, C, ids.device)
+    _chk(_L().mmr_bert_embed_q8(_lib.ptr(ids), _lib.ptr(word), _lib.ptr(pos), _lib.ptr(type0), _lib.ptr(g),
+                                _lib.ptr(b), _lib.ptr(y), _lib.ptr(q), _lib.ptr(s), B, L, C, float(eps), _s(ids)),
+         "mmr_bert_embed_q8")
+    return y, MXFP8(q, s, C, 0)
+
+
 def bert_attention(qkv, mask, heads, dh=64, q8=False, bf16=True):
     """ctx (B, L, C) bf16; q8: the context as an MX-fp8 activation operand too, returned as
     (ctx or None, MXFP8) — bf16=False skips the bf16 copy ((B*L) % 256 == 0, C % 256 == 0)."""
@@ -256,6 +270,19 @@ def patch_merge_ln(x, g, b, eps):
     _chk(_L().mmr_patch_merge_ln(_lib.ptr(x), _lib.ptr(g), _lib.ptr(b), _lib.ptr(y), B, H, C, float(eps),
                                  _s(x)), "mmr_patch_merge_ln")
     return y
+
+
+def patch_merge_ln_q8(x, g, b, eps, want_y=False):
+    """patch_merge_ln emitting the reduction GEMM's MX-fp8 operand: (y or None, MXFP8) with the operand
+    == quantize_mxfp8(patch_merge_ln(...)); merged rows % 256 == 0, 4C % 256 == 0."""
+    B, H, W, C = x.shape
+    rows = B * (H // 2) * (W // 2)
+    y = torch.empty((B, H // 2, W // 2, 4 * C), dtype=torch.bfloat16, device=x.device) if want_y else None
+    q = torch.empty((rows, 4 * C), dtype=torch.uint8, device=x.device)
+    s = torch.empty(((rows // 256) * (4 * C // 128) * 1024,), dtype=torch.uint8, device=x.device)
+    _chk(_L().mmr_patch_merge_ln_q8(_lib.ptr(x), _lib.ptr(g), _lib.ptr(b), _lib.ptr(y), _lib.ptr(q), _lib.ptr(s), B, H,
+                                    C, float(eps), _s(x)), "mmr_patch_merge_ln_q8")
+    return y, MXFP8(q, s, 4 * C, 0)
 
 
 def swin_head(x, g, b, eps, want_patches=True):

@@ -192,7 +192,14 @@ class SwinTower:
         ws0 = cfg["window_size"]
         for i, st in enumerate(self.stages):
             if i > 0:
-                x = _lin(ops.patch_merge_ln(x, st["ds_g"], st["ds_b"], 1e-5), st["ds_w"], w8=st["ds_w8"])
+                w8 = st["ds_w8"]
+                B, H2 = x.shape[0], x.shape[1] // 2
+                if (_SWA_Q8 and w8 is not None and (B * H2 * H2) % 256 == 0 and w8.kp == 4 * x.shape[-1]
+                        and w8.kp <= 2048):  # the gather + LN writes the reduction's fp8 operand
+                    _, m8 = ops.patch_merge_ln_q8(x, st["ds_g"], st["ds_b"], 1e-5)
+                    x = ops.linear_mxfp8(m8, w8, None, lead=(B, H2, H2))
+                else:
+                    x = _lin(ops.patch_merge_ln(x, st["ds_g"], st["ds_b"], 1e-5), st["ds_w"], w8=w8)
             H = x.shape[1]
             C = x.shape[-1]
             heads = cfg["num_heads"][i]
@@ -288,8 +295,16 @@ class BertTower:
             ids, mask = ids[:, :max_len], mask[:, :max_len]
         ids, mask = ids.contiguous(), mask.contiguous()
         heads = cfg["num_attention_heads"]
-        h = ops.bert_embed(ids, self.word, self.pos, self.type0, self.eg, self.eb, 1e-12)
         ev = self.gemm_events
+        rows, C = ids.numel(), self.hidden
+        # fp8 fast path: every LayerNorm also emits the next GEMM's MX-fp8 operand (the embedding
+        # LayerNorm the first QKV's), FFN1 emits FFN2's
+        fast8 = (self.fp8 and ev is None and C % 256 == 0 and C <= 1024 and rows % 256 == 0
+                 and all(ly["qkv_w8"].kp == C and ly["i_w8"].layout == 2 for ly in self.layers))
+        if fast8:
+            h, h8 = ops.bert_embed_q8(ids, self.word, self.pos, self.type0, self.eg, self.eb, 1e-12)
+        else:
+            h, h8 = ops.bert_embed(ids, self.word, self.pos, self.type0, self.eg, self.eb, 1e-12), None
 
         def gemm(name, x, w, b, act=0, w8=None):
             if ev is None:
@@ -300,10 +315,6 @@ class BertTower:
             e1.record()
             ev.setdefault(name, []).append((e0, e1))
             return y
-        # fp8 fast path: every LayerNorm also emits the next GEMM's MX-fp8 operand, FFN1 emits FFN2's
-        fast8 = (self.fp8 and ev is None and all(_ln8_ok(h, ly["qkv_w8"]) and ly["qkv_w8"].kp == h.shape[-1]
-                                                  and ly["i_w8"].layout == 2 for ly in self.layers))
-        h8 = ops.quantize_mxfp8(h.reshape(-1, h.shape[-1]), layout=0) if fast8 else None
         lead = tuple(h.shape[:-1])
         for ly in self.layers:
             if fast8:

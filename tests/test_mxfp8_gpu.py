@@ -236,3 +236,22 @@ def test_assemble_seq_q8_equals_quantised_sequence(B, np_, c):
     ref8 = ops.quantize_mxfp8(seq, layout=0)
     torch.cuda.synchronize()
     assert torch.equal(s8.q, ref8.q) and torch.equal(s8.s, ref8.s)
+
+
+@pytest.mark.parametrize("B,L,C", [(2, 128, 768), (4, 64, 256), (8, 96, 1024)])
+def test_bert_embed_q8_equals_quantised_embedding(B, L, C):
+    """The fp8 BERT tower's embedding LayerNorm writes the first QKV operand: y equal to bert_embed bit
+    for bit, the operand equal to quantize_mxfp8(y) (values and scale bytes)."""
+    g = torch.Generator().manual_seed(B * L + C)
+    word = (torch.randn(1000, C, generator=g) * 0.05).to(DEV)
+    pos = (torch.randn(512, C, generator=g) * 0.02).to(DEV)
+    type0 = (torch.randn(C, generator=g) * 0.02).to(DEV)
+    gam, bet = (torch.randn(C, generator=g) * 0.3 + 1).to(DEV), (torch.randn(C, generator=g) * 0.1).to(DEV)
+    ids = torch.randint(0, 1000, (B, L), generator=g).to(DEV)
+    y, y8 = ops.bert_embed_q8(ids, word, pos, type0, gam, bet, 1e-12)
+    ref = ops.bert_embed(ids, word, pos, type0, gam, bet, 1e-12)
+    ref8 = ops.quantize_mxfp8(ref.reshape(-1, C), layout=0)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+    assert torch.equal(y8.q, ref8.q)
+    assert torch.equal(y8.s, ref8.s)

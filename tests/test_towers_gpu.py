@@ -226,6 +226,25 @@ def test_swin_window_attention(H, heads, shift):
     assert rel_err(y, ref) < 2e-2
 
 
+@pytest.mark.parametrize("B,H,c,want_y", [(64, 28, 192, True), (256, 28, 192, False), (256, 14, 384, True),
+                                          (512, 14, 384, False)])
+def test_patch_merge_ln_q8(B, H, c, want_y):
+    """PatchMerging gather + LN(4c) emitting the reduction GEMM's MX-fp8 operand (fp8 stages 3-4: 4c =
+    768 / 1536): y equal to the bf16 kernel bit for bit, the operand equal to quantize_mxfp8 of it."""
+    g = torch.Generator().manual_seed(B + H + c)
+    x = bf(torch.randn(B, H, H, c, generator=g)).to(DEV)
+    gam, bet = (torch.randn(4 * c, generator=g) * 0.5 + 1).to(DEV), (torch.randn(4 * c, generator=g) * 0.1).to(DEV)
+    y, m8 = ops.patch_merge_ln_q8(x, gam, bet, 1e-5, want_y=want_y)
+    ref = ops.patch_merge_ln(x, gam, bet, 1e-5)
+    ref8 = ops.quantize_mxfp8(ref.reshape(-1, 4 * c), layout=0)
+    torch.cuda.synchronize()
+    assert (y is None) == (not want_y)
+    if want_y:
+        assert torch.equal(y, ref)
+    assert torch.equal(m8.q, ref8.q)
+    assert torch.equal(m8.s, ref8.s)
+
+
 @pytest.mark.parametrize("B,H,heads,shift,kp", [(128, 14, 12, 3, 512), (128, 14, 12, 0, 512), (256, 7, 24, 0, 768),
                                                 (256, 7, 24, 0, 1024)])
 def test_swin_window_attention_q8(B, H, heads, shift, kp):
