@@ -237,6 +237,9 @@ __global__ __launch_bounds__(256) void bert_embed(const int64_t* __restrict__ id
 // once per block by swin_attn_bias for the <= 4 window types (interior / last column / last row
 // / corner), softmax over keys in registers, O^T = V^T . P^T with V^T staged per wave in LDS.
 constexpr int SW_DH = 32;
+#ifndef SWA_LATE_BIAS
+#define SWA_LATE_BIAS 1
+#endif
 
 __device__ __forceinline__ int region_of(int rc, int H, int ws, int shift) {
   return rc < H - ws ? 0 : (rc < H - shift ? 1 : 2);
@@ -313,6 +316,23 @@ __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __r
     const int h0 = (hr + shift) % H, w0 = (wr + shift) % H;
     tl = (int)(bi * H * H + h0 * H + w0);
   }
+  if constexpr (Q8) {
+    // K padding C .. kp of this window's tokens: zero bytes, zero scale bytes, written up front by the
+    // waves of the last head group (no registers held across the attention)
+    if (kp > C && hpw * hp + hpw >= heads) {
+      const int r = lane & 31, hf = lane >> 5;
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const int qi = qt * 32 + r;
+        const int tqi = __shfl(tl, qi, 64);
+        if (qi < N) {
+          uint8_t* qrow = q8 + (int64_t)tqi * kp;
+          for (int off = C + 16 * hf; off < kp; off += 32) *(uint4*)(qrow + off) = make_uint4(0u, 0u, 0u, 0u);
+          for (int bk = C / 32 + hf; bk < kp / 32; bk += 2) q8s[mmr::q8_soff(tqi, bk * 32, kp)] = 0;
+        }
+      }
+    }
+  }
 #pragma unroll 1
   for (int h2 = 0; h2 < hpw; ++h2) {
     const int hh = hpw * hp + h2;
@@ -323,7 +343,9 @@ __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __r
     const uint16_t* hb = qkv + hh * SW_DH;
     const uint32_t rs = 3u * (uint32_t)C;  // element offsets fit 32 bits (launcher)
     bf16x8 qf[2][2], kf[2][2], vr[4];
-    float4 bb[2][2][4];  // bias rows of this lane's two queries: [qt][kt][g4] (keys kt 32 + 8 g4 + 4 hf ..)
+    // bias rows of this lane's two queries, loaded straight into the S accumulators as bias / scale
+    // (S = (q k^T + bias / scale) * scale: no separate 64-VGPR bias array live across the head)
+    f32x16 sacc[2][2];  // [qt][kt], element 4 g4 + e = key kt 32 + 8 g4 + 4 hf + e
 #pragma unroll
     for (int it = 0; it < 4; ++it)  // V rows: lane (key 16 it + lane / 4, 16-B chunk lane % 4)
       vr[it] = *(const bf16x8*)(hb + (uint32_t)__shfl(tl, 16 * it + (lane >> 2), 64) * rs + 2 * C + (lane & 3) * 8);
@@ -336,12 +358,20 @@ __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __r
         kf[t2][ks] = *(const bf16x8*)(row + C + ks * 16 + 8 * hf);
       }
     }
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
+    auto load_bias = [&](int qt) {
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) bb[qt][kt][g4] = *(const float4*)(bt + (qt * 32 + r) * 64 + kt * 32 + 8 * g4 + 4 * hf);
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const float4 bv = *(const float4*)(bt + (qt * 32 + r) * 64 + kt * 32 + 8 * g4 + 4 * hf);
+          sacc[qt][kt][4 * g4] = bv.x;
+          sacc[qt][kt][4 * g4 + 1] = bv.y;
+          sacc[qt][kt][4 * g4 + 2] = bv.z;
+          sacc[qt][kt][4 * g4 + 3] = bv.w;
+        }
+    };
+    load_bias(0);
+    if (!SWA_LATE_BIAS) load_bias(1);
     __builtin_amdgcn_sched_barrier(0);  // every load above in flight before the first use
 #pragma unroll
     for (int it = 0; it < 4; ++it) *(bf16x8*)(vs + (16 * it + (lane >> 2)) * VROW + (lane & 3) * 8) = vr[it];
@@ -351,14 +381,16 @@ __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __r
 
     constexpr float L2E = 1.4426950408889634f;
     const float scale = 0.17677669529663687f;  // 32^-0.5
+    const float rscale = 5.656854249492381f;     // 32^0.5
     const int grp = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       const int qi = qt * 32 + r;  // this lane's query (local index)
-      f32x16 s[2];
+      if (SWA_LATE_BIAS && qt == 1) load_bias(1);  // second query tile's bias after the first tile's S is free
+      f32x16* s = sacc[qt];  // in place: the bias rows become this query tile's S
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
-        s[kt] = (f32x16){0};
+        s[kt] *= rscale;  // bias / scale (-FLT_MAX padding -> -inf: exp2 -> 0)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
           s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kt][ks], qf[qt][ks], s[kt], 0, 0, 0);
@@ -369,14 +401,10 @@ __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __r
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const float bv[4] = {bb[qt][kt][g4].x, bb[qt][kt][g4].y, bb[qt][kt][g4].z, bb[qt][kt][g4].w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float v = fmaf(s[kt][4 * g4 + e], scale, bv[e]);
-            s[kt][4 * g4 + e] = v;
-            m4[e] = fmaxf(m4[e], v);
-          }
+        for (int rg = 0; rg < 16; ++rg) {
+          const float v = s[kt][rg] * scale;
+          s[kt][rg] = v;
+          m4[rg & 3] = fmaxf(m4[rg & 3], v);
         }
       float mloc = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
       mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
@@ -412,25 +440,24 @@ __global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __r
       const int tqi = __shfl(tl, qi, 64);
       if constexpr (Q8) {
         const float inv = 1.0f / psum;
-        float vb[16];
+        // amax of the bf16 values the plain kernel stores = the bf16 rounding of max |o * inv| (RNE is
+        // monotonic), and the values are re-rounded at the packing: no 16-register copy stays live
         float amax = 0.f;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          vb[e] = bf2f(f2bf(o[e] * inv));  // the bf16 value the plain kernel stores
-          amax = fmaxf(amax, fabsf(vb[e]));
-        }
+        for (int e = 0; e < 16; ++e) amax = fmaxf(amax, fabsf(o[e] * inv));
+        amax = bf2f(f2bf(amax));
         amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
         const int ex = mmr::q8_exp(amax);
         const float qinv = mmr::q8_inv(ex);
         if (qi < N) {
           uint8_t* qrow = q8 + (int64_t)tqi * kp;
 #pragma unroll
-          for (int g4 = 0; g4 < 4; ++g4) *(uint32_t*)(qrow + hh * SW_DH + 8 * g4 + 4 * hf) = mmr::q8_pack4(vb + 4 * g4, qinv);
-          if (hf == 0) q8s[mmr::q8_soff(tqi, hh * SW_DH, kp)] = (uint8_t)(ex + 127);
-          if (hh == heads - 1) {
-            for (int off = C + 16 * hf; off < kp; off += 32) *(uint4*)(qrow + off) = make_uint4(0u, 0u, 0u, 0u);
-            for (int bk = C / 32 + hf; bk < kp / 32; bk += 2) q8s[mmr::q8_soff(tqi, bk * 32, kp)] = 0;
+          for (int g4 = 0; g4 < 4; ++g4) {
+            const float vb[4] = {bf2f(f2bf(o[4 * g4] * inv)), bf2f(f2bf(o[4 * g4 + 1] * inv)),
+                                 bf2f(f2bf(o[4 * g4 + 2] * inv)), bf2f(f2bf(o[4 * g4 + 3] * inv))};
+            *(uint32_t*)(qrow + hh * SW_DH + 8 * g4 + 4 * hf) = mmr::q8_pack4(vb, qinv);
           }
+          if (hf == 0) q8s[mmr::q8_soff(tqi, hh * SW_DH, kp)] = (uint8_t)(ex + 127);
         }
       } else if (qi < N) {
         const float inv = 1.0f / psum;

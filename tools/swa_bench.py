@@ -16,7 +16,10 @@ for H, heads, shift in [(28, 6, 0), (28, 6, 3), (14, 12, 3), (7, 24, 0)]:
     C = heads * 32
     qkv = torch.randn(B, H, H, 3 * C, device="cuda").to(torch.bfloat16)
     bias = ops.swin_attn_bias(torch.randn(169, heads, device="cuda"), heads, 7, H, shift)
-    f = lambda: ops.swin_window_attention(qkv, bias, H, heads, 7, shift)  # noqa: E731
+    if os.environ.get("SWA_Q8") == "1":  # the MX-fp8-emitting form (fp8 stages)
+        f = lambda: ops.swin_window_attention_q8(qkv, bias, H, heads, 7, shift)  # noqa: E731
+    else:
+        f = lambda: ops.swin_window_attention(qkv, bias, H, heads, 7, shift)  # noqa: E731
     f()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
