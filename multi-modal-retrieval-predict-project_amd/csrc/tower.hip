@@ -275,8 +275,10 @@ __global__ __launch_bounds__(256) void swin_attn_bias(const float* __restrict__ 
 // head's 32 dims are one 32-block: the lane pair (r, r + 32) holds them, one lane swap for the
 // amax), bit-identical to mmr_quantize_mxfp8(out, kp); the K padding C..kp is written by the last
 // head's waves (zero bytes, zero scale bytes).
+// 4 waves per SIMD: without the bound hipcc kept the MFMA results in AGPRs and allocated 140-146
+// registers (3 waves); with it 110 VGPRs, no AGPRs, no spills
 template <bool Q8 = false>
-__global__ __launch_bounds__(256) void swin_window_attention(const uint16_t* __restrict__ qkv,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void swin_window_attention(const uint16_t* __restrict__ qkv,
                                                              const float* __restrict__ bias,
                                                              uint16_t* __restrict__ out,
                                                              int64_t units, int H, int C,

@@ -23,7 +23,7 @@ def timeit(fn, iters=20):
     return e0.elapsed_time(e1) / iters * 1e3
 
 
-B, h, D = 256, 8, 768
+B, h, D = int(os.environ.get("MHA_B", "256")), 8, int(os.environ.get("MHA_D", "768"))  # cfg5: MHA_D=1024 (dh 128)
 dh = D // h
 shapes = ((128, 128), (49, 49), (128, 49), (49, 128), (51, 51))
 if len(sys.argv) > 2:  # one shape: python tools/mha_bench.py LQ LK
