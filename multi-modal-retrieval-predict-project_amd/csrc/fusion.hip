@@ -40,9 +40,10 @@ constexpr int MHA_KB = 128;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 // occupancy targets (waves per SIMD; without them hipcc splits o into AGPRs and lands at 2 / 1):
-// head_dim <= 32 -> 4, <= 96 -> 3 (BERT 64, fusion 96), 128 unmasked -> 3 (168 VGPRs, no spill), else 2
+// head_dim <= 32 -> 4, <= 96 -> 3 (BERT 64, fusion 96), else 2 (128 unmasked at 3: 168 VGPRs, no spill, but
+// measured neutral to 4 % slower, profiles/r03_s5_attn_occupancy_ab.txt)
 template <int DT, bool MASK>
-__global__ __launch_bounds__(256, DT == 1 ? 4 : (DT <= 3 || (DT == 4 && !MASK) ? 3 : 2)) void mha_small(const uint16_t* __restrict__ q, int64_t ldq,
+__global__ __launch_bounds__(256, DT == 1 ? 4 : (DT <= 3 ? 3 : 2)) void mha_small(const uint16_t* __restrict__ q, int64_t ldq,
                                                  const uint16_t* __restrict__ k, int64_t ldk,
                                                  const uint16_t* __restrict__ v, int64_t ldv,
                                                  uint16_t* __restrict__ out, int64_t ldo,
