@@ -427,6 +427,54 @@ mmr_status mmr_assemble_seq_q8(const float* x1, const uint16_t* patches_fused, c
 /* y (b, c) f32 = x[i*ldx + 0..c) (bf16 rows, e.g. the CLS token of each sequence). */
 mmr_status mmr_rows_to_f32(const uint16_t* x, int64_t ldx, float* y, int32_t b, int32_t c, void* stream);
 
+/* ---------------------------------------------------------------- fp32-faithful tower mode ("x3") */
+/* The towers and the multimodal head with f32 activations and every contraction on bf16 MFMA with
+ * three-term splits (a = a_hi + a_lo, a.b ~= a_hi.b_hi + a_hi.b_lo + a_lo.b_hi in f32, ~2^-17
+ * relative per product); LayerNorm / softmax (expf) / GELU (erff) / means in f32.  The reference runs
+ * the same towers in fp32 (src/Model/fusion.py:198-199, 322-325; model.py:365-479): this mode holds the
+ * end-to-end lists to BASELINE.md §3's bar.  All activations f32. */
+
+/* y = act(x @ W^T + bias) (+ residual) for any m: x (m, k) rows at stride ldx, W given as its bf16
+ * split w_hi = bf16(W), w_lo = bf16(W - w_hi) ([n][k] each, contiguous); act 0 none, 1 GELU(erf).
+ * k % 32 == 0; residual may alias y. */
+mmr_status mmr_x3_linear(const float* x, int64_t ldx, const uint16_t* w_hi, const uint16_t* w_lo, const float* bias,
+                         const float* residual, int64_t ldr, float* y, int64_t ldy, int64_t m, int32_t n, int32_t k,
+                         int32_t act, void* stream);
+/* Attention core (nn.MultiheadAttention / BERT self-attention, eval): per (batch, head)
+ * softmax(q k^T * scale (+ key mask)) v; rows as mmr_mha (q row bi*lq + i at q + row*ldq + head*dh);
+ * mask01 (b, lk) int64 or NULL (0 -> key excluded, HF's additive finfo.min); out (b*lq, ldo) and/or
+ * mean_out (b, heads*dh) = mean over the lq query rows (deterministic).  dh % 8 == 0, dh <= 128. */
+mmr_status mmr_x3_attention(const float* q, int64_t ldq, const float* k, int64_t ldk, const float* v, int64_t ldv,
+                            float* out, int64_t ldo, float* mean_out, const int64_t* mask01, int32_t b, int32_t lq,
+                            int32_t lk, int32_t heads, int32_t dh, float scale, void* stream);
+/* Swin (shifted-)window attention as mmr_swin_window_attention on f32 qkv (b*hw*hw, 3c) -> out
+ * (b*hw*hw, c), q scaled by dh^-0.5 before q k^T (timm), bias from mmr_swin_attn_bias.  head_dim <= 32. */
+mmr_status mmr_x3_swin_window_attention(const float* qkv, const float* bias, float* out, int32_t b, int32_t hw,
+                                        int32_t c, int32_t heads, int32_t ws, int32_t shift, void* stream);
+/* Patch-embed im2col, f32: (b, cin, hw, hw) -> (b*(hw/patch)^2, kp) columns (k = c*p^2 + ky*p + kx, zero
+ * for k >= cin*p^2). */
+mmr_status mmr_x3_patch_im2col(const float* image, float* cols, int32_t b, int32_t cin, int32_t hw, int32_t patch,
+                               int32_t kp, void* stream);
+/* PatchMerging gather (timm order) + LayerNorm(4c), f32 in / out; 4c <= 4096. */
+mmr_status mmr_x3_patch_merge_ln(const float* x, const float* gamma, const float* beta, float* y, int32_t b,
+                                 int32_t hw, int32_t c, float eps, void* stream);
+/* BERT embeddings LN((word[id] + type[0]) + pos[l]) -> f32 (b*l, c), c <= 1024. */
+mmr_status mmr_x3_bert_embed(const int64_t* ids, const float* word, const float* pos, const float* type0,
+                             const float* gamma, const float* beta, float* y, int32_t b, int32_t l, int32_t c, float eps,
+                             void* stream);
+/* y = x + pos[row % l], f32 (rows, c). */
+mmr_status mmr_x3_add_pos(const float* x, const float* pos, float* y, int64_t rows, int32_t l, int32_t c, void* stream);
+/* seq (b, np+2, c) f32 = [x1; patches_fused; x2] + pe. */
+mmr_status mmr_x3_assemble_seq(const float* x1, const float* patches_fused, const float* x2, const float* pe,
+                               float* seq, int32_t b, int32_t np, int32_t c, void* stream);
+/* y (b, c) = (extra[b] + sum_t x[b][t]) / (l + 1) with extra (b, c), or sum_t x[b][t] / l when extra is
+ * NULL; x (b, l, c) f32, summed in token order (unmasked token mean, model.py:370; the Swin global /
+ * pooled means, fusion.py:263-265, model.py:463-468). */
+mmr_status mmr_x3_mean_rows(const float* x, const float* extra, float* y, int32_t b, int32_t l, int32_t c,
+                            void* stream);
+/* y (b, c) = x[i*ldx + 0..c), f32 (the CLS rows, fusion.py:447). */
+mmr_status mmr_x3_gather_rows(const float* x, int64_t ldx, float* y, int32_t b, int32_t c, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

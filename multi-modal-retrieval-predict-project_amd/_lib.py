@@ -85,6 +85,17 @@ SIGNATURES = {
     "mmr_assemble_seq": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
     "mmr_assemble_seq_q8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
     "mmr_rows_to_f32": [c_vp, c_i64, c_vp, c_i32, c_i32, c_vp],
+    "mmr_x3_linear": [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp],
+    "mmr_x3_attention": [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32,
+                         c_i32, c_f32, c_vp],
+    "mmr_x3_swin_window_attention": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp],
+    "mmr_x3_patch_im2col": [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp],
+    "mmr_x3_patch_merge_ln": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp],
+    "mmr_x3_bert_embed": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp],
+    "mmr_x3_add_pos": [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp],
+    "mmr_x3_assemble_seq": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
+    "mmr_x3_mean_rows": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
+    "mmr_x3_gather_rows": [c_vp, c_i64, c_vp, c_i32, c_i32, c_vp],
 }
 _RESTYPES = {"mmr_last_error": ctypes.c_char_p, "mmr_version": ctypes.c_int, "mmr_max_k": ctypes.c_int,
              "mmr_linear_bf16_variant": ctypes.c_int32, "mmr_linear_rw_parts": ctypes.c_int32,

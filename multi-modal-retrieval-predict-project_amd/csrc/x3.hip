@@ -1,0 +1,712 @@
+// fp32-faithful tower mode ("x3", Backbones(tower_dtype="x3")): the Swin / BERT towers and the
+// multimodal head with f32 activations between kernels and every contraction (linears and both
+// attention products) on bf16 MFMA with three-term splits: a = a_hi + a_lo (a_hi = bf16(a),
+// a_lo = bf16(a - a_hi), |a - a_hi - a_lo| <= 2^-18 |a|), a.b ~= a_hi.b_hi + a_hi.b_lo + a_lo.b_hi
+// summed in f32 (~2^-17 relative per product, f32 accumulation).  Everything else — LayerNorm,
+// softmax (expf), GELU (erff), means — runs in f32 as torch does.  The reference runs these towers
+// in fp32 (src/Model/fusion.py:198-199 timm forward_features, :322-325 BertModel, model.py:365-479
+// heads); this mode exists so the end-to-end lists can be held to BASELINE.md §3's bar (identical
+// top-K up to 1e-6 ties, scores within 1e-4, identical P@10) — the bf16 / MX-fp8 tower modes move
+// embeddings by ~1e-3 and reorder near-ties.
+//
+// Kernels:
+//   x3_gemm        Y = act(X W^T + bias) (+ R), X f32 split in registers while staged to LDS, W
+//                  pre-split (hi / lo bf16 copies made once at load); 128 x 128 tiles, 4 waves of
+//                  64 x 64, K-steps of 32 on v_mfma_f32_16x16x32_bf16 (3 per fragment pair),
+//                  register-prefetched next K-step, XCD-contiguous tile order.
+//   x3_attention   per (sequence or window, head): softmax(q k^T * scale + bias / mask) v, keys in
+//                  LDS chunks of 64 (hi / lo K rows, hi / lo V^T), online softmax (running max and
+//                  sum per query row, expf), P re-split through a wave-private LDS tile; optional
+//                  mean over the query rows (fixed-order reduction, deterministic).  Modes: strided
+//                  rows (nn.MultiheadAttention, BERT with a key-padding mask) and Swin windows (the
+//                  roll + window partition / reverse folded into the token index map, the dense
+//                  rel-pos + shift-mask bias of mmr_swin_attn_bias).
+//   small f32 kernels: patch im2col, PatchMerging gather + LN(4C), BERT embeddings + LN, add-pos,
+//                  fused-sequence assembly, row means, row gather.
+#include <float.h>
+
+#include "common.h"
+
+namespace {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// f32 x4 -> (hi, lo) bf16 x4 each, packed as two dwords
+__device__ __forceinline__ void split4(const float4 v, uint2& hi, uint2& lo) {
+  const uint32_t h0 = mmr::pack2bf(v.x, v.y), h1 = mmr::pack2bf(v.z, v.w);
+  const float r0 = v.x - __uint_as_float(h0 << 16), r1 = v.y - __uint_as_float(h0 & 0xFFFF0000u);
+  const float r2 = v.z - __uint_as_float(h1 << 16), r3 = v.w - __uint_as_float(h1 & 0xFFFF0000u);
+  hi = make_uint2(h0, h1);
+  lo = make_uint2(mmr::pack2bf(r0, r1), mmr::pack2bf(r2, r3));
+}
+
+__device__ __forceinline__ void split8(const float4 a, const float4 b, bf16x8& hi, bf16x8& lo) {
+  uint2 h0, l0, h1, l1;
+  split4(a, h0, l0);
+  split4(b, h1, l1);
+  hi = __builtin_bit_cast(bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
+  lo = __builtin_bit_cast(bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
+}
+
+__device__ __forceinline__ f32x4 mfma3(const bf16x8 ah, const bf16x8 al, const bf16x8 bh, const bf16x8 bl, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc, 0, 0, 0);
+}
+
+// GELU exactly as torch's default (erf form), ocml erff
+__device__ __forceinline__ float gelu_exact(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+// ------------------------------------------------------------------ GEMM
+constexpr int GX_BM = 128, GX_BN = 128, GX_BK = 32, GX_LD = 40;  // LDS row stride 80 B: conflict-free 16-B reads
+
+template <int ACT, bool BIAS, bool RES>
+__global__ __launch_bounds__(256, 2) void x3_gemm(const float* __restrict__ X, int64_t ldx,
+                                                  const uint16_t* __restrict__ Wh, const uint16_t* __restrict__ Wl,
+                                                  const float* __restrict__ bias, const float* R, int64_t ldr,
+                                                  float* Y, int64_t ldy, int M, int N, int K, int tiles_n,
+                                                  int ntiles) {
+  __shared__ __attribute__((aligned(16))) uint16_t sAh[GX_BM * GX_LD], sAl[GX_BM * GX_LD];
+  __shared__ __attribute__((aligned(16))) uint16_t sBh[GX_BN * GX_LD], sBl[GX_BN * GX_LD];
+  const int tile = mmr::xcd_contiguous((int)blockIdx.x, ntiles);
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int m0 = tm * GX_BM, n0 = tn * GX_BN;
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int r = lane & 15, g = lane >> 4;
+  // staging: thread -> (row t / 2, 16 k from 16 (t % 2)); rows past M / N clamped (loaded, never stored)
+  const int srow = t >> 1, sk = (t & 1) * 16;
+  const int xr = m0 + srow < M ? m0 + srow : M - 1, wr = n0 + srow < N ? n0 + srow : N - 1;
+  const float* xp = X + (int64_t)xr * ldx + sk;
+  const uint16_t* whp = Wh + (int64_t)wr * K + sk;
+  const uint16_t* wlp = Wl + (int64_t)wr * K + sk;
+  float4 xv[4];
+  uint4 wv[4];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xv[j] = *(const float4*)(xp + k0 + 4 * j);
+    wv[0] = *(const uint4*)(whp + k0);
+    wv[1] = *(const uint4*)(whp + k0 + 8);
+    wv[2] = *(const uint4*)(wlp + k0);
+    wv[3] = *(const uint4*)(wlp + k0 + 8);
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int nk = K / GX_BK;
+  gload(0);
+  for (int kt = 0; kt < nk; ++kt) {
+    __syncthreads();  // every wave done reading the previous K-step
+    {
+      uint2 h[4], l[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) split4(xv[j], h[j], l[j]);
+      uint16_t* ah = sAh + srow * GX_LD + sk;
+      uint16_t* al = sAl + srow * GX_LD + sk;
+      *(uint4*)ah = make_uint4(h[0].x, h[0].y, h[1].x, h[1].y);
+      *(uint4*)(ah + 8) = make_uint4(h[2].x, h[2].y, h[3].x, h[3].y);
+      *(uint4*)al = make_uint4(l[0].x, l[0].y, l[1].x, l[1].y);
+      *(uint4*)(al + 8) = make_uint4(l[2].x, l[2].y, l[3].x, l[3].y);
+      *(uint4*)(sBh + srow * GX_LD + sk) = wv[0];
+      *(uint4*)(sBh + srow * GX_LD + sk + 8) = wv[1];
+      *(uint4*)(sBl + srow * GX_LD + sk) = wv[2];
+      *(uint4*)(sBl + srow * GX_LD + sk + 8) = wv[3];
+    }
+    __syncthreads();
+    if (kt + 1 < nk) gload((kt + 1) * GX_BK);  // next K-step in flight under this one's MFMAs
+    bf16x8 bh[4], bl[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int row = wn * 64 + 16 * n + r;
+      bh[n] = *(const bf16x8*)(sBh + row * GX_LD + 8 * g);
+      bl[n] = *(const bf16x8*)(sBl + row * GX_LD + 8 * g);
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int row = wm * 64 + 16 * m + r;
+      const bf16x8 ah = *(const bf16x8*)(sAh + row * GX_LD + 8 * g);
+      const bf16x8 al = *(const bf16x8*)(sAl + row * GX_LD + 8 * g);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = mfma3(ah, al, bh[n], bl[n], acc[m][n]);
+    }
+  }
+  // lane (r, g): rows 16 m + 4 g + i, column 16 n + r of the wave's 64 x 64 block
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int col = n0 + wn * 64 + 16 * n + r;
+    if (col >= N) continue;
+    const float bv = BIAS ? bias[col] : 0.f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wm * 64 + 16 * m + 4 * g + i;
+        if (row >= M) continue;
+        float v = acc[m][n][i];
+        if (BIAS) v += bv;
+        if (ACT == 1) v = gelu_exact(v);
+        if (RES) v += R[(int64_t)row * ldr + col];
+        Y[(int64_t)row * ldy + col] = v;
+      }
+  }
+}
+
+// ------------------------------------------------------------------ attention
+// Workgroup = (sequence / window bb, head); 4 waves, wave w owns query tiles of 16 rows (w + 4 j);
+// keys in chunks of 64 staged in LDS as hi / lo K rows [key][DH + 8] and hi / lo V^T rows
+// [d][64 + 8]; head dims padded to DH = 32 DT with zeros (dh % 8 == 0).
+// S (16 x 64 per wave): lane (r, g) holds S[4 g + i][16 n + r]; P goes back through a wave-private
+// hi / lo LDS tile [16][64 + 8] as the A operand of O += P V (lane holds O[4 g + i][16 nd + r]).
+struct AttnArgs {
+  const float* q;
+  int64_t ldq;
+  const float* k;
+  int64_t ldk;
+  const float* v;
+  int64_t ldv;
+  float* out;
+  int64_t ldo;
+  float* mean_out;
+  const int64_t* kmask;
+  const float* bias;  // Swin: [types][heads][64][64]
+  int lq, lk, heads, dh;
+  float scale;
+  int hw, ws, shift;  // Swin windows
+};
+
+template <int DT, bool SWIN>
+__global__ __launch_bounds__(256) void x3_attention(const AttnArgs a) {
+  constexpr int DH = 32 * DT, KLD = DH + 8, VLD = 72;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint16_t* sKh = (uint16_t*)smem;
+  uint16_t* sKl = sKh + 64 * KLD;
+  uint16_t* sVh = sKl + 64 * KLD;
+  uint16_t* sVl = sVh + DH * VLD;
+  uint16_t* sPh = sVl + DH * VLD;    // [4 waves][16][VLD]
+  uint16_t* sPl = sPh + 4 * 16 * VLD;
+  float* sMean = (float*)(sPl + 4 * 16 * VLD);  // [4][DH]
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const int r = lane & 15, g = lane >> 4;
+  const int head = (int)(blockIdx.x % (unsigned)a.heads);
+  const int64_t bb = blockIdx.x / (unsigned)a.heads;
+  const int lq = a.lq, lk = a.lk, dh = a.dh;
+  // token maps
+  int64_t sw_base = 0;
+  int wy = 0, wx = 0, type = 0, nwin1 = 1;
+  if constexpr (SWIN) {
+    nwin1 = a.hw / a.ws;
+    const int nwin = nwin1 * nwin1;
+    const int win = (int)(bb % nwin);
+    sw_base = (bb / nwin) * (int64_t)a.hw * a.hw;
+    wy = win / nwin1;
+    wx = win % nwin1;
+    type = a.shift > 0 ? ((wy == nwin1 - 1) ? 2 : 0) + ((wx == nwin1 - 1) ? 1 : 0) : 0;
+  }
+  auto qtok = [&](int i) -> int64_t {
+    if constexpr (SWIN) {
+      const int hr = wy * a.ws + i / a.ws, wr = wx * a.ws + i % a.ws;
+      return sw_base + (int64_t)((hr + a.shift) % a.hw) * a.hw + (wr + a.shift) % a.hw;
+    } else {
+      return bb * lq + i;
+    }
+  };
+  auto ktok = [&](int j) -> int64_t {
+    if constexpr (SWIN) return qtok(j);
+    else return bb * lk + j;
+  };
+  const float* qb = a.q + head * dh;
+  const float* kb = a.k + head * dh;
+  const float* vb = a.v + head * dh;
+  float macc[2 * DT];
+#pragma unroll
+  for (int nd = 0; nd < 2 * DT; ++nd) macc[nd] = 0.f;
+  uint16_t* pH = sPh + wave * 16 * VLD;
+  uint16_t* pL = sPl + wave * 16 * VLD;
+  for (int q0 = 0; q0 < lq; q0 += 64) {
+    const int qbase = q0 + wave * 16;
+    bf16x8 qh[DT], ql[DT];
+    {
+      const int qi = qbase + r < lq ? qbase + r : lq - 1;
+      const float* qp = qb + qtok(qi) * a.ldq;
+#pragma unroll
+      for (int ks = 0; ks < DT; ++ks) {
+        const int d = 32 * ks + 8 * g;
+        const int dc = d < dh ? d : 0;  // clamped, masked below
+        float4 x0 = *(const float4*)(qp + dc), x1 = *(const float4*)(qp + dc + 4);
+        if (d >= dh) x0 = x1 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (SWIN) {  // timm scales q before q k^T
+          x0 = make_float4(x0.x * a.scale, x0.y * a.scale, x0.z * a.scale, x0.w * a.scale);
+          x1 = make_float4(x1.x * a.scale, x1.y * a.scale, x1.z * a.scale, x1.w * a.scale);
+        }
+        split8(x0, x1, qh[ks], ql[ks]);
+      }
+    }
+    float mrow[4], lrow[4];
+    f32x4 o[2 * DT];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      mrow[i] = -INFINITY;
+      lrow[i] = 0.f;
+    }
+#pragma unroll
+    for (int nd = 0; nd < 2 * DT; ++nd) o[nd] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int kc = 0; kc < lk; kc += 64) {
+      __syncthreads();  // every wave done with the previous chunk's K / V
+      for (int e = t; e < 64 * (DH / 4); e += 256) {
+        const int key = e / (DH / 4), d4 = e % (DH / 4), d = 4 * d4;
+        const int j = kc + key < lk ? kc + key : lk - 1;
+        const int64_t tk = ktok(j);
+        const int dc = d < dh ? d : 0;
+        float4 kv = *(const float4*)(kb + tk * a.ldk + dc);
+        float4 vv = *(const float4*)(vb + tk * a.ldv + dc);
+        if (d >= dh) kv = vv = make_float4(0.f, 0.f, 0.f, 0.f);
+        uint2 h, l;
+        split4(kv, h, l);
+        *(uint2*)(sKh + key * KLD + d) = h;
+        *(uint2*)(sKl + key * KLD + d) = l;
+        split4(vv, h, l);
+        sVh[(d + 0) * VLD + key] = (uint16_t)(h.x & 0xFFFF);
+        sVh[(d + 1) * VLD + key] = (uint16_t)(h.x >> 16);
+        sVh[(d + 2) * VLD + key] = (uint16_t)(h.y & 0xFFFF);
+        sVh[(d + 3) * VLD + key] = (uint16_t)(h.y >> 16);
+        sVl[(d + 0) * VLD + key] = (uint16_t)(l.x & 0xFFFF);
+        sVl[(d + 1) * VLD + key] = (uint16_t)(l.x >> 16);
+        sVl[(d + 2) * VLD + key] = (uint16_t)(l.y & 0xFFFF);
+        sVl[(d + 3) * VLD + key] = (uint16_t)(l.y >> 16);
+      }
+      __syncthreads();
+      f32x4 s[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        s[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < DT; ++ks) {
+          const bf16x8 khv = *(const bf16x8*)(sKh + (16 * n + r) * KLD + 32 * ks + 8 * g);
+          const bf16x8 klv = *(const bf16x8*)(sKl + (16 * n + r) * KLD + 32 * ks + 8 * g);
+          s[n] = mfma3(qh[ks], ql[ks], khv, klv, s[n]);
+        }
+      }
+      // scale / bias / mask, then the online softmax update per query row 4 g + i
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int key = kc + 16 * n + r;
+        bool valid = key < lk;
+        if (!SWIN && a.kmask) valid = valid && a.kmask[bb * lk + (valid ? key : 0)] != 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float x = s[n][i];
+          if constexpr (SWIN) {
+            const int qi = qbase + 4 * g + i;
+            x += a.bias[(((int64_t)type * a.heads + head) * 64 + (qi < 64 ? qi : 63)) * 64 + (key < 64 ? key : 63)];
+          } else {
+            x *= a.scale;
+          }
+          s[n][i] = valid ? x : -INFINITY;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float cm = fmaxf(fmaxf(s[0][i], s[1][i]), fmaxf(s[2][i], s[3][i]));
+#pragma unroll
+        for (int m = 1; m < 16; m <<= 1) cm = fmaxf(cm, __shfl_xor(cm, m, 64));
+        const float mnew = fmaxf(mrow[i], cm);
+        float corr = 1.f, ps = 0.f;
+        if (mnew != -INFINITY) {
+          corr = mrow[i] == -INFINITY ? 0.f : expf(mrow[i] - mnew);
+#pragma unroll
+          for (int n = 0; n < 4; ++n) {
+            const float p = s[n][i] == -INFINITY ? 0.f : expf(s[n][i] - mnew);
+            s[n][i] = p;
+            ps += p;
+          }
+        } else {
+#pragma unroll
+          for (int n = 0; n < 4; ++n) s[n][i] = 0.f;
+        }
+#pragma unroll
+        for (int m = 1; m < 16; m <<= 1) ps += __shfl_xor(ps, m, 64);
+        lrow[i] = lrow[i] * corr + ps;
+        mrow[i] = mnew;
+#pragma unroll
+        for (int nd = 0; nd < 2 * DT; ++nd) o[nd][i] *= corr;
+      }
+      // P (f32) -> hi / lo through the wave's LDS tile
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = s[n][i];
+          const uint16_t h = mmr::f2bf(p);
+          const uint16_t l = mmr::f2bf(p - mmr::bf2f(h));
+          pH[(4 * g + i) * VLD + 16 * n + r] = h;
+          pL[(4 * g + i) * VLD + 16 * n + r] = l;
+        }
+      __syncthreads();
+#pragma unroll
+      for (int ks2 = 0; ks2 < 2; ++ks2) {
+        const bf16x8 pah = *(const bf16x8*)(pH + r * VLD + 32 * ks2 + 8 * g);
+        const bf16x8 pal = *(const bf16x8*)(pL + r * VLD + 32 * ks2 + 8 * g);
+#pragma unroll
+        for (int nd = 0; nd < 2 * DT; ++nd) {
+          const bf16x8 vbh = *(const bf16x8*)(sVh + (16 * nd + r) * VLD + 32 * ks2 + 8 * g);
+          const bf16x8 vbl = *(const bf16x8*)(sVl + (16 * nd + r) * VLD + 32 * ks2 + 8 * g);
+          o[nd] = mfma3(pah, pal, vbh, vbl, o[nd]);
+        }
+      }
+    }
+    // finalise this query tile: O / l (a row with every key masked -> 0)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int qi = qbase + 4 * g + i;
+      const float inv = lrow[i] > 0.f ? 1.0f / lrow[i] : 0.f;
+      const bool ok = qi < lq;
+      float* orow = a.out ? a.out + qtok(ok ? qi : 0) * a.ldo + head * dh : nullptr;
+#pragma unroll
+      for (int nd = 0; nd < 2 * DT; ++nd) {
+        const int d = 16 * nd + r;
+        const float val = o[nd][i] * inv;
+        if (ok) {
+          if (orow && d < dh) orow[d] = val;
+          macc[nd] += val;
+        }
+      }
+    }
+  }
+  if (a.mean_out) {
+#pragma unroll
+    for (int nd = 0; nd < 2 * DT; ++nd) {
+      float v = macc[nd];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (g == 0) sMean[wave * DH + 16 * nd + r] = v;
+    }
+    __syncthreads();
+    if (t < dh) {
+      const float s4 = ((sMean[t] + sMean[DH + t]) + sMean[2 * DH + t]) + sMean[3 * DH + t];
+      a.mean_out[bb * (int64_t)a.heads * dh + head * dh + t] = s4 / lq;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ small f32 kernels
+// im2col of the patch-embed conv: (b, cin, hw, hw) -> (b * g * g, kp) f32, k = c p^2 + ky p + kx,
+// zero for k >= cin p^2
+__global__ __launch_bounds__(256) void x3_im2col(const float* __restrict__ img, float* __restrict__ cols, int64_t ntok,
+                                                 int cin, int hw, int patch, int kp) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= ntok * kp) return;
+  const int64_t tk = idx / kp;
+  const int k = (int)(idx % kp);
+  const int gg = hw / patch;
+  const int64_t bi = tk / (gg * gg);
+  const int py = (int)((tk / gg) % gg), px = (int)(tk % gg);
+  float val = 0.f;
+  if (k < cin * patch * patch) {
+    const int c = k / (patch * patch), ky = (k / patch) % patch, kx = k % patch;
+    val = img[((bi * cin + c) * hw + (py * patch + ky)) * (int64_t)hw + px * patch + kx];
+  }
+  cols[idx] = val;
+}
+
+// One wave per merged row: gather [x(2i,2j), x(2i+1,2j), x(2i,2j+1), x(2i+1,2j+1)] (timm order),
+// LayerNorm over 4c (two-pass, centred), f32 out.  4c <= 4096.
+__global__ __launch_bounds__(256) void x3_patch_merge_ln(const float* __restrict__ x, const float* __restrict__ gm,
+                                                         const float* __restrict__ bt, float* __restrict__ y,
+                                                         int64_t nout, int hw, int c, float eps) {
+  const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (o >= nout) return;
+  const int h2 = hw / 2;
+  const int64_t bi = o / (h2 * h2);
+  const int i = (int)((o / h2) % h2), j = (int)(o % h2);
+  const int c4 = 4 * c;
+  float v[64];
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 64; ++e) {
+    const int k = lane + 64 * e;
+    v[e] = 0.f;
+    if (k < c4) {
+      const int p = k / c, off = k % c;
+      const int yy = 2 * i + (p & 1), xx = 2 * j + (p >> 1);
+      v[e] = x[((bi * hw + yy) * hw + xx) * (int64_t)c + off];
+      s += v[e];
+    }
+  }
+  const float mean = mmr::wave_sum(s) / c4;
+  float ss = 0.f;
+#pragma unroll
+  for (int e = 0; e < 64; ++e)
+    if (lane + 64 * e < c4) ss += (v[e] - mean) * (v[e] - mean);
+  const float rstd = 1.0f / sqrtf(mmr::wave_sum(ss) / c4 + eps);
+#pragma unroll
+  for (int e = 0; e < 64; ++e) {
+    const int k = lane + 64 * e;
+    if (k < c4) y[o * c4 + k] = (v[e] - mean) * rstd * gm[k] + bt[k];
+  }
+}
+
+// HF BertEmbeddings: LN(word[id] + pos[l] + type[0]) -> f32 (one wave per token, c <= 1024)
+__global__ __launch_bounds__(256) void x3_bert_embed(const int64_t* __restrict__ ids, const float* __restrict__ word,
+                                                     const float* __restrict__ pos, const float* __restrict__ type0,
+                                                     const float* __restrict__ gm, const float* __restrict__ bt,
+                                                     float* __restrict__ y, int64_t ntok, int l, int c, float eps) {
+  const int64_t tk = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (tk >= ntok) return;
+  const float* wr = word + ids[tk] * (int64_t)c;
+  const float* pr = pos + (int64_t)(tk % l) * c;
+  float v[16];
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int k = lane + 64 * e;
+    v[e] = 0.f;
+    if (k < c) {
+      v[e] = (wr[k] + type0[k]) + pr[k];  // HF: inputs_embeds + token_type_embeddings, then + position
+      s += v[e];
+    }
+  }
+  const float mean = mmr::wave_sum(s) / c;
+  float ss = 0.f;
+#pragma unroll
+  for (int e = 0; e < 16; ++e)
+    if (lane + 64 * e < c) ss += (v[e] - mean) * (v[e] - mean);
+  const float rstd = 1.0f / sqrtf(mmr::wave_sum(ss) / c + eps);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int k = lane + 64 * e;
+    if (k < c) y[tk * c + k] = (v[e] - mean) * rstd * gm[k] + bt[k];
+  }
+}
+
+// y = x + pos[row % l] (f32)
+__global__ __launch_bounds__(256) void x3_add_pos(const float* __restrict__ x, const float* __restrict__ pos,
+                                                  float* __restrict__ y, int64_t rows, int l, int c) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * c) return;
+  const int64_t row = i / c;
+  y[i] = x[i] + pos[(row % l) * c + i % c];
+}
+
+// seq (b, np + 2, c) = [x1; pf; x2] + pe (f32)
+__global__ __launch_bounds__(256) void x3_assemble_seq(const float* __restrict__ x1, const float* __restrict__ pf,
+                                                       const float* __restrict__ x2, const float* __restrict__ pe,
+                                                       float* __restrict__ seq, int nb, int np, int c) {
+  const int ls = np + 2;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)nb * ls * c) return;
+  const int ch = (int)(i % c);
+  const int64_t row = i / c;
+  const int tt = (int)(row % ls);
+  const int64_t bi = row / ls;
+  float v;
+  if (tt == 0) v = x1[bi * c + ch];
+  else if (tt == ls - 1) v = x2[bi * c + ch];
+  else v = pf[(bi * np + tt - 1) * c + ch];
+  seq[i] = v + pe[(int64_t)tt * c + ch];
+}
+
+// y[b][ch] = (extra[b][ch] + sum_t x[b][t][ch]) / (l + has_extra), summed in token order
+__global__ __launch_bounds__(256) void x3_mean_rows(const float* __restrict__ x, const float* __restrict__ extra,
+                                                    float* __restrict__ y, int l, int c) {
+  const int bi = blockIdx.y;
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= c) return;
+  const float* xr = x + (int64_t)bi * l * c + k;
+  float s = 0.f;
+  for (int tt = 0; tt < l; ++tt) s += xr[(int64_t)tt * c];
+  if (extra) y[(int64_t)bi * c + k] = (extra[(int64_t)bi * c + k] + s) / (l + 1);
+  else y[(int64_t)bi * c + k] = s / l;
+}
+
+// y[b][:] = x[b * ldx + 0..c)
+__global__ __launch_bounds__(256) void x3_gather_rows(const float* __restrict__ x, int64_t ldx, float* __restrict__ y,
+                                                      int nb, int c) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)nb * c) return;
+  y[i] = x[(i / c) * ldx + (i % c)];
+}
+
+bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+mmr_status launch_attention(const char* who, AttnArgs a, int64_t nbh, bool swin, void* stream) {
+  MMR_REQUIRE(a.q && a.k && a.v && (a.out || a.mean_out), "%s: NULL pointer", who);
+  MMR_REQUIRE(a.lq > 0 && a.lk > 0 && a.heads > 0 && a.dh > 0 && a.dh % 8 == 0 && a.dh <= 128,
+              "%s: bad shape lq=%d lk=%d heads=%d dh=%d (dh %% 8 == 0, <= 128)", who, a.lq, a.lk, a.heads, a.dh);
+  MMR_REQUIRE(a.ldq % 4 == 0 && a.ldk % 4 == 0 && a.ldv % 4 == 0 && al16(a.q) && al16(a.k) && al16(a.v) &&
+                  (((int64_t)a.heads * a.dh) <= a.ldq),
+              "%s: rows must be 16-B aligned with strides >= heads*dh", who);
+  if (nbh == 0) return MMR_OK;
+  const int dt = (a.dh + 31) / 32;
+  const int DH = 32 * dt;
+  const size_t lds = (size_t)2 * 64 * (DH + 8) * 2 + (size_t)2 * DH * 72 * 2 + (size_t)2 * 4 * 16 * 72 * 2 +
+                     (size_t)4 * DH * 4;
+  const dim3 grid((unsigned)nbh);
+  hipStream_t st = mmr::as_stream(stream);
+  if (swin) {
+    MMR_REQUIRE(dt == 1, "%s: Swin head_dim %d must be <= 32", who, a.dh);
+    x3_attention<1, true><<<grid, 256, lds, st>>>(a);
+  } else {
+    switch (dt) {
+      case 1: x3_attention<1, false><<<grid, 256, lds, st>>>(a); break;
+      case 2: x3_attention<2, false><<<grid, 256, lds, st>>>(a); break;
+      case 3: x3_attention<3, false><<<grid, 256, lds, st>>>(a); break;
+      default: x3_attention<4, false><<<grid, 256, lds, st>>>(a); break;
+    }
+  }
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+}  // namespace
+
+// ================================================================== C ABI
+extern "C" {
+
+mmr_status mmr_x3_linear(const float* x, int64_t ldx, const uint16_t* w_hi, const uint16_t* w_lo, const float* bias,
+                         const float* residual, int64_t ldr, float* y, int64_t ldy, int64_t m, int32_t n, int32_t k,
+                         int32_t act, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && w_hi && w_lo && y && m >= 0 && n > 0 && k > 0, "mmr_x3_linear: bad arguments");
+  MMR_REQUIRE(k % 32 == 0 && ldx >= k && ldx % 4 == 0 && ldy >= n && (!residual || ldr >= n),
+              "mmr_x3_linear: k=%d must be a multiple of 32 (ldx=%lld ldy=%lld)", k, (long long)ldx, (long long)ldy);
+  MMR_REQUIRE(al16(x) && al16(w_hi) && al16(w_lo), "mmr_x3_linear: x / w must be 16-B aligned");
+  MMR_REQUIRE(act == 0 || act == 1, "mmr_x3_linear: act=%d", act);
+  MMR_REQUIRE(m < (int64_t(1) << 31), "mmr_x3_linear: m=%lld too large", (long long)m);
+  if (m == 0) return MMR_OK;
+  const int tiles_n = (int)mmr::ceil_div(n, GX_BN);
+  const int64_t ntiles = mmr::ceil_div(m, GX_BM) * tiles_n;
+  MMR_REQUIRE(ntiles < (int64_t(1) << 31), "mmr_x3_linear: too many tiles");
+  const dim3 grid((unsigned)ntiles);
+  hipStream_t st = mmr::as_stream(stream);
+  const bool hb = bias != nullptr, hr = residual != nullptr;
+#define X3G(A, B_, R_)                                                                                    \
+  x3_gemm<A, B_, R_><<<grid, 256, 0, st>>>(x, ldx, w_hi, w_lo, bias, residual, ldr, y, ldy, (int)m, n, k, \
+                                           tiles_n, (int)ntiles)
+  if (act == 1) {
+    if (hb && hr) X3G(1, true, true);
+    else if (hb) X3G(1, true, false);
+    else if (hr) X3G(1, false, true);
+    else X3G(1, false, false);
+  } else {
+    if (hb && hr) X3G(0, true, true);
+    else if (hb) X3G(0, true, false);
+    else if (hr) X3G(0, false, true);
+    else X3G(0, false, false);
+  }
+#undef X3G
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_x3_attention(const float* q, int64_t ldq, const float* k, int64_t ldk, const float* v, int64_t ldv,
+                            float* out, int64_t ldo, float* mean_out, const int64_t* mask01, int32_t b, int32_t lq,
+                            int32_t lk, int32_t heads, int32_t dh, float scale, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(b >= 0, "mmr_x3_attention: b=%d", b);
+  MMR_REQUIRE(!out || ldo >= (int64_t)heads * dh, "mmr_x3_attention: ldo below heads*dh");
+  AttnArgs a{q, ldq, k, ldk, v, ldv, out, ldo, mean_out, mask01, nullptr, lq, lk, heads, dh, scale, 0, 1, 0};
+  return launch_attention("mmr_x3_attention", a, (int64_t)b * heads, false, stream);
+}
+
+mmr_status mmr_x3_swin_window_attention(const float* qkv, const float* bias, float* out, int32_t b, int32_t hw,
+                                        int32_t c, int32_t heads, int32_t ws, int32_t shift, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(qkv && bias && out && b >= 0 && hw > 0 && ws > 0 && hw % ws == 0 && ws * ws <= 64 && heads > 0 &&
+                  c % heads == 0 && shift >= 0 && shift < ws,
+              "mmr_x3_swin_window_attention: bad shape hw=%d ws=%d c=%d heads=%d shift=%d", hw, ws, c, heads, shift);
+  const int dh = c / heads;
+  const int64_t nwin = (int64_t)b * (hw / ws) * (hw / ws);
+  AttnArgs a{qkv,     3 * (int64_t)c, qkv + c, 3 * (int64_t)c, qkv + 2 * c, 3 * (int64_t)c, out, c, nullptr, nullptr,
+             bias,    ws * ws,        ws * ws, heads,          dh,          1.0f / sqrtf((float)dh), hw, ws, shift};
+  return launch_attention("mmr_x3_swin_window_attention", a, nwin * heads, true, stream);
+}
+
+mmr_status mmr_x3_patch_im2col(const float* image, float* cols, int32_t b, int32_t cin, int32_t hw, int32_t patch,
+                               int32_t kp, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(image && cols && b >= 0 && cin > 0 && patch > 0 && hw % patch == 0 && kp >= cin * patch * patch,
+              "mmr_x3_patch_im2col: bad arguments");
+  const int64_t ntok = (int64_t)b * (hw / patch) * (hw / patch);
+  if (ntok == 0) return MMR_OK;
+  x3_im2col<<<dim3((unsigned)mmr::ceil_div(ntok * kp, 256)), 256, 0, mmr::as_stream(stream)>>>(image, cols, ntok, cin,
+                                                                                              hw, patch, kp);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_x3_patch_merge_ln(const float* x, const float* gamma, const float* beta, float* y, int32_t b,
+                                 int32_t hw, int32_t c, float eps, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && gamma && beta && y && b >= 0 && hw % 2 == 0 && c > 0 && 4 * c <= 4096,
+              "mmr_x3_patch_merge_ln: bad arguments (4c <= 4096)");
+  const int64_t nout = (int64_t)b * (hw / 2) * (hw / 2);
+  if (nout == 0) return MMR_OK;
+  x3_patch_merge_ln<<<dim3((unsigned)mmr::ceil_div(nout, 4)), 256, 0, mmr::as_stream(stream)>>>(x, gamma, beta, y, nout,
+                                                                                               hw, c, eps);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_x3_bert_embed(const int64_t* ids, const float* word, const float* pos, const float* type0,
+                             const float* gamma, const float* beta, float* y, int32_t b, int32_t l, int32_t c, float eps,
+                             void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(ids && word && pos && type0 && gamma && beta && y && b >= 0 && l > 0 && c > 0 && c <= 1024,
+              "mmr_x3_bert_embed: bad arguments (c <= 1024)");
+  const int64_t ntok = (int64_t)b * l;
+  if (ntok == 0) return MMR_OK;
+  x3_bert_embed<<<dim3((unsigned)mmr::ceil_div(ntok, 4)), 256, 0, mmr::as_stream(stream)>>>(ids, word, pos, type0, gamma,
+                                                                                           beta, y, ntok, l, c, eps);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_x3_add_pos(const float* x, const float* pos, float* y, int64_t rows, int32_t l, int32_t c,
+                          void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && pos && y && rows >= 0 && l > 0 && c > 0, "mmr_x3_add_pos: bad arguments");
+  if (rows == 0) return MMR_OK;
+  x3_add_pos<<<dim3((unsigned)mmr::ceil_div(rows * c, 256)), 256, 0, mmr::as_stream(stream)>>>(x, pos, y, rows, l, c);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_x3_assemble_seq(const float* x1, const float* patches_fused, const float* x2, const float* pe,
+                               float* seq, int32_t b, int32_t np, int32_t c, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x1 && patches_fused && x2 && pe && seq && b >= 0 && np > 0 && c > 0, "mmr_x3_assemble_seq: bad arguments");
+  if (b == 0) return MMR_OK;
+  const int64_t n = (int64_t)b * (np + 2) * c;
+  x3_assemble_seq<<<dim3((unsigned)mmr::ceil_div(n, 256)), 256, 0, mmr::as_stream(stream)>>>(x1, patches_fused, x2, pe,
+                                                                                             seq, b, np, c);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_x3_mean_rows(const float* x, const float* extra, float* y, int32_t b, int32_t l, int32_t c,
+                            void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && y && b >= 0 && l > 0 && c > 0, "mmr_x3_mean_rows: bad arguments");
+  if (b == 0) return MMR_OK;
+  x3_mean_rows<<<dim3((unsigned)mmr::ceil_div(c, 256), (unsigned)b), 256, 0, mmr::as_stream(stream)>>>(x, extra, y, l,
+                                                                                                      c);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_x3_gather_rows(const float* x, int64_t ldx, float* y, int32_t b, int32_t c, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && y && b >= 0 && c > 0 && ldx >= c, "mmr_x3_gather_rows: bad arguments");
+  if (b == 0) return MMR_OK;
+  x3_gather_rows<<<dim3((unsigned)mmr::ceil_div((int64_t)b * c, 256)), 256, 0, mmr::as_stream(stream)>>>(x, ldx, y, b,
+                                                                                                        c);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+}  // extern "C"

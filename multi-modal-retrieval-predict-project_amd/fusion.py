@@ -60,10 +60,13 @@ def _w8(w):
 class _Enhancer:
     """PreFusionEnhancer weights (fusion.py:20-35)."""
 
-    def __init__(self, sd, p, heads, dev, fp8=False):
+    def __init__(self, sd, p, heads, dev, fp8=False, x3=False):
         C = sd[p + "self_attn.in_proj_weight"].shape[1]
         self.C, self.heads, self.dh = C, heads, C // heads
         self.pos = _f(sd[p + "pos_embed"][0], dev)                       # [max_len][C]
+        if x3:  # fp32-faithful mode: f32 weights split once for the bf16x3 GEMM
+            self.w_in_x3 = ops.X3W(_f(sd[p + "self_attn.in_proj_weight"], dev))
+            self.w_o_x3 = ops.X3W(_f(sd[p + "self_attn.out_proj.weight"], dev))
         self.w_in, self.b_in = _bf(sd[p + "self_attn.in_proj_weight"], dev), _f(sd[p + "self_attn.in_proj_bias"], dev)
         self.w_o, self.b_o = _bf(sd[p + "self_attn.out_proj.weight"], dev), _f(sd[p + "self_attn.out_proj.bias"], dev)
         self.alpha = _f(sd[p + "alpha"].reshape(1), dev)
@@ -94,6 +97,17 @@ class _Enhancer:
             x2 = ops.linear(a, self.w_o, self.b_o)
         return ops.scaled_add_layernorm(X, self.alpha, x2, self.g, self.b, eps, q8=q8)
 
+    def x3(self, x, B, L, eps):
+        """x3 mode: x (B*L, C) f32 -> LN(alpha*(x + pos) + MHA(x + pos)) f32 (B*L, C)."""
+        C = self.C
+        X = ops.x3_add_pos(x, self.pos, L)
+        qkv = ops.x3_linear(X, self.w_in_x3, self.b_in)
+        a = torch.empty_like(X)
+        ops.x3_attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], B, L, L, self.heads, self.dh,
+                         1.0 / math.sqrt(self.dh), out=a)
+        x2 = ops.x3_linear(a, self.w_o_x3, self.b_o)
+        return ops.ln_rows(X, self.g, self.b, eps, alpha=self.alpha, residual=x2)
+
 
 class FusionStack:
     """The multimodal head: num_fusion_layers x CrossModalFusion + combiner (model.py:375-459)."""
@@ -103,6 +117,8 @@ class FusionStack:
         self.device, self.heads, self.eps = dev, num_heads, eps
         fp8 = tower_dtype == "fp8"
         self.fp8 = fp8
+        x3 = tower_dtype == "x3"
+        self.x3 = x3
         n = 1 + max(int(k.split(".")[1]) for k in sd if k.startswith("fusion_layers."))
         self.layers = []
         D = sd["self_attn.in_proj_weight"].shape[1]
@@ -110,8 +126,8 @@ class FusionStack:
         for i in range(n):
             p = f"fusion_layers.{i}."
             g = lambda k: sd[p + k]  # noqa: E731
-            L = {"txt": _Enhancer(sd, p + "txt_self_attn.", num_heads, dev, fp8),
-                 "patch": _Enhancer(sd, p + "img_patch_self_attn.", num_heads, dev, fp8)}
+            L = {"txt": _Enhancer(sd, p + "txt_self_attn.", num_heads, dev, fp8, x3),
+                 "patch": _Enhancer(sd, p + "img_patch_self_attn.", num_heads, dev, fp8, x3)}
             # global enhancer: softmax over ONE key is 1 -> x2 = Wo (Wv x + bv) + bo; with x = G + pos0
             # and the LN input alpha*x + x2 = alpha*G + (Wov G + Wov pos0 + bov + alpha*pos0)
             pg = "img_global_self_attn."
@@ -135,6 +151,12 @@ class FusionStack:
             ki = _fold(wi1[sl[1]], bi1[sl[1]], g("key_img.weight"), g("key_img.bias"))
             vi = _fold(wi1[sl[2]], bi1[sl[2]], g("value_img.weight"), g("value_img.bias"))
             qi = _fold(wi2[sl[0]], bi2[sl[0]], g("query_img.weight"), g("query_img.bias"))
+            if x3:  # the folded token-level weights in f32 (folded in f64), split for bf16x3
+                L["t_x3"] = ops.X3W(_f(torch.cat([qt[0], kt[0], vt[0]]), dev))
+                L["p_x3"] = ops.X3W(_f(torch.cat([ki[0], vi[0], qi[0]]), dev))
+                L["pp_x3"] = ops.X3W(_f(g("img_patch_proj.weight"), dev))
+                L["o2_x3t"] = ops.X3W(_f(g("attn_img2txt.out_proj.weight"), dev))
+                L["default_txt32"] = _f(g("default_txt_token").reshape(1, -1), dev)
             L["t_w"] = _bf(torch.cat([qt[0], kt[0], vt[0]]), dev)
             L["t_b"] = _f(torch.cat([qt[1], kt[1], vt[1]]), dev)
             L["p_w"] = _bf(torch.cat([ki[0], vi[0], qi[0]]), dev)
@@ -163,6 +185,7 @@ class FusionStack:
         # combiner QKV on MX-fp8 (its operand written by the sequence assembly itself)
         self.s_w8 = (_w8(self.s_w) if fp8 and D % 256 == 0 and os.environ.get("MMR_COMB_FP8", "1") != "0"
                      else None)  # MMR_COMB_FP8=0: bf16 combiner QKV (A/B)
+        self.s_x3 = ops.X3W(_f(sd["self_attn.in_proj_weight"], dev)) if x3 else None
         self.s_ow, self.s_ob = _f(sd["self_attn.out_proj.weight"], dev), _f(sd["self_attn.out_proj.bias"], dev)
         self.pe = _f(sd["pos_encoder.pe"][0], dev)
         self.alpha = _f(sd["alpha"].reshape(1), dev)
@@ -211,6 +234,8 @@ class FusionStack:
         Phase 3 (all layers together): sequence assembly, the shared self_attn QKV GEMM over
         nl*B*(Np+2) rows, its attention means and out-projection.
         Phase 4 (sequential): the joint chain (norm1 / alpha, norm2 -> FFN, adapter)."""
+        if self.x3:
+            return self._forward_x3(img_global, img_patches, txt_feats)
         B, Np, Ci = img_patches.shape
         D, h, eps, dev = self.D, self.heads, self.eps, self.device
         nl = len(self.layers)
@@ -284,6 +309,49 @@ class FusionStack:
                 ops.mha(PQ[:, 2 * D:], TQ[:, D:2 * D], TQ[:, 2 * D:], B, Np, Lt, h, dh, sc, out=a2, mean_out=m2[i])
                 ops.linear(a2, L["o2_wb"], L["o2_b"], residual=PP, out=PF[i])  # patches_fused (fusion.py:437)
         del pq, pp
+        return self._finish(G, m1, m2, cls, PF, B, Np, Ci)
+
+    def _forward_x3(self, img_global, img_patches, txt_feats):
+        """Phase 1 of forward in the fp32-faithful mode: f32 token rows, every GEMM and attention on
+        bf16x3 (ops.x3_linear / ops.x3_attention), one stream (a parity mode, not a throughput one)."""
+        B, Np, Ci = img_patches.shape
+        D, h, eps, dev = self.D, self.heads, self.eps, self.device
+        nl = len(self.layers)
+        dh = D // h
+        sc = 1.0 / math.sqrt(dh)
+        G = img_global.float().contiguous()
+        P = img_patches.float().contiguous().view(B * Np, Ci)
+        m1 = torch.empty((nl, B, D), dtype=torch.float32, device=dev)
+        m2 = torch.empty((nl, B, D), dtype=torch.float32, device=dev)
+        PF = torch.empty((nl, B * Np, D), dtype=torch.float32, device=dev)
+        cls = None
+        for i, L in enumerate(self.layers):
+            Pe = L["patch"].x3(P, B, Np, eps)                                # (B*Np, Ci) f32
+            PQ = ops.x3_linear(Pe, L["p_x3"], L["p_b"])                     # k_t2i | v_t2i | q_i2t
+            PP = ops.x3_linear(Pe, L["pp_x3"], L["pp_b"])                   # img_patch_proj
+            if txt_feats is None:  # learnable default text token (fusion.py:404-407)
+                T, Lt = L["default_txt32"].expand(B, -1).contiguous(), 1
+            else:
+                Lt = txt_feats.shape[1]
+                T = txt_feats.float().contiguous().view(B * Lt, -1)
+            Te = L["txt"].x3(T, B, Lt, eps)                                  # (B*Lt, Ct) f32
+            Ct = Te.shape[1]
+            if cls is None:
+                cls = torch.empty((nl, B, Ct), dtype=torch.float32, device=dev)
+            ops.x3_gather_rows(Te, B, Ct, Lt * Ct, out=cls[i])              # CLS rows (fusion.py:447)
+            TQ = ops.x3_linear(Te, L["t_x3"], L["t_b"])                     # q_t2i | k_i2t | v_i2t
+            ops.x3_attention(TQ[:, :D], PQ[:, :D], PQ[:, D:2 * D], B, Lt, Np, h, dh, sc, mean_out=m1[i])
+            a2 = torch.empty((B * Np, D), dtype=torch.float32, device=dev)
+            ops.x3_attention(PQ[:, 2 * D:], TQ[:, D:2 * D], TQ[:, 2 * D:], B, Np, Lt, h, dh, sc, out=a2, mean_out=m2[i])
+            ops.x3_linear(a2, L["o2_x3t"], L["o2_b"], residual=PP, out=PF[i])  # patches_fused (fusion.py:437)
+        return self._finish(G, m1, m2, cls, PF, B, Np, Ci)
+
+    def _finish(self, G, m1, m2, cls, PF, B, Np, Ci):
+        """Phases 2-4 of forward (shared by the bf16 / fp8 and x3 modes)."""
+        D, h, eps, dev = self.D, self.heads, self.eps, self.device
+        nl = len(self.layers)
+        dh = D // h
+        sc = 1.0 / math.sqrt(dh)
         # phase 2: per-query vectors of all layers
         Ge = ops.linear_x3(G, self.g_w_x3, self.g_b_all)               # (B, nl*Ci), layer-minor
         Ge = ops.ln_rows(Ge.view(B * nl, Ci), *self.g_ln_all, eps, groups=nl).view(B, nl * Ci)
@@ -294,14 +362,19 @@ class FusionStack:
         x2 = ops.linear_x3_batched(cls, self.tp_x3, self.tp_b_all, nl, B, residual=i2t)
         x2 = ops.ln_rows(x2.view(nl * B, D), *self.ln_txt_all, eps, groups=nl, group_div=B)
         # phase 3: the shared combiner self-attention over every layer's fused sequence
-        if self.s_w8 is not None and (nl * B * (Np + 2)) % 256 == 0:
+        m3 = torch.empty((nl * B, D), dtype=torch.float32, device=dev)
+        if self.x3:
+            S = ops.x3_assemble_seq(x1, PF.view(nl * B * Np, D), x2, self.pe, Np).view(nl * B * (Np + 2), D)
+            SQ = ops.x3_linear(S, self.s_x3, self.s_b)
+            ops.x3_attention(SQ[:, :D], SQ[:, D:2 * D], SQ[:, 2 * D:], nl * B, Np + 2, Np + 2, h, dh, sc, mean_out=m3)
+        elif self.s_w8 is not None and (nl * B * (Np + 2)) % 256 == 0:
             S8 = ops.assemble_seq(x1, PF.view(nl * B * Np, D), x2, self.pe, Np, q8=True)
             SQ = ops.linear_mxfp8(S8, self.s_w8, self.s_b)
         else:
             S = ops.assemble_seq(x1, PF.view(nl * B * Np, D), x2, self.pe, Np).view(nl * B * (Np + 2), D)
             SQ = ops.linear(S, self.s_w, self.s_b)
-        m3 = torch.empty((nl * B, D), dtype=torch.float32, device=dev)
-        ops.mha(SQ[:, :D], SQ[:, D:2 * D], SQ[:, 2 * D:], nl * B, Np + 2, Np + 2, h, dh, sc, mean_out=m3)
+        if not self.x3:
+            ops.mha(SQ[:, :D], SQ[:, D:2 * D], SQ[:, 2 * D:], nl * B, Np + 2, Np + 2, h, dh, sc, mean_out=m3)
         fused = ops.linear_x3(m3, self.s_ow_x3, self.s_ob).view(nl, B, D)  # mean of self_attn output
         # phase 4: the joint chain
         joint = None

@@ -26,6 +26,7 @@ import torch
 from . import ops
 from .fusion import FusionStack
 from .towers import BERT_BASE, SWIN_T, SWIN_ARCHS, BertTower, SwinTower, init_bert_state, init_swin_state
+from .towers_x3 import BertTowerX3, SwinTowerX3
 
 
 def _sub(sd, prefix):
@@ -124,14 +125,15 @@ class Backbones:
     channel (the same response on the grey-replicated inputs, tensorDICOM.py:150).
     Extras (keyword-only): swin_state / bert_state (state dicts), swin_cfg / bert_cfg (geometry
     overrides), device, seed, tower_dtype ("bf16" configs 1-4, "fp8" config 5: MX-fp8 linears in
-    every BERT layer and Swin stages 3-4)."""
+    every BERT layer and Swin stages 3-4, "x3": the fp32-faithful parity mode — f32 activations,
+    every contraction on bf16x3 MFMA, towers_x3.py)."""
 
     def __init__(self, img_backbone="swin", swin_model_name="swin_base_patch4_window7_224", cnn_model_name="resnet50",
                  bert_model_name="emilyalsentzer/Bio_ClinicalBERT", swin_checkpoint_path=None, bert_local_dir=None,
                  pretrained=True, img_dim=None, txt_dim=None, *, swin_state=None, bert_state=None, swin_cfg=None,
                  bert_cfg=None, device="cuda", seed=2709, tower_dtype="bf16"):
-        if tower_dtype not in ("bf16", "fp8"):
-            raise ValueError(f"tower_dtype {tower_dtype!r}: bf16 or fp8")
+        if tower_dtype not in ("bf16", "fp8", "x3"):
+            raise ValueError(f"tower_dtype {tower_dtype!r}: bf16, fp8 or x3")
         self.tower_dtype = tower_dtype
         if img_backbone != "swin":
             raise ValueError(f"image backbone {img_backbone!r} is outside the accelerated path (swin only)")
@@ -167,9 +169,13 @@ class Backbones:
             bert_state = init_bert_state(bert_cfg, seed + 1)
         fp8 = tower_dtype == "fp8"
         self.swin_cfg, self.bert_cfg = swin_cfg, bert_cfg
-        self.vision = SwinTower(swin_state, swin_cfg, self.device, fp8_stages=(2, 3) if fp8 else ())
+        if tower_dtype == "x3":  # fp32-faithful mode (towers_x3.py): f32 activations, bf16x3 contractions
+            self.vision = SwinTowerX3(swin_state, swin_cfg, self.device)
+            self.bert = BertTowerX3(bert_state, bert_cfg, self.device)
+        else:
+            self.vision = SwinTower(swin_state, swin_cfg, self.device, fp8_stages=(2, 3) if fp8 else ())
+            self.bert = BertTower(bert_state, bert_cfg, self.device, fp8=fp8)
         self.swin = self.vision
-        self.bert = BertTower(bert_state, bert_cfg, self.device, fp8=fp8)
         self.img_dim = self.vision.num_features if img_dim is None else img_dim
         self.txt_dim = self.bert.hidden if txt_dim is None else txt_dim
         if self.img_dim != self.vision.num_features or self.txt_dim != self.bert.hidden:
@@ -179,6 +185,8 @@ class Backbones:
     # fast path: bf16 hidden states + fused pooling, no f32 copies of the full token grids
     def encode_image(self, image, want_patches=True):
         tok = self.vision.tokens(image)
+        if self.tower_dtype == "x3":
+            return self.vision.head(tok)
         B, H, W, C = tok.shape
         patches, glob, pool = ops.swin_head(tok.view(B, H * W, C), self.vision.norm_g, self.vision.norm_b, 1e-5,
                                             want_patches=want_patches)
@@ -310,7 +318,9 @@ class MultiModalRetrievalModel:
         self.retriever = retriever
 
     def _txt_pool(self, hidden):
-        return hidden[:, 0, :].float().contiguous() if self.use_cls_only else ops.mean_tokens(hidden)
+        if self.use_cls_only:
+            return hidden[:, 0, :].float().contiguous()
+        return ops.x3_mean_rows(hidden) if hidden.dtype == torch.float32 else ops.mean_tokens(hidden)
 
     def _head(self, x, proj, l2norm=False):
         return ops.proj_head(x, proj[0], proj[1], *self.ffn, l2norm=l2norm)

@@ -517,3 +517,96 @@ def swin_attn_block(x, pack, bias, ws, shift, eps):
     _chk(_L().mmr_swin_attn_block(_lib.ptr(x), _lib.ptr(pack), _lib.ptr(bias), _lib.ptr(y), B, H, C, ws, shift,
                                   float(eps), _s(x)), "mmr_swin_attn_block")
     return y
+
+
+# ---------------------------------------------------------------- fp32-faithful tower mode ("x3")
+# f32 activations, every contraction on bf16x3 MFMA (csrc/x3.hip); weights as X3W (hi / lo splits).
+def x3_linear(x, wx, bias=None, residual=None, act=0, out=None):
+    """act(x @ w.T + bias) (+ residual) for any number of rows: x (..., K) f32 (last-dim contiguous rows),
+    wx an X3W of w (N, K), K % 32 == 0; residual may be `out`."""
+    _lib.require_gpu(x)
+    K = x.shape[-1]
+    N, Kw = wx.w.shape
+    assert K == Kw, f"x3_linear: K {K} != weight K {Kw}"
+    x2 = x.reshape(-1, K)
+    assert x2.stride(1) == 1
+    M = x2.shape[0]
+    y = out if out is not None else torch.empty(x.shape[:-1] + (N,), dtype=torch.float32, device=x.device)
+    r2 = residual.reshape(-1, N) if residual is not None else None
+    _chk(_L().mmr_x3_linear(_lib.ptr(x2), x2.stride(0), _lib.ptr(wx.hi), _lib.ptr(wx.lo), _lib.ptr(bias), _lib.ptr(r2),
+                            r2.stride(0) if r2 is not None else 0, _lib.ptr(y), N, M, N, K, act, _s(x)),
+         "mmr_x3_linear")
+    return y
+
+
+def x3_attention(q, k, v, b, lq, lk, heads, dh, scale, out=None, mean_out=None, mask=None):
+    """f32 attention core over strided row views (mmr_x3_attention); mask (b, lk) int64 or None."""
+    _lib.require_gpu(q)
+    _chk(_L().mmr_x3_attention(_lib.ptr(q), q.stride(0), _lib.ptr(k), k.stride(0), _lib.ptr(v), v.stride(0),
+                               _lib.ptr(out), out.stride(0) if out is not None else 0, _lib.ptr(mean_out),
+                               _lib.ptr(mask), b, lq, lk, heads, dh, float(scale), _s(q)), "mmr_x3_attention")
+    return out, mean_out
+
+
+def x3_swin_window_attention(qkv, bias, hw, heads, ws, shift):
+    B = qkv.shape[0]
+    C = qkv.shape[-1] // 3
+    out = torch.empty(qkv.shape[:-1] + (C,), dtype=torch.float32, device=qkv.device)
+    _chk(_L().mmr_x3_swin_window_attention(_lib.ptr(qkv), _lib.ptr(bias), _lib.ptr(out), B, hw, C, heads, ws, shift,
+                                           _s(qkv)), "mmr_x3_swin_window_attention")
+    return out
+
+
+def x3_patch_im2col(img, patch=4, kp=64):
+    B, Cin, H, W = img.shape
+    g = H // patch
+    cols = torch.empty((B, g * g, kp), dtype=torch.float32, device=img.device)
+    _chk(_L().mmr_x3_patch_im2col(_lib.ptr(img), _lib.ptr(cols), B, Cin, H, patch, kp, _s(img)), "mmr_x3_patch_im2col")
+    return cols
+
+
+def x3_patch_merge_ln(x, g, b, eps):
+    B, H, W, C = x.shape
+    y = torch.empty((B, H // 2, W // 2, 4 * C), dtype=torch.float32, device=x.device)
+    _chk(_L().mmr_x3_patch_merge_ln(_lib.ptr(x), _lib.ptr(g), _lib.ptr(b), _lib.ptr(y), B, H, C, float(eps), _s(x)),
+         "mmr_x3_patch_merge_ln")
+    return y
+
+
+def x3_bert_embed(ids, word, pos, type0, g, b, eps):
+    B, L = ids.shape
+    C = word.shape[1]
+    y = torch.empty((B, L, C), dtype=torch.float32, device=ids.device)
+    _chk(_L().mmr_x3_bert_embed(_lib.ptr(ids), _lib.ptr(word), _lib.ptr(pos), _lib.ptr(type0), _lib.ptr(g), _lib.ptr(b),
+                                _lib.ptr(y), B, L, C, float(eps), _s(ids)), "mmr_x3_bert_embed")
+    return y
+
+
+def x3_add_pos(x, pos, l):
+    c = x.shape[-1]
+    rows = x.numel() // c
+    y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+    _chk(_L().mmr_x3_add_pos(_lib.ptr(x), _lib.ptr(pos), _lib.ptr(y), rows, l, c, _s(x)), "mmr_x3_add_pos")
+    return y
+
+
+def x3_assemble_seq(x1, pf, x2, pe, np_):
+    B, c = x1.shape
+    seq = torch.empty((B, np_ + 2, c), dtype=torch.float32, device=x1.device)
+    _chk(_L().mmr_x3_assemble_seq(_lib.ptr(x1), _lib.ptr(pf), _lib.ptr(x2), _lib.ptr(pe), _lib.ptr(seq), B, np_, c,
+                                  _s(x1)), "mmr_x3_assemble_seq")
+    return seq
+
+
+def x3_mean_rows(x, extra=None):
+    """(B, L, C) f32 -> (B, C): sum_t x / L, or (extra + sum_t x) / (L + 1)."""
+    B, L, C = x.shape
+    y = torch.empty((B, C), dtype=torch.float32, device=x.device)
+    _chk(_L().mmr_x3_mean_rows(_lib.ptr(x), _lib.ptr(extra), _lib.ptr(y), B, L, C, _s(x)), "mmr_x3_mean_rows")
+    return y
+
+
+def x3_gather_rows(x, b, c, ldx, out=None):
+    y = out if out is not None else torch.empty((b, c), dtype=torch.float32, device=x.device)
+    _chk(_L().mmr_x3_gather_rows(_lib.ptr(x), ldx, _lib.ptr(y), b, c, _s(x)), "mmr_x3_gather_rows")
+    return y

@@ -1,0 +1,251 @@
+"""GPU parity of the fp32-faithful tower mode (tower_dtype="x3", csrc/x3.hip, towers_x3.py).
+
+The reference computes its towers and heads in fp32 (src/Model/fusion.py:198-199, 322-325,
+model.py:365-479); the x3 mode keeps f32 activations and runs every contraction as
+a_hi.b_hi + a_hi.b_lo + a_lo.b_hi on bf16 MFMA (~2^-17 relative per product, f32 accumulation).
+
+Bars (written per test):
+  * kernels vs f64 of the same f32 inputs: linear |err| <= 2^-15 * (|x| @ |w|^T) + 1e-6 * max|ref|
+    (the split's per-product bound with margin), attention max|err| <= 5e-5 * max|ref|;
+  * towers vs the f64 oracle (oracle/towers.py run in double): max|err| <= 5e-4 * max|ref| — an
+    order below the bf16 towers' 4e-2 — and vs the reference's own fp32 goldens (towers_mini.npz);
+  * end to end: x3 towers + GPU exact kNN against the fp32 oracle towers + the
+    sklearn-path top-10 (src/Evaluate/retrieval_overlap.py:84-115) on EVERY query of a B = 256 batch
+    over the 100k x 768 labelled gallery: oracle.knn.topk_equivalent (tie_tol 1e-6, scores within
+    1e-4) and identical P@10 / R@10 / MRR under random labels.
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mmr_amd import metrics, ops, synthetic
+from mmr_amd.model import Backbones, MultiModalRetrievalModel, build_bench_model
+from mmr_amd.retrieval import MI355XRetrievalEngine
+from mmr_amd.towers import BERT_BASE, SWIN_T, init_bert_state, init_swin_state
+from mmr_amd.towers_x3 import BertTowerX3, SwinTowerX3
+from oracle import knn as oknn
+from oracle import towers as otw
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(got, ref):
+    got = got.detach().double().cpu()
+    ref = ref.detach().double().cpu()
+    return (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-30)
+
+
+@pytest.mark.parametrize("M,N,K,act,bias,res", [(1000, 96, 96, 0, True, False), (513, 2304, 768, 0, True, False),
+                                                (300, 3072, 768, 1, True, False), (257, 768, 3072, 0, True, True),
+                                                (77, 288, 64, 1, True, True), (4096, 200, 384, 0, False, False),
+                                                (20000, 384, 1536, 0, False, False)])
+def test_x3_linear_vs_f64(M, N, K, act, bias, res):
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) * 0.05
+    b = torch.randn(N, generator=g) if bias else None
+    r = torch.randn(M, N, generator=g) if res else None
+    ref = x.double() @ w.double().T
+    if b is not None:
+        ref = ref + b.double()
+    if act == 1:
+        ref = F.gelu(ref)
+    if r is not None:
+        ref = ref + r.double()
+    y = ops.x3_linear(x.to(DEV), ops.X3W(w.to(DEV)), b.to(DEV) if b is not None else None,
+                      residual=r.to(DEV) if r is not None else None, act=act)
+    err = (y.double().cpu() - ref).abs()
+    absdot = x.double().abs() @ w.double().abs().T
+    bound = 2.0 ** -15 * absdot + 1e-6 * ref.abs().max()
+    f32 = x @ w.T  # the reference's own f32 GEMM, for scale
+    print(json.dumps({"x3_max_err": err.max().item(), "f32_gemm_max_err": (f32.double() - x.double() @ w.double().T)
+                      .abs().max().item()}))
+    assert (err <= bound).all(), (err - bound).max().item()
+
+
+def _attn_ref(q, k, v, b, lq, lk, heads, dh, scale, mask=None):
+    qh = q.double().view(b, lq, heads, dh).transpose(1, 2)
+    kh = k.double().view(b, lk, heads, dh).transpose(1, 2)
+    vh = v.double().view(b, lk, heads, dh).transpose(1, 2)
+    s = qh @ kh.transpose(-1, -2) * scale
+    if mask is not None:
+        s = s.masked_fill(mask[:, None, None, :] == 0, float("-inf"))
+    return (s.softmax(-1) @ vh).transpose(1, 2).reshape(b, lq, heads * dh)
+
+
+@pytest.mark.parametrize("b,lq,lk,heads,dh,use_mask,mean", [(3, 128, 128, 12, 64, True, False),
+                                                          (5, 49, 128, 8, 96, False, True),
+                                                          (4, 51, 51, 8, 128, False, True),
+                                                          (2, 1, 49, 8, 96, False, True),
+                                                          (3, 130, 70, 2, 48, True, True),
+                                                          (2, 128, 1, 8, 96, False, True)])
+def test_x3_attention_vs_f64(b, lq, lk, heads, dh, use_mask, mean):
+    g = torch.Generator().manual_seed(b * 1000 + lq + lk + dh)
+    C = heads * dh
+    q = torch.randn(b * lq, 3 * C, generator=g) * 0.7           # strided views of packed rows
+    kv = torch.randn(b * lk, 3 * C, generator=g) * 0.7
+    mask = None
+    if use_mask:
+        lens = torch.randint(1, lk + 1, (b,), generator=g)
+        mask = (torch.arange(lk)[None, :] < lens[:, None]).to(torch.int64)
+    scale = 1.0 / math.sqrt(dh)
+    ref = _attn_ref(q[:, :C], kv[:, C:2 * C], kv[:, 2 * C:], b, lq, lk, heads, dh, scale, mask)
+    qd, kvd = q.to(DEV), kv.to(DEV)
+    out = torch.empty((b * lq, C), dtype=torch.float32, device=DEV)
+    m = torch.empty((b, C), dtype=torch.float32, device=DEV) if mean else None
+    ops.x3_attention(qd[:, :C], kvd[:, C:2 * C], kvd[:, 2 * C:], b, lq, lk, heads, dh, scale, out=out, mean_out=m,
+                     mask=mask.to(DEV) if mask is not None else None)
+    assert _rel(out.view(b, lq, C), ref) <= 5e-5
+    if mean:
+        assert _rel(m, ref.mean(1)) <= 5e-5
+
+
+@pytest.mark.parametrize("hw,c,heads,shift", [(56, 96, 3, 0), (56, 96, 3, 3), (14, 384, 12, 3), (7, 768, 24, 0)])
+def test_x3_swin_window_attention_vs_f64(hw, c, heads, shift):
+    """roll(-shift) / window partition / q*dh^-0.5 k^T + rel-pos bias + shift mask / softmax / v /
+    reverse / roll(+shift) (timm WindowAttention, restated with oracle/towers.py's helpers) in f64."""
+    B, ws = 2, 7
+    g = torch.Generator().manual_seed(hw + c + shift)
+    qkv = torch.randn(B, hw, hw, 3 * c, generator=g) * 0.7
+    table = torch.randn((2 * ws - 1) ** 2, heads, generator=g) * 0.5
+    bias = ops.swin_attn_bias(table.to(DEV), heads, ws, hw, shift)
+    out = ops.x3_swin_window_attention(qkv.to(DEV).contiguous(), bias, hw, heads, ws, shift)
+    dh, N = c // heads, ws * ws
+    x = qkv.double()
+    if shift:
+        x = torch.roll(x, shifts=(-shift, -shift), dims=(1, 2))
+    win = otw.window_partition(x, ws).view(-1, N, 3, heads, dh).permute(2, 0, 3, 1, 4)
+    q, k, v = win[0] * dh ** -0.5, win[1], win[2]
+    a = q @ k.transpose(-2, -1)
+    a = a + table.double()[otw.relative_position_index(ws).view(-1)].view(N, N, heads).permute(2, 0, 1)[None]
+    if shift:
+        msk = otw.shift_mask(hw, hw, ws, shift).double()
+        nW = msk.shape[0]
+        a = (a.view(-1, nW, heads, N, N) + msk[None, :, None]).view(-1, heads, N, N)
+    o = (a.softmax(-1) @ v).transpose(1, 2).reshape(-1, ws, ws, c)
+    o = otw.window_reverse(o, ws, hw, hw)
+    if shift:
+        o = torch.roll(o, shifts=(shift, shift), dims=(1, 2))
+    assert _rel(out, o) <= 5e-5
+
+
+def _double(sd):
+    return {k: v.double() for k, v in sd.items()}
+
+
+def test_x3_towers_vs_f64_oracle():
+    """Swin-T + BERT-base (random init, the bench geometry) at B = 2 against the oracle run in f64,
+    with the fp32 oracle's own distance from f64 printed beside it."""
+    ssd, bsd = init_swin_state(SWIN_T, 5), init_bert_state(BERT_BASE, 6)
+    img = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(2, 9)))
+    ids, mask = (torch.from_numpy(a) for a in synthetic.reports(2, 128, 10))
+    sw = SwinTowerX3(ssd, SWIN_T, DEV)
+    bt = BertTowerX3(bsd, BERT_BASE, DEV)
+    f_gpu = sw.forward_features(img.to(DEV))
+    t_gpu = bt.forward(ids.to(DEV), mask.to(DEV))
+    with torch.no_grad():
+        f64 = otw.swin_forward_features(img.double(), _double(ssd), SWIN_T["depths"], SWIN_T["num_heads"])
+        t64 = otw.bert_forward(ids, mask, _double(bsd), 12, 12)
+        f32 = otw.swin_forward_features(img, ssd, SWIN_T["depths"], SWIN_T["num_heads"])
+        t32 = otw.bert_forward(ids, mask, bsd, 12, 12)
+    rep = {"swin_x3": _rel(f_gpu, f64), "swin_f32_oracle": _rel(f32, f64), "bert_x3": _rel(t_gpu, t64),
+           "bert_f32_oracle": _rel(t32, t64)}
+    print(json.dumps(rep))
+    assert rep["swin_x3"] <= 5e-4 and rep["bert_x3"] <= 5e-4
+
+
+def test_x3_mini_towers_match_reference_golden():
+    """The reference's own fp32 outputs (towers_mini.npz: Backbones.forward + all three heads,
+    multimodal with 2 fusion layers) reproduced by the x3 mode to 2e-4 * max|ref| (the bf16 mode: 4e-2)."""
+    f = np.load(os.path.join(GOLDEN, "towers_mini.npz"), allow_pickle=False)
+    cfg = json.loads(bytes(f["cfg"]).decode())
+    w = {k[2:]: torch.from_numpy(synthetic.bf16_bits_to_f32(f[k]).copy()) for k in f.files if k.startswith("w:")}
+    swin = {k[5:]: v for k, v in w.items() if k.startswith("swin.")}
+    bert = {k[5:]: v for k, v in w.items() if k.startswith("bert.")}
+    head = {k[5:]: v for k, v in w.items() if k.startswith("head.")}
+    scfg = dict(SWIN_T, embed_dim=cfg["swin"]["embed_dim"], depths=cfg["swin"]["depths"],
+                num_heads=cfg["swin"]["num_heads"])
+    bcfg = dict(BERT_BASE, **cfg["bert"])
+    bb = Backbones(swin_state=swin, bert_state=bert, swin_cfg=scfg, bert_cfg=bcfg, device=DEV, tower_dtype="x3")
+    image = torch.from_numpy(synthetic.image_from_u8(f["img_u8"])).to(DEV)
+    ids = torch.from_numpy(f["input_ids"]).to(DEV)
+    mask = torch.from_numpy(f["attention_mask"]).to(DEV)
+    (g, p), t = bb(image, ids, mask)
+    errs = {"img_global": _rel(g, torch.from_numpy(f["img_global"])),
+            "img_patches": _rel(p, torch.from_numpy(f["img_patches"])),
+            "txt_feats": _rel(t, torch.from_numpy(f["txt_feats"]))}
+    for mt in ("text", "image", "multimodal"):
+        m = MultiModalRetrievalModel(joint_dim=cfg["joint_dim"], num_heads=cfg["num_heads"], model_type=mt,
+                                     backbones=bb, head_state=head, device=DEV, use_shared_ffn=False)
+        o = m(image, ids, mask)
+        for k in ("joint_emb", "img_emb", "txt_emb"):
+            errs[f"{mt}_{k}"] = _rel(o[k], torch.from_numpy(f[f"{mt}_{k}"]))
+    print(json.dumps(errs))
+    assert max(errs.values()) <= 2e-4, errs
+
+
+def _labels(n, seed):
+    rng = np.random.default_rng(seed)
+    lab = np.zeros((n, synthetic.NUM_LABELS), np.uint8)
+    for i in range(n):
+        lab[i, rng.choice(synthetic.NUM_LABELS, size=int(rng.integers(1, 4)), replace=False)] = 1
+    return synthetic.labels_to_bits(lab)
+
+
+def _metrics(idx, qb, gbits, K=10):
+    rel = [[str(j) for j in np.nonzero(gbits & qb[q])[0]] for q in range(len(qb))]
+    p = np.mean([metrics.precision_at_k([str(j) for j in idx[q]], rel[q], K) for q in range(len(qb))])
+    mrr, _, rec = metrics.ranking_metrics(idx, qb, gbits, K)
+    return {"P@10": float(p), "R@10": float(rec), "MRR": float(mrr)}
+
+
+@pytest.mark.parametrize("model_type", ["multimodal", "text"])
+def test_e2e_x3_batch_256_identical_topk(model_type):
+    """BASELINE.md §3 end to end: the bench model (Swin-T + BERT-base + 5-layer multimodal head, or the
+    text head) in the x3 mode at B = 256, every query against the fp32 oracle path (oracle towers +
+    head -> sklearn cosine_similarity + argsort, retrieval_overlap.py:84-115) over a 100k x 768
+    labelled gallery: topk_equivalent on every query (tie_tol 1e-6, scores within 1e-4) and identical
+    P@10 / R@10 / MRR under random query labels."""
+    m = build_bench_model(device=DEV, joint_dim=768, model_type=model_type, tower_dtype="x3")
+    B = 256
+    img = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(B, 71)))
+    ids, mask = (torch.from_numpy(a) for a in synthetic.reports(B, 128, 72))
+    imgd = img.to(DEV) if model_type == "multimodal" else None
+    q_gpu = m.query_embeddings(imgd, ids.to(DEV), mask.to(DEV)).float().cpu().numpy()
+    from mmr_amd.model import init_fusion_state, init_head_state
+    ssd, bsd = init_swin_state(SWIN_T, 2709), init_bert_state(BERT_BASE, 2710)
+    hsd = init_head_state(768, 768, 768, 2711)
+    with torch.no_grad():
+        if model_type == "multimodal":
+            hsd.update(init_fusion_state(768, 768, 768, 8, 5, 2712))
+            (g, p), t = otw.backbones_forward(img, ids, mask, ssd, bsd, SWIN_T, BERT_BASE)
+            q_cpu = otw.heads(g, p, t, hsd, "multimodal", mm_cfg={"num_heads": 8})["joint_emb"].numpy()
+        else:
+            t = otw.bert_forward(ids, mask, bsd, 12, 12)
+            q_cpu = otw.heads(None, None, t, hsd, "text")["joint_emb"].numpy()
+    G, gl = synthetic.labelled_gallery(100_000, 768, 73)
+    gbits = synthetic.labels_to_bits(gl)
+    eng = MI355XRetrievalEngine(embs=G, ids=[str(i) for i in range(len(G))], dtype="fp32")
+    gi, gs = eng.search(np.ascontiguousarray(q_gpu), K=10)
+    eng.close()
+    gi = gi.cpu().numpy() if isinstance(gi, torch.Tensor) else np.asarray(gi)
+    gs = gs.cpu().numpy() if isinstance(gs, torch.Tensor) else np.asarray(gs)
+    ci, cs = oknn.sklearn_topk(q_cpu, G, 10)
+    cos = np.sum(q_gpu * q_cpu, 1) / (np.linalg.norm(q_gpu, axis=1) * np.linalg.norm(q_cpu, axis=1))
+    ok, msg = oknn.topk_equivalent(ci, cs, gi, gs, tie_tol=1e-6, score_tol=1e-4)
+    qb = _labels(B, 74)
+    mg, mc = _metrics(gi, qb, gbits), _metrics(ci, qb, gbits)
+    print(json.dumps({"model_type": model_type, "topk_equivalent": msg, "min_embedding_cosine": float(cos.min()),
+                      "max_rel_emb_err": float(np.abs(q_gpu - q_cpu).max() / np.abs(q_cpu).max()),
+                      "exact_list_match": float(np.mean([np.array_equal(gi[i], ci[i]) for i in range(B)])),
+                      "gpu": mg, "cpu": mc}))
+    assert ok, msg
+    assert mg == mc
