@@ -128,6 +128,15 @@ mmr_status mmr_merge_topk_payload(const double* scores, const int64_t* idx, cons
                                   int64_t nq, int32_t k_in, int32_t k_out, int64_t* out_idx, float* out_score,
                                   double* out_score64, double* out_payload, void* stream);
 
+/* mmr_merge_topk_payload over ONE packed all-gather buffer (the sharded search's single collective,
+ * SURVEY.md §8e): packed = [n_lists][nq_total][k_in][2 + payload_width] 8-byte words per entry =
+ * {f64 score, int64 global index (-1 = empty), payload_width f64 payload values}; merges queries
+ * [q0, q0 + nq) (score desc, index asc) into out_idx / out_score / out_score64 / out_payload
+ * [nq][k_out][payload_width] (each output but out_idx may be NULL). */
+mmr_status mmr_merge_topk_packed(const void* packed, int32_t payload_width, int32_t n_lists, int64_t nq_total,
+                                 int64_t q0, int64_t nq, int32_t k_in, int32_t k_out, int64_t* out_idx,
+                                 float* out_score, double* out_score64, double* out_payload, void* stream);
+
 /* Sharded KG / label rerank (Reranker.rerank, src/Retrieval/reranker.py:240-333, over a row-sharded
  * gallery).  Shard side: mmr_index_rerank_components writes, for each of this shard's candidates
  * cand (nq, kc) (global indices into this index, -1 = empty), the three RAW components

@@ -33,6 +33,7 @@ SIGNATURES = {
     "mmr_merge_topk": [c_vp, c_vp, c_i32, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp],
     "mmr_merge_topk_payload": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp,
                                c_vp, c_vp],
+    "mmr_merge_topk_packed": [c_vp, c_i32, c_i32, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
     "mmr_index_rerank_components": [c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp],
     "mmr_rerank_mix": [c_vp, c_vp, c_i64, c_i32, ctypes.c_double, ctypes.c_double, ctypes.c_double, c_i32, c_vp, c_vp,
                        c_vp, c_vp, c_vp, c_vp],

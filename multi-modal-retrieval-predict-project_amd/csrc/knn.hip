@@ -1817,7 +1817,10 @@ __global__ __launch_bounds__(T) void knn_select_t(
 // ------------------------------------------------------------------ shard merge
 // Lists [n_lists][nq_total][k_in]; workgroup qi merges query q0 + qi.  Optional payload
 // pay [n_lists][nq_total][k_in][P] f64 rides with each entry into out_pay [nq][k_out][P] (the
-// sharded rerank's per-candidate components, computed on the shard that owns the row).
+// sharded rerank's per-candidate components, computed on the shard that owns the row).  Entry e's
+// score / index / payload sit at scores[e * ss], idx[e * si], pay[e * sp + p]: separate arrays
+// (1, 1, P) or ONE packed all-gather buffer of 8-byte words [n_lists][nq_total][k_in][W] = {f64 score,
+// int64 index, P f64 payload} (W, W, W: mmr_merge_topk_packed).
 __global__ __launch_bounds__(256) void knn_merge(const double* __restrict__ scores,
                                                  const int64_t* __restrict__ idx, int n_lists,
                                                  int64_t nq_total, int64_t q0, int k_in, int k_out,
@@ -1825,7 +1828,7 @@ __global__ __launch_bounds__(256) void knn_merge(const double* __restrict__ scor
                                                  float* __restrict__ out_score,
                                                  double* __restrict__ out_score64,
                                                  const double* __restrict__ pay, int P,
-                                                 double* __restrict__ out_pay) {
+                                                 double* __restrict__ out_pay, int64_t ss, int64_t si, int64_t sp) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* cs = (double*)smem;
   int64_t* ci = (int64_t*)(smem + sizeof(double) * n_lists * k_in);
@@ -1834,8 +1837,8 @@ __global__ __launch_bounds__(256) void knn_merge(const double* __restrict__ scor
   auto src = [&](int c) { return ((int64_t)(c / k_in) * nq_total + q0 + qi) * k_in + c % k_in; };
   for (int c = threadIdx.x; c < m; c += blockDim.x) {
     const int64_t off = src(c);
-    cs[c] = scores[off];
-    ci[c] = idx[off];
+    cs[c] = scores[off * ss];
+    ci[c] = idx[off * si];
   }
   __syncthreads();
   int nvalid = 0;
@@ -1856,7 +1859,7 @@ __global__ __launch_bounds__(256) void knn_merge(const double* __restrict__ scor
       if (out_score) out_score[qi * k_out + rank] = (float)sc;
       if (out_score64) out_score64[qi * k_out + rank] = sc;
       if (out_pay)
-        for (int p = 0; p < P; ++p) out_pay[(qi * k_out + rank) * P + p] = pay[src(c) * P + p];
+        for (int p = 0; p < P; ++p) out_pay[(qi * k_out + rank) * P + p] = pay[src(c) * sp + p];
     }
   }
   for (int r = nvalid + threadIdx.x; r < k_out; r += blockDim.x) {
@@ -2275,6 +2278,47 @@ mmr_status build_x3_copies(mmr_index* ix) {
   return MMR_OK;
 }
 
+mmr_status build_f16_copies(mmr_index* ix) {
+  DeviceGuard g(ix->device);
+  hipError_t e;
+  if (ix->gh == nullptr) {
+    if ((e = hipMalloc(&ix->gh, sizeof(uint16_t) * ix->Np * ix->Dp)) != hipSuccess) {
+      ix->gh = nullptr;
+      mmr::set_error("mmr_index: hipMalloc(fp16 copy) failed: %s", hipGetErrorString(e));
+      return MMR_ERR_OOM;
+    }
+    const int64_t total8 = ix->Np * ix->Dp / 8;
+    knn_tile_gallery_f16<<<dim3((unsigned)ceil_div(total8, 256)), dim3(256)>>>(ix->gal, ix->inv_norm, ix->Dp, total8,
+                                                                             ix->gh);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+      mmr::set_error("mmr_index: fp16 copy kernel failed: %s", hipGetErrorString(e));
+      return MMR_ERR_HIP;
+    }
+  }
+  if (ix->ghr == nullptr && ix->Dp % 128 == 0 && ix->Dp <= 1024) {
+    // row-major fp16 unit rows for the p8 scan of 129-1024-query passes (whole 256-row tiles)
+    const int64_t np256 = round_up(ix->Np, 256);
+    if ((e = hipMalloc(&ix->ghr, sizeof(uint16_t) * np256 * ix->Dp)) != hipSuccess) {
+      ix->ghr = nullptr;
+      mmr::set_error("mmr_index: hipMalloc(fp16 row copy) failed: %s", hipGetErrorString(e));
+      return MMR_ERR_OOM;
+    }
+    const int64_t total8 = np256 * ix->Dp / 8;
+    knn_rows_f16<<<dim3((unsigned)ceil_div(total8, 256)), dim3(256)>>>(ix->gal, ix->inv_norm, ix->Np, ix->Dp, total8,
+                                                                     ix->ghr);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+      mmr::set_error("mmr_index: fp16 row copy kernel failed: %s", hipGetErrorString(e));
+      return MMR_ERR_HIP;
+    }
+    ix->Np256 = np256;
+  }
+  return MMR_OK;
+}
+
 void free_copies(mmr_index* ix, bool x3, bool f16) {
   DeviceGuard g(ix->device);
   if (x3 || f16) (void)hipDeviceSynchronize();  // no search still reads them
@@ -2441,6 +2485,7 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
   mmr_status s = ensure_ws(ix, nq);
   if (s != MMR_OK) return s;
   if (ix->mode == 1 && (s = build_x3_copies(ix)) != MMR_OK) return s;  // default mode, first search
+  if (ix->mode == 2 && (s = build_f16_copies(ix)) != MMR_OK) return s;  // never scan a missing copy
   // |s_approx - s64| <= delta; threshold margin 2*delta.
   //  f32 (knn_scores, knn_scan_f32_gmax): (Dp + 16) 2^-24 — f32 products accumulated in f32 over Dp
   //      terms of a unit query against g/|g| (|sum| <= 1), plus the normalisations;
@@ -2721,50 +2766,15 @@ mmr_status mmr_index_set_mode(mmr_index* ix, int32_t mode) {
   MMR_REQUIRE(ix != nullptr && mode >= 0 && mode <= 2, "mmr_index_set_mode: bad arguments");
   std::lock_guard<std::mutex> lk(ix->mu);
   if (mode == ix->mode && (mode != 1 || ix->gs != nullptr) && (mode != 2 || ix->gh != nullptr)) return MMR_OK;
+  // the new mode's copies are built BEFORE the old mode's are freed: on a failure (e.g. an OOM on a
+  // shard sized for fp16) the index stays in its previous mode with its copies intact, and only the
+  // partial new copies are released (freeing first left mode 2 with a null gh)
+  mmr_status s = mode == 1 ? build_x3_copies(ix) : mode == 2 ? build_f16_copies(ix) : MMR_OK;
+  if (s != MMR_OK) {
+    if (ix->mode != mode) free_copies(ix, mode == 1, mode == 2);
+    return s;
+  }
   free_copies(ix, mode != 1, mode != 2);
-  if (mode == 1) {
-    mmr_status s = build_x3_copies(ix);
-    if (s != MMR_OK) return s;
-  }
-  if (mode == 2 && ix->gh == nullptr) {
-    DeviceGuard g(ix->device);
-    hipError_t e = hipMalloc(&ix->gh, sizeof(uint16_t) * ix->Np * ix->Dp);
-    if (e != hipSuccess) {
-      ix->gh = nullptr;
-      mmr::set_error("mmr_index_set_mode: hipMalloc(fp16 copy) failed: %s", hipGetErrorString(e));
-      return MMR_ERR_OOM;
-    }
-    const int64_t total8 = ix->Np * ix->Dp / 8;
-    knn_tile_gallery_f16<<<dim3((unsigned)ceil_div(total8, 256)), dim3(256)>>>(ix->gal, ix->inv_norm, ix->Dp,
-                                                                             total8, ix->gh);
-    e = hipGetLastError();
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-    if (e != hipSuccess) {
-      mmr::set_error("mmr_index_set_mode: fp16 copy kernel failed: %s", hipGetErrorString(e));
-      return MMR_ERR_HIP;
-    }
-  }
-  if (mode == 2 && ix->ghr == nullptr && ix->Dp % 128 == 0 && ix->Dp <= 1024) {
-    // row-major fp16 unit rows for the p8 scan of 33-256-query passes (whole 256-row tiles)
-    DeviceGuard g(ix->device);
-    const int64_t np256 = round_up(ix->Np, 256);
-    hipError_t e = hipMalloc(&ix->ghr, sizeof(uint16_t) * np256 * ix->Dp);
-    if (e != hipSuccess) {
-      ix->ghr = nullptr;
-      mmr::set_error("mmr_index_set_mode: hipMalloc(fp16 row copy) failed: %s", hipGetErrorString(e));
-      return MMR_ERR_OOM;
-    }
-    const int64_t total8 = np256 * ix->Dp / 8;
-    knn_rows_f16<<<dim3((unsigned)ceil_div(total8, 256)), dim3(256)>>>(ix->gal, ix->inv_norm, ix->Np, ix->Dp,
-                                                                     total8, ix->ghr);
-    e = hipGetLastError();
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-    if (e != hipSuccess) {
-      mmr::set_error("mmr_index_set_mode: fp16 row copy kernel failed: %s", hipGetErrorString(e));
-      return MMR_ERR_HIP;
-    }
-    ix->Np256 = np256;
-  }
   ix->mode = mode;
   return MMR_OK;
 }
@@ -2792,7 +2802,29 @@ mmr_status mmr_merge_topk_payload(const double* scores, const int64_t* idx, cons
   const size_t lds = (sizeof(double) + sizeof(int64_t)) * (size_t)n_lists * k_in;
   knn_merge<<<dim3((unsigned)nq), dim3(256), lds, mmr::as_stream(stream)>>>(
       scores, idx, n_lists, nq_total, q0, k_in, k_out, out_idx, out_score, out_score64, payload, payload_width,
-      out_payload);
+      out_payload, 1, 1, payload_width);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_merge_topk_packed(const void* packed, int32_t payload_width, int32_t n_lists, int64_t nq_total,
+                                 int64_t q0, int64_t nq, int32_t k_in, int32_t k_out, int64_t* out_idx,
+                                 float* out_score, double* out_score64, double* out_payload, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(n_lists >= 1 && k_in >= 1 && k_out >= 1 && nq >= 0 && q0 >= 0 && q0 + nq <= nq_total,
+              "mmr_merge_topk_packed: bad sizes");
+  MMR_REQUIRE((int64_t)n_lists * k_in <= 4096, "mmr_merge_topk_packed: n_lists*k_in > 4096");
+  MMR_REQUIRE(payload_width >= 0 && payload_width <= 16 && (out_payload == nullptr || payload_width > 0),
+              "mmr_merge_topk_packed: payload width %d", payload_width);
+  if (nq == 0) return MMR_OK;
+  MMR_REQUIRE(packed && out_idx, "mmr_merge_topk_packed: NULL pointer");
+  MMR_REQUIRE(((uintptr_t)packed & 7u) == 0, "mmr_merge_topk_packed: packed buffer must be 8-B aligned");
+  const int64_t W = 2 + payload_width;
+  const double* base = (const double*)packed;
+  const size_t lds = (sizeof(double) + sizeof(int64_t)) * (size_t)n_lists * k_in;
+  knn_merge<<<dim3((unsigned)nq), dim3(256), lds, mmr::as_stream(stream)>>>(
+      base, (const int64_t*)(base + 1), n_lists, nq_total, q0, k_in, k_out, out_idx, out_score, out_score64,
+      out_payload ? base + 2 : nullptr, payload_width, out_payload, W, W, W);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }

@@ -30,6 +30,7 @@ the folded text / patch cross projections + img_patch_proj, and the img2txt out-
 add-pos / attention / LayerNorm kernels (no quantise pass).  Batches whose token rows are not a 256
 multiple keep bf16 there.
 """
+import collections
 import math
 import os
 
@@ -71,8 +72,11 @@ class _Enhancer:
         self.w_o, self.b_o = _bf(sd[p + "self_attn.out_proj.weight"], dev), _f(sd[p + "self_attn.out_proj.bias"], dev)
         self.alpha = _f(sd[p + "alpha"].reshape(1), dev)
         self.g, self.b = _f(sd[p + "norm1.weight"], dev), _f(sd[p + "norm1.bias"], dev)
-        self.w_in8 = _w8(self.w_in) if fp8 and C % 256 == 0 else None
-        self.w_o8 = _w8(self.w_o) if fp8 and C % 256 == 0 else None
+        # MX-fp8 needs C % 256 (operand panels) and head_dim % 32 (the attention core's q8 output is
+        # one 32-block per lane pair); otherwise this enhancer stays bf16
+        f8 = fp8 and C % 256 == 0 and self.dh % 32 == 0
+        self.w_in8 = _w8(self.w_in) if f8 else None
+        self.w_o8 = _w8(self.w_o) if f8 else None
 
     def fp8_ok(self, rows):
         return self.w_in8 is not None and rows % 256 == 0
@@ -217,11 +221,8 @@ class FusionStack:
     def _side_stream(self, main):
         # one side stream per calling stream (pipelined callers keep their batches independent)
         if getattr(self, "_side", None) is None:
-            self._side = {}
-        side = self._side.get(main.cuda_stream)
-        if side is None:
-            side = self._side[main.cuda_stream] = torch.cuda.Stream(self.device)
-        return side
+            self._side = collections.OrderedDict()
+        return ops.side_stream(self._side, main, self.device)
 
     def forward(self, img_global, img_patches, txt_feats):
         """img_global (B, Ci) f32, img_patches (B, Np, Ci) f32, txt_feats (B, L, Ct) bf16/f32 or None
@@ -300,7 +301,7 @@ class FusionStack:
                 main.wait_event(ev[i])
             PQ, PP = pq[i], pp[i]
             ops.mha(TQ[:, :D], PQ[:, :D], PQ[:, D:2 * D], B, Lt, Np, h, dh, sc, mean_out=m1[i])
-            if self.fp8 and (B * Np) % 256 == 0 and D % 256 == 0:  # the attention core emits the o2 operand
+            if self.fp8 and (B * Np) % 256 == 0 and D % 256 == 0 and dh % 32 == 0:  # the attention core emits the o2 operand
                 _, _, a28 = ops.mha(PQ[:, 2 * D:], TQ[:, D:2 * D], TQ[:, 2 * D:], B, Np, Lt, h, dh, sc, mean_out=m2[i],
                                     q8=True)
                 ops.linear_mxfp8(a28, L["o2_wb8"], L["o2_b"], residual=PP, out=PF[i])  # patches_fused (fusion.py:437)

@@ -17,6 +17,7 @@ MultiModalRetrievalModel.forward(...) -> {"joint_emb", "img_emb", "txt_emb", "lo
     (model.py:375-459) on libmmr kernels (mmr_amd/fusion.py); the classifier (logits) is
     classification, out of scope -> None; attention maps (return_attention) are not produced.
 """
+import collections
 import json
 import os
 from pathlib import Path
@@ -141,7 +142,8 @@ class Backbones:
         self.swin_model_name, self.bert_model_name = swin_model_name, bert_model_name
         self.device = torch.device(device)
         arch = SWIN_ARCHS.get(swin_model_name)
-        if swin_state is None and swin_checkpoint_path and (pretrained or not Path(str(swin_checkpoint_path)).exists()):
+        # fusion.py:83: the checkpoint is read only when pretrained (pretrained=False builds random weights)
+        if swin_state is None and swin_checkpoint_path and pretrained:
             if not Path(str(swin_checkpoint_path)).exists():
                 raise FileNotFoundError(f"Swin checkpoint not found at {swin_checkpoint_path} (no hub access here)")
             swin_state = _load_tensors(swin_checkpoint_path)
@@ -380,10 +382,8 @@ class MultiModalRetrievalModel:
         # one side stream per calling stream: callers that pipeline batches over several streams
         # (bench.py --pipeline) keep their batches independent
         if self._side is None:
-            self._side = {}
-        side = self._side.get(main.cuda_stream)
-        if side is None:
-            side = self._side[main.cuda_stream] = torch.cuda.Stream(self.device)
+            self._side = collections.OrderedDict()
+        side = ops.side_stream(self._side, main, self.device)
         side.wait_stream(main)                        # the image batch is ready
         with torch.cuda.stream(side):
             img = self.backbones.encode_image(image, want_patches=want_patches)

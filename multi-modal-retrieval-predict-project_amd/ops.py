@@ -11,6 +11,23 @@ def _L():
     return _lib.lib()
 
 
+def side_stream(cache, main, device, limit=8):
+    """The side stream paired with calling stream `main` (towers / fusion overlap): one per calling
+    stream so pipelined callers keep their batches independent, held in a small LRU (`cache`, an
+    OrderedDict keyed by the raw stream handle) — a caller creating a stream per request reuses at
+    most `limit` side streams instead of leaking one per call; a recycled handle value maps to a side
+    stream this object owns, which stays valid."""
+    key = main.cuda_stream
+    side = cache.get(key)
+    if side is None:
+        if len(cache) >= limit:
+            cache.popitem(last=False)
+        side = cache[key] = torch.cuda.Stream(device)
+    else:
+        cache.move_to_end(key)
+    return side
+
+
 def _s(t):
     return _lib.stream_ptr(t.device)
 

@@ -5,9 +5,11 @@ multi-GPU component the path needs.
 Each rank owns rows [start_r, end_r) of the gallery (balanced split).  A search:
   1. all-gather the ranks' query batches (every rank scores every query against its shard),
   2. local exact top-K on the shard (libmmr; global index = local + start_r, f64 scores),
-  3. all-gather the per-shard (f64 score, int64 index) lists — 16*Q*K bytes per rank, latency-
-     bound (30 KB at Q=256, K=10): one collective per query batch, no data-path exchange,
-  4. deterministic k-way merge: score desc, then global index asc — so the sharded result is
+  3. ONE all-gather of the per-shard lists packed into 8-byte words per entry {f64 score, int64
+     index (+ the rerank payload)} (pack_lists) — 16*Q*K bytes per rank, latency-bound (30 KB at
+     Q=256, K=10): one collective per query batch for the results, no data-path exchange,
+  4. deterministic k-way merge straight from the gathered buffer (merge_gathered ->
+     mmr_merge_topk_packed): score desc, then global index asc — so the sharded result is
      bit-identical to the single-device result (ranking on the same f64 scores).
 Sharded rerank (BASELINE config 5's KG-rerank head at world > 1; Reranker.rerank,
 src/Retrieval/reranker.py:240-333, min-max scales each component over the FINAL candidate list, so
@@ -20,7 +22,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from .retrieval import GalleryIndex, RetrievalEngine, check_status, merge_topk, rerank_mix
+from .retrieval import GalleryIndex, RetrievalEngine, check_status, merge_topk_packed, rerank_mix
 
 
 def shard_bounds(n, world):
@@ -95,15 +97,37 @@ def rerank_mix_host(cand, comp, topk, alpha=0.6, beta=0.25, gamma=0.15):
     return tuple(out)
 
 
+def pack_lists(idx, s64, comp=None):
+    """One rank's search result as the single all-gather payload: (Q, K) int64 + (Q, K) f64 (+ (Q, K, P)
+    f64 rerank components) -> (Q, K, 2 + P) f64 words {score, index bits, payload} (int64 bits carried
+    in an 8-byte slot: copies and all-gathers move bytes, nothing re-interprets them)."""
+    parts = [s64.to(torch.float64).unsqueeze(-1), idx.to(torch.int64).contiguous().view(torch.float64).unsqueeze(-1)]
+    if comp is not None:
+        parts.append(comp.to(torch.float64))
+    return torch.cat(parts, -1).contiguous()
+
+
+def merge_gathered(gathered, q0, nq, k_out, payload_width=0):
+    """The post-gather merge: gathered [world][Q][K][2 + P] (all ranks' pack_lists, world = shards)
+    -> this rank's queries [q0, q0 + nq): (idx, f32, f64) (+ payload (nq, k_out, P)).  Device tensors:
+    mmr_merge_topk_packed reads the gathered buffer directly; host tensors (gloo): merge_topk_host."""
+    if gathered.is_cuda:
+        return merge_topk_packed(gathered, k_out, payload_width, q0=q0, nq=nq)
+    g = gathered[:, q0:q0 + nq]
+    s = g[..., 0].contiguous()
+    i = g[..., 1].contiguous().view(torch.int64)
+    pay = g[..., 2:].contiguous() if payload_width else None
+    return merge_topk_host(s, i, k_out, payload=pay)
+
+
 class ShardedIndex:
     """This rank's gallery shard + the collective search.
 
     `local_search(q, k) -> (idx, f64) or (idx, f64, status)` may be injected (tests); by default it
     is the rank's GPU GalleryIndex in `mode` ("x3" | "f16" | "f32").  A non-zero per-query status
-    (candidate-buffer overflow — the library now resolves it in-kernel, so this is a guard) makes
-    those queries re-run through `fallback_search` (default: the same index in "x3", as
-    MI355XRetrievalEngine did) before the lists are exchanged, so every rank always contributes an
-    exact list."""
+    would flag an inexact list; the selection kernel resolves candidate-buffer overflow in-kernel, so
+    it never occurs — this is a guard: an injected `fallback_search` re-runs such queries, else the
+    search raises (no mode switch inside a collective: ADVICE r03)."""
 
     def __init__(self, gallery_rows, n_total, start, group=None, device=None, local_search=None, mode="x3",
                  fallback_search=None, local_components=None, index=None, status_out=None):
@@ -120,13 +144,9 @@ class ShardedIndex:
         self.status_out = status_out
         if local_search is None and index is not None:
             local_search = self._index_search
-            if fallback_search is None:
-                fallback_search = self._index_search_x3
         if local_search is None:
             self.index = GalleryIndex(gallery_rows, device=device, idx_base=start, mode=mode)
             local_search = self._index_search
-            if fallback_search is None:
-                fallback_search = self._index_search_x3
         self.local_search = local_search
         self.fallback_search = fallback_search
         self.local_components = local_components  # (q, cand) -> (nq, kc, 3) raw rerank components
@@ -135,12 +155,6 @@ class ShardedIndex:
     def _index_search(self, q, k):
         i, _, s64, st = self.index.search(q, k, want_f64=True, want_status=True)
         return i, s64, st
-
-    def _index_search_x3(self, q, k):
-        # per-call mode override: the switch and the search hold the index's lock together
-        i, _, s64, st = self.index.search(q, k, want_f64=True, want_status=True, mode="x3")
-        check_status(st)
-        return i, s64
 
     @classmethod
     def from_full(cls, gallery, group=None, device=None, local_search=None, mode="x3", fallback_search=None):
@@ -174,22 +188,25 @@ class ShardedIndex:
 
     def search(self, q_local, k):
         """Collective: every rank passes its own (b, D) queries (same b on every rank); returns
-        this rank's (idx int64 (b,k), score f32 (b,k), score f64 (b,k)) over the whole gallery."""
+        this rank's (idx int64 (b,k), score f32 (b,k), score f64 (b,k)) over the whole gallery.
+        Two collectives: the queries' all-gather and ONE packed all-gather of the result lists."""
         b = q_local.shape[0]
-        allq = torch.empty((self.world * b,) + tuple(q_local.shape[1:]), dtype=q_local.dtype,
+        allq = self._gather_queries(q_local)
+        i, s64 = self._local(allq, k)
+        g = self._gather(pack_lists(i, s64))
+        return merge_gathered(g, self.rank * b, b, k)
+
+    def _gather_queries(self, q_local):
+        allq = torch.empty((self.world * q_local.shape[0],) + tuple(q_local.shape[1:]), dtype=q_local.dtype,
                            device=q_local.device)
         dist.all_gather_into_tensor(allq, q_local.contiguous(), group=self.group)
-        i, s64 = self._local(allq, k)
-        gi = torch.empty((self.world * i.shape[0], i.shape[1]), dtype=i.dtype, device=i.device)
-        gs = torch.empty((self.world * s64.shape[0], s64.shape[1]), dtype=s64.dtype, device=s64.device)
-        dist.all_gather_into_tensor(gi, i.contiguous(), group=self.group)
-        dist.all_gather_into_tensor(gs, s64.contiguous(), group=self.group)
-        gi = gi.view(self.world, i.shape[0], i.shape[1])
-        gs = gs.view(self.world, s64.shape[0], s64.shape[1])
-        if gi.is_cuda:  # merge this rank's queries only
-            return merge_topk(gs, gi, k, q0=self.rank * b, nq=b)
-        sl = slice(self.rank * b, (self.rank + 1) * b)
-        return merge_topk_host(gs[:, sl], gi[:, sl], k)
+        return allq
+
+    def _gather(self, packed):
+        g = torch.empty((self.world * packed.shape[0],) + tuple(packed.shape[1:]), dtype=packed.dtype,
+                        device=packed.device)
+        dist.all_gather_into_tensor(g, packed, group=self.group)
+        return g.view((self.world,) + tuple(packed.shape))
 
     def _components(self, q, cand, tables):
         """Raw rerank components of this shard's candidates (nq, kc, 3) f64."""
@@ -206,24 +223,13 @@ class ShardedIndex:
         kg_n) — bit-identical to GalleryIndex.rerank of the single-index top-k."""
         b = q_local.shape[0]
         topk = k if topk is None else topk
-        allq = torch.empty((self.world * b,) + tuple(q_local.shape[1:]), dtype=q_local.dtype,
-                           device=q_local.device)
-        dist.all_gather_into_tensor(allq, q_local.contiguous(), group=self.group)
+        allq = self._gather_queries(q_local)
         i, s64 = self._local(allq, k)
         comp = self._components(allq, i, tables).to(s64.device)
-        W = self.world
-        gi = torch.empty((W * i.shape[0],) + tuple(i.shape[1:]), dtype=i.dtype, device=i.device)
-        gs = torch.empty((W * s64.shape[0],) + tuple(s64.shape[1:]), dtype=s64.dtype, device=s64.device)
-        gc = torch.empty((W * comp.shape[0],) + tuple(comp.shape[1:]), dtype=comp.dtype, device=comp.device)
-        dist.all_gather_into_tensor(gi, i.contiguous(), group=self.group)
-        dist.all_gather_into_tensor(gs, s64.contiguous(), group=self.group)
-        dist.all_gather_into_tensor(gc, comp.contiguous(), group=self.group)
-        gi, gs, gc = gi.view((W,) + tuple(i.shape)), gs.view((W,) + tuple(s64.shape)), gc.view((W,) + tuple(comp.shape))
-        if gi.is_cuda:
-            mi, _, _, mc = merge_topk(gs, gi, k, payload=gc, q0=self.rank * b, nq=b)
+        g = self._gather(pack_lists(i, s64, comp))              # one collective: lists + components
+        mi, _, _, mc = merge_gathered(g, self.rank * b, b, k, payload_width=comp.shape[-1])
+        if mi.is_cuda:
             return rerank_mix(mi, mc, topk, alpha, beta, gamma)
-        sl = slice(self.rank * b, (self.rank + 1) * b)
-        mi, _, _, mc = merge_topk_host(gs[:, sl], gi[:, sl], k, payload=gc[:, sl])
         return rerank_mix_host(mi, mc, topk, alpha, beta, gamma)
 
 

@@ -237,6 +237,26 @@ def merge_topk(scores64: torch.Tensor, idx: torch.Tensor, k_out: int, payload=No
     return (oi, os_, o64) if payload is None else (oi, os_, o64, op)
 
 
+def merge_topk_packed(packed: torch.Tensor, k_out: int, payload_width: int = 0, q0: int = 0, nq=None):
+    """Merge of ONE packed all-gather buffer [L][B][k_in][2 + P] of 8-byte words per entry = {f64 score,
+    int64 index bits, P f64 payload} (parallel.pack_lists) for queries [q0, q0 + nq) on device
+    (mmr_merge_topk_packed) -> (idx, f32, f64) or (idx, f32, f64, payload (nq, k_out, P))."""
+    _lib.require_gpu(packed)
+    L_, B, k_in, W = packed.shape
+    assert W == 2 + payload_width and packed.dtype == torch.float64
+    packed = packed.contiguous()
+    nq = B - q0 if nq is None else nq
+    dev = packed.device
+    oi = torch.empty((nq, k_out), dtype=torch.int64, device=dev)
+    os_ = torch.empty((nq, k_out), dtype=torch.float32, device=dev)
+    o64 = torch.empty((nq, k_out), dtype=torch.float64, device=dev)
+    op = torch.empty((nq, k_out, payload_width), dtype=torch.float64, device=dev) if payload_width else None
+    _lib.check(_lib.lib().mmr_merge_topk_packed(_lib.ptr(packed), payload_width, L_, B, q0, nq, k_in, k_out,
+                                                _lib.ptr(oi), _lib.ptr(os_), _lib.ptr(o64), _lib.ptr(op),
+                                                _lib.stream_ptr(dev)), "mmr_merge_topk_packed")
+    return (oi, os_, o64) if op is None else (oi, os_, o64, op)
+
+
 def rerank_mix(cand: torch.Tensor, comp: torch.Tensor, topk: int, alpha=0.6, beta=0.25, gamma=0.15,
                want_components=True):
     """After the shard merge (mmr_rerank_mix): cand (nq, kc) global indices (-1 = empty) + their raw

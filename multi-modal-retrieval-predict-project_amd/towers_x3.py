@@ -147,6 +147,18 @@ class BertTowerX3:
                 "ln2_g": _f(sd[p + "output.LayerNorm.weight"], dev), "ln2_b": _f(sd[p + "output.LayerNorm.bias"], dev),
             })
         self.hidden = self.word.shape[1]
+        self.gemm_events = None  # as BertTower.gemm_events (the bench's per-GEMM roofline pass)
+
+    def _gemm(self, name, x, w, b, act=0):
+        ev = self.gemm_events
+        if ev is None:
+            return ops.x3_linear(x, w, b, act=act)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        y = ops.x3_linear(x, w, b, act=act)
+        e1.record()
+        ev.setdefault(name, []).append((e0, e1))
+        return y
 
     def forward(self, input_ids, attention_mask=None):
         """(B, L) ids / mask -> (B, L, C) f32 last_hidden_state (L truncated to max_position_embeddings)."""
@@ -165,12 +177,12 @@ class BertTowerX3:
         dh = C // heads
         h = ops.x3_bert_embed(ids, self.word, self.pos, self.type0, self.eg, self.eb, 1e-12)
         for ly in self.layers:
-            qkv = ops.x3_linear(h, ly["qkv_w"], ly["qkv_b"]).view(B * L, 3 * C)
+            qkv = self._gemm("qkv", h, ly["qkv_w"], ly["qkv_b"]).view(B * L, 3 * C)
             ctx = torch.empty((B, L, C), dtype=torch.float32, device=self.device)
             ops.x3_attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], B, L, L, heads, dh, 1.0 / math.sqrt(dh),
                              out=ctx.view(B * L, C), mask=mask)
-            a = ops.x3_linear(ctx, ly["o_w"], ly["o_b"])
+            a = self._gemm("o", ctx, ly["o_w"], ly["o_b"])
             h = _ln(a, ly["ln1_g"], ly["ln1_b"], 1e-12, residual=h)           # LN(dense(ctx) + h)
-            f = ops.x3_linear(ops.x3_linear(h, ly["i_w"], ly["i_b"], act=1), ly["f_w"], ly["f_b"])
+            f = self._gemm("ffn2", self._gemm("ffn1", h, ly["i_w"], ly["i_b"], act=1), ly["f_w"], ly["f_b"])
             h = _ln(f, ly["ln2_g"], ly["ln2_b"], 1e-12, residual=h)
         return h

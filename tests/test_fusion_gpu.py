@@ -273,3 +273,24 @@ def test_fusion_stack_fp8_vs_oracle():
     assert cos.min().item() >= 0.995, cos
     assert rel_err(got8, ref) <= 1e-1
     assert not torch.equal(got8, got.detach().float().cpu()[rows])  # the fp8 path really ran
+
+
+def test_fusion_stack_fp8_head_dim_not_multiple_of_32_falls_back():
+    """tower_dtype="fp8" with D = 768 and 16 heads (head_dim 48): the MX-fp8 attention
+    output needs head_dim % 32 == 0, so every enhancer / o2 path stays bf16 (no MMRError) and the
+    result matches the oracle like the bf16 stack."""
+    g = torch.Generator().manual_seed(14)
+    B, Lt, Np, C, D, H = 256, 128, 49, 768, 768, 16
+    hs = init_head_state(C, C, D, 27)
+    hs.update(init_fusion_state(C, C, D, H, 2, 28))
+    G = torch.randn(B, C, generator=g)
+    P = torch.randn(B, Np, C, generator=g)
+    T = bf(torch.randn(B, Lt, C, generator=g)).float()
+    from mmr_amd.fusion import FusionStack
+    fs8 = FusionStack(hs, H, device=DEV, tower_dtype="fp8")
+    assert not any(L["txt"].fp8_ok(B * Lt) or L["patch"].fp8_ok(B * Np) for L in fs8.layers)
+    got8 = fs8.forward(G.to(DEV), P.to(DEV), T.to(DEV))
+    rows = [0, 100, 255]
+    with torch.no_grad():
+        ref = otw.multimodal(G[rows], P[rows], T[rows], hs, num_heads=H)
+    _check_emb(got8[rows], ref)

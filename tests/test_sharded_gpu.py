@@ -162,3 +162,100 @@ def test_sharded_rerank_world2_matches_single_index():
         np.testing.assert_array_equal(got[0], ref[0][sl])
         for a, b in zip(got[1:], ref[1:]):
             np.testing.assert_allclose(a, b[sl], rtol=0, atol=1e-12)
+
+
+def _simulated_gather(shards, Q, K, world, comps=None):
+    """What the all-gather delivers on the 8-GPU node, built on one GPU: every shard searches ALL
+    world*b queries, packs its lists (pack_lists) and the packs are stacked in rank order
+    ([world][world*b][K][2 + P], the layout all_gather_into_tensor produces)."""
+    from mmr_amd.parallel import pack_lists
+    packs = []
+    for r, ix in enumerate(shards):
+        i, _, s64 = ix.search(Q, K, want_f64=True)
+        packs.append(pack_lists(i, s64, comps[r](Q, i) if comps else None))
+    return torch.stack(packs)
+
+
+@pytest.mark.parametrize("mode", ["f16", "x3"])
+def test_device_merge_simulated_world2_equals_single_index(mode):
+    """The device branch of ShardedIndex.search (merge_gathered -> mmr_merge_topk_packed straight
+    from the gathered buffer, each rank merging its own queries q0 = rank*b) on one GPU with a
+    simulated 2-rank gather: bit-identical to one index over the whole gallery (indices, f32 and f64
+    scores), exact duplicates across the shards tie-broken by global index."""
+    from mmr_amd.parallel import merge_gathered
+    N, D, B, K, world = 30_011, 384, 24, 16, 2
+    G = _gallery(N, D)
+    Q = synthetic.gauss_gallery(world * B, D, 502)
+    Q[0] = G[17]
+    Qd = torch.from_numpy(Q).cuda()
+    shards = [GalleryIndex(G[s:e], device=0, idx_base=s, mode=mode) for s, e in shard_bounds(N, world)]
+    g = _simulated_gather(shards, Qd, K, world)
+    ix = GalleryIndex(G, mode=mode)
+    si, ss, s64 = ix.search(Qd, K, want_f64=True)
+    for rank in range(world):
+        mi, ms, m64 = merge_gathered(g, rank * B, B, K)
+        assert mi.is_cuda
+        sl = slice(rank * B, (rank + 1) * B)
+        assert torch.equal(mi, si[sl]) and torch.equal(m64, s64[sl]) and torch.equal(ms, ss[sl])
+    assert si[0, :2].tolist() == [17, N - 5]
+    for x in shards + [ix]:
+        x.close()
+
+
+def test_device_merge_simulated_world2_rerank_equals_single_index():
+    """ShardedIndex.search_rerank's device branch (components ride in the same packed gather,
+    merge_gathered with payload, then mmr_rerank_mix) on one GPU, simulated 2-rank gather:
+    equal to the single-index fused rerank (order exactly, components within 1e-12)."""
+    from mmr_amd.parallel import merge_gathered
+    from mmr_amd.retrieval import rerank_mix
+    N, D, B, K, DK, world = 20_011, 256, 16, 12, 64, 2
+    G, gb, qb, gk, qk = _rerank_data(N, D, world * B, DK)
+    Q = torch.from_numpy(synthetic.gauss_gallery(world * B, D, 512)).cuda()
+    dev = torch.device("cuda:0")
+    bounds = shard_bounds(N, world)
+    shards = [GalleryIndex(G[s:e], device=0, idx_base=s, mode="f16") for s, e in bounds]
+    comps = [(lambda q, cand, ix=ix, s=s, e=e: ix.rerank_components(q, cand, _t(qb, dev), _t(gb[s:e], dev),
+                                                                     _t(qk, dev), _t(gk[s:e], dev)))
+             for ix, (s, e) in zip(shards, bounds)]
+    g = _simulated_gather(shards, Q, K, world, comps)
+    ix = GalleryIndex(G, mode="f16")
+    i = ix.search(Q, K)[0]
+    ref = ix.rerank(Q, i, _t(qb, dev), _t(gb, dev), _t(qk, dev), _t(gk, dev), K)
+    for rank in range(world):
+        mi, _, _, mc = merge_gathered(g, rank * B, B, K, payload_width=3)
+        out = rerank_mix(mi, mc, K)
+        sl = slice(rank * B, (rank + 1) * B)
+        assert torch.equal(out[0], ref[0][sl])
+        for a, b in zip(out[1:], ref[1:]):
+            assert (a - b[sl]).abs().max().item() <= 1e-12
+    for x in shards + [ix]:
+        x.close()
+
+
+def test_set_mode_failure_keeps_index_usable():
+    """a mode switch whose copies cannot be built (here a real device OOM: the free memory
+    is taken first) must leave the index in its previous mode with its copies intact — the next
+    search in that mode returns the exact list (it used to scan a freed fp16 copy)."""
+    from mmr_amd._lib import MMRError
+    N, D, B, K = 200_000, 1024, 16, 10
+    G = synthetic.gauss_gallery(N, D, 601)
+    Q = torch.from_numpy(synthetic.gauss_gallery(B, D, 602)).cuda()
+    ix = GalleryIndex(G, mode="f16")
+    ref_i, _, ref64 = ix.search(Q, K, want_f64=True)
+    torch.cuda.synchronize()
+    free, _ = torch.cuda.mem_get_info()
+    hog = torch.empty(max(0, free - (256 << 20)), dtype=torch.uint8, device="cuda")  # x3 copies need ~1.6 GB
+    try:
+        with pytest.raises(MMRError):
+            ix.set_mode("x3")
+        i, _, s64 = ix.search(Q, K, want_f64=True)
+        assert torch.equal(i, ref_i) and torch.equal(s64, ref64)
+        gb, _ = ix.device_bytes()
+        assert gb <= N * D * 4 + N * 12 + 2 * (N + 256) * D * 2 + (1 << 20)  # f32 rows + fp16 copies only
+    finally:
+        del hog
+        torch.cuda.empty_cache()
+    ix.set_mode("x3")
+    i, _, s64 = ix.search(Q, K, want_f64=True)
+    assert torch.equal(i, ref_i) and torch.equal(s64, ref64)
+    ix.close()
