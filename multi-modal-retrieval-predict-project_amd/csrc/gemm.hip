@@ -580,7 +580,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
                                                        uint8_t* __restrict__ YS = nullptr,
                                                        float* __restrict__ GM = nullptr, float* __restrict__ BM = nullptr,
                                                        int64_t ldG = 0, int64_t ldB = 0, int64_t nval = 0,
-                                                       int ntst = 0) {
+                                                       int ntst = 0, const float* __restrict__ RS = nullptr) {
   static_assert(!OUT8 || (FP8 && NT == 4 && !HAS_RES), "OUT8: MX-fp8 256x256 tiles without residual");
   static_assert(KNN == 0 || ((KNN == 2 || KNN == 4) && NT == 4 && !FP8 && !HAS_BIAS && !HAS_RES && ACT == 0),
                 "KNN (rows per unit 2 / 4): plain 256x256 fp16 tiles");
@@ -655,6 +655,14 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   const int row0 = 8 * wave + prow;
   const uint32_t off0 = (uint32_t)(row0 * K * ESZ + swz(row0, pch) * 16);
   const uint32_t pstride = (uint32_t)(64 * K * ESZ);  // bytes between consecutive pieces of an operand
+  // KNN: the gallery W is in the index's tile32h layout (16-row x 32-half 1-KB pieces, knn.hip
+  // tile32h_index) — the same image every other fp16 scan reads, so the index keeps ONE fp16 copy.
+  // Logical chunk c of row r in K-tile kt = piece (r/16, 2 kt + c/4), lane slot (c%4) 16 + r%16: the
+  // per-lane offset is fixed, a K-tile adds 2 KB (uniform soffset), and 64 rows are still pstride.
+  const int wch = swz(row0, pch);
+  const uint32_t off0w = KNN ? (uint32_t)(((row0 >> 4) * (K / 32) + (wch >> 2)) * 1024 + (((wch & 3) << 4) + (row0 & 15)) * 16)
+                             : off0;
+  constexpr int KTW = KNN ? 2048 : KB * 2;  // W bytes per K-tile
   const int nk = K * ESZ / 128;  // 128-byte K-tiles; even (launcher)
   // operand panels as buffer descriptors (uniform, SGPRs): a piece is buffer_load ... lds with the
   // per-lane offset in voffset and the K-tile offset in soffset — no per-piece address registers
@@ -685,8 +693,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
                                              kt * (KB * 2) + j * pstride, 0, 0);
   };
   auto gB = [&](__amdgpu_buffer_rsrc_t wb, int buf, int j, int kt) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(wb, (lds_ptr_t)(dsm + boff(buf) + (64 * j + 8 * wave) * KB), 16, off0,
-                                             kt * (KB * 2) + j * pstride, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wb, (lds_ptr_t)(dsm + boff(buf) + (64 * j + 8 * wave) * KB), 16, off0w,
+                                             kt * KTW + j * pstride, 0, 0);
   };
   // fragment reads: the swizzle of row 16i + fr is a function of fr only, so every A (B) fragment
   // address is one of two per-lane bases (k-step 0 / 1: logical chunk fq or 4 + fq) plus an
@@ -924,6 +932,15 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
       // 4 efq) = the 2-row units rj / 2 and rj / 2 + 1 (one 8-B store); the wave column's 64 rows =
       // one block.  Every store issued (NSTORE exact for the next tile's counted wait)
       const int64_t r0 = n0 + wc * 64;
+      // RS (raw-row galleries, the native fp16 index): the per-row 1 / |g| turning q^ . g into the cosine
+      f32x4 rs[4];
+      if (RS) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) rs[j] = *(const f32x4*)(RS + r0 + 16 * j + 4 * efq);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) rs[j] = (f32x4){1.f, 1.f, 1.f, 1.f};
+      }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int64_t q = m0 + wr * 128 + i * 16 + efr;
@@ -933,7 +950,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
           const int64_t rj = r0 + 16 * j + 4 * efq;
           float a[4];
 #pragma unroll
-          for (int rg = 0; rg < 4; ++rg) a[rg] = rj + rg < nval ? acc[i][j][rg] : -INFINITY;
+          for (int rg = 0; rg < 4; ++rg) a[rg] = rj + rg < nval ? acc[i][j][rg] * rs[j][rg] : -INFINITY;
           const float2 u2 = make_float2(fmaxf(a[0], a[1]), fmaxf(a[2], a[3]));
           if constexpr (skip_gm) {
             asm volatile("" ::"v"(u2.x), "v"(u2.y));
@@ -1730,21 +1747,23 @@ extern "C" mmr_status mmr_linear_mxfp8_q8(const uint8_t* xq, const uint8_t* xs, 
 
 namespace mmr {
 // The fp16 kNN scan on the persistent 8-phase GEMM (gemm_bf16_tn_p8<KNN>): qh [256 tiles_m][K] fp16
-// unit queries (zero rows past the pass; tiles_m 1 or 2), gh [tiles_n * 256][K] fp16 unit gallery rows
-// (zero rows past nval); writes unit maxima of unit_rows (2 or 4) consecutive rows gm [256 tiles_m][ldG]
-// (ldG >= tiles_n * 256 / unit_rows) and block maxima bm [256 tiles_m][ldB].
+// unit queries, row-major (zero rows past the pass; tiles_m 1-4), gh = the index's fp16 gallery in the
+// tile32h layout, tiles_n * 256 rows (zero rows past nval); rs (optional) the per-row inverse norms of a
+// raw-row gallery (NULL: unit rows); writes unit maxima of unit_rows (2 or 4) consecutive rows gm
+// [256 tiles_m][ldG] (ldG >= tiles_n * 256 / unit_rows) and block maxima bm [256 tiles_m][ldB].
 // K % 128 == 0 (the caller checks).
 hipError_t knn_scan_p8(const uint16_t* qh, const uint16_t* gh, int K, int tiles_n, int64_t nval, float* gm,
-                       int64_t ldG, float* bm, int64_t ldB, int unit_rows, hipStream_t st, int tiles_m) {
+                       int64_t ldG, float* bm, int64_t ldB, int unit_rows, hipStream_t st, int tiles_m,
+                       const float* rs) {
   const int grid = std::max(8, std::min(cu_count(), tiles_m * tiles_n) / 8 * 8);
   if (unit_rows == 2)
     gemm_bf16_tn_p8<4, 0, false, false, false, false, 2><<<dim3(grid), dim3(512), P8<4>::LDS_B, st>>>(
         qh, gh, nullptr, nullptr, nullptr, 256 * tiles_m, tiles_n * 256, K, tiles_m, tiles_n, nullptr, nullptr, nullptr,
-        gm, bm, ldG, ldB, nval);
+        gm, bm, ldG, ldB, nval, 0, rs);
   else
     gemm_bf16_tn_p8<4, 0, false, false, false, false, 4><<<dim3(grid), dim3(512), P8<4>::LDS_B, st>>>(
         qh, gh, nullptr, nullptr, nullptr, 256 * tiles_m, tiles_n * 256, K, tiles_m, tiles_n, nullptr, nullptr, nullptr,
-        gm, bm, ldG, ldB, nval);
+        gm, bm, ldG, ldB, nval, 0, rs);
   return hipGetLastError();
 }
 }  // namespace mmr

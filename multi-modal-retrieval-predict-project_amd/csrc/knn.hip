@@ -45,7 +45,7 @@
 namespace mmr {
 hipError_t knn_scan_p8(const uint16_t* qh, const uint16_t* gh, int K, int tiles_n, int64_t nval, float* gm,
                        int64_t ldG, float* bm, int64_t ldB, int unit_rows, hipStream_t st,
-                       int tiles_m = 1);  // gemm.hip
+                       int tiles_m = 1, const float* rs = nullptr);  // gemm.hip
 }
 
 namespace {
@@ -110,6 +110,54 @@ __host__ __device__ __forceinline__ int64_t tile16_index(int64_t row, int k, int
 // ((row/16)*(Dp/32) + k/32)*512 + ((k%32)/8*16 + row%16)*8 + k%8.
 __host__ __device__ __forceinline__ int64_t tile32h_index(int64_t row, int k, int Dp) {
   return ((row >> 4) * (Dp >> 5) + (k >> 5)) * 512 + ((((k & 31) >> 3) << 4) + (row & 15)) * 8 + (k & 7);
+}
+
+// 4 fp16 (one 8-B load) -> float4 (exact)
+__device__ __forceinline__ float4 h4_to_f4(uint2 u) {
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  const h4 v = __builtin_bit_cast(h4, u);
+  return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+}
+
+// element (row, k) of the gallery as f64: the f32 rows, or the native fp16 index's raw tile32h rows
+__device__ __forceinline__ double gal_elem(const float* gal, const uint16_t* galh, int64_t row, int k, int Dp) {
+  if (galh) return (double)(float)__builtin_bit_cast(_Float16, galh[tile32h_index(row, k, Dp)]);
+  return (double)gal[row * Dp + k];
+}
+
+// native fp16 gallery (mmr_index_create with MMR_F16): the raw rows [n][d] fp16 -> the tile32h image
+// gh [Np][Dp] (zero padded; it is both the scan operand and the exact rows of the f64 re-score) + the
+// f64 norms / f32 inverse norms of the f32-upcast values, summed in knn_prep_gallery's order (so an
+// fp16 index and an f32 index of the upcast rows hold bit-identical norms).  One wave per row.
+__global__ __launch_bounds__(256) void knn_prep_gallery_f16(const uint16_t* __restrict__ src, int64_t n, int d,
+                                                            uint16_t* __restrict__ gh, int Dp, int64_t Np,
+                                                            float* __restrict__ inv_norm, double* __restrict__ norm64) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= Np) return;
+  double ss = 0.0;
+  for (int k = lane; k < Dp; k += 64) {
+    const uint16_t v = (row < n && k < d) ? src[row * (int64_t)d + k] : (uint16_t)0;
+    gh[tile32h_index(row, k, Dp)] = v;
+    const double x = (double)(float)__builtin_bit_cast(_Float16, v);
+    ss += x * x;
+  }
+  ss = mmr::wave_sum(ss);
+  if (lane == 0) {
+    const double nrm = sqrt(ss);
+    norm64[row] = nrm;
+    inv_norm[row] = nrm > 0.0 ? (float)(1.0 / nrm) : 0.0f;
+  }
+}
+
+// rows [row0, row0 + nrows) of a native fp16 index -> f32 [nrows][d] (the link graph's self-join queries)
+__global__ __launch_bounds__(256) void knn_rows_from_f16(const uint16_t* __restrict__ gh, int64_t row0, int64_t nrows,
+                                                         int d, int Dp, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nrows * d) return;
+  const int64_t r = i / d;
+  const int k = (int)(i % d);
+  out[i] = (float)__builtin_bit_cast(_Float16, gh[tile32h_index(row0 + r, k, Dp)]);
 }
 
 __global__ __launch_bounds__(256) void knn_prep_queries(const float* __restrict__ q, int64_t nq,
@@ -337,24 +385,6 @@ __global__ __launch_bounds__(256) void knn_tile_gallery_f16(const float* __restr
   ((h8*)gh)[i] = v;
 }
 
-// row-major fp16 unit rows [total8 / (Dp/8)][Dp] (rows >= Np zero): the p8 scan's gallery operand
-__global__ __launch_bounds__(256) void knn_rows_f16(const float* __restrict__ gal, const float* __restrict__ inv_g,
-                                                    int64_t Np, int Dp, int64_t total8, uint16_t* __restrict__ ghr) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // 16-B unit index in ghr
-  if (i >= total8) return;
-  const int64_t row = i / (Dp >> 3);
-  const int c8 = (int)(i % (Dp >> 3));
-  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-  h8 v = (h8){0, 0, 0, 0, 0, 0, 0, 0};
-  if (row < Np) {
-    const float ig = inv_g[row];
-    const float* src = gal + row * Dp + c8 * 8;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = (_Float16)(src[e] * ig);
-  }
-  ((h8*)ghr)[i] = v;
-}
-
 __device__ __forceinline__ int xswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
 // S[m][n] = inv_g[n] * sum_k' Qs[m][k'] Gs'[n][k'] over K' = 3 Dp; tile 128 x 128 x 64, 4 waves
@@ -488,7 +518,8 @@ __global__ __launch_bounds__(64 * WQ) void knn_scan_f16_gmax(const uint16_t* __r
                                                         const float* __restrict__ qraw, int64_t nq, int d,
                                                         const uint16_t* __restrict__ gh,
                                                         float* __restrict__ gmax, float* __restrict__ bmax,
-                                                        int Dp, int64_t ldG, int64_t ldB, int64_t n) {
+                                                        int Dp, int64_t ldG, int64_t ldB, int64_t n,
+                                                        const float* __restrict__ rs = nullptr) {
   typedef _Float16 h8 __attribute__((ext_vector_type(8)));
   constexpr int L = KC / 32;  // 1-KB pieces per tile per chunk
   static_assert(!RAW || WQ == 1, "raw queries: one wave per block");
@@ -597,15 +628,19 @@ __global__ __launch_bounds__(64 * WQ) void knn_scan_f16_gmax(const uint16_t* __r
   mma(kc);
   const int64_t gcol = blk * 16 + r;
   bool pad[4];
+  float rsv[4];  // raw-row (native fp16) gallery: 1 / |g| per row, else 1
 #pragma unroll
-  for (int j = 0; j < 4; ++j) pad[j] = g0 + 16 * j + r >= n;
+  for (int j = 0; j < 4; ++j) {
+    pad[j] = g0 + 16 * j + r >= n;
+    rsv[j] = rs ? rs[g0 + 16 * j + r] : 1.f;
+  }
 #pragma unroll
   for (int t = 0; t < QT; ++t)
 #pragma unroll
     for (int rg = 0; rg < 4; ++rg) {
       float mx = -INFINITY;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) mx = fmaxf(mx, pad[j] ? -INFINITY : acc[t][j][rg]);
+      for (int j = 0; j < 4; ++j) mx = fmaxf(mx, pad[j] ? -INFINITY : acc[t][j][rg] * rsv[j]);
       const int64_t qrw = 16 * (wq * QT + t) + 4 * h + rg;
       gmax[qrw * ldG + gcol] = mx;
       // block max over the 16 lanes of this h (rows r of the block's 4 tiles)
@@ -627,7 +662,7 @@ __global__ __launch_bounds__(64 * NWV) void knn_scan_f16_lq(const float* __restr
                                                           const uint16_t* __restrict__ gh,
                                                           float* __restrict__ gmax, float* __restrict__ bmax,
                                                           int Dp, int64_t ldG, int64_t ldB, int64_t n, int64_t nblk,
-                                                          double* __restrict__ qpre) {
+                                                          double* __restrict__ qpre, const float* __restrict__ rs) {
   typedef _Float16 h8 __attribute__((ext_vector_type(8)));
   constexpr int L = KC / 32;  // 1-KB pieces per tile per chunk
   extern __shared__ __attribute__((aligned(16))) uint16_t qs[];  // [QT][Dp/32][512] halfs
@@ -717,15 +752,19 @@ __global__ __launch_bounds__(64 * NWV) void knn_scan_f16_lq(const float* __restr
     mma(kc);
     const int64_t gcol = blk * 16 + r;
     bool pad[4];
+    float rsv[4];  // raw-row (native fp16) gallery: 1 / |g| per row, else 1
 #pragma unroll
-    for (int j = 0; j < 4; ++j) pad[j] = g0 + 16 * j + r >= n;
+    for (int j = 0; j < 4; ++j) {
+      pad[j] = g0 + 16 * j + r >= n;
+      rsv[j] = rs ? rs[g0 + 16 * j + r] : 1.f;
+    }
 #pragma unroll
     for (int t = 0; t < QT; ++t)
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg) {
         float mx = -INFINITY;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) mx = fmaxf(mx, pad[j] ? -INFINITY : acc[t][j][rg]);
+        for (int j = 0; j < 4; ++j) mx = fmaxf(mx, pad[j] ? -INFINITY : acc[t][j][rg] * rsv[j]);
         const int64_t qrw = 16 * t + 4 * h + rg;
         gmax[qrw * ldG + gcol] = mx;
         float bm = mx;
@@ -817,7 +856,7 @@ __global__ __launch_bounds__(64 * WQ * WR) void knn_scan_f16_tile(const uint16_t
                                                                   const uint16_t* __restrict__ gh,
                                                                   float* __restrict__ gmax, float* __restrict__ bmax,
                                                                   int Dp, int64_t ldG, int64_t ldB, int64_t n,
-                                                                  int64_t n_rt) {
+                                                                  int64_t n_rt, const float* __restrict__ rs) {
   using C = F16TileCfg<WQ, MQ, WR, MR, PF>;
   typedef _Float16 h8 __attribute__((ext_vector_type(8)));
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];  // [STAGES][P][512] halfs
@@ -830,7 +869,6 @@ __global__ __launch_bounds__(64 * WQ * WR) void knn_scan_f16_tile(const uint16_t
   if (lo >= hi) return;
   const int KP = Dp / 32;                          // k-pieces = slices per tile
   const int ntiles = (int)((hi - lo + C::RT - 1) / C::RT);
-  const int nslices = ntiles * KP;
   const int64_t tile_b = (int64_t)KP * 1024;       // bytes of one 16-row tile (all k-pieces)
   // this wave's glds pieces p0 .. p0+PW-1: gallery row tiles (p < RT), then query tiles
   const int p0 = wave * C::PW;
@@ -947,9 +985,11 @@ __global__ __launch_bounds__(64 * WQ * WR) void knn_scan_f16_tile(const uint16_t
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const int64_t r0 = (rtb + c) * 16 + 4 * h;
+            const int64_t rc = r0 < 16 * n_rt ? r0 : 16 * n_rt - 4;  // past-range row tiles: clamped (discarded)
+            const f32x4 rv = rs ? *(const f32x4*)(rs + rc) : (f32x4){1.f, 1.f, 1.f, 1.f};
             float mx = -INFINITY;
 #pragma unroll
-            for (int rg = 0; rg < 4; ++rg) mx = fmaxf(mx, r0 + rg < n ? acc[t][4 * b4 + c][rg] : -INFINITY);
+            for (int rg = 0; rg < 4; ++rg) mx = fmaxf(mx, r0 + rg < n ? acc[t][4 * b4 + c][rg] * rv[rg] : -INFINITY);
             v[c] = mx;
           }
           const f32x4 o = transpose4(v, h, qc);
@@ -1222,9 +1262,8 @@ __device__ __forceinline__ int64_t unit_row(int64_t u, int m) {
 }
 
 constexpr int kBlkCap = 1024;
-// A/B switch of the select's first bound (MMR_KNN_TOP4=0: the 2-pass radix), set by mmr_index_create
-__constant__ int g_top4_bound = 1;
-__device__ __forceinline__ bool top4_bound_enabled() { return g_top4_bound != 0; }  // 64-row blocks collected by the coarse pass (more: the unit-level pass)
+// the select's first bound from per-wave top-4 keys (K <= 32; else the 2-pass radix)
+__device__ __forceinline__ constexpr bool top4_bound_enabled() { return true; }
 
 template <int T>
 struct SelLds {
@@ -1360,6 +1399,7 @@ __global__ __launch_bounds__(T) void knn_select_t(
     const float* __restrict__ bvals, int64_t ldB, float two_delta_abs,
     const float* __restrict__ q_raw, int d, const double* __restrict__ qnorm64,
     const float* __restrict__ gal, int Dp, const double* __restrict__ gnorm64, int64_t idx_base,
+    const uint16_t* __restrict__ galh,
     int64_t* __restrict__ out_idx, float* __restrict__ out_score, double* __restrict__ out_score64,
     int32_t* __restrict__ status, const double* __restrict__ qpre = nullptr) {
   constexpr int GS = MODE == 0 ? 1 : MODE == 3 ? 2 : 4;  // rows per unit
@@ -1563,18 +1603,34 @@ __global__ __launch_bounds__(T) void knn_select_t(
         // wait for it before the next — 9 serial round trips, measured 5 us of the 12 us select):
         // padding slots read row 0 (score discarded), lanes past Dp re-read the row's last float4
         // (their query elements in LDS are 0, so the product is 0)
+        if (galh) {  // native fp16 gallery: the raw rows from the tile32h image (4 halfs = 8 B per load)
 #pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          const int s = s0 + r;
-          const int64_t gi = s < nslot ? L.row_s[kMaxK + s] : n;
-          gir[r] = gi;
-          const int64_t gl = gi < n ? gi : 0;
-          gnr[r] = gnorm64[gl];
-          const float* gr = gal + gl * Dp;
+          for (int r = 0; r < RB; ++r) {
+            const int s = s0 + r;
+            const int64_t gi = s < nslot ? L.row_s[kMaxK + s] : n;
+            gir[r] = gi;
+            const int64_t gl = gi < n ? gi : 0;
+            gnr[r] = gnorm64[gl];
 #pragma unroll
-          for (int c = 0; c < NC; ++c) {
-            const int e = c * 256 + lane * 4;
-            gv[r][c] = *(const float4*)(gr + (e < Dp ? e : Dp - 4));
+            for (int c = 0; c < NC; ++c) {
+              const int e = c * 256 + lane * 4;
+              gv[r][c] = h4_to_f4(*(const uint2*)(galh + tile32h_index(gl, e < Dp ? e : Dp - 4, Dp)));
+            }
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < RB; ++r) {
+            const int s = s0 + r;
+            const int64_t gi = s < nslot ? L.row_s[kMaxK + s] : n;
+            gir[r] = gi;
+            const int64_t gl = gi < n ? gi : 0;
+            gnr[r] = gnorm64[gl];
+            const float* gr = gal + gl * Dp;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+              const int e = c * 256 + lane * 4;
+              gv[r][c] = *(const float4*)(gr + (e < Dp ? e : Dp - 4));
+            }
           }
         }
 #pragma unroll
@@ -1599,9 +1655,8 @@ __global__ __launch_bounds__(T) void knn_select_t(
         const int64_t gi = L.row_s[kMaxK + s];
         double sc = -INFINITY;
         if (gi < n) {
-          const float* gr = gal + gi * Dp;
           double acc = 0.0;
-          for (int kq = lane; kq < d; kq += 64) acc += (double)qr[kq] * (double)gr[kq];
+          for (int kq = lane; kq < d; kq += 64) acc += (double)qr[kq] * gal_elem(gal, galh, gi, kq, Dp);
           acc = mmr::wave_sum(acc);
           const double gn = gnorm64[gi];
           sc = (qn > 0.0 && gn > 0.0) ? acc / (qn * gn) : 0.0;
@@ -1926,7 +1981,8 @@ struct RerankRaw {
   double e, lab, kg;
   int64_t my;
 };
-__device__ RerankRaw rerank_raw(const float* __restrict__ qe, int d, const float* __restrict__ gal, int Dp,
+__device__ RerankRaw rerank_raw(const float* __restrict__ qe, int d, const float* __restrict__ gal,
+                                const uint16_t* __restrict__ galh, int Dp,
                                 const double* __restrict__ gnorm64, int64_t n, int64_t idx_base,
                                 const int64_t* __restrict__ cand, int kc, const uint64_t* __restrict__ qlab,
                                 const uint64_t* __restrict__ glab, const float* __restrict__ qkg,
@@ -1944,9 +2000,8 @@ __device__ RerankRaw rerank_raw(const float* __restrict__ qe, int d, const float
     const bool ok = cq[c] >= 0 && g >= 0 && g < n;
     double de = 0.0, dkg = 0.0, gk = 0.0;
     if (ok) {
-      const float* gr = gal + g * Dp;
       const float* gq = gkg + g * (int64_t)dk;
-      for (int t = lane; t < d; t += 64) de += (double)qr[t] * (double)gr[t];
+      for (int t = lane; t < d; t += 64) de += (double)qr[t] * gal_elem(gal, galh, g, t, Dp);
       for (int t = lane; t < dk; t += 64) {
         dkg += (double)qk[t] * (double)gq[t];
         gk += (double)gq[t] * (double)gq[t];
@@ -1998,7 +2053,7 @@ __device__ void rerank_mix_out(double e, double lab, double kgs, bool valid, int
 }
 
 __global__ __launch_bounds__(64) void knn_rerank(
-    const float* __restrict__ qe, int d, const float* __restrict__ gal, int Dp,
+    const float* __restrict__ qe, int d, const float* __restrict__ gal, const uint16_t* __restrict__ galh, int Dp,
     const double* __restrict__ gnorm64, int64_t n, int64_t idx_base, const int64_t* __restrict__ cand,
     int kc, const uint64_t* __restrict__ qlab, const uint64_t* __restrict__ glab,
     const float* __restrict__ qkg, const float* __restrict__ gkg, int dk, double wa, double wb,
@@ -2006,7 +2061,7 @@ __global__ __launch_bounds__(64) void knn_rerank(
     double* __restrict__ out_emb, double* __restrict__ out_lab, double* __restrict__ out_kg) {
   const int64_t qi = blockIdx.x;
   const int lane = threadIdx.x;
-  const RerankRaw r = rerank_raw(qe, d, gal, Dp, gnorm64, n, idx_base, cand, kc, qlab, glab, qkg, gkg, dk, qi, lane);
+  const RerankRaw r = rerank_raw(qe, d, gal, galh, Dp, gnorm64, n, idx_base, cand, kc, qlab, glab, qkg, gkg, dk, qi, lane);
   rerank_mix_out(r.e, r.lab, r.kg, lane < kc && r.my >= 0, r.my + idx_base, wa, wb, wg, topk, qi, lane, out_idx,
                  out_final, out_emb, out_lab, out_kg);
 }
@@ -2014,13 +2069,13 @@ __global__ __launch_bounds__(64) void knn_rerank(
 // Sharded rerank, shard side: the raw components of this shard's candidates -> comp [nq][kc][3]
 // (zeros for an empty slot).
 __global__ __launch_bounds__(64) void knn_rerank_comp(
-    const float* __restrict__ qe, int d, const float* __restrict__ gal, int Dp,
+    const float* __restrict__ qe, int d, const float* __restrict__ gal, const uint16_t* __restrict__ galh, int Dp,
     const double* __restrict__ gnorm64, int64_t n, int64_t idx_base, const int64_t* __restrict__ cand,
     int kc, const uint64_t* __restrict__ qlab, const uint64_t* __restrict__ glab,
     const float* __restrict__ qkg, const float* __restrict__ gkg, int dk, double* __restrict__ comp) {
   const int64_t qi = blockIdx.x;
   const int lane = threadIdx.x;
-  const RerankRaw r = rerank_raw(qe, d, gal, Dp, gnorm64, n, idx_base, cand, kc, qlab, glab, qkg, gkg, dk, qi, lane);
+  const RerankRaw r = rerank_raw(qe, d, gal, galh, Dp, gnorm64, n, idx_base, cand, kc, qlab, glab, qkg, gkg, dk, qi, lane);
   if (lane < kc) {
     double* o = comp + (qi * kc + lane) * 3;
     o[0] = r.e;
@@ -2051,15 +2106,17 @@ struct mmr_index {
   int device = 0;
   int64_t n = 0, Np = 0, idx_base = 0;
   int d = 0, Dp = 0;
-  float* gal = nullptr;       // [Np][Dp]
+  int dtype = 0;              // MMR_F32 (f32 rows in gal) | MMR_F16 (native fp16: raw rows in gh, no gal)
+  float* gal = nullptr;       // [Np][Dp] f32 rows (MMR_F32 index)
   float* inv_norm = nullptr;  // [Np]
   double* norm64 = nullptr;   // [Np]
   uint16_t* gs = nullptr;     // [Np][2Dp] bf16 hi/lo split (mode x3)
   float* gt = nullptr;        // [Np][Dp] f32 in the tile16 layout (skinny scan)
-  uint16_t* gh = nullptr;     // [Np][Dp] fp16 unit rows in the tile32h layout (mode f16; built on first use)
-  uint16_t* ghr = nullptr;    // [Np256][Dp] fp16 unit rows, row-major, zero rows past n (mode f16, p8 scan)
-  int64_t Np256 = 0;          // rows of ghr (a multiple of 256)
-  int mode = 1;               // 0: f32 MFMA scores, 1: bf16x3 split scores, 2: fp16 unit-row scan
+  // [Np][Dp] fp16 in the tile32h layout, the operand of every fp16 scan (lq / gmax / tile / p8): the unit
+  // rows g/|g| of an MMR_F32 index in mode f16 (built on first use), or the raw rows of an MMR_F16 index
+  // (its only copy of the gallery: 2 B per element; scans scale by inv_norm per row)
+  uint16_t* gh = nullptr;
+  int mode = 1;               // 0: f32 MFMA scores, 1: bf16x3 split scores, 2: fp16 scan
   // Workspace: one set per index, sized by what the mode needs (grown on demand).  `mu` serialises
   // the enqueue of searches; across streams the workspace follows the stream: a search on another
   // stream records ws_event on ws_stream (the last user's) and waits for it, so two streams never race
@@ -2095,22 +2152,18 @@ int64_t chunk_queries(const mmr_index* ix) {
   return c < 256 ? 256 : c;
 }
 
-// A/B: record ws_event after every search (MMR_KNN_EAGER_EVENT=1) instead of at a stream switch /
-// workspace growth, on the stream that ran the last search
-bool eager_ws_event() {
-  static const bool v = [] {
-    const char* e = getenv("MMR_KNN_EAGER_EVENT");
-    return e && atoi(e) == 1;
-  }();
-  return v;
-}
+// the p8 GEMM scan takes the fp16 passes of > 128 queries when the row length fits its K tiles
+bool p8_ok(const mmr_index* ix) { return ix->Dp % 128 == 0 && ix->Dp <= 1024; }
+
+// raw-row galleries (native fp16 index): the scans' per-row 1 / |g|; unit-row copies: none
+const float* scan_rscale(const mmr_index* ix) { return ix->dtype == MMR_F16 ? ix->inv_norm : nullptr; }
 
 template <class T>
 mmr_status grow(mmr_index* ix, T*& buf, int64_t& have, int64_t want, size_t elem_bytes) {
   if (want <= have) return MMR_OK;
   if (buf) {
     if (ix->ws_used) {  // the last search has released it
-      if (!eager_ws_event()) (void)hipEventRecord(ix->ws_event, ix->ws_stream);
+      (void)hipEventRecord(ix->ws_event, ix->ws_stream);
       (void)hipEventSynchronize(ix->ws_event);
     }
     (void)hipFree(buf);
@@ -2135,8 +2188,8 @@ mmr_status ensure_ws(mmr_index* ix, int64_t nq) {
     // passes of <= 256 queries, or on the p8 scan 512 (2-row units) / 1024 (4-row units): the same
     // unit-maxima bytes; fp16 query rows of a pass take half the f32 rows of qn
     rows = 1024;
-    const int64_t nr = ix->Np256 > ix->Np ? ix->Np256 : ix->Np;  // the p8 scan writes whole 256-row tiles
-    vals = ix->Np256 > 0 ? 512 * (nr / 2) : 256 * (nr / 4);  // p8: up to 512 queries of 2-row unit maxima
+    const int64_t nr = ix->Np;  // a multiple of 256: the p8 scan's whole gallery tiles
+    vals = p8_ok(ix) ? 512 * (nr / 2) : 256 * (nr / 4);  // p8: up to 512 queries of 2-row unit maxima
     bvals = 1024 * (nr / 64);
   }
   int64_t hq = ix->ws_qrows, hq2 = ix->ws_qrows;
@@ -2150,17 +2203,12 @@ mmr_status ensure_ws(mmr_index* ix, int64_t nq) {
   return MMR_OK;
 }
 
-// Largest query chunk routed to the skinny scan in mode x3 (MMR_KNN_SKINNY_MAX: 0 disables; <= 64).
-// Measured (100k x 768, MI355X): Q <= 16 scan 58 us (5.3 TB/s) vs the x3 GEMM's ~110 us; Q = 32
-// 132 vs ~145 us per search; Q = 64 (4 query tiles, MFMA-paced with ~1.5 waves per SIMD) 196 vs ~145.
-int64_t skinny_max_q() {
-  static const int64_t v = [] {
-    const char* e = getenv("MMR_KNN_SKINNY_MAX");
-    int64_t x = e ? atoll(e) : 32;
-    return x < 0 ? 0 : x > 64 ? 64 : x;
-  }();
-  return v;
-}
+// Largest query chunk routed to the skinny scan in mode x3.  Measured (100k x 768, MI355X): Q <= 16 scan
+// 58 us (5.3 TB/s) vs the x3 GEMM's ~110 us; Q = 32 132 vs ~145 us per search; Q = 64 (4 query tiles,
+// MFMA-paced with ~1.5 waves per SIMD) 196 vs ~145.
+constexpr int64_t kSkinnyMaxQ = 32;
+// query tiles per p8 pass with 4-row units (2 / 4 measured: 4, profiles/r03_s4_knn_pair_ab.txt)
+constexpr int kP8PairTiles = 4;
 
 struct DeviceGuard {
   int prev = -1;
@@ -2173,56 +2221,13 @@ struct DeviceGuard {
   }
 };
 
-// The LDS-staged fp16 tile scan for 33-256-query passes (MMR_KNN_F16_TILE=0: the one-wave stream
-// kernel instead, for A/B measurements).
-// The raw-query small-Q f16 scan (MMR_KNN_F16_RAW=0: prep launch + normalised scan, for A/B).
-bool raw_scan_enabled() {
-  const char* e = getenv("MMR_KNN_F16_RAW");
-  return !(e && atoi(e) == 0);
-}
-
-// The LDS-query persistent small-Q scan (MMR_KNN_F16_LQ=0: the one-wave-per-block RAW stream, for A/B).
-bool lq_scan_enabled() {
-  const char* e = getenv("MMR_KNN_F16_LQ");
-  return !(e && atoi(e) == 0);
-}
-
-// The p8 GEMM scan for 129-256-query f16 passes (MMR_KNN_P8=0: the LDS-ring tile scan, for A/B).
-// query tiles per p8 pass with 4-row units (MMR_KNN_P8_TILES 2 / 4, default 4)
-int p8_pair_tiles() {
-  static const int v = [] {
-    const char* e = getenv("MMR_KNN_P8_TILES");
-    return (e && atoi(e) == 2) ? 2 : 4;
-  }();
-  return v;
-}
-
-// A/B: multi-query-tile passes of the p8 scan (MMR_KNN_P8_PAIR=0: 256)
-bool p8_pair_enabled() {
-  static const bool v = [] {
-    const char* e = getenv("MMR_KNN_P8_PAIR");
-    return !(e && atoi(e) == 0);
-  }();
-  return v;
-}
-
-bool p8_scan_enabled() {
-  const char* e = getenv("MMR_KNN_P8");
-  return !(e && atoi(e) == 0);
-}
-
-bool f16_tile_enabled() {
-  const char* e = getenv("MMR_KNN_F16_TILE");
-  return !(e && atoi(e) == 0);
-}
-
 template <int WQ, int MQ, int WR, int MR, bool PF>
 void launch_f16_tile(hipStream_t st, const mmr_index* ix, const uint16_t* qh, float* gm, float* bm, int64_t ldG,
                      int64_t ldB, int64_t n_rt) {
   using C = F16TileCfg<WQ, MQ, WR, MR, PF>;
   const size_t lds = (size_t)C::STAGES * C::SLICE_B;
   knn_scan_f16_tile<WQ, MQ, WR, MR, PF><<<dim3((unsigned)ix->n_cu), dim3(64 * C::NW), lds, st>>>(
-      qh, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, n_rt);
+      qh, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, n_rt, scan_rscale(ix));
 }
 
 // COARSE selections (block maxima first) run 512-thread workgroups, the unit-level ones 1024
@@ -2236,7 +2241,9 @@ void launch_select(hipStream_t st, int64_t nq, const float* vals, int64_t ldV, i
 #define MMR_SEL(NC)                                                                                              \
   knn_select_t<MODE, NC, T, COARSE, RAW><<<g, b, 0, st>>>(vals, ldV, nunits, ix->n, k, two_delta, bvals, ldB,    \
                                                           two_delta_abs, q_raw, ix->d, qnorm64, ix->gal, ix->Dp,  \
-                                                          ix->norm64, ix->idx_base, oi, os, os64, ost, qpre)
+                                                          ix->norm64, ix->idx_base,                               \
+                                                          ix->dtype == MMR_F16 ? ix->gh : nullptr, oi, os, os64,  \
+                                                          ost, qpre)
   // NC = 256-float chunks of a row in the f64 re-score (0: d > 1024, strided loop)
   switch (ix->d > 1024 ? 0 : (int)ceil_div(ix->Dp, 256)) {
     case 1: MMR_SEL(1); break;
@@ -2279,42 +2286,22 @@ mmr_status build_x3_copies(mmr_index* ix) {
 }
 
 mmr_status build_f16_copies(mmr_index* ix) {
+  if (ix->gh != nullptr) return MMR_OK;  // built, or the native fp16 index's own rows
   DeviceGuard g(ix->device);
   hipError_t e;
-  if (ix->gh == nullptr) {
-    if ((e = hipMalloc(&ix->gh, sizeof(uint16_t) * ix->Np * ix->Dp)) != hipSuccess) {
-      ix->gh = nullptr;
-      mmr::set_error("mmr_index: hipMalloc(fp16 copy) failed: %s", hipGetErrorString(e));
-      return MMR_ERR_OOM;
-    }
-    const int64_t total8 = ix->Np * ix->Dp / 8;
-    knn_tile_gallery_f16<<<dim3((unsigned)ceil_div(total8, 256)), dim3(256)>>>(ix->gal, ix->inv_norm, ix->Dp, total8,
-                                                                             ix->gh);
-    e = hipGetLastError();
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-    if (e != hipSuccess) {
-      mmr::set_error("mmr_index: fp16 copy kernel failed: %s", hipGetErrorString(e));
-      return MMR_ERR_HIP;
-    }
+  if ((e = hipMalloc(&ix->gh, sizeof(uint16_t) * ix->Np * ix->Dp)) != hipSuccess) {
+    ix->gh = nullptr;
+    mmr::set_error("mmr_index: hipMalloc(fp16 copy) failed: %s", hipGetErrorString(e));
+    return MMR_ERR_OOM;
   }
-  if (ix->ghr == nullptr && ix->Dp % 128 == 0 && ix->Dp <= 1024) {
-    // row-major fp16 unit rows for the p8 scan of 129-1024-query passes (whole 256-row tiles)
-    const int64_t np256 = round_up(ix->Np, 256);
-    if ((e = hipMalloc(&ix->ghr, sizeof(uint16_t) * np256 * ix->Dp)) != hipSuccess) {
-      ix->ghr = nullptr;
-      mmr::set_error("mmr_index: hipMalloc(fp16 row copy) failed: %s", hipGetErrorString(e));
-      return MMR_ERR_OOM;
-    }
-    const int64_t total8 = np256 * ix->Dp / 8;
-    knn_rows_f16<<<dim3((unsigned)ceil_div(total8, 256)), dim3(256)>>>(ix->gal, ix->inv_norm, ix->Np, ix->Dp, total8,
-                                                                     ix->ghr);
-    e = hipGetLastError();
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-    if (e != hipSuccess) {
-      mmr::set_error("mmr_index: fp16 row copy kernel failed: %s", hipGetErrorString(e));
-      return MMR_ERR_HIP;
-    }
-    ix->Np256 = np256;
+  const int64_t total8 = ix->Np * ix->Dp / 8;
+  knn_tile_gallery_f16<<<dim3((unsigned)ceil_div(total8, 256)), dim3(256)>>>(ix->gal, ix->inv_norm, ix->Dp, total8,
+                                                                           ix->gh);
+  e = hipGetLastError();
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    mmr::set_error("mmr_index: fp16 copy kernel failed: %s", hipGetErrorString(e));
+    return MMR_ERR_HIP;
   }
   return MMR_OK;
 }
@@ -2328,12 +2315,9 @@ void free_copies(mmr_index* ix, bool x3, bool f16) {
     ix->gs = nullptr;
     ix->gt = nullptr;
   }
-  if (f16) {
+  if (f16 && ix->dtype != MMR_F16) {  // a native fp16 index's gh IS its gallery
     if (ix->gh) (void)hipFree(ix->gh);
-    if (ix->ghr) (void)hipFree(ix->ghr);
     ix->gh = nullptr;
-    ix->ghr = nullptr;
-    ix->Np256 = 0;
   }
 }
 
@@ -2351,15 +2335,11 @@ mmr_status mmr_index_create(const void* gallery, int64_t n, int32_t d, mmr_dtype
   MMR_REQUIRE(n == 0 || gallery != nullptr, "mmr_index_create: gallery is NULL");
   MMR_REQUIRE(n < (int64_t(1) << 31), "mmr_index_create: n=%lld exceeds 2^31 rows per shard",
               (long long)n);
-  if (dtype != MMR_F32) {
-    mmr::set_error("mmr_index_create: dtype %d not built (only MMR_F32)", (int)dtype);
+  if (dtype != MMR_F32 && dtype != MMR_F16) {
+    mmr::set_error("mmr_index_create: dtype %d not built (MMR_F32 | MMR_F16)", (int)dtype);
     return MMR_ERR_UNSUPPORTED;
   }
   DeviceGuard g(device);
-  if (const char* e = getenv("MMR_KNN_TOP4"); e && atoi(e) == 0) {  // A/B: the radix first bound
-    const int zero = 0;
-    MMR_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_top4_bound), &zero, sizeof(int)));
-  }
   mmr_index* ix = new mmr_index();
   ix->device = device;
   ix->n = n;
@@ -2367,6 +2347,7 @@ mmr_status mmr_index_create(const void* gallery, int64_t n, int32_t d, mmr_dtype
   ix->Dp = (int)round_up(d, 64);
   ix->Np = round_up(n > 0 ? n : 1, kRowPad);
   ix->idx_base = idx_base;
+  ix->dtype = dtype;
   auto fail = [&](mmr_status s) {
     mmr_index_destroy(ix);
     return s;
@@ -2379,29 +2360,38 @@ mmr_status mmr_index_create(const void* gallery, int64_t n, int32_t d, mmr_dtype
     mmr::set_error("mmr_index_create: hipEventCreate failed: %s", hipGetErrorString(e));
     return fail(MMR_ERR_HIP);
   }
-  if ((e = hipMalloc(&ix->gal, sizeof(float) * ix->Np * ix->Dp)) != hipSuccess ||
+  const size_t esz = dtype == MMR_F16 ? sizeof(uint16_t) : sizeof(float);
+  if ((dtype == MMR_F16 ? (e = hipMalloc(&ix->gh, sizeof(uint16_t) * ix->Np * ix->Dp))
+                        : (e = hipMalloc(&ix->gal, sizeof(float) * ix->Np * ix->Dp))) != hipSuccess ||
       (e = hipMalloc(&ix->inv_norm, sizeof(float) * ix->Np)) != hipSuccess ||
       (e = hipMalloc(&ix->norm64, sizeof(double) * ix->Np)) != hipSuccess) {
     mmr::set_error("mmr_index_create: hipMalloc failed: %s", hipGetErrorString(e));
     return fail(MMR_ERR_OOM);
   }
   // stage the raw rows into a contiguous device buffer, then pad + norm in one kernel
-  float* raw = nullptr;
+  void* raw = nullptr;
   if (n > 0) {
-    if ((e = hipMalloc(&raw, sizeof(float) * n * d)) != hipSuccess) {
+    if ((e = hipMalloc(&raw, esz * n * d)) != hipSuccess) {
       mmr::set_error("mmr_index_create: hipMalloc(raw) failed: %s", hipGetErrorString(e));
       return fail(MMR_ERR_OOM);
     }
-    e = hipMemcpy(raw, gallery, sizeof(float) * n * d,
-                  gallery_is_host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice);
+    e = hipMemcpy(raw, gallery, esz * n * d, gallery_is_host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice);
     if (e != hipSuccess) {
       (void)hipFree(raw);
       mmr::set_error("mmr_index_create: hipMemcpy failed: %s", hipGetErrorString(e));
       return fail(MMR_ERR_HIP);
     }
   }
-  knn_prep_gallery<<<dim3((unsigned)ceil_div(ix->Np, 4)), dim3(256)>>>(
-      raw, n, d, ix->gal, ix->Dp, ix->Np, ix->inv_norm, ix->norm64);
+  if (dtype == MMR_F16) {
+    // native fp16 gallery: the raw rows ARE the scan operand (tile32h) and the exact re-score rows; the
+    // index runs the fp16 scan only (mode 2)
+    knn_prep_gallery_f16<<<dim3((unsigned)ceil_div(ix->Np, 4)), dim3(256)>>>(
+        (const uint16_t*)raw, n, d, ix->gh, ix->Dp, ix->Np, ix->inv_norm, ix->norm64);
+    ix->mode = 2;
+  } else {
+    knn_prep_gallery<<<dim3((unsigned)ceil_div(ix->Np, 4)), dim3(256)>>>(
+        (const float*)raw, n, d, ix->gal, ix->Dp, ix->Np, ix->inv_norm, ix->norm64);
+  }
   e = hipGetLastError();
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (raw) (void)hipFree(raw);
@@ -2422,7 +2412,6 @@ mmr_status mmr_index_destroy(mmr_index* ix) {
   if (ix->gs) (void)hipFree(ix->gs);
   if (ix->gt) (void)hipFree(ix->gt);
   if (ix->gh) (void)hipFree(ix->gh);
-  if (ix->ghr) (void)hipFree(ix->ghr);
   if (ix->qs) (void)hipFree(ix->qs);
   if (ix->qn) (void)hipFree(ix->qn);
   if (ix->qnorm64) (void)hipFree(ix->qnorm64);
@@ -2437,11 +2426,10 @@ mmr_status mmr_index_device_bytes(const mmr_index* ix, int64_t* gallery_bytes, i
   mmr::clear_error();
   MMR_REQUIRE(ix != nullptr, "mmr_index_device_bytes: index is NULL");
   const int64_t e = ix->Np * ix->Dp;
-  int64_t gb = e * 4 + ix->Np * (4 + 8);
+  int64_t gb = (ix->gal ? e * 4 : 0) + ix->Np * (4 + 8);
   if (ix->gs) gb += e * 2 * 2;
   if (ix->gt) gb += e * 4;
   if (ix->gh) gb += e * 2;
-  if (ix->ghr) gb += ix->Np256 * ix->Dp * 2;
   const int64_t wb = ix->ws_qrows * (ix->Dp * 4 + 8) + ix->ws_vals * 4 + ix->ws_bvals * 4 + ix->ws_qsrows * 3 * ix->Dp * 2;
   if (gallery_bytes) *gallery_bytes = gb;
   if (workspace_bytes) *workspace_bytes = wb;
@@ -2479,7 +2467,7 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
   hipStream_t st = mmr::as_stream(stream);
   // the workspace follows the stream: wait for the previous search if it ran on another stream
   if (ix->ws_used && ix->ws_stream != st) {
-    if (!eager_ws_event()) MMR_CHECK_HIP(hipEventRecord(ix->ws_event, ix->ws_stream));
+    MMR_CHECK_HIP(hipEventRecord(ix->ws_event, ix->ws_stream));
     MMR_CHECK_HIP(hipStreamWaitEvent(st, ix->ws_event, 0));
   }
   mmr_status s = ensure_ws(ix, nq);
@@ -2518,10 +2506,12 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
     if (ix->mode == 2) {
       // fp16 scan, passes of <= 256 queries (16 * QT, QT a power of two), or on the p8 scan <= 512
       // (2-row units) / 1024 (4-row units): its query tiles share every gallery tile read (cfg5: Q =
-      // 2048 over 1M rows reads the 2 GB fp16 gallery twice instead of 8 times)
-      const bool p8ok = ix->ghr != nullptr && p8_scan_enabled();
+      // 2048 over 1M rows reads the 2 GB fp16 gallery twice instead of 8 times).  Every scan reads the
+      // tile32h fp16 image gh; rs scales raw rows (native fp16 index) by 1 / |g|.
+      const bool p8 = p8_ok(ix);
+      const float* rs = scan_rscale(ix);
       const bool u2 = ix->n <= (int64_t(1) << 18) || k >= 32;
-      const int64_t pass = (p8ok && p8_pair_enabled()) ? 256 * (u2 ? 2 : p8_pair_tiles()) : 256;
+      const int64_t pass = p8 ? 256 * (u2 ? 2 : kP8PairTiles) : 256;
       for (int64_t p0 = 0; p0 < cq; p0 += pass) {
         const int64_t pq = cq - p0 < pass ? cq - p0 : pass;
         int qt = 1;
@@ -2532,10 +2522,10 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
         float* gm = ix->vals;
         float* bm = ix->bvals;
         const int64_t ldG = ix->Np / 4, ldB = ix->Np / 64;
-        if (pq > 128 && p8ok) {
-          // 129-256 queries: the persistent 8-phase GEMM (gemm.hip) with the unit-max epilogue —
-          // one 256-query M tile x 256-row gallery tiles, row-major fp16 operands.  (It computes
-          // all 256 query rows; at 100k x 768 it beats the LDS-ring tile scan from Q ~ 160:
+        if (pq > 128 && p8) {
+          // 129-1024 queries: the persistent 8-phase GEMM (gemm.hip) with the unit-max epilogue —
+          // 256-query M tiles x 256-row gallery tiles, row-major fp16 queries, the tile32h gallery.
+          // (It computes all 256 query rows; at 100k x 768 it beats the LDS-ring tile scan from Q ~ 160:
           // Q = 64 / 128 / 192 / 256: 81 / 83 / 86 / 88 us vs 62 / 69 / 96 / 100.)
           const int tm = (int)((pq + 255) / 256);  // query tiles of this pass
           knn_prep_queries<<<dim3(64 * tm), dim3(256), 0, st>>>(qp, pq, ix->d, ix->qn, ix->Dp, 256 * tm, ix->qnorm64, 3);
@@ -2544,9 +2534,9 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
           // the unit maxima the scan writes (512 vs 256 MB per pass at 1M rows): 2 for small
           // galleries or large K (cfg2 100k / K 10: select 22 -> 16 us; cfg3 1M / K 50: 104 -> 65 us for
           // +30 us of scan), 4 for large galleries at small K (cfg5 1M / K 10: +37 us scan, -9 select)
-          const int64_t ldG8 = ix->Np256 / (u2 ? 2 : 4), ldB8 = ix->Np256 / 64;
-          MMR_CHECK_HIP(mmr::knn_scan_p8(qh, ix->ghr, ix->Dp, (int)(ix->Np256 / 256), ix->n, gm, ldG8, bm, ldB8,
-                                         u2 ? 2 : 4, st, tm));
+          const int64_t ldG8 = ix->Np / (u2 ? 2 : 4), ldB8 = ix->Np / 64;
+          MMR_CHECK_HIP(mmr::knn_scan_p8(qh, ix->gh, ix->Dp, (int)(ix->Np / 256), ix->n, gm, ldG8, bm, ldB8,
+                                         u2 ? 2 : 4, st, tm, rs));
           if (u2)
             launch_select<3, true>(st, pq, gm, ldG8, ldG8, ix, k, two_delta16, qp, ix->qnorm64, oi + p0 * k,
                                    os ? os + p0 * k : nullptr, os64 ? os64 + p0 * k : nullptr, ost ? ost + p0 : nullptr,
@@ -2558,7 +2548,7 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
           MMR_LAUNCH_CHECK();
           continue;
         }
-        if (pq > 32 && f16_tile_enabled()) {
+        if (pq > 32) {
           // 33-256 queries: the LDS-staged tile scan (64 / 128 / 256-query tiles), contiguous units
           const int wq = pq <= 64 ? 1 : pq <= 128 ? 2 : 4;
           const int64_t Qt = 64 * wq;
@@ -2566,19 +2556,9 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
               qp, pq, ix->d, ix->qn, ix->Dp, Qt, ix->qnorm64, 2);
           MMR_LAUNCH_CHECK();
           const int64_t n_rt = ix->Np / 16;
-          const char* ce = getenv("MMR_KNN_F16_CFG");  // tile shape (A/B measurements)
-          const int cfg = ce ? atoi(ce) : 0;
-          if (wq == 1) {
-            if (cfg == 1) launch_f16_tile<1, 4, 4, 4, true>(st, ix, qh, gm, bm, ldG, ldB, n_rt);
-            else launch_f16_tile<1, 4, 4, 4, false>(st, ix, qh, gm, bm, ldG, ldB, n_rt);
-          } else if (wq == 2) {
-            if (cfg == 1) launch_f16_tile<1, 8, 4, 4, true>(st, ix, qh, gm, bm, ldG, ldB, n_rt);
-            else launch_f16_tile<2, 4, 4, 4, false>(st, ix, qh, gm, bm, ldG, ldB, n_rt);
-          } else {
-            if (cfg == 1) launch_f16_tile<4, 4, 2, 8, true>(st, ix, qh, gm, bm, ldG, ldB, n_rt);
-            else if (cfg == 2) launch_f16_tile<2, 8, 2, 8, true>(st, ix, qh, gm, bm, ldG, ldB, n_rt);
-            else launch_f16_tile<4, 4, 2, 8, false>(st, ix, qh, gm, bm, ldG, ldB, n_rt);
-          }
+          if (wq == 1) launch_f16_tile<1, 4, 4, 4, false>(st, ix, qh, gm, bm, ldG, ldB, n_rt);
+          else if (wq == 2) launch_f16_tile<2, 4, 4, 4, false>(st, ix, qh, gm, bm, ldG, ldB, n_rt);
+          else launch_f16_tile<4, 4, 2, 8, false>(st, ix, qh, gm, bm, ldG, ldB, n_rt);
           MMR_LAUNCH_CHECK();
           launch_select<2, true>(st, pq, gm, ldG, ldG, ix, k, two_delta16, qp, ix->qnorm64, oi + p0 * k,
                                  os ? os + p0 * k : nullptr, os64 ? os64 + p0 * k : nullptr, ost ? ost + p0 : nullptr,
@@ -2587,54 +2567,47 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
           continue;
         }
         const dim3 grid((unsigned)(ix->Np / 64));
-        if (qt <= 2 && ix->d % 8 == 0 && ((uintptr_t)qp & 15) == 0 && raw_scan_enabled()) {
+        if (qt <= 2 && ix->d % 8 == 0 && ((uintptr_t)qp & 15) == 0) {
           // <= 32 queries: the scan reads the caller's f32 rows itself (no prep launch), per-query margin
           const int64_t nqp = pq;
-          const bool lq = lq_scan_enabled();
-          if (lq && ix->Dp <= 1024) {
+          const bool lq = ix->Dp <= 1024;
+          if (lq) {
             const size_t lds = (size_t)qt * 16 * ix->Dp * 2;
             const int64_t nblk = ix->Np / 64;
             const dim3 g2((unsigned)ix->n_cu);
             if (qt == 1) {
               if (ix->Dp % 128 == 0)
-                knn_scan_f16_lq<1, 128, 8><<<g2, 512, lds, st>>>(qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, nblk, ix->qnorm64);
+                knn_scan_f16_lq<1, 128, 8><<<g2, 512, lds, st>>>(qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, nblk, ix->qnorm64, rs);
               else
-                knn_scan_f16_lq<1, 64, 8><<<g2, 512, lds, st>>>(qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, nblk, ix->qnorm64);
+                knn_scan_f16_lq<1, 64, 8><<<g2, 512, lds, st>>>(qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, nblk, ix->qnorm64, rs);
             } else {
-              knn_scan_f16_lq<2, 64, 8><<<g2, 512, lds, st>>>(qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, nblk, ix->qnorm64);
+              knn_scan_f16_lq<2, 64, 8><<<g2, 512, lds, st>>>(qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, nblk, ix->qnorm64, rs);
             }
           } else if (qt == 1) {
             if (ix->Dp % 128 == 0)
-              knn_scan_f16_gmax<1, 128, 1, true><<<grid, 64, 0, st>>>(nullptr, qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n);
+              knn_scan_f16_gmax<1, 128, 1, true><<<grid, 64, 0, st>>>(nullptr, qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, rs);
             else
-              knn_scan_f16_gmax<1, 64, 1, true><<<grid, 64, 0, st>>>(nullptr, qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n);
+              knn_scan_f16_gmax<1, 64, 1, true><<<grid, 64, 0, st>>>(nullptr, qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, rs);
           } else {
-            knn_scan_f16_gmax<2, 64, 1, true><<<grid, 64, 0, st>>>(nullptr, qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n);
+            knn_scan_f16_gmax<2, 64, 1, true><<<grid, 64, 0, st>>>(nullptr, qp, nqp, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, rs);
           }
           MMR_LAUNCH_CHECK();
           launch_select<1, true, true>(st, pq, gm, ldG, ldG, ix, k, two_delta16r, qp, ix->qnorm64, oi + p0 * k,
                                        os ? os + p0 * k : nullptr, os64 ? os64 + p0 * k : nullptr,
-                                       ost ? ost + p0 : nullptr, bm, ldB, two_delta16a,
-                                       lq && ix->Dp <= 1024 ? ix->qnorm64 : nullptr);
+                                       ost ? ost + p0 : nullptr, bm, ldB, two_delta16a, lq ? ix->qnorm64 : nullptr);
           MMR_LAUNCH_CHECK();
           continue;
         }
+        // <= 32 queries whose rows are not 16-B aligned / d % 8 != 0: prep + the one-wave stream
         knn_prep_queries<<<dim3((unsigned)ceil_div(Qp, 4)), dim3(256), 0, st>>>(
             qp, pq, ix->d, ix->qn, ix->Dp, Qp, ix->qnorm64, 2);
         MMR_LAUNCH_CHECK();
-        switch (qt) {
-          // KC must divide Dp (a multiple of 64): the 128-wide chunk only when Dp % 128 == 0
-          case 1:
-            if (ix->Dp % 128 == 0) knn_scan_f16_gmax<1, 128><<<grid, 64, 0, st>>>(qh, nullptr, 0, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n);
-            else knn_scan_f16_gmax<1, 64><<<grid, 64, 0, st>>>(qh, nullptr, 0, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n);
-            break;
-          case 2:
-            if (ix->Dp % 128 == 0) knn_scan_f16_gmax<2, 128><<<grid, 64, 0, st>>>(qh, nullptr, 0, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n);
-            else knn_scan_f16_gmax<2, 64><<<grid, 64, 0, st>>>(qh, nullptr, 0, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n);
-            break;
-          case 4: knn_scan_f16_gmax<4, 64><<<grid, 64, 0, st>>>(qh, nullptr, 0, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n); break;
-          case 8: knn_scan_f16_gmax<8, 64><<<grid, 64, 0, st>>>(qh, nullptr, 0, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n); break;
-          default: knn_scan_f16_gmax<16, 32><<<grid, 64, 0, st>>>(qh, nullptr, 0, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n); break;
+        if (qt == 1) {
+          if (ix->Dp % 128 == 0) knn_scan_f16_gmax<1, 128><<<grid, 64, 0, st>>>(qh, nullptr, 0, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, rs);
+          else knn_scan_f16_gmax<1, 64><<<grid, 64, 0, st>>>(qh, nullptr, 0, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, rs);
+        } else {
+          if (ix->Dp % 128 == 0) knn_scan_f16_gmax<2, 128><<<grid, 64, 0, st>>>(qh, nullptr, 0, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, rs);
+          else knn_scan_f16_gmax<2, 64><<<grid, 64, 0, st>>>(qh, nullptr, 0, ix->d, ix->gh, gm, bm, ix->Dp, ldG, ldB, ix->n, rs);
         }
         MMR_LAUNCH_CHECK();
         launch_select<1, true>(st, pq, gm, ldG, ldG, ix, k, two_delta16, qp, ix->qnorm64, oi + p0 * k,
@@ -2642,7 +2615,7 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
                                bm, ldB);
         MMR_LAUNCH_CHECK();
       }
-    } else if (ix->mode == 1 && cq <= skinny_max_q()) {
+    } else if (ix->mode == 1 && cq <= kSkinnyMaxQ) {
       // skinny scan: HBM-streaming f32 MFMA, f32-mode delta
       const int qt = cq <= 16 ? 1 : cq <= 32 ? 2 : 4;
       const int64_t Qp = 16 * qt;
@@ -2696,7 +2669,6 @@ mmr_status mmr_index_search(mmr_index* ix, const float* q, int64_t nq, int32_t k
       MMR_LAUNCH_CHECK();
     }
   }
-  if (eager_ws_event()) MMR_CHECK_HIP(hipEventRecord(ix->ws_event, st));
   ix->ws_stream = st;
   ix->ws_used = true;
   return MMR_OK;
@@ -2719,8 +2691,14 @@ mmr_status mmr_index_link_graph(mmr_index* ix, double threshold, int32_t max_lin
   float* qc = nullptr;
   MMR_CHECK_HIP(hipMallocAsync((void**)&ti, sizeof(int64_t) * nrows * k, st));
   MMR_CHECK_HIP(hipMallocAsync((void**)&ts, sizeof(double) * nrows * k, st));
-  const float* q = ix->gal + row0 * ix->Dp;  // padded rows double as queries when d == Dp
-  if (ix->d != ix->Dp) {
+  const float* q = ix->gal ? ix->gal + row0 * ix->Dp : nullptr;  // padded rows double as queries when d == Dp
+  if (ix->dtype == MMR_F16) {  // native fp16 rows -> f32 query rows (exact)
+    MMR_CHECK_HIP(hipMallocAsync((void**)&qc, sizeof(float) * nrows * ix->d, st));
+    knn_rows_from_f16<<<dim3((unsigned)ceil_div(nrows * ix->d, 256)), dim3(256), 0, st>>>(ix->gh, row0, nrows, ix->d,
+                                                                                         ix->Dp, qc);
+    MMR_LAUNCH_CHECK();
+    q = qc;
+  } else if (ix->d != ix->Dp) {
     MMR_CHECK_HIP(hipMallocAsync((void**)&qc, sizeof(float) * nrows * ix->d, st));
     MMR_CHECK_HIP(hipMemcpy2DAsync(qc, sizeof(float) * ix->d, q, sizeof(float) * ix->Dp, sizeof(float) * ix->d,
                                    nrows, hipMemcpyDeviceToDevice, st));
@@ -2755,7 +2733,7 @@ mmr_status mmr_index_rerank(const mmr_index* ix, const float* q_emb, int64_t nq,
   MMR_REQUIRE(q_emb && cand && q_labels && g_labels && q_kg && g_kg && out_idx, "mmr_index_rerank: NULL pointer");
   DeviceGuard g(ix->device);
   knn_rerank<<<dim3((unsigned)nq), dim3(64), 0, mmr::as_stream(stream)>>>(
-      q_emb, ix->d, ix->gal, ix->Dp, ix->norm64, ix->n, ix->idx_base, cand, kc, q_labels, g_labels, q_kg,
+      q_emb, ix->d, ix->gal, ix->dtype == MMR_F16 ? ix->gh : nullptr, ix->Dp, ix->norm64, ix->n, ix->idx_base, cand, kc, q_labels, g_labels, q_kg,
       g_kg, dk, alpha, beta, gamma, topk, out_idx, out_final, out_emb, out_lab, out_kg);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
@@ -2765,6 +2743,10 @@ mmr_status mmr_index_set_mode(mmr_index* ix, int32_t mode) {
   mmr::clear_error();
   MMR_REQUIRE(ix != nullptr && mode >= 0 && mode <= 2, "mmr_index_set_mode: bad arguments");
   std::lock_guard<std::mutex> lk(ix->mu);
+  if (ix->dtype == MMR_F16 && mode != 2) {
+    mmr::set_error("mmr_index_set_mode: a native fp16 index (MMR_F16) scans its fp16 rows only (mode 2)");
+    return MMR_ERR_UNSUPPORTED;
+  }
   if (mode == ix->mode && (mode != 1 || ix->gs != nullptr) && (mode != 2 || ix->gh != nullptr)) return MMR_OK;
   // the new mode's copies are built BEFORE the old mode's are freed: on a failure (e.g. an OOM on a
   // shard sized for fp16) the index stays in its previous mode with its copies intact, and only the
@@ -2842,7 +2824,7 @@ mmr_status mmr_index_rerank_components(const mmr_index* ix, const float* q_emb, 
               "mmr_index_rerank_components: NULL pointer");
   DeviceGuard g(ix->device);
   knn_rerank_comp<<<dim3((unsigned)nq), dim3(64), 0, mmr::as_stream(stream)>>>(
-      q_emb, ix->d, ix->gal, ix->Dp, ix->norm64, ix->n, ix->idx_base, cand, kc, q_labels, g_labels, q_kg, g_kg, dk,
+      q_emb, ix->d, ix->gal, ix->dtype == MMR_F16 ? ix->gh : nullptr, ix->Dp, ix->norm64, ix->n, ix->idx_base, cand, kc, q_labels, g_labels, q_kg, g_kg, dk,
       out_comp);
   MMR_LAUNCH_CHECK();
   return MMR_OK;

@@ -162,8 +162,11 @@ class ShardedIndex:
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
         s, e = shard_bounds(len(gallery), world)[rank]
-        rows = np.ascontiguousarray(gallery[s:e], dtype=np.float32) if not isinstance(gallery, torch.Tensor) \
-            else gallery[s:e]
+        if isinstance(gallery, torch.Tensor):
+            rows = gallery[s:e]
+        else:  # an fp16 gallery in f16 mode stays fp16 (the native fp16 index: 2 B per element on device)
+            keep16 = np.asarray(gallery[:0]).dtype == np.float16 and mode == "f16"
+            rows = np.ascontiguousarray(gallery[s:e], dtype=np.float16 if keep16 else np.float32)
         return cls(rows, len(gallery), s, group=group, device=device, local_search=local_search, mode=mode,
                    fallback_search=fallback_search)
 
@@ -236,8 +239,9 @@ class ShardedIndex:
 class ShardedRetrievalEngine(RetrievalEngine):
     """make_retrieval_engine(method="mi355x_sharded"): every rank mmaps the .npy, keeps its row
     shard on its GPU; retrieve()/search() are collective calls (all ranks, same batch size).
-    dtype "fp32" scans the bf16x3 split copy, "fp16" the fp16 unit-row copy (BASELINE cfg5's fp16
-    gallery); both rank exactly (f64 re-score from the f32 rows), so results are identical.
+    dtype "fp32" scans the bf16x3 split copy, "fp16" the fp16 scan (an fp16 .npy — BASELINE cfg5's fp16
+    gallery — becomes a native fp16 index per shard: its raw rows are the only device copy); both rank
+    exactly (f64 re-score from the gallery's own rows), so results are identical.
     Host memory: `embs` stays the memmap (no whole-gallery f32 copy per rank, unlike the ABC's
     astype), so a rank's resident host bytes are its shard's, read once into its GPU."""
 

@@ -30,6 +30,7 @@ class RetrievalEngine(abc.ABC):
         instead of materialising a float32 copy — the sharded engine converts only its rows."""
         if embs is None:
             embs = np.load(features_path)
+        self._raw = embs if isinstance(embs, np.ndarray) else None  # the file's own dtype (fp16 galleries)
         if lazy:
             self.embs = embs if isinstance(embs, np.ndarray) else np.asarray(embs)
         else:
@@ -58,12 +59,15 @@ class RetrievalEngine(abc.ABC):
 class GalleryIndex:
     """Owning wrapper of an mmr_index (one device-resident gallery shard).
 
-    Scan modes (all exact: candidates re-scored in f64 from the f32 rows): "x3" bf16 3-term split
-    GEMM (default; Q <= 32 use the skinny f32 stream), "f32" f32 MFMA, "f16" fp16 unit-row copy of
-    the gallery (half the scan bytes, wider candidate margin).  Heavily tied galleries (more
-    candidates within the margin than the selection buffer holds) are handled inside the selection
-    kernel by batched exact merging, so the per-query status is always 0 (checked by callers that
-    ask for it)."""
+    Scan modes (all exact: candidates re-scored in f64 from the gallery's own rows): "x3" bf16 3-term
+    split GEMM (default; Q <= 32 use the skinny f32 stream), "f32" f32 MFMA, "f16" fp16 unit-row copy
+    of the gallery (half the scan bytes, wider candidate margin).  An fp16 gallery (numpy float16 /
+    torch.float16 rows: BASELINE config 5) builds a NATIVE fp16 index (MMR_F16): its raw fp16 rows are
+    the only device copy (2 B per element + norms), scanned in mode "f16" and re-scored exactly (fp16 is
+    exact in f64) — the same results as an index of the f32-upcast rows (the reference's
+    .astype("float32"), retrieval.py:24-32).  Heavily tied galleries (more candidates within the
+    margin than the selection buffer holds) are handled inside the selection kernel by batched exact
+    merging, so the per-query status is always 0 (checked by callers that ask for it)."""
 
     MODES = {"f32": 0, "x3": 1, "f16": 2}
 
@@ -74,7 +78,8 @@ class GalleryIndex:
             device = torch.cuda.current_device()
         self.device = int(device)
         if isinstance(embs, torch.Tensor):
-            src = embs.detach().to(torch.float32).contiguous()
+            half = embs.dtype == torch.float16
+            src = embs.detach().to(torch.float16 if half else torch.float32).contiguous()
             is_host = 0 if src.is_cuda else 1
             if src.is_cuda and src.device.index != self.device:
                 src = src.to(f"cuda:{self.device}")
@@ -82,14 +87,18 @@ class GalleryIndex:
             p = ctypes.c_void_p(src.data_ptr())
             keep = src
         else:
-            keep = np.ascontiguousarray(np.asarray(embs, dtype=np.float32))
+            half = np.asarray(embs).dtype == np.float16
+            keep = np.ascontiguousarray(np.asarray(embs, dtype=np.float16 if half else np.float32))
             n, d = keep.shape
             is_host = 1
             p = keep.ctypes.data_as(ctypes.c_void_p)
         if not is_host:
             torch.cuda.synchronize(self.device)  # the copy runs on the default stream
         h = ctypes.c_void_p()
-        _lib.check(L.mmr_index_create(p, n, d, 0, is_host, idx_base, self.device, ctypes.byref(h)),
+        self.native_f16 = bool(half)
+        if half:
+            mode = "f16"  # a native fp16 index scans its own fp16 rows
+        _lib.check(L.mmr_index_create(p, n, d, 1 if half else 0, is_host, idx_base, self.device, ctypes.byref(h)),
                    "mmr_index_create")
         del keep
         self._h = h
@@ -281,9 +290,13 @@ class MI355XRetrievalEngine(RetrievalEngine):
         super().__init__(features_path, ids_path, embs=embs, ids=ids)
         if dtype not in ("fp32", "fp16"):
             raise ValueError(f"gallery dtype {dtype!r} (fp32 | fp16)")
-        # fp16: the scan reads an fp16 copy of the unit rows (BASELINE cfg5's fp16 gallery); the f32
-        # rows stay resident for the exact f64 re-score, so results are identical to fp32
-        self.index = GalleryIndex(self.embs, device=device, mode="f16" if dtype == "fp16" else "x3")
+        # fp16: an fp16 gallery file (BASELINE cfg5's fp16 gallery) builds the native fp16 index (its raw
+        # rows are the only device copy, re-scored exactly); an f32 gallery keeps its f32 rows for the
+        # exact f64 re-score and scans an fp16 copy of the unit rows — either way the results equal the
+        # fp32 engine's (the reference upcasts with .astype("float32"), retrieval.py:24-32)
+        src = self._raw if (dtype == "fp16" and self._raw is not None and self._raw.dtype == np.float16) else self.embs
+        self.index = GalleryIndex(src, device=device, mode="f16" if dtype == "fp16" else "x3")
+        self._raw = None
         self.device = self.index.device
 
     def search(self, Q, K: int = 10, check: bool = True):

@@ -223,14 +223,16 @@ def test_cfg3_text_tower_batch_1024_vs_oracle():
 
 def test_index_device_bytes_per_mode():
     """Scan copies exist only in the mode that reads them: f32 rows + norms always; x3 adds the bf16
-    hi/lo split + tile16 f32 copies (8 B per element); f16 the two fp16 copies (4 B per element) and
-    frees the x3 ones — a 1M x 1024 fp16-gallery index holds f32 rows + fp16 copies only."""
+    hi/lo split + tile16 f32 copies (8 B per element); f16 the ONE tile32h fp16 copy every fp16 scan
+    reads (2 B per element; round 4: the p8 scan reads it too, no row-major copy) and frees the x3 ones.
+    (An fp16 gallery builds the native fp16 index instead: 2 B per element in all,
+    test_knn_f16_native_gpu.py.)"""
     N, D = 1_000_000, 1024
     G = synthetic.gauss_gallery(N, D, synthetic.SEED + 60)
     base = N * D * 4 + N * 12
     ix = GalleryIndex(G, mode="f16")
     g16, _ = ix.device_bytes()
-    assert base + N * D * 4 <= g16 <= base + N * D * 4 + 512 * D * 4 + 512 * 12
+    assert base + N * D * 2 <= g16 <= base + N * D * 2 + 512 * D * 6 + 512 * 12
     ix.set_mode("x3")
     g3, _ = ix.device_bytes()
     assert base + N * D * 8 <= g3 <= base + N * D * 8 + 512 * D * 12
