@@ -40,7 +40,8 @@ PRESETS = {
     "cfg2": {},
     "cfg3": {"model_type": "text", "batch": 1024, "gallery": 1_000_000, "k": 50},
     "cfg4": {"gallery": 1_000_000},
-    "cfg5": {"batch": 2048, "gallery": 1_000_000, "dim": 1024, "k": 10, "tower_dtype": "fp8", "rerank": True},
+    "cfg5": {"batch": 2048, "gallery": 1_000_000, "dim": 1024, "k": 10, "tower_dtype": "fp8", "rerank": True,
+             "gallery_dtype": "fp16"},
 }
 RERANK_DK = 128  # synthetic KG embedding width of the rerank tables
 
@@ -67,6 +68,9 @@ def parse(argv=None):
                    help="gallery scan: f16 (fp16 unit-row copy, default) or x3 (bf16 split GEMM; skinny f32 "
                         "stream for Q <= 32); both exact (f64 re-rank from the f32 rows)")
     p.add_argument("--gallery", type=int, default=None, help="gallery rows per GPU")
+    p.add_argument("--gallery-dtype", choices=["fp32", "fp16"], default=None,
+                   help="gallery rows: fp32 (configs 1-4), or fp16 (config 5: a native fp16 index, 2 B per element "
+                        "on the device, exact f64 re-score from the fp16 rows)")
     p.add_argument("--dim", type=int, default=None)
     p.add_argument("--k", type=int, default=None)
     p.add_argument("--model-type", choices=["multimodal", "text", "image", "both"], default=None,
@@ -78,7 +82,7 @@ def parse(argv=None):
                    help="queries re-embedded by the fp32 oracle for recall / P@10 vs the CPU path")
     a = p.parse_args(argv)
     pre = dict({"batch": 256, "gallery": 100_000, "k": 10, "model_type": "multimodal", "dim": 768,
-                "tower_dtype": "bf16", "rerank": False}, **PRESETS[a.preset])
+                "tower_dtype": "bf16", "rerank": False, "gallery_dtype": "fp32"}, **PRESETS[a.preset])
     for key, v in pre.items():
         if getattr(a, key) is None:
             setattr(a, key, v)
@@ -150,6 +154,9 @@ def main():
     # gallery shard: rows [rank*n, (rank+1)*n) of a virtual (world*n, d) N(0,1) gallery
     n, d, K, B = a.gallery, a.dim, a.k, a.batch
     G = synthetic.gauss_gallery(n, d, synthetic.SEED + 17 * rank)
+    if a.gallery_dtype == "fp16":  # config 5's fp16 gallery: a native fp16 index (fp16 scan only)
+        G = G.astype(np.float16)
+        a.knn_mode = "f16"
     index = GalleryIndex(G, device=local, idx_base=rank * n, mode=a.knn_mode)
     index.reserve(2 * B * world)
 
@@ -368,11 +375,14 @@ def main():
             "dtype": ({"fp8": "MX-fp8 (e4m3 + E8M0/32) tower linears, bf16 elsewhere / ",
                        "x3": "f32 towers (every contraction bf16x3 MFMA, f32 accumulate) / "}.get(a.tower_dtype, "bf16 towers / ")
                       if a.mode == "full" else "") + (
+                "fp16 gallery (native fp16 index: the raw rows are the scan operand), exact f64 re-rank"
+                if a.gallery_dtype == "fp16" else
                 "f32 gallery, fp16 unit-row scan copy, exact f64 re-rank" if a.knn_mode == "f16"
                 else "f32 gallery, bf16x3 scan, exact f64 re-rank"),
             "data": "synthetic (seeded N(0,1) gallery; random-init weights)",
-            "config": {"workload": ("%s: %s%s, B=%d, top-%d over %dx%d f32 per GPU%s" % (
+            "config": {"workload": ("%s: %s%s, B=%d, top-%d over %dx%d %s per GPU%s" % (
                 a.preset, workload, " (MX-fp8 BERT + Swin stage 3-4 linears)" if a.tower_dtype == "fp8" else "", B, K, n, d,
+                "fp16" if a.gallery_dtype == "fp16" else "f32",
                 " + fused KG/label rerank of the %d candidates" % K if a.rerank else ""))
                        if a.mode == "full" else ("%s kNN only: Q=%d, top-%d over %dx%d f32 per GPU" % (a.preset, B, K, n, d)),
                        "global_batch": world * B, "gallery_rows": world * n, "dim": d, "k": K,
@@ -453,13 +463,13 @@ def roofline(a, n, d, K, Qs, ms_search, ms_small, q_small, gemm_ms, B, lat_small
         fl = 2.0 * M * 3072 * 768
         roof = {"bound": "mfma", "achieved": wmul * fl / (ms_ffn1 / 1e3) / 1e12, "peak": peak_gemm / 1e12,
                 "unit": "TFLOP/s", "traffic": None,
-                "kernel": ("BERT FFN1 bf16x3 GEMM + GELU (M=%d, N=3072, K=768; x3_gemm, f32 in / out; achieved = "
-                           "MFMA work, 3 bf16 products per f32 product), " % M if x3 else
-                           ("BERT FFN1 MX-fp8 GEMM + GELU (M=%d, N=3072, K=768; gemm_bf16_tn_p8<4, FP8>, bf16 "
+                "kernel": (("BERT FFN1 bf16x3 GEMM + GELU (M=%d, N=3072, K=768; x3_gemm, f32 in / out; achieved = "
+                            "MFMA work, 3 bf16 products per f32 product), " if x3 else
+                            "BERT FFN1 MX-fp8 GEMM + GELU (M=%d, N=3072, K=768; gemm_bf16_tn_p8<4, FP8>, bf16 "
                             "output) + its activation quantiser launch: the per-GEMM timing pass runs the "
                             "UNFUSED form (in the timed steps FFN1 emits FFN2's fp8 operand directly, "
                             "mmr_linear_mxfp8_q8), " if fp8 else
-                            "BERT FFN1 GEMM + GELU (M=%d, N=3072, K=768; tuned variant), ") % M)
+                            "BERT FFN1 GEMM + GELU (M=%d, N=3072, K=768; tuned variant), ") % M
                            + "timed per launch with HIP events in a towers-in-sequence pass after the timed region"),
                 "ms_per_launch": ms_ffn1, "flops_per_launch": fl, "bert_gemms": fam, "knn": knn_roof}
     elif a.mode == "full":

@@ -12,6 +12,9 @@ void set_error(const char* fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
+  // a failed HIP call (e.g. an out-of-memory hipMalloc) leaves a sticky per-thread error that the NEXT
+  // call's launch check would report as its own: the failing call reports it here, then clears it
+  (void)hipGetLastError();
 }
 void clear_error() { g_err[0] = 0; }
 }  // namespace mmr

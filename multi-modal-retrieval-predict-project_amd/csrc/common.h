@@ -164,6 +164,7 @@ __device__ __forceinline__ void q8_chunk8(const float* vb, int64_t row, int ch, 
   do {                                                                                     \
     hipError_t _e = (expr);                                                                \
     if (_e != hipSuccess) {                                                                \
+      (void)hipGetLastError(); /* clear the sticky error: the next launch check is clean */ \
       mmr::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__,      \
                      __LINE__);                                                            \
       return _e == hipErrorOutOfMemory ? MMR_ERR_OOM : MMR_ERR_HIP;                        \

@@ -2266,6 +2266,7 @@ mmr_status build_x3_copies(mmr_index* ix) {
   hipError_t e;
   if ((ix->gs == nullptr && (e = hipMalloc(&ix->gs, sizeof(uint16_t) * ix->Np * 2 * ix->Dp)) != hipSuccess) ||
       (ix->gt == nullptr && (e = hipMalloc(&ix->gt, sizeof(float) * ix->Np * ix->Dp)) != hipSuccess)) {
+    (void)hipGetLastError();  // a failed hipMalloc leaves a sticky error the next launch check would report
     mmr::set_error("mmr_index: hipMalloc(x3 scan copies) failed: %s", hipGetErrorString(e));
     return MMR_ERR_OOM;
   }
@@ -2291,6 +2292,7 @@ mmr_status build_f16_copies(mmr_index* ix) {
   hipError_t e;
   if ((e = hipMalloc(&ix->gh, sizeof(uint16_t) * ix->Np * ix->Dp)) != hipSuccess) {
     ix->gh = nullptr;
+    (void)hipGetLastError();
     mmr::set_error("mmr_index: hipMalloc(fp16 copy) failed: %s", hipGetErrorString(e));
     return MMR_ERR_OOM;
   }
