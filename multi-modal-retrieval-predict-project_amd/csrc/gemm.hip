@@ -23,6 +23,8 @@
 #include <mutex>
 #include <utility>
 
+#include <stdio.h>
+
 #include "common.h"
 
 namespace {
@@ -1122,7 +1124,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
         }
         const int64_t m = m0 + wr * 128 + rd * 16 + rr;
         const int n = n0 + wc * 64 + hb * 16;
-        st16((uint8_t*)Y + m * N + n, make_uint4(w4[0], w4[1], w4[2], w4[3]), ntst != 0);
+        st16((uint8_t*)Y + m * N + n, make_uint4(w4[0], w4[1], w4[2], w4[3]), (ntst & 1) != 0);
         if ((hb & 1) == 0) {  // one scale byte per 32-block, layout-0 image: [m/256][n/128][wr][fq][fr][i]
           const int fq = (n % 128) / 32;
           YS[((m0 / 256) * (N / 128) + n / 128) * 1024 + ((wr * 4 + fq) * 16 + rr) * 8 + rd] = (uint8_t)(ex + 127);
@@ -1139,7 +1141,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
           const int idx = c * 64 + le;
           const int64_t m = m0 + wr * 128 + rd * 16 * C::RM + idx / (2 * NT);
           const int n = n0 + wc * 16 * NT + (idx % (2 * NT)) * 8;
-          if (!skip_st) st16(Y + m * N + n, __builtin_bit_cast(uint4, ov[c]), ntst != 0);
+          if (!skip_st) st16(Y + m * N + n, __builtin_bit_cast(uint4, ov[c]), (ntst & 1) != 0);
           else asm volatile("" ::"v"(ov[c]));
         }
       }
