@@ -59,6 +59,9 @@ def parse(argv=None):
     p.add_argument("--tower-dtype", choices=["bf16", "fp8", "x3"], default=None,
                    help="tower linears: bf16 (configs 2-4), MX-fp8 (config 5) or x3 (fp32-faithful parity mode: f32 "
                         "activations, every contraction on bf16x3 MFMA)")
+    p.add_argument("--sequential-towers", action="store_true",
+                   help="run the towers and the fusion layers on one stream (for rocprof per-kernel stats; the "
+                        "default overlaps the Swin tower and the patch-side fusion work on side streams)")
     p.add_argument("--no-x3-line", action="store_true",
                    help="skip the x3 (fp32-faithful) throughput + parity block reported beside a bf16 / fp8 run")
     p.add_argument("--rerank", action="store_true", default=None,
@@ -166,6 +169,8 @@ def main():
         from mmr_amd.model import build_bench_model
         mt = "text" if a.model_type == "both" else a.model_type
         model = build_bench_model(device=dev, joint_dim=d, model_type=mt, tower_dtype=a.tower_dtype)
+        if a.sequential_towers:
+            model.concurrent_towers = model.fusion.side_streams = False
         if a.model_type != "text":
             imgs = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(B, synthetic.SEED + rank))).to(dev)
         if a.model_type != "image":
@@ -319,17 +324,12 @@ def main():
         # timed region with the towers in sequence: inside the timed steps the Swin tower runs
         # concurrently on a side stream, and events around one kernel would also count the
         # co-running kernels' share
-        saved = {k: os.environ.get(k) for k in ("MMR_TOWER_STREAMS", "MMR_FUSION_STREAMS")}
-        os.environ.update({k: "0" for k in saved})
+        model.concurrent_towers = model.fusion.side_streams = False
         model.backbones.bert.gemm_events = {}
         for _ in range(3):
             step(False)
         torch.cuda.synchronize(dev)
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+        model.concurrent_towers = model.fusion.side_streams = not a.sequential_towers
         for name, evs in model.backbones.bert.gemm_events.items():
             gemm_ms[name] = sum(e0.elapsed_time(e1) for e0, e1 in evs) / max(len(evs), 1)
         model.backbones.bert.gemm_events = None

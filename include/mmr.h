@@ -165,6 +165,16 @@ mmr_status mmr_linear_bf16(const uint16_t* x, const uint16_t* w, const float* bi
  * Diagnostic: lets a benchmark name the kernel it measured. */
 int32_t mmr_linear_bf16_variant(int64_t m, int32_t n, int32_t k, int32_t act, int32_t has_bias,
                                 int32_t has_residual);
+/* Number of launch variants mmr_linear_bf16 chooses among (indices 0 .. n-1 of its table). */
+int32_t mmr_linear_bf16_n_variants(void);
+
+/* Test / A-B hook (the product path never calls it): pin a launch variant for the whole process.
+ *   MMR_PIN_GEMM_BF16: value = mmr_linear_bf16 variant index, or -1 = per-shape tuning (default);
+ *   MMR_PIN_X3_WAVES:  value = 4 or 8 waves per mmr_linear_x3 tile (8 only where K % 256 == 0),
+ *                      or -1 = automatic (default).
+ * MMR_ERR_INVALID for an unknown pin or value. */
+enum { MMR_PIN_GEMM_BF16 = 0, MMR_PIN_X3_WAVES = 1 };
+mmr_status mmr_pin_variant(int32_t which, int32_t value);
 
 /* Resident-weight streaming linear for the short-K, narrow tower linears (Swin patch embed, stage-2
  * qkv / proj, PatchMerging 1->2; timm nn.Linear, reference fusion.py:198-199):

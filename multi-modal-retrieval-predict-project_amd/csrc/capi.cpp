@@ -17,9 +17,28 @@ void set_error(const char* fmt, ...) {
   (void)hipGetLastError();
 }
 void clear_error() { g_err[0] = 0; }
+std::atomic<int> pin_gemm_bf16{-1};
+std::atomic<int> pin_x3_waves{-1};
 }  // namespace mmr
 
 extern "C" {
 const char* mmr_last_error(void) { return mmr::g_err; }
 int mmr_version(void) { return 1; }
+
+mmr_status mmr_pin_variant(int32_t which, int32_t value) {
+  mmr::clear_error();
+  if (which == MMR_PIN_GEMM_BF16) {
+    const int nv = mmr_linear_bf16_n_variants();
+    MMR_REQUIRE(value >= -1 && value < nv, "mmr_pin_variant: gemm variant %d (-1 or 0..%d)", value, nv - 1);
+    mmr::pin_gemm_bf16.store(value);
+    return MMR_OK;
+  }
+  if (which == MMR_PIN_X3_WAVES) {
+    MMR_REQUIRE(value == -1 || value == 4 || value == 8, "mmr_pin_variant: x3 waves %d (-1, 4, 8)", value);
+    mmr::pin_x3_waves.store(value);
+    return MMR_OK;
+  }
+  mmr::set_error("mmr_pin_variant: unknown pin %d", which);
+  return MMR_ERR_INVALID;
+}
 }

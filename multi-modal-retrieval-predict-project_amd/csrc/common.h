@@ -3,12 +3,18 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "mmr.h"
 
 namespace mmr {
 
 void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 void clear_error();
+
+// process-wide launch-variant pins (mmr_pin_variant; -1 = the launcher's own choice)
+extern std::atomic<int> pin_gemm_bf16;
+extern std::atomic<int> pin_x3_waves;
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -575,10 +575,6 @@ mmr_status launch_mha(const char* who, const uint16_t* q, int64_t ldq, const uin
   // key block: all keys when lk <= 64; 64 for a 1-2-wave block (its LDS, and with it the workgroups
   // per CU, is then set by the K/V image); else 128
   int kbs = (lk <= 64 || nwv <= 2) ? 64 : MHA_KB;
-  if (const char* e = getenv("MMR_MHA_KB")) {  // A/B override (64 / 128)
-    const int v = atoi(e);
-    if (v == 64 || v == 128) kbs = v;
-  }
   kbs = std::min(kbs, (lk + 31) & ~31);
   const size_t kv_bytes = (size_t)kbs * (dt * 32 + 8) * 2 + (size_t)kbs * (dt * 32 + ((dt & 1) ? 0 : 16)) * 2;
   const size_t lds =

@@ -507,16 +507,10 @@ __device__ __forceinline__ void st16(void* p, uint4 v, bool nt) {
   else *(uint4*)p = v;
 }
 
-// the launchers' choice (MMR_P8_NT=0 / 1 forces it, A/B)
-inline int p8_nt(int64_t m, int64_t n, int64_t esz) {
-  static const int force = [] {
-    const char* e = getenv("MMR_P8_NT");
-    return e ? atoi(e) : -1;
-  }();
-  // 128 MB: the cfg2 BERT / fusion QKV outputs (151 MB) stream too (QKV 121 -> 118.5 us, step
-  // 15.58 -> 15.51 ms same box, profiles/r03_s4_nt_store_step.txt); the 50 MB O / FFN2 outputs measured equal
-  return force >= 0 ? force : (m * n * esz > (int64_t)128 << 20 ? 1 : 0);
-}
+// the launchers' choice: outputs above 128 MB stream (the cfg2 BERT / fusion QKV outputs, 151 MB:
+// QKV 121 -> 118.5 us, step 15.58 -> 15.51 ms same box, profiles/r03_s4_nt_store_step.txt); the 50 MB
+// O / FFN2 outputs measured equal
+inline int p8_nt(int64_t m, int64_t n, int64_t esz) { return m * n * esz > (int64_t)128 << 20 ? 1 : 0; }
 
 template <int NT, bool FP8 = false, int KNN = 0>
 struct P8 {
@@ -605,10 +599,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   // 64 B stores are twice the L2 write requests of the LDS path's 8 rows x 128 B).  OUT8 / KNN keep
   // their own epilogues.
   constexpr bool epi_pl = !OUT8 && !KNN && ACT == 1;
-  // OUT8 + GELU in registers (the permlane row chunks, a 32-column block = the 4 lanes fq = 0..3 of
-  // one row, quantised after two lane swaps) measured slower than the LDS-staged OUT8 rounds: FFN1
-  // 1060 -> 1197 us at M = 262144 (8-B stores, 32-B row segments; profiles/r03_out8_permlane_ab.txt)
-  constexpr bool epi_pl8 = false;
+  // (OUT8 + GELU in registers — permlane row chunks quantised after two lane swaps — measured slower
+  // than the LDS-staged OUT8 rounds and was removed: profiles/r03_out8_permlane_ab.txt)
 #ifdef MMR_P8_NOSTORE
   constexpr bool skip_st = !KNN && !OUT8;  // diagnostic build: bf16 outputs computed, not stored
   constexpr bool skip_gm = KNN != 0;       // ... and the kNN unit maxima (block maxima still stored)
@@ -617,7 +609,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   constexpr bool skip_gm = false;
 #endif
   constexpr int nstore = skip_st ? 0
-                                 : (skip_gm ? 8 : (epi_pl ? C::NSTORE_PL : (epi_pl8 ? 2 * C::NSTORE_PL : C::NSTORE_LDS)));
+                                 : (skip_gm ? 8 : (epi_pl ? C::NSTORE_PL : C::NSTORE_LDS));
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
 
   const int ntiles = tiles_m * tiles_n;
@@ -1026,53 +1018,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
         }
       }
     }
-    if constexpr (epi_pl8) {
-      // lane: row m0 + wr 128 + 16 i + efr; after the swap, 8 consecutive columns of the n-tile pair
-      // (j, j + 1) = one quarter of the pair's 32-column block (the quarter index is efq)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int64_t row = m0 + wr * 128 + i * 16 + efr;
-#pragma unroll
-        for (int j = 0; j < NT; j += 2) {
-          uint2 pk[2];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int jj = j + h;
-            float v[4];
-#pragma unroll
-            for (int rg = 0; rg < 4; rg += 2) {
-              mmr::f32x2_t u = {acc[i][jj][rg] + bq[jj][rg], acc[i][jj][rg + 1] + bq[jj][rg + 1]};
-              u = mmr::gelu_fast2(u);
-              v[rg] = u.x;
-              v[rg + 1] = u.y;
-            }
-            pk[h] = make_uint2(mmr::pack2bf(v[0], v[1]), mmr::pack2bf(v[2], v[3]));
-          }
-          const auto sx = __builtin_amdgcn_permlane16_swap(pk[0].x, pk[1].x, false, false);
-          const auto sy = __builtin_amdgcn_permlane16_swap(pk[0].y, pk[1].y, false, false);
-          const uint32_t d4[4] = {sx[0], sy[0], sx[1], sy[1]};  // 8 bf16 columns, in order
-          float vb[8];
-          float amax = 0.f;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            vb[2 * e] = __uint_as_float(d4[e] << 16);
-            vb[2 * e + 1] = __uint_as_float(d4[e] & 0xFFFF0000u);
-            amax = fmaxf(amax, fmaxf(fabsf(vb[2 * e]), fabsf(vb[2 * e + 1])));
-          }
-          amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
-          amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
-          const int ex = mmr::q8_exp(amax);
-          const float iv = mmr::q8_inv(ex);
-          const int col = n0 + wc * 16 * NT + 16 * j + ((efq & 1) ? 16 : 0) + (efq >> 1) * 8;
-          if (!skip_st) {
-            *(uint2*)((uint8_t*)Y + row * N + col) = make_uint2(mmr::q8_pack4(vb, iv), mmr::q8_pack4(vb + 4, iv));
-            if (efq == 0) YS[mmr::q8_soff(row, col, N)] = (uint8_t)(ex + 127);
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int rd = 0; rd < ((epi_pl || epi_pl8) ? 0 : 8 / C::RM); ++rd) {  // LDS-staged rounds
+    for (int rd = 0; rd < (epi_pl ? 0 : 8 / C::RM); ++rd) {  // LDS-staged rounds
 #pragma unroll
       for (int ii = 0; ii < C::RM; ++ii) {
         const int i = rd * C::RM + ii;
@@ -1537,7 +1484,8 @@ void launch(const uint16_t* x, const uint16_t* w, const float* b, const uint16_t
 // the caller's stream (HIP events, 3 launches each after one warm-up) and keeps the fastest for
 // the rest of the process — tile shape / persistence / pipeline depth trade off differently per
 // shape (K = 96 ... 3072, N = 96 ... 3072).  Skipped (default variant) while the stream is being
-// captured, when the output aliases an input, or with MMR_GEMM_TUNE=0.
+// captured or when the output aliases an input.  mmr_pin_variant(MMR_PIN_GEMM_BF16, v) pins one
+// variant for the process (tests / A/B tools).
 struct TuneKey {
   int64_t m;
   int n, k, act, hb, hr;
@@ -1556,8 +1504,6 @@ std::map<std::pair<int, TuneKey>, int> g_tuned;  // (device, key) -> variant
 template <class Run>
 int tuned_variant(int64_t m, int n, int k, int act, bool hb, bool hr, const void* x, const void* r, const void* y,
                   hipStream_t st, Run&& run) {
-  const char* te = getenv("MMR_GEMM_TUNE");
-  if (te && atoi(te) == 0) return 0;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   const auto key = std::make_pair(dev, TuneKey{m, n, k, act, (int)hb, (int)hr});
@@ -1611,6 +1557,8 @@ extern "C" int mmr_diag_p8_stamps(unsigned long long* out, int64_t n) {
 }
 #endif
 
+extern "C" int32_t mmr_linear_bf16_n_variants(void) { return kVariants; }
+
 extern "C" int32_t mmr_linear_bf16_variant(int64_t m, int32_t n, int32_t k, int32_t act, int32_t has_bias,
                                            int32_t has_residual) {
   int dev = 0;
@@ -1645,16 +1593,11 @@ extern "C" mmr_status mmr_linear_bf16(const uint16_t* x, const uint16_t* w, cons
       else launch<1, false, false>(x, w, bias, residual, y, m, n, k, st, w4, cfg);
     }
   };
-  // diagnostic overrides (MMR_GEMM_W4 / MMR_GEMM_BIG) pin one variant; otherwise the shape's tuned
-  // variant (tuned once per process on the first call with that shape)
-  const char* w4e = getenv("MMR_GEMM_W4");
-  const char* cfge = getenv("MMR_GEMM_BIG");
-  if (w4e || cfge) {
-    run(w4e ? atoi(w4e) : 1, cfge ? atoi(cfge) : 1);
-  } else {
-    const int v = tuned_variant(m, n, k, act, hb, hr, x, residual, y, st, run);
-    run(kVarW4[v], kVarCfg[v]);
-  }
+  // the pinned variant (mmr_pin_variant), else the shape's tuned variant (tuned once per process on
+  // the first call with that shape)
+  const int pin = mmr::pin_gemm_bf16.load(std::memory_order_relaxed);
+  const int v = (pin >= 0 && pin < kVariants) ? pin : tuned_variant(m, n, k, act, hb, hr, x, residual, y, st, run);
+  run(kVarW4[v], kVarCfg[v]);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }

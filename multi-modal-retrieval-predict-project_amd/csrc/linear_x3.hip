@@ -149,10 +149,8 @@ extern "C" mmr_status mmr_linear_x3(const float* x, int64_t ldx, int64_t bsx, co
   // 8 waves per tile when the launch has fewer than 2 tiles per CU (the joint chain at B = 256:
   // 96-384 tiles) and the K range splits evenly into 8
   int nw = (cin % 256 == 0 && (int64_t)grid.x * grid.y < 512) ? 8 : 4;
-  if (const char* e = getenv("MMR_X3_NW")) {  // A/B override (4 / 8)
-    const int v = atoi(e);
-    if (v == 4 || (v == 8 && cin % 256 == 0)) nw = v;
-  }
+  const int pin = mmr::pin_x3_waves.load(std::memory_order_relaxed);  // mmr_pin_variant (tests)
+  if (pin == 4 || (pin == 8 && cin % 256 == 0)) nw = pin;
 #define X3_L(A, B_, R_)                                                                                          \
   (nw == 8 ? linear_x3<A, B_, R_, 8><<<grid, 512, 0, st>>>(x, ldx, w_hi, w_lo, bias, residual, ldr, y, ldy, b, cin, \
                                                          cout, bsx, bsw, bsb, bsr, bsy)                          \

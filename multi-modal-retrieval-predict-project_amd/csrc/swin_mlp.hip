@@ -7,8 +7,8 @@
 // k-permutation that the packed W2 columns mirror), bias + GELU, then accumulate fc2 (C^T, A = W2
 // from LDS).  Weights are repacked once at load into per-64-hidden-unit chunks
 // [W1 rows | W2 columns] that are exact, bank-conflict-free LDS images.
-//   C = 96  (swin_mlp_res): all of W1 + W2 (147 KiB) resident in LDS, one persistent workgroup per
-//           CU, waves walk token tiles independently (no barriers), next tile's x prefetched.
+//   C = 96  (swin_mlp_sp): all of W1 + W2 (147 KiB) resident in LDS, one persistent workgroup per
+//           CU, waves walk token tiles independently (no barriers), software-pipelined fc1 / GELU / fc2.
 //   C = 192 (swin_mlp): 590 KiB of weights streamed through a 3-deep LDS ring by global_load_lds,
 //           shared by the workgroup's 256 tokens.
 // HBM traffic per token: 2C (x) + 2C (y) bytes, vs ~24C for the LN -> GEMM -> GEMM chain.
@@ -103,18 +103,6 @@ template <bool FAST>
 __device__ __forceinline__ float gelu_t(float v) {
   if constexpr (FAST) return mmr::gelu_fast(v);
   else return mmr::gelu_erf(v);
-}
-
-// bias + GELU of two hidden values -> packed bf16 pair; FAST on packed f32 math (v_pk_add / v_pk_fma
-// / v_pk_mul: half the VALU issues — the kernel is VALU-bound on GELU)
-template <bool FAST>
-__device__ __forceinline__ uint32_t gelu_pack(float a0, float a1, float b0, float b1) {
-  if constexpr (FAST) {
-    const mmr::f32x2_t u = mmr::gelu_fast2((mmr::f32x2_t){a0, a1} + (mmr::f32x2_t){b0, b1});
-    return mmr::pack2bf(u.x, u.y);
-  } else {
-    return mmr::pack2bf(gelu_t<FAST>(a0 + b0), gelu_t<FAST>(a1 + b1));
-  }
 }
 
 // GELU of two hidden values whose bias is already in the accumulator -> packed bf16 pair
@@ -279,409 +267,13 @@ __global__ __launch_bounds__(64 * NW) void swin_mlp(const uint16_t* __restrict__
 }
 
 
-// Software-pipelined streamed variant (C = 192): the swin_mlp_sp schedule — iteration t runs fc1 of
-// hidden block t+1 and fc2 of block t-1 beside the GELU of block t — over the streamed weight ring.
-// Step t uses chunk t / 2 (HC = 64: two 32-wide blocks per chunk); at odd t = 2c+1 the waves wait
-// for chunk c+1 (fc1 of block 2c+2) and, past the barrier, every wave is done with chunk c-1 (its
-// last fc2 ran at t = 2c), so its ring slot is refilled with chunk c+2 — needed two iterations on.
-template <int C, int NW, int HC, bool FAST>
-__global__ __launch_bounds__(64 * NW) void swin_mlp_sps(const uint16_t* __restrict__ x,
-                                                        const float* __restrict__ lng,
-                                                        const float* __restrict__ lnb,
-                                                        const uint16_t* __restrict__ pack,
-                                                        const float* __restrict__ b1,
-                                                        const float* __restrict__ b2,
-                                                        uint16_t* __restrict__ y, int64_t T, float eps) {
-  constexpr int R = 3;
-  using G = MlpGeo<C, NW, HC, R>;
-  static_assert(HC == 64, "two 32-wide hidden blocks per chunk");
-  constexpr int NB = 4 * C / 32;  // hidden blocks
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // the weight ring only
-  __shared__ __attribute__((aligned(16))) float Pg[6 * C];
-  const float* Pb = Pg + C;
-  const float* Pb1 = Pg + 2 * C;
-
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r = lane & 31, h = lane >> 5;
-  const int64_t tok = (int64_t)blockIdx.x * G::TOK + wave * 32 + r;
-  const bool ok = tok < T;
-  const uint16_t* xr = x + (ok ? tok : 0) * C;
-
-  for (int i = threadIdx.x; i < 6 * C; i += 64 * NW)
-    Pg[i] = i < C ? lng[i] : (i < 2 * C ? lnb[i - C] : b1[i - 2 * C]);
-  bf16x8 xb[G::KS1];
-#pragma unroll
-  for (int ks = 0; ks < G::KS1; ++ks) {
-    const bf16x8 v = *(const bf16x8*)(xr + 16 * ks + 8 * h);  // clamped row: unconditional load
-    xb[ks] = ok ? v : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-  }
-  auto stage = [&](int ch) {
-    const unsigned char* src = (const unsigned char*)pack + (size_t)ch * G::CHUNK_B;
-    unsigned char* dst = smem + (ch % R) * G::CHUNK_B;
-#pragma unroll
-    for (int p = 0; p < G::PW; ++p) {
-      const int piece = wave * G::PW + p;
-      __builtin_amdgcn_global_load_lds((const void*)(src + piece * 1024 + lane * 16),
-                                       (lds_ptr_t)(dst + piece * 1024), 16, 0, 0);
-    }
-  };
-  stage(0);
-  stage(1);
-  stage(2);
-  // x, the parameters and chunks 0, 1 landed (chunk 2 may still be in flight)
-  __builtin_amdgcn_s_waitcnt(vmcnt_n(G::PW));
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-
-  // LayerNorm (row split over the lane pair h = 0, 1), written back over xb as the fc1 B operand
-  {
-    float s = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < G::KS1; ++ks)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s += mmr::bf2f((uint16_t)xb[ks][j]);
-    s += __shfl_xor(s, 32, 64);
-    const float mean = s * (1.0f / C);
-    float ss = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < G::KS1; ++ks)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float d = mmr::bf2f((uint16_t)xb[ks][j]) - mean;
-        ss += d * d;
-      }
-    ss += __shfl_xor(ss, 32, 64);
-    const float rstd = rsqrtf(ss * (1.0f / C) + eps);
-#pragma unroll
-    for (int ks = 0; ks < G::KS1; ++ks) {
-      const int k0 = 16 * ks + 8 * h;
-      const f32x4 g0 = *(const f32x4*)(Pg + k0), g1 = *(const f32x4*)(Pg + k0 + 4);
-      const f32x4 c0 = *(const f32x4*)(Pb + k0), c1 = *(const f32x4*)(Pb + k0 + 4);
-      const float gg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
-      const float cc[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (mmr::bf2f((uint16_t)xb[ks][j]) - mean) * rstd * gg[j] + cc[j];
-      xb[ks] = __builtin_bit_cast(bf16x8, make_uint4(mmr::pack2bf(v[0], v[1]), mmr::pack2bf(v[2], v[3]),
-                                                     mmr::pack2bf(v[4], v[5]), mmr::pack2bf(v[6], v[7])));
-    }
-  }
-
-  f32x16 acc2[G::NU];
-#pragma unroll
-  for (int u = 0; u < G::NU; ++u)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc2[u][e] = 0.f;
-
-  auto fc1 = [&](int t) {
-    f32x16 a;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const f32x4 bb = *(const f32x4*)(Pb1 + 32 * t + 8 * i + 4 * h);
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) a[4 * i + rr] = bb[rr];
-    }
-    const unsigned char* W1s = smem + ((t >> 1) % R) * G::CHUNK_B;
-    const int row = 32 * (t & 1) + r;
-#pragma unroll
-    for (int ks = 0; ks < G::KS1; ++ks) {
-      const bf16x8 w = *(const bf16x8*)(W1s + (row * G::U1 + unit_swz<G::U1>(row, 2 * ks + h)) * 16);
-      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w, xb[ks], a, 0, 0, 0);
-    }
-    return a;
-  };
-  auto gelu = [&](const f32x16& a, uint32_t* hp) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      hp[2 * i] = gelu_pack2<FAST>(a[4 * i], a[4 * i + 1]);
-      hp[2 * i + 1] = gelu_pack2<FAST>(a[4 * i + 2], a[4 * i + 3]);
-    }
-  };
-  auto fc2 = [&](int t, const uint32_t* hp) {
-    const unsigned char* W2s = smem + ((t >> 1) % R) * G::CHUNK_B + G::W1B;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8 hf = __builtin_bit_cast(bf16x8, make_uint4(hp[4 * s2], hp[4 * s2 + 1], hp[4 * s2 + 2], hp[4 * s2 + 3]));
-      const int q = 2 * (2 * (t & 1) + s2) + h;
-#pragma unroll
-      for (int u = 0; u < G::NU; ++u) {
-        const int c = 32 * u + r;
-        const bf16x8 w = *(const bf16x8*)(W2s + (c * G::U2 + unit_swz<G::U2>(c, q)) * 16);
-        acc2[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w, hf, acc2[u], 0, 0, 0);
-      }
-    }
-  };
-
-  f32x16 a1 = fc1(0);
-  uint32_t hp[8];
-  {
-    const f32x16 an = fc1(1);
-    gelu(a1, hp);
-    a1 = an;
-  }
-#pragma unroll 1
-  for (int t = 1; t < NB - 1; ++t) {
-    if (t & 1) {  // t = 2c + 1: chunk c + 1 landed everywhere; chunk c - 1's slot is free
-      const int c = t >> 1;
-      // outstanding: chunk c + 1 (issued at t = 2c - 1, or in the prologue) and nothing newer
-      __builtin_amdgcn_s_waitcnt(vmcnt_n(0));
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (c >= 1 && c + 2 < G::NCH) stage(c + 2);
-    }
-    const f32x16 an = fc1(t + 1);
-    uint32_t hn[8];
-    gelu(a1, hn);
-    fc2(t - 1, hp);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) hp[e] = hn[e];
-    a1 = an;
-  }
-  {
-    uint32_t hn[8];
-    gelu(a1, hn);
-    fc2(NB - 2, hp);
-    fc2(NB - 1, hn);
-  }
-
-  // y[tok][c] = x + b2 + fc2, c = 32u + 8i + 4h + rr
-  if (ok) {
-#pragma unroll
-    for (int u = 0; u < G::NU; ++u)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int c = 32 * u + 8 * i + 4 * h;
-        const float4 bb = *(const float4*)(b2 + c);
-        const uint2 xv = *(const uint2*)(xr + c);
-        const float v0 = acc2[u][4 * i] + bb.x + __uint_as_float(xv.x << 16);
-        const float v1 = acc2[u][4 * i + 1] + bb.y + __uint_as_float(xv.x & 0xFFFF0000u);
-        const float v2 = acc2[u][4 * i + 2] + bb.z + __uint_as_float(xv.y << 16);
-        const float v3 = acc2[u][4 * i + 3] + bb.w + __uint_as_float(xv.y & 0xFFFF0000u);
-        *(uint2*)(y + tok * C + c) = make_uint2(mmr::pack2bf(v0, v1), mmr::pack2bf(v2, v3));
-      }
-  }
-}
-
-// Resident-weight variant (C = 96: W1 + W2 = 147 KiB fit in one CU's LDS).  One workgroup per CU,
-// persistent: each wave walks 32-token tiles on its own (no barrier after the one-time weight
-// load), prefetching the next tile's x into registers while it computes the current one.
-template <int C, int NW, bool FAST, bool XRES, bool PF = true>
-__global__ __launch_bounds__(64 * NW) void swin_mlp_res(const uint16_t* __restrict__ x,
-                                                        const float* __restrict__ lng,
-                                                        const float* __restrict__ lnb,
-                                                        const uint16_t* __restrict__ pack,
-                                                        const float* __restrict__ b1,
-                                                        const float* __restrict__ b2,
-                                                        uint16_t* __restrict__ y, int64_t T, float eps) {
-  using G = MlpGeo<C, NW, 64, 2>;
-  constexpr int WB = G::NCH * G::CHUNK_B;
-  constexpr int PWW = WB / 1024 / NW;
-  static_assert(WB % (1024 * NW) == 0, "weights must split evenly over the waves");
-  // all weight chunks, then the f32 parameters (one dynamic LDS object: reads of a separate static
-  // array after global_load_lds draw a conservative vmcnt(0) from hipcc)
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* Pg = (float*)(smem + WB);
-  const float* Pb = Pg + C;
-  const float* Pb1 = Pg + 2 * C;
-  const float* Pb2 = Pg + 6 * C;
-
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r = lane & 31, h = lane >> 5;
-  const int64_t ntile = (T + 31) / 32, stride = (int64_t)gridDim.x * NW;
-  int64_t tile = (int64_t)blockIdx.x * NW + wave;
-
-  for (int i = threadIdx.x; i < 7 * C; i += 64 * NW)
-    Pg[i] = i < C ? lng[i] : (i < 2 * C ? lnb[i - C] : (i < 6 * C ? b1[i - 2 * C] : b2[i - 6 * C]));
-#pragma unroll
-  for (int p = 0; p < PWW; ++p) {
-    const int piece = wave * PWW + p;
-    __builtin_amdgcn_global_load_lds((const void*)((const unsigned char*)pack + piece * 1024 + lane * 16),
-                                     (lds_ptr_t)(smem + piece * 1024), 16, 0, 0);
-  }
-  auto load_x = [&](int64_t tl, bf16x8* dst) {
-    const int64_t tk = tl * 32 + r;
-    const bool ok = tl < ntile && tk < T;
-    const uint16_t* xr = x + (ok ? tk : 0) * C;
-#pragma unroll
-    for (int ks = 0; ks < G::KS1; ++ks)
-      dst[ks] = ok ? *(const bf16x8*)(xr + 16 * ks + 8 * h) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-  };
-  bf16x8 xn[G::KS1];
-  if constexpr (PF) load_x(tile, xn);
-  __builtin_amdgcn_s_waitcnt(vmcnt_n(0));
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-
-  for (; tile < ntile; tile += stride) {
-    asm volatile("" ::: "memory");  // keep the LN/bias parameter reads in the loop (LICM would pin
-                                    // ~100 VGPRs of them across it)
-    bf16x8 xr[G::KS1], xb[G::KS1];
-    if constexpr (PF) {
-#pragma unroll
-      for (int ks = 0; ks < G::KS1; ++ks) xr[ks] = xn[ks];
-      load_x(tile + stride, xn);  // next tile's x in flight during this one
-    } else {
-      load_x(tile, xr);  // (3 waves per SIMD hide the latency instead of a prefetch register set)
-    }
-    const int64_t tok = tile * 32 + r;
-
-    // LayerNorm (row split over the lane pair h = 0, 1) -> fc1 B operand
-    {
-      float s = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < G::KS1; ++ks)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s += mmr::bf2f((uint16_t)xr[ks][j]);
-      s += __shfl_xor(s, 32, 64);
-      const float mean = s * (1.0f / C);
-      float ss = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < G::KS1; ++ks)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float d = mmr::bf2f((uint16_t)xr[ks][j]) - mean;
-          ss += d * d;
-        }
-      ss += __shfl_xor(ss, 32, 64);
-      const float rstd = rsqrtf(ss * (1.0f / C) + eps);
-#pragma unroll
-      for (int ks = 0; ks < G::KS1; ++ks) {
-        const int k0 = 16 * ks + 8 * h;
-        const f32x4 g0 = *(const f32x4*)(Pg + k0), g1 = *(const f32x4*)(Pg + k0 + 4);
-        const f32x4 c0 = *(const f32x4*)(Pb + k0), c1 = *(const f32x4*)(Pb + k0 + 4);
-        const float gg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
-        const float cc[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (mmr::bf2f((uint16_t)xr[ks][j]) - mean) * rstd * gg[j] + cc[j];
-        xb[ks] = __builtin_bit_cast(bf16x8, make_uint4(mmr::pack2bf(v[0], v[1]), mmr::pack2bf(v[2], v[3]),
-                                                       mmr::pack2bf(v[4], v[5]), mmr::pack2bf(v[6], v[7])));
-      }
-    }
-
-    f32x16 acc2[G::NU];
-#pragma unroll
-    for (int u = 0; u < G::NU; ++u)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc2[u][e] = 0.f;
-
-    // hidden loop, software-pipelined: the W1 fragments of step t+1 and the W2 fragments of step t
-    // are in flight while step t's GELU runs
-    auto rd_w1 = [&](int t, bf16x8* f) {
-      const unsigned char* W1s = smem + (t >> 1) * G::CHUNK_B;
-      const int row = 32 * (t & 1) + r;
-#pragma unroll
-      for (int ks = 0; ks < G::KS1; ++ks)
-        f[ks] = *(const bf16x8*)(W1s + (row * G::U1 + unit_swz<G::U1>(row, 2 * ks + h)) * 16);
-    };
-    auto rd_w2 = [&](int t, bf16x8* f) {
-      const unsigned char* W2s = smem + (t >> 1) * G::CHUNK_B + G::W1B;
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int u = 0; u < G::NU; ++u) {
-          const int c = 32 * u + r, q = 2 * (2 * (t & 1) + s2) + h;
-          f[s2 * G::NU + u] = *(const bf16x8*)(W2s + (c * G::U2 + unit_swz<G::U2>(c, q)) * 16);
-        }
-    };
-    if constexpr (!PF) {
-      // 3 waves per SIMD (register budget 168): fragments read just in time, no prefetch
-      // register sets — the co-resident waves hide the LDS latency
-#pragma unroll 1
-      for (int t = 0; t < 4 * C / 32; ++t) {
-        f32x16 a1;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const f32x4 bb = *(const f32x4*)(Pb1 + 32 * t + 8 * i + 4 * h);
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) a1[4 * i + rr] = bb[rr];
-        }
-        {
-          bf16x8 w1f[G::KS1];
-          rd_w1(t, w1f);
-#pragma unroll
-          for (int ks = 0; ks < G::KS1; ++ks) a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1f[ks], xb[ks], a1, 0, 0, 0);
-        }
-        uint32_t hp[8];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          hp[2 * i] = gelu_pack2<FAST>(a1[4 * i], a1[4 * i + 1]);
-          hp[2 * i + 1] = gelu_pack2<FAST>(a1[4 * i + 2], a1[4 * i + 3]);
-        }
-        const unsigned char* W2s = smem + (t >> 1) * G::CHUNK_B + G::W1B;
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16x8 hf = __builtin_bit_cast(bf16x8, make_uint4(hp[4 * s2], hp[4 * s2 + 1], hp[4 * s2 + 2],
-                                                                  hp[4 * s2 + 3]));
-#pragma unroll
-          for (int u = 0; u < G::NU; ++u) {
-            const int c = 32 * u + r, q = 2 * (2 * (t & 1) + s2) + h;
-            const bf16x8 w = *(const bf16x8*)(W2s + (c * G::U2 + unit_swz<G::U2>(c, q)) * 16);
-            acc2[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w, hf, acc2[u], 0, 0, 0);
-          }
-        }
-      }
-    }
-    bf16x8 w1f[G::KS1], w2f[2 * G::NU];
-    if constexpr (PF) rd_w1(0, w1f);
-#pragma unroll 1
-    for (int t = 0; t < (PF ? 4 * C / 32 : 0); ++t) {  // 32 hidden units per step
-      f32x16 a1;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) a1[e] = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < G::KS1; ++ks) a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1f[ks], xb[ks], a1, 0, 0, 0);
-      rd_w2(t, w2f);
-      if (t + 1 < 4 * C / 32) rd_w1(t + 1, w1f);
-      uint32_t hp[8];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const f32x4 bb = *(const f32x4*)(Pb1 + 32 * t + 8 * i + 4 * h);
-        hp[2 * i] = gelu_pack<FAST>(a1[4 * i], a1[4 * i + 1], bb[0], bb[1]);
-        hp[2 * i + 1] = gelu_pack<FAST>(a1[4 * i + 2], a1[4 * i + 3], bb[2], bb[3]);
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 hf = __builtin_bit_cast(bf16x8, make_uint4(hp[4 * s2], hp[4 * s2 + 1], hp[4 * s2 + 2],
-                                                                hp[4 * s2 + 3]));
-#pragma unroll
-        for (int u = 0; u < G::NU; ++u)
-          acc2[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2f[s2 * G::NU + u], hf, acc2[u], 0, 0, 0);
-      }
-    }
-
-    // y = x + b2 + fc2: lane half h holds channels 32u + 16 half + 8h + 0..7 (w2_channel order)
-    if (tok < T) {
-#pragma unroll
-      for (int u = 0; u < G::NU; ++u)
-#pragma unroll
-        for (int hf2 = 0; hf2 < 2; ++hf2) {
-          const int c0 = 32 * u + 16 * hf2 + 8 * h;
-          const f32x4 bl = *(const f32x4*)(Pb2 + c0), bh = *(const f32x4*)(Pb2 + c0 + 4);
-          const bf16x8 xv = XRES ? xr[2 * u + hf2] : *(const bf16x8*)(x + tok * C + c0);
-          float v[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            v[j] = acc2[u][8 * hf2 + j] + (j < 4 ? bl[j] : bh[j - 4]) + mmr::bf2f((uint16_t)xv[j]);
-          *(uint4*)(y + tok * C + c0) = make_uint4(mmr::pack2bf(v[0], v[1]), mmr::pack2bf(v[2], v[3]),
-                                                   mmr::pack2bf(v[4], v[5]), mmr::pack2bf(v[6], v[7]));
-        }
-    }
-  }
-}
-
 // Software-pipelined resident variant (C = 96): iteration t runs fc1 of hidden block t+1 and fc2 of
 // block t-1 (12 MFMAs) beside the bias'd GELU of block t (VALU) — three mutually independent
 // streams in one basic block, so the matrix pipe works under the GELU instead of waiting for it
 // (the forms above serialise fc1 -> GELU -> fc2 inside a wave and rely on other waves to fill the
 // gaps).  2 waves per SIMD (<= 256 VGPRs: two fc1 accumulators, both packed hidden sets, the fc2
 // accumulators, the LN'd x of this tile and the next tile's x; the residual is re-read from L2).
-template <int C, int NW, bool FAST, bool SCAL = false>
+template <int C, int NW, bool FAST>
 __global__ __launch_bounds__(64 * NW) void swin_mlp_sp(const uint16_t* __restrict__ x,
                                                        const float* __restrict__ lng,
                                                        const float* __restrict__ lnb,
@@ -754,13 +346,8 @@ __global__ __launch_bounds__(64 * NW) void swin_mlp_sp(const uint16_t* __restric
   auto gelu = [&](const f32x16& a, uint32_t* hp) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      if constexpr (SCAL) {  // scalar f32 (packed f32 math is slow beside MFMAs)
-        hp[2 * i] = mmr::pack2bf(mmr::gelu_fast1(a[4 * i]), mmr::gelu_fast1(a[4 * i + 1]));
-        hp[2 * i + 1] = mmr::pack2bf(mmr::gelu_fast1(a[4 * i + 2]), mmr::gelu_fast1(a[4 * i + 3]));
-      } else {
-        hp[2 * i] = gelu_pack2<FAST>(a[4 * i], a[4 * i + 1]);
-        hp[2 * i + 1] = gelu_pack2<FAST>(a[4 * i + 2], a[4 * i + 3]);
-      }
+      hp[2 * i] = gelu_pack2<FAST>(a[4 * i], a[4 * i + 1]);
+      hp[2 * i + 1] = gelu_pack2<FAST>(a[4 * i + 2], a[4 * i + 3]);
     }
   };
   auto fc2 = [&](int t, const uint32_t* hp, f32x16* acc2) {
@@ -885,26 +472,13 @@ int cu_count() {
   return n;
 }
 
-template <int C, int NW, bool FAST, bool XRES, bool PF = true>
-mmr_status launch_res(const uint16_t* x, const float* g, const float* b, const uint16_t* pack,
-                      const float* b1, const float* b2, uint16_t* y, int64_t T, float eps,
-                      hipStream_t st) {
-  using G = MlpGeo<C, NW, 64, 2>;
-  const int64_t wave_tiles = (T + 31) / 32;
-  const int64_t grid = std::min<int64_t>(cu_count(), (wave_tiles + NW - 1) / NW);
-  swin_mlp_res<C, NW, FAST, XRES, PF><<<dim3((unsigned)grid), 64 * NW, G::NCH * G::CHUNK_B + 7 * C * 4, st>>>(
-      x, g, b, pack, b1, b2, y, T, eps);
-  MMR_LAUNCH_CHECK();
-  return MMR_OK;
-}
-
-template <int C, int NW, bool FAST, bool SCAL = false>
+template <int C, int NW, bool FAST>
 mmr_status launch_sp(const uint16_t* x, const float* g, const float* b, const uint16_t* pack,
                      const float* b1, const float* b2, uint16_t* y, int64_t T, float eps, hipStream_t st) {
   using G = MlpGeo<C, NW, 64, 2>;
   const int64_t wave_tiles = (T + 31) / 32;
   const int64_t grid = std::min<int64_t>(cu_count(), (wave_tiles + NW - 1) / NW);
-  swin_mlp_sp<C, NW, FAST, SCAL><<<dim3((unsigned)grid), 64 * NW, G::NCH * G::CHUNK_B + 7 * C * 4, st>>>(
+  swin_mlp_sp<C, NW, FAST><<<dim3((unsigned)grid), 64 * NW, G::NCH * G::CHUNK_B + 7 * C * 4, st>>>(
       x, g, b, pack, b1, b2, y, T, eps);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
@@ -914,16 +488,6 @@ template <int C, int HC, bool PERM>
 mmr_status launch_pack(const uint16_t* w1, const uint16_t* w2, uint16_t* pack, hipStream_t st) {
   const int64_t n = (int64_t)8 * C * C;
   swin_mlp_pack<C, HC, PERM><<<dim3((unsigned)mmr::ceil_div(n, 256)), 256, 0, st>>>(w1, w2, pack);
-  MMR_LAUNCH_CHECK();
-  return MMR_OK;
-}
-
-template <int C, int NW, int HC, bool FAST>
-mmr_status launch_stream_sp(const uint16_t* x, const float* g, const float* b, const uint16_t* pack,
-                            const float* b1, const float* b2, uint16_t* y, int64_t T, float eps, hipStream_t st) {
-  using G = MlpGeo<C, NW, HC, 3>;
-  swin_mlp_sps<C, NW, HC, FAST><<<dim3((unsigned)mmr::ceil_div(T, G::TOK)), 64 * NW, G::LDS_B, st>>>(
-      x, g, b, pack, b1, b2, y, T, eps);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }
@@ -968,24 +532,11 @@ mmr_status mmr_swin_mlp(const uint16_t* x, const float* ln_g, const float* ln_b,
   MMR_REQUIRE(x != y, "mmr_swin_mlp: in-place not supported");
   if (tokens == 0) return MMR_OK;
   hipStream_t st = mmr::as_stream(stream);
-  if (c == 96) {
-    // default (MMR_SWIN_MLP_CFG=3): the software-pipelined form, 2 waves per SIMD — 215 -> 199 us at
-    // B = 256, bitwise equal (profiles/r03_swin_mlp_sp_ab.txt); =1: 12 waves (3 per SIMD) reading
-    // fragments just in time; =0: the 8-wave prefetching form; =2: 8 waves without prefetch
-    // (profiles/r03_swin_mlp_ab.txt)
-    const char* e = getenv("MMR_SWIN_MLP_CFG");
-    const int cfg = e ? atoi(e) : 3;
-    if (cfg == 0) return launch_res<96, 8, true, true>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
-    if (cfg == 1) return launch_res<96, 12, true, false, false>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
-    if (cfg == 2) return launch_res<96, 8, true, false, false>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
-    if (cfg == 4) return launch_sp<96, 8, true, true>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
-    return launch_sp<96, 8, true>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
-  }
-  if (c == 192) {
-    const char* e = getenv("MMR_SWIN_MLP_CFG");
-    if (e && atoi(e) == 5) return launch_stream_sp<192, 8, 64, true>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
-    return launch_stream<192, 8, 64, 3, true>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
-  }
+  // C = 96: the software-pipelined resident form, 2 waves per SIMD (215 -> 199 us at B = 256 over the
+  // serial resident forms, which were removed: profiles/r03_swin_mlp_sp_ab.txt, r03_swin_mlp_ab.txt);
+  // C = 192: the streamed form (its software-pipelined twin measured equal and was removed)
+  if (c == 96) return launch_sp<96, 8, true>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
+  if (c == 192) return launch_stream<192, 8, 64, 3, true>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
   mmr::set_error("mmr_swin_mlp: C=%d not built (96, 192)", c);
   return MMR_ERR_UNSUPPORTED;
 }

@@ -938,10 +938,6 @@ static mmr_status layernorm_launch(const uint16_t* x, const uint16_t* r, const f
     lpr = 64;
     while (lpr > 8 && nch <= (lpr / 2) * 2) lpr /= 2;
   }
-  if (const char* e = getenv("MMR_LN_LPR")) {  // diagnostic override (8/16/32/64; <= 8 chunks per lane)
-    const int l = atoi(e);
-    if ((l == 8 || l == 16 || l == 32 || l == 64) && (nch + l - 1) / l <= 8) lpr = l;
-  }
   const int cpl = (nch + lpr - 1) / lpr;                   // chunks per lane
   const int64_t rows_per_block = 4 * (64 / lpr);
   const dim3 grid((unsigned)mmr::ceil_div(rows, rows_per_block));

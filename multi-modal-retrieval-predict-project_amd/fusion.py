@@ -32,7 +32,6 @@ multiple keep bf16 there.
 """
 import collections
 import math
-import os
 
 import torch
 
@@ -119,6 +118,7 @@ class FusionStack:
     def __init__(self, sd, num_heads, device="cuda", use_shared_ffn=False, eps=1e-5, tower_dtype="bf16"):
         dev = torch.device(device)
         self.device, self.heads, self.eps = dev, num_heads, eps
+        self.side_streams = True  # patch-side layer work on a side stream (False: one stream)
         fp8 = tower_dtype == "fp8"
         self.fp8 = fp8
         x3 = tower_dtype == "x3"
@@ -187,8 +187,7 @@ class FusionStack:
             self.layers.append(L)
         self.s_w, self.s_b = _bf(sd["self_attn.in_proj_weight"], dev), _f(sd["self_attn.in_proj_bias"], dev)
         # combiner QKV on MX-fp8 (its operand written by the sequence assembly itself)
-        self.s_w8 = (_w8(self.s_w) if fp8 and D % 256 == 0 and os.environ.get("MMR_COMB_FP8", "1") != "0"
-                     else None)  # MMR_COMB_FP8=0: bf16 combiner QKV (A/B)
+        self.s_w8 = _w8(self.s_w) if fp8 and D % 256 == 0 else None
         self.s_x3 = ops.X3W(_f(sd["self_attn.in_proj_weight"], dev)) if x3 else None
         self.s_ow, self.s_ob = _f(sd["self_attn.out_proj.weight"], dev), _f(sd["self_attn.out_proj.bias"], dev)
         self.pe = _f(sd["pos_encoder.pe"][0], dev)
@@ -251,9 +250,9 @@ class FusionStack:
         # the patch-side token work of every layer (enhancer, folded k/v/q projection, patch
         # projection) depends only on the image tower: it runs on a side stream, ahead of and
         # concurrently with the text-side work, which waits per layer on an event before the
-        # cross attentions (MMR_FUSION_STREAMS=0: one stream)
+        # cross attentions (side_streams = False: one stream)
         # (first call in sequence: see MultiModalRetrievalModel._towers)
-        two = getattr(self, "_warm", False) and os.environ.get("MMR_FUSION_STREAMS", "1") != "0"
+        two = getattr(self, "_warm", False) and self.side_streams
         self._warm = True
         main = torch.cuda.current_stream(dev)
         side = self._side_stream(main) if two else main

@@ -271,6 +271,7 @@ class MultiModalRetrievalModel:
         self.retriever = retriever
         self._side = None
         self._warm = False
+        self.concurrent_towers = True  # Swin tower on a side stream beside BERT (False: in sequence)
         hs = head_state if head_state is not None else sd
         if hs is None:  # training=True without a checkpoint: seeded random init (the reference's fresh model)
             hs = init_head_state(self.backbones.img_dim, self.backbones.txt_dim, joint_dim, seed + 2)
@@ -372,10 +373,10 @@ class MultiModalRetrievalModel:
         kernels leave idle (wave-quantisation tails, small LayerNorm / attention launches); the
         two towers share no data until the heads.  The first call runs them in sequence: the GEMM
         launcher times its variants per shape on first use, which concurrent kernels would skew.
-        MMR_TOWER_STREAMS=0 always runs them in sequence."""
+        concurrent_towers = False always runs them in sequence."""
         first = not self._warm
         self._warm = True
-        if first or os.environ.get("MMR_TOWER_STREAMS", "1") == "0":
+        if first or not self.concurrent_towers:
             return (self.backbones.encode_image(image, want_patches=want_patches),
                     self.backbones.encode_text(input_ids, attention_mask))
         main = torch.cuda.current_stream(self.device)

@@ -2,6 +2,8 @@
 hand-written gfx950 kernel on torch's current stream and raises if the library or the GPU is
 missing — there is no torch fallback.  bf16 activations travel as torch.bfloat16 tensors (same
 bits as the C ABI's uint16)."""
+import contextlib
+
 import torch
 
 from . import _lib
@@ -34,6 +36,20 @@ def _s(t):
 
 def _chk(status, what):
     _lib.check(status, what)
+
+
+PIN_GEMM_BF16, PIN_X3_WAVES = 0, 1  # mmr.h MMR_PIN_*
+
+
+@contextlib.contextmanager
+def pinned(which, value):
+    """Pin a launch variant for the duration (mmr_pin_variant: tests and A/B tools only; the product
+    path never pins).  PIN_GEMM_BF16: mmr_linear_bf16 variant index; PIN_X3_WAVES: 4 / 8."""
+    _chk(_L().mmr_pin_variant(which, value), "mmr_pin_variant")
+    try:
+        yield
+    finally:
+        _chk(_L().mmr_pin_variant(which, -1), "mmr_pin_variant")
 
 
 def linear(x, w, bias=None, residual=None, act=0, out=None):

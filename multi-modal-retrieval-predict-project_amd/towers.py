@@ -17,7 +17,6 @@ Per-block dataflow (all hand-written kernels, bf16 activations, f32 accumulation
                FFN1 GEMM(+bias, GELU) -> FFN2 GEMM(+bias) -> LN(+residual)   (post-LN residual
                adds ride in the LayerNorm kernel, so the GEMMs run the residual-free epilogue)
 """
-import os
 
 import torch
 
@@ -88,16 +87,10 @@ def _mlp8(h, w1_8, b1, w2_8, b2, residual=None, h8=None):
     return (y if rp == rows else y[:rows]).reshape(tuple(h.shape[:-1]) + (y.shape[-1],))
 
 
-_LN8_PAD = os.environ.get("MMR_LN8_PAD", "1") != "0"
-_SWA_Q8 = os.environ.get("MMR_SWA_Q8", "1") != "0"  # A/B switch: window attention emits the proj operand
-
-
 def _ln8_ok(x, w8):
     """The LayerNorm can emit the fp8 operand itself: rows a multiple of 256, C of 32 (K padded to the
     weight's kp, e.g. stage 3's C = 384 -> 512, is written by the LayerNorm too)."""
     C = x.shape[-1]
-    if not _LN8_PAD:  # A/B switch (MMR_LN8_PAD=0): unpadded C % 256 == 0 only, as before
-        return w8 is not None and C % 256 == 0 and (x.numel() // C) % 256 == 0 and w8.kp == C
     return w8 is not None and C % 32 == 0 and (x.numel() // C) % 256 == 0 and w8.kp >= C
 
 
@@ -194,7 +187,7 @@ class SwinTower:
             if i > 0:
                 w8 = st["ds_w8"]
                 B, H2 = x.shape[0], x.shape[1] // 2
-                if (_SWA_Q8 and w8 is not None and (B * H2 * H2) % 256 == 0 and w8.kp == 4 * x.shape[-1]
+                if (w8 is not None and (B * H2 * H2) % 256 == 0 and w8.kp == 4 * x.shape[-1]
                         and w8.kp <= 2048):  # the gather + LN writes the reduction's fp8 operand
                     _, m8 = ops.patch_merge_ln_q8(x, st["ds_g"], st["ds_b"], 1e-5)
                     x = ops.linear_mxfp8(m8, w8, None, lead=(B, H2, H2))
@@ -210,13 +203,9 @@ class SwinTower:
                 elif _ln8_ok(x, bk["qkv_w8"]):  # fp8 stage: the LN emits the QKV operand (no bf16 rows)
                     _, h8 = ops.layernorm_q8(x, None, bk["n1g"], bk["n1b"], 1e-5, kp=bk["qkv_w8"].kp, want_y=False)
                     qkv = ops.linear_mxfp8(h8, bk["qkv_w8"], bk["qkv_b"], lead=tuple(x.shape[:-1]))
-                    if _SWA_Q8:  # the attention core writes the proj operand (no bf16 rows, no quantise pass)
-                        a8 = ops.swin_window_attention_q8(qkv, bk["bias"], H, heads, ws, bk["shift"],
-                                                          kp=bk["proj_w8"].kp)
-                        x = ops.linear_mxfp8(a8, bk["proj_w8"], bk["proj_b"], x, lead=tuple(x.shape[:-1]))
-                    else:
-                        a = ops.swin_window_attention(qkv, bk["bias"], H, heads, ws, bk["shift"])
-                        x = _lin(a, bk["proj_w"], bk["proj_b"], residual=x, w8=bk["proj_w8"])
+                    # the attention core writes the proj operand (no bf16 rows, no quantise pass)
+                    a8 = ops.swin_window_attention_q8(qkv, bk["bias"], H, heads, ws, bk["shift"], kp=bk["proj_w8"].kp)
+                    x = ops.linear_mxfp8(a8, bk["proj_w8"], bk["proj_b"], x, lead=tuple(x.shape[:-1]))
                 else:
                     h = ops.layernorm(x, bk["n1g"], bk["n1b"], 1e-5)
                     qkv = (ops.linear_rw(h, bk["qkv_rw"], bk["qkv_b"]) if bk["qkv_rw"] is not None

@@ -87,15 +87,15 @@ def test_linear_x3(B, cin, cout, act, bias, res):
     assert err < 2e-5, err
 
 
-def test_linear_x3_wave_split(monkeypatch):
+def test_linear_x3_wave_split():
     """The 8-wave K split (small launches) and the 4-wave one agree with the f64 reference alike."""
     g = torch.Generator().manual_seed(11)
     x, w = torch.randn(96, 1536, generator=g), torch.randn(768, 1536, generator=g) * 1536 ** -0.5
     b = torch.randn(768, generator=g)
     ref = x.double() @ w.double().T + b.double()
-    for nw in ("4", "8"):
-        monkeypatch.setenv("MMR_X3_NW", nw)
-        out = ops.linear_x3(x.to(DEV), ops.X3W(w.to(DEV)), b.to(DEV))
+    for nw in (4, 8):
+        with ops.pinned(ops.PIN_X3_WAVES, nw):
+            out = ops.linear_x3(x.to(DEV), ops.X3W(w.to(DEV)), b.to(DEV))
         err = (out.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
         assert err < 2e-5, (nw, err)
 

@@ -338,11 +338,7 @@ def test_knn_f16_raw_query_range():
     qv = buf[1:].view(12, 256)
     ix = GalleryIndex(G, mode="f16")
     i2, _, s2, st2 = ix.search(qv, 12, want_f64=True, want_status=True)
-    os.environ["MMR_KNN_F16_RAW"] = "0"
-    try:
-        i3, _, s3, _ = ix.search(torch.from_numpy(Qm).cuda(), 12, want_f64=True, want_status=True)
-    finally:
-        del os.environ["MMR_KNN_F16_RAW"]
+    i3, _, s3, _ = ix.search(torch.from_numpy(Qm).cuda(), 12, want_f64=True, want_status=True)
     torch.cuda.synchronize()
     ix.close()
     assert int(st2.max()) == 0

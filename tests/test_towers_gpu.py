@@ -60,15 +60,16 @@ def test_linear_bf16(M, N, K, act, bias, res):
 @pytest.mark.parametrize("M,N,K,act,bias,res", [(32768, 1152, 128, 0, True, False), (32768, 1152, 384, 0, True, True),
                                                 (65536, 768, 768, 0, False, True), (32768, 2304, 256, 0, False, False),
                                                 (16384, 768, 3072, 0, True, True), (32768, 1536, 384, 1, True, False)])
-def test_linear_bf16_p8_persistent(monkeypatch, cfg, M, N, K, act, bias, res):
-    """The persistent 8-phase GEMM pinned (MMR_GEMM_BIG=7: 256x256 tiles, 8: 256x192) on shapes with
+def test_linear_bf16_p8_persistent(request, cfg, M, N, K, act, bias, res):
+    """The persistent 8-phase GEMM pinned (mmr_pin_variant: variant 9 = 256x256 tiles, 10 = 256x192) on shapes with
     2-4 tiles per workgroup and K = 128 ... 3072 (1 ... 12 K iterations per tile: the K stream runs
     on across tile boundaries), every epilogue; vs torch fp32 of the same bf16 operands (tolerance
     1e-2 * max|ref|: bf16 output rounding)."""
     if N % (256 if cfg == 7 else 192):
         pytest.skip("tile width")
-    monkeypatch.setenv("MMR_GEMM_W4", "0")
-    monkeypatch.setenv("MMR_GEMM_BIG", str(cfg))
+    pin = ops.pinned(ops.PIN_GEMM_BF16, {7: 9, 8: 10}[cfg])
+    pin.__enter__()
+    request.addfinalizer(lambda: pin.__exit__(None, None, None))
     g = torch.Generator(device=DEV).manual_seed(M + N + K + cfg)
     x = torch.randn(M, K, generator=g, device=DEV).to(torch.bfloat16)
     w = (torch.randn(N, K, generator=g, device=DEV) * 0.05).to(torch.bfloat16)

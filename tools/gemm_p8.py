@@ -1,4 +1,4 @@
-"""A/B of the 8-phase GEMM (MMR_GEMM_BIG=7 / 8) against the tuned production variant and torch
+"""A/B of the 8-phase GEMM (pinned variants 9 / 10) against the tuned production variant and torch
 F.linear (hipBLASLt) on the tower shapes, interleaved rounds in one process, random operands; each
 variant's output is checked against an fp32 torch reference of the same bf16 operands.
 Diagnostic only.  usage: python tools/gemm_p8.py [--rounds 3]"""
@@ -16,8 +16,7 @@ from mmr_amd import ops  # noqa: E402
 SHAPES = [(32768, 2304, 768, "b"), (32768, 3072, 768, "bg"), (32768, 768, 3072, "b"), (32768, 768, 768, "b"),
           (12544, 2304, 768, "b"), (50176, 1536, 384, "bg"), (50176, 384, 1536, "br"), (50176, 1152, 384, "b"),
           (12544, 768, 3072, "br"), (12544, 3072, 768, "bg"), (65280, 2304, 768, "b"), (32768, 768, 3072, "br")]
-VARIANTS = [("tuned", {}), ("p8_256", {"MMR_GEMM_W4": "0", "MMR_GEMM_BIG": "7"}),
-            ("p8_192", {"MMR_GEMM_W4": "0", "MMR_GEMM_BIG": "8"})]
+VARIANTS = [("tuned", -1), ("p8_256", 9), ("p8_192", 10)]  # mmr_pin_variant indices
 
 
 def timeit(fn, it=10):
@@ -50,25 +49,19 @@ def main():
             ref = ref + r.float()
         res = {}
         for _ in range(args.rounds):
-            for name, env in VARIANTS:
-                for k in ("MMR_GEMM_W4", "MMR_GEMM_BIG"):
-                    os.environ.pop(k, None)
-                os.environ.update(env)
+            for name, v in VARIANTS:
                 if name != "tuned" and (N % (256 if name == "p8_256" else 192) or K % 128):
                     continue
-                us = timeit(lambda: ops.linear(x, w, b, r, act=act))
+                with ops.pinned(ops.PIN_GEMM_BF16, v):
+                    us = timeit(lambda: ops.linear(x, w, b, r, act=act))
                 res.setdefault(name, []).append(us)
             res.setdefault("blas", []).append(timeit(lambda: F.linear(x, w)))
-        for k in ("MMR_GEMM_W4", "MMR_GEMM_BIG"):
-            os.environ.pop(k, None)
         errs = {}
-        for name, env in VARIANTS:
+        for name, v in VARIANTS:
             if name not in res:
                 continue
-            os.environ.update(env)
-            y = ops.linear(x, w, b, r, act=act).float()
-            for k in ("MMR_GEMM_W4", "MMR_GEMM_BIG"):
-                os.environ.pop(k, None)
+            with ops.pinned(ops.PIN_GEMM_BF16, v):
+                y = ops.linear(x, w, b, r, act=act).float()
             errs[name] = ((y - ref).abs() / (ref.abs() + 1.0)).max().item()
         fl = 2.0 * M * N * K
         line = f"{M:6d} {N:5d} {K:5d} {epi:3s}"

@@ -37,12 +37,11 @@ if act == 1:
     ref = F.gelu(ref)
 if res:
     ref = ref + r.float()
-for w4, big in (("1", "1"), ("2", "1"), ("0", "1"), ("0", "2"), ("0", "3"), ("0", "4"), ("0", "5"), ("0", "6"),
-                ("0", "0")):
-    os.environ["MMR_GEMM_W4"], os.environ["MMR_GEMM_BIG"] = w4, big
-    t = timeit(lambda: ops.linear(x, w, b, r, act=act))
-    err = (ops.linear(x, w, b, r, act=act).float() - ref).abs().max().item()
-    out.append(f"  w4={w4} big={big}: {t:8.1f} us  {fl / t / 1e6:7.0f} TF/s  max|err| {err:.3g}")
+for v in range(ops._L().mmr_linear_bf16_n_variants()):
+    with ops.pinned(ops.PIN_GEMM_BF16, v):
+        t = timeit(lambda: ops.linear(x, w, b, r, act=act))
+        err = (ops.linear(x, w, b, r, act=act).float() - ref).abs().max().item()
+    out.append(f"  variant {v:2d}: {t:8.1f} us  {fl / t / 1e6:7.0f} TF/s  max|err| {err:.3g}")
 t = timeit(lambda: F.linear(x, w, b.to(torch.bfloat16)))
 out.append(f"  hipBLASLt plain: {t:8.1f} us  {fl / t / 1e6:7.0f} TF/s")
 print("\n".join(out), flush=True)

@@ -25,20 +25,20 @@ for s in $STEPS; do
       timeout -k 10 800 python -u bench.py --preset cfg5 --steps 5 --warmup 2 > $OUT/bench_cfg5.json 2> $OUT/bench_cfg5.err
       echo presets ok ;;
     prof)
-      MMR_TOWER_STREAMS=0 MMR_FUSION_STREAMS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o full \
-        -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof_full.log 2>&1
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o full \
+        -- python3 bench.py --sequential-towers --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof_full.log 2>&1
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o knn \
-        -- python3 bench.py --mode knn --steps 20 --warmup 3 --no-cpu-baseline > $OUT/prof_knn.log 2>&1
+        -- python3 bench.py --sequential-towers --mode knn --steps 20 --warmup 3 --no-cpu-baseline > $OUT/prof_knn.log 2>&1
       echo prof ok ;;
     prof5)  # cfg5 kernel stats, towers / fusion in sequence
-      MMR_TOWER_STREAMS=0 MMR_FUSION_STREAMS=0 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o cfg5 \
-        -- python3 bench.py --preset cfg5 --steps 3 --warmup 2 --no-cpu-baseline > $OUT/prof_cfg5.log 2>&1
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o cfg5 \
+        -- python3 bench.py --sequential-towers --preset cfg5 --steps 3 --warmup 2 --no-cpu-baseline > $OUT/prof_cfg5.log 2>&1
       echo prof5 ok ;;
     pmck)
       timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc -o kfetch \
-        -- python3 bench.py --mode knn --steps 5 --warmup 1 --no-cpu-baseline > $OUT/pmc_kfetch.log 2>&1
+        -- python3 bench.py --sequential-towers --mode knn --steps 5 --warmup 1 --no-cpu-baseline > $OUT/pmc_kfetch.log 2>&1
       timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc -o kwrite \
-        -- python3 bench.py --mode knn --steps 5 --warmup 1 --no-cpu-baseline > $OUT/pmc_kwrite.log 2>&1
+        -- python3 bench.py --sequential-towers --mode knn --steps 5 --warmup 1 --no-cpu-baseline > $OUT/pmc_kwrite.log 2>&1
       echo pmc ok ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

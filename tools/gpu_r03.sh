@@ -28,14 +28,10 @@ for s in $STEPS; do
       timeout -k 10 500 python -u bench.py --preset cfg5 --steps 5 --warmup 2 > $OUT/bench_cfg5.json 2> $OUT/bench_cfg5.err
       echo presets ok ;;
     prof)
-      MMR_TOWER_STREAMS=0 MMR_FUSION_STREAMS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o full \
-        -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof_full.log 2>&1
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o full \
+        -- python3 bench.py --sequential-towers --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof_full.log 2>&1
       f=$(find $OUT/prof -name "*kernel_stats.csv" | head -1); python tools/prof_csv_summary.py "$f" > $OUT/prof_summary.txt 2>&1 || cp "$f" $OUT/prof_summary.txt
       head -45 $OUT/prof_summary.txt ;;
-    epi)
-      timeout -k 10 300 python -u tools/gemm_ab.py --env MMR_P8_EPI --values 0,1 > $OUT/gemm_epi.txt 2>&1; cat $OUT/gemm_epi.txt ;;
-    mlp)
-      timeout -k 10 300 python -u tools/mlp_ab.py ${MLP_CFGS:-0,1,2} > $OUT/mlp_ab.txt 2>&1; cat $OUT/mlp_ab.txt ;;
     abr02)  # same-box A/B of the cfg2 step: this tree's libmmr vs tools/ab/${ABLIB:-libmmr_r02.so} (round 2's)
       for i in 1 2; do
         for lib in new old; do
@@ -46,8 +42,8 @@ for s in $STEPS; do
       done
       unset MMR_LIBMMR ;;
     prof5)
-      MMR_TOWER_STREAMS=0 MMR_FUSION_STREAMS=0 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof5 -o cfg5 \
-        -- python3 bench.py --preset cfg5 --steps 4 --warmup 2 --no-cpu-baseline > $OUT/prof5.log 2>&1
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof5 -o cfg5 \
+        -- python3 bench.py --sequential-towers --preset cfg5 --steps 4 --warmup 2 --no-cpu-baseline > $OUT/prof5.log 2>&1
       f=$(find $OUT/prof5 -name "*kernel_stats.csv" | head -1); python tools/prof_csv_summary.py "$f" > $OUT/prof5_summary.txt 2>&1 || cp "$f" $OUT/prof5_summary.txt
       head -45 $OUT/prof5_summary.txt ;;
     mxab)  # same-box A/B of the MX-fp8 / bf16 GEMMs: this tree's libmmr vs tools/ab/${ABLIB:-libmmr_head.so}
@@ -76,7 +72,7 @@ for s in $STEPS; do
     knnprof)  # kNN search (bench --mode knn) kernel stats: this tree vs tools/ab/${ABLIB:-libmmr_nostore.so}
       for lib in new old; do
         if [ $lib = old ]; then export MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/${ABLIB:-libmmr_nostore.so}; else unset MMR_LIBMMR; fi
-        timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/knn_$lib -o k -- python3 bench.py --mode knn --no-cpu-baseline > $OUT/knn_$lib.log 2>&1 || true
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/knn_$lib -o k -- python3 bench.py --sequential-towers --mode knn --no-cpu-baseline > $OUT/knn_$lib.log 2>&1 || true
         f=$(find $OUT/knn_$lib -name "*kernel_stats.csv" | head -1); echo "== $lib"; python tools/prof_csv_summary.py "$f" | head -8
       done; unset MMR_LIBMMR ;;
     libab)  # same-box A/B of the tuned bf16 GEMM on the cfg2 shapes: this tree vs tools/ab/${ABLIB:-libmmr_nostore.so}
@@ -89,19 +85,14 @@ for s in $STEPS; do
         timeout -k 10 120 python -u tools/swa_bench.py new >> $OUT/swa.txt 2>&1
         MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/${ABLIB:-libmmr_head.so} timeout -k 10 120 python -u tools/swa_bench.py old >> $OUT/swa.txt 2>&1
       done; grep -v amdgpu.ids $OUT/swa.txt ;;
-    envab)  # cfg2 step with env setting A / B (ENVA / ENVB, e.g. "MMR_P8_NT=1"), same box
-      for i in 1 2; do for e in "${ENVA:-X=0}" "${ENVB:-X=1}"; do
-        env $e timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 30 ${BENCHARGS:-} > $OUT/envab.json 2> $OUT/envab.err
-        python -c "import json;d=json.load(open('$OUT/envab.json'));print('$e', round(d['ms_per_step'],3), round(d['value']), {k:round(v['ms_per_launch']*1e3,1) for k,v in d['roofline']['bert_gemms'].items()})"
-      done; done ;;
     mlpab)  # fused Swin MLP: this tree vs tools/ab/${ABLIB}
       for i in 1 2; do
         timeout -k 10 120 python -u tools/mlp_bench.py >> $OUT/mlpab_new.txt 2>&1
         MMR_LIBMMR=$GRAFT_REPO_ROOT/tools/ab/${ABLIB} timeout -k 10 120 python -u tools/mlp_bench.py >> $OUT/mlpab_old.txt 2>&1
       done; echo new; grep -v amdgpu.ids $OUT/mlpab_new.txt; echo $ABLIB; grep -v amdgpu.ids $OUT/mlpab_old.txt ;;
     trace)  # kernel trace of sequential cfg2 steps; launch list of step 4 (TRACEFLT filters names)
-      MMR_TOWER_STREAMS=0 MMR_FUSION_STREAMS=0 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace -o tr \
-        -- python3 bench.py --steps 6 --warmup 2 --no-cpu-baseline > $OUT/trace.log 2>&1
+      timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace -o tr \
+        -- python3 bench.py --sequential-towers --steps 6 --warmup 2 --no-cpu-baseline > $OUT/trace.log 2>&1
       f=$(find $OUT/trace -name "*kernel_trace.csv" | head -1); python tools/step_list.py "$f" 4 "${TRACEFLT:-}" > $OUT/step_list.txt; cat $OUT/step_list.txt | tail -${TRACEN:-60} ;;
     attab)  # attention cores (tools/mha_bench.py + tools/attn_ab.py): this tree vs tools/ab/${ABLIB:-libmmr_prev.so}
       for i in 1 2; do
@@ -133,9 +124,7 @@ for s in $STEPS; do
     rw)
       timeout -k 10 200 python -u tools/rw_bench.py > $OUT/rw.txt 2>&1; grep -v amdgpu.ids $OUT/rw.txt ;;
     breakdown)  # per-(op, shape) times of one sequential cfg2 step
-      MMR_TOWER_STREAMS=0 MMR_FUSION_STREAMS=0 timeout -k 10 300 python -u tools/step_breakdown.py ${BDARGS:-} > $OUT/breakdown.txt 2>&1; grep -v amdgpu.ids $OUT/breakdown.txt | head -70 ;;
-    nck)
-      timeout -k 10 300 python -u tools/gemm_nck.py > $OUT/gemm_nck.txt 2>&1; cat $OUT/gemm_nck.txt ;;
+      timeout -k 10 300 python -u tools/step_breakdown.py ${BDARGS:-} > $OUT/breakdown.txt 2>&1; grep -v amdgpu.ids $OUT/breakdown.txt | head -70 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

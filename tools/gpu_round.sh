@@ -23,28 +23,28 @@ for s in $STEPS; do
       timeout -k 10 300 python -u bench.py --mode knn > "$OUT/bench_knn.json" 2> "$OUT/bench_knn.err"
       cat "$OUT/bench_knn.json" ;;
     prof)
-      MMR_TOWER_STREAMS=0 MMR_FUSION_STREAMS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o full \
-        -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/prof_full.log" 2>&1
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o full \
+        -- python bench.py --sequential-towers --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/prof_full.log" 2>&1
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o knn \
-        -- python bench.py --mode knn --steps 20 --warmup 3 --no-cpu-baseline > "$OUT/prof_knn.log" 2>&1
+        -- python bench.py --sequential-towers --mode knn --steps 20 --warmup 3 --no-cpu-baseline > "$OUT/prof_knn.log" 2>&1
       ls -R "$OUT/prof" | head -20 ;;
     pmc)
       # HBM traffic: FETCH_SIZE and WRITE_SIZE in separate passes (TCC slot budget)
       timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o fetch \
-        -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_fetch.log" 2>&1
+        -- python bench.py --sequential-towers --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_fetch.log" 2>&1
       timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc" -o write \
-        -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_write.log" 2>&1
+        -- python bench.py --sequential-towers --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_write.log" 2>&1
       timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o kfetch \
-        -- python bench.py --mode knn --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/pmc_kfetch.log" 2>&1
+        -- python bench.py --sequential-towers --mode knn --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/pmc_kfetch.log" 2>&1
       timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc" -o kwrite \
-        -- python bench.py --mode knn --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/pmc_kwrite.log" 2>&1
+        -- python bench.py --sequential-towers --mode knn --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/pmc_kwrite.log" 2>&1
       ls -R "$OUT/pmc" | head -20 ;;
     pmck)
       # kNN-mode HBM traffic only (default scan mode), FETCH_SIZE and WRITE_SIZE in separate passes
       timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o kfetch \
-        -- python bench.py --mode knn --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/pmc_kfetch.log" 2>&1
+        -- python bench.py --sequential-towers --mode knn --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/pmc_kfetch.log" 2>&1
       timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc" -o kwrite \
-        -- python bench.py --mode knn --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/pmc_kwrite.log" 2>&1
+        -- python bench.py --sequential-towers --mode knn --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/pmc_kwrite.log" 2>&1
       ls -R "$OUT/pmc" | head -20 ;;
     pmcg)
       # FFN1 GEMM traffic per candidate launch variant (the tuner's pick varies by box)

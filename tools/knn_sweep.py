@@ -1,7 +1,6 @@
 """In-process kNN search timing sweep (one process, interleaved variants, HIP events on the launch
 stream).  usage: python tools/knn_sweep.py [--n 100000] [--d 768] [--k 10] [--qs 1,16,64,128,256,1024]
-Variants: f16 (tile scan for 33-256-query passes), f16 with MMR_KNN_F16_TILE=0 (one-wave stream
-scan), x3.  Prints one JSON line per (variant, Q) with the median us per search and the fraction of
+Variants: f16 (the fp16 scan the index dispatches for each Q), x3.  Prints one JSON line per (variant, Q) with the median us per search and the fraction of
 the search's HBM / MFMA bound; checks that every variant returns the same lists."""
 import argparse
 import json
@@ -26,7 +25,7 @@ def main():
     p.add_argument("--qs", default="1,16,64,128,256,1024")
     p.add_argument("--reps", type=int, default=30)
     p.add_argument("--rounds", type=int, default=3)
-    p.add_argument("--variants", default="f16,f16_stream,x3")
+    p.add_argument("--variants", default="f16,x3")
     a = p.parse_args()
     G = synthetic.gauss_gallery(a.n, a.d, synthetic.SEED)
     ix = GalleryIndex(G, mode="f16")
@@ -40,8 +39,6 @@ def main():
         for _ in range(a.rounds):
             for v in times:
                 ix.set_mode("x3" if v.startswith("x3") else "f16")
-                os.environ["MMR_KNN_F16_TILE"] = "0" if v == "f16_stream" else "1"
-                os.environ["MMR_KNN_F16_CFG"] = v[5:6] if v.startswith("f16_c") else "0"
                 for _ in range(3):
                     i, s, stt = ix.search(Q, a.k, want_status=True)
                 torch.cuda.synchronize()

@@ -2,7 +2,7 @@
 with HIP events on the current stream and prints, per (op, shape), calls / total ms / TF/s for the
 GEMMs.  Diagnostic only.
 usage: python tools/step_breakdown.py [--model-type multimodal|text] [--batch B] [--dim D] [--tower-dtype bf16|fp8]
-(MMR_TOWER_STREAMS=0 MMR_FUSION_STREAMS=0 for a sequential step: per-op events are exact only then)"""
+(the towers and fusion layers run on one stream here: per-op events are exact only then)"""
 import argparse
 import collections
 import os
@@ -25,6 +25,7 @@ mt = args.model_type
 torch.cuda.set_device(0)
 dev = torch.device("cuda:0")
 model = build_bench_model(device=dev, joint_dim=args.dim, model_type=mt, tower_dtype=args.tower_dtype)
+model.concurrent_towers = model.fusion.side_streams = False
 B = args.batch
 imgs = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(B, synthetic.SEED))).to(dev)
 ids_np, mask_np = synthetic.reports(B, 128, synthetic.SEED + 100)
