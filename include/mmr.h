@@ -165,6 +165,34 @@ mmr_status mmr_linear_bf16(const uint16_t* x, const uint16_t* w, const float* bi
  * Diagnostic: lets a benchmark name the kernel it measured. */
 int32_t mmr_linear_bf16_variant(int64_t m, int32_t n, int32_t k, int32_t act, int32_t has_bias,
                                 int32_t has_residual);
+/* The BERT linears with the residual LayerNorm folded in, so no LayerNorm pass runs between the
+ * GEMMs of a layer (HF BertLayer: LN(dense(x) + residual), reference fusion.py:322-325 via BertModel).
+ * Persistent 8-phase bf16 GEMM, 256-row tiles: m % 256 == 0, k % 128 == 0, n % 192 == 0 or n % 256 == 0.
+ *   stats_out (optional, act == 0): per row, mmr_linear_bf16_ln_parts(m, n, ln_mode) f32 pairs
+ *     (sum, sum of squares) of the bf16 outputs as stored — [m][parts][2], summed they give the row's
+ *     LayerNorm statistics (deterministic: one pair per tile column and wave column, no atomics).
+ *   ln_mode 0: y = act(x W^T + bias) (+ residual).
+ *   ln_mode 1: x is a raw residual-stream row y_in produced with stats, ln_coef = its mmr_ln_row_coef
+ *     (f32 [m][2]); w = W diag(gamma) (bf16), ln_v1 = c = row sums of w (f32 [n]),
+ *     bias = W beta + b:  y = act(LN(y_in) W^T + b) = act(rstd (y_in w^T) - rstd mean c + bias).
+ *   ln_mode 2: residual is a raw row r produced with stats, ln_coef its coefficients; ln_v1 / ln_v2 =
+ *     gamma / beta (f32 [n]):
+ *     y = x W^T + bias + LN(r)  (n % 192 == 0).
+ * Built: mode 1 with or without GELU (no residual, no stats); mode 2 with or without stats; mode 0
+ * with stats, with or without a residual.  bias is required.  MMR_ERR_UNSUPPORTED otherwise. */
+mmr_status mmr_linear_bf16_ln(const uint16_t* x, const uint16_t* w, const float* bias,
+                              const uint16_t* residual, uint16_t* y, int64_t m, int32_t n, int32_t k,
+                              int32_t act, int32_t ln_mode, const float* ln_coef, const float* ln_v1,
+                              const float* ln_v2, float* stats_out, void* stream);
+
+/* The row statistics of a producer (stats [m][nparts][2], nparts even) -> LayerNorm coefficients
+ * coef [m][2] = (rstd, -mean rstd) over a row width n, rstd = 1 / sqrt(var + eps). */
+mmr_status mmr_ln_row_coef(const float* stats, int64_t m, int32_t nparts, int32_t n, float eps, float* coef,
+                           void* stream);
+
+/* Row-statistics pairs per row mmr_linear_bf16_ln writes for an m x n output in ln_mode (0: not built). */
+int32_t mmr_linear_bf16_ln_parts(int64_t m, int32_t n, int32_t ln_mode);
+
 /* Number of launch variants mmr_linear_bf16 chooses among (indices 0 .. n-1 of its table). */
 int32_t mmr_linear_bf16_n_variants(void);
 

@@ -40,6 +40,10 @@ SIGNATURES = {
     "mmr_linear_bf16": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp],
     "mmr_linear_bf16_variant": [c_i64, c_i32, c_i32, c_i32, c_i32, c_i32],
     "mmr_linear_bf16_n_variants": [],
+    "mmr_linear_bf16_ln_parts": [c_i64, c_i32, c_i32],
+    "mmr_linear_bf16_ln": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp,
+                           c_vp],
+    "mmr_ln_row_coef": [c_vp, c_i64, c_i32, c_i32, c_f32, c_vp, c_vp],
     "mmr_pin_variant": [c_i32, c_i32],
     "mmr_linear_rw_parts": [c_i32, c_i32],
     "mmr_linear_rw_pack": [c_vp, c_i32, c_i32, c_vp, c_vp],
@@ -102,6 +106,7 @@ SIGNATURES = {
 }
 _RESTYPES = {"mmr_last_error": ctypes.c_char_p, "mmr_version": ctypes.c_int, "mmr_max_k": ctypes.c_int,
              "mmr_linear_bf16_variant": ctypes.c_int32, "mmr_linear_bf16_n_variants": ctypes.c_int32,
+             "mmr_linear_bf16_ln_parts": ctypes.c_int32,
              "mmr_linear_rw_parts": ctypes.c_int32,
              "mmr_swin_mlp_pack_elems": ctypes.c_int64, "mmr_swin_attn_block_pack_bytes": ctypes.c_int64}
 

@@ -512,9 +512,10 @@ __device__ __forceinline__ void st16(void* p, uint4 v, bool nt) {
 // O / FFN2 outputs measured equal
 inline int p8_nt(int64_t m, int64_t n, int64_t esz) { return m * n * esz > (int64_t)128 << 20 ? 1 : 0; }
 
-template <int NT, bool FP8 = false, int KNN = 0>
+template <int NT, bool FP8 = false, int KNN = 0, int NV = 1>
 struct P8 {
   static constexpr int TBN = 64 * NT;
+  // NV: per-column f32 vectors staged per tile (bias; + the LayerNorm-fold vectors, see LNM)
   static constexpr int SC = FP8 ? 1024 : 0;            // uint16 elements of per-K-tile scales (2 KB)
   static constexpr int RM = NT == 3 ? 2 : 1;           // m-tiles per epilogue round
   static constexpr int ELD = 16 * NT + 8;              // bf16 row stride of the epilogue area
@@ -534,7 +535,8 @@ struct P8 {
 #else
   static constexpr size_t STAMP_B = 0;
 #endif
-  static constexpr size_t LDS_B = 2 * BUF_B + EPI_B + 2 * TBN * 4 + STAMP_B;
+  static constexpr size_t COEF_B = NV > 1 ? 2 * 256 * 2 * 4 : 0;  // LNM: [2][256 rows][rstd, -mean rstd]
+  static constexpr size_t LDS_B = 2 * BUF_B + EPI_B + 2 * NV * TBN * 4 + COEF_B + STAMP_B;
 };
 
 #ifdef MMR_P8_STAMPS
@@ -564,7 +566,19 @@ __device__ unsigned long long p8_stamps[1024 * 8 * 8 * 4];
 // (KNN = 2: knn_select_t<3>'s 2-row units, one 8-B store) or of all four (KNN = 4: knn_select_t<2>'s
 // 4-row units) — GM[q][unit] (ldG) — and each wave column's 64-row block max BM[q][block] (ldB),
 // rows >= nval as -inf, instead of the tile.
-template <int NT, int ACT, bool HAS_BIAS, bool HAS_RES, bool FP8 = false, bool OUT8 = false, int KNN = 0>
+// LNM / STO (bf16, 256-row tiles): the BERT residual + LayerNorm folded into the GEMMs around it, so
+// no LayerNorm pass runs between them (mmr_linear_bf16_ln).  A producer (STO) writes, besides its
+// bf16 output y, one (sum y, sum y^2) f32 pair per row, tile column and wave column — SP[row][4 n-tile
+// + wc], over the bf16-ROUNDED outputs (deterministic, no atomics).  A consumer reads the LP pairs of
+// input rows, reduced by mmr_ln_row_coef to LC[row] = (rstd, -mean rstd) — staged per tile into LDS
+// by LDS-DMA beside the bias (a global load in the epilogue would retire behind the next tile's
+// prefetch and expose it) — and either
+//   LNM = 1: takes the raw y as X and applies LN(y) W^T + b = rstd (y W'^T) - rstd mean c + d in the
+//            epilogue (W' = W diag(gamma) pre-folded, LV1 = c = row sums of W', bias = d = W beta + b);
+//   LNM = 2: takes the raw y as the residual R and adds LN(y) = gamma (rstd y - rstd mean) + beta
+//            (LV1 = gamma, LV2 = beta over the output columns).
+template <int NT, int ACT, bool HAS_BIAS, bool HAS_RES, bool FP8 = false, bool OUT8 = false, int KNN = 0,
+          int LNM = 0, bool STO = false>
 __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restrict__ X,
                                                        const uint16_t* __restrict__ W,
                                                        const float* __restrict__ bias,
@@ -576,12 +590,20 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
                                                        uint8_t* __restrict__ YS = nullptr,
                                                        float* __restrict__ GM = nullptr, float* __restrict__ BM = nullptr,
                                                        int64_t ldG = 0, int64_t ldB = 0, int64_t nval = 0,
-                                                       int ntst = 0, const float* __restrict__ RS = nullptr) {
+                                                       int ntst = 0, const float* __restrict__ RS = nullptr,
+                                                       const float* __restrict__ LC = nullptr,
+                                                       const float* __restrict__ LV1 = nullptr,
+                                                       const float* __restrict__ LV2 = nullptr,
+                                                       float* __restrict__ SP = nullptr) {
   static_assert(!OUT8 || (FP8 && NT == 4 && !HAS_RES), "OUT8: MX-fp8 256x256 tiles without residual");
+  static_assert((LNM == 0 && !STO) || (!FP8 && !KNN), "LayerNorm fold: bf16 GEMMs");
+  static_assert(LNM != 2 || HAS_RES, "LNM = 2 normalises the residual");
+  static_assert(!STO || ACT == 0, "row statistics: LDS-staged (non-GELU) epilogue");
   static_assert(KNN == 0 || ((KNN == 2 || KNN == 4) && NT == 4 && !FP8 && !HAS_BIAS && !HAS_RES && ACT == 0),
                 "KNN (rows per unit 2 / 4): plain 256x256 fp16 tiles");
 #if defined(__HIP_DEVICE_COMPILE__)  // buffer-descriptor builtins exist in the device pass only
-  using C = P8<NT, FP8, KNN>;
+  constexpr int NV = LNM == 2 ? 3 : (LNM == 1 ? 2 : 1);
+  using C = P8<NT, FP8, KNN, NV>;
   constexpr int KB = 64, TBN = C::TBN;                  // KB: 128-byte LDS rows (64 bf16 / 128 fp8)
   constexpr int TA = 256 * KB, TB = TBN * KB, BUF = TA + TB + C::SC;  // uint16 elements per K-tile buffer
   // LDS image: [A_E | A_O | B_E | B_O | S_E | S_O] — the two buffers of an operand 32 KB apart, so one
@@ -608,8 +630,9 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   constexpr bool skip_st = false;
   constexpr bool skip_gm = false;
 #endif
+  // STO: 8 more (one row-statistics store per m-tile, lanes fq = 0 — the instruction always issues)
   constexpr int nstore = skip_st ? 0
-                                 : (skip_gm ? 8 : (epi_pl ? C::NSTORE_PL : C::NSTORE_LDS));
+                                 : (skip_gm ? 8 : (epi_pl ? C::NSTORE_PL : C::NSTORE_LDS) + (STO ? 8 : 0));
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
 
   const int ntiles = tiles_m * tiles_n;
@@ -631,13 +654,27 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   const int wr = wave >> 2, wc = wave & 3;  // m-group (stagger group), n position
   const int fr = lane & 15, fq = lane >> 4;
   uint16_t* et = dsm + 2 * BUF + wave * 16 * C::RM * C::ELD;         // this wave's epilogue area
-  float* lbias = (float*)(dsm + 2 * BUF + 8 * 16 * C::RM * C::ELD);  // [2][TBN] f32, by tile parity
-  // bias of a tile -> LDS by one LDS-DMA from wave 0: the first tile's in the prologue, each next
-  // tile's at the end of wave 0's epilogue (the other parity; no registers live across the loop)
+  float* lbias = (float*)(dsm + 2 * BUF + 8 * 16 * C::RM * C::ELD);  // [2][NV][TBN] f32, by tile parity
+  // bias (and LNM vectors) of a tile -> LDS by LDS-DMA from wave 0: the first tile's in the prologue,
+  // each next tile's at the end of wave 0's epilogue (the other parity; no registers live across the loop)
+  float* lcoef = lbias + 2 * NV * TBN;  // LNM: [2][256][2] f32 row coefficients, by tile parity
   auto bias_dma = [&](int tile, int par) {
-    if (HAS_BIAS && wave == 0 && lane < TBN / 4)
-      __builtin_amdgcn_global_load_lds((const void*)(bias + nof(tile) * TBN + lane * 4),
-                                       (lds_ptr_t)(lbias + par * TBN), 16, 0, 0);
+    if (LNM != 0 && wave == 0) {  // the tile's 256 row-coefficient pairs: 2 x 1 KB
+      const float* src = LC + (int64_t)mof(tile) * 512 + lane * 4;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(lcoef + par * 512), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(src + 256), (lds_ptr_t)(lcoef + par * 512 + 256), 16, 0, 0);
+    }
+    if (wave == 0 && lane < TBN / 4) {
+      if (HAS_BIAS)
+        __builtin_amdgcn_global_load_lds((const void*)(bias + nof(tile) * TBN + lane * 4),
+                                         (lds_ptr_t)(lbias + par * NV * TBN), 16, 0, 0);
+      if (LNM != 0)
+        __builtin_amdgcn_global_load_lds((const void*)(LV1 + nof(tile) * TBN + lane * 4),
+                                         (lds_ptr_t)(lbias + (par * NV + 1) * TBN), 16, 0, 0);
+      if (LNM == 2)
+        __builtin_amdgcn_global_load_lds((const void*)(LV2 + nof(tile) * TBN + lane * 4),
+                                         (lds_ptr_t)(lbias + (par * NV + 2) * TBN), 16, 0, 0);
+    }
   };
 
   // glds: piece j of an operand stages LDS rows 64j + 8 wave + lane/8, physical chunk lane%8 <-
@@ -967,7 +1004,18 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
     f32x4 bq[NT];
 #pragma unroll
     for (int j = 0; j < NT; ++j)
-      bq[j] = HAS_BIAS ? *(const f32x4*)(lbias + par * TBN + wc * 16 * NT + j * 16 + efq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      bq[j] = HAS_BIAS ? *(const f32x4*)(lbias + par * NV * TBN + wc * 16 * NT + j * 16 + efq * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    // LNM: the column vectors of this lane's columns and the row coefficients of its 8 rows (LDS)
+    auto lvec = [&](int v, int j) { return *(const f32x4*)(lbias + (par * NV + v) * TBN + wc * 16 * NT + j * 16 + efq * 4); };
+    float ra[LNM ? 8 : 1], rb[LNM ? 8 : 1];  // LN(y) = ra y + rb per row (rstd, -mean rstd)
+    if constexpr (LNM != 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float2 cf = *(const float2*)(lcoef + par * 512 + (wr * 128 + i * 16 + efr) * 2);
+        ra[i] = cf.x;
+        rb[i] = cf.y;
+      }
+    }
     uint2 rq[HAS_RES ? 8 : 1][HAS_RES ? NT : 1];
     if constexpr (HAS_RES) {
 #pragma unroll
@@ -975,6 +1023,11 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
 #pragma unroll
         for (int j = 0; j < NT; ++j)
           rq[i][j] = *(const uint2*)(R + (m0 + wr * 128 + i * 16 + efr) * N + n0 + wc * 16 * NT + j * 16 + efq * 4);
+    }
+    f32x4 cqr[LNM == 1 && epi_pl ? NT : 1];  // the fold vector of the lane's columns, held for the GELU epilogue
+    if constexpr (LNM == 1 && epi_pl) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j) cqr[j] = lvec(1, j);
     }
     if constexpr (epi_pl) {
       // C^T fragment -> 16-B row chunks in registers: for an n-tile pair (j, j + 1) one
@@ -996,7 +1049,12 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
             float v[4];
 #pragma unroll
             for (int rg = 0; rg < 4; rg += 2) {
-              mmr::f32x2_t u = {acc[i][jj][rg] + bq[jj][rg], acc[i][jj][rg + 1] + bq[jj][rg + 1]};
+              mmr::f32x2_t u;
+              if constexpr (LNM == 1)
+                u = (mmr::f32x2_t){fmaf(ra[i], acc[i][jj][rg], fmaf(rb[i], cqr[jj][rg], bq[jj][rg])),
+                                   fmaf(ra[i], acc[i][jj][rg + 1], fmaf(rb[i], cqr[jj][rg + 1], bq[jj][rg + 1]))};
+              else
+                u = (mmr::f32x2_t){acc[i][jj][rg] + bq[jj][rg], acc[i][jj][rg + 1] + bq[jj][rg + 1]};
               if (ACT == 1) u = mmr::gelu_fast2(u);
               v[rg] = u.x;
               v[rg + 1] = u.y;
@@ -1023,24 +1081,58 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
 #pragma unroll
       for (int ii = 0; ii < C::RM; ++ii) {
         const int i = rd * C::RM + ii;
+        float st1 = 0.f, st2 = 0.f;  // STO: this row's sum / sum of squares over the lane's columns
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
           float v[4];
+          f32x4 cq;
+          if constexpr (LNM == 1) cq = lvec(1, j);
 #pragma unroll
           for (int rg = 0; rg < 4; rg += 2) {
-            mmr::f32x2_t u = {acc[i][j][rg] + bq[j][rg], acc[i][j][rg + 1] + bq[j][rg + 1]};
+            mmr::f32x2_t u;
+            if constexpr (LNM == 1)
+              u = (mmr::f32x2_t){fmaf(ra[i], acc[i][j][rg], fmaf(rb[i], cq[rg], bq[j][rg])),
+                                 fmaf(ra[i], acc[i][j][rg + 1], fmaf(rb[i], cq[rg + 1], bq[j][rg + 1]))};
+            else
+              u = (mmr::f32x2_t){acc[i][j][rg] + bq[j][rg], acc[i][j][rg + 1] + bq[j][rg + 1]};
             if (ACT == 1) u = mmr::gelu_fast2(u);
             v[rg] = u.x;
             v[rg + 1] = u.y;
           }
           if constexpr (HAS_RES) {
             const uint2 rv = rq[i][j];
-            v[0] += __uint_as_float(rv.x << 16);
-            v[1] += __uint_as_float(rv.x & 0xFFFF0000u);
-            v[2] += __uint_as_float(rv.y << 16);
-            v[3] += __uint_as_float(rv.y & 0xFFFF0000u);
+            float r4[4] = {__uint_as_float(rv.x << 16), __uint_as_float(rv.x & 0xFFFF0000u),
+                           __uint_as_float(rv.y << 16), __uint_as_float(rv.y & 0xFFFF0000u)};
+            if constexpr (LNM == 2) {
+              const f32x4 g = lvec(1, j), be = lvec(2, j);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) r4[e] = fmaf(g[e], fmaf(ra[i], r4[e], rb[i]), be[e]);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += r4[e];
           }
-          ds_write_b64_untracked(et + (ii * 16 + efr) * C::ELD + j * 16 + efq * 4, mmr::pack2bf(v[0], v[1]), mmr::pack2bf(v[2], v[3]));
+          const uint32_t p0 = mmr::pack2bf(v[0], v[1]), p1 = mmr::pack2bf(v[2], v[3]);
+          if constexpr (STO) {
+            const float w0 = __uint_as_float(p0 << 16), w1 = __uint_as_float(p0 & 0xFFFF0000u);
+            const float w2 = __uint_as_float(p1 << 16), w3 = __uint_as_float(p1 & 0xFFFF0000u);
+            st1 += (w0 + w1) + (w2 + w3);
+            st2 = fmaf(w0, w0, fmaf(w1, w1, fmaf(w2, w2, fmaf(w3, w3, st2))));
+          }
+          ds_write_b64_untracked(et + (ii * 16 + efr) * C::ELD + j * 16 + efq * 4, p0, p1);
+        }
+        if constexpr (STO) {
+          // sum over the row's 4 lanes (fq): lane swaps on the VALU (no LDS round trip)
+          auto sum4 = [](float v) {
+            const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+            const float h = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+            const auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(h), __float_as_uint(h), false, false);
+            return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+          };
+          st1 = sum4(st1);
+          st2 = sum4(st2);
+          if (efq == 0)
+            *(float2*)(SP + ((m0 + wr * 128 + i * 16 + efr) * (int64_t)(4 * tiles_n) + nof(t) * 4 + wc) * 2) =
+                make_float2(st1, st2);
         }
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
@@ -1598,6 +1690,127 @@ extern "C" mmr_status mmr_linear_bf16(const uint16_t* x, const uint16_t* w, cons
   const int pin = mmr::pin_gemm_bf16.load(std::memory_order_relaxed);
   const int v = (pin >= 0 && pin < kVariants) ? pin : tuned_variant(m, n, k, act, hb, hr, x, residual, y, st, run);
   run(kVarW4[v], kVarCfg[v]);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+namespace {
+// the tile width of the LayerNorm-fused GEMMs: 256 x 192 or 256 x 256, whichever fills whole rounds of
+// the CUs (N = 768: 192 -> 512 tiles at M = 32768; 2304: 192; 3072: 256), ties to 256
+int ln_nt(int64_t m, int n) {
+  const bool ok3 = n % 192 == 0, ok4 = n % 256 == 0;
+  if (!ok3 || !ok4) return ok4 ? 4 : (ok3 ? 3 : 0);
+  const int64_t cus = std::max(8, cu_count() / 8 * 8), tm = m / 256;
+  auto eff = [&](int nt) {
+    const int64_t tiles = tm * (n / (64 * nt));
+    return (double)tiles / (double)(mmr::ceil_div(tiles, cus) * cus);
+  };
+  return eff(3) > eff(4) + 1e-9 ? 3 : 4;
+}
+
+template <int NT, int ACT, bool HR, int LNM, bool STO>
+void launch_ln(const uint16_t* x, const uint16_t* w, const float* b, const uint16_t* r, uint16_t* y, int64_t m,
+               int n, int k, const float* lc, const float* v1, const float* v2, float* sp, hipStream_t st) {
+  constexpr int NV = LNM == 2 ? 3 : (LNM == 1 ? 2 : 1);
+  const int grid = std::max(8, cu_count() / 8 * 8);
+  const int tm = (int)(m / 256), tn = n / (64 * NT);
+  gemm_bf16_tn_p8<NT, ACT, true, HR, false, false, 0, LNM, STO>
+      <<<dim3(std::max<int64_t>(8, std::min<int64_t>(grid, (int64_t)tm * tn) / 8 * 8)), dim3(512),
+         P8<NT, false, 0, NV>::LDS_B, st>>>(x, w, b, r, y, m, n, k, tm, tn, nullptr, nullptr, nullptr, nullptr,
+                                            nullptr, 0, 0, 0, p8_nt(m, n, 2), nullptr, lc, v1, v2, sp);
+}
+}  // namespace
+
+namespace {
+// row statistics pairs -> LayerNorm coefficients (rstd, -mean rstd): 8 lanes per row, 2 pairs each per
+// step (np % 2 == 0), reduced by three xor swaps
+__global__ __launch_bounds__(256) void ln_row_coef(const float* __restrict__ part, int64_t m, int np, float inv_n,
+                                                   float eps, float* __restrict__ coef) {
+  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 3;
+  const int sub = threadIdx.x & 7;
+  float s1 = 0.f, s2 = 0.f;
+  if (row < m) {
+    const float* p = part + row * np * 2;
+    for (int q = 2 * sub; q < np; q += 16) {
+      const float4 v = *(const float4*)(p + 2 * q);
+      s1 += v.x + v.z;
+      s2 += v.y + v.w;
+    }
+  }
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) {
+    s1 += __shfl_xor(s1, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
+  }
+  if (row < m && sub == 0) {
+    const float mean = s1 * inv_n;
+    const float rstd = rsqrtf(fmaxf(s2 * inv_n - mean * mean, 0.f) + eps);
+    *(float2*)(coef + 2 * row) = make_float2(rstd, -mean * rstd);
+  }
+}
+}  // namespace
+
+extern "C" mmr_status mmr_ln_row_coef(const float* stats, int64_t m, int32_t nparts, int32_t n, float eps, float* coef,
+                                      void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(stats && coef, "mmr_ln_row_coef: NULL pointer");
+  MMR_REQUIRE(m >= 0 && nparts > 0 && nparts % 2 == 0 && n > 0, "mmr_ln_row_coef: m=%lld nparts=%d n=%d", (long long)m,
+              nparts, n);
+  MMR_REQUIRE(((uintptr_t)stats & 15u) == 0 && ((uintptr_t)coef & 7u) == 0, "mmr_ln_row_coef: alignment");
+  if (m == 0) return MMR_OK;
+  ln_row_coef<<<dim3((unsigned)mmr::ceil_div(m * 8, 256)), dim3(256), 0, mmr::as_stream(stream)>>>(stats, m, nparts,
+                                                                                              1.0f / (float)n, eps, coef);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+extern "C" int32_t mmr_linear_bf16_ln_parts(int64_t m, int32_t n, int32_t ln_mode) {
+  const int nt = ln_mode == 2 ? (n % 192 == 0 ? 3 : 0) : ln_nt(m, n);
+  return nt ? 4 * (n / (64 * nt)) : 0;
+}
+
+extern "C" mmr_status mmr_linear_bf16_ln(const uint16_t* x, const uint16_t* w, const float* bias,
+                                         const uint16_t* residual, uint16_t* y, int64_t m, int32_t n, int32_t k,
+                                         int32_t act, int32_t ln_mode, const float* ln_coef, const float* ln_v1,
+                                         const float* ln_v2, float* stats_out, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && w && bias && y, "mmr_linear_bf16_ln: NULL pointer");
+  MMR_REQUIRE(m > 0 && m % 256 == 0 && k > 0 && k % 128 == 0,
+              "mmr_linear_bf16_ln: m=%lld (multiple of 256), k=%d (multiple of 128)", (long long)m, k);
+  const int nt = ln_nt(m, n);
+  MMR_REQUIRE(n > 0 && nt != 0, "mmr_linear_bf16_ln: n=%d (multiple of 192 or 256)", n);
+  MMR_REQUIRE(act == 0 || act == 1, "mmr_linear_bf16_ln: act=%d", act);
+  MMR_REQUIRE(ln_mode >= 0 && ln_mode <= 2, "mmr_linear_bf16_ln: ln_mode=%d", ln_mode);
+  MMR_REQUIRE(ln_mode == 0 || (ln_coef && ln_v1 && (ln_mode == 1 || ln_v2)),
+              "mmr_linear_bf16_ln: ln_mode=%d needs the row coefficients and its column vectors", ln_mode);
+  MMR_REQUIRE(ln_mode != 2 || residual, "mmr_linear_bf16_ln: ln_mode 2 normalises the residual");
+  MMR_REQUIRE(!stats_out || act == 0, "mmr_linear_bf16_ln: row statistics only without GELU");
+  hipStream_t st = mmr::as_stream(stream);
+  const bool hr = residual != nullptr, so = stats_out != nullptr;
+  // the combinations the BERT layer uses (towers.py): QKV / FFN1 (fold, + GELU for FFN1), O-proj /
+  // FFN2 (normalised or plain residual, row statistics out)
+#define LN_L(NT_, A_, HR_, M_, S_)                                                                              \
+  launch_ln<NT_, A_, HR_, M_, S_>(x, w, bias, residual, y, m, n, k, ln_coef, ln_v1, ln_v2, stats_out, st)
+#define LN_NT(A_, HR_, M_, S_) (nt == 3 ? LN_L(3, A_, HR_, M_, S_) : LN_L(4, A_, HR_, M_, S_))
+  if (ln_mode == 1 && !hr && !so) {
+    if (act) LN_NT(1, false, 1, false);
+    else LN_NT(0, false, 1, false);
+  } else if (ln_mode == 2 && act == 0) {
+    // 256 x 192 tiles only: the 256 x 256 form of the normalised residual exceeds 256 VGPRs (a spill
+    // in this kernel would also skew the K loop's counted vmcnt waits)
+    MMR_REQUIRE(n % 192 == 0, "mmr_linear_bf16_ln: ln_mode 2 needs n %% 192 == 0 (n=%d)", n);
+    if (so) LN_L(3, 0, true, 2, true);
+    else LN_L(3, 0, true, 2, false);
+  } else if (ln_mode == 0 && act == 0 && so) {
+    if (hr) LN_NT(0, true, 0, true);
+    else LN_NT(0, false, 0, true);
+  } else {
+    mmr::set_error("mmr_linear_bf16_ln: ln_mode=%d act=%d residual=%d stats_out=%d not built", ln_mode, act, (int)hr,
+                   (int)so);
+    return MMR_ERR_UNSUPPORTED;
+  }
+#undef LN_NT
+#undef LN_L
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }

@@ -73,6 +73,47 @@ class RWPack:
         self.img, self.n, self.k = img, n, k
 
 
+def linear_ln_parts(rows, n, ln_mode=0):
+    """Row-statistics pairs per row that mmr_linear_bf16_ln writes for an (rows x n) output (0: shape not
+    built)."""
+    return int(_L().mmr_linear_bf16_ln_parts(rows, n, ln_mode))
+
+
+def ln_row_coef(stats, n, eps):
+    """Row statistics [rows, parts, 2] of a linear_ln producer -> LayerNorm coefficients [rows, 2]
+    (rstd, -mean rstd) over a row width n (mmr_ln_row_coef)."""
+    rows, parts = stats.shape[0], stats.shape[1]
+    coef = torch.empty((rows, 2), dtype=torch.float32, device=stats.device)
+    _chk(_L().mmr_ln_row_coef(_lib.ptr(stats), rows, parts, n, float(eps), _lib.ptr(coef), _s(stats)),
+         "mmr_ln_row_coef")
+    return coef
+
+
+def linear_ln(x, w, bias, residual=None, act=0, ln_mode=0, coef=None, v1=None, v2=None, want_stats=False):
+    """mmr_linear_bf16_ln: the BERT linears with the residual LayerNorm folded in (no LayerNorm pass).
+    coef = ln_row_coef of the producer of x (ln_mode 1: x raw, w = W diag(gamma), v1 = row sums of w,
+    bias = W beta + b) or of the residual (ln_mode 2: residual raw, v1 / v2 = gamma / beta).
+    Returns (y, stats) — stats [rows, parts, 2] f32 (sum, sum of squares of the bf16 outputs) when
+    want_stats, else None."""
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, x.shape[-1])
+    M, K = x2.shape
+    N = w.shape[0]
+    assert x2.is_contiguous() and w.is_contiguous() and w.shape[1] == K
+    y = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    r = residual.reshape(M, N) if residual is not None else None
+    st = None
+    if want_stats:
+        np_ = linear_ln_parts(M, N, ln_mode)
+        if np_ == 0:
+            raise _lib.MMRError(f"mmr_linear_bf16_ln: no row statistics for {M} x {N}")
+        st = torch.empty((M, np_, 2), dtype=torch.float32, device=x.device)
+    _chk(_L().mmr_linear_bf16_ln(_lib.ptr(x2), _lib.ptr(w), _lib.ptr(bias), _lib.ptr(r), _lib.ptr(y), M, N, K, act,
+                                 ln_mode, _lib.ptr(coef), _lib.ptr(v1), _lib.ptr(v2), _lib.ptr(st), _s(x)),
+         "mmr_linear_bf16_ln")
+    return y.view(*lead, N), st
+
+
 def rw_pack(w):
     """bf16 W (N, K) -> RWPack, or None (K not in {64, 192, 384} or W too large for LDS parts)."""
     _lib.require_gpu(w)

@@ -234,6 +234,16 @@ class SwinTower:
         return ops.layernorm(x, self.norm_g, self.norm_b, 1e-5)
 
 
+def _ln_fold(w, b, gamma, beta):
+    """A linear that consumes LayerNorm(y) rewritten on the raw y (ops.linear_ln ln_mode 1):
+    LN(y) W^T + b = rstd (y W'^T) - rstd mean c + d with W' = bf16(W diag(gamma)), c = row sums of W'
+    (as stored), d = W beta + b.  w bf16 [N, K]; b, gamma, beta f32."""
+    wf = (w.double() * gamma.double()[None, :]).to(torch.bfloat16).contiguous()
+    c = wf.double().sum(1).float().contiguous()
+    d = (w.double() @ beta.double() + b.double()).float().contiguous()
+    return wf, c, d
+
+
 class BertTower:
     """HF BertModel(input_ids, attention_mask).last_hidden_state semantics (eval).  fp8: the four
     linears of every layer run as MX-fp8 GEMMs (config 5; B * L must be a multiple of 256)."""
@@ -266,10 +276,52 @@ class BertTower:
             for n in ("qkv", "o", "i", "f"):
                 ly[n + "_w8"] = _w8(ly[n + "_w"], plain=True) if fp8 else None
         self.hidden = self.word.shape[1]
+        # bf16 towers: every LayerNorm but the embedding's and the last is folded into the GEMMs around
+        # it (ops.linear_ln): FFN1 and the next layer's QKV read the raw residual stream with W' =
+        # W diag(gamma), c = row sums of W', d = W beta + b; O-proj / FFN2 normalise their raw residual
+        # in the epilogue and emit the row statistics the next consumer needs
+        self.ln_fold = not fp8 and self.hidden % 192 == 0
+        if self.ln_fold:
+            for i, ly in enumerate(self.layers):
+                ly["i_wf"], ly["i_c"], ly["i_d"] = _ln_fold(ly["i_w"], ly["i_b"], ly["ln1_g"], ly["ln1_b"])
+                if i > 0:
+                    prev = self.layers[i - 1]
+                    ly["qkv_wf"], ly["qkv_c"], ly["qkv_d"] = _ln_fold(ly["qkv_w"], ly["qkv_b"], prev["ln2_g"],
+                                                                      prev["ln2_b"])
         # optional dict name -> list of (start, end) torch.cuda.Event pairs around every launch of the
         # four GEMMs of a layer ("qkv", "o", "ffn1", "ffn2"): the bench's per-kernel roofline (events
         # ride torch's current stream = the launch stream)
         self.gemm_events = None
+
+    def _forward_folded(self, ids, mask, gemm_ln):
+        """The bf16 layer stack with the LayerNorms folded into the GEMMs (see __init__): per layer
+        QKV (fold LN2 of the previous layer) -> attention -> O-proj (+ LN2(previous raw output),
+        statistics) -> FFN1 (fold LN1, GELU) -> FFN2 (+ LN1(raw O-proj output), statistics); one
+        LayerNorm at the end materialises last_hidden_state.  Same maths as forward's unfused path:
+        HF BertLayer (reference fusion.py:322-325), the normalised rows just never round-trip HBM."""
+        heads = self.cfg["num_attention_heads"]
+        C, eps = self.hidden, 1e-12
+        h0 = ops.bert_embed(ids, self.word, self.pos, self.type0, self.eg, self.eb, eps)
+        y2 = cf2 = None
+        for i, ly in enumerate(self.layers):
+            if i == 0:
+                qkv, _ = gemm_ln("qkv", h0, ly["qkv_w"], ly["qkv_b"], plain=True)
+            else:
+                qkv, _ = gemm_ln("qkv", y2, ly["qkv_wf"], ly["qkv_d"], ln_mode=1, coef=cf2, v1=ly["qkv_c"])
+            ctx = ops.bert_attention(qkv, mask, heads, C // heads)
+            if i == 0:
+                y1, st1 = gemm_ln("o", ctx, ly["o_w"], ly["o_b"], residual=h0, want_stats=True)
+            else:
+                prev = self.layers[i - 1]
+                y1, st1 = gemm_ln("o", ctx, ly["o_w"], ly["o_b"], residual=y2, ln_mode=2, coef=cf2,
+                                  v1=prev["ln2_g"], v2=prev["ln2_b"], want_stats=True)
+            cf1 = ops.ln_row_coef(st1, C, eps)
+            f1, _ = gemm_ln("ffn1", y1, ly["i_wf"], ly["i_d"], act=1, ln_mode=1, coef=cf1, v1=ly["i_c"])
+            y2, st2 = gemm_ln("ffn2", f1, ly["f_w"], ly["f_b"], residual=y1, ln_mode=2, coef=cf1, v1=ly["ln1_g"],
+                              v2=ly["ln1_b"], want_stats=True)
+            cf2 = ops.ln_row_coef(st2, C, eps)
+        last = self.layers[-1]
+        return ops.layernorm(y2, last["ln2_g"], last["ln2_b"], eps)
 
     def forward(self, input_ids, attention_mask=None):
         """(B, L) ids/mask -> (B, L, C) bf16 last_hidden_state.  L is truncated to
@@ -290,10 +342,6 @@ class BertTower:
         # LayerNorm the first QKV's), FFN1 emits FFN2's
         fast8 = (self.fp8 and ev is None and C % 256 == 0 and C <= 1024 and rows % 256 == 0
                  and all(ly["qkv_w8"].kp == C and ly["i_w8"].layout == 2 for ly in self.layers))
-        if fast8:
-            h, h8 = ops.bert_embed_q8(ids, self.word, self.pos, self.type0, self.eg, self.eb, 1e-12)
-        else:
-            h, h8 = ops.bert_embed(ids, self.word, self.pos, self.type0, self.eg, self.eb, 1e-12), None
 
         def gemm(name, x, w, b, act=0, w8=None):
             if ev is None:
@@ -304,6 +352,24 @@ class BertTower:
             e1.record()
             ev.setdefault(name, []).append((e0, e1))
             return y
+
+        if self.ln_fold and rows % 256 == 0 and ops.linear_ln_parts(rows, C, 2) > 0:
+            def gemm_ln(name, x, w, b, plain=False, **kw):
+                if plain:
+                    return gemm(name, x, w, b), None
+                if ev is None:
+                    return ops.linear_ln(x, w, b, **kw)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                out = ops.linear_ln(x, w, b, **kw)
+                e1.record()
+                ev.setdefault(name, []).append((e0, e1))
+                return out
+            return self._forward_folded(ids, mask, gemm_ln)
+        if fast8:
+            h, h8 = ops.bert_embed_q8(ids, self.word, self.pos, self.type0, self.eg, self.eb, 1e-12)
+        else:
+            h, h8 = ops.bert_embed(ids, self.word, self.pos, self.type0, self.eg, self.eb, 1e-12), None
         lead = tuple(h.shape[:-1])
         for ly in self.layers:
             if fast8:

@@ -422,3 +422,92 @@ def test_checkpoint_path_reference_layout(tmp_path):
         _check_emb(o["txt_emb"], torch.from_numpy(f[f"{mt}_txt_emb"]))
     with pytest.raises(ValueError, match="checkpoint_path must be provided"):
         MultiModalRetrievalModel(joint_dim=64, device=DEV)
+
+
+def _ln_ref(y, g, b, eps):
+    """LayerNorm over the last dim in f64 (the folded GEMMs' reference)."""
+    y = y.double()
+    mu = y.mean(-1, keepdim=True)
+    var = ((y - mu) ** 2).mean(-1, keepdim=True)
+    return (y - mu) / torch.sqrt(var + eps) * g.double() + b.double()
+
+
+@pytest.mark.parametrize("M", [256, 4096])
+def test_linear_ln_modes(M):
+    """mmr_linear_bf16_ln, every built combination, vs f64 torch on the same bf16 operands:
+    (0) plain residual + row statistics: the pairs sum to (sum y, sum y^2) of the stored bf16 rows;
+    (1) LayerNorm folded into the consumer (QKV N=2304; FFN1 N=3072 + GELU): == LN(y) W^T + b;
+    (2) normalised residual + statistics (O-proj / FFN2): == ctx W^T + b + LN(r).
+    Raw rows carry a per-row mean and scale (the un-normalised BERT residual stream).  Tolerance
+    1e-2 * max|ref| (bf16 output rounding + bf16 W diag(gamma))."""
+    g = torch.Generator(device=DEV).manual_seed(M)
+    C, eps = 768, 1e-12
+    rnd = lambda *s: torch.randn(*s, generator=g, device=DEV)  # noqa: E731
+    # producer: y = ctx Wo^T + bo + h (plain residual), with statistics
+    ctx, h = bf(rnd(M, C)), bf(rnd(M, C) * 3 + rnd(M, 1) * 2)
+    wo, bo = bf(rnd(C, C) * C ** -0.5), rnd(C)
+    y, st = ops.linear_ln(ctx, wo, bo, residual=h, want_stats=True)
+    ref_y = ctx.double() @ wo.double().T + bo.double() + h.double()
+    assert rel_err(y, ref_y) < 1e-2
+    yd = y.double()
+    assert st.shape == (M, ops.linear_ln_parts(M, C, 0), 2)
+    s = st.double().sum(1)
+    assert torch.allclose(s[:, 0], yd.sum(1), rtol=1e-5, atol=1e-3)
+    assert torch.allclose(s[:, 1], (yd * yd).sum(1), rtol=1e-5, atol=1e-3)
+    cf = ops.ln_row_coef(st, C, eps)
+    yd64 = yd - yd.mean(1, keepdim=True)
+    ref_cf = torch.stack([1 / torch.sqrt((yd64 ** 2).mean(1) + eps), -yd.mean(1) / torch.sqrt((yd64 ** 2).mean(1) + eps)], 1)
+    assert torch.allclose(cf.double(), ref_cf, rtol=1e-4, atol=1e-5)
+    gam, bet = 1 + 0.2 * rnd(C), 0.2 * rnd(C)
+    from mmr_amd.towers import _ln_fold
+    # fold (1): QKV-like and FFN1-like consumers
+    for N, act in ((2304, 0), (3072, 1)):
+        w, b = bf(rnd(N, C) * C ** -0.5), rnd(N)
+        wf, c, d = _ln_fold(w, b, gam, bet)
+        out, none = ops.linear_ln(y, wf, d, act=act, ln_mode=1, coef=cf, v1=c)
+        assert none is None
+        ref = _ln_ref(yd, gam, bet, eps) @ w.double().T + b.double()
+        if act:
+            ref = F.gelu(ref)
+        assert rel_err(out, ref) < 1e-2, (N, act, rel_err(out, ref))
+    # normalised residual (2) + statistics: FFN2-like (K = 3072)
+    f1, w2, b2 = bf(rnd(M, 3072)), bf(rnd(C, 3072) * 3072 ** -0.5), rnd(C)
+    y2, st2 = ops.linear_ln(f1, w2, b2, residual=y, ln_mode=2, coef=cf, v1=gam, v2=bet, want_stats=True)
+    ref2 = f1.double() @ w2.double().T + b2.double() + _ln_ref(yd, gam, bet, eps)
+    assert rel_err(y2, ref2) < 1e-2
+    s2 = st2.double().sum(1)
+    assert torch.allclose(s2[:, 0], y2.double().sum(1), rtol=1e-5, atol=1e-3)
+
+
+def test_linear_ln_rejects():
+    """Shapes and combinations the LayerNorm-fused GEMM does not build fail loudly."""
+    x, w, b = bf(torch.randn(100, 768, device=DEV)), bf(torch.randn(768, 768, device=DEV)), torch.randn(768, device=DEV)
+    with pytest.raises(Exception, match="multiple of 256"):
+        ops.linear_ln(x, w, b, want_stats=True)
+    x = bf(torch.randn(256, 768, device=DEV))
+    with pytest.raises(Exception, match="without GELU"):
+        ops.linear_ln(x, w, b, act=1, want_stats=True)
+    with pytest.raises(Exception, match="not built"):
+        ops.linear_ln(x, w, b, residual=x)
+
+
+def test_bert_ln_fold_matches_unfused():
+    """BERT-base tower (random init), B=4 x L=128: the LayerNorm-folded layer stack (towers.py
+    _forward_folded) and the unfused one (add_layernorm passes) against the fp32 oracle — both at the
+    end-to-end embedding bar (cosine >= 0.999, max|err| <= 4e-2 * max|ref|), and the folded stack's
+    error no worse than 1.5x the unfused one's."""
+    bsd = init_bert_state(BERT_BASE, 11)
+    from mmr_amd.towers import BertTower
+    tw = BertTower(bsd, BERT_BASE, device=DEV)
+    assert tw.ln_fold
+    ids, mask = (torch.from_numpy(a) for a in synthetic.reports(4, 128, 12))
+    fold = tw.forward(ids.to(DEV), mask.to(DEV))
+    tw.ln_fold = False
+    unf = tw.forward(ids.to(DEV), mask.to(DEV))
+    with torch.no_grad():
+        ref = otw.bert_forward(ids, mask, bsd, BERT_BASE["num_hidden_layers"], BERT_BASE["num_attention_heads"])
+    for got in (fold, unf):
+        cos = F.cosine_similarity(got.float().cpu().reshape(-1, 768), ref.float().reshape(-1, 768), dim=-1)
+        assert cos.min().item() >= 0.999
+        assert rel_err(got, ref) <= 4e-2
+    assert rel_err(fold, ref) <= 1.5 * rel_err(unf, ref) + 1e-3, (rel_err(fold, ref), rel_err(unf, ref))
