@@ -340,7 +340,10 @@ def main():
     q_per_s = world * nq_step * a.steps / elapsed
     pairs_per_s = (world * nq_step) * (world * n) * a.steps / elapsed
     Qs = world * nq_step
-    roof, knn_roof = roofline(a, n, d, K, Qs, ms_search, ms_small, q16.shape[0], gemm_ms, B, lat_small, lat_cold)
+    ln_fold = bool(model is not None and a.model_type != "image" and getattr(model.backbones.bert, "ln_fold", False)
+                   and (B * 128) % 256 == 0)
+    roof, knn_roof = roofline(a, n, d, K, Qs, ms_search, ms_small, q16.shape[0], gemm_ms, B, lat_small, lat_cold,
+                              ln_fold=ln_fold)
 
     cpu = cpu_knn = recall = p10 = x3_line = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -401,7 +404,7 @@ def main():
         dist.destroy_process_group()
 
 
-def roofline(a, n, d, K, Qs, ms_search, ms_small, q_small, gemm_ms, B, lat_small=None, lat_cold=None):
+def roofline(a, n, d, K, Qs, ms_search, ms_small, q_small, gemm_ms, B, lat_small=None, lat_cold=None, ln_fold=False):
     """Roofline object of the dominant kernel (full: the BERT FFN1 GEMM, with the other BERT GEMM
     families beside it; knn: the search call) + the kNN search's own roofline."""
     # kNN search: algorithmic flops 2*Q*N*D; bytes = the scanned gallery copy once + norms + queries +
@@ -461,15 +464,17 @@ def roofline(a, n, d, K, Qs, ms_search, ms_small, q_small, gemm_ms, B, lat_small
                          "frac": wmul * fl / (ms / 1e3) / peak_gemm}
         ms_ffn1 = gemm_ms["ffn1"]
         fl = 2.0 * M * 3072 * 768
+        ln_fold = ln_fold and not (fp8 or x3)
+        ffn1_kind = ("LayerNorm-folded mmr_linear_bf16_ln = gemm_bf16_tn_p8<4, 1, LNM=1>" if ln_fold
+                     else "tuned variant")
         roof = {"bound": "mfma", "achieved": wmul * fl / (ms_ffn1 / 1e3) / 1e12, "peak": peak_gemm / 1e12,
                 "unit": "TFLOP/s", "traffic": None,
                 "kernel": (("BERT FFN1 bf16x3 GEMM + GELU (M=%d, N=3072, K=768; x3_gemm, f32 in / out; achieved = "
                             "MFMA work, 3 bf16 products per f32 product), " if x3 else
-                            "BERT FFN1 MX-fp8 GEMM + GELU (M=%d, N=3072, K=768; gemm_bf16_tn_p8<4, FP8>, bf16 "
-                            "output) + its activation quantiser launch: the per-GEMM timing pass runs the "
-                            "UNFUSED form (in the timed steps FFN1 emits FFN2's fp8 operand directly, "
-                            "mmr_linear_mxfp8_q8), " if fp8 else
-                            "BERT FFN1 GEMM + GELU (M=%d, N=3072, K=768; tuned variant), ") % M
+                            "BERT FFN1 MX-fp8 GEMM + GELU (M=%d, N=3072, K=768; the kernel the timed steps run: "
+                            "mmr_linear_mxfp8_q8 = gemm_bf16_tn_p8<4, 1, FP8, OUT8>, emitting FFN2's fp8 operand), "
+                            if fp8 else
+                            "BERT FFN1 GEMM + GELU (M=%d, N=3072, K=768; %s), ") % ((M,) if (x3 or fp8) else (M, ffn1_kind))
                            + "timed per launch with HIP events in a towers-in-sequence pass after the timed region"),
                 "ms_per_launch": ms_ffn1, "flops_per_launch": fl, "bert_gemms": fam, "knn": knn_roof}
     elif a.mode == "full":
@@ -490,6 +495,12 @@ def roofline(a, n, d, K, Qs, ms_search, ms_small, q_small, gemm_ms, B, lat_small
     tr = pmc_traffic()
     if gemm_ms and (fp8 or x3):
         roof["variant"] = "mxfp8" if fp8 else "x3"
+    elif gemm_ms and ln_fold and not (fp8 or x3):
+        roof["variant"] = "ln_fold"
+        rec = tr.get("bert_ffn1_ln_fold")
+        if rec is not None:
+            roof["traffic"] = rec["hbm_bytes"]
+            roof["traffic_source"] = rec["source"]
     elif gemm_ms:
         from mmr_amd import _lib
         var = int(_lib.lib().mmr_linear_bf16_variant(B * 128, 3072, 768, 1, 1, 0))

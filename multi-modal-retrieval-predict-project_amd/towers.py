@@ -74,16 +74,29 @@ def _rows256(x):
     return rows, -(-rows // 256) * 256
 
 
-def _mlp8(h, w1_8, b1, w2_8, b2, residual=None, h8=None):
+def _timed(ev, name, fn):
+    """fn() with a HIP event pair around it appended to ev[name] (ev None: just fn())."""
+    if ev is None:
+        return fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    out = fn()
+    e1.record()
+    ev.setdefault(name, []).append((e0, e1))
+    return out
+
+
+def _mlp8(h, w1_8, b1, w2_8, b2, residual=None, h8=None, ev=None):
     """fc1 (+ GELU) -> fc2 on the MX-fp8 path with fc1's epilogue emitting fc2's fp8 operand
     (mmr_linear_mxfp8_q8): the hidden activation never exists in bf16.  h8: h's fp8 operand when
-    the producing LayerNorm already emitted it (rows a multiple of 256)."""
+    the producing LayerNorm already emitted it (rows a multiple of 256).  ev: per-GEMM event dict
+    ("ffn1" / "ffn2"), as BertTower.gemm_events."""
     K = h.shape[-1]
     rows, rp = _rows256(h)
     x8 = h8 if h8 is not None else ops.quantize_mxfp8(_pad_rows(h.reshape(-1, K), rp), layout=0, kp=w1_8.kp)
-    f8 = ops.linear_mxfp8_q8(x8, w1_8, b1, act=1)
+    f8 = _timed(ev, "ffn1", lambda: ops.linear_mxfp8_q8(x8, w1_8, b1, act=1))
     r = None if residual is None else _pad_rows(residual.reshape(rows, -1), rp)
-    y = ops.linear_mxfp8(f8, w2_8, b2, r)
+    y = _timed(ev, "ffn2", lambda: ops.linear_mxfp8(f8, w2_8, b2, r))
     return (y if rp == rows else y[:rows]).reshape(tuple(h.shape[:-1]) + (y.shape[-1],))
 
 
@@ -340,7 +353,7 @@ class BertTower:
         rows, C = ids.numel(), self.hidden
         # fp8 fast path: every LayerNorm also emits the next GEMM's MX-fp8 operand (the embedding
         # LayerNorm the first QKV's), FFN1 emits FFN2's
-        fast8 = (self.fp8 and ev is None and C % 256 == 0 and C <= 1024 and rows % 256 == 0
+        fast8 = (self.fp8 and C % 256 == 0 and C <= 1024 and rows % 256 == 0
                  and all(ly["qkv_w8"].kp == C and ly["i_w8"].layout == 2 for ly in self.layers))
 
         def gemm(name, x, w, b, act=0, w8=None):
@@ -373,16 +386,17 @@ class BertTower:
         lead = tuple(h.shape[:-1])
         for ly in self.layers:
             if fast8:
-                qkv = ops.linear_mxfp8(h8, ly["qkv_w8"], ly["qkv_b"], lead=lead)
+                # (events, when set, time the very kernels the timed steps run)
+                qkv = _timed(ev, "qkv", lambda: ops.linear_mxfp8(h8, ly["qkv_w8"], ly["qkv_b"], lead=lead))
                 dh = self.hidden // heads
                 if dh % 32 == 0 and ly["o_w8"].kp == self.hidden:  # the attention emits O-proj's operand
                     _, c8 = ops.bert_attention(qkv, mask, heads, dh, q8=True, bf16=False)
-                    a = ops.linear_mxfp8(c8, ly["o_w8"], ly["o_b"], lead=lead)
+                    a = _timed(ev, "o", lambda: ops.linear_mxfp8(c8, ly["o_w8"], ly["o_b"], lead=lead))
                 else:
                     ctx = ops.bert_attention(qkv, mask, heads, dh)
-                    a = _lin(ctx, ly["o_w"], ly["o_b"], w8=ly["o_w8"])
+                    a = gemm("o", ctx, ly["o_w"], ly["o_b"], w8=ly["o_w8"])
                 h, h8 = ops.layernorm_q8(a, h, ly["ln1_g"], ly["ln1_b"], 1e-12)
-                f = _mlp8(h, ly["i_w8"], ly["i_b"], ly["f_w8"], ly["f_b"], h8=h8)
+                f = _mlp8(h, ly["i_w8"], ly["i_b"], ly["f_w8"], ly["f_b"], h8=h8, ev=ev)
                 h, h8 = ops.layernorm_q8(f, h, ly["ln2_g"], ly["ln2_b"], 1e-12)
                 continue
             qkv = gemm("qkv", h, ly["qkv_w"], ly["qkv_b"], w8=ly["qkv_w8"])
