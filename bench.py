@@ -170,7 +170,7 @@ def main():
         mt = "text" if a.model_type == "both" else a.model_type
         model = build_bench_model(device=dev, joint_dim=d, model_type=mt, tower_dtype=a.tower_dtype)
         if a.sequential_towers:
-            model.concurrent_towers = model.fusion.side_streams = False
+            set_streams(model, False)
         if a.model_type != "text":
             imgs = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(B, synthetic.SEED + rank))).to(dev)
         if a.model_type != "image":
@@ -324,12 +324,12 @@ def main():
         # timed region with the towers in sequence: inside the timed steps the Swin tower runs
         # concurrently on a side stream, and events around one kernel would also count the
         # co-running kernels' share
-        model.concurrent_towers = model.fusion.side_streams = False
+        set_streams(model, False)
         model.backbones.bert.gemm_events = {}
         for _ in range(3):
             step(False)
         torch.cuda.synchronize(dev)
-        model.concurrent_towers = model.fusion.side_streams = not a.sequential_towers
+        set_streams(model, not a.sequential_towers)
         for name, evs in model.backbones.bert.gemm_events.items():
             gemm_ms[name] = sum(e0.elapsed_time(e1) for e0, e1 in evs) / max(len(evs), 1)
         model.backbones.bert.gemm_events = None
@@ -358,8 +358,8 @@ def main():
             recall = recall_vs_cpu(index, q_par, emb_par, G, K)
             p10 = precision_vs_cpu(q_par, emb_par, d, a.knn_mode)
             del emb_cpu
-            if a.tower_dtype != "x3" and not a.no_x3_line and a.model_type in ("multimodal", "text") and B <= 1024:
-                x3_line = x3_block(a, index, G, imgs, ids, mask, emb_par, nq_par, K, dev)
+            if a.tower_dtype != "x3" and not a.no_x3_line and a.model_type in ("multimodal", "text") and B <= 2048:
+                x3_line = x3_block(a, index, G, imgs, ids, mask, emb_par, nq_par, K, dev, steps=5 if B <= 1024 else 3)
 
     if rank == 0:
         workload = {
@@ -402,6 +402,13 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def set_streams(model, on):
+    """Side-stream overlap of the Swin tower (and of the fusion stack's patch-side work) on / off."""
+    model.concurrent_towers = on
+    if getattr(model, "fusion", None) is not None:
+        model.fusion.side_streams = on
 
 
 def roofline(a, n, d, K, Qs, ms_search, ms_small, q_small, gemm_ms, B, lat_small=None, lat_cold=None, ln_fold=False):

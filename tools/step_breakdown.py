@@ -25,7 +25,9 @@ mt = args.model_type
 torch.cuda.set_device(0)
 dev = torch.device("cuda:0")
 model = build_bench_model(device=dev, joint_dim=args.dim, model_type=mt, tower_dtype=args.tower_dtype)
-model.concurrent_towers = model.fusion.side_streams = False
+model.concurrent_towers = False
+if model.fusion is not None:
+    model.fusion.side_streams = False
 B = args.batch
 imgs = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(B, synthetic.SEED))).to(dev)
 ids_np, mask_np = synthetic.reports(B, 128, synthetic.SEED + 100)
