@@ -697,11 +697,17 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   const int nk = K * ESZ / 128;  // 128-byte K-tiles; even (launcher)
   // operand panels as buffer descriptors (uniform, SGPRs): a piece is buffer_load ... lds with the
   // per-lane offset in voffset and the K-tile offset in soffset — no per-piece address registers
+#ifdef MMR_P8_SAMEPANEL
+  // diagnostic build: every tile stages the FIRST X / W panels (L2-resident operand stream; results wrong)
+  auto pan = [](int) { return 0; };
+#else
+  auto pan = [](int v) { return v; };
+#endif
   auto xbase = [&](int tile) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)X + (int64_t)mof(tile) * 256 * K * ESZ), 0, 0x7FFFFFFF, 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)X + (int64_t)pan(mof(tile)) * 256 * K * ESZ), 0, 0x7FFFFFFF, 0x00020000);
   };
   auto wbase = [&](int tile) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)W + (int64_t)nof(tile) * TBN * K * ESZ), 0, 0x7FFFFFFF, 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)W + (int64_t)pan(nof(tile)) * TBN * K * ESZ), 0, 0x7FFFFFFF, 0x00020000);
   };
   // MX scales: one 1-KB piece per operand panel and K-tile (wave 0: X's, wave 1: W's); a wave issues
   // it with its first piece of that K-tile, so every count-based wait below still covers it

@@ -20,7 +20,8 @@ Every fusion layer reads the SAME backbone features (img_global, img_patches, tx
   fused sequence   [ln_img(.); img_patch_proj(P) + out_proj(img2txt); ln_txt(.)] + pe  ->  QKV GEMM
                    -> mha with mean output -> one f32 out_proj row per batch (model.py:431 mean)
   joint chain      f32 (B, D): norm1 / alpha residual, norm2 -> FFN, adapter (f32 vectors, linears on
-                   bf16x3 MFMA: ops.linear_x3, ~2^-17 relative per product)
+                   bf16x3 MFMA: ops.linear_x3, ~2^-17 relative per product; exact f32 with
+                   exact_query_linears=True)
 
 bf16 activations / f32 accumulation for the token-level work, f32 for every per-query vector (its
 linears on bf16x3 MFMA).
@@ -115,9 +116,13 @@ class _Enhancer:
 class FusionStack:
     """The multimodal head: num_fusion_layers x CrossModalFusion + combiner (model.py:375-459)."""
 
-    def __init__(self, sd, num_heads, device="cuda", use_shared_ffn=False, eps=1e-5, tower_dtype="bf16"):
+    def __init__(self, sd, num_heads, device="cuda", use_shared_ffn=False, eps=1e-5, tower_dtype="bf16",
+                 exact_query_linears=False):
         dev = torch.device(device)
         self.device, self.heads, self.eps = dev, num_heads, eps
+        # the per-query linears (phases 2-4) on bf16x3 MFMA (default, ~2^-17 relative per product) or,
+        # exact_query_linears = True, on exact f32 (ops.linear_f32 / linear_f32_batched, ~5x slower)
+        self.exact_query_linears = exact_query_linears
         self.side_streams = True  # patch-side layer work on a side stream (False: one stream)
         fp8 = tower_dtype == "fp8"
         self.fp8 = fp8
@@ -216,6 +221,16 @@ class FusionStack:
             L["ad_x3"] = (X3(L["ad"][0]), X3(L["ad"][2]))
         self.ln_img_all = tuple(torch.stack([L["ln_img"][k] for L in Ls]).contiguous() for k in (0, 1))
         self.ln_txt_all = tuple(torch.stack([L["ln_txt"][k] for L in Ls]).contiguous() for k in (0, 1))
+
+    def _ql(self, x, wx, bias=None, residual=None, act=0, out=None):
+        if self.exact_query_linears:
+            return ops.linear_f32(x, wx.w, bias, residual=residual, act=act, out=out)
+        return ops.linear_x3(x, wx, bias, residual=residual, act=act, out=out)
+
+    def _qlb(self, x, wx, bias, nbatch, b, **kw):
+        if self.exact_query_linears:
+            return ops.linear_f32_batched(x, wx.w, bias, nbatch, b, **kw)
+        return ops.linear_x3_batched(x, wx, bias, nbatch, b, **kw)
 
     def _side_stream(self, main):
         # one side stream per calling stream (pipelined callers keep their batches independent)
@@ -353,13 +368,13 @@ class FusionStack:
         dh = D // h
         sc = 1.0 / math.sqrt(dh)
         # phase 2: per-query vectors of all layers
-        Ge = ops.linear_x3(G, self.g_w_x3, self.g_b_all)               # (B, nl*Ci), layer-minor
+        Ge = self._ql(G, self.g_w_x3, self.g_b_all)               # (B, nl*Ci), layer-minor
         Ge = ops.ln_rows(Ge.view(B * nl, Ci), *self.g_ln_all, eps, groups=nl).view(B, nl * Ci)
-        t2i = ops.linear_x3_batched(m1, self.o1_x3, self.o1_b_all, nl, B)              # mean_L att_txt2img
-        x1 = ops.linear_x3_batched(Ge, self.gp_x3, self.gp_b_all, nl, B, residual=t2i, ldx=nl * Ci, bsx=Ci)
+        t2i = self._qlb(m1, self.o1_x3, self.o1_b_all, nl, B)              # mean_L att_txt2img
+        x1 = self._qlb(Ge, self.gp_x3, self.gp_b_all, nl, B, residual=t2i, ldx=nl * Ci, bsx=Ci)
         x1 = ops.ln_rows(x1.view(nl * B, D), *self.ln_img_all, eps, groups=nl, group_div=B)
-        i2t = ops.linear_x3_batched(m2, self.o2_x3, self.o2_b_all, nl, B)              # mean_Np att_img2txt
-        x2 = ops.linear_x3_batched(cls, self.tp_x3, self.tp_b_all, nl, B, residual=i2t)
+        i2t = self._qlb(m2, self.o2_x3, self.o2_b_all, nl, B)              # mean_Np att_img2txt
+        x2 = self._qlb(cls, self.tp_x3, self.tp_b_all, nl, B, residual=i2t)
         x2 = ops.ln_rows(x2.view(nl * B, D), *self.ln_txt_all, eps, groups=nl, group_div=B)
         # phase 3: the shared combiner self-attention over every layer's fused sequence
         m3 = torch.empty((nl * B, D), dtype=torch.float32, device=dev)
@@ -375,7 +390,7 @@ class FusionStack:
             SQ = ops.linear(S, self.s_w, self.s_b)
         if not self.x3:
             ops.mha(SQ[:, :D], SQ[:, D:2 * D], SQ[:, 2 * D:], nl * B, Np + 2, Np + 2, h, dh, sc, mean_out=m3)
-        fused = ops.linear_x3(m3, self.s_ow_x3, self.s_ob).view(nl, B, D)  # mean of self_attn output
+        fused = self._ql(m3, self.s_ow_x3, self.s_ob).view(nl, B, D)  # mean of self_attn output
         # phase 4: the joint chain
         joint = None
         for i, L in enumerate(self.layers):
@@ -386,9 +401,9 @@ class FusionStack:
             xf = ops.ln_rows(x, *L["n2"], eps)
             _, b1, _, b2 = L["ffn"]
             w1, w2 = L["ffn_x3"]
-            ops.linear_x3(ops.linear_x3(xf, w1, b1, act=1), w2, b2, residual=x, out=x)
+            self._ql(self._ql(xf, w1, b1, act=1), w2, b2, residual=x, out=x)
             _, c1, _, c2 = L["ad"]
             a1, a2 = L["ad_x3"]
-            ops.linear_x3(ops.linear_x3(x, a1, c1, act=1), a2, c2, residual=x, out=x)
+            self._ql(self._ql(x, a1, c1, act=1), a2, c2, residual=x, out=x)
             joint = x
         return joint.contiguous()

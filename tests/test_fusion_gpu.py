@@ -187,6 +187,30 @@ def test_fusion_stack_vs_oracle_on_backbone_features(text):
     _check_emb(got, ref)
 
 
+def test_fusion_stack_exact_query_linears():
+    """exact_query_linears=True routes the per-query linears (global enhancer, out-projections, the
+    joint chain) to exact f32 (mmr_linear_f32*): same result as the bf16x3 default within 1e-5
+    relative, both against the oracle."""
+    g = torch.Generator().manual_seed(13)
+    B, Lt, Np, C, D = 3, 128, 49, 768, 768
+    hs = init_head_state(C, C, D, 25)
+    hs.update(init_fusion_state(C, C, D, 8, 3, 26))
+    G = torch.randn(B, C, generator=g)
+    P = torch.randn(B, Np, C, generator=g)
+    T = bf(torch.randn(B, Lt, C, generator=g)).float()
+    with torch.no_grad():
+        ref = otw.multimodal(G, P, T, hs, num_heads=8)
+    from mmr_amd.fusion import FusionStack
+    fs = FusionStack(hs, 8, device=DEV)
+    x3 = fs.forward(G.to(DEV), P.to(DEV), T.to(DEV))
+    fs.exact_query_linears = True
+    ex = fs.forward(G.to(DEV), P.to(DEV), T.to(DEV))
+    assert FusionStack(hs, 8, device=DEV, exact_query_linears=True).exact_query_linears
+    _check_emb(ex, ref)
+    assert rel_err(ex.cpu(), x3.cpu()) <= 1e-5
+    assert not torch.equal(ex, x3)  # the two routes really differ (bf16x3 vs f32 products)
+
+
 def test_full_size_multimodal_vs_oracle():
     """Swin-T + BERT-base + 5-layer multimodal head (joint 768, 8 heads) end to end, B=2."""
     ssd, bsd = init_swin_state(SWIN_T, 5), init_bert_state(BERT_BASE, 6)

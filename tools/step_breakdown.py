@@ -1,7 +1,7 @@
 """Per-op time breakdown of one bench step (multimodal default): wraps the mmr_amd.ops entry points
 with HIP events on the current stream and prints, per (op, shape), calls / total ms / TF/s for the
 GEMMs.  Diagnostic only.
-usage: python tools/step_breakdown.py [--model-type multimodal|text] [--batch B] [--dim D] [--tower-dtype bf16|fp8]
+usage: python tools/step_breakdown.py [--model-type multimodal|text] [--batch B] [--dim D] [--tower-dtype bf16|fp8] [--no-ln-fold]
 (the towers and fusion layers run on one stream here: per-op events are exact only then)"""
 import argparse
 import collections
@@ -20,12 +20,15 @@ ap.add_argument("--model-type", default="multimodal")
 ap.add_argument("--batch", type=int, default=256)
 ap.add_argument("--dim", type=int, default=768)
 ap.add_argument("--tower-dtype", default="bf16")
+ap.add_argument("--no-ln-fold", action="store_true", help="BERT with its LayerNorm passes (unfolded)")
 args = ap.parse_args()
 mt = args.model_type
 torch.cuda.set_device(0)
 dev = torch.device("cuda:0")
 model = build_bench_model(device=dev, joint_dim=args.dim, model_type=mt, tower_dtype=args.tower_dtype)
 model.concurrent_towers = False
+if args.no_ln_fold and getattr(model, "bert", None) is not None:
+    model.bert.ln_fold = False
 if model.fusion is not None:
     model.fusion.side_streams = False
 B = args.batch
