@@ -109,9 +109,6 @@ __device__ __forceinline__ float gelu_t(float v) {
 template <bool FAST>
 __device__ __forceinline__ uint32_t gelu_pack2(float a0, float a1) {
   if constexpr (FAST) {
-#ifdef MMR_MLP_GELU_SCALAR
-    return mmr::pack2bf(mmr::gelu_fast1(a0), mmr::gelu_fast1(a1));
-#endif
     const mmr::f32x2_t u = mmr::gelu_fast2((mmr::f32x2_t){a0, a1});
     return mmr::pack2bf(u.x, u.y);
   } else {
