@@ -206,7 +206,7 @@ mmr_status mmr_pin_variant(int32_t which, int32_t value);
 
 /* Resident-weight streaming linear for the short-K, narrow tower linears (Swin patch embed, stage-2
  * qkv / proj, PatchMerging 1->2; timm nn.Linear, reference fusion.py:198-199):
- * y = x @ W^T + bias (+ residual), K in {64, 192, 384}.  W is kept in LDS for the whole launch, as
+ * y = x @ W^T + bias (+ residual), K in {64, 192}.  W is kept in LDS for the whole launch, as
  * mmr_linear_rw_parts(n, k) parts of N / P channels, from an image built once by
  * mmr_linear_rw_pack (n * k bf16 elements, caller-allocated).  mmr_linear_rw_parts returns 0 for
  * shapes it does not take (then use mmr_linear_bf16). */

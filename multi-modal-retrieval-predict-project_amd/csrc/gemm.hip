@@ -613,7 +613,13 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   auto soff = [](int buf) { return 2 * (TA + TB) + buf * C::SC; };
   constexpr int ESZ = FP8 ? 1 : 2;                      // operand element bytes
   constexpr int NH0 = NT / 2;                           // n-tiles in n-half 0
-  static_assert(C::NSTORE_LDS + 5 <= 63 && C::NSTORE_PL + 5 <= 63, "vmcnt range");
+  // Residual of NT = 3 tiles loaded at the START of the tile (24 x 8 B per lane into 48 VGPRs, held
+  // through the K loop) instead of in the epilogue: an epilogue load retires (vmcnt, in order) behind
+  // the next tile's K-tile prefetch and exposes it at every tile.  The tile's first counted wait
+  // leaves them in flight (NRES more younger ops).  NT = 4 tiles have no registers for them.
+  constexpr bool early_res = HAS_RES && NT == 3 && !FP8;  // (FP8 tiles: no registers either)
+  constexpr int NRES = early_res ? 8 * NT : 0;
+  static_assert(C::NSTORE_LDS + 13 + NRES <= 63 && C::NSTORE_PL + 5 + NRES <= 63, "vmcnt range");
   // Epilogue: permlane row chunks straight from registers (no LDS round trips) for GELU epilogues,
   // the per-wave LDS staging otherwise: measured (random operands, profiles/r03_gemm_epilogue_ab.txt)
   // FFN1 + GELU 925 -> 1015 TF and Swin fc1 + GELU +8 % with permlane, but the plain / residual
@@ -658,22 +664,27 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   // bias (and LNM vectors) of a tile -> LDS by LDS-DMA from wave 0: the first tile's in the prologue,
   // each next tile's at the end of wave 0's epilogue (the other parity; no registers live across the loop)
   float* lcoef = lbias + 2 * NV * TBN;  // LNM: [2][256][2] f32 row coefficients, by tile parity
+  // (buffer-descriptor form: uniform bases in SGPRs, the lane's byte offset recomputed from an opaque
+  // lane id — a 64-bit per-lane address kept live across the loop was spilled in the MX-fp8 kernels,
+  // and its reload, a vmcnt op, drained the next tile's prefetch at every tile)
   auto bias_dma = [&](int tile, int par) {
-    if (LNM != 0 && wave == 0) {  // the tile's 256 row-coefficient pairs: 2 x 1 KB
-      const float* src = LC + (int64_t)mof(tile) * 512 + lane * 4;
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(lcoef + par * 512), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(src + 256), (lds_ptr_t)(lcoef + par * 512 + 256), 16, 0, 0);
+    if (wave != 0) return;
+    int ll;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ll));
+    const uint32_t lo16 = (uint32_t)ll * 16;
+    auto dma = [&](const float* base, float* dst, int soff) {
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7FFFFFFF, 0x00020000);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)dst, 16, lo16, soff, 0, 0);
+    };
+    if (LNM != 0) {  // the tile's 256 row-coefficient pairs: 2 x 1 KB
+      const float* src = LC + (int64_t)mof(tile) * 512;
+      dma(src, lcoef + par * 512, 0);
+      dma(src, lcoef + par * 512 + 256, 1024);
     }
-    if (wave == 0 && lane < TBN / 4) {
-      if (HAS_BIAS)
-        __builtin_amdgcn_global_load_lds((const void*)(bias + nof(tile) * TBN + lane * 4),
-                                         (lds_ptr_t)(lbias + par * NV * TBN), 16, 0, 0);
-      if (LNM != 0)
-        __builtin_amdgcn_global_load_lds((const void*)(LV1 + nof(tile) * TBN + lane * 4),
-                                         (lds_ptr_t)(lbias + (par * NV + 1) * TBN), 16, 0, 0);
-      if (LNM == 2)
-        __builtin_amdgcn_global_load_lds((const void*)(LV2 + nof(tile) * TBN + lane * 4),
-                                         (lds_ptr_t)(lbias + (par * NV + 2) * TBN), 16, 0, 0);
+    if (ll < TBN / 4) {
+      if (HAS_BIAS) dma(bias + nof(tile) * TBN, lbias + par * NV * TBN, 0);
+      if (LNM != 0) dma(LV1 + nof(tile) * TBN, lbias + (par * NV + 1) * TBN, 0);
+      if (LNM == 2) dma(LV2 + nof(tile) * TBN, lbias + (par * NV + 2) * TBN, 0);
     }
   };
 
@@ -839,6 +850,15 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    // the residual (early_res): lane row 16 i + fr, columns 16 j + 4 fq .. + 3 of the wave tile
+    uint2 rq[HAS_RES ? 8 : 1][HAS_RES ? NT : 1];
+    if constexpr (early_res) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          rq[i][j] = *(const uint2*)(R + (m0 + wr * 128 + i * 16 + fr) * N + n0 + wc * 16 * NT + j * 16 + fq * 4);
+    }
 
     for (int it = 0; it < nk / 2; ++it) {
       const bool last_it = it + 1 == nk / 2;
@@ -857,11 +877,15 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
             // at every K-tile: fp8 phases ran ~30 % longer than bf16's)
             typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
             typedef uint32_t u32x1_t __attribute__((ext_vector_type(1)));
+            // lane offsets from a freshly computed lane id (opaque to hipcc): kept live across the
+            // K loop they were spilled, and a spill reload is a vmcnt op that drains the prefetch
+            int ll;
+            asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ll));
             const uint8_t* sb = (const uint8_t*)(dsm + soff(buf));
-            const u32x2_t sa2 = *(const u32x2_t*)(sb + ((wr * 4 + fq) * 16 + fr) * 8);
+            const u32x2_t sa2 = *(const u32x2_t*)(sb + wr * 512 + ll * 8);  // ((wr 4 + fq) 16 + fr) 8
             sca[0] = sa2[0];
             sca[1] = sa2[1];
-            scb = (*(const u32x1_t*)(sb + 1024 + ((wc * 4 + fq) * 16 + fr) * 4))[0];
+            scb = (*(const u32x1_t*)(sb + 1024 + wc * 256 + ll * 4))[0];
           }
 #pragma unroll
           for (int i = 0; i < 4; ++i) ldA(buf, i, i);
@@ -892,7 +916,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
         issue(2 * p);
         if (p == 3) {  // end of s6: O complete (younger: E pieces, + last tile's stores at it 0)
           if (!loads) __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
-          else if (it == 0 && !first) __builtin_amdgcn_s_waitcnt(vmcnt_imm(5 + nstore));
+          else if (it == 0 && !first) __builtin_amdgcn_s_waitcnt(vmcnt_imm(5 + nstore + NRES));
+          else if (it == 0) __builtin_amdgcn_s_waitcnt(vmcnt_imm(5 + NRES));
           else __builtin_amdgcn_s_waitcnt(vmcnt_imm(5));
         } else if (p == 7) {  // end of s14: E complete (younger: 5 O pieces)
           if (loads) __builtin_amdgcn_s_waitcnt(vmcnt_imm(5));
@@ -1022,8 +1047,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
         rb[i] = cf.y;
       }
     }
-    uint2 rq[HAS_RES ? 8 : 1][HAS_RES ? NT : 1];
-    if constexpr (HAS_RES) {
+    if constexpr (HAS_RES && !early_res) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll

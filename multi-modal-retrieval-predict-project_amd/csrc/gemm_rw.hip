@@ -1,6 +1,6 @@
 // Resident-weight streaming GEMM for the short-K, narrow-N tower linears (Swin patch embed, stage-2
 // qkv / proj, the stage-1 -> 2 PatchMerging reduction):  Y = X W^T + b (+ R), X [M][K] bf16,
-// W [N][K] bf16 (nn.Linear), K in {64, 192, 384}.  These shapes are HBM-bound (K = 64 ... 384:
+// W [N][K] bf16 (nn.Linear), K in {64, 192}.  These shapes are HBM-bound (K = 64 ... 192:
 // 2K bytes read and 2N written per token against 2NK flops), and the general GEMM tiles re-stream
 // W per 256-row tile and pay a K-loop prologue per tile that such short K never amortises
 // (M = 200704, N = 576, K = 192: 124 us = 2.5 TB/s).
@@ -186,7 +186,9 @@ void launch_rw(const uint16_t* x, const uint16_t* img, const float* bias, const 
 }  // namespace
 
 extern "C" int32_t mmr_linear_rw_parts(int32_t n, int32_t k) {
-  if (!(k == 64 || k == 192 || k == 384) || n <= 0 || n % 32) return 0;
+  // (K = 384 dropped: its 32-token tile needs more than 256 VGPRs — 21-143 spilled — and measured
+  // slower than the GEMM, profiles/r03_s4_linear_rw.txt)
+  if (!(k == 64 || k == 192) || n <= 0 || n % 32) return 0;
   return rw_parts(n, k);
 }
 
@@ -194,13 +196,12 @@ extern "C" mmr_status mmr_linear_rw_pack(const uint16_t* w, int32_t n, int32_t k
   mmr::clear_error();
   MMR_REQUIRE(w && img, "mmr_linear_rw_pack: NULL pointer");
   const int parts = mmr_linear_rw_parts(n, k);
-  MMR_REQUIRE(parts > 0, "mmr_linear_rw_pack: N=%d K=%d not supported (K in {64, 192, 384}, N %% 32 == 0, N/P * K * 2 <= 150 KiB)", n, k);
+  MMR_REQUIRE(parts > 0, "mmr_linear_rw_pack: N=%d K=%d not supported (K in {64, 192}, N %% 32 == 0, N/P * K * 2 <= 150 KiB)", n, k);
   const int no = n / parts;
   hipStream_t st = mmr::as_stream(stream);
   const dim3 grid((unsigned)mmr::ceil_div((int64_t)n * k, 256));
   if (k == 64) rw_pack<64><<<grid, 256, 0, st>>>(w, n, no, img);
-  else if (k == 192) rw_pack<192><<<grid, 256, 0, st>>>(w, n, no, img);
-  else rw_pack<384><<<grid, 256, 0, st>>>(w, n, no, img);
+  else rw_pack<192><<<grid, 256, 0, st>>>(w, n, no, img);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }
@@ -222,7 +223,7 @@ extern "C" mmr_status mmr_linear_rw(const uint16_t* x, const uint16_t* img, cons
     else launch_rw<KK, false, false>(x, img, bias, residual, y, m, n, parts, st);          \
   }
   RW_K(64)
-  else RW_K(192) else RW_K(384)
+  else RW_K(192)
 #undef RW_K
   MMR_LAUNCH_CHECK();
   return MMR_OK;

@@ -126,7 +126,6 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
   const float* Pb = P + 5 * AC;
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int r = lane & 31, h = lane >> 5;
   unsigned char* xs = smem + IMG_B + wave * XBUF_B;
   uint32_t* gco = (uint32_t*)(smem + IMG_B + NWV * XBUF_B);
 
@@ -148,11 +147,12 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
     gco[p] = (uint32_t)(t / AWS) | ((uint32_t)(t % AWS) << 8) | ((uint32_t)unit << 16);
   }
   // window token -> row of x inside the image (rolled by -shift: token (hr, wr) reads (hr+s, wr+s))
+  // (wrap as an unsigned min: no VGPR copy of H for a v_cndmask — such copies were hoisted and spilled)
   auto img_row = [&](int hs, int ws_, int ty, int tx) -> int {
-    int hh = hs + ty, ww = ws_ + tx;
-    hh = hh >= H ? hh - H : hh;
-    ww = ww >= H ? ww - H : ww;
-    return hh * H + ww;
+    uint32_t hh = (uint32_t)(hs + ty), ww = (uint32_t)(ws_ + tx);
+    hh = min(hh, hh - (uint32_t)H);
+    ww = min(ww, ww - (uint32_t)H);
+    return (int)(hh * (uint32_t)H + ww);
   };
   struct Win {
     const uint16_t* xi;
@@ -173,25 +173,24 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
     return o;
   };
   // gather window w's x into this wave's buffer: LDS chunk p = token * 13 + unit
-  auto gather = [&](const Win& wd) {
+  auto gather = [&](const Win& wd, int ln) {
     unsigned char* dst = xs;
 #pragma unroll
     for (int it = 0; it < XCH / 64; ++it) {
-      const uint32_t c = gco[it * 64 + lane];
+      const uint32_t c = gco[it * 64 + ln];
       const int row = img_row(wd.hs, wd.ws_, (int)(c & 0xff), (int)((c >> 8) & 0xff));
       const uint16_t* src = wd.xi + row * AC + (int)(c >> 16) * 8;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(dst + it * 1024), 16, 0, 0);
     }
   };
   __syncthreads();  // gather table
-  if (win < total) gather(win_of(win));
+  if (win < total) gather(win_of(win), lane);
   __builtin_amdgcn_s_waitcnt(vmcnt_n(0));
   __builtin_amdgcn_s_waitcnt(0xC07F);
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();  // weights visible to every wave; no barrier after this point
   asm volatile("" ::: "memory");
 
-  const uint32_t boff = (uint32_t)(r * 64 + 4 * h);  // this lane's bias row / column offset
   const float scale = 0.17677669529663687f;  // 32^-0.5
   const f2 L2E = pk(1.4426950408889634f, 1.4426950408889634f);
   for (; win < total; win += stride) {
@@ -199,6 +198,15 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
     __builtin_amdgcn_s_waitcnt(vmcnt_n(12));
     asm volatile("" ::: "memory");
     const Win wd = win_of(win);
+    // every lane-derived value is recomputed per window from an opaque lane id: held across the
+    // loop they were spilled, and the reloads at the loop top (vmcnt ops) waited for the previous
+    // window's row stores
+    int lnv;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lnv));
+    const int r = lnv & 31, h = lnv >> 5;
+    const uint32_t boff = (uint32_t)(r * 64 + 4 * h);  // this lane's bias row / column offset
+    float epsv;  // eps in a VGPR made per window (a hoisted copy was spilled)
+    asm volatile("v_mov_b32 %0, %1" : "=v"(epsv) : "s"(eps));
 
     // ---- LN1 -> hB[t2][ks]: B fragments, token t2*32 + r, channels 16ks + 8h + 0..7
     bf16x8 hB[2][AC / 16];
@@ -234,7 +242,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
         }
       float ss = q2.x + q2.y;
       ss = half_sum(ss);
-      const float rstd = rsqrtf(ss * (1.0f / AC) + eps);
+      const float rstd = rsqrtf(ss * (1.0f / AC) + epsv);
       const f2 rs = pk(rstd, rstd);
 #pragma unroll
       for (int ks = 0; ks < AC / 16; ++ks) {
@@ -260,7 +268,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
     uint32_t orow[2];   // element offset of each token tile's row in the image (residual + store)
 
     auto wfrag = [&](const uint16_t* W, int tile, int ks) {  // A/B fragment: 32-row tile, k-step ks
-      return *(const bf16x8*)(W + lane * 8 + (tile * (AC / 16) + ks) * 512);
+      return *(const bf16x8*)(W + lnv * 8 + (tile * (AC / 16) + ks) * 512);
     };
 
 #pragma unroll
@@ -399,13 +407,21 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // LN's reads of the buffer (long done) before the DMA
     asm volatile("" ::: "memory");
-    if (win + stride < total) gather(win_of(win + stride));
+    if (win + stride < total) gather(win_of(win + stride), lnv);
+    // the proj's lane values from a fresh opaque lane id: an address kept from the LN phase was
+    // spilled, and its reload here (a vmcnt op, younger than the gather) drained the gather
+    int lnp;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lnp));
+    const int rp = lnp & 31, hp = lnp >> 5;
 
+    auto wfragp = [&](const uint16_t* W, int tile, int ks) {
+      return *(const bf16x8*)(W + lnp * 8 + (tile * (AC / 16) + ks) * 512);
+    };
     // ---- proj: out^T[c][query] = Wproj[c][hd*32 + dh] O^T[dh][query] (+ proj_b in the accumulator);
     // y = x + out: lane half h holds channels 32u + 16 hf + 8h + 0..7 of token r
 #pragma unroll
     for (int t2 = 0; t2 < 2; ++t2) {
-      const int t = t2 * 32 + r;
+      const int t = t2 * 32 + rp;
       const bool tok_ok = t < ATOK;
       uint16_t* yr = wd.yi + orow[t2];
       f32x16 acc[3];
@@ -413,7 +429,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
       for (int u = 0; u < 3; ++u) {
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
-          const int c0 = 32 * u + 16 * hf + 8 * h;
+          const int c0 = 32 * u + 16 * hf + 8 * hp;
           const f32x4 b0 = *(const f32x4*)(Ppb + c0), b1 = *(const f32x4*)(Ppb + c0 + 4);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -423,8 +439,8 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
         }
 #pragma unroll
         for (int hd = 0; hd < AH; ++hd) {
-          acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wfrag(Wproj, u, 2 * hd), ost[hd][t2][0], acc[u], 0, 0, 0);
-          acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wfrag(Wproj, u, 2 * hd + 1), ost[hd][t2][1], acc[u], 0, 0, 0);
+          acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wfragp(Wproj, u, 2 * hd), ost[hd][t2][0], acc[u], 0, 0, 0);
+          acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wfragp(Wproj, u, 2 * hd + 1), ost[hd][t2][1], acc[u], 0, 0, 0);
         }
       }
       if (!tok_ok) continue;
@@ -432,7 +448,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
       for (int u = 0; u < 3; ++u)
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
-          const int c0 = 32 * u + 16 * hf + 8 * h;
+          const int c0 = 32 * u + 16 * hf + 8 * hp;
           const uint32_t xw[4] = {xv[t2][u][hf].x, xv[t2][u][hf].y, xv[t2][u][hf].z, xv[t2][u][hf].w};
           uint32_t o[4];
 #pragma unroll

@@ -720,19 +720,20 @@ __global__ __launch_bounds__(64 * SH_WAVES) void swin_head(const uint16_t* __res
                                                  float* __restrict__ pool, int t, int c,
                                                  float eps) {
   __shared__ float part[SH_WAVES][1024];
+  __shared__ float gs[1024], bs[1024];  // LN parameters (in registers they pushed the 128-VGPR budget into spills)
   const int bi = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int per = c / 64;
-  float acc1[SH_MAXPL], acc2[SH_MAXPL], gk[SH_MAXPL], bk[SH_MAXPL];
+  float acc1[SH_MAXPL], acc2[SH_MAXPL];
   // every load unconditional (index clamped, value masked; a "load if e < per" branch makes hipcc wait
-  // for each load before the next), the LN parameters loaded once for all tokens
-#pragma unroll
-  for (int e = 0; e < SH_MAXPL; ++e) {
-    acc1[e] = acc2[e] = 0.f;
-    const int k = lane + 64 * (e < per ? e : per - 1);
-    gk[e] = g[k];
-    bk[e] = b[k];
+  // for each load before the next)
+  for (int k = threadIdx.x; k < c; k += 64 * SH_WAVES) {
+    gs[k] = g[k];
+    bs[k] = b[k];
   }
+#pragma unroll
+  for (int e = 0; e < SH_MAXPL; ++e) acc1[e] = acc2[e] = 0.f;
+  __syncthreads();
   for (int tk = wave; tk < t; tk += SH_WAVES) {
     const uint16_t* xr = x + ((int64_t)bi * t + tk) * c;
     float v[SH_MAXPL];
@@ -752,7 +753,7 @@ __global__ __launch_bounds__(64 * SH_WAVES) void swin_head(const uint16_t* __res
 #pragma unroll
     for (int e = 0; e < SH_MAXPL; ++e)
       if (e < per) {
-        v[e] = (v[e] - mean) * rstd * gk[e] + bk[e];  // once-normed token (forward_features output)
+        v[e] = (v[e] - mean) * rstd * gs[lane + 64 * e] + bs[lane + 64 * e];  // once-normed token (forward_features output)
         acc1[e] += v[e];
         s += v[e];
       }
@@ -766,7 +767,7 @@ __global__ __launch_bounds__(64 * SH_WAVES) void swin_head(const uint16_t* __res
     for (int e = 0; e < SH_MAXPL; ++e)
       if (e < per) {
         const int k = lane + 64 * e;
-        const float p2 = (v[e] - mean) * rstd * gk[e] + bk[e];  // swin_norm applied again
+        const float p2 = (v[e] - mean) * rstd * gs[k] + bs[k];  // swin_norm applied again
         acc2[e] += p2;
         if (patches) patches[((int64_t)bi * t + tk) * c + k] = p2;
       }

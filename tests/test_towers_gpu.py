@@ -90,8 +90,8 @@ def test_linear_bf16_p8_persistent(request, cfg, M, N, K, act, bias, res):
 
 
 @pytest.mark.parametrize("M,N,K,bias,res", [(3136 * 4 + 17, 96, 64, True, False), (784 * 8 + 5, 576, 192, True, False),
-                                            (784 * 8 + 5, 192, 192, True, True), (784 * 2, 192, 384, False, False),
-                                            (1000, 384, 384, True, True), (31, 576, 192, True, True),
+                                            (784 * 8 + 5, 192, 192, True, True), (784 * 2, 192, 192, False, False),
+                                            (1000, 384, 192, True, True), (31, 576, 192, True, True),
                                             (500, 32, 64, True, False), (300, 160, 192, False, True)])
 def test_linear_rw(M, N, K, bias, res):
     """mmr_linear_rw (resident-weight streaming linear: Swin patch embed / stage-2 qkv, proj /
@@ -119,6 +119,7 @@ def test_linear_rw(M, N, K, bias, res):
 def test_linear_rw_rejects():
     assert ops.rw_pack(bf(torch.randn(96, 96)).to(DEV)) is None       # K = 96
     assert ops.rw_pack(bf(torch.randn(3072, 768)).to(DEV)) is None    # K = 768
+    assert ops.rw_pack(bf(torch.randn(384, 384)).to(DEV)) is None     # K = 384 (dropped: spilled)
 
 
 @pytest.mark.parametrize("T,C", [(1000, 96), (3136 * 4 + 17, 96), (64, 192), (784 * 8 + 5, 192), (1, 96)])

@@ -41,6 +41,7 @@ for name, K in (("o", 768), ("ffn2", 3072)):
     w, b = bf(rnd(C, K) * K ** -0.5), rnd(C)
     rows.append((f"{name} plain tuned (+res)", timeit(lambda: ops.linear(x, w, b, residual=h))))
     with ops.pinned(ops.PIN_GEMM_BF16, 10):
+        rows.append((f"{name} plain p8 256x192 (no res)", timeit(lambda: ops.linear(x, w, b))))
         rows.append((f"{name} plain p8 256x192 (+res)", timeit(lambda: ops.linear(x, w, b, residual=h))))
     rows.append((f"{name} mode0 +res +stats", timeit(lambda: ops.linear_ln(x, w, b, residual=h, want_stats=True))))
     rows.append((f"{name} mode2 (LN res)", timeit(lambda: ops.linear_ln(x, w, b, residual=h, ln_mode=2, coef=cf,

@@ -27,8 +27,8 @@ torch.cuda.set_device(0)
 dev = torch.device("cuda:0")
 model = build_bench_model(device=dev, joint_dim=args.dim, model_type=mt, tower_dtype=args.tower_dtype)
 model.concurrent_towers = False
-if args.no_ln_fold and getattr(model, "bert", None) is not None:
-    model.bert.ln_fold = False
+if args.no_ln_fold:
+    model.backbones.bert.ln_fold = False
 if model.fusion is not None:
     model.fusion.side_streams = False
 B = args.batch
