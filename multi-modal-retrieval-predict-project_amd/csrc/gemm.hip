@@ -483,6 +483,11 @@ __device__ __forceinline__ void ds_write_b64_untracked(const void* p, uint32_t l
   const unsigned long long d = ((unsigned long long)hi << 32) | lo;
   asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(d) : "memory");
 }
+__device__ __forceinline__ void ds_write_b128_untracked(const void* p, uint4 v) {
+  const uint32_t a = (uint32_t)(uintptr_t)p;
+  typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+  asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(__builtin_bit_cast(u32x4_t, v)) : "memory");
+}
 
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 // v_mfma_scale_f32_16x16x128_f8f6f4, e4m3 x e4m3; scale bytes selected by (compile-time) opsel
@@ -613,12 +618,15 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   auto soff = [](int buf) { return 2 * (TA + TB) + buf * C::SC; };
   constexpr int ESZ = FP8 ? 1 : 2;                      // operand element bytes
   constexpr int NH0 = NT / 2;                           // n-tiles in n-half 0
-  // Residual of NT = 3 tiles loaded at the START of the tile (24 x 8 B per lane into 48 VGPRs, held
-  // through the K loop) instead of in the epilogue: an epilogue load retires (vmcnt, in order) behind
-  // the next tile's K-tile prefetch and exposes it at every tile.  The tile's first counted wait
-  // leaves them in flight (NRES more younger ops).  NT = 4 tiles have no registers for them.
-  constexpr bool early_res = HAS_RES && NT == 3 && !FP8;  // (FP8 tiles: no registers either)
-  constexpr int NRES = early_res ? 8 * NT : 0;
+  // Residual of bf16 NT = 3 tiles with the LDS-staged epilogue: loaded at the START of the tile as
+  // 16-B row chunks (the layout the epilogue stores in; 12 loads per lane into 48 VGPRs, held through
+  // the K loop) and turned into the fragment layout through the wave's LDS epilogue area, instead of
+  // 24 x 8-B fragment-layout loads in the epilogue (16 half-used lines per load instruction, and an
+  // epilogue load retires — vmcnt, in order — behind the next tile's K-tile prefetch).  The tile's
+  // first counted wait leaves them in flight (NRES more younger ops).  NT = 4 / FP8 tiles have no
+  // registers for them.
+  constexpr bool early_res = HAS_RES && NT == 3 && !FP8 && !(!OUT8 && !KNN && ACT == 1);
+  constexpr int NRES = early_res ? (8 / C::RM) * C::CPL : 0;
   static_assert(C::NSTORE_LDS + 13 + NRES <= 63 && C::NSTORE_PL + 5 + NRES <= 63, "vmcnt range");
   // Epilogue: permlane row chunks straight from registers (no LDS round trips) for GELU epilogues,
   // the per-wave LDS staging otherwise: measured (random operands, profiles/r03_gemm_epilogue_ab.txt)
@@ -850,14 +858,18 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    // the residual (early_res): lane row 16 i + fr, columns 16 j + 4 fq .. + 3 of the wave tile
-    uint2 rq[HAS_RES ? 8 : 1][HAS_RES ? NT : 1];
+    // the residual (early_res): round rd, chunk c = the 16-B output chunk idx = 64 c + lane of the
+    // epilogue's store pass (row idx / 2NT of the round's 16 RM rows, columns 8 (idx % 2NT) ..)
+    uint4 rr16[early_res ? 8 / C::RM : 1][early_res ? C::CPL : 1];
     if constexpr (early_res) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int rd = 0; rd < 8 / C::RM; ++rd)
 #pragma unroll
-        for (int j = 0; j < NT; ++j)
-          rq[i][j] = *(const uint2*)(R + (m0 + wr * 128 + i * 16 + fr) * N + n0 + wc * 16 * NT + j * 16 + fq * 4);
+        for (int c = 0; c < C::CPL; ++c) {
+          const int idx = c * 64 + lane;
+          rr16[rd][c] = *(const uint4*)(R + (m0 + wr * 128 + rd * 16 * C::RM + idx / (2 * NT)) * N + n0 + wc * 16 * NT +
+                                        (idx % (2 * NT)) * 8);
+        }
     }
 
     for (int it = 0; it < nk / 2; ++it) {
@@ -1047,6 +1059,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
         rb[i] = cf.y;
       }
     }
+    uint2 rq[HAS_RES && !early_res ? 8 : 1][HAS_RES && !early_res ? NT : 1];
     if constexpr (HAS_RES && !early_res) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -1108,6 +1121,15 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
     }
 #pragma unroll
     for (int rd = 0; rd < (epi_pl ? 0 : 8 / C::RM); ++rd) {  // LDS-staged rounds
+      if constexpr (early_res) {  // the round's residual chunks -> the wave's LDS area (row layout)
+#pragma unroll
+        for (int c = 0; c < C::CPL; ++c) {
+          const int idx = c * 64 + le;
+          ds_write_b128_untracked(et + (idx / (2 * NT)) * C::ELD + (idx % (2 * NT)) * 8, rr16[rd][c]);
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+      }
 #pragma unroll
       for (int ii = 0; ii < C::RM; ++ii) {
         const int i = rd * C::RM + ii;
@@ -1130,7 +1152,9 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
             v[rg + 1] = u.y;
           }
           if constexpr (HAS_RES) {
-            const uint2 rv = rq[i][j];
+            // early_res: read back in the fragment layout from the very 8 bytes this lane overwrites
+            // with its output below (lane-private: no barrier between the read and the write)
+            const uint2 rv = early_res ? *(const uint2*)(et + (ii * 16 + efr) * C::ELD + j * 16 + efq * 4) : rq[i][j];
             float r4[4] = {__uint_as_float(rv.x << 16), __uint_as_float(rv.x & 0xFFFF0000u),
                            __uint_as_float(rv.y << 16), __uint_as_float(rv.y & 0xFFFF0000u)};
             if constexpr (LNM == 2) {
