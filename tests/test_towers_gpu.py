@@ -59,11 +59,13 @@ def test_linear_bf16(M, N, K, act, bias, res):
 @pytest.mark.parametrize("cfg", [7, 8])
 @pytest.mark.parametrize("M,N,K,act,bias,res", [(32768, 1152, 128, 0, True, False), (32768, 1152, 384, 0, True, True),
                                                 (65536, 768, 768, 0, False, True), (32768, 2304, 256, 0, False, False),
-                                                (16384, 768, 3072, 0, True, True), (32768, 1536, 384, 1, True, False)])
+                                                (16384, 768, 3072, 0, True, True), (32768, 1536, 384, 1, True, False),
+                                                (32768, 768, 128, 0, True, True), (4096, 1536, 128, 0, False, True)])
 def test_linear_bf16_p8_persistent(request, cfg, M, N, K, act, bias, res):
     """The persistent 8-phase GEMM pinned (mmr_pin_variant: variant 9 = 256x256 tiles, 10 = 256x192) on shapes with
     2-4 tiles per workgroup and K = 128 ... 3072 (1 ... 12 K iterations per tile: the K stream runs
-    on across tile boundaries), every epilogue; vs torch fp32 of the same bf16 operands (tolerance
+    on across tile boundaries; K = 128 with a residual: the one-iteration tile whose residual, loaded at
+    the tile start, is counted out of the first wait), every epilogue; vs torch fp32 of the same bf16 operands (tolerance
     1e-2 * max|ref|: bf16 output rounding)."""
     if N % (256 if cfg == 7 else 192):
         pytest.skip("tile width")
