@@ -487,6 +487,17 @@ mmr_status mmr_rows_to_f32(const uint16_t* x, int64_t ldx, float* y, int32_t b, 
 mmr_status mmr_x3_linear(const float* x, int64_t ldx, const uint16_t* w_hi, const uint16_t* w_lo, const float* bias,
                          const float* residual, int64_t ldr, float* y, int64_t ldy, int64_t m, int32_t n, int32_t k,
                          int32_t act, void* stream);
+/* The same linear at the 8-phase GEMM's rate, as ONE K' = 3 kp bf16 GEMM with f32 accumulation:
+ * X' = [x_hi | x_hi | x_lo], W' = [w_hi | w_lo | w_hi], each segment kp = mmr_x3_p8_kpad(k) wide (k
+ * rounded up to 128, zero padding; 0 = k not taken), so X'.W'^T = x_hi.w_hi + x_hi.w_lo + x_lo.w_hi.
+ * mmr_x3_split_rows writes X' ([m][3 kp] bf16, caller-allocated) from x rows at stride ldx;
+ * mmr_x3_linear_p8 takes X' and the weight image W' ([n][3 kp] bf16, built once at load) and writes
+ * y (m, n) f32 contiguous: m % 256 == 0, n % 192 == 0 or n % 256 == 0, act 0 / 1 (GELU, erf), residual
+ * (m, n) f32 contiguous or NULL (may be y). */
+int32_t mmr_x3_p8_kpad(int32_t k);
+mmr_status mmr_x3_split_rows(const float* x, int64_t ldx, int64_t m, int32_t k, uint16_t* xs, void* stream);
+mmr_status mmr_x3_linear_p8(const uint16_t* xs, const uint16_t* w3, const float* bias, const float* residual,
+                            float* y, int64_t m, int32_t n, int32_t k, int32_t act, void* stream);
 /* Attention core (nn.MultiheadAttention / BERT self-attention, eval): per (batch, head)
  * softmax(q k^T * scale (+ key mask)) v; rows as mmr_mha (q row bi*lq + i at q + row*ldq + head*dh);
  * mask01 (b, lk) int64 or NULL (0 -> key excluded, HF's additive finfo.min); out (b*lq, ldo) and/or

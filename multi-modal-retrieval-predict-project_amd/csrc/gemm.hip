@@ -583,7 +583,7 @@ __device__ unsigned long long p8_stamps[1024 * 8 * 8 * 4];
 //   LNM = 2: takes the raw y as the residual R and adds LN(y) = gamma (rstd y - rstd mean) + beta
 //            (LV1 = gamma, LV2 = beta over the output columns).
 template <int NT, int ACT, bool HAS_BIAS, bool HAS_RES, bool FP8 = false, bool OUT8 = false, int KNN = 0,
-          int LNM = 0, bool STO = false>
+          int LNM = 0, bool STO = false, bool OF32 = false>
 __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restrict__ X,
                                                        const uint16_t* __restrict__ W,
                                                        const float* __restrict__ bias,
@@ -604,6 +604,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   static_assert((LNM == 0 && !STO) || (!FP8 && !KNN), "LayerNorm fold: bf16 GEMMs");
   static_assert(LNM != 2 || HAS_RES, "LNM = 2 normalises the residual");
   static_assert(!STO || ACT == 0, "row statistics: LDS-staged (non-GELU) epilogue");
+  static_assert(!OF32 || (!FP8 && !OUT8 && !KNN && LNM == 0 && !STO), "f32 output: plain bf16 operands");
   static_assert(KNN == 0 || ((KNN == 2 || KNN == 4) && NT == 4 && !FP8 && !HAS_BIAS && !HAS_RES && ACT == 0),
                 "KNN (rows per unit 2 / 4): plain 256x256 fp16 tiles");
 #if defined(__HIP_DEVICE_COMPILE__)  // buffer-descriptor builtins exist in the device pass only
@@ -625,7 +626,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   // epilogue load retires — vmcnt, in order — behind the next tile's K-tile prefetch).  The tile's
   // first counted wait leaves them in flight (NRES more younger ops).  NT = 4 / FP8 tiles have no
   // registers for them.
-  constexpr bool early_res = HAS_RES && NT == 3 && !FP8 && !(!OUT8 && !KNN && ACT == 1);
+  constexpr bool early_res = HAS_RES && NT == 3 && !FP8 && !OF32 && !(!OUT8 && !KNN && ACT == 1);
   constexpr int NRES = early_res ? (8 / C::RM) * C::CPL : 0;
   static_assert(C::NSTORE_LDS + 13 + NRES <= 63 && C::NSTORE_PL + 5 + NRES <= 63, "vmcnt range");
   // Epilogue: permlane row chunks straight from registers (no LDS round trips) for GELU epilogues,
@@ -634,7 +635,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   // epilogues 3-7 % slower than with the LDS path (QKV 1041 vs 947 TF at 256 x 192: its 16 rows x
   // 64 B stores are twice the L2 write requests of the LDS path's 8 rows x 128 B).  OUT8 / KNN keep
   // their own epilogues.
-  constexpr bool epi_pl = !OUT8 && !KNN && ACT == 1;
+  constexpr bool epi_pl = !OUT8 && !KNN && !OF32 && ACT == 1;
   // (OUT8 + GELU in registers — permlane row chunks quantised after two lane swaps — measured slower
   // than the LDS-staged OUT8 rounds and was removed: profiles/r03_out8_permlane_ab.txt)
 #ifdef MMR_P8_NOSTORE
@@ -645,8 +646,11 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   constexpr bool skip_gm = false;
 #endif
   // STO: 8 more (one row-statistics store per m-tile, lanes fq = 0 — the instruction always issues)
+  // OF32: one 16-B store per (m-tile, n-tile) straight from the accumulators
   constexpr int nstore = skip_st ? 0
-                                 : (skip_gm ? 8 : (epi_pl ? C::NSTORE_PL : C::NSTORE_LDS) + (STO ? 8 : 0));
+                                 : (OF32 ? 8 * NT
+                                         : (skip_gm ? 8 : (epi_pl ? C::NSTORE_PL : C::NSTORE_LDS) + (STO ? 8 : 0)));
+  static_assert(!OF32 || 8 * NT + 5 <= 63, "vmcnt range");
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
 
   const int ntiles = tiles_m * tiles_n;
@@ -1059,8 +1063,34 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
         rb[i] = cf.y;
       }
     }
-    uint2 rq[HAS_RES && !early_res ? 8 : 1][HAS_RES && !early_res ? NT : 1];
-    if constexpr (HAS_RES && !early_res) {
+    if constexpr (OF32) {
+      // f32 output (the x3 towers' K' = 3K split GEMM): lane row 16 i + efr, columns 16 j + 4 efq .. + 3
+      // -> one 16-B store per (i, j), no LDS round; bias, exact-erf GELU (as torch), then the f32 residual
+      // (loaded per m-tile: they retire behind the next tile's prefetch, once per tile)
+      float* Yf = (float*)Y;
+      const float* Rf = (const float*)R;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int64_t row = m0 + wr * 128 + i * 16 + efr;
+        f32x4 rr4[HAS_RES ? NT : 1];
+        if constexpr (HAS_RES) {
+#pragma unroll
+          for (int j = 0; j < NT; ++j) rr4[j] = *(const f32x4*)(Rf + row * N + n0 + wc * 16 * NT + j * 16 + efq * 4);
+        }
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          f32x4 v = acc[i][j] + bq[j];
+          if constexpr (ACT == 1) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = 0.5f * v[e] * (1.0f + erff(v[e] * 0.70710678118654752f));
+          }
+          if constexpr (HAS_RES) v += rr4[j];
+          if (!skip_st) *(f32x4*)(Yf + row * N + n0 + wc * 16 * NT + j * 16 + efq * 4) = v;
+        }
+      }
+    }
+    uint2 rq[HAS_RES && !early_res ? 8 : 1][HAS_RES && !early_res ? NT : 1];  // (unused by OF32)
+    if constexpr (HAS_RES && !early_res && !OF32) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -1120,7 +1150,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
       }
     }
 #pragma unroll
-    for (int rd = 0; rd < (epi_pl ? 0 : 8 / C::RM); ++rd) {  // LDS-staged rounds
+    for (int rd = 0; rd < ((epi_pl || OF32) ? 0 : 8 / C::RM); ++rd) {  // LDS-staged rounds
       if constexpr (early_res) {  // the round's residual chunks -> the wave's LDS area (row layout)
 #pragma unroll
         for (int c = 0; c < C::CPL; ++c) {
@@ -1773,6 +1803,50 @@ void launch_ln(const uint16_t* x, const uint16_t* w, const float* b, const uint1
          P8<NT, false, 0, NV>::LDS_B, st>>>(x, w, b, r, y, m, n, k, tm, tn, nullptr, nullptr, nullptr, nullptr,
                                             nullptr, 0, 0, 0, p8_nt(m, n, 2), nullptr, lc, v1, v2, sp);
 }
+
+// ---- fp32-faithful (x3) linears on the 8-phase GEMM: Y = X W^T + b as ONE K' = 3 kp bf16 GEMM with f32
+// accumulation, X' = [x_hi | x_hi | x_lo] and W' = [w_hi | w_lo | w_hi] (kp = K padded to 128 with zeros):
+// X'.W'^T = x_hi.w_hi + x_hi.w_lo + x_lo.w_hi, the three-term split of csrc/x3.hip at the 8-phase GEMM's
+// rate instead of the 128 x 128 x3_gemm's.  x3_split_rows writes X' (6 bytes per element of x).
+template <bool VEC>
+__global__ __launch_bounds__(256) void x3_split_rows(const float* __restrict__ x, int64_t ldx, int64_t m, int k, int kp,
+                                                     uint16_t* __restrict__ xs) {
+  const int g8 = kp / 8;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= m * g8) return;
+  const int64_t row = t / g8;
+  const int c0 = (int)(t % g8) * 8;
+  const float* xr = x + row * ldx;
+  float v[8];
+  if (VEC && c0 + 8 <= k) {
+    const float4 a = *(const float4*)(xr + c0), b = *(const float4*)(xr + c0 + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = c0 + e < k ? xr[c0 + e] : 0.f;
+  }
+  uint32_t hi[4], lo[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    hi[e] = mmr::pack2bf(v[2 * e], v[2 * e + 1]);
+    lo[e] = mmr::pack2bf(v[2 * e] - __uint_as_float(hi[e] << 16), v[2 * e + 1] - __uint_as_float(hi[e] & 0xFFFF0000u));
+  }
+  uint16_t* o = xs + row * 3 * kp + c0;
+  const uint4 h4 = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+  *(uint4*)o = h4;
+  *(uint4*)(o + kp) = h4;
+  *(uint4*)(o + 2 * kp) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+}
+
+template <int NT, int ACT, bool HB, bool HR>
+void launch_x3p8(const uint16_t* xs, const uint16_t* w3, const float* b, const float* r, float* y, int64_t m, int n,
+                 int k3, hipStream_t st) {
+  const int grid = std::max(8, cu_count() / 8 * 8);
+  const int tm = (int)(m / 256), tn = n / (64 * NT);
+  gemm_bf16_tn_p8<NT, ACT, HB, HR, false, false, 0, 0, false, true>
+      <<<dim3(std::max<int64_t>(8, std::min<int64_t>(grid, (int64_t)tm * tn) / 8 * 8)), dim3(512), P8<NT>::LDS_B, st>>>(
+          xs, w3, b, (const uint16_t*)r, (uint16_t*)y, m, n, k3, tm, tn);
+}
 }  // namespace
 
 namespace {
@@ -1821,6 +1895,58 @@ extern "C" mmr_status mmr_ln_row_coef(const float* stats, int64_t m, int32_t npa
 extern "C" int32_t mmr_linear_bf16_ln_parts(int64_t m, int32_t n, int32_t ln_mode) {
   const int nt = ln_mode == 2 ? (n % 192 == 0 ? 3 : 0) : ln_nt(m, n);
   return nt ? 4 * (n / (64 * nt)) : 0;
+}
+
+extern "C" int32_t mmr_x3_p8_kpad(int32_t k) { return k > 0 && k <= 4096 ? (k + 127) / 128 * 128 : 0; }
+
+extern "C" mmr_status mmr_x3_split_rows(const float* x, int64_t ldx, int64_t m, int32_t k, uint16_t* xs, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && xs, "mmr_x3_split_rows: NULL pointer");
+  const int kp = mmr_x3_p8_kpad(k);
+  MMR_REQUIRE(kp > 0 && m >= 0 && ldx >= k, "mmr_x3_split_rows: m=%lld k=%d ldx=%lld", (long long)m, k, (long long)ldx);
+  if (m == 0) return MMR_OK;
+  const int64_t n8 = m * (kp / 8);
+  const dim3 grid((unsigned)mmr::ceil_div(n8, 256));
+  hipStream_t st = mmr::as_stream(stream);
+  if (((uintptr_t)x & 15) == 0 && ldx % 4 == 0 && k % 8 == 0)
+    x3_split_rows<true><<<grid, 256, 0, st>>>(x, ldx, m, k, kp, xs);
+  else
+    x3_split_rows<false><<<grid, 256, 0, st>>>(x, ldx, m, k, kp, xs);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+extern "C" mmr_status mmr_x3_linear_p8(const uint16_t* xs, const uint16_t* w3, const float* bias, const float* residual,
+                                       float* y, int64_t m, int32_t n, int32_t k, int32_t act, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(xs && w3 && y, "mmr_x3_linear_p8: NULL pointer");
+  const int kp = mmr_x3_p8_kpad(k);
+  MMR_REQUIRE(kp > 0 && m > 0 && m % 256 == 0, "mmr_x3_linear_p8: m=%lld (multiple of 256), k=%d", (long long)m, k);
+  MMR_REQUIRE(n > 0 && (n % 192 == 0 || n % 256 == 0), "mmr_x3_linear_p8: n=%d (multiple of 192 or 256)", n);
+  MMR_REQUIRE(act == 0 || act == 1, "mmr_x3_linear_p8: act=%d", act);
+  // (residual == y is fine: every output element is read, then written, by the one lane that owns it)
+  hipStream_t st = mmr::as_stream(stream);
+  const int nt = n % 192 == 0 && n % 256 == 0 ? ln_nt(m, n) : (n % 256 == 0 ? 4 : 3);
+  const bool hb = bias != nullptr, hr = residual != nullptr;
+#define X3P8(NT_)                                                                                         \
+  do {                                                                                                     \
+    if (act) {                                                                                             \
+      if (hb && hr) launch_x3p8<NT_, 1, true, true>(xs, w3, bias, residual, y, m, n, 3 * kp, st);          \
+      else if (hb) launch_x3p8<NT_, 1, true, false>(xs, w3, bias, residual, y, m, n, 3 * kp, st);          \
+      else if (hr) launch_x3p8<NT_, 1, false, true>(xs, w3, bias, residual, y, m, n, 3 * kp, st);          \
+      else launch_x3p8<NT_, 1, false, false>(xs, w3, bias, residual, y, m, n, 3 * kp, st);                 \
+    } else {                                                                                               \
+      if (hb && hr) launch_x3p8<NT_, 0, true, true>(xs, w3, bias, residual, y, m, n, 3 * kp, st);          \
+      else if (hb) launch_x3p8<NT_, 0, true, false>(xs, w3, bias, residual, y, m, n, 3 * kp, st);          \
+      else if (hr) launch_x3p8<NT_, 0, false, true>(xs, w3, bias, residual, y, m, n, 3 * kp, st);          \
+      else launch_x3p8<NT_, 0, false, false>(xs, w3, bias, residual, y, m, n, 3 * kp, st);                 \
+    }                                                                                                      \
+  } while (0)
+  if (nt == 4) X3P8(4);
+  else X3P8(3);
+#undef X3P8
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
 }
 
 extern "C" mmr_status mmr_linear_bf16_ln(const uint16_t* x, const uint16_t* w, const float* bias,

@@ -403,13 +403,26 @@ def linear_f32(x, w, bias=None, residual=None, act=0, out=None):
 
 class X3W:
     """A per-query linear weight for linear_x3: the f32 weight (kept for the exact-f32 fallback) and its
-    bf16 split hi = bf16(w), lo = bf16(w - hi); (..., cout, cin)."""
-    __slots__ = ("w", "hi", "lo")
+    bf16 split hi = bf16(w), lo = bf16(w - hi); (..., cout, cin).  `w3()`: the 8-phase GEMM image
+    [hi | lo | hi] (each segment kp = mmr_x3_p8_kpad(cin) wide, zero-padded) of a 2-D weight, built on
+    first use (x3_linear)."""
+    __slots__ = ("w", "hi", "lo", "_w3")
 
     def __init__(self, w):
         self.w = w.contiguous()
         self.hi = self.w.to(torch.bfloat16)
         self.lo = (self.w - self.hi.float()).to(torch.bfloat16)
+        self._w3 = None
+
+    def w3(self, kp):
+        if self._w3 is None:
+            n, k = self.w.shape
+            img = torch.zeros((n, 3 * kp), dtype=torch.bfloat16, device=self.w.device)
+            img[:, :k] = self.hi
+            img[:, kp:kp + k] = self.lo
+            img[:, 2 * kp:2 * kp + k] = self.hi
+            self._w3 = img
+        return self._w3
 
 
 def _x3_ok(cin, cout):
@@ -597,7 +610,9 @@ def swin_attn_block(x, pack, bias, ws, shift, eps):
 # f32 activations, every contraction on bf16x3 MFMA (csrc/x3.hip); weights as X3W (hi / lo splits).
 def x3_linear(x, wx, bias=None, residual=None, act=0, out=None):
     """act(x @ w.T + bias) (+ residual) for any number of rows: x (..., K) f32 (last-dim contiguous rows),
-    wx an X3W of w (N, K), K % 32 == 0; residual may be `out`."""
+    wx an X3W of w (N, K), K % 32 == 0; residual may be `out`.  Row counts that fill 256-row tiles with
+    N % 192 or N % 256 == 0 run as one K' = 3 kp split GEMM on the 8-phase kernel (mmr_x3_split_rows +
+    mmr_x3_linear_p8); the rest on mmr_x3_linear (128 x 128 tiles)."""
     _lib.require_gpu(x)
     K = x.shape[-1]
     N, Kw = wx.w.shape
@@ -607,6 +622,14 @@ def x3_linear(x, wx, bias=None, residual=None, act=0, out=None):
     M = x2.shape[0]
     y = out if out is not None else torch.empty(x.shape[:-1] + (N,), dtype=torch.float32, device=x.device)
     r2 = residual.reshape(-1, N) if residual is not None else None
+    kp = _L().mmr_x3_p8_kpad(K)
+    if (M > 0 and M % 256 == 0 and (N % 192 == 0 or N % 256 == 0) and kp > 0 and y.is_contiguous()
+            and (r2 is None or r2.is_contiguous())):
+        xs = torch.empty((M, 3 * kp), dtype=torch.bfloat16, device=x.device)
+        _chk(_L().mmr_x3_split_rows(_lib.ptr(x2), x2.stride(0), M, K, _lib.ptr(xs), _s(x)), "mmr_x3_split_rows")
+        _chk(_L().mmr_x3_linear_p8(_lib.ptr(xs), _lib.ptr(wx.w3(kp)), _lib.ptr(bias), _lib.ptr(r2), _lib.ptr(y), M, N,
+                                   K, act, _s(x)), "mmr_x3_linear_p8")
+        return y
     _chk(_L().mmr_x3_linear(_lib.ptr(x2), x2.stride(0), _lib.ptr(wx.hi), _lib.ptr(wx.lo), _lib.ptr(bias), _lib.ptr(r2),
                             r2.stride(0) if r2 is not None else 0, _lib.ptr(y), N, M, N, K, act, _s(x)),
          "mmr_x3_linear")

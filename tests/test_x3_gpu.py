@@ -46,7 +46,13 @@ def _rel(got, ref):
 @pytest.mark.parametrize("M,N,K,act,bias,res", [(1000, 96, 96, 0, True, False), (513, 2304, 768, 0, True, False),
                                                 (300, 3072, 768, 1, True, False), (257, 768, 3072, 0, True, True),
                                                 (77, 288, 64, 1, True, True), (4096, 200, 384, 0, False, False),
-                                                (20000, 384, 1536, 0, False, False)])
+                                                (20000, 384, 1536, 0, False, False),
+                                                # M % 256 == 0, N % 192 / 256 == 0: the K' = 3 kp split GEMM on the
+                                                # 8-phase kernel (mmr_x3_linear_p8), K padded to 128 where needed
+                                                (4096, 2304, 768, 0, True, False), (2048, 3072, 768, 1, True, False),
+                                                (2048, 768, 3072, 0, True, True), (8192, 384, 96, 1, True, False),
+                                                (4096, 192, 384, 0, False, True), (256, 1152, 200, 0, True, True),
+                                                (65536, 576, 192, 0, True, False)])
 def test_x3_linear_vs_f64(M, N, K, act, bias, res):
     g = torch.Generator().manual_seed(M + N + K)
     x = torch.randn(M, K, generator=g)
@@ -69,6 +75,25 @@ def test_x3_linear_vs_f64(M, N, K, act, bias, res):
     print(json.dumps({"x3_max_err": err.max().item(), "f32_gemm_max_err": (f32.double() - x.double() @ w.double().T)
                       .abs().max().item()}))
     assert (err <= bound).all(), (err - bound).max().item()
+
+
+def test_x3_linear_p8_inplace_residual_and_route():
+    """The split-GEMM route with the residual in place (residual = out, as the towers call it) equals
+    the out-of-place result bit for bit, and agrees with the 128 x 128 x3 kernel (the rows-not-a-
+    multiple-of-256 route) within the split's error."""
+    g = torch.Generator().manual_seed(3)
+    M, N, K = 1024, 768, 768
+    x = torch.randn(M, K, generator=g).to(DEV)
+    wx = ops.X3W((torch.randn(N, K, generator=g) * 0.05).to(DEV))
+    b = torch.randn(N, generator=g).to(DEV)
+    r = torch.randn(M, N, generator=g).to(DEV)
+    y = ops.x3_linear(x, wx, b, residual=r)
+    r2 = r.clone()
+    ops.x3_linear(x, wx, b, residual=r2, out=r2)
+    assert torch.equal(y, r2)
+    # the first M - 1 rows through the 128 x 128 kernel (M - 1 is not a multiple of 256)
+    y_old = ops.x3_linear(x[:M - 1], wx, b, residual=r[:M - 1])
+    assert (y_old - y[:M - 1]).abs().max().item() <= 1e-5 * y.abs().max().item()
 
 
 def _attn_ref(q, k, v, b, lq, lk, heads, dh, scale, mask=None):

@@ -41,7 +41,9 @@ names = ["linear", "layernorm", "add_layernorm", "scaled_add_layernorm", "bert_e
          "swin_window_attention", "patch_im2col", "patch_merge_ln", "swin_head", "mean_tokens", "proj_head",
          "swin_mlp", "swin_attn_block", "linear_f32", "linear_f32_batched", "mha", "add_pos", "ln_rows",
          "assemble_seq", "rows_to_f32", "quantize_mxfp8", "linear_mxfp8", "linear_mxfp8_q8", "layernorm_q8",
-         "linear_rw", "linear_ln", "ln_row_coef", "linear_x3", "linear_x3_batched"]
+         "linear_rw", "linear_ln", "ln_row_coef", "linear_x3", "linear_x3_batched",
+         "x3_linear", "x3_attention", "x3_swin_window_attention", "x3_patch_im2col", "x3_patch_merge_ln",
+         "x3_bert_embed", "x3_add_pos", "x3_assemble_seq", "x3_mean_rows", "x3_gather_rows"]
 
 
 def wrap(name, fn):
@@ -61,12 +63,12 @@ def wrap(name, fn):
             x, pk = a[0], a[1]
             res = (k.get("residual") if "residual" in k else (a[3] if len(a) > 3 else None)) is not None
             key = (name, x.numel() // pk.k, pk.n, pk.k, 0, res)
-        if name in ("linear_ln", "linear_x3"):
+        if name in ("linear_ln", "linear_x3", "x3_linear"):
             x, wt = a[0], a[1]
             K = x.shape[-1]
             n_out = wt.shape[0] if name == "linear_ln" else wt.w.shape[-2]
             key = (name, x.numel() // K, n_out, K, k.get("act", 0),
-                   k.get("ln_mode", 0) if name == "linear_ln" else (k.get("residual") is not None))
+                   k.get("ln_mode", 0) if name == "linear_ln" else (k.get("residual") is not None or len(a) > 3 and a[3] is not None))
         if name == "linear":
             x, wt = a[0], a[1]
             K = x.shape[-1]
