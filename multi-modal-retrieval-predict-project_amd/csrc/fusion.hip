@@ -390,7 +390,7 @@ __global__ __launch_bounds__(256) void add_pos_bf16(const TX* __restrict__ x, co
 // Covers PreFusionEnhancer norm1(alpha*x + x2) (fusion.py:34), ln_img / ln_txt (fusion.py:443,449),
 // norm1_i(joint) + alpha*fused and norm2_i (model.py:437-441).  Row kept in registers
 // (c <= 1024), centred two-pass variance like torch.
-template <typename TI, typename TO>
+template <typename TI, typename TO, int NI = 16>
 __global__ __launch_bounds__(256) void ln_rows(const TI* __restrict__ x, int64_t ldx, const float* __restrict__ a,
                                                const TI* __restrict__ r, int64_t ldr,
                                                const float* __restrict__ g, const float* __restrict__ b,
@@ -412,25 +412,25 @@ __global__ __launch_bounds__(256) void ln_rows(const TI* __restrict__ x, int64_t
   const float av = a ? *a : 1.f;
   // all loads unconditional and issued before any use (index clamped, value masked): a "load if
   // ch < c" branch makes hipcc wait for each load before the next — 16-32 serial round trips
-  float v[16], rv[16];
+  float v[NI], rv[NI];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < NI; ++i) {
     const int ch = lane + 64 * i;
     v[i] = ld(x, row * ldx + (ch < c ? ch : c - 1));
   }
   if (r) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < NI; ++i) {
       const int ch = lane + 64 * i;
       rv[i] = ld(r, row * ldr + (ch < c ? ch : c - 1));
     }
   } else {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) rv[i] = 0.f;
+    for (int i = 0; i < NI; ++i) rv[i] = 0.f;
   }
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < NI; ++i) {
     const float t = av * v[i] + rv[i];
     v[i] = lane + 64 * i < c ? t : 0.f;
     s += v[i];
@@ -438,35 +438,95 @@ __global__ __launch_bounds__(256) void ln_rows(const TI* __restrict__ x, int64_t
   const float mean = mmr::wave_sum(s) / c;
   float ss = 0.f;
 #pragma unroll
-  for (int i = 0; i < 16; ++i)
+  for (int i = 0; i < NI; ++i)
     if (lane + 64 * i < c) ss += (v[i] - mean) * (v[i] - mean);
   const float rstd = rsqrtf(mmr::wave_sum(ss) / c + eps);
   const float pv = ps ? *ps : 1.f;
-  float gv[16], bv[16], pp[16];
+  float gv[NI], bv[NI], pp[NI];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < NI; ++i) {
     const int ch = lane + 64 * i, chc = ch < c ? ch : c - 1;
     gv[i] = g[chc];
     bv[i] = b[chc];
   }
   if (post) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < NI; ++i) {
       const int ch = lane + 64 * i;
       pp[i] = pv * post[row * ldp + (ch < c ? ch : c - 1)];
     }
   } else {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) pp[i] = 0.f;
+    for (int i = 0; i < NI; ++i) pp[i] = 0.f;
   }
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < NI; ++i) {
     const int ch = lane + 64 * i;
     const float t = (v[i] - mean) * rstd * gv[i] + bv[i] + pp[i];
     if (ch < c) {
       if constexpr (sizeof(TO) == 4) ((float*)y)[row * ldy + ch] = t;
       else ((uint16_t*)y)[row * ldy + ch] = f2bf(t);
     }
+  }
+}
+
+// f32 rows with c % (64 VW) == 0 and VW-aligned rows (the x3 towers' LayerNorms, c = 384 ... 1024): the
+// same arithmetic as ln_rows<float, float> with VW-wide loads / stores (lane owns channels
+// VW lane + 64 VW i ...), so a row moves in c / (64 VW) instructions per operand instead of 16
+template <int VW>
+__global__ __launch_bounds__(256) void ln_rows_v(const float* __restrict__ x, int64_t ldx, const float* __restrict__ a,
+                                                 const float* __restrict__ r, int64_t ldr, const float* __restrict__ g,
+                                                 const float* __restrict__ b, const float* __restrict__ post, int64_t ldp,
+                                                 const float* __restrict__ ps, float* __restrict__ y, int64_t ldy,
+                                                 int64_t rows, int c, float eps, int groups, int64_t gdiv) {
+  typedef float fv_t __attribute__((ext_vector_type(VW)));
+  constexpr int NI = 1024 / (64 * VW);
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int grp = (int)((row / gdiv) % groups);
+  g += (int64_t)grp * c;
+  b += (int64_t)grp * c;
+  if (a) a += grp;
+  if (ps) ps += grp;
+  const int ni = c / (64 * VW);  // wave-uniform
+  const float av = a ? *a : 1.f;
+  auto ofs = [&](int i) { return VW * lane + 64 * VW * (i < ni ? i : ni - 1); };  // clamped: loads unconditional
+  fv_t v[NI], rv[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) v[i] = *(const fv_t*)(x + row * ldx + ofs(i));
+  if (r) {  // (the residual loads in one uniform branch, issued back to back)
+#pragma unroll
+    for (int i = 0; i < NI; ++i) rv[i] = *(const fv_t*)(r + row * ldr + ofs(i));
+  } else {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) rv[i] = (fv_t)0.f;
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    v[i] = i < ni ? av * v[i] + rv[i] : (fv_t)0.f;
+#pragma unroll
+    for (int e = 0; e < VW; ++e) s += v[i][e];
+  }
+  const float mean = mmr::wave_sum(s) / c;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+    if (i < ni)
+#pragma unroll
+      for (int e = 0; e < VW; ++e) ss += (v[i][e] - mean) * (v[i][e] - mean);
+  const float rstd = rsqrtf(mmr::wave_sum(ss) / c + eps);
+  const float pv = ps ? *ps : 1.f;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    if (i >= ni) break;
+    const fv_t gv = *(const fv_t*)(g + ofs(i)), bv = *(const fv_t*)(b + ofs(i));
+    const fv_t pp = post ? pv * *(const fv_t*)(post + row * ldp + ofs(i)) : (fv_t)0.f;
+    fv_t t;
+#pragma unroll
+    for (int e = 0; e < VW; ++e) t[e] = (v[i][e] - mean) * rstd * gv[e] + bv[e] + pp[e];
+    *(fv_t*)(y + row * ldy + ofs(i)) = t;
   }
 }
 
@@ -692,14 +752,42 @@ mmr_status mmr_ln_rows(const void* x, int64_t ldx, const float* alpha, const voi
   if (rows == 0) return MMR_OK;
   const dim3 grid((unsigned)mmr::ceil_div(rows, 4));
   hipStream_t st = mmr::as_stream(stream);
+  // the scalar forms load ceil(c / 64) channels per lane (NI), not 16: at c = 96 / 192 the clamped
+  // duplicate loads of a fixed 16 were most of the instructions
+  const int ni = (c + 63) / 64;
+#define LNS(TI_, NI_)                                                                                            \
+  ln_rows<TI_, TI_, NI_><<<grid, 256, 0, st>>>((const TI_*)x, ldx, alpha, (const TI_*)residual, ldr, gamma, beta, \
+                                               post, ldp, post_scale, (TI_*)y, ldy, rows, c, eps, groups, group_div)
+#define LNS_DISPATCH(TI_)                        \
+  do {                                           \
+    if (ni <= 2) LNS(TI_, 2);                    \
+    else if (ni <= 3) LNS(TI_, 3);               \
+    else if (ni <= 4) LNS(TI_, 4);               \
+    else if (ni <= 6) LNS(TI_, 6);               \
+    else if (ni <= 8) LNS(TI_, 8);               \
+    else if (ni <= 12) LNS(TI_, 12);             \
+    else LNS(TI_, 16);                           \
+  } while (0)
   if (io_bf16)
-    ln_rows<uint16_t, uint16_t><<<grid, 256, 0, st>>>((const uint16_t*)x, ldx, alpha, (const uint16_t*)residual, ldr,
-                                                      gamma, beta, post, ldp, post_scale, (uint16_t*)y, ldy, rows, c, eps,
-                                                      groups, group_div);
-  else
-    ln_rows<float, float><<<grid, 256, 0, st>>>((const float*)x, ldx, alpha, (const float*)residual, ldr, gamma, beta,
-                                                post, ldp, post_scale, (float*)y, ldy, rows, c, eps, groups,
-                                                group_div);
+    LNS_DISPATCH(uint16_t);
+  else {
+    auto al = [](const void* p, int64_t ld, int vw) {
+      return p == nullptr || (((uintptr_t)p & (4 * vw - 1)) == 0 && ld % vw == 0);
+    };
+    auto ok = [&](int vw) {
+      return c % (64 * vw) == 0 && al(x, ldx, vw) && al(residual, ldr, vw) && al(post, ldp, vw) && al(y, ldy, vw) &&
+             al(gamma, 0, vw) && al(beta, 0, vw);
+    };
+#define LNV(VW_)                                                                                                  \
+  ln_rows_v<VW_><<<grid, 256, 0, st>>>((const float*)x, ldx, alpha, (const float*)residual, ldr, gamma, beta, post, \
+                                       ldp, post_scale, (float*)y, ldy, rows, c, eps, groups, group_div)
+    if (ok(4)) LNV(4);
+    else if (ok(2)) LNV(2);
+    else LNS_DISPATCH(float);
+#undef LNV
+  }
+#undef LNS_DISPATCH
+#undef LNS
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }

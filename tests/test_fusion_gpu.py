@@ -146,6 +146,24 @@ def test_ln_rows(dtype):
         assert rel_err(y, F.layer_norm(x, (768,), ga, be, 1e-5) + 1.3 * post) < 1e-5
 
 
+@pytest.mark.parametrize("c,ld,groups", [(768, 768, 1), (384, 384, 3), (1024, 1024, 1), (96, 96, 1), (768, 770, 2),
+                                         (256, 258, 1)])
+def test_ln_rows_f32_widths(c, ld, groups):
+    """f32 rows at the widths the vector forms take (c % 256: 4-wide, c % 128: 2-wide) and the scalar form
+    (c = 96, or rows at an odd stride), grouped parameters, residual + post: vs torch fp32 within 1e-5."""
+    g = torch.Generator().manual_seed(c + ld + groups)
+    rows = 6 * groups
+    xb = torch.randn(rows, ld, generator=g)
+    x, r, post = xb[:, :c], torch.randn(rows, c, generator=g), torch.randn(rows, c, generator=g)
+    ga, be = 1 + 0.1 * torch.randn(groups, c, generator=g), 0.1 * torch.randn(groups, c, generator=g)
+    a, ps = 0.5 + torch.rand(groups, generator=g), torch.rand(groups, generator=g)
+    y = ops.ln_rows(xb.to(DEV)[:, :c], ga.to(DEV), be.to(DEV), 1e-5, alpha=a.to(DEV), residual=r.to(DEV),
+                    post=post.to(DEV), post_scale=ps.to(DEV), groups=groups)
+    gi = torch.arange(rows) % groups
+    ref = F.layer_norm(a[gi, None] * x + r, (c,), None, None, 1e-5) * ga[gi] + be[gi] + ps[gi, None] * post
+    assert rel_err(y, ref) < 1e-5
+
+
 def test_add_pos_and_assemble():
     g = torch.Generator().manual_seed(9)
     x = torch.randn(3, 49, 96, generator=g)
