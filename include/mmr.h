@@ -491,10 +491,12 @@ mmr_status mmr_x3_linear(const float* x, int64_t ldx, const uint16_t* w_hi, cons
  * X' = [x_hi | x_hi | x_lo], W' = [w_hi | w_lo | w_hi], each segment kp = mmr_x3_p8_kpad(k) wide (k
  * rounded up to 128, zero padding; 0 = k not taken), so X'.W'^T = x_hi.w_hi + x_hi.w_lo + x_lo.w_hi.
  * mmr_x3_split_rows writes X' ([m][3 kp] bf16, caller-allocated) from x rows at stride ldx;
- * mmr_x3_linear_p8 takes X' and the weight image W' ([n][3 kp] bf16, built once at load) and writes
- * y (m, n) f32 contiguous: m % 256 == 0, n % 192 == 0 or n % 256 == 0, act 0 / 1 (GELU, erf), residual
- * (m, n) f32 contiguous or NULL (may be y). */
+ * mmr_x3_linear_p8 takes X' and the weight image W' ([npad][3 kp] bf16, built once at load, npad =
+ * mmr_x3_p8_npad(n): n itself when it is a multiple of 192 or 256, else n rounded up to 192 with zero
+ * rows; 0 = n not taken) and writes y (m, n) f32 contiguous: m % 256 == 0, act 0 / 1 (GELU, erf), bias
+ * NULL or npad floats (zero-padded), residual (m, n) f32 contiguous or NULL (may be y). */
 int32_t mmr_x3_p8_kpad(int32_t k);
+int32_t mmr_x3_p8_npad(int32_t n);
 mmr_status mmr_x3_split_rows(const float* x, int64_t ldx, int64_t m, int32_t k, uint16_t* xs, void* stream);
 mmr_status mmr_x3_linear_p8(const uint16_t* xs, const uint16_t* w3, const float* bias, const float* residual,
                             float* y, int64_t m, int32_t n, int32_t k, int32_t act, void* stream);

@@ -599,7 +599,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
                                                        const float* __restrict__ LC = nullptr,
                                                        const float* __restrict__ LV1 = nullptr,
                                                        const float* __restrict__ LV2 = nullptr,
-                                                       float* __restrict__ SP = nullptr) {
+                                                       float* __restrict__ SP = nullptr, int ldn = 0) {
   static_assert(!OUT8 || (FP8 && NT == 4 && !HAS_RES), "OUT8: MX-fp8 256x256 tiles without residual");
   static_assert((LNM == 0 && !STO) || (!FP8 && !KNN), "LayerNorm fold: bf16 GEMMs");
   static_assert(LNM != 2 || HAS_RES, "LNM = 2 normalises the residual");
@@ -1067,15 +1067,28 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
       // f32 output (the x3 towers' K' = 3K split GEMM): lane row 16 i + efr, columns 16 j + 4 efq .. + 3
       // -> one 16-B store per (i, j), no LDS round; bias, exact-erf GELU (as torch), then the f32 residual
       // (loaded per m-tile: they retire behind the next tile's prefetch, once per tile)
-      float* Yf = (float*)Y;
-      const float* Rf = (const float*)R;
+      // Y / R are [M][ldn] f32 with ldn <= N (N = the weight image's rows, padded to whole tiles): the
+      // tile's 256 rows as one buffer (64-bit base in SGPRs, 32-bit offsets), columns >= ldn get an
+      // offset past num_records — the store is dropped and the load returns 0 by the buffer range check,
+      // while the instruction still issues, so the next tile's counted wait stays exact
+      const int64_t tb = m0 * ldn * 4;
+      const uint32_t nrec = (uint32_t)(256 * ldn * 4);
+      const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)((char*)Y + tb), 0, (int)nrec, 0x00020000);
+      const auto rr = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)R + (HAS_RES ? tb : 0)), 0, (int)nrec,
+                                                        0x00020000);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const int64_t row = m0 + wr * 128 + i * 16 + efr;
+        const int rl = wr * 128 + i * 16 + efr;  // row in the tile
+        uint32_t off[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int col = n0 + wc * 16 * NT + j * 16 + efq * 4;
+          off[j] = col < ldn ? (uint32_t)((rl * ldn + col) * 4) : 0x7FFFFFF0u;
+        }
         f32x4 rr4[HAS_RES ? NT : 1];
         if constexpr (HAS_RES) {
 #pragma unroll
-          for (int j = 0; j < NT; ++j) rr4[j] = *(const f32x4*)(Rf + row * N + n0 + wc * 16 * NT + j * 16 + efq * 4);
+          for (int j = 0; j < NT; ++j) rr4[j] = __builtin_amdgcn_raw_buffer_load_b128(rr, off[j], 0, 0);
         }
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
@@ -1085,7 +1098,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
             for (int e = 0; e < 4; ++e) v[e] = 0.5f * v[e] * (1.0f + erff(v[e] * 0.70710678118654752f));
           }
           if constexpr (HAS_RES) v += rr4[j];
-          if (!skip_st) *(f32x4*)(Yf + row * N + n0 + wc * 16 * NT + j * 16 + efq * 4) = v;
+          if (!skip_st) __builtin_amdgcn_raw_buffer_store_b128(v, ry, off[j], 0, 0);
         }
       }
     }
@@ -1839,13 +1852,14 @@ __global__ __launch_bounds__(256) void x3_split_rows(const float* __restrict__ x
 }
 
 template <int NT, int ACT, bool HB, bool HR>
-void launch_x3p8(const uint16_t* xs, const uint16_t* w3, const float* b, const float* r, float* y, int64_t m, int n,
-                 int k3, hipStream_t st) {
+void launch_x3p8(const uint16_t* xs, const uint16_t* w3, const float* b, const float* r, float* y, int64_t m, int npad,
+                 int n, int k3, hipStream_t st) {
   const int grid = std::max(8, cu_count() / 8 * 8);
-  const int tm = (int)(m / 256), tn = n / (64 * NT);
+  const int tm = (int)(m / 256), tn = npad / (64 * NT);
   gemm_bf16_tn_p8<NT, ACT, HB, HR, false, false, 0, 0, false, true>
       <<<dim3(std::max<int64_t>(8, std::min<int64_t>(grid, (int64_t)tm * tn) / 8 * 8)), dim3(512), P8<NT>::LDS_B, st>>>(
-          xs, w3, b, (const uint16_t*)r, (uint16_t*)y, m, n, k3, tm, tn);
+          xs, w3, b, (const uint16_t*)r, (uint16_t*)y, m, npad, k3, tm, tn, nullptr, nullptr, nullptr, nullptr, nullptr,
+          0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, n);
 }
 }  // namespace
 
@@ -1899,6 +1913,11 @@ extern "C" int32_t mmr_linear_bf16_ln_parts(int64_t m, int32_t n, int32_t ln_mod
 
 extern "C" int32_t mmr_x3_p8_kpad(int32_t k) { return k > 0 && k <= 4096 ? (k + 127) / 128 * 128 : 0; }
 
+extern "C" int32_t mmr_x3_p8_npad(int32_t n) {
+  if (n <= 0 || n > 16384 || n % 4) return 0;
+  return n % 192 == 0 || n % 256 == 0 ? n : (n + 191) / 192 * 192;
+}
+
 extern "C" mmr_status mmr_x3_split_rows(const float* x, int64_t ldx, int64_t m, int32_t k, uint16_t* xs, void* stream) {
   mmr::clear_error();
   MMR_REQUIRE(x && xs, "mmr_x3_split_rows: NULL pointer");
@@ -1922,24 +1941,25 @@ extern "C" mmr_status mmr_x3_linear_p8(const uint16_t* xs, const uint16_t* w3, c
   MMR_REQUIRE(xs && w3 && y, "mmr_x3_linear_p8: NULL pointer");
   const int kp = mmr_x3_p8_kpad(k);
   MMR_REQUIRE(kp > 0 && m > 0 && m % 256 == 0, "mmr_x3_linear_p8: m=%lld (multiple of 256), k=%d", (long long)m, k);
-  MMR_REQUIRE(n > 0 && (n % 192 == 0 || n % 256 == 0), "mmr_x3_linear_p8: n=%d (multiple of 192 or 256)", n);
+  const int npad = mmr_x3_p8_npad(n);
+  MMR_REQUIRE(npad > 0, "mmr_x3_linear_p8: n=%d (multiple of 4, <= 16384)", n);
   MMR_REQUIRE(act == 0 || act == 1, "mmr_x3_linear_p8: act=%d", act);
   // (residual == y is fine: every output element is read, then written, by the one lane that owns it)
   hipStream_t st = mmr::as_stream(stream);
-  const int nt = n % 192 == 0 && n % 256 == 0 ? ln_nt(m, n) : (n % 256 == 0 ? 4 : 3);
+  const int nt = npad % 192 == 0 && npad % 256 == 0 ? ln_nt(m, npad) : (npad % 256 == 0 ? 4 : 3);
   const bool hb = bias != nullptr, hr = residual != nullptr;
 #define X3P8(NT_)                                                                                         \
   do {                                                                                                     \
     if (act) {                                                                                             \
-      if (hb && hr) launch_x3p8<NT_, 1, true, true>(xs, w3, bias, residual, y, m, n, 3 * kp, st);          \
-      else if (hb) launch_x3p8<NT_, 1, true, false>(xs, w3, bias, residual, y, m, n, 3 * kp, st);          \
-      else if (hr) launch_x3p8<NT_, 1, false, true>(xs, w3, bias, residual, y, m, n, 3 * kp, st);          \
-      else launch_x3p8<NT_, 1, false, false>(xs, w3, bias, residual, y, m, n, 3 * kp, st);                 \
+      if (hb && hr) launch_x3p8<NT_, 1, true, true>(xs, w3, bias, residual, y, m, npad, n, 3 * kp, st);          \
+      else if (hb) launch_x3p8<NT_, 1, true, false>(xs, w3, bias, residual, y, m, npad, n, 3 * kp, st);          \
+      else if (hr) launch_x3p8<NT_, 1, false, true>(xs, w3, bias, residual, y, m, npad, n, 3 * kp, st);          \
+      else launch_x3p8<NT_, 1, false, false>(xs, w3, bias, residual, y, m, npad, n, 3 * kp, st);                 \
     } else {                                                                                               \
-      if (hb && hr) launch_x3p8<NT_, 0, true, true>(xs, w3, bias, residual, y, m, n, 3 * kp, st);          \
-      else if (hb) launch_x3p8<NT_, 0, true, false>(xs, w3, bias, residual, y, m, n, 3 * kp, st);          \
-      else if (hr) launch_x3p8<NT_, 0, false, true>(xs, w3, bias, residual, y, m, n, 3 * kp, st);          \
-      else launch_x3p8<NT_, 0, false, false>(xs, w3, bias, residual, y, m, n, 3 * kp, st);                 \
+      if (hb && hr) launch_x3p8<NT_, 0, true, true>(xs, w3, bias, residual, y, m, npad, n, 3 * kp, st);          \
+      else if (hb) launch_x3p8<NT_, 0, true, false>(xs, w3, bias, residual, y, m, npad, n, 3 * kp, st);          \
+      else if (hr) launch_x3p8<NT_, 0, false, true>(xs, w3, bias, residual, y, m, npad, n, 3 * kp, st);          \
+      else launch_x3p8<NT_, 0, false, false>(xs, w3, bias, residual, y, m, npad, n, 3 * kp, st);                 \
     }                                                                                                      \
   } while (0)
   if (nt == 4) X3P8(4);

@@ -406,23 +406,35 @@ class X3W:
     bf16 split hi = bf16(w), lo = bf16(w - hi); (..., cout, cin).  `w3()`: the 8-phase GEMM image
     [hi | lo | hi] (each segment kp = mmr_x3_p8_kpad(cin) wide, zero-padded) of a 2-D weight, built on
     first use (x3_linear)."""
-    __slots__ = ("w", "hi", "lo", "_w3")
+    __slots__ = ("w", "hi", "lo", "_w3", "_bpad")
 
     def __init__(self, w):
         self.w = w.contiguous()
         self.hi = self.w.to(torch.bfloat16)
         self.lo = (self.w - self.hi.float()).to(torch.bfloat16)
         self._w3 = None
+        self._bpad = None
 
-    def w3(self, kp):
+    def w3(self, kp, npad):
+        """[npad][3 kp] bf16: rows n.. npad - 1 and each segment's columns k.. kp - 1 zero."""
         if self._w3 is None:
             n, k = self.w.shape
-            img = torch.zeros((n, 3 * kp), dtype=torch.bfloat16, device=self.w.device)
-            img[:, :k] = self.hi
-            img[:, kp:kp + k] = self.lo
-            img[:, 2 * kp:2 * kp + k] = self.hi
+            img = torch.zeros((npad, 3 * kp), dtype=torch.bfloat16, device=self.w.device)
+            img[:n, :k] = self.hi
+            img[:n, kp:kp + k] = self.lo
+            img[:n, 2 * kp:2 * kp + k] = self.hi
             self._w3 = img
         return self._w3
+
+    def bias_padded(self, bias, npad):
+        """bias zero-padded to npad entries (cached for the last bias seen)."""
+        if bias is None or bias.shape[0] == npad:
+            return bias
+        if self._bpad is None or self._bpad[0] is not bias:
+            bp = torch.zeros(npad, dtype=torch.float32, device=bias.device)
+            bp[:bias.shape[0]] = bias
+            self._bpad = (bias, bp)
+        return self._bpad[1]
 
 
 def _x3_ok(cin, cout):
@@ -611,8 +623,8 @@ def swin_attn_block(x, pack, bias, ws, shift, eps):
 def x3_linear(x, wx, bias=None, residual=None, act=0, out=None):
     """act(x @ w.T + bias) (+ residual) for any number of rows: x (..., K) f32 (last-dim contiguous rows),
     wx an X3W of w (N, K), K % 32 == 0; residual may be `out`.  Row counts that fill 256-row tiles with
-    N % 192 or N % 256 == 0 run as one K' = 3 kp split GEMM on the 8-phase kernel (mmr_x3_split_rows +
-    mmr_x3_linear_p8); the rest on mmr_x3_linear (128 x 128 tiles)."""
+    N >= 192 run as one K' = 3 kp split GEMM on the 8-phase kernel (mmr_x3_split_rows +
+    mmr_x3_linear_p8, N padded to whole tiles); the rest on mmr_x3_linear (128 x 128 tiles)."""
     _lib.require_gpu(x)
     K = x.shape[-1]
     N, Kw = wx.w.shape
@@ -622,13 +634,15 @@ def x3_linear(x, wx, bias=None, residual=None, act=0, out=None):
     M = x2.shape[0]
     y = out if out is not None else torch.empty(x.shape[:-1] + (N,), dtype=torch.float32, device=x.device)
     r2 = residual.reshape(-1, N) if residual is not None else None
-    kp = _L().mmr_x3_p8_kpad(K)
-    if (M > 0 and M % 256 == 0 and (N % 192 == 0 or N % 256 == 0) and kp > 0 and y.is_contiguous()
+    kp, npad = _L().mmr_x3_p8_kpad(K), _L().mmr_x3_p8_npad(N)
+    # (N < 192: the split pass, 6 bytes written per element of x, costs more than the GEMM saves —
+    # Swin stage-1 fc2, N = 96 K = 384: 0.96 -> 1.11 ms per call)
+    if (M > 0 and M % 256 == 0 and N >= 192 and kp > 0 and npad > 0 and y.is_contiguous()
             and (r2 is None or r2.is_contiguous())):
         xs = torch.empty((M, 3 * kp), dtype=torch.bfloat16, device=x.device)
         _chk(_L().mmr_x3_split_rows(_lib.ptr(x2), x2.stride(0), M, K, _lib.ptr(xs), _s(x)), "mmr_x3_split_rows")
-        _chk(_L().mmr_x3_linear_p8(_lib.ptr(xs), _lib.ptr(wx.w3(kp)), _lib.ptr(bias), _lib.ptr(r2), _lib.ptr(y), M, N,
-                                   K, act, _s(x)), "mmr_x3_linear_p8")
+        _chk(_L().mmr_x3_linear_p8(_lib.ptr(xs), _lib.ptr(wx.w3(kp, npad)), _lib.ptr(wx.bias_padded(bias, npad)),
+                                   _lib.ptr(r2), _lib.ptr(y), M, N, K, act, _s(x)), "mmr_x3_linear_p8")
         return y
     _chk(_L().mmr_x3_linear(_lib.ptr(x2), x2.stride(0), _lib.ptr(wx.hi), _lib.ptr(wx.lo), _lib.ptr(bias), _lib.ptr(r2),
                             r2.stride(0) if r2 is not None else 0, _lib.ptr(y), N, M, N, K, act, _s(x)),
