@@ -177,8 +177,10 @@ struct AttnArgs {
   int hw, ws, shift;  // Swin windows
 };
 
-template <int DT, bool SWIN>
+template <int DT, bool SWIN, int QTW = 1>
 __global__ __launch_bounds__(256) void x3_attention(const AttnArgs a) {
+  // QTW query tiles of 64 rows per pass (wave w owns rows 64 u + 16 w ..): each staged key chunk serves
+  // QTW tiles (lq <= 128 with QTW = 2: K / V split and staged once instead of twice)
   constexpr int DH = 32 * DT, KLD = DH + 8, VLD = 72;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* sKh = (uint16_t*)smem;
@@ -225,11 +227,13 @@ __global__ __launch_bounds__(256) void x3_attention(const AttnArgs a) {
   for (int nd = 0; nd < 2 * DT; ++nd) macc[nd] = 0.f;
   uint16_t* pH = sPh + wave * 16 * VLD;
   uint16_t* pL = sPl + wave * 16 * VLD;
-  for (int q0 = 0; q0 < lq; q0 += 64) {
-    const int qbase = q0 + wave * 16;
-    bf16x8 qh[DT], ql[DT];
-    {
-      const int qi = qbase + r < lq ? qbase + r : lq - 1;
+  for (int q0 = 0; q0 < lq; q0 += 64 * QTW) {
+    int qbase[QTW];
+    bf16x8 qh[QTW][DT], ql[QTW][DT];
+#pragma unroll
+    for (int u = 0; u < QTW; ++u) {
+      qbase[u] = q0 + 64 * u + wave * 16;
+      const int qi = qbase[u] + r < lq ? qbase[u] + r : lq - 1;
       const float* qp = qb + qtok(qi) * a.ldq;
 #pragma unroll
       for (int ks = 0; ks < DT; ++ks) {
@@ -241,18 +245,21 @@ __global__ __launch_bounds__(256) void x3_attention(const AttnArgs a) {
           x0 = make_float4(x0.x * a.scale, x0.y * a.scale, x0.z * a.scale, x0.w * a.scale);
           x1 = make_float4(x1.x * a.scale, x1.y * a.scale, x1.z * a.scale, x1.w * a.scale);
         }
-        split8(x0, x1, qh[ks], ql[ks]);
+        split8(x0, x1, qh[u][ks], ql[u][ks]);
       }
     }
-    float mrow[4], lrow[4];
-    f32x4 o[2 * DT];
+    float mrow[QTW][4], lrow[QTW][4];
+    f32x4 o[QTW][2 * DT];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      mrow[i] = -INFINITY;
-      lrow[i] = 0.f;
+    for (int u = 0; u < QTW; ++u) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        mrow[u][i] = -INFINITY;
+        lrow[u][i] = 0.f;
+      }
+#pragma unroll
+      for (int nd = 0; nd < 2 * DT; ++nd) o[u][nd] = (f32x4){0.f, 0.f, 0.f, 0.f};
     }
-#pragma unroll
-    for (int nd = 0; nd < 2 * DT; ++nd) o[nd] = (f32x4){0.f, 0.f, 0.f, 0.f};
     for (int kc = 0; kc < lk; kc += 64) {
       __syncthreads();  // every wave done with the previous chunk's K / V
       for (int e = t; e < 64 * (DH / 4); e += 256) {
@@ -278,102 +285,108 @@ __global__ __launch_bounds__(256) void x3_attention(const AttnArgs a) {
         sVl[(d + 3) * VLD + key] = (uint16_t)(l.y >> 16);
       }
       __syncthreads();
-      f32x4 s[4];
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        s[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int u = 0; u < QTW; ++u) {
+        f32x4 s[4];
 #pragma unroll
-        for (int ks = 0; ks < DT; ++ks) {
-          const bf16x8 khv = *(const bf16x8*)(sKh + (16 * n + r) * KLD + 32 * ks + 8 * g);
-          const bf16x8 klv = *(const bf16x8*)(sKl + (16 * n + r) * KLD + 32 * ks + 8 * g);
-          s[n] = mfma3(qh[ks], ql[ks], khv, klv, s[n]);
+        for (int n = 0; n < 4; ++n) {
+          s[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < DT; ++ks) {
+            const bf16x8 khv = *(const bf16x8*)(sKh + (16 * n + r) * KLD + 32 * ks + 8 * g);
+            const bf16x8 klv = *(const bf16x8*)(sKl + (16 * n + r) * KLD + 32 * ks + 8 * g);
+            s[n] = mfma3(qh[u][ks], ql[u][ks], khv, klv, s[n]);
+          }
         }
-      }
-      // scale / bias / mask, then the online softmax update per query row 4 g + i
+        // scale / bias / mask, then the online softmax update per query row 4 g + i
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int key = kc + 16 * n + r;
-        bool valid = key < lk;
-        if (!SWIN && a.kmask) valid = valid && a.kmask[bb * lk + (valid ? key : 0)] != 0;
+        for (int n = 0; n < 4; ++n) {
+          const int key = kc + 16 * n + r;
+          bool valid = key < lk;
+          if (!SWIN && a.kmask) valid = valid && a.kmask[bb * lk + (valid ? key : 0)] != 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float x = s[n][i];
+            if constexpr (SWIN) {
+              const int qi = qbase[u] + 4 * g + i;
+              x += a.bias[(((int64_t)type * a.heads + head) * 64 + (qi < 64 ? qi : 63)) * 64 + (key < 64 ? key : 63)];
+            } else {
+              x *= a.scale;
+            }
+            s[n][i] = valid ? x : -INFINITY;
+          }
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          float x = s[n][i];
-          if constexpr (SWIN) {
-            const int qi = qbase + 4 * g + i;
-            x += a.bias[(((int64_t)type * a.heads + head) * 64 + (qi < 64 ? qi : 63)) * 64 + (key < 64 ? key : 63)];
+          float cm = fmaxf(fmaxf(s[0][i], s[1][i]), fmaxf(s[2][i], s[3][i]));
+#pragma unroll
+          for (int m = 1; m < 16; m <<= 1) cm = fmaxf(cm, __shfl_xor(cm, m, 64));
+          const float mnew = fmaxf(mrow[u][i], cm);
+          float corr = 1.f, ps = 0.f;
+          if (mnew != -INFINITY) {
+            corr = mrow[u][i] == -INFINITY ? 0.f : expf(mrow[u][i] - mnew);
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+              const float p = s[n][i] == -INFINITY ? 0.f : expf(s[n][i] - mnew);
+              s[n][i] = p;
+              ps += p;
+            }
           } else {
-            x *= a.scale;
+#pragma unroll
+            for (int n = 0; n < 4; ++n) s[n][i] = 0.f;
           }
-          s[n][i] = valid ? x : -INFINITY;
+#pragma unroll
+          for (int m = 1; m < 16; m <<= 1) ps += __shfl_xor(ps, m, 64);
+          lrow[u][i] = lrow[u][i] * corr + ps;
+          mrow[u][i] = mnew;
+#pragma unroll
+          for (int nd = 0; nd < 2 * DT; ++nd) o[u][nd][i] *= corr;
         }
+        // P (f32) -> hi / lo through the wave's LDS tile
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float p = s[n][i];
+            const uint16_t h = mmr::f2bf(p);
+            const uint16_t l = mmr::f2bf(p - mmr::bf2f(h));
+            pH[(4 * g + i) * VLD + 16 * n + r] = h;
+            pL[(4 * g + i) * VLD + 16 * n + r] = l;
+          }
+        __syncthreads();
+#pragma unroll
+        for (int ks2 = 0; ks2 < 2; ++ks2) {
+          const bf16x8 pah = *(const bf16x8*)(pH + r * VLD + 32 * ks2 + 8 * g);
+          const bf16x8 pal = *(const bf16x8*)(pL + r * VLD + 32 * ks2 + 8 * g);
+#pragma unroll
+          for (int nd = 0; nd < 2 * DT; ++nd) {
+            const bf16x8 vbh = *(const bf16x8*)(sVh + (16 * nd + r) * VLD + 32 * ks2 + 8 * g);
+            const bf16x8 vbl = *(const bf16x8*)(sVl + (16 * nd + r) * VLD + 32 * ks2 + 8 * g);
+            o[u][nd] = mfma3(pah, pal, vbh, vbl, o[u][nd]);
+          }
+        }
+        if (QTW > 1) __syncthreads();  // the wave's P tile is rewritten by the next query tile
       }
+    }
+    // finalise these query tiles: O / l (a row with every key masked -> 0)
+#pragma unroll
+    for (int u = 0; u < QTW; ++u)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float cm = fmaxf(fmaxf(s[0][i], s[1][i]), fmaxf(s[2][i], s[3][i]));
-#pragma unroll
-        for (int m = 1; m < 16; m <<= 1) cm = fmaxf(cm, __shfl_xor(cm, m, 64));
-        const float mnew = fmaxf(mrow[i], cm);
-        float corr = 1.f, ps = 0.f;
-        if (mnew != -INFINITY) {
-          corr = mrow[i] == -INFINITY ? 0.f : expf(mrow[i] - mnew);
-#pragma unroll
-          for (int n = 0; n < 4; ++n) {
-            const float p = s[n][i] == -INFINITY ? 0.f : expf(s[n][i] - mnew);
-            s[n][i] = p;
-            ps += p;
-          }
-        } else {
-#pragma unroll
-          for (int n = 0; n < 4; ++n) s[n][i] = 0.f;
-        }
-#pragma unroll
-        for (int m = 1; m < 16; m <<= 1) ps += __shfl_xor(ps, m, 64);
-        lrow[i] = lrow[i] * corr + ps;
-        mrow[i] = mnew;
-#pragma unroll
-        for (int nd = 0; nd < 2 * DT; ++nd) o[nd][i] *= corr;
-      }
-      // P (f32) -> hi / lo through the wave's LDS tile
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float p = s[n][i];
-          const uint16_t h = mmr::f2bf(p);
-          const uint16_t l = mmr::f2bf(p - mmr::bf2f(h));
-          pH[(4 * g + i) * VLD + 16 * n + r] = h;
-          pL[(4 * g + i) * VLD + 16 * n + r] = l;
-        }
-      __syncthreads();
-#pragma unroll
-      for (int ks2 = 0; ks2 < 2; ++ks2) {
-        const bf16x8 pah = *(const bf16x8*)(pH + r * VLD + 32 * ks2 + 8 * g);
-        const bf16x8 pal = *(const bf16x8*)(pL + r * VLD + 32 * ks2 + 8 * g);
+        const int qi = qbase[u] + 4 * g + i;
+        const float inv = lrow[u][i] > 0.f ? 1.0f / lrow[u][i] : 0.f;
+        const bool ok = qi < lq;
+        float* orow = a.out ? a.out + qtok(ok ? qi : 0) * a.ldo + head * dh : nullptr;
 #pragma unroll
         for (int nd = 0; nd < 2 * DT; ++nd) {
-          const bf16x8 vbh = *(const bf16x8*)(sVh + (16 * nd + r) * VLD + 32 * ks2 + 8 * g);
-          const bf16x8 vbl = *(const bf16x8*)(sVl + (16 * nd + r) * VLD + 32 * ks2 + 8 * g);
-          o[nd] = mfma3(pah, pal, vbh, vbl, o[nd]);
+          const int d = 16 * nd + r;
+          const float val = o[u][nd][i] * inv;
+          if (ok) {
+            if (orow && d < dh) orow[d] = val;
+            macc[nd] += val;
+          }
         }
       }
-    }
-    // finalise this query tile: O / l (a row with every key masked -> 0)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int qi = qbase + 4 * g + i;
-      const float inv = lrow[i] > 0.f ? 1.0f / lrow[i] : 0.f;
-      const bool ok = qi < lq;
-      float* orow = a.out ? a.out + qtok(ok ? qi : 0) * a.ldo + head * dh : nullptr;
-#pragma unroll
-      for (int nd = 0; nd < 2 * DT; ++nd) {
-        const int d = 16 * nd + r;
-        const float val = o[nd][i] * inv;
-        if (ok) {
-          if (orow && d < dh) orow[d] = val;
-          macc[nd] += val;
-        }
-      }
-    }
   }
   if (a.mean_out) {
 #pragma unroll
@@ -551,10 +564,13 @@ mmr_status launch_attention(const char* who, AttnArgs a, int64_t nbh, bool swin,
     MMR_REQUIRE(dt == 1, "%s: Swin head_dim %d must be <= 32", who, a.dh);
     x3_attention<1, true><<<grid, 256, lds, st>>>(a);
   } else {
+    // 65-128 query rows: both 64-row query tiles per key chunk (dh <= 64; at 96 / 128 the second tile's
+    // registers do not fit)
+    const bool two = a.lq > 64 && a.lq <= 128 && dt <= 2;
     switch (dt) {
-      case 1: x3_attention<1, false><<<grid, 256, lds, st>>>(a); break;
-      case 2: x3_attention<2, false><<<grid, 256, lds, st>>>(a); break;
-      case 3: x3_attention<3, false><<<grid, 256, lds, st>>>(a); break;
+      case 1: if (two) x3_attention<1, false, 2><<<grid, 256, lds, st>>>(a); else x3_attention<1, false><<<grid, 256, lds, st>>>(a); break;
+      case 2: if (two) x3_attention<2, false, 2><<<grid, 256, lds, st>>>(a); else x3_attention<2, false><<<grid, 256, lds, st>>>(a); break;
+      case 3: if (two) x3_attention<3, false, 2><<<grid, 256, lds, st>>>(a); else x3_attention<3, false><<<grid, 256, lds, st>>>(a); break;
       default: x3_attention<4, false><<<grid, 256, lds, st>>>(a); break;
     }
   }

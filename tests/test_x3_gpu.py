@@ -115,7 +115,8 @@ def _attn_ref(q, k, v, b, lq, lk, heads, dh, scale, mask=None):
                                                           (4, 51, 51, 8, 128, False, True),
                                                           (2, 1, 49, 8, 96, False, True),
                                                           (3, 130, 70, 2, 48, True, True),
-                                                          (2, 128, 1, 8, 96, False, True)])
+                                                          (2, 128, 1, 8, 96, False, True),
+                                                          (2, 100, 77, 4, 64, True, True), (3, 65, 128, 2, 32, False, False)])
 def test_x3_attention_vs_f64(b, lq, lk, heads, dh, use_mask, mean):
     g = torch.Generator().manual_seed(b * 1000 + lq + lk + dh)
     C = heads * dh

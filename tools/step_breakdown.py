@@ -69,6 +69,8 @@ def wrap(name, fn):
             n_out = wt.shape[0] if name == "linear_ln" else wt.w.shape[-2]
             key = (name, x.numel() // K, n_out, K, k.get("act", 0),
                    k.get("ln_mode", 0) if name == "linear_ln" else (k.get("residual") is not None or len(a) > 3 and a[3] is not None))
+        if name in ("x3_attention", "mha"):
+            key = f"{name} b={a[3]} lq={a[4]} lk={a[5]} h={a[6]} dh={a[7]}"
         if name == "linear":
             x, wt = a[0], a[1]
             K = x.shape[-1]
