@@ -530,6 +530,62 @@ __global__ __launch_bounds__(256) void ln_rows_v(const float* __restrict__ x, in
   }
 }
 
+// f32 rows of c <= 64 LPR / ... short rows (the x3 Swin stages 1-2, c = 96 / 192): LPR lanes per row (64 / LPR
+// rows per wave), PER channels per lane (lane j: channels j + LPR i), reductions over the row's lane
+// group — one row per wave left 2/3 of a c = 96 wave idle and paid a full wave reduction per row
+template <int LPR, int PER>
+__global__ __launch_bounds__(256) void ln_rows_s(const float* __restrict__ x, int64_t ldx, const float* __restrict__ a,
+                                                 const float* __restrict__ r, int64_t ldr, const float* __restrict__ g,
+                                                 const float* __restrict__ b, const float* __restrict__ post, int64_t ldp,
+                                                 const float* __restrict__ ps, float* __restrict__ y, int64_t ldy,
+                                                 int64_t rows, int c, float eps, int groups, int64_t gdiv) {
+  constexpr int RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, j = lane % LPR;
+  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  const bool live = row < rows;
+  const int64_t rw = live ? row : rows - 1;  // dead lanes compute a valid row and store nothing
+  const int grp = (int)((rw / gdiv) % groups);
+  g += (int64_t)grp * c;
+  b += (int64_t)grp * c;
+  const float av = a ? a[grp] : 1.f;
+  const float pv = ps ? ps[grp] : 1.f;
+  auto chc = [&](int i) { const int ch = j + LPR * i; return ch < c ? ch : c - 1; };
+  float v[PER], rv[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) v[i] = x[rw * ldx + chc(i)];
+  if (r) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) rv[i] = r[rw * ldr + chc(i)];
+  } else {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) rv[i] = 0.f;
+  }
+  auto gsum = [](float t) {
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) t += __shfl_xor(t, o, 64);
+    return t;
+  };
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    v[i] = j + LPR * i < c ? av * v[i] + rv[i] : 0.f;
+    s += v[i];
+  }
+  const float mean = gsum(s) / c;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i)
+    if (j + LPR * i < c) ss += (v[i] - mean) * (v[i] - mean);
+  const float rstd = rsqrtf(gsum(ss) / c + eps);
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int ch = j + LPR * i;
+    const float pp = post ? pv * post[rw * ldp + chc(i)] : 0.f;
+    const float t = (v[i] - mean) * rstd * g[chc(i)] + b[chc(i)] + pp;
+    if (live && ch < c) y[rw * ldy + ch] = t;
+  }
+}
+
 // ------------------------------------------------------------------ fused-sequence assembly
 // seq[b] = [x1[b]; patches_fused[b][0..np); x2[b]] + pe[0..np+2)  -> bf16 (b, np+2, c)
 // (fusion.py:451-468 cat, model.py:396-397 dropout(eval) + pos_encoder).
@@ -781,9 +837,16 @@ mmr_status mmr_ln_rows(const void* x, int64_t ldx, const float* alpha, const voi
 #define LNV(VW_)                                                                                                  \
   ln_rows_v<VW_><<<grid, 256, 0, st>>>((const float*)x, ldx, alpha, (const float*)residual, ldr, gamma, beta, post, \
                                        ldp, post_scale, (float*)y, ldy, rows, c, eps, groups, group_div)
+#define LNSM(LPR_, PER_)                                                                                          \
+  ln_rows_s<LPR_, PER_><<<dim3((unsigned)mmr::ceil_div(rows, 4 * (64 / LPR_))), 256, 0, st>>>(                  \
+      (const float*)x, ldx, alpha, (const float*)residual, ldr, gamma, beta, post, ldp, post_scale, (float*)y, ldy, \
+      rows, c, eps, groups, group_div)
     if (ok(4)) LNV(4);
     else if (ok(2)) LNV(2);
+    else if (c <= 128) LNSM(16, 8);
+    else if (c <= 256) LNSM(32, 8);
     else LNS_DISPATCH(float);
+#undef LNSM
 #undef LNV
   }
 #undef LNS_DISPATCH

@@ -147,12 +147,13 @@ def test_ln_rows(dtype):
 
 
 @pytest.mark.parametrize("c,ld,groups", [(768, 768, 1), (384, 384, 3), (1024, 1024, 1), (96, 96, 1), (768, 770, 2),
-                                         (256, 258, 1)])
+                                         (256, 258, 1), (192, 192, 2), (200, 201, 1), (520, 521, 1), (40, 40, 1)])
 def test_ln_rows_f32_widths(c, ld, groups):
-    """f32 rows at the widths the vector forms take (c % 256: 4-wide, c % 128: 2-wide) and the scalar form
-    (c = 96, or rows at an odd stride), grouped parameters, residual + post: vs torch fp32 within 1e-5."""
+    """f32 rows at the widths the vector forms take (c % 256: 4-wide, c % 128: 2-wide), the short-row form
+    (c <= 256: 16 / 32 lanes per row) and the scalar form (longer rows at an odd stride), grouped
+    parameters, residual + post, a row count that leaves dead lanes: vs torch fp32 within 1e-5."""
     g = torch.Generator().manual_seed(c + ld + groups)
-    rows = 6 * groups
+    rows = 6 * groups + 1
     xb = torch.randn(rows, ld, generator=g)
     x, r, post = xb[:, :c], torch.randn(rows, c, generator=g), torch.randn(rows, c, generator=g)
     ga, be = 1 + 0.1 * torch.randn(groups, c, generator=g), 0.1 * torch.randn(groups, c, generator=g)
