@@ -494,12 +494,17 @@ mmr_status mmr_x3_linear(const float* x, int64_t ldx, const uint16_t* w_hi, cons
  * mmr_x3_linear_p8 takes X' and the weight image W' ([npad][3 kp] bf16, built once at load, npad =
  * mmr_x3_p8_npad(n): n itself when it is a multiple of 192 or 256, else n rounded up to 192 with zero
  * rows; 0 = n not taken) and writes y (m, n) f32 contiguous: m % 256 == 0, act 0 / 1 (GELU, erf), bias
- * NULL or npad floats (zero-padded), residual (m, n) f32 contiguous or NULL (may be y). */
+ * NULL or npad floats (zero-padded), residual (m, n) f32 contiguous or NULL (may be y).
+ * x_hilo != 0: xs holds [x_hi | x_lo] rows (2 kp wide; the x_hi segment is read twice); needs bias, act 0.
+ * out_hilo != 0: y is written as the NEXT x3 GEMM's x_hilo operand, [y_hi | y_lo] bf16 rows 2 n wide
+ * (the split of the f32 value mmr_x3_split_rows would make, bit for bit); needs n % 384 == 0 and no
+ * residual — a FFN1 -> FFN2 pair then skips the f32 round trip and the split pass. */
 int32_t mmr_x3_p8_kpad(int32_t k);
 int32_t mmr_x3_p8_npad(int32_t n);
 mmr_status mmr_x3_split_rows(const float* x, int64_t ldx, int64_t m, int32_t k, uint16_t* xs, void* stream);
-mmr_status mmr_x3_linear_p8(const uint16_t* xs, const uint16_t* w3, const float* bias, const float* residual,
-                            float* y, int64_t m, int32_t n, int32_t k, int32_t act, void* stream);
+mmr_status mmr_x3_linear_p8(const uint16_t* xs, int32_t x_hilo, const uint16_t* w3, const float* bias,
+                            const float* residual, void* y, int64_t m, int32_t n, int32_t k, int32_t act,
+                            int32_t out_hilo, void* stream);
 /* Attention core (nn.MultiheadAttention / BERT self-attention, eval): per (batch, head)
  * softmax(q k^T * scale (+ key mask)) v; rows as mmr_mha (q row bi*lq + i at q + row*ldq + head*dh);
  * mask01 (b, lk) int64 or NULL (0 -> key excluded, HF's additive finfo.min); out (b*lq, ldo) and/or

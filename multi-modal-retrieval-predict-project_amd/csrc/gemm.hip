@@ -583,7 +583,7 @@ __device__ unsigned long long p8_stamps[1024 * 8 * 8 * 4];
 //   LNM = 2: takes the raw y as the residual R and adds LN(y) = gamma (rstd y - rstd mean) + beta
 //            (LV1 = gamma, LV2 = beta over the output columns).
 template <int NT, int ACT, bool HAS_BIAS, bool HAS_RES, bool FP8 = false, bool OUT8 = false, int KNN = 0,
-          int LNM = 0, bool STO = false, bool OF32 = false>
+          int LNM = 0, bool STO = false, bool OF32 = false, bool OSPL = false, bool XHL = false>
 __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restrict__ X,
                                                        const uint16_t* __restrict__ W,
                                                        const float* __restrict__ bias,
@@ -599,12 +599,16 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
                                                        const float* __restrict__ LC = nullptr,
                                                        const float* __restrict__ LV1 = nullptr,
                                                        const float* __restrict__ LV2 = nullptr,
-                                                       float* __restrict__ SP = nullptr, int ldn = 0) {
+                                                       float* __restrict__ SP = nullptr, int ldn = 0, int xseg = 0) {
   static_assert(!OUT8 || (FP8 && NT == 4 && !HAS_RES), "OUT8: MX-fp8 256x256 tiles without residual");
   static_assert((LNM == 0 && !STO) || (!FP8 && !KNN), "LayerNorm fold: bf16 GEMMs");
   static_assert(LNM != 2 || HAS_RES, "LNM = 2 normalises the residual");
   static_assert(!STO || ACT == 0, "row statistics: LDS-staged (non-GELU) epilogue");
   static_assert(!OF32 || (!FP8 && !OUT8 && !KNN && LNM == 0 && !STO), "f32 output: plain bf16 operands");
+  // OSPL (with OF32): the output written as the next x3 GEMM's split operand rows [hi | lo] (bf16, row
+  // width 2 N) instead of f32 — one 8-B store of each per (m-tile, n-tile)
+  static_assert(!OSPL || (OF32 && NT == 3 && !HAS_RES), "split output: OF32 256 x 192 tiles without residual");
+  static_assert(!XHL || OF32, "split input: the x3 split GEMM");
   static_assert(KNN == 0 || ((KNN == 2 || KNN == 4) && NT == 4 && !FP8 && !HAS_BIAS && !HAS_RES && ACT == 0),
                 "KNN (rows per unit 2 / 4): plain 256x256 fp16 tiles");
 #if defined(__HIP_DEVICE_COMPILE__)  // buffer-descriptor builtins exist in the device pass only
@@ -648,9 +652,9 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   // STO: 8 more (one row-statistics store per m-tile, lanes fq = 0 — the instruction always issues)
   // OF32: one 16-B store per (m-tile, n-tile) straight from the accumulators
   constexpr int nstore = skip_st ? 0
-                                 : (OF32 ? 8 * NT
+                                 : (OF32 ? (OSPL ? 16 : 8) * NT
                                          : (skip_gm ? 8 : (epi_pl ? C::NSTORE_PL : C::NSTORE_LDS) + (STO ? 8 : 0)));
-  static_assert(!OF32 || 8 * NT + 5 <= 63, "vmcnt range");
+  static_assert(!OF32 || (OSPL ? 16 : 8) * NT + 5 <= 63, "vmcnt range");
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
 
   const int ntiles = tiles_m * tiles_n;
@@ -709,6 +713,14 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   const int row0 = 8 * wave + prow;
   const uint32_t off0 = (uint32_t)(row0 * K * ESZ + swz(row0, pch) * 16);
   const uint32_t pstride = (uint32_t)(64 * K * ESZ);  // bytes between consecutive pieces of an operand
+  // OF32, xseg > 0 (the x3 split GEMM fed [x_hi | x_lo] rows, 2 kp wide, against W' = [w_hi | w_lo |
+  // w_hi], 3 kp): X K-tile kt is read from kt - xseg once kt >= xseg (segment 1 re-reads x_hi, segment
+  // 2 reads x_lo), X rows are Kx = K - 64 xseg wide
+  // (XHL instantiations only: a per-lane offset more costs the others a spill)
+  const int Kx = XHL ? K - 64 * xseg : K;
+  const uint32_t off0x = XHL ? (uint32_t)(row0 * Kx * ESZ + swz(row0, pch) * 16) : off0;
+  const uint32_t pstridex = XHL ? (uint32_t)(64 * Kx * ESZ) : pstride;
+  auto kxt = [&](int kt) { return XHL && kt >= xseg ? kt - xseg : kt; };
   // KNN: the gallery W is in the index's tile32h layout (16-row x 32-half 1-KB pieces, knn.hip
   // tile32h_index) — the same image every other fp16 scan reads, so the index keeps ONE fp16 copy.
   // Logical chunk c of row r in K-tile kt = piece (r/16, 2 kt + c/4), lane slot (c%4) 16 + r%16: the
@@ -727,7 +739,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   auto pan = [](int v) { return v; };
 #endif
   auto xbase = [&](int tile) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)X + (int64_t)pan(mof(tile)) * 256 * K * ESZ), 0, 0x7FFFFFFF, 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)X + (int64_t)pan(mof(tile)) * 256 * Kx * ESZ), 0, 0x7FFFFFFF, 0x00020000);
   };
   auto wbase = [&](int tile) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)W + (int64_t)pan(nof(tile)) * TBN * K * ESZ), 0, 0x7FFFFFFF, 0x00020000);
@@ -749,8 +761,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
     }
   };
   auto gA = [&](__amdgpu_buffer_rsrc_t xb, int buf, int j, int kt) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(xb, (lds_ptr_t)(dsm + aoff(buf) + (64 * j + 8 * wave) * KB), 16, off0,
-                                             kt * (KB * 2) + j * pstride, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(xb, (lds_ptr_t)(dsm + aoff(buf) + (64 * j + 8 * wave) * KB), 16, off0x,
+                                             kxt(kt) * (KB * 2) + j * pstridex, 0, 0);
   };
   auto gB = [&](__amdgpu_buffer_rsrc_t wb, int buf, int j, int kt) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(wb, (lds_ptr_t)(dsm + boff(buf) + (64 * j + 8 * wave) * KB), 16, off0w,
@@ -1098,7 +1110,19 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
             for (int e = 0; e < 4; ++e) v[e] = 0.5f * v[e] * (1.0f + erff(v[e] * 0.70710678118654752f));
           }
           if constexpr (HAS_RES) v += rr4[j];
-          if (!skip_st) __builtin_amdgcn_raw_buffer_store_b128(v, ry, off[j], 0, 0);
+          if constexpr (OSPL) {
+            // [hi | lo] bf16 of the f32 value (the split mmr_x3_split_rows would make), row width 2 N
+            const uint32_t h0 = mmr::pack2bf(v[0], v[1]), h1 = mmr::pack2bf(v[2], v[3]);
+            const uint32_t l0 = mmr::pack2bf(v[0] - __uint_as_float(h0 << 16), v[1] - __uint_as_float(h0 & 0xFFFF0000u));
+            const uint32_t l1 = mmr::pack2bf(v[2] - __uint_as_float(h1 << 16), v[3] - __uint_as_float(h1 & 0xFFFF0000u));
+            uint16_t* ys = Y + (m0 + rl) * 2 * (int64_t)N + n0 + wc * 16 * NT + j * 16 + efq * 4;
+            if (!skip_st) {
+              *(uint2*)ys = make_uint2(h0, h1);
+              *(uint2*)(ys + N) = make_uint2(l0, l1);
+            }
+          } else if (!skip_st) {
+            __builtin_amdgcn_raw_buffer_store_b128(v, ry, off[j], 0, 0);
+          }
         }
       }
     }
@@ -1851,15 +1875,15 @@ __global__ __launch_bounds__(256) void x3_split_rows(const float* __restrict__ x
   *(uint4*)(o + 2 * kp) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
 }
 
-template <int NT, int ACT, bool HB, bool HR>
-void launch_x3p8(const uint16_t* xs, const uint16_t* w3, const float* b, const float* r, float* y, int64_t m, int npad,
-                 int n, int k3, hipStream_t st) {
+template <int NT, int ACT, bool HB, bool HR, bool OSPL = false, bool XHL = false>
+void launch_x3p8(const uint16_t* xs, const uint16_t* w3, const float* b, const float* r, void* y, int64_t m, int npad,
+                 int n, int k3, int xseg, hipStream_t st) {
   const int grid = std::max(8, cu_count() / 8 * 8);
   const int tm = (int)(m / 256), tn = npad / (64 * NT);
-  gemm_bf16_tn_p8<NT, ACT, HB, HR, false, false, 0, 0, false, true>
+  gemm_bf16_tn_p8<NT, ACT, HB, HR, false, false, 0, 0, false, true, OSPL, XHL>
       <<<dim3(std::max<int64_t>(8, std::min<int64_t>(grid, (int64_t)tm * tn) / 8 * 8)), dim3(512), P8<NT>::LDS_B, st>>>(
           xs, w3, b, (const uint16_t*)r, (uint16_t*)y, m, npad, k3, tm, tn, nullptr, nullptr, nullptr, nullptr, nullptr,
-          0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, n);
+          0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, n, xseg);
 }
 }  // namespace
 
@@ -1935,8 +1959,9 @@ extern "C" mmr_status mmr_x3_split_rows(const float* x, int64_t ldx, int64_t m, 
   return MMR_OK;
 }
 
-extern "C" mmr_status mmr_x3_linear_p8(const uint16_t* xs, const uint16_t* w3, const float* bias, const float* residual,
-                                       float* y, int64_t m, int32_t n, int32_t k, int32_t act, void* stream) {
+extern "C" mmr_status mmr_x3_linear_p8(const uint16_t* xs, int32_t x_hilo, const uint16_t* w3, const float* bias,
+                                       const float* residual, void* y, int64_t m, int32_t n, int32_t k, int32_t act,
+                                       int32_t out_hilo, void* stream) {
   mmr::clear_error();
   MMR_REQUIRE(xs && w3 && y, "mmr_x3_linear_p8: NULL pointer");
   const int kp = mmr_x3_p8_kpad(k);
@@ -1944,23 +1969,52 @@ extern "C" mmr_status mmr_x3_linear_p8(const uint16_t* xs, const uint16_t* w3, c
   const int npad = mmr_x3_p8_npad(n);
   MMR_REQUIRE(npad > 0, "mmr_x3_linear_p8: n=%d (multiple of 4, <= 16384)", n);
   MMR_REQUIRE(act == 0 || act == 1, "mmr_x3_linear_p8: act=%d", act);
+  MMR_REQUIRE(!out_hilo || (n % 384 == 0 && residual == nullptr),
+              "mmr_x3_linear_p8: split output needs n %% 384 == 0 and no residual (n=%d)", n);
   // (residual == y is fine: every output element is read, then written, by the one lane that owns it)
   hipStream_t st = mmr::as_stream(stream);
-  const int nt = npad % 192 == 0 && npad % 256 == 0 ? ln_nt(m, npad) : (npad % 256 == 0 ? 4 : 3);
+  const int xseg = x_hilo ? kp / 64 : 0;  // [x_hi | x_lo] rows: segment 1 re-reads x_hi
+  const int nt = out_hilo ? 3 : (npad % 192 == 0 && npad % 256 == 0 ? ln_nt(m, npad) : (npad % 256 == 0 ? 4 : 3));
   const bool hb = bias != nullptr, hr = residual != nullptr;
-#define X3P8(NT_)                                                                                         \
-  do {                                                                                                     \
-    if (act) {                                                                                             \
-      if (hb && hr) launch_x3p8<NT_, 1, true, true>(xs, w3, bias, residual, y, m, npad, n, 3 * kp, st);          \
-      else if (hb) launch_x3p8<NT_, 1, true, false>(xs, w3, bias, residual, y, m, npad, n, 3 * kp, st);          \
-      else if (hr) launch_x3p8<NT_, 1, false, true>(xs, w3, bias, residual, y, m, npad, n, 3 * kp, st);          \
-      else launch_x3p8<NT_, 1, false, false>(xs, w3, bias, residual, y, m, npad, n, 3 * kp, st);                 \
-    } else {                                                                                               \
-      if (hb && hr) launch_x3p8<NT_, 0, true, true>(xs, w3, bias, residual, y, m, npad, n, 3 * kp, st);          \
-      else if (hb) launch_x3p8<NT_, 0, true, false>(xs, w3, bias, residual, y, m, npad, n, 3 * kp, st);          \
-      else if (hr) launch_x3p8<NT_, 0, false, true>(xs, w3, bias, residual, y, m, npad, n, 3 * kp, st);          \
-      else launch_x3p8<NT_, 0, false, false>(xs, w3, bias, residual, y, m, npad, n, 3 * kp, st);                 \
-    }                                                                                                      \
+  MMR_REQUIRE(!x_hilo || (act == 0 && bias), "mmr_x3_linear_p8: split input is taken with bias, without activation");
+  MMR_REQUIRE(!(x_hilo && out_hilo), "mmr_x3_linear_p8: split input and split output together");
+  if (out_hilo) {
+    if (act) {
+      if (hb) launch_x3p8<3, 1, true, false, true>(xs, w3, bias, nullptr, y, m, npad, n, 3 * kp, 0, st);
+      else launch_x3p8<3, 1, false, false, true>(xs, w3, bias, nullptr, y, m, npad, n, 3 * kp, 0, st);
+    } else {
+      if (hb) launch_x3p8<3, 0, true, false, true>(xs, w3, bias, nullptr, y, m, npad, n, 3 * kp, 0, st);
+      else launch_x3p8<3, 0, false, false, true>(xs, w3, bias, nullptr, y, m, npad, n, 3 * kp, 0, st);
+    }
+    MMR_LAUNCH_CHECK();
+    return MMR_OK;
+  }
+  void* yf = y;
+  if (x_hilo) {
+#define X3P8H(NT_)                                                                                                  \
+  do {                                                                                                               \
+    if (hr) launch_x3p8<NT_, 0, true, true, false, true>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, xseg, st); \
+    else launch_x3p8<NT_, 0, true, false, false, true>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, xseg, st);   \
+  } while (0)
+    if (nt == 4) X3P8H(4);
+    else X3P8H(3);
+#undef X3P8H
+    MMR_LAUNCH_CHECK();
+    return MMR_OK;
+  }
+#define X3P8(NT_)                                                                                             \
+  do {                                                                                                         \
+    if (act) {                                                                                                 \
+      if (hb && hr) launch_x3p8<NT_, 1, true, true>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, 0, st); \
+      else if (hb) launch_x3p8<NT_, 1, true, false>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, 0, st); \
+      else if (hr) launch_x3p8<NT_, 1, false, true>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, 0, st); \
+      else launch_x3p8<NT_, 1, false, false>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, 0, st);        \
+    } else {                                                                                                   \
+      if (hb && hr) launch_x3p8<NT_, 0, true, true>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, 0, st); \
+      else if (hb) launch_x3p8<NT_, 0, true, false>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, 0, st); \
+      else if (hr) launch_x3p8<NT_, 0, false, true>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, 0, st); \
+      else launch_x3p8<NT_, 0, false, false>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, 0, st);        \
+    }                                                                                                          \
   } while (0)
   if (nt == 4) X3P8(4);
   else X3P8(3);

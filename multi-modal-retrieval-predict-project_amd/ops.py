@@ -641,12 +641,40 @@ def x3_linear(x, wx, bias=None, residual=None, act=0, out=None):
             and (r2 is None or r2.is_contiguous())):
         xs = torch.empty((M, 3 * kp), dtype=torch.bfloat16, device=x.device)
         _chk(_L().mmr_x3_split_rows(_lib.ptr(x2), x2.stride(0), M, K, _lib.ptr(xs), _s(x)), "mmr_x3_split_rows")
-        _chk(_L().mmr_x3_linear_p8(_lib.ptr(xs), _lib.ptr(wx.w3(kp, npad)), _lib.ptr(wx.bias_padded(bias, npad)),
-                                   _lib.ptr(r2), _lib.ptr(y), M, N, K, act, _s(x)), "mmr_x3_linear_p8")
+        _chk(_L().mmr_x3_linear_p8(_lib.ptr(xs), 0, _lib.ptr(wx.w3(kp, npad)), _lib.ptr(wx.bias_padded(bias, npad)),
+                                   _lib.ptr(r2), _lib.ptr(y), M, N, K, act, 0, _s(x)), "mmr_x3_linear_p8")
         return y
     _chk(_L().mmr_x3_linear(_lib.ptr(x2), x2.stride(0), _lib.ptr(wx.hi), _lib.ptr(wx.lo), _lib.ptr(bias), _lib.ptr(r2),
                             r2.stride(0) if r2 is not None else 0, _lib.ptr(y), N, M, N, K, act, _s(x)),
          "mmr_x3_linear")
+    return y
+
+
+def x3_ffn(x, w1, b1, w2, b2, residual=None):
+    """fc2(GELU(fc1(x))) (+ residual), f32 in and out (the BERT / Swin MLP in the x3 mode).  When both
+    linears take the 8-phase split GEMM and fc1's width is a multiple of 384, fc1 writes its output
+    straight as fc2's [hi | lo] bf16 operand rows (mmr_x3_linear_p8 out_hilo / x_hilo): the f32 round
+    trip and the split pass drop out and the result is bit-identical to the two x3_linear calls."""
+    _lib.require_gpu(x)
+    K = x.shape[-1]
+    N1, N2 = w1.w.shape[0], w2.w.shape[0]
+    x2 = x.reshape(-1, K)
+    M = x2.shape[0]
+    L = _L()
+    kp1, kp2, np1, np2 = L.mmr_x3_p8_kpad(K), L.mmr_x3_p8_kpad(N1), L.mmr_x3_p8_npad(N1), L.mmr_x3_p8_npad(N2)
+    r2 = residual.reshape(-1, N2) if residual is not None else None
+    if not (M > 0 and M % 256 == 0 and N1 % 384 == 0 and N2 >= 192 and kp1 > 0 and kp2 == N1 and np1 == N1
+            and np2 > 0 and b1 is not None and b2 is not None and x2.stride(1) == 1
+            and (r2 is None or r2.is_contiguous())):
+        return x3_linear(x3_linear(x, w1, b1, act=1), w2, b2, residual=residual)
+    xs = torch.empty((M, 3 * kp1), dtype=torch.bfloat16, device=x.device)
+    _chk(L.mmr_x3_split_rows(_lib.ptr(x2), x2.stride(0), M, K, _lib.ptr(xs), _s(x)), "mmr_x3_split_rows")
+    hl = torch.empty((M, 2 * N1), dtype=torch.bfloat16, device=x.device)  # [h_hi | h_lo] rows
+    _chk(L.mmr_x3_linear_p8(_lib.ptr(xs), 0, _lib.ptr(w1.w3(kp1, N1)), _lib.ptr(w1.bias_padded(b1, N1)), None,
+                            _lib.ptr(hl), M, N1, K, 1, 1, _s(x)), "mmr_x3_linear_p8")
+    y = torch.empty(x.shape[:-1] + (N2,), dtype=torch.float32, device=x.device)
+    _chk(L.mmr_x3_linear_p8(_lib.ptr(hl), 1, _lib.ptr(w2.w3(kp2, np2)), _lib.ptr(w2.bias_padded(b2, np2)),
+                            _lib.ptr(r2), _lib.ptr(y), M, N2, N1, 0, 0, _s(x)), "mmr_x3_linear_p8")
     return y
 
 

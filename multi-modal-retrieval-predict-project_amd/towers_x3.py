@@ -101,8 +101,7 @@ class SwinTowerX3:
                 a = ops.x3_swin_window_attention(qkv, bk["bias"], H, heads, ws, bk["shift"])
                 x = ops.x3_linear(a, bk["proj_w"], bk["proj_b"], residual=x)
                 h = _ln(x, bk["n2g"], bk["n2b"], 1e-5)
-                h = ops.x3_linear(h, bk["fc1_w"], bk["fc1_b"], act=1)
-                x = ops.x3_linear(h, bk["fc2_w"], bk["fc2_b"], residual=x)
+                x = ops.x3_ffn(h, bk["fc1_w"], bk["fc1_b"], bk["fc2_w"], bk["fc2_b"], residual=x)
         return x
 
     def forward_features(self, image):
@@ -183,6 +182,9 @@ class BertTowerX3:
                              out=ctx.view(B * L, C), mask=mask)
             a = self._gemm("o", ctx, ly["o_w"], ly["o_b"])
             h = _ln(a, ly["ln1_g"], ly["ln1_b"], 1e-12, residual=h)           # LN(dense(ctx) + h)
-            f = self._gemm("ffn2", self._gemm("ffn1", h, ly["i_w"], ly["i_b"], act=1), ly["f_w"], ly["f_b"])
+            if self.gemm_events is None:
+                f = ops.x3_ffn(h, ly["i_w"], ly["i_b"], ly["f_w"], ly["f_b"])
+            else:
+                f = self._gemm("ffn2", self._gemm("ffn1", h, ly["i_w"], ly["i_b"], act=1), ly["f_w"], ly["f_b"])
             h = _ln(f, ly["ln2_g"], ly["ln2_b"], 1e-12, residual=h)
         return h

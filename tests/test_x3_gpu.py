@@ -23,7 +23,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from mmr_amd import metrics, ops, synthetic
+from mmr_amd import _lib, metrics, ops, synthetic
 from mmr_amd.model import Backbones, MultiModalRetrievalModel, build_bench_model
 from mmr_amd.retrieval import MI355XRetrievalEngine
 from mmr_amd.towers import BERT_BASE, SWIN_T, init_bert_state, init_swin_state
@@ -98,6 +98,48 @@ def test_x3_linear_p8_inplace_residual_and_route():
     # the first M - 1 rows through the 128 x 128 kernel (M - 1 is not a multiple of 256)
     y_old = ops.x3_linear(x[:M - 1], wx, b, residual=r[:M - 1])
     assert (y_old - y[:M - 1]).abs().max().item() <= 1e-5 * y.abs().max().item()
+
+
+@pytest.mark.parametrize("M,C,Fw,res", [(2048, 768, 3072, False),   # BERT FFN (fc1 -> fc2, no residual)
+                                       (1024, 96, 384, True),      # Swin stage-1 MLP: fc2 N = 96 stays unfused
+                                       (2048, 192, 768, True),     # Swin stage-2 MLP, residual in fc2
+                                       (512, 768, 3072, True), (768, 384, 1536, True),
+                                       (1000, 768, 3072, False)])  # rows not a multiple of 256: unfused
+def test_x3_ffn_split_handoff_bitwise(M, C, Fw, res):
+    """x3_ffn (fc1 writes fc2's [hi | lo] operand rows, fc2 reads them with the hi segment twice)
+    equals x3_linear(GELU) -> x3_linear bit for bit, and stays within the x3 bound of f64."""
+    g = torch.Generator().manual_seed(M + C + Fw)
+    x = torch.randn(M, C, generator=g).to(DEV)
+    w1 = ops.X3W((torch.randn(Fw, C, generator=g) * C ** -0.5).to(DEV))
+    b1 = (torch.randn(Fw, generator=g) * 0.1).to(DEV)
+    w2 = ops.X3W((torch.randn(C, Fw, generator=g) * Fw ** -0.5).to(DEV))
+    b2 = (torch.randn(C, generator=g) * 0.1).to(DEV)
+    r = torch.randn(M, C, generator=g).to(DEV) if res else None
+    y = ops.x3_ffn(x, w1, b1, w2, b2, residual=r)
+    ref = ops.x3_linear(ops.x3_linear(x, w1, b1, act=1), w2, b2, residual=r)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+    h64 = F.gelu(x.double() @ w1.w.double().T + b1.double())
+    y64 = h64 @ w2.w.double().T + b2.double() + (r.double() if r is not None else 0)
+    assert _rel(y, y64) < 1e-5
+
+
+def test_x3_linear_p8_split_flags_rejected():
+    """The split operand flags' preconditions fail loudly at the C-ABI."""
+    L = _lib.lib()
+    x = torch.zeros(256, 3 * 384, dtype=torch.bfloat16, device=DEV)
+    w = torch.zeros(384, 3 * 384, dtype=torch.bfloat16, device=DEV)
+    b = torch.zeros(384, dtype=torch.float32, device=DEV)
+    y = torch.zeros(256, 2 * 384, dtype=torch.bfloat16, device=DEV)
+    s = _lib.stream_ptr()
+    P = _lib.ptr
+    # split output with a residual / n not a multiple of 384; split input without bias / with GELU; both
+    assert L.mmr_x3_linear_p8(P(x), 0, P(w), P(b), P(b), P(y), 256, 384, 384, 0, 1, s) != 0
+    assert L.mmr_x3_linear_p8(P(x), 0, P(w), P(b), None, P(y), 256, 192, 384, 0, 1, s) != 0
+    assert L.mmr_x3_linear_p8(P(x), 1, P(w), None, None, P(y), 256, 384, 384, 0, 0, s) != 0
+    assert L.mmr_x3_linear_p8(P(x), 1, P(w), P(b), None, P(y), 256, 384, 384, 1, 0, s) != 0
+    assert L.mmr_x3_linear_p8(P(x), 1, P(w), P(b), None, P(y), 256, 384, 384, 0, 1, s) != 0
+    torch.cuda.synchronize()
 
 
 def _attn_ref(q, k, v, b, lq, lk, heads, dh, scale, mask=None):

@@ -43,14 +43,21 @@ names = ["linear", "layernorm", "add_layernorm", "scaled_add_layernorm", "bert_e
          "assemble_seq", "rows_to_f32", "quantize_mxfp8", "linear_mxfp8", "linear_mxfp8_q8", "layernorm_q8",
          "linear_rw", "linear_ln", "ln_row_coef", "linear_x3", "linear_x3_batched",
          "x3_linear", "x3_attention", "x3_swin_window_attention", "x3_patch_im2col", "x3_patch_merge_ln",
-         "x3_bert_embed", "x3_add_pos", "x3_assemble_seq", "x3_mean_rows", "x3_gather_rows"]
+         "x3_bert_embed", "x3_add_pos", "x3_assemble_seq", "x3_mean_rows", "x3_gather_rows", "x3_ffn"]
+depth = [0]  # ops called from inside a wrapped op (x3_ffn's unfused route) are not counted twice
 
 
 def wrap(name, fn):
     def w(*a, **k):
+        if depth[0]:
+            return fn(*a, **k)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        out = fn(*a, **k)
+        depth[0] += 1
+        try:
+            out = fn(*a, **k)
+        finally:
+            depth[0] -= 1
         e1.record()
         key = name
         if name == "linear_mxfp8_q8":
@@ -69,6 +76,10 @@ def wrap(name, fn):
             n_out = wt.shape[0] if name == "linear_ln" else wt.w.shape[-2]
             key = (name, x.numel() // K, n_out, K, k.get("act", 0),
                    k.get("ln_mode", 0) if name == "linear_ln" else (k.get("residual") is not None or len(a) > 3 and a[3] is not None))
+        if name == "x3_ffn":
+            x, w1, w2 = a[0], a[1], a[3]
+            K = x.shape[-1]
+            key = (name, x.numel() // K, w1.w.shape[0], K, 1, (k.get("residual") is not None or len(a) > 5 and a[5] is not None))
         if name in ("x3_attention", "mha"):
             key = f"{name} b={a[3]} lq={a[4]} lk={a[5]} h={a[6]} dh={a[7]}"
         if name == "linear":
@@ -100,7 +111,7 @@ print(f"total {tot:.3f} ms per step (sum of op times)")
 for key, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
     if isinstance(key, tuple):
         nm, M, N, K, act, res = key
-        tf = 2.0 * M * N * K * (c / 3) / (t * 1e-3) / 1e12
+        tf = 2.0 * M * N * K * (c / 3) * (2 if nm == "x3_ffn" else 1) / (t * 1e-3) / 1e12
         print(f"{t:8.3f} ms {c // 3:4d}x  {nm:14s} M={M:7d} N={N:5d} K={K:5d} act={act} res={int(res)}  {tf:6.0f} TF/s")
     else:
         print(f"{t:8.3f} ms {c // 3:4d}x  {key}")
