@@ -460,6 +460,13 @@ mmr_status mmr_ln_rows(const void* x, int64_t ldx, const float* alpha, const voi
                        const float* post_scale, void* y, int64_t ldy, int64_t rows, int32_t c, float eps,
                        int32_t io_bf16, int32_t groups, int64_t group_div, void* stream);
 
+/* f32 y = LayerNorm(x + residual) (residual may be NULL, y may be NULL) that also writes xs, the
+ * x3 split GEMM's x_hilo operand: [hi | lo] bf16 rows 2 kp wide (kp = mmr_x3_p8_kpad(c), zero columns
+ * c..kp), the split mmr_x3_split_rows would make of y.  c % 4 == 0, c <= 1024; rows 16-B aligned. */
+mmr_status mmr_ln_rows_split(const float* x, int64_t ldx, const float* residual, int64_t ldr, const float* gamma,
+                             const float* beta, float* y, int64_t ldy, uint16_t* xs, int64_t rows, int32_t c, float eps,
+                             void* stream);
+
 /* seq (b, np+2, c) bf16 = [x1; patches_fused; x2] + pe[0..np+2) (fusion.py:468 + model.py:397);
  * x1, x2 f32 (b, c), patches_fused bf16 (b*np, c), pe f32 [>= np+2][c]. */
 mmr_status mmr_assemble_seq(const float* x1, const uint16_t* patches_fused, const float* x2, const float* pe,
@@ -495,7 +502,8 @@ mmr_status mmr_x3_linear(const float* x, int64_t ldx, const uint16_t* w_hi, cons
  * mmr_x3_p8_npad(n): n itself when it is a multiple of 192 or 256, else n rounded up to 192 with zero
  * rows; 0 = n not taken) and writes y (m, n) f32 contiguous: m % 256 == 0, act 0 / 1 (GELU, erf), bias
  * NULL or npad floats (zero-padded), residual (m, n) f32 contiguous or NULL (may be y).
- * x_hilo != 0: xs holds [x_hi | x_lo] rows (2 kp wide; the x_hi segment is read twice); needs bias, act 0.
+ * x_hilo != 0: xs holds [x_hi | x_lo] rows (2 kp wide; the x_hi segment is read twice; mmr_ln_rows_split
+ * or a split output below writes them); needs a bias.
  * out_hilo != 0: y is written as the NEXT x3 GEMM's x_hilo operand, [y_hi | y_lo] bf16 rows 2 n wide
  * (the split of the f32 value mmr_x3_split_rows would make, bit for bit); needs n % 384 == 0 and no
  * residual — a FFN1 -> FFN2 pair then skips the f32 round trip and the split pass. */

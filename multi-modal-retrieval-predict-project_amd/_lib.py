@@ -85,6 +85,7 @@ SIGNATURES = {
                    c_i32, c_f32, c_vp],
     "mmr_add_pos_bf16": [c_vp, c_i32, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp],
     "mmr_add_pos_bf16_q8": [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp],
+    "mmr_ln_rows_split": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_f32, c_vp],
     "mmr_ln_rows": [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_i32, c_f32,
                     c_i32, c_i32, c_i64, c_vp],
     "mmr_linear_f32_batched": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,

@@ -586,6 +586,75 @@ __global__ __launch_bounds__(256) void ln_rows_s(const float* __restrict__ x, in
   }
 }
 
+// f32 LayerNorm(x + residual) that also writes the x3 split GEMM's operand rows (the x3 towers' LN ->
+// QKV / fc1 pairs): xs row = [hi | lo] bf16, 2 kp wide (kp = c rounded up to 128, zero columns c..kp),
+// the split mmr_x3_split_rows would make of the f32 output, which is written too when y != NULL.
+// 32 lanes per row, NCH = kp / 128 4-wide chunks per lane (lane j: columns 4 (j + 32 i) ..+3).
+template <int NCH>
+__global__ __launch_bounds__(256) void ln_rows_split(const float* __restrict__ x, int64_t ldx, const float* __restrict__ r,
+                                                     int64_t ldr, const float* __restrict__ g, const float* __restrict__ b,
+                                                     float* __restrict__ y, int64_t ldy, uint16_t* __restrict__ xs,
+                                                     int64_t rows, int c, float eps) {
+  constexpr int KP = 128 * NCH;
+  const int lane = threadIdx.x & 63, j = lane & 31;
+  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  const bool live = row < rows;
+  const int64_t rw = live ? row : rows - 1;
+  float4 v[NCH];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int col = 4 * (j + 32 * i);
+    v[i] = col < c ? *(const float4*)(x + rw * ldx + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (r) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int col = 4 * (j + 32 * i);
+      if (col < c) {
+        const float4 t = *(const float4*)(r + rw * ldr + col);
+        v[i].x += t.x, v[i].y += t.y, v[i].z += t.z, v[i].w += t.w;
+      }
+    }
+  }
+  auto gsum = [](float t) {
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) t += __shfl_xor(t, o, 64);
+    return t;
+  };
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  const float mean = gsum(s) / c;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    if (4 * (j + 32 * i) < c) {
+      const float a0 = v[i].x - mean, a1 = v[i].y - mean, a2 = v[i].z - mean, a3 = v[i].w - mean;
+      ss += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+    }
+  }
+  const float rstd = rsqrtf(gsum(ss) / c + eps);
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int col = 4 * (j + 32 * i);
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (col < c) {
+      const float4 gg = *(const float4*)(g + col), bb = *(const float4*)(b + col);
+      t = make_float4((v[i].x - mean) * rstd * gg.x + bb.x, (v[i].y - mean) * rstd * gg.y + bb.y,
+                      (v[i].z - mean) * rstd * gg.z + bb.z, (v[i].w - mean) * rstd * gg.w + bb.w);
+      if (live && y) *(float4*)(y + rw * ldy + col) = t;
+    }
+    const uint32_t h0 = mmr::pack2bf(t.x, t.y), h1 = mmr::pack2bf(t.z, t.w);
+    const uint32_t l0 = mmr::pack2bf(t.x - __uint_as_float(h0 << 16), t.y - __uint_as_float(h0 & 0xFFFF0000u));
+    const uint32_t l1 = mmr::pack2bf(t.z - __uint_as_float(h1 << 16), t.w - __uint_as_float(h1 & 0xFFFF0000u));
+    if (live) {
+      uint16_t* o = xs + rw * 2 * KP + col;
+      *(uint2*)o = make_uint2(h0, h1);
+      *(uint2*)(o + KP) = make_uint2(l0, l1);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ fused-sequence assembly
 // seq[b] = [x1[b]; patches_fused[b][0..np); x2[b]] + pe[0..np+2)  -> bf16 (b, np+2, c)
 // (fusion.py:451-468 cat, model.py:396-397 dropout(eval) + pos_encoder).
@@ -851,6 +920,35 @@ mmr_status mmr_ln_rows(const void* x, int64_t ldx, const float* alpha, const voi
   }
 #undef LNS_DISPATCH
 #undef LNS
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_ln_rows_split(const float* x, int64_t ldx, const float* residual, int64_t ldr, const float* gamma,
+                             const float* beta, float* y, int64_t ldy, uint16_t* xs, int64_t rows, int32_t c, float eps,
+                             void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && gamma && beta && xs && rows >= 0 && c > 0 && c % 4 == 0 && c <= 1024,
+              "mmr_ln_rows_split: bad arguments (c %% 4 == 0, c <= 1024; rows=%lld c=%d)", (long long)rows, c);
+  auto al = [](const void* p, int64_t ld) { return p == nullptr || (((uintptr_t)p & 15) == 0 && ld % 4 == 0); };
+  MMR_REQUIRE(al(x, ldx) && al(residual, ldr) && al(y, ldy) && al(gamma, 0) && al(beta, 0) && al(xs, 0),
+              "mmr_ln_rows_split: rows / parameters must be 16-B aligned (row strides multiples of 4)");
+  if (rows == 0) return MMR_OK;
+  const int nch = (c + 127) / 128;
+  const dim3 grid((unsigned)mmr::ceil_div(rows, 8));
+  hipStream_t st = mmr::as_stream(stream);
+#define LNSP(N_) ln_rows_split<N_><<<grid, 256, 0, st>>>(x, ldx, residual, ldr, gamma, beta, y, ldy, xs, rows, c, eps)
+  switch (nch) {
+    case 1: LNSP(1); break;
+    case 2: LNSP(2); break;
+    case 3: LNSP(3); break;
+    case 4: LNSP(4); break;
+    case 5: LNSP(5); break;
+    case 6: LNSP(6); break;
+    case 7: LNSP(7); break;
+    default: LNSP(8); break;
+  }
+#undef LNSP
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }

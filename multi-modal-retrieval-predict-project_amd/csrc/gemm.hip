@@ -1976,10 +1976,12 @@ extern "C" mmr_status mmr_x3_linear_p8(const uint16_t* xs, int32_t x_hilo, const
   const int xseg = x_hilo ? kp / 64 : 0;  // [x_hi | x_lo] rows: segment 1 re-reads x_hi
   const int nt = out_hilo ? 3 : (npad % 192 == 0 && npad % 256 == 0 ? ln_nt(m, npad) : (npad % 256 == 0 ? 4 : 3));
   const bool hb = bias != nullptr, hr = residual != nullptr;
-  MMR_REQUIRE(!x_hilo || (act == 0 && bias), "mmr_x3_linear_p8: split input is taken with bias, without activation");
-  MMR_REQUIRE(!(x_hilo && out_hilo), "mmr_x3_linear_p8: split input and split output together");
+  MMR_REQUIRE(!x_hilo || bias, "mmr_x3_linear_p8: split input is taken with a bias");
   if (out_hilo) {
-    if (act) {
+    if (x_hilo) {
+      if (act) launch_x3p8<3, 1, true, false, true, true>(xs, w3, bias, nullptr, y, m, npad, n, 3 * kp, xseg, st);
+      else launch_x3p8<3, 0, true, false, true, true>(xs, w3, bias, nullptr, y, m, npad, n, 3 * kp, xseg, st);
+    } else if (act) {
       if (hb) launch_x3p8<3, 1, true, false, true>(xs, w3, bias, nullptr, y, m, npad, n, 3 * kp, 0, st);
       else launch_x3p8<3, 1, false, false, true>(xs, w3, bias, nullptr, y, m, npad, n, 3 * kp, 0, st);
     } else {
@@ -1991,13 +1993,18 @@ extern "C" mmr_status mmr_x3_linear_p8(const uint16_t* xs, int32_t x_hilo, const
   }
   void* yf = y;
   if (x_hilo) {
-#define X3P8H(NT_)                                                                                                  \
-  do {                                                                                                               \
-    if (hr) launch_x3p8<NT_, 0, true, true, false, true>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, xseg, st); \
-    else launch_x3p8<NT_, 0, true, false, false, true>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, xseg, st);   \
+#define X3P8H(NT_, A_)                                                                                               \
+  do {                                                                                                                \
+    if (hr) launch_x3p8<NT_, A_, true, true, false, true>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, xseg, st); \
+    else launch_x3p8<NT_, A_, true, false, false, true>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, xseg, st);   \
   } while (0)
-    if (nt == 4) X3P8H(4);
-    else X3P8H(3);
+    if (nt == 4) {
+      if (act) X3P8H(4, 1);
+      else X3P8H(4, 0);
+    } else {
+      if (act) X3P8H(3, 1);
+      else X3P8H(3, 0);
+    }
 #undef X3P8H
     MMR_LAUNCH_CHECK();
     return MMR_OK;

@@ -620,11 +620,65 @@ def swin_attn_block(x, pack, bias, ws, shift, eps):
 
 # ---------------------------------------------------------------- fp32-faithful tower mode ("x3")
 # f32 activations, every contraction on bf16x3 MFMA (csrc/x3.hip); weights as X3W (hi / lo splits).
+class X3Rows:
+    """An x3 GEMM operand already split: t = [hi | lo] bf16 rows (rows, 2 kp), kp = mmr_x3_p8_kpad(k),
+    standing for f32 rows of width k with leading shape `lead` (mmr_ln_rows_split's output)."""
+    __slots__ = ("t", "k", "kp", "lead")
+
+    def __init__(self, t, k, kp, lead):
+        self.t, self.k, self.kp, self.lead = t, k, kp, lead
+
+    @property
+    def rows(self):
+        return self.t.shape[0]
+
+
+def x3_ln_split(x, g, b, eps, residual=None, keep_f32=False):
+    """LayerNorm(x + residual) over the last dim of f32 rows for an x3 linear: rows filling 256-row
+    tiles come back as X3Rows (mmr_ln_rows_split: the next GEMM skips its split pass), with the f32
+    output too when keep_f32 (-> (y, X3Rows)); other row counts as plain f32 rows (ln_rows)."""
+    _lib.require_gpu(x)
+    c = x.shape[-1]
+    x2 = x.reshape(-1, c)
+    r2 = residual.reshape(-1, c) if residual is not None else None
+    M = x2.shape[0]
+    kp = _L().mmr_x3_p8_kpad(c)
+    if not (M > 0 and M % 256 == 0 and kp > 0 and c % 4 == 0 and c <= 1024 and x2.stride(1) == 1
+            and (r2 is None or r2.stride(1) == 1)):
+        y = ln_rows(x2, g, b, eps, residual=r2).view(x.shape)
+        return (y, y) if keep_f32 else y
+    xs = torch.empty((M, 2 * kp), dtype=torch.bfloat16, device=x.device)
+    y = torch.empty(x.shape, dtype=torch.float32, device=x.device) if keep_f32 else None
+    _chk(_L().mmr_ln_rows_split(_lib.ptr(x2), x2.stride(0), _lib.ptr(r2), r2.stride(0) if r2 is not None else 0,
+                                _lib.ptr(g), _lib.ptr(b), _lib.ptr(y), c, _lib.ptr(xs), M, c, float(eps), _s(x)),
+         "mmr_ln_rows_split")
+    xr = X3Rows(xs, c, kp, tuple(x.shape[:-1]))
+    return (y, xr) if keep_f32 else xr
+
+
+def _x3_linear_split_in(xr, wx, bias, residual, act, out):
+    """x3_linear of an X3Rows operand (mmr_x3_linear_p8 x_hilo)."""
+    N, Kw = wx.w.shape
+    assert xr.k == Kw, f"x3_linear: K {xr.k} != weight K {Kw}"
+    M = xr.rows
+    npad = _L().mmr_x3_p8_npad(N)
+    assert npad > 0 and bias is not None, "x3_linear: a split operand needs N % 4 == 0 and a bias"
+    y = out if out is not None else torch.empty(xr.lead + (N,), dtype=torch.float32, device=xr.t.device)
+    r2 = residual.reshape(-1, N) if residual is not None else None
+    assert y.is_contiguous() and (r2 is None or r2.is_contiguous())
+    _chk(_L().mmr_x3_linear_p8(_lib.ptr(xr.t), 1, _lib.ptr(wx.w3(xr.kp, npad)), _lib.ptr(wx.bias_padded(bias, npad)),
+                               _lib.ptr(r2), _lib.ptr(y), M, N, xr.k, act, 0, _s(xr.t)), "mmr_x3_linear_p8")
+    return y
+
+
 def x3_linear(x, wx, bias=None, residual=None, act=0, out=None):
     """act(x @ w.T + bias) (+ residual) for any number of rows: x (..., K) f32 (last-dim contiguous rows),
     wx an X3W of w (N, K), K % 32 == 0; residual may be `out`.  Row counts that fill 256-row tiles with
     N >= 192 run as one K' = 3 kp split GEMM on the 8-phase kernel (mmr_x3_split_rows +
-    mmr_x3_linear_p8, N padded to whole tiles); the rest on mmr_x3_linear (128 x 128 tiles)."""
+    mmr_x3_linear_p8, N padded to whole tiles); the rest on mmr_x3_linear (128 x 128 tiles).  x may be
+    an X3Rows (x3_ln_split), read as is."""
+    if isinstance(x, X3Rows):
+        return _x3_linear_split_in(x, wx, bias, residual, act, out)
     _lib.require_gpu(x)
     K = x.shape[-1]
     N, Kw = wx.w.shape
@@ -652,18 +706,35 @@ def x3_linear(x, wx, bias=None, residual=None, act=0, out=None):
 
 def x3_ffn(x, w1, b1, w2, b2, residual=None):
     """fc2(GELU(fc1(x))) (+ residual), f32 in and out (the BERT / Swin MLP in the x3 mode).  When both
-    linears take the 8-phase split GEMM and fc1's width is a multiple of 384, fc1 writes its output
-    straight as fc2's [hi | lo] bf16 operand rows (mmr_x3_linear_p8 out_hilo / x_hilo): the f32 round
-    trip and the split pass drop out and the result is bit-identical to the two x3_linear calls."""
+    rows fill 256-row tiles and fc1's width is a multiple of 384, fc1 writes its output straight as
+    fc2's [hi | lo] bf16 operand rows (mmr_x3_linear_p8 out_hilo / x_hilo): the f32 round trip and the
+    split pass drop out; bit-identical to the two x3_linear calls where those take the 8-phase route
+    (fc2 N >= 192), within the split's rounding of them otherwise.  x may be an X3Rows."""
+    L = _L()
+    N1, N2 = w1.w.shape[0], w2.w.shape[0]
+    kp2, np1, np2 = L.mmr_x3_p8_kpad(N1), L.mmr_x3_p8_npad(N1), L.mmr_x3_p8_npad(N2)
+    r2 = residual.reshape(-1, N2) if residual is not None else None
+    if isinstance(x, X3Rows):
+        M = x.rows
+        if not (N1 % 384 == 0 and kp2 == N1 and np1 == N1 and np2 > 0 and b1 is not None and b2 is not None
+                and (r2 is None or r2.is_contiguous())):
+            return x3_linear(x3_linear(x, w1, b1, act=1), w2, b2, residual=residual)
+        assert x.k == w1.w.shape[1]
+        hl = torch.empty((M, 2 * N1), dtype=torch.bfloat16, device=x.t.device)
+        _chk(L.mmr_x3_linear_p8(_lib.ptr(x.t), 1, _lib.ptr(w1.w3(x.kp, N1)), _lib.ptr(b1), None, _lib.ptr(hl), M, N1,
+                                x.k, 1, 1, _s(x.t)), "mmr_x3_linear_p8")
+        y = torch.empty(x.lead + (N2,), dtype=torch.float32, device=x.t.device)
+        _chk(L.mmr_x3_linear_p8(_lib.ptr(hl), 1, _lib.ptr(w2.w3(kp2, np2)), _lib.ptr(w2.bias_padded(b2, np2)),
+                                _lib.ptr(r2), _lib.ptr(y), M, N2, N1, 0, 0, _s(x.t)), "mmr_x3_linear_p8")
+        return y
     _lib.require_gpu(x)
     K = x.shape[-1]
-    N1, N2 = w1.w.shape[0], w2.w.shape[0]
     x2 = x.reshape(-1, K)
     M = x2.shape[0]
-    L = _L()
-    kp1, kp2, np1, np2 = L.mmr_x3_p8_kpad(K), L.mmr_x3_p8_kpad(N1), L.mmr_x3_p8_npad(N1), L.mmr_x3_p8_npad(N2)
-    r2 = residual.reshape(-1, N2) if residual is not None else None
-    if not (M > 0 and M % 256 == 0 and N1 % 384 == 0 and N2 >= 192 and kp1 > 0 and kp2 == N1 and np1 == N1
+    kp1 = L.mmr_x3_p8_kpad(K)
+    # (fc2 with N2 < 192 — Swin stage 1, N2 = 96 — included: its weight rows pad to one 192 tile, which
+    # the MFMA has room for, while the unfused route's split pass is what made it slower there)
+    if not (M > 0 and M % 256 == 0 and N1 % 384 == 0 and kp1 > 0 and kp2 == N1 and np1 == N1
             and np2 > 0 and b1 is not None and b2 is not None and x2.stride(1) == 1
             and (r2 is None or r2.is_contiguous())):
         return x3_linear(x3_linear(x, w1, b1, act=1), w2, b2, residual=residual)

@@ -96,11 +96,11 @@ class SwinTowerX3:
             heads = cfg["num_heads"][i]
             ws = min(cfg["window_size"], H)
             for bk in st["blocks"]:
-                h = _ln(x, bk["n1g"], bk["n1b"], 1e-5)
+                h = ops.x3_ln_split(x, bk["n1g"], bk["n1b"], 1e-5)
                 qkv = ops.x3_linear(h, bk["qkv_w"], bk["qkv_b"])
                 a = ops.x3_swin_window_attention(qkv, bk["bias"], H, heads, ws, bk["shift"])
                 x = ops.x3_linear(a, bk["proj_w"], bk["proj_b"], residual=x)
-                h = _ln(x, bk["n2g"], bk["n2b"], 1e-5)
+                h = ops.x3_ln_split(x, bk["n2g"], bk["n2b"], 1e-5)
                 x = ops.x3_ffn(h, bk["fc1_w"], bk["fc1_b"], bk["fc2_w"], bk["fc2_b"], residual=x)
         return x
 
@@ -175,16 +175,23 @@ class BertTowerX3:
         C = self.hidden
         dh = C // heads
         h = ops.x3_bert_embed(ids, self.word, self.pos, self.type0, self.eg, self.eb, 1e-12)
-        for ly in self.layers:
-            qkv = self._gemm("qkv", h, ly["qkv_w"], ly["qkv_b"]).view(B * L, 3 * C)
+        hs = h  # the QKV operand: the previous layer's LayerNorm output as split rows (X3Rows)
+        for li, ly in enumerate(self.layers):
+            qkv = self._gemm("qkv", hs, ly["qkv_w"], ly["qkv_b"]).view(B * L, 3 * C)
             ctx = torch.empty((B, L, C), dtype=torch.float32, device=self.device)
             ops.x3_attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], B, L, L, heads, dh, 1.0 / math.sqrt(dh),
                              out=ctx.view(B * L, C), mask=mask)
             a = self._gemm("o", ctx, ly["o_w"], ly["o_b"])
-            h = _ln(a, ly["ln1_g"], ly["ln1_b"], 1e-12, residual=h)           # LN(dense(ctx) + h)
             if self.gemm_events is None:
-                f = ops.x3_ffn(h, ly["i_w"], ly["i_b"], ly["f_w"], ly["f_b"])
+                # LN(dense(ctx) + h), kept f32 for the next residual and split for FFN1
+                h, hs = ops.x3_ln_split(a, ly["ln1_g"], ly["ln1_b"], 1e-12, residual=h, keep_f32=True)
+                f = ops.x3_ffn(hs, ly["i_w"], ly["i_b"], ly["f_w"], ly["f_b"])
+                if li + 1 < len(self.layers):
+                    h, hs = ops.x3_ln_split(f, ly["ln2_g"], ly["ln2_b"], 1e-12, residual=h, keep_f32=True)
+                else:
+                    h = _ln(f, ly["ln2_g"], ly["ln2_b"], 1e-12, residual=h)
             else:
+                h = _ln(a, ly["ln1_g"], ly["ln1_b"], 1e-12, residual=h)
                 f = self._gemm("ffn2", self._gemm("ffn1", h, ly["i_w"], ly["i_b"], act=1), ly["f_w"], ly["f_b"])
-            h = _ln(f, ly["ln2_g"], ly["ln2_b"], 1e-12, residual=h)
+                h = hs = _ln(f, ly["ln2_g"], ly["ln2_b"], 1e-12, residual=h)
         return h
