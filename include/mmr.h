@@ -524,6 +524,14 @@ mmr_status mmr_x3_attention(const float* q, int64_t ldq, const float* k, int64_t
  * (b*hw*hw, c), q scaled by dh^-0.5 before q k^T (timm), bias from mmr_swin_attn_bias.  head_dim <= 32. */
 mmr_status mmr_x3_swin_window_attention(const float* qkv, const float* bias, float* out, int32_t b, int32_t hw,
                                         int32_t c, int32_t heads, int32_t ws, int32_t shift, void* stream);
+/* The two above writing their output as the x3 split GEMM's x_hilo operand instead (the O-proj / proj
+ * input): xs = [hi | lo] bf16 rows 2 kp wide, kp = mmr_x3_p8_kpad(heads*dh) (columns heads*dh..kp zero),
+ * the split mmr_x3_split_rows would make of the f32 output. */
+mmr_status mmr_x3_attention_xs(const float* q, int64_t ldq, const float* k, int64_t ldk, const float* v, int64_t ldv,
+                               uint16_t* xs, const int64_t* mask01, int32_t b, int32_t lq, int32_t lk, int32_t heads,
+                               int32_t dh, float scale, void* stream);
+mmr_status mmr_x3_swin_window_attention_xs(const float* qkv, const float* bias, uint16_t* xs, int32_t b, int32_t hw,
+                                           int32_t c, int32_t heads, int32_t ws, int32_t shift, void* stream);
 /* Patch-embed im2col, f32: (b, cin, hw, hw) -> (b*(hw/patch)^2, kp) columns (k = c*p^2 + ky*p + kx, zero
  * for k >= cin*p^2). */
 mmr_status mmr_x3_patch_im2col(const float* image, float* cols, int32_t b, int32_t cin, int32_t hw, int32_t patch,

@@ -100,6 +100,9 @@ SIGNATURES = {
     "mmr_x3_linear_p8": [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_x3_attention": [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32,
                          c_i32, c_f32, c_vp],
+    "mmr_x3_attention_xs": [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_f32,
+                            c_vp],
+    "mmr_x3_swin_window_attention_xs": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_x3_swin_window_attention": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_x3_patch_im2col": [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_x3_patch_merge_ln": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp],

@@ -160,6 +160,26 @@ __global__ __launch_bounds__(256, 2) void x3_gemm(const float* __restrict__ X, i
 // [d][64 + 8]; head dims padded to DH = 32 DT with zeros (dh % 8 == 0).
 // S (16 x 64 per wave): lane (r, g) holds S[4 g + i][16 n + r]; P goes back through a wave-private
 // hi / lo LDS tile [16][64 + 8] as the A operand of O += P V (lane holds O[4 g + i][16 nd + r]).
+// 16-lane butterfly reductions by DPP (row = 16 lanes): quad_perm [1,0,3,2] / [2,3,0,1] are xor 1 / 2,
+// then row_half_mirror / row_mirror pair quads / halves whose lanes already agree — the same sums,
+// bit for bit, as the xor-1/2/4/8 shuffle butterfly, without its 4 LDS permutes
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dppf<0xB1>(v));
+  v = fmaxf(v, dppf<0x4E>(v));
+  v = fmaxf(v, dppf<0x141>(v));
+  return fmaxf(v, dppf<0x140>(v));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dppf<0xB1>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0x141>(v);
+  return v + dppf<0x140>(v);
+}
+
 struct AttnArgs {
   const float* q;
   int64_t ldq;
@@ -175,6 +195,8 @@ struct AttnArgs {
   int lq, lk, heads, dh;
   float scale;
   int hw, ws, shift;  // Swin windows
+  uint16_t* xs;       // non-NULL: the output as the x3 split GEMM's operand rows [hi | lo] (2 kp wide)
+  int kp;             //   instead of out; columns heads*dh .. kp written zero by the last head
 };
 
 template <int DT, bool SWIN, int QTW = 1>
@@ -319,8 +341,7 @@ __global__ __launch_bounds__(256) void x3_attention(const AttnArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           float cm = fmaxf(fmaxf(s[0][i], s[1][i]), fmaxf(s[2][i], s[3][i]));
-#pragma unroll
-          for (int m = 1; m < 16; m <<= 1) cm = fmaxf(cm, __shfl_xor(cm, m, 64));
+          cm = row16_max(cm);
           const float mnew = fmaxf(mrow[u][i], cm);
           float corr = 1.f, ps = 0.f;
           if (mnew != -INFINITY) {
@@ -335,8 +356,7 @@ __global__ __launch_bounds__(256) void x3_attention(const AttnArgs a) {
 #pragma unroll
             for (int n = 0; n < 4; ++n) s[n][i] = 0.f;
           }
-#pragma unroll
-          for (int m = 1; m < 16; m <<= 1) ps += __shfl_xor(ps, m, 64);
+          ps = row16_sum(ps);
           lrow[u][i] = lrow[u][i] * corr + ps;
           mrow[u][i] = mnew;
 #pragma unroll
@@ -377,15 +397,32 @@ __global__ __launch_bounds__(256) void x3_attention(const AttnArgs a) {
         const float inv = lrow[u][i] > 0.f ? 1.0f / lrow[u][i] : 0.f;
         const bool ok = qi < lq;
         float* orow = a.out ? a.out + qtok(ok ? qi : 0) * a.ldo + head * dh : nullptr;
+        uint16_t* xrow = a.xs ? a.xs + qtok(ok ? qi : 0) * 2 * a.kp : nullptr;
 #pragma unroll
         for (int nd = 0; nd < 2 * DT; ++nd) {
           const int d = 16 * nd + r;
           const float val = o[u][nd][i] * inv;
+          if (xrow) {
+            // lane pair (r, r ^ 1) holds columns d0, d0 + 1: the even lane stores their hi pair, the odd
+            // lane their lo pair (one 4-B store per lane, as the f32 output's)
+            const float oth = dppf<0xB1>(val);  // quad_perm [1,0,3,2]: lane r ^ 1
+            const bool odd = r & 1;
+            const float v0 = odd ? oth : val, v1 = odd ? val : oth;
+            const uint32_t hp = mmr::pack2bf(v0, v1);
+            const uint32_t word =
+                odd ? mmr::pack2bf(v0 - __uint_as_float(hp << 16), v1 - __uint_as_float(hp & 0xFFFF0000u)) : hp;
+            if (ok && d < dh) *(uint32_t*)(xrow + (odd ? a.kp : 0) + head * dh + (d & ~1)) = word;
+          }
           if (ok) {
-            if (orow && d < dh) orow[d] = val;
+            if (xrow) {
+            } else if (orow && d < dh) {
+              orow[d] = val;
+            }
             macc[nd] += val;
           }
         }
+        if (xrow && ok && head == a.heads - 1)
+          for (int z = a.heads * dh + r; z < a.kp; z += 16) xrow[z] = xrow[a.kp + z] = 0;
       }
   }
   if (a.mean_out) {
@@ -547,7 +584,7 @@ __global__ __launch_bounds__(256) void x3_gather_rows(const float* __restrict__ 
 bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 mmr_status launch_attention(const char* who, AttnArgs a, int64_t nbh, bool swin, void* stream) {
-  MMR_REQUIRE(a.q && a.k && a.v && (a.out || a.mean_out), "%s: NULL pointer", who);
+  MMR_REQUIRE(a.q && a.k && a.v && (a.out || a.mean_out || a.xs), "%s: NULL pointer", who);
   MMR_REQUIRE(a.lq > 0 && a.lk > 0 && a.heads > 0 && a.dh > 0 && a.dh % 8 == 0 && a.dh <= 128,
               "%s: bad shape lq=%d lk=%d heads=%d dh=%d (dh %% 8 == 0, <= 128)", who, a.lq, a.lk, a.heads, a.dh);
   MMR_REQUIRE(a.ldq % 4 == 0 && a.ldk % 4 == 0 && a.ldv % 4 == 0 && al16(a.q) && al16(a.k) && al16(a.v) &&
@@ -640,6 +677,30 @@ mmr_status mmr_x3_swin_window_attention(const float* qkv, const float* bias, flo
   AttnArgs a{qkv,     3 * (int64_t)c, qkv + c, 3 * (int64_t)c, qkv + 2 * c, 3 * (int64_t)c, out, c, nullptr, nullptr,
              bias,    ws * ws,        ws * ws, heads,          dh,          1.0f / sqrtf((float)dh), hw, ws, shift};
   return launch_attention("mmr_x3_swin_window_attention", a, nwin * heads, true, stream);
+}
+
+mmr_status mmr_x3_attention_xs(const float* q, int64_t ldq, const float* k, int64_t ldk, const float* v, int64_t ldv,
+                               uint16_t* xs, const int64_t* mask01, int32_t b, int32_t lq, int32_t lk, int32_t heads,
+                               int32_t dh, float scale, void* stream) {
+  mmr::clear_error();
+  const int kp = mmr_x3_p8_kpad(heads * dh);
+  MMR_REQUIRE(xs && b >= 0 && kp > 0, "mmr_x3_attention_xs: bad arguments (heads*dh=%d)", heads * dh);
+  AttnArgs a{q, ldq, k, ldk, v, ldv, nullptr, 0, nullptr, mask01, nullptr, lq, lk, heads, dh, scale, 0, 1, 0, xs, kp};
+  return launch_attention("mmr_x3_attention_xs", a, (int64_t)b * heads, false, stream);
+}
+
+mmr_status mmr_x3_swin_window_attention_xs(const float* qkv, const float* bias, uint16_t* xs, int32_t b, int32_t hw,
+                                           int32_t c, int32_t heads, int32_t ws, int32_t shift, void* stream) {
+  mmr::clear_error();
+  const int kp = mmr_x3_p8_kpad(c);
+  MMR_REQUIRE(qkv && bias && xs && kp > 0 && b >= 0 && hw > 0 && ws > 0 && hw % ws == 0 && ws * ws <= 64 && heads > 0 &&
+                  c % heads == 0 && shift >= 0 && shift < ws,
+              "mmr_x3_swin_window_attention_xs: bad shape hw=%d ws=%d c=%d heads=%d shift=%d", hw, ws, c, heads, shift);
+  const int dh = c / heads;
+  const int64_t nwin = (int64_t)b * (hw / ws) * (hw / ws);
+  AttnArgs a{qkv,  3 * (int64_t)c, qkv + c, 3 * (int64_t)c, qkv + 2 * c, 3 * (int64_t)c, nullptr, 0,  nullptr, nullptr,
+             bias, ws * ws,        ws * ws, heads,          dh,          1.0f / sqrtf((float)dh), hw, ws, shift, xs, kp};
+  return launch_attention("mmr_x3_swin_window_attention_xs", a, nwin * heads, true, stream);
 }
 
 mmr_status mmr_x3_patch_im2col(const float* image, float* cols, int32_t b, int32_t cin, int32_t hw, int32_t patch,

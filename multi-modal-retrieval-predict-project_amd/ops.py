@@ -767,6 +767,36 @@ def x3_swin_window_attention(qkv, bias, hw, heads, ws, shift):
     return out
 
 
+def x3_swin_window_attention_split(qkv, bias, hw, heads, ws, shift):
+    """x3_swin_window_attention with its output as X3Rows (the proj GEMM's split operand), for token
+    counts filling 256-row tiles; plain f32 rows otherwise."""
+    C = qkv.shape[-1] // 3
+    M = qkv.numel() // (3 * C)
+    kp = _L().mmr_x3_p8_kpad(C)
+    if not (M > 0 and M % 256 == 0 and kp > 0):
+        return x3_swin_window_attention(qkv, bias, hw, heads, ws, shift)
+    xs = torch.empty((M, 2 * kp), dtype=torch.bfloat16, device=qkv.device)
+    _chk(_L().mmr_x3_swin_window_attention_xs(_lib.ptr(qkv), _lib.ptr(bias), _lib.ptr(xs), qkv.shape[0], hw, C, heads,
+                                              ws, shift, _s(qkv)), "mmr_x3_swin_window_attention_xs")
+    return X3Rows(xs, C, kp, tuple(qkv.shape[:-1]))
+
+
+def x3_attention_split(q, k, v, b, lq, lk, heads, dh, scale, mask=None):
+    """x3_attention's output rows (b*lq, heads*dh) as X3Rows when b*lq fills 256-row tiles, else f32."""
+    C = heads * dh
+    kp = _L().mmr_x3_p8_kpad(C)
+    if not (b * lq > 0 and (b * lq) % 256 == 0 and kp > 0):
+        out = torch.empty((b * lq, C), dtype=torch.float32, device=q.device)
+        x3_attention(q, k, v, b, lq, lk, heads, dh, scale, out=out, mask=mask)
+        return out.view(b, lq, C)
+    _lib.require_gpu(q)
+    xs = torch.empty((b * lq, 2 * kp), dtype=torch.bfloat16, device=q.device)
+    _chk(_L().mmr_x3_attention_xs(_lib.ptr(q), q.stride(0), _lib.ptr(k), k.stride(0), _lib.ptr(v), v.stride(0),
+                                  _lib.ptr(xs), _lib.ptr(mask), b, lq, lk, heads, dh, float(scale), _s(q)),
+         "mmr_x3_attention_xs")
+    return X3Rows(xs, C, kp, (b, lq))
+
+
 def x3_patch_im2col(img, patch=4, kp=64):
     B, Cin, H, W = img.shape
     g = H // patch

@@ -98,7 +98,7 @@ class SwinTowerX3:
             for bk in st["blocks"]:
                 h = ops.x3_ln_split(x, bk["n1g"], bk["n1b"], 1e-5)
                 qkv = ops.x3_linear(h, bk["qkv_w"], bk["qkv_b"])
-                a = ops.x3_swin_window_attention(qkv, bk["bias"], H, heads, ws, bk["shift"])
+                a = ops.x3_swin_window_attention_split(qkv, bk["bias"], H, heads, ws, bk["shift"])
                 x = ops.x3_linear(a, bk["proj_w"], bk["proj_b"], residual=x)
                 h = ops.x3_ln_split(x, bk["n2g"], bk["n2b"], 1e-5)
                 x = ops.x3_ffn(h, bk["fc1_w"], bk["fc1_b"], bk["fc2_w"], bk["fc2_b"], residual=x)
@@ -178,9 +178,8 @@ class BertTowerX3:
         hs = h  # the QKV operand: the previous layer's LayerNorm output as split rows (X3Rows)
         for li, ly in enumerate(self.layers):
             qkv = self._gemm("qkv", hs, ly["qkv_w"], ly["qkv_b"]).view(B * L, 3 * C)
-            ctx = torch.empty((B, L, C), dtype=torch.float32, device=self.device)
-            ops.x3_attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], B, L, L, heads, dh, 1.0 / math.sqrt(dh),
-                             out=ctx.view(B * L, C), mask=mask)
+            ctx = ops.x3_attention_split(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], B, L, L, heads, dh,
+                                         1.0 / math.sqrt(dh), mask=mask)
             a = self._gemm("o", ctx, ly["o_w"], ly["o_b"])
             if self.gemm_events is None:
                 # LN(dense(ctx) + h), kept f32 for the next residual and split for FFN1

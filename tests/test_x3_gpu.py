@@ -276,6 +276,62 @@ def test_x3_swin_window_attention_vs_f64(hw, c, heads, shift):
     assert _rel(out, o) <= 5e-5
 
 
+def _split_bits(y, kp):
+    """[hi | lo] rows (int16 view) of f32 rows y (rows, c), zero columns c..kp: mmr_x3_split_rows' split."""
+    c = y.shape[-1]
+    hi = y.to(torch.bfloat16)
+    lo = (y - hi.float()).to(torch.bfloat16)
+    out = torch.zeros(y.shape[0], 2 * kp, dtype=torch.int16, device=y.device)
+    out[:, :c] = hi.view(torch.int16)
+    out[:, kp:kp + c] = lo.view(torch.int16)
+    return out
+
+
+@pytest.mark.parametrize("hw,c,heads,shift,B", [(56, 96, 3, 3, 4), (28, 192, 6, 0, 16), (14, 384, 12, 3, 64),
+                                                (7, 768, 24, 0, 256)])  # B hw^2 = 12544 tokens = 49 x 256
+def test_x3_swin_window_attention_split_rows(hw, c, heads, shift, B):
+    """The window attention's split-row output (the proj operand) equals the split of its f32 output
+    bit for bit, padding columns zero; proj through it equals proj through the f32 rows."""
+    ws = 7
+    g = torch.Generator().manual_seed(hw + c + shift + 1)
+    qkv = (torch.randn(B, hw, hw, 3 * c, generator=g) * 0.7).to(DEV)
+    table = torch.randn((2 * ws - 1) ** 2, heads, generator=g) * 0.5
+    bias = ops.swin_attn_bias(table.to(DEV), heads, ws, hw, shift)
+    ref = ops.x3_swin_window_attention(qkv, bias, hw, heads, ws, shift)
+    xr = ops.x3_swin_window_attention_split(qkv, bias, hw, heads, ws, shift)
+    assert isinstance(xr, ops.X3Rows) and xr.lead == (B, hw, hw)
+    assert torch.equal(xr.t.view(torch.int16), _split_bits(ref.reshape(-1, c), xr.kp))
+    w = ops.X3W((torch.randn(c, c, generator=g) * c ** -0.5).to(DEV))
+    b = torch.randn(c, generator=g).to(DEV)
+    r = torch.randn(B, hw, hw, c, generator=g).to(DEV)
+    torch.cuda.synchronize()
+    y_split = ops.x3_linear(xr, w, b, residual=r)
+    if c >= 192:  # N = 96 alone runs the 128 x 128 x3 kernel (another summation order)
+        assert torch.equal(y_split, ops.x3_linear(ref, w, b, residual=r))
+    y64 = ref.double() @ w.w.double().T + b.double() + r.double()
+    assert _rel(y_split, y64) < 1e-5
+
+
+@pytest.mark.parametrize("b,l,heads,dh,use_mask", [(8, 128, 12, 64, True), (4, 64, 8, 96, False)])
+def test_x3_attention_split_rows(b, l, heads, dh, use_mask):
+    """BERT-shaped x3 attention with split-row output (the O-proj operand) = the split of the f32 output."""
+    g = torch.Generator().manual_seed(b * l + dh)
+    C = heads * dh
+    qkv = (torch.randn(b * l, 3 * C, generator=g) * 0.7).to(DEV)
+    mask = torch.ones(b, l, dtype=torch.int64)
+    if use_mask:
+        for i in range(b):
+            mask[i, l - 7 * i:] = 0
+    mask = mask.to(DEV)
+    q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    out = torch.empty(b * l, C, device=DEV)
+    ops.x3_attention(q, k, v, b, l, l, heads, dh, dh ** -0.5, out=out, mask=mask)
+    xr = ops.x3_attention_split(q, k, v, b, l, l, heads, dh, dh ** -0.5, mask=mask)
+    torch.cuda.synchronize()
+    assert isinstance(xr, ops.X3Rows)
+    assert torch.equal(xr.t.view(torch.int16), _split_bits(out, xr.kp))
+
+
 def _double(sd):
     return {k: v.double() for k, v in sd.items()}
 

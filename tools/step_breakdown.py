@@ -43,7 +43,7 @@ names = ["linear", "layernorm", "add_layernorm", "scaled_add_layernorm", "bert_e
          "assemble_seq", "rows_to_f32", "quantize_mxfp8", "linear_mxfp8", "linear_mxfp8_q8", "layernorm_q8",
          "linear_rw", "linear_ln", "ln_row_coef", "linear_x3", "linear_x3_batched",
          "x3_linear", "x3_attention", "x3_swin_window_attention", "x3_patch_im2col", "x3_patch_merge_ln",
-         "x3_bert_embed", "x3_add_pos", "x3_assemble_seq", "x3_mean_rows", "x3_gather_rows", "x3_ffn", "x3_ln_split"]
+         "x3_bert_embed", "x3_add_pos", "x3_assemble_seq", "x3_mean_rows", "x3_gather_rows", "x3_ffn", "x3_ln_split", "x3_attention_split", "x3_swin_window_attention_split"]
 depth = [0]  # ops called from inside a wrapped op (x3_ffn's unfused route) are not counted twice
 
 
@@ -80,7 +80,7 @@ def wrap(name, fn):
             x, w1, w2 = a[0], a[1], a[3]
             K = x.k if isinstance(x, ops.X3Rows) else x.shape[-1]
             key = (name, x.rows if isinstance(x, ops.X3Rows) else x.numel() // K, w1.w.shape[0], K, 1, (k.get("residual") is not None or len(a) > 5 and a[5] is not None))
-        if name in ("x3_attention", "mha"):
+        if name in ("x3_attention", "mha", "x3_attention_split"):
             key = f"{name} b={a[3]} lq={a[4]} lk={a[5]} h={a[6]} dh={a[7]}"
         if name == "linear":
             x, wt = a[0], a[1]
