@@ -45,6 +45,27 @@ template <class T>
 __device__ __forceinline__ void pin(T& v) {
   asm volatile("" : "+v"(v));
 }
+// max over each 16-lane row by DPP: quad_perm [1,0,3,2] / [2,3,0,1] (xor 1 / 2), then row_half_mirror /
+// row_mirror, which pair quads / halves whose lanes already agree — the xor-1/2/4/8 butterfly's result
+// without its 4 LDS permutes
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dppf<0xB1>(v));
+  v = fmaxf(v, dppf<0x4E>(v));
+  v = fmaxf(v, dppf<0x141>(v));
+  return fmaxf(v, dppf<0x140>(v));
+}
+// the same butterfly for sums (bit-identical to the xor 1/2/4/8 shuffle order)
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dppf<0xB1>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0x141>(v);
+  return v + dppf<0x140>(v);
+}
+
 __device__ __forceinline__ uint32_t pack2bf(float a, float b) {
   const bf16x2_t v = {(__bf16)a, (__bf16)b};
   return __builtin_bit_cast(uint32_t, v);

@@ -645,8 +645,7 @@ __global__ __launch_bounds__(64 * WQ) void knn_scan_f16_gmax(const uint16_t* __r
       gmax[qrw * ldG + gcol] = mx;
       // block max over the 16 lanes of this h (rows r of the block's 4 tiles)
       float bm = mx;
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) bm = fmaxf(bm, __shfl_xor(bm, o, 64));
+      bm = mmr::row16_max(bm);
       if (r == 0) bmax[qrw * ldB + blk] = bm;
     }
 }
@@ -768,8 +767,7 @@ __global__ __launch_bounds__(64 * NWV) void knn_scan_f16_lq(const float* __restr
         const int64_t qrw = 16 * t + 4 * h + rg;
         gmax[qrw * ldG + gcol] = mx;
         float bm = mx;
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) bm = fmaxf(bm, __shfl_xor(bm, o, 64));
+        bm = mmr::row16_max(bm);
         if (r == 0) bmax[qrw * ldB + blk] = bm;
       }
   }

@@ -160,26 +160,6 @@ __global__ __launch_bounds__(256, 2) void x3_gemm(const float* __restrict__ X, i
 // [d][64 + 8]; head dims padded to DH = 32 DT with zeros (dh % 8 == 0).
 // S (16 x 64 per wave): lane (r, g) holds S[4 g + i][16 n + r]; P goes back through a wave-private
 // hi / lo LDS tile [16][64 + 8] as the A operand of O += P V (lane holds O[4 g + i][16 nd + r]).
-// 16-lane butterfly reductions by DPP (row = 16 lanes): quad_perm [1,0,3,2] / [2,3,0,1] are xor 1 / 2,
-// then row_half_mirror / row_mirror pair quads / halves whose lanes already agree — the same sums,
-// bit for bit, as the xor-1/2/4/8 shuffle butterfly, without its 4 LDS permutes
-template <int CTRL>
-__device__ __forceinline__ float dppf(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float row16_max(float v) {
-  v = fmaxf(v, dppf<0xB1>(v));
-  v = fmaxf(v, dppf<0x4E>(v));
-  v = fmaxf(v, dppf<0x141>(v));
-  return fmaxf(v, dppf<0x140>(v));
-}
-__device__ __forceinline__ float row16_sum(float v) {
-  v += dppf<0xB1>(v);
-  v += dppf<0x4E>(v);
-  v += dppf<0x141>(v);
-  return v + dppf<0x140>(v);
-}
-
 struct AttnArgs {
   const float* q;
   int64_t ldq;
@@ -341,7 +321,7 @@ __global__ __launch_bounds__(256) void x3_attention(const AttnArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           float cm = fmaxf(fmaxf(s[0][i], s[1][i]), fmaxf(s[2][i], s[3][i]));
-          cm = row16_max(cm);
+          cm = mmr::row16_max(cm);
           const float mnew = fmaxf(mrow[u][i], cm);
           float corr = 1.f, ps = 0.f;
           if (mnew != -INFINITY) {
@@ -356,7 +336,7 @@ __global__ __launch_bounds__(256) void x3_attention(const AttnArgs a) {
 #pragma unroll
             for (int n = 0; n < 4; ++n) s[n][i] = 0.f;
           }
-          ps = row16_sum(ps);
+          ps = mmr::row16_sum(ps);
           lrow[u][i] = lrow[u][i] * corr + ps;
           mrow[u][i] = mnew;
 #pragma unroll
@@ -405,7 +385,7 @@ __global__ __launch_bounds__(256) void x3_attention(const AttnArgs a) {
           if (xrow) {
             // lane pair (r, r ^ 1) holds columns d0, d0 + 1: the even lane stores their hi pair, the odd
             // lane their lo pair (one 4-B store per lane, as the f32 output's)
-            const float oth = dppf<0xB1>(val);  // quad_perm [1,0,3,2]: lane r ^ 1
+            const float oth = mmr::dppf<0xB1>(val);  // quad_perm [1,0,3,2]: lane r ^ 1
             const bool odd = r & 1;
             const float v0 = odd ? oth : val, v1 = odd ? val : oth;
             const uint32_t hp = mmr::pack2bf(v0, v1);
