@@ -539,6 +539,10 @@ mmr_status mmr_x3_patch_im2col(const float* image, float* cols, int32_t b, int32
 /* PatchMerging gather (timm order) + LayerNorm(4c), f32 in / out; 4c <= 4096. */
 mmr_status mmr_x3_patch_merge_ln(const float* x, const float* gamma, const float* beta, float* y, int32_t b,
                                  int32_t hw, int32_t c, float eps, void* stream);
+/* The same writing the reduction linear's x3 split operand instead: xs = [hi | lo] bf16 rows 2 kp wide,
+ * kp = mmr_x3_p8_kpad(4c) (zero columns 4c..kp); c % 4 == 0, 16-B aligned pointers. */
+mmr_status mmr_x3_patch_merge_ln_xs(const float* x, const float* gamma, const float* beta, uint16_t* xs, int32_t b,
+                                    int32_t hw, int32_t c, float eps, void* stream);
 /* BERT embeddings LN((word[id] + type[0]) + pos[l]) -> f32 (b*l, c), c <= 1024. */
 mmr_status mmr_x3_bert_embed(const int64_t* ids, const float* word, const float* pos, const float* type0,
                              const float* gamma, const float* beta, float* y, int32_t b, int32_t l, int32_t c, float eps,

@@ -106,6 +106,7 @@ SIGNATURES = {
     "mmr_x3_swin_window_attention": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_x3_patch_im2col": [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_x3_patch_merge_ln": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp],
+    "mmr_x3_patch_merge_ln_xs": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp],
     "mmr_x3_bert_embed": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp],
     "mmr_x3_add_pos": [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp],
     "mmr_x3_assemble_seq": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],

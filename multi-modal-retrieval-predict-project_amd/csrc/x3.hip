@@ -479,6 +479,66 @@ __global__ __launch_bounds__(256) void x3_patch_merge_ln(const float* __restrict
   }
 }
 
+// The same for c % 4 == 0, by 16-B chunks: lane takes chunks lane + 64 e (e < NCH) of the 4c-wide
+// merged row (a chunk never straddles two source pixels); writes the f32 row to y and / or the x3
+// split GEMM's [hi | lo] operand row to xs (2 kp wide, zero columns 4c..kp) — the reduction linear
+// then skips its split pass.  (The scalar form above spent 64 unrolled element slots and an integer
+// division per element on every lane: ~4x its bytes' time.)
+template <int NCH>
+__global__ __launch_bounds__(256) void x3_patch_merge_ln_v(const float* __restrict__ x, const float* __restrict__ gm,
+                                                           const float* __restrict__ bt, float* __restrict__ y,
+                                                           uint16_t* __restrict__ xs, int kp, int64_t nout, int hw,
+                                                           int c, float eps) {
+  const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (o >= nout) return;  // wave-uniform
+  const int h2 = hw / 2;
+  const int64_t bi = o / (h2 * h2);
+  const int i = (int)((o / h2) % h2), j = (int)(o % h2);
+  const int c4 = 4 * c;
+  float4 v[NCH];
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < NCH; ++e) {
+    const int k = 4 * (lane + 64 * e);
+    v[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (k < c4) {
+      const int p = k / c, off = k - p * c;
+      const int yy = 2 * i + (p & 1), xx = 2 * j + (p >> 1);
+      v[e] = *(const float4*)(x + ((bi * hw + yy) * hw + xx) * (int64_t)c + off);
+    }
+    s += (v[e].x + v[e].y) + (v[e].z + v[e].w);
+  }
+  const float mean = mmr::wave_sum(s) / c4;
+  float ss = 0.f;
+#pragma unroll
+  for (int e = 0; e < NCH; ++e)
+    if (4 * (lane + 64 * e) < c4) {
+      const float a0 = v[e].x - mean, a1 = v[e].y - mean, a2 = v[e].z - mean, a3 = v[e].w - mean;
+      ss += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+    }
+  const float rstd = 1.0f / sqrtf(mmr::wave_sum(ss) / c4 + eps);
+#pragma unroll
+  for (int e = 0; e < NCH; ++e) {
+    const int k = 4 * (lane + 64 * e);
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (k < c4) {
+      const float4 g = *(const float4*)(gm + k), b = *(const float4*)(bt + k);
+      t = make_float4((v[e].x - mean) * rstd * g.x + b.x, (v[e].y - mean) * rstd * g.y + b.y,
+                      (v[e].z - mean) * rstd * g.z + b.z, (v[e].w - mean) * rstd * g.w + b.w);
+      if (y) *(float4*)(y + o * c4 + k) = t;
+    }
+    if (xs && k < kp) {
+      const uint32_t h0 = mmr::pack2bf(t.x, t.y), h1 = mmr::pack2bf(t.z, t.w);
+      const uint32_t l0 = mmr::pack2bf(t.x - __uint_as_float(h0 << 16), t.y - __uint_as_float(h0 & 0xFFFF0000u));
+      const uint32_t l1 = mmr::pack2bf(t.z - __uint_as_float(h1 << 16), t.w - __uint_as_float(h1 & 0xFFFF0000u));
+      uint16_t* xo = xs + o * 2 * kp + k;
+      *(uint2*)xo = make_uint2(h0, h1);
+      *(uint2*)(xo + kp) = make_uint2(l0, l1);
+    }
+  }
+}
+
 // HF BertEmbeddings: LN(word[id] + pos[l] + type[0]) -> f32 (one wave per token, c <= 1024)
 __global__ __launch_bounds__(256) void x3_bert_embed(const int64_t* __restrict__ ids, const float* __restrict__ word,
                                                      const float* __restrict__ pos, const float* __restrict__ type0,
@@ -595,6 +655,23 @@ mmr_status launch_attention(const char* who, AttnArgs a, int64_t nbh, bool swin,
   return MMR_OK;
 }
 
+mmr_status launch_patch_merge_v(const float* x, const float* g, const float* b, float* y, uint16_t* xs, int kp,
+                                int64_t nout, int hw, int c, float eps, hipStream_t st) {
+  const int nch = (int)mmr::ceil_div(std::max(4 * c, kp), 256);
+  const dim3 grid((unsigned)mmr::ceil_div(nout, 4));
+#define PMV(N_) x3_patch_merge_ln_v<N_><<<grid, 256, 0, st>>>(x, g, b, y, xs, kp, nout, hw, c, eps)
+  if (nch <= 2) PMV(2);
+  else if (nch <= 3) PMV(3);
+  else if (nch <= 4) PMV(4);
+  else if (nch <= 6) PMV(6);
+  else if (nch <= 8) PMV(8);
+  else if (nch <= 12) PMV(12);
+  else PMV(16);
+#undef PMV
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
 }  // namespace
 
 // ================================================================== C ABI
@@ -703,10 +780,24 @@ mmr_status mmr_x3_patch_merge_ln(const float* x, const float* gamma, const float
               "mmr_x3_patch_merge_ln: bad arguments (4c <= 4096)");
   const int64_t nout = (int64_t)b * (hw / 2) * (hw / 2);
   if (nout == 0) return MMR_OK;
+  if (c % 4 == 0 && al16(x) && al16(gamma) && al16(beta) && al16(y))
+    return launch_patch_merge_v(x, gamma, beta, y, nullptr, 0, nout, hw, c, eps, mmr::as_stream(stream));
   x3_patch_merge_ln<<<dim3((unsigned)mmr::ceil_div(nout, 4)), 256, 0, mmr::as_stream(stream)>>>(x, gamma, beta, y, nout,
                                                                                                hw, c, eps);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
+}
+
+mmr_status mmr_x3_patch_merge_ln_xs(const float* x, const float* gamma, const float* beta, uint16_t* xs, int32_t b,
+                                    int32_t hw, int32_t c, float eps, void* stream) {
+  mmr::clear_error();
+  const int kp = mmr_x3_p8_kpad(4 * c);
+  MMR_REQUIRE(x && gamma && beta && xs && b >= 0 && hw % 2 == 0 && c > 0 && c % 4 == 0 && 4 * c <= 4096 && kp > 0 &&
+                  al16(x) && al16(gamma) && al16(beta) && al16(xs),
+              "mmr_x3_patch_merge_ln_xs: bad arguments (c %% 4 == 0, 4c <= 4096, 16-B aligned)");
+  const int64_t nout = (int64_t)b * (hw / 2) * (hw / 2);
+  if (nout == 0) return MMR_OK;
+  return launch_patch_merge_v(x, gamma, beta, nullptr, xs, kp, nout, hw, c, eps, mmr::as_stream(stream));
 }
 
 mmr_status mmr_x3_bert_embed(const int64_t* ids, const float* word, const float* pos, const float* type0,

@@ -662,10 +662,20 @@ def _x3_linear_split_in(xr, wx, bias, residual, act, out):
     assert xr.k == Kw, f"x3_linear: K {xr.k} != weight K {Kw}"
     M = xr.rows
     npad = _L().mmr_x3_p8_npad(N)
-    assert npad > 0 and bias is not None, "x3_linear: a split operand needs N % 4 == 0 and a bias"
-    y = out if out is not None else torch.empty(xr.lead + (N,), dtype=torch.float32, device=xr.t.device)
+    if npad <= 0:
+        # N not a split-GEMM width (N % 4 != 0 or > 16384): the f32 rows back — hi + lo is exact in f32;
+        # its re-split can differ from (hi, lo) where lo rounded to half an ulp of hi (same value)
+        x = (xr.t[:, :xr.k].float() + xr.t[:, xr.kp:xr.kp + xr.k].float()).view(xr.lead + (xr.k,))
+        return x3_linear(x, wx, bias, residual=residual, act=act, out=out)
+    if bias is None:  # the split-input kernels take a bias: zeros add exactly (v + 0 = v)
+        bias = torch.zeros(npad, dtype=torch.float32, device=xr.t.device)
+    if out is not None and not out.is_contiguous():
+        out.copy_(_x3_linear_split_in(xr, wx, bias, residual, act, None))
+        return out
+    if residual is not None and not residual.is_contiguous():
+        residual = residual.contiguous()
     r2 = residual.reshape(-1, N) if residual is not None else None
-    assert y.is_contiguous() and (r2 is None or r2.is_contiguous())
+    y = out if out is not None else torch.empty(xr.lead + (N,), dtype=torch.float32, device=xr.t.device)
     _chk(_L().mmr_x3_linear_p8(_lib.ptr(xr.t), 1, _lib.ptr(wx.w3(xr.kp, npad)), _lib.ptr(wx.bias_padded(bias, npad)),
                                _lib.ptr(r2), _lib.ptr(y), M, N, xr.k, act, 0, _s(xr.t)), "mmr_x3_linear_p8")
     return y
@@ -803,6 +813,20 @@ def x3_patch_im2col(img, patch=4, kp=64):
     cols = torch.empty((B, g * g, kp), dtype=torch.float32, device=img.device)
     _chk(_L().mmr_x3_patch_im2col(_lib.ptr(img), _lib.ptr(cols), B, Cin, H, patch, kp, _s(img)), "mmr_x3_patch_im2col")
     return cols
+
+
+def x3_patch_merge_ln_split(x, g, b, eps):
+    """x3_patch_merge_ln as X3Rows (the reduction linear's split operand) when the merged token count
+    fills 256-row tiles, else f32 rows."""
+    B, H, W, C = x.shape
+    nout = B * (H // 2) * (W // 2)
+    kp = _L().mmr_x3_p8_kpad(4 * C)
+    if not (nout > 0 and nout % 256 == 0 and kp > 0 and C % 4 == 0):
+        return x3_patch_merge_ln(x, g, b, eps)
+    xs = torch.empty((nout, 2 * kp), dtype=torch.bfloat16, device=x.device)
+    _chk(_L().mmr_x3_patch_merge_ln_xs(_lib.ptr(x), _lib.ptr(g), _lib.ptr(b), _lib.ptr(xs), B, H, C, float(eps), _s(x)),
+         "mmr_x3_patch_merge_ln_xs")
+    return X3Rows(xs, 4 * C, kp, (B, H // 2, W // 2))
 
 
 def x3_patch_merge_ln(x, g, b, eps):

@@ -91,7 +91,7 @@ class SwinTowerX3:
         x = _ln(x, self.pe_g, self.pe_beta, 1e-5).view(B, g, g, -1)
         for i, st in enumerate(self.stages):
             if i > 0:
-                x = ops.x3_linear(ops.x3_patch_merge_ln(x, st["ds_g"], st["ds_b"], 1e-5), st["ds_w"])
+                x = ops.x3_linear(ops.x3_patch_merge_ln_split(x, st["ds_g"], st["ds_b"], 1e-5), st["ds_w"])
             H = x.shape[1]
             heads = cfg["num_heads"][i]
             ws = min(cfg["window_size"], H)

@@ -185,6 +185,11 @@ def test_x3_split_rows_operand_bitwise(M, C, Fw):
     assert torch.equal(ops.x3_linear(xr, wq, bq), ops.x3_linear(y, wq, bq))
     assert torch.equal(ops.x3_linear(xr, w1, b1, act=1), ops.x3_linear(y, w1, b1, act=1))
     assert torch.equal(ops.x3_ffn(xr, w1, b1, w2, b2, residual=x), ops.x3_ffn(y, w1, b1, w2, b2, residual=x))
+    # no bias (a zero bias on the split-input kernel) and a strided output: the same bits
+    assert torch.equal(ops.x3_linear(xr, wq), ops.x3_linear(y, wq))
+    o = torch.empty(3 * C, M, device=DEV).t()
+    ops.x3_linear(xr, wq, bq, out=o)
+    assert torch.equal(o, ops.x3_linear(y, wq, bq))
     torch.cuda.synchronize()
 
 
@@ -330,6 +335,31 @@ def test_x3_attention_split_rows(b, l, heads, dh, use_mask):
     torch.cuda.synchronize()
     assert isinstance(xr, ops.X3Rows)
     assert torch.equal(xr.t.view(torch.int16), _split_bits(out, xr.kp))
+
+
+@pytest.mark.parametrize("B,hw,c", [(16, 56, 96), (64, 28, 192), (256, 14, 384), (256, 14, 100), (2, 6, 52),
+                                    (2, 6, 50)])  # 12544 merged tokens = 49 x 256; 4c = 400: kp 512; c % 4 != 0
+def test_x3_patch_merge_ln(B, hw, c):
+    """timm PatchMerging (2x2 gather in x0..x3 order, LayerNorm over 4c) in f32 vs f64; the split-row
+    form (the reduction linear's operand) = the split of the f32 rows, and the reduction through it
+    equals the reduction through the f32 rows bit for bit (merged token counts of 256-row tiles)."""
+    g_ = torch.Generator().manual_seed(B * hw + c)
+    x = (torch.randn(B, hw, hw, c, generator=g_) * 2 + 0.5).to(DEV)
+    gm = (1 + 0.1 * torch.randn(4 * c, generator=g_)).to(DEV)
+    bt = (0.1 * torch.randn(4 * c, generator=g_)).to(DEV)
+    y = ops.x3_patch_merge_ln(x, gm, bt, 1e-5)
+    xd = x.double()
+    m = torch.cat([xd[:, 0::2, 0::2], xd[:, 1::2, 0::2], xd[:, 0::2, 1::2], xd[:, 1::2, 1::2]], -1)
+    ref = (m - m.mean(-1, keepdim=True)) / torch.sqrt(m.var(-1, unbiased=False, keepdim=True) + 1e-5) * gm.double() + bt.double()
+    assert _rel(y, ref) < 2e-6
+    xr = ops.x3_patch_merge_ln_split(x, gm, bt, 1e-5)
+    if not isinstance(xr, ops.X3Rows):
+        assert (B * (hw // 2) ** 2) % 256 or c % 4
+        return
+    assert torch.equal(xr.t.view(torch.int16), _split_bits(y.reshape(-1, 4 * c), xr.kp))
+    w = ops.X3W((torch.randn(2 * c, 4 * c, generator=g_) * (4 * c) ** -0.5).to(DEV))
+    assert torch.equal(ops.x3_linear(xr, w), ops.x3_linear(y, w))
+    torch.cuda.synchronize()
 
 
 def _double(sd):

@@ -43,7 +43,7 @@ names = ["linear", "layernorm", "add_layernorm", "scaled_add_layernorm", "bert_e
          "assemble_seq", "rows_to_f32", "quantize_mxfp8", "linear_mxfp8", "linear_mxfp8_q8", "layernorm_q8",
          "linear_rw", "linear_ln", "ln_row_coef", "linear_x3", "linear_x3_batched",
          "x3_linear", "x3_attention", "x3_swin_window_attention", "x3_patch_im2col", "x3_patch_merge_ln",
-         "x3_bert_embed", "x3_add_pos", "x3_assemble_seq", "x3_mean_rows", "x3_gather_rows", "x3_ffn", "x3_ln_split", "x3_attention_split", "x3_swin_window_attention_split"]
+         "x3_bert_embed", "x3_add_pos", "x3_assemble_seq", "x3_mean_rows", "x3_gather_rows", "x3_ffn", "x3_ln_split", "x3_attention_split", "x3_swin_window_attention_split", "x3_patch_merge_ln_split"]
 depth = [0]  # ops called from inside a wrapped op (x3_ffn's unfused route) are not counted twice
 
 
