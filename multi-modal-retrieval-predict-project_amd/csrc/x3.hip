@@ -539,6 +539,25 @@ __global__ __launch_bounds__(256) void x3_patch_merge_ln_v(const float* __restri
   }
 }
 
+// patch = 4 (Swin-T): one thread per 4 consecutive columns = one 16-B image row segment (kx 0..3)
+__global__ __launch_bounds__(256) void x3_im2col_p4(const float* __restrict__ img, float* __restrict__ cols,
+                                                    int64_t ntok, int cin, int hw, int kp) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int kq = kp / 4;
+  if (idx >= ntok * kq) return;
+  const int64_t tk = idx / kq;
+  const int k = 4 * (int)(idx - tk * kq);
+  const int gg = hw / 4;
+  const int64_t bi = tk / (gg * gg);
+  const int py = (int)((tk / gg) % gg), px = (int)(tk % gg);
+  float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (k < cin * 16) {
+    const int c = k / 16, ky = (k / 4) % 4;
+    val = *(const float4*)(img + ((bi * cin + c) * hw + (py * 4 + ky)) * (int64_t)hw + px * 4);
+  }
+  *(float4*)(cols + tk * kp + k) = val;
+}
+
 // HF BertEmbeddings: LN(word[id] + pos[l] + type[0]) -> f32 (one wave per token, c <= 1024)
 __global__ __launch_bounds__(256) void x3_bert_embed(const int64_t* __restrict__ ids, const float* __restrict__ word,
                                                      const float* __restrict__ pos, const float* __restrict__ type0,
@@ -580,6 +599,17 @@ __global__ __launch_bounds__(256) void x3_add_pos(const float* __restrict__ x, c
   if (i >= rows * c) return;
   const int64_t row = i / c;
   y[i] = x[i] + pos[(row % l) * c + i % c];
+}
+
+__global__ __launch_bounds__(256) void x3_add_pos4(const float* __restrict__ x, const float* __restrict__ pos,
+                                                   float* __restrict__ y, int64_t rows, int l, int c) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // 4-float chunk
+  const int c4 = c / 4;
+  if (i >= rows * c4) return;
+  const int64_t row = i / c4;
+  const int col = 4 * (int)(i - row * c4);
+  const float4 a = *(const float4*)(x + 4 * i), p = *(const float4*)(pos + (row % l) * c + col);
+  *(float4*)(y + 4 * i) = make_float4(a.x + p.x, a.y + p.y, a.z + p.z, a.w + p.w);
 }
 
 // seq (b, np + 2, c) = [x1; pf; x2] + pe (f32)
@@ -767,8 +797,12 @@ mmr_status mmr_x3_patch_im2col(const float* image, float* cols, int32_t b, int32
               "mmr_x3_patch_im2col: bad arguments");
   const int64_t ntok = (int64_t)b * (hw / patch) * (hw / patch);
   if (ntok == 0) return MMR_OK;
-  x3_im2col<<<dim3((unsigned)mmr::ceil_div(ntok * kp, 256)), 256, 0, mmr::as_stream(stream)>>>(image, cols, ntok, cin,
-                                                                                              hw, patch, kp);
+  if (patch == 4 && hw % 4 == 0 && kp % 4 == 0 && al16(image) && al16(cols))
+    x3_im2col_p4<<<dim3((unsigned)mmr::ceil_div(ntok * (kp / 4), 256)), 256, 0, mmr::as_stream(stream)>>>(
+        image, cols, ntok, cin, hw, kp);
+  else
+    x3_im2col<<<dim3((unsigned)mmr::ceil_div(ntok * kp, 256)), 256, 0, mmr::as_stream(stream)>>>(image, cols, ntok, cin,
+                                                                                                hw, patch, kp);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }
@@ -819,7 +853,11 @@ mmr_status mmr_x3_add_pos(const float* x, const float* pos, float* y, int64_t ro
   mmr::clear_error();
   MMR_REQUIRE(x && pos && y && rows >= 0 && l > 0 && c > 0, "mmr_x3_add_pos: bad arguments");
   if (rows == 0) return MMR_OK;
-  x3_add_pos<<<dim3((unsigned)mmr::ceil_div(rows * c, 256)), 256, 0, mmr::as_stream(stream)>>>(x, pos, y, rows, l, c);
+  if (c % 4 == 0 && al16(x) && al16(pos) && al16(y))
+    x3_add_pos4<<<dim3((unsigned)mmr::ceil_div(rows * (c / 4), 256)), 256, 0, mmr::as_stream(stream)>>>(x, pos, y, rows,
+                                                                                                       l, c);
+  else
+    x3_add_pos<<<dim3((unsigned)mmr::ceil_div(rows * c, 256)), 256, 0, mmr::as_stream(stream)>>>(x, pos, y, rows, l, c);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }

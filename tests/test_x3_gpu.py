@@ -362,6 +362,27 @@ def test_x3_patch_merge_ln(B, hw, c):
     torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("B,cin,hw,kp", [(3, 3, 224, 64), (2, 3, 32, 48), (2, 5, 16, 96)])
+def test_x3_patch_im2col_exact(B, cin, hw, kp):
+    """The patch-embed im2col (k = c p^2 + ky p + kx, zero columns past cin p^2) = torch's unfold, bit for bit."""
+    img = torch.randn(B, cin, hw, hw, generator=torch.Generator().manual_seed(hw + cin)).to(DEV)
+    cols = ops.x3_patch_im2col(img, 4, kp)
+    g = hw // 4
+    ref = img.view(B, cin, g, 4, g, 4).permute(0, 2, 4, 1, 3, 5).reshape(B, g * g, cin * 16)
+    torch.cuda.synchronize()
+    assert torch.equal(cols[..., :cin * 16], ref) and (cols[..., cin * 16:] == 0).all()
+
+
+@pytest.mark.parametrize("rows,l,c", [(256 * 51, 51, 768), (1000, 7, 6), (4 * 130, 130, 1024)])
+def test_x3_add_pos_exact(rows, l, c):
+    g = torch.Generator().manual_seed(rows + c)
+    x = torch.randn(rows, c, generator=g).to(DEV)
+    pos = torch.randn(l, c, generator=g).to(DEV)
+    y = ops.x3_add_pos(x, pos, l)
+    torch.cuda.synchronize()
+    assert torch.equal(y, x + pos.repeat(rows // l + 1, 1)[:rows])
+
+
 def _double(sd):
     return {k: v.double() for k, v in sd.items()}
 
