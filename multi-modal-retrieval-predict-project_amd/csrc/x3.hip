@@ -612,6 +612,22 @@ __global__ __launch_bounds__(256) void x3_add_pos4(const float* __restrict__ x, 
   *(float4*)(y + 4 * i) = make_float4(a.x + p.x, a.y + p.y, a.z + p.z, a.w + p.w);
 }
 
+// the same by 16-B chunks (c % 4 == 0)
+__global__ __launch_bounds__(256) void x3_assemble_seq4(const float* __restrict__ x1, const float* __restrict__ pf,
+                                                        const float* __restrict__ x2, const float* __restrict__ pe,
+                                                        float* __restrict__ seq, int nb, int np, int c) {
+  const int ls = np + 2, c4 = c / 4;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)nb * ls * c4) return;
+  const int64_t row = i / c4;
+  const int ch = 4 * (int)(i - row * c4);
+  const int tt = (int)(row % ls);
+  const int64_t bi = row / ls;
+  const float* src = tt == 0 ? x1 + bi * c : tt == ls - 1 ? x2 + bi * c : pf + (bi * np + tt - 1) * c;
+  const float4 v = *(const float4*)(src + ch), p = *(const float4*)(pe + (int64_t)tt * c + ch);
+  *(float4*)(seq + 4 * i) = make_float4(v.x + p.x, v.y + p.y, v.z + p.z, v.w + p.w);
+}
+
 // seq (b, np + 2, c) = [x1; pf; x2] + pe (f32)
 __global__ __launch_bounds__(256) void x3_assemble_seq(const float* __restrict__ x1, const float* __restrict__ pf,
                                                        const float* __restrict__ x2, const float* __restrict__ pe,
@@ -868,8 +884,12 @@ mmr_status mmr_x3_assemble_seq(const float* x1, const float* patches_fused, cons
   MMR_REQUIRE(x1 && patches_fused && x2 && pe && seq && b >= 0 && np > 0 && c > 0, "mmr_x3_assemble_seq: bad arguments");
   if (b == 0) return MMR_OK;
   const int64_t n = (int64_t)b * (np + 2) * c;
-  x3_assemble_seq<<<dim3((unsigned)mmr::ceil_div(n, 256)), 256, 0, mmr::as_stream(stream)>>>(x1, patches_fused, x2, pe,
-                                                                                             seq, b, np, c);
+  if (c % 4 == 0 && al16(x1) && al16(patches_fused) && al16(x2) && al16(pe) && al16(seq))
+    x3_assemble_seq4<<<dim3((unsigned)mmr::ceil_div(n / 4, 256)), 256, 0, mmr::as_stream(stream)>>>(
+        x1, patches_fused, x2, pe, seq, b, np, c);
+  else
+    x3_assemble_seq<<<dim3((unsigned)mmr::ceil_div(n, 256)), 256, 0, mmr::as_stream(stream)>>>(x1, patches_fused, x2, pe,
+                                                                                               seq, b, np, c);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }

@@ -383,6 +383,19 @@ def test_x3_add_pos_exact(rows, l, c):
     assert torch.equal(y, x + pos.repeat(rows // l + 1, 1)[:rows])
 
 
+@pytest.mark.parametrize("b,np_,c", [(256, 49, 768), (3, 5, 6)])
+def test_x3_assemble_seq_exact(b, np_, c):
+    """seq = [x1; patches; x2] + pe (fusion.py:451-468 + model.py:397), bit for bit."""
+    g = torch.Generator().manual_seed(b + c)
+    x1, x2 = torch.randn(b, c, generator=g).to(DEV), torch.randn(b, c, generator=g).to(DEV)
+    pf = torch.randn(b * np_, c, generator=g).to(DEV)
+    pe = torch.randn(np_ + 2, c, generator=g).to(DEV)
+    seq = ops.x3_assemble_seq(x1, pf, x2, pe, np_)
+    ref = torch.cat([x1[:, None], pf.view(b, np_, c), x2[:, None]], 1) + pe[None]
+    torch.cuda.synchronize()
+    assert torch.equal(seq, ref)
+
+
 def _double(sd):
     return {k: v.double() for k, v in sd.items()}
 
