@@ -162,8 +162,10 @@ class FusionStack:
             qi = _fold(wi2[sl[0]], bi2[sl[0]], g("query_img.weight"), g("query_img.bias"))
             if x3:  # the folded token-level weights in f32 (folded in f64), split for bf16x3
                 L["t_x3"] = ops.X3W(_f(torch.cat([qt[0], kt[0], vt[0]]), dev))
-                L["p_x3"] = ops.X3W(_f(torch.cat([ki[0], vi[0], qi[0]]), dev))
-                L["pp_x3"] = ops.X3W(_f(g("img_patch_proj.weight"), dev))
+                # the patch tokens' two linears (k_t2i | v_t2i | q_i2t and img_patch_proj) as ONE N = 4D
+                # GEMM: 4x the tiles of the M = B*Np launch (49 row tiles at B = 256 filled 196 of 256
+                # CUs), one split pass; each column's sum is the same K loop, so the same bits
+                L["ppp_x3"] = ops.X3W(_f(torch.cat([ki[0], vi[0], qi[0], g("img_patch_proj.weight")]), dev))
                 L["o2_x3t"] = ops.X3W(_f(g("attn_img2txt.out_proj.weight"), dev))
                 L["default_txt32"] = _f(g("default_txt_token").reshape(1, -1), dev)
             L["t_w"] = _bf(torch.cat([qt[0], kt[0], vt[0]]), dev)
@@ -171,6 +173,8 @@ class FusionStack:
             L["p_w"] = _bf(torch.cat([ki[0], vi[0], qi[0]]), dev)
             L["p_b"] = _f(torch.cat([ki[1], vi[1], qi[1]]), dev)
             L["pp_w"], L["pp_b"] = _bf(g("img_patch_proj.weight"), dev), _f(g("img_patch_proj.bias"), dev)
+            if x3:
+                L["ppp_b"] = torch.cat([L["p_b"], L["pp_b"]])
             L["o1_w"], L["o1_b"] = _f(g("attn_txt2img.out_proj.weight"), dev), _f(g("attn_txt2img.out_proj.bias"), dev)
             L["o2_wb"] = _bf(g("attn_img2txt.out_proj.weight"), dev)
             if fp8:
@@ -342,8 +346,8 @@ class FusionStack:
         cls = None
         for i, L in enumerate(self.layers):
             Pe = L["patch"].x3(P, B, Np, eps)                                # (B*Np, Ci) f32
-            PQ = ops.x3_linear(Pe, L["p_x3"], L["p_b"])                     # k_t2i | v_t2i | q_i2t
-            PP = ops.x3_linear(Pe, L["pp_x3"], L["pp_b"])                   # img_patch_proj
+            PQPP = ops.x3_linear(Pe, L["ppp_x3"], L["ppp_b"])              # k_t2i | v_t2i | q_i2t | img_patch_proj
+            PQ, PP = PQPP[:, :3 * D], PQPP[:, 3 * D:].contiguous()
             if txt_feats is None:  # learnable default text token (fusion.py:404-407)
                 T, Lt = L["default_txt32"].expand(B, -1).contiguous(), 1
             else:
