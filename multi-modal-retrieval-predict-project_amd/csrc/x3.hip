@@ -30,7 +30,10 @@
 namespace {
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 // f32 x4 -> (hi, lo) bf16 x4 each, packed as two dwords
 __device__ __forceinline__ void split4(const float4 v, uint2& hi, uint2& lo) {
@@ -421,6 +424,312 @@ __global__ __launch_bounds__(256) void x3_attention(const AttnArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ attention, round 5 (x3_mha)
+// The bf16 core's structure (fusion.hip mha_small) on bf16x3 operands.  Block = (sequence or window,
+// head); nwv = min(4, ceil(lq / 32)) waves, one 32-query tile per wave, the block walking its query
+// chunks of 32 nwv rows (one chunk up to lq = 128; the mean then reduces in a fixed order inside the
+// block).  S^T = K . Q^T on v_mfma_f32_32x32x16_bf16 as Kh.Qh + Kh.Ql + Kl.Qh puts the query on the
+// lane: the softmax (f32, expf, online over 64-key sub-blocks of kbs-key staged blocks) stays in
+// registers, and P^T is split in registers into the B operands of O^T += V^T . P^T (Vh.Ph + Vh.Pl +
+// Vl.Ph), V^T read from key-major hi / lo images by ds_read_b64_tr_b16 in P^T's key permutation.
+// K / V f32 rows are split ONCE per block while staged (16-B LDS writes), Q once per wave in registers.
+// (The round-4 kernel above ran 16-query tiles on 16x16x32 MFMAs with P re-split through LDS by
+// 2-byte stores and V^T written by 2-byte transposing stores: 0.06 of the bf16 MFMA peak.)
+// MODE 0: plain (nn.MultiheadAttention); 1: key-padding mask as HF's additive finfo.min (a row with
+// every key masked -> HF's uniform softmax, the mean of V over the lk keys); 2: Swin windows (roll /
+// partition folded into the token map, q pre-scaled as timm, rel-pos + shift-mask bias added).
+template <int DT, int MODE>
+__global__ __launch_bounds__(256, 2) void x3_mha(const AttnArgs a, int kbs) {
+  constexpr int DHP = DT * 32, KS = DHP / 16, KROW = DHP + 8, VROW = DHP + ((DT & 1) ? 0 : 16);
+  constexpr int C8 = DHP / 8, OROW = DHP + 4;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6, nwv = nthr >> 6;
+  uint16_t* Kh = (uint16_t*)smem;  // [kbs][KROW]
+  uint16_t* Kl = Kh + kbs * KROW;
+  uint16_t* Vh = Kl + kbs * KROW;  // [kbs][VROW], key-major
+  uint16_t* Vl = Vh + kbs * VROW;
+  const int kv_bytes = kbs * (KROW + VROW) * 4, epi_bytes = nwv * 32 * OROW * 4;
+  float* msum = (float*)(smem + (kv_bytes > epi_bytes ? kv_bytes : epi_bytes));  // [nwv][DHP]
+  float* madd = msum + nwv * DHP;                                                  // [kbs] (MODE 1)
+  const int unit = mmr::xcd_contiguous((int)blockIdx.x, (int)gridDim.x);
+  const int head = unit % a.heads;
+  const int64_t bb = unit / a.heads;
+  const int lq = a.lq, lk = a.lk, dh = a.dh;
+  int64_t sw_base = 0;
+  int wy = 0, wx = 0, type = 0;
+  if constexpr (MODE == 2) {
+    const int nwin1 = a.hw / a.ws, nwin = nwin1 * nwin1;
+    const int win = (int)(bb % nwin);
+    sw_base = (bb / nwin) * (int64_t)a.hw * a.hw;
+    wy = win / nwin1;
+    wx = win % nwin1;
+    type = a.shift > 0 ? ((wy == nwin1 - 1) ? 2 : 0) + ((wx == nwin1 - 1) ? 1 : 0) : 0;
+  }
+  auto qtok = [&](int i) -> int64_t {
+    if constexpr (MODE == 2) {
+      const int hr = wy * a.ws + i / a.ws, wr = wx * a.ws + i % a.ws;
+      return sw_base + (int64_t)((hr + a.shift) % a.hw) * a.hw + (wr + a.shift) % a.hw;
+    } else {
+      return bb * lq + i;
+    }
+  };
+  auto ktok = [&](int j) -> int64_t {
+    if constexpr (MODE == 2) return qtok(j);
+    else return bb * lk + j;
+  };
+  const float* qb = a.q + head * dh;
+  const float* kb = a.k + head * dh;
+  const float* vb = a.v + head * dh;
+  const int r = lane & 31, hf = lane >> 5;
+  const int lkp = (lk + 31) & ~31;
+  // MODE 1: a sequence with no unmasked key keeps every key tile (uniform softmax, as HF)
+  bool anyv = true;
+  if constexpr (MODE == 1) {
+    int f = 0;
+    for (int j = tid; j < lk; j += nthr) f |= a.kmask[bb * lk + j] != 0;
+    anyv = __syncthreads_or(f) != 0;
+  }
+  if (a.mean_out)
+    for (int d = lane; d < DHP; d += 64) msum[wave * DHP + d] = 0.f;
+
+  // kn keys from k0 (kn % 32 == 0): f32 rows -> hi / lo images, 8 elements per chunk, 4 chunks per
+  // thread in flight (keys past lk / columns past dh read a clamped in-bounds chunk; columns past dh
+  // are zeroed, keys past lk are -inf in the scores)
+  auto stage = [&](int k0, int kn) {
+    constexpr int UB = DT >= 3 ? 2 : 4;  // chunks in flight per thread (register budget at DT 3 / 4)
+    const int nch = kn * C8, tot = 2 * nch;
+    for (int e0 = tid; e0 < tot; e0 += UB * nthr) {
+      float4 xa[UB], xb[UB];
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int e = e0 + u * nthr < tot ? e0 + u * nthr : 0;
+        const bool isv = e >= nch;
+        const int e2 = isv ? e - nch : e;
+        const int key = e2 / C8, d = (e2 % C8) * 8;
+        const int j = k0 + key < lk ? k0 + key : lk - 1;
+        const float* src = (isv ? vb + ktok(j) * a.ldv : kb + ktok(j) * a.ldk) + (d < dh ? d : 0);
+        xa[u] = *(const float4*)src;
+        xb[u] = *(const float4*)(src + 4);
+      }
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int e = e0 + u * nthr;
+        if (e < tot) {
+          const bool isv = e >= nch;
+          const int e2 = isv ? e - nch : e;
+          const int key = e2 / C8, d = (e2 % C8) * 8;
+          if (d >= dh) xa[u] = xb[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+          bf16x8 h, l;
+          split8(xa[u], xb[u], h, l);
+          const int off = isv ? key * VROW + d : key * KROW + d;
+          *(bf16x8*)((isv ? Vh : Kh) + off) = h;
+          *(bf16x8*)((isv ? Vl : Kl) + off) = l;
+        }
+      }
+    }
+    if constexpr (MODE == 1)
+      for (int i = tid; i < kn; i += nthr) {
+        const int key = k0 + i;
+        madd[i] = key >= lk ? -INFINITY : (a.kmask[bb * lk + key] != 0 ? 0.f : -FLT_MAX);
+      }
+  };
+
+  const int grp = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+  for (int qc = 0; qc < lq; qc += 32 * nwv) {
+    const int q0 = qc + wave * 32;
+    const bool active = q0 < lq;  // wave-uniform
+    const int qi = q0 + r < lq ? q0 + r : lq - 1;
+    // Q^T fragments: lane (query r, half hf) holds d = 16 ks + 8 hf .. + 7, split in registers
+    bf16x8 qh[KS], ql[KS];
+    {
+      const float* qrow = qb + qtok(qi) * a.ldq;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int d = 16 * ks + 8 * hf;
+        float4 x0 = *(const float4*)(qrow + (d < dh ? d : 0)), x1 = *(const float4*)(qrow + (d < dh ? d : 0) + 4);
+        if (d >= dh) x0 = x1 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (MODE == 2) {  // timm scales q before q k^T
+          x0 = make_float4(x0.x * a.scale, x0.y * a.scale, x0.z * a.scale, x0.w * a.scale);
+          x1 = make_float4(x1.x * a.scale, x1.y * a.scale, x1.z * a.scale, x1.w * a.scale);
+        }
+        split8(x0, x1, qh[ks], ql[ks]);
+      }
+    }
+    f32x16 o[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[dt] = (f32x16){0};
+    float m_run = -INFINITY, l_run = 0.f;
+    for (int k0 = 0; k0 < lkp; k0 += kbs) {
+      const int kn = min(kbs, lkp - k0);
+      __syncthreads();  // previous key block / previous chunk's epilogue done with the LDS
+      stage(k0, kn);
+      __syncthreads();
+      if (!active) continue;
+      for (int kb0 = 0; kb0 < kn; kb0 += 64) {
+        const int nt = min(64, kn - kb0) / 32;
+        bool live[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          live[t] = t < nt;
+          // fully masked 32-key tiles contribute exactly 0 once the row has an unmasked key
+          if (MODE == 1 && live[t] && anyv) live[t] = __ballot(madd[kb0 + t * 32 + r] == 0.f) != 0;
+        }
+        f32x16 s[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          s[t] = (f32x16){0};
+          if (live[t]) {
+            const int key = kb0 + t * 32 + r;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+              const bf16x8 kh = *(const bf16x8*)(Kh + key * KROW + 16 * ks + 8 * hf);
+              const bf16x8 kl = *(const bf16x8*)(Kl + key * KROW + 16 * ks + 8 * hf);
+              s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, qh[ks], s[t], 0, 0, 0);
+              s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, ql[ks], s[t], 0, 0, 0);
+              s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl, qh[ks], s[t], 0, 0, 0);
+            }
+          }
+        }
+        // scores (lane: query r; register rg: key kb0 + 32 t + (rg & 3) + 8 (rg >> 2) + 4 hf)
+        float mloc = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          if (!live[t]) continue;
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4) {
+            const int kl0 = kb0 + t * 32 + 8 * g4 + 4 * hf;  // local key of register 4 g4
+            float4 add = make_float4(0.f, 0.f, 0.f, 0.f);
+            if constexpr (MODE == 1) add = *(const float4*)(madd + kl0);
+            if constexpr (MODE == 2) {
+              const int kc = k0 + kl0 < 64 ? k0 + kl0 : 60;
+              add = *(const float4*)(a.bias + (((int64_t)type * a.heads + head) * 64 + (qi < 64 ? qi : 63)) * 64 + kc);
+            }
+            const float ad[4] = {add.x, add.y, add.z, add.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float x = s[t][4 * g4 + e];
+              if constexpr (MODE == 2) x += ad[e];
+              else x = x * a.scale + ad[e];
+              if (MODE != 1 && k0 + kl0 + e >= lk) x = -INFINITY;
+              s[t][4 * g4 + e] = x;
+              mloc = fmaxf(mloc, x);
+            }
+          }
+        }
+        mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+        const float m_new = fmaxf(m_run, mloc);
+        const float alpha = m_run == -INFINITY ? 0.f : expf(m_run - m_new);
+        m_run = m_new;
+        float psum = 0.f;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          if (!live[t]) continue;
+#pragma unroll
+          for (int rg = 0; rg < 16; ++rg) {
+            const float x = s[t][rg];
+            const float p = (x == -INFINITY || m_new == -INFINITY) ? 0.f : expf(x - m_new);
+            s[t][rg] = p;
+            psum += p;
+          }
+        }
+        l_run = l_run * alpha + psum;
+        if (k0 + kb0 > 0) {
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+        }
+        // O^T[d][q] += V^T[d][key] . P^T[key][q] (three products), P^T split in registers
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          if (!live[t]) continue;
+#pragma unroll
+          for (int sidx = 0; sidx < 2; ++sidx) {
+            uint32_t ph[4], pl[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float v0 = s[t][8 * sidx + 2 * j], v1 = s[t][8 * sidx + 2 * j + 1];
+              ph[j] = mmr::pack2bf(v0, v1);
+              pl[j] = mmr::pack2bf(v0 - __uint_as_float(ph[j] << 16), v1 - __uint_as_float(ph[j] & 0xFFFF0000u));
+            }
+            const bf16x8 pfh = __builtin_bit_cast(bf16x8, make_uint4(ph[0], ph[1], ph[2], ph[3]));
+            const bf16x8 pfl = __builtin_bit_cast(bf16x8, make_uint4(pl[0], pl[1], pl[2], pl[3]));
+            const int r0 = kb0 + t * 32 + 16 * sidx + 4 * (grp >> 1);
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+              const int off = (r0 + tq) * VROW + dt * 32 + (grp & 1) * 16 + 4 * tp;
+              const bf16x4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(Vh + off));
+              const bf16x4 h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(Vh + off + 8 * VROW));
+              const bf16x4 l0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(Vl + off));
+              const bf16x4 l1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(Vl + off + 8 * VROW));
+              const bf16x8 vfh = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+              const bf16x8 vfl = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+              o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfh, pfh, o[dt], 0, 0, 0);
+              o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfh, pfl, o[dt], 0, 0, 0);
+              o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfl, pfh, o[dt], 0, 0, 0);
+            }
+          }
+        }
+      }
+    }
+    // epilogue: the wave's O tile (f32, / l) staged [32 q][OROW] over the K / V image, then written as
+    // row chunks (f32 rows and / or the split operand rows [hi | lo]) and summed for the mean
+    __syncthreads();
+    if (active) {
+      float* st = (float*)smem + wave * 32 * OROW;
+      const float inv = 1.0f / (l_run + __shfl_xor(l_run, 32, 64));
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4)
+          *(float4*)(st + r * OROW + dt * 32 + 8 * g4 + 4 * hf) =
+              make_float4(o[dt][4 * g4] * inv, o[dt][4 * g4 + 1] * inv, o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes landed
+      __builtin_amdgcn_wave_barrier();
+      const int nc4 = dh / 4;
+      if (a.out != nullptr || a.xs != nullptr)
+        for (int c = lane; c < 32 * nc4; c += 64) {
+          const int row = c / nc4, ch = c - row * nc4;
+          if (q0 + row >= lq) continue;
+          const float4 v = *(const float4*)(st + row * OROW + 4 * ch);
+          const int64_t tk = qtok(q0 + row);
+          if (a.xs != nullptr) {
+            uint2 h, l;
+            split4(v, h, l);
+            uint16_t* xr = a.xs + tk * 2 * a.kp + head * dh + 4 * ch;
+            *(uint2*)xr = h;
+            *(uint2*)(xr + a.kp) = l;
+          } else {
+            *(float4*)(a.out + tk * a.ldo + head * dh + 4 * ch) = v;
+          }
+        }
+      if (a.xs != nullptr && head == a.heads - 1) {  // zero columns heads*dh .. kp of these rows
+        const int z0 = a.heads * dh, nz4 = (a.kp - z0) / 4;
+        for (int c = lane; c < 32 * nz4; c += 64) {
+          const int row = c / nz4, ch = c - row * nz4;
+          if (q0 + row >= lq) continue;
+          uint16_t* xr = a.xs + qtok(q0 + row) * 2 * a.kp + z0 + 4 * ch;
+          *(uint2*)xr = make_uint2(0u, 0u);
+          *(uint2*)(xr + a.kp) = make_uint2(0u, 0u);
+        }
+      }
+      if (a.mean_out != nullptr)
+        for (int d = lane; d < DHP; d += 64) {
+          float acc = msum[wave * DHP + d];
+          for (int row = 0; row < 32; ++row)
+            if (q0 + row < lq) acc += st[row * OROW + d];
+          msum[wave * DHP + d] = acc;
+        }
+    }
+  }
+  if (a.mean_out != nullptr) {
+    __syncthreads();
+    for (int d = tid; d < dh; d += nthr) {
+      float sm = 0.f;
+      for (int w = 0; w < nwv; ++w) sm += msum[w * DHP + d];  // fixed order: deterministic
+      a.mean_out[bb * (int64_t)a.heads * dh + head * dh + d] = sm / lq;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ small f32 kernels
 // im2col of the patch-embed conv: (b, cin, hw, hw) -> (b * g * g, kp) f32, k = c p^2 + ky p + kx,
 // zero for k >= cin p^2
@@ -678,11 +987,42 @@ mmr_status launch_attention(const char* who, AttnArgs a, int64_t nbh, bool swin,
               "%s: rows must be 16-B aligned with strides >= heads*dh", who);
   if (nbh == 0) return MMR_OK;
   const int dt = (a.dh + 31) / 32;
+  hipStream_t st = mmr::as_stream(stream);
+  if (mmr::pin_x3_attn.load(std::memory_order_relaxed) != 1) {
+    MMR_REQUIRE(!swin || dt == 1, "%s: Swin head_dim %d must be <= 32", who, a.dh);
+    const int nwv = std::min(4, (a.lq + 31) / 32);
+    const int lkp = (a.lk + 31) & ~31;
+    const int kbs = dt <= 2 ? std::min(128, lkp) : std::min(64, lkp);
+    const int dhp = 32 * dt, krow = dhp + 8, vrow = dhp + ((dt & 1) ? 0 : 16), orow = dhp + 4;
+    const size_t kv = (size_t)kbs * (krow + vrow) * 4, epi = (size_t)nwv * 32 * orow * 4;
+    const size_t lds = std::max(kv, epi) + (size_t)nwv * dhp * 4 + (size_t)kbs * 4;
+    const dim3 grid((unsigned)nbh), blk(64 * nwv);
+    const int mode = swin ? 2 : (a.kmask ? 1 : 0);
+#define XM(D_, M_) x3_mha<D_, M_><<<grid, blk, lds, st>>>(a, kbs)
+    if (mode == 2) XM(1, 2);
+    else if (mode == 1) {
+      switch (dt) {
+        case 1: XM(1, 1); break;
+        case 2: XM(2, 1); break;
+        case 3: XM(3, 1); break;
+        default: XM(4, 1); break;
+      }
+    } else {
+      switch (dt) {
+        case 1: XM(1, 0); break;
+        case 2: XM(2, 0); break;
+        case 3: XM(3, 0); break;
+        default: XM(4, 0); break;
+      }
+    }
+#undef XM
+    MMR_LAUNCH_CHECK();
+    return MMR_OK;
+  }
   const int DH = 32 * dt;
   const size_t lds = (size_t)2 * 64 * (DH + 8) * 2 + (size_t)2 * DH * 72 * 2 + (size_t)2 * 4 * 16 * 72 * 2 +
                      (size_t)4 * DH * 4;
   const dim3 grid((unsigned)nbh);
-  hipStream_t st = mmr::as_stream(stream);
   if (swin) {
     MMR_REQUIRE(dt == 1, "%s: Swin head_dim %d must be <= 32", who, a.dh);
     x3_attention<1, true><<<grid, 256, lds, st>>>(a);

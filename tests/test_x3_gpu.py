@@ -252,6 +252,36 @@ def test_x3_attention_vs_f64(b, lq, lk, heads, dh, use_mask, mean):
         assert _rel(m, ref.mean(1)) <= 5e-5
 
 
+@pytest.mark.parametrize("lq,lk,dh", [(40, 40, 64), (128, 128, 64), (7, 70, 96)])
+def test_x3_attention_all_masked_row_is_hf_uniform(lq, lk, dh):
+    """HF BertSelfAttention adds (1 - mask) * finfo(f32).min to the scaled scores: a sequence whose keys
+    are ALL masked gets a uniform softmax (every score rounds to finfo.min), i.e. the mean of V over the lk
+    keys — not zeros.  f64 restatement of that additive mask; batch 1 keeps a partial mask, batch 2 none
+    (parity unpinned: the reference holds no fixture for an all-zero attention_mask)."""
+    b, heads = 3, 2
+    g = torch.Generator().manual_seed(lq + lk + dh)
+    C = heads * dh
+    q = torch.randn(b * lq, C, generator=g) * 0.7
+    k = torch.randn(b * lk, C, generator=g) * 0.7
+    v = torch.randn(b * lk, C, generator=g) * 0.7
+    mask = torch.ones(b, lk, dtype=torch.int64)
+    mask[0] = 0
+    mask[1, lk // 3:] = 0
+    scale = 1.0 / math.sqrt(dh)
+    qh = q.double().view(b, lq, heads, dh).transpose(1, 2)
+    kh = k.double().view(b, lk, heads, dh).transpose(1, 2)
+    vh = v.double().view(b, lk, heads, dh).transpose(1, 2)
+    s = qh @ kh.transpose(-1, -2) * scale + (1.0 - mask.double())[:, None, None, :] * torch.finfo(torch.float32).min
+    ref = (s.softmax(-1) @ vh).transpose(1, 2).reshape(b, lq, C)
+    assert torch.allclose(ref[0], vh[0].mean(1).reshape(1, C).expand(lq, C))
+    out = torch.empty((b * lq, C), dtype=torch.float32, device=DEV)
+    m = torch.empty((b, C), dtype=torch.float32, device=DEV)
+    ops.x3_attention(q.to(DEV), k.to(DEV), v.to(DEV), b, lq, lk, heads, dh, scale, out=out, mean_out=m,
+                     mask=mask.to(DEV))
+    assert _rel(out.view(b, lq, C), ref) <= 5e-5
+    assert _rel(m, ref.mean(1)) <= 5e-5
+
+
 @pytest.mark.parametrize("hw,c,heads,shift", [(56, 96, 3, 0), (56, 96, 3, 3), (14, 384, 12, 3), (7, 768, 24, 0)])
 def test_x3_swin_window_attention_vs_f64(hw, c, heads, shift):
     """roll(-shift) / window partition / q*dh^-0.5 k^T + rel-pos bias + shift mask / softmax / v /
