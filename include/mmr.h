@@ -462,12 +462,13 @@ mmr_status mmr_ln_rows(const void* x, int64_t ldx, const float* alpha, const voi
                        const float* post_scale, void* y, int64_t ldy, int64_t rows, int32_t c, float eps,
                        int32_t io_bf16, int32_t groups, int64_t group_div, void* stream);
 
-/* f32 y = LayerNorm(x + residual) (residual may be NULL, y may be NULL) that also writes xs, the
- * x3 split GEMM's x_hilo operand: [hi | lo] bf16 rows 2 kp wide (kp = mmr_x3_p8_kpad(c), zero columns
- * c..kp), the split mmr_x3_split_rows would make of y.  c % 4 == 0, c <= 1024; rows 16-B aligned. */
-mmr_status mmr_ln_rows_split(const float* x, int64_t ldx, const float* residual, int64_t ldr, const float* gamma,
-                             const float* beta, float* y, int64_t ldy, uint16_t* xs, int64_t rows, int32_t c, float eps,
-                             void* stream);
+/* f32 y = LayerNorm(alpha * x + residual) (alpha: a DEVICE f32 scalar or NULL = 1; residual may be NULL,
+ * y may be NULL) that also writes xs, the x3 split GEMM's x_hilo operand: [hi | lo] bf16 rows 2 kp wide
+ * (kp = mmr_x3_p8_kpad(c), zero columns c..kp), the split mmr_x3_split_rows would make of y.
+ * c % 4 == 0, c <= 1024; rows 16-B aligned. */
+mmr_status mmr_ln_rows_split(const float* x, int64_t ldx, const float* alpha, const float* residual, int64_t ldr,
+                             const float* gamma, const float* beta, float* y, int64_t ldy, uint16_t* xs, int64_t rows,
+                             int32_t c, float eps, void* stream);
 
 /* seq (b, np+2, c) bf16 = [x1; patches_fused; x2] + pe[0..np+2) (fusion.py:468 + model.py:397);
  * x1, x2 f32 (b, c), patches_fused bf16 (b*np, c), pe f32 [>= np+2][c]. */
@@ -530,8 +531,8 @@ mmr_status mmr_x3_swin_window_attention(const float* qkv, const float* bias, flo
  * input): xs = [hi | lo] bf16 rows 2 kp wide, kp = mmr_x3_p8_kpad(heads*dh) (columns heads*dh..kp zero),
  * the split mmr_x3_split_rows would make of the f32 output. */
 mmr_status mmr_x3_attention_xs(const float* q, int64_t ldq, const float* k, int64_t ldk, const float* v, int64_t ldv,
-                               uint16_t* xs, const int64_t* mask01, int32_t b, int32_t lq, int32_t lk, int32_t heads,
-                               int32_t dh, float scale, void* stream);
+                               uint16_t* xs, float* mean_out, const int64_t* mask01, int32_t b, int32_t lq, int32_t lk,
+                               int32_t heads, int32_t dh, float scale, void* stream);  /* mean_out may be NULL */
 mmr_status mmr_x3_swin_window_attention_xs(const float* qkv, const float* bias, uint16_t* xs, int32_t b, int32_t hw,
                                            int32_t c, int32_t heads, int32_t ws, int32_t shift, void* stream);
 /* Patch-embed im2col, f32: (b, cin, hw, hw) -> (b*(hw/patch)^2, kp) columns (k = c*p^2 + ky*p + kx, zero
@@ -551,9 +552,16 @@ mmr_status mmr_x3_bert_embed(const int64_t* ids, const float* word, const float*
                              void* stream);
 /* y = x + pos[row % l], f32 (rows, c). */
 mmr_status mmr_x3_add_pos(const float* x, const float* pos, float* y, int64_t rows, int32_t l, int32_t c, void* stream);
+/* The same written as the x3 split GEMM's operand: xs = [hi | lo] bf16 rows 2 kp wide (kp =
+ * mmr_x3_p8_kpad(c), zero columns c..kp), plus the f32 rows y when y != NULL; c % 4 == 0, 16-B aligned. */
+mmr_status mmr_x3_add_pos_split(const float* x, const float* pos, float* y, uint16_t* xs, int64_t rows, int32_t l,
+                                int32_t c, void* stream);
 /* seq (b, np+2, c) f32 = [x1; patches_fused; x2] + pe. */
 mmr_status mmr_x3_assemble_seq(const float* x1, const float* patches_fused, const float* x2, const float* pe,
                                float* seq, int32_t b, int32_t np, int32_t c, void* stream);
+/* The same written only as the combiner QKV GEMM's x3 split operand rows (as mmr_x3_add_pos_split). */
+mmr_status mmr_x3_assemble_seq_split(const float* x1, const float* patches_fused, const float* x2, const float* pe,
+                                     uint16_t* xs, int32_t b, int32_t np, int32_t c, void* stream);
 /* y (b, c) = (extra[b] + sum_t x[b][t]) / (l + 1) with extra (b, c), or sum_t x[b][t] / l when extra is
  * NULL; x (b, l, c) f32, summed in token order (unmasked token mean, model.py:370; the Swin global /
  * pooled means, fusion.py:263-265, model.py:463-468). */

@@ -85,7 +85,7 @@ SIGNATURES = {
                    c_i32, c_f32, c_vp],
     "mmr_add_pos_bf16": [c_vp, c_i32, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp],
     "mmr_add_pos_bf16_q8": [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp],
-    "mmr_ln_rows_split": [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_f32, c_vp],
+    "mmr_ln_rows_split": [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_f32, c_vp],
     "mmr_ln_rows": [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_i64, c_i32, c_f32,
                     c_i32, c_i32, c_i64, c_vp],
     "mmr_linear_f32_batched": [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,
@@ -100,8 +100,8 @@ SIGNATURES = {
     "mmr_x3_linear_p8": [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_x3_attention": [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32,
                          c_i32, c_f32, c_vp],
-    "mmr_x3_attention_xs": [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_f32,
-                            c_vp],
+    "mmr_x3_attention_xs": [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32,
+                            c_f32, c_vp],
     "mmr_x3_swin_window_attention_xs": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_x3_swin_window_attention": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_x3_patch_im2col": [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp],
@@ -109,7 +109,9 @@ SIGNATURES = {
     "mmr_x3_patch_merge_ln_xs": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp],
     "mmr_x3_bert_embed": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_vp],
     "mmr_x3_add_pos": [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp],
+    "mmr_x3_add_pos_split": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp],
     "mmr_x3_assemble_seq": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
+    "mmr_x3_assemble_seq_split": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
     "mmr_x3_mean_rows": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
     "mmr_x3_gather_rows": [c_vp, c_i64, c_vp, c_i32, c_i32, c_vp],
 }

@@ -591,7 +591,8 @@ __global__ __launch_bounds__(256) void ln_rows_s(const float* __restrict__ x, in
 // the split mmr_x3_split_rows would make of the f32 output, which is written too when y != NULL.
 // 32 lanes per row, NCH = kp / 128 4-wide chunks per lane (lane j: columns 4 (j + 32 i) ..+3).
 template <int NCH>
-__global__ __launch_bounds__(256) void ln_rows_split(const float* __restrict__ x, int64_t ldx, const float* __restrict__ r,
+__global__ __launch_bounds__(256) void ln_rows_split(const float* __restrict__ x, int64_t ldx,
+                                                     const float* __restrict__ alpha, const float* __restrict__ r,
                                                      int64_t ldr, const float* __restrict__ g, const float* __restrict__ b,
                                                      float* __restrict__ y, int64_t ldy, uint16_t* __restrict__ xs,
                                                      int64_t rows, int c, float eps) {
@@ -605,6 +606,11 @@ __global__ __launch_bounds__(256) void ln_rows_split(const float* __restrict__ x
   for (int i = 0; i < NCH; ++i) {
     const int col = 4 * (j + 32 * i);
     v[i] = col < c ? *(const float4*)(x + rw * ldx + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (alpha) {  // LN(alpha x + r) (PreFusionEnhancer, fusion.py:33): the product rounded, then the sum
+    const float av = *alpha;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) v[i] = make_float4(av * v[i].x, av * v[i].y, av * v[i].z, av * v[i].w);
   }
   if (r) {
 #pragma unroll
@@ -924,7 +930,8 @@ mmr_status mmr_ln_rows(const void* x, int64_t ldx, const float* alpha, const voi
   return MMR_OK;
 }
 
-mmr_status mmr_ln_rows_split(const float* x, int64_t ldx, const float* residual, int64_t ldr, const float* gamma,
+mmr_status mmr_ln_rows_split(const float* x, int64_t ldx, const float* alpha, const float* residual, int64_t ldr,
+                             const float* gamma,
                              const float* beta, float* y, int64_t ldy, uint16_t* xs, int64_t rows, int32_t c, float eps,
                              void* stream) {
   mmr::clear_error();
@@ -937,7 +944,8 @@ mmr_status mmr_ln_rows_split(const float* x, int64_t ldx, const float* residual,
   const int nch = (c + 127) / 128;
   const dim3 grid((unsigned)mmr::ceil_div(rows, 8));
   hipStream_t st = mmr::as_stream(stream);
-#define LNSP(N_) ln_rows_split<N_><<<grid, 256, 0, st>>>(x, ldx, residual, ldr, gamma, beta, y, ldy, xs, rows, c, eps)
+#define LNSP(N_) \
+  ln_rows_split<N_><<<grid, 256, 0, st>>>(x, ldx, alpha, residual, ldr, gamma, beta, y, ldy, xs, rows, c, eps)
   switch (nch) {
     case 1: LNSP(1); break;
     case 2: LNSP(2); break;

@@ -937,6 +937,53 @@ __global__ __launch_bounds__(256) void x3_assemble_seq4(const float* __restrict_
   *(float4*)(seq + 4 * i) = make_float4(v.x + p.x, v.y + p.y, v.z + p.z, v.w + p.w);
 }
 
+// The split-operand forms (round 5): the same sums written as the x3 split GEMM's [hi | lo] operand rows
+// (2 kp wide, zero columns c..kp) — and, for add-pos, the f32 rows too when y != NULL (the enhancer's
+// LayerNorm residual) — so the in-proj / combiner QKV GEMMs skip their split pass.  One thread per
+// 4-column chunk of the kp-wide row.
+__device__ __forceinline__ void store_split4(uint16_t* xr, int kp, const float4 v) {
+  uint2 h, l;
+  split4(v, h, l);
+  *(uint2*)xr = h;
+  *(uint2*)(xr + kp) = l;
+}
+
+__global__ __launch_bounds__(256) void x3_add_pos_split(const float* __restrict__ x, const float* __restrict__ pos,
+                                                        float* __restrict__ y, uint16_t* __restrict__ xs, int64_t rows,
+                                                        int l, int c, int kp) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int k4 = kp / 4;
+  if (i >= rows * k4) return;
+  const int64_t row = i / k4;
+  const int col = 4 * (int)(i - row * k4);
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col < c) {
+    const float4 a = *(const float4*)(x + row * c + col), p = *(const float4*)(pos + (row % l) * c + col);
+    v = make_float4(a.x + p.x, a.y + p.y, a.z + p.z, a.w + p.w);
+    if (y) *(float4*)(y + row * c + col) = v;
+  }
+  store_split4(xs + row * 2 * kp + col, kp, v);
+}
+
+__global__ __launch_bounds__(256) void x3_assemble_seq_split(const float* __restrict__ x1, const float* __restrict__ pf,
+                                                             const float* __restrict__ x2, const float* __restrict__ pe,
+                                                             uint16_t* __restrict__ xs, int nb, int np, int c, int kp) {
+  const int ls = np + 2, k4 = kp / 4;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)nb * ls * k4) return;
+  const int64_t row = i / k4;
+  const int ch = 4 * (int)(i - row * k4);
+  const int tt = (int)(row % ls);
+  const int64_t bi = row / ls;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ch < c) {
+    const float* src = tt == 0 ? x1 + bi * c : tt == ls - 1 ? x2 + bi * c : pf + (bi * np + tt - 1) * c;
+    const float4 a = *(const float4*)(src + ch), p = *(const float4*)(pe + (int64_t)tt * c + ch);
+    v = make_float4(a.x + p.x, a.y + p.y, a.z + p.z, a.w + p.w);
+  }
+  store_split4(xs + row * 2 * kp + ch, kp, v);
+}
+
 // seq (b, np + 2, c) = [x1; pf; x2] + pe (f32)
 __global__ __launch_bounds__(256) void x3_assemble_seq(const float* __restrict__ x1, const float* __restrict__ pf,
                                                        const float* __restrict__ x2, const float* __restrict__ pe,
@@ -1123,12 +1170,12 @@ mmr_status mmr_x3_swin_window_attention(const float* qkv, const float* bias, flo
 }
 
 mmr_status mmr_x3_attention_xs(const float* q, int64_t ldq, const float* k, int64_t ldk, const float* v, int64_t ldv,
-                               uint16_t* xs, const int64_t* mask01, int32_t b, int32_t lq, int32_t lk, int32_t heads,
-                               int32_t dh, float scale, void* stream) {
+                               uint16_t* xs, float* mean_out, const int64_t* mask01, int32_t b, int32_t lq, int32_t lk,
+                               int32_t heads, int32_t dh, float scale, void* stream) {
   mmr::clear_error();
   const int kp = mmr_x3_p8_kpad(heads * dh);
   MMR_REQUIRE(xs && b >= 0 && kp > 0, "mmr_x3_attention_xs: bad arguments (heads*dh=%d)", heads * dh);
-  AttnArgs a{q, ldq, k, ldk, v, ldv, nullptr, 0, nullptr, mask01, nullptr, lq, lk, heads, dh, scale, 0, 1, 0, xs, kp};
+  AttnArgs a{q, ldq, k, ldk, v, ldv, nullptr, 0, mean_out, mask01, nullptr, lq, lk, heads, dh, scale, 0, 1, 0, xs, kp};
   return launch_attention("mmr_x3_attention_xs", a, (int64_t)b * heads, false, stream);
 }
 
@@ -1214,6 +1261,35 @@ mmr_status mmr_x3_add_pos(const float* x, const float* pos, float* y, int64_t ro
                                                                                                        l, c);
   else
     x3_add_pos<<<dim3((unsigned)mmr::ceil_div(rows * c, 256)), 256, 0, mmr::as_stream(stream)>>>(x, pos, y, rows, l, c);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_x3_add_pos_split(const float* x, const float* pos, float* y, uint16_t* xs, int64_t rows, int32_t l,
+                                int32_t c, void* stream) {
+  mmr::clear_error();
+  const int kp = mmr_x3_p8_kpad(c);
+  MMR_REQUIRE(x && pos && xs && rows >= 0 && l > 0 && c > 0 && c % 4 == 0 && kp > 0 && al16(x) && al16(pos) &&
+                  (!y || al16(y)) && al16(xs),
+              "mmr_x3_add_pos_split: bad arguments (c %% 4 == 0, c <= 4096, 16-B aligned; c=%d)", c);
+  if (rows == 0) return MMR_OK;
+  x3_add_pos_split<<<dim3((unsigned)mmr::ceil_div(rows * (kp / 4), 256)), 256, 0, mmr::as_stream(stream)>>>(
+      x, pos, y, xs, rows, l, c, kp);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_x3_assemble_seq_split(const float* x1, const float* patches_fused, const float* x2, const float* pe,
+                                     uint16_t* xs, int32_t b, int32_t np, int32_t c, void* stream) {
+  mmr::clear_error();
+  const int kp = mmr_x3_p8_kpad(c);
+  MMR_REQUIRE(x1 && patches_fused && x2 && pe && xs && b >= 0 && np > 0 && c > 0 && c % 4 == 0 && kp > 0 && al16(x1) &&
+                  al16(patches_fused) && al16(x2) && al16(pe) && al16(xs),
+              "mmr_x3_assemble_seq_split: bad arguments (c %% 4 == 0, c <= 4096, 16-B aligned; c=%d)", c);
+  if (b == 0) return MMR_OK;
+  const int64_t n4 = (int64_t)b * (np + 2) * (kp / 4);
+  x3_assemble_seq_split<<<dim3((unsigned)mmr::ceil_div(n4, 256)), 256, 0, mmr::as_stream(stream)>>>(
+      x1, patches_fused, x2, pe, xs, b, np, c, kp);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }

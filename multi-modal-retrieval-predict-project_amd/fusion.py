@@ -101,16 +101,19 @@ class _Enhancer:
             x2 = ops.linear(a, self.w_o, self.b_o)
         return ops.scaled_add_layernorm(X, self.alpha, x2, self.g, self.b, eps, q8=q8)
 
-    def x3(self, x, B, L, eps):
-        """x3 mode: x (B*L, C) f32 -> LN(alpha*(x + pos) + MHA(x + pos)) f32 (B*L, C)."""
+    def x3(self, x, B, L, eps, keep_f32=True):
+        """x3 mode: x (B*L, C) f32 -> (y, ys): y = LN(alpha*(x + pos) + MHA(x + pos)) f32 (B*L, C) (None
+        unless keep_f32) and ys its x3 split-operand rows (ops.X3Rows; the f32 rows where the row count
+        does not fill 256-row tiles).  Every GEMM operand is written split by its producer: add-pos -> in_proj,
+        attention -> out_proj, LayerNorm -> the cross projections (no split passes)."""
         C = self.C
-        X = ops.x3_add_pos(x, self.pos, L)
-        qkv = ops.x3_linear(X, self.w_in_x3, self.b_in)
-        a = torch.empty_like(X)
-        ops.x3_attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], B, L, L, self.heads, self.dh,
-                         1.0 / math.sqrt(self.dh), out=a)
+        X, Xs = ops.x3_add_pos_split(x, self.pos, L)
+        qkv = ops.x3_linear(Xs, self.w_in_x3, self.b_in)
+        a = ops.x3_attention_split(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], B, L, L, self.heads, self.dh,
+                                   1.0 / math.sqrt(self.dh))
         x2 = ops.x3_linear(a, self.w_o_x3, self.b_o)
-        return ops.ln_rows(X, self.g, self.b, eps, alpha=self.alpha, residual=x2)
+        y = ops.x3_ln_split(X, self.g, self.b, eps, residual=x2, keep_f32=keep_f32, alpha=self.alpha)
+        return y if keep_f32 else (None, y)
 
 
 class FusionStack:
@@ -345,23 +348,24 @@ class FusionStack:
         PF = torch.empty((nl, B * Np, D), dtype=torch.float32, device=dev)
         cls = None
         for i, L in enumerate(self.layers):
-            Pe = L["patch"].x3(P, B, Np, eps)                                # (B*Np, Ci) f32
-            PQPP = ops.x3_linear(Pe, L["ppp_x3"], L["ppp_b"])              # k_t2i | v_t2i | q_i2t | img_patch_proj
+            _, Pes = L["patch"].x3(P, B, Np, eps, keep_f32=False)            # (B*Np, Ci), split rows
+            PQPP = ops.x3_linear(Pes, L["ppp_x3"], L["ppp_b"])             # k_t2i | v_t2i | q_i2t | img_patch_proj
+            PQPP = PQPP.reshape(B * Np, -1)
             PQ, PP = PQPP[:, :3 * D], PQPP[:, 3 * D:].contiguous()
             if txt_feats is None:  # learnable default text token (fusion.py:404-407)
                 T, Lt = L["default_txt32"].expand(B, -1).contiguous(), 1
             else:
                 Lt = txt_feats.shape[1]
                 T = txt_feats.float().contiguous().view(B * Lt, -1)
-            Te = L["txt"].x3(T, B, Lt, eps)                                  # (B*Lt, Ct) f32
+            Te, Tes = L["txt"].x3(T, B, Lt, eps)                             # (B*Lt, Ct) f32 + split rows
             Ct = Te.shape[1]
             if cls is None:
                 cls = torch.empty((nl, B, Ct), dtype=torch.float32, device=dev)
             ops.x3_gather_rows(Te, B, Ct, Lt * Ct, out=cls[i])              # CLS rows (fusion.py:447)
-            TQ = ops.x3_linear(Te, L["t_x3"], L["t_b"])                     # q_t2i | k_i2t | v_i2t
+            TQ = ops.x3_linear(Tes, L["t_x3"], L["t_b"]).reshape(B * Lt, -1)  # q_t2i | k_i2t | v_i2t
             ops.x3_attention(TQ[:, :D], PQ[:, :D], PQ[:, D:2 * D], B, Lt, Np, h, dh, sc, mean_out=m1[i])
-            a2 = torch.empty((B * Np, D), dtype=torch.float32, device=dev)
-            ops.x3_attention(PQ[:, 2 * D:], TQ[:, D:2 * D], TQ[:, 2 * D:], B, Np, Lt, h, dh, sc, out=a2, mean_out=m2[i])
+            a2 = ops.x3_attention_split(PQ[:, 2 * D:], TQ[:, D:2 * D], TQ[:, 2 * D:], B, Np, Lt, h, dh, sc,
+                                        mean_out=m2[i])
             ops.x3_linear(a2, L["o2_x3t"], L["o2_b"], residual=PP, out=PF[i])  # patches_fused (fusion.py:437)
         return self._finish(G, m1, m2, cls, PF, B, Np, Ci)
 
@@ -383,8 +387,8 @@ class FusionStack:
         # phase 3: the shared combiner self-attention over every layer's fused sequence
         m3 = torch.empty((nl * B, D), dtype=torch.float32, device=dev)
         if self.x3:
-            S = ops.x3_assemble_seq(x1, PF.view(nl * B * Np, D), x2, self.pe, Np).view(nl * B * (Np + 2), D)
-            SQ = ops.x3_linear(S, self.s_x3, self.s_b)
+            S = ops.x3_assemble_seq_split(x1, PF.view(nl * B * Np, D), x2, self.pe, Np)
+            SQ = ops.x3_linear(S, self.s_x3, self.s_b).reshape(nl * B * (Np + 2), -1)
             ops.x3_attention(SQ[:, :D], SQ[:, D:2 * D], SQ[:, 2 * D:], nl * B, Np + 2, Np + 2, h, dh, sc, mean_out=m3)
         elif self.s_w8 is not None and (nl * B * (Np + 2)) % 256 == 0:
             S8 = ops.assemble_seq(x1, PF.view(nl * B * Np, D), x2, self.pe, Np, q8=True)

@@ -633,10 +633,11 @@ class X3Rows:
         return self.t.shape[0]
 
 
-def x3_ln_split(x, g, b, eps, residual=None, keep_f32=False):
-    """LayerNorm(x + residual) over the last dim of f32 rows for an x3 linear: rows filling 256-row
-    tiles come back as X3Rows (mmr_ln_rows_split: the next GEMM skips its split pass), with the f32
-    output too when keep_f32 (-> (y, X3Rows)); other row counts as plain f32 rows (ln_rows)."""
+def x3_ln_split(x, g, b, eps, residual=None, keep_f32=False, alpha=None):
+    """LayerNorm(alpha * x + residual) over the last dim of f32 rows for an x3 linear (alpha: a device f32
+    scalar or None): rows filling 256-row tiles come back as X3Rows (mmr_ln_rows_split: the next GEMM
+    skips its split pass), with the f32 output too when keep_f32 (-> (y, X3Rows)); other row counts as
+    plain f32 rows (ln_rows)."""
     _lib.require_gpu(x)
     c = x.shape[-1]
     x2 = x.reshape(-1, c)
@@ -645,11 +646,12 @@ def x3_ln_split(x, g, b, eps, residual=None, keep_f32=False):
     kp = _L().mmr_x3_p8_kpad(c)
     if not (M > 0 and M % 256 == 0 and kp > 0 and c % 4 == 0 and c <= 1024 and x2.stride(1) == 1
             and (r2 is None or r2.stride(1) == 1)):
-        y = ln_rows(x2, g, b, eps, residual=r2).view(x.shape)
+        y = ln_rows(x2, g, b, eps, alpha=alpha, residual=r2).view(x.shape)
         return (y, y) if keep_f32 else y
     xs = torch.empty((M, 2 * kp), dtype=torch.bfloat16, device=x.device)
     y = torch.empty(x.shape, dtype=torch.float32, device=x.device) if keep_f32 else None
-    _chk(_L().mmr_ln_rows_split(_lib.ptr(x2), x2.stride(0), _lib.ptr(r2), r2.stride(0) if r2 is not None else 0,
+    _chk(_L().mmr_ln_rows_split(_lib.ptr(x2), x2.stride(0), _lib.ptr(alpha), _lib.ptr(r2),
+                                r2.stride(0) if r2 is not None else 0,
                                 _lib.ptr(g), _lib.ptr(b), _lib.ptr(y), c, _lib.ptr(xs), M, c, float(eps), _s(x)),
          "mmr_ln_rows_split")
     xr = X3Rows(xs, c, kp, tuple(x.shape[:-1]))
@@ -791,18 +793,20 @@ def x3_swin_window_attention_split(qkv, bias, hw, heads, ws, shift):
     return X3Rows(xs, C, kp, tuple(qkv.shape[:-1]))
 
 
-def x3_attention_split(q, k, v, b, lq, lk, heads, dh, scale, mask=None):
-    """x3_attention's output rows (b*lq, heads*dh) as X3Rows when b*lq fills 256-row tiles, else f32."""
+def x3_attention_split(q, k, v, b, lq, lk, heads, dh, scale, mask=None, mean_out=None):
+    """x3_attention's output rows (b*lq, heads*dh) as X3Rows when b*lq fills 256-row tiles, else f32;
+    mean_out (b, heads*dh) f32 or None: also the mean over the query rows."""
     C = heads * dh
     kp = _L().mmr_x3_p8_kpad(C)
     if not (b * lq > 0 and (b * lq) % 256 == 0 and kp > 0):
         out = torch.empty((b * lq, C), dtype=torch.float32, device=q.device)
-        x3_attention(q, k, v, b, lq, lk, heads, dh, scale, out=out, mask=mask)
+        x3_attention(q, k, v, b, lq, lk, heads, dh, scale, out=out, mask=mask, mean_out=mean_out)
         return out.view(b, lq, C)
     _lib.require_gpu(q)
     xs = torch.empty((b * lq, 2 * kp), dtype=torch.bfloat16, device=q.device)
     _chk(_L().mmr_x3_attention_xs(_lib.ptr(q), q.stride(0), _lib.ptr(k), k.stride(0), _lib.ptr(v), v.stride(0),
-                                  _lib.ptr(xs), _lib.ptr(mask), b, lq, lk, heads, dh, float(scale), _s(q)),
+                                  _lib.ptr(xs), _lib.ptr(mean_out), _lib.ptr(mask), b, lq, lk, heads, dh, float(scale),
+                                  _s(q)),
          "mmr_x3_attention_xs")
     return X3Rows(xs, C, kp, (b, lq))
 
@@ -852,6 +856,36 @@ def x3_add_pos(x, pos, l):
     y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
     _chk(_L().mmr_x3_add_pos(_lib.ptr(x), _lib.ptr(pos), _lib.ptr(y), rows, l, c, _s(x)), "mmr_x3_add_pos")
     return y
+
+
+def x3_add_pos_split(x, pos, l, keep_f32=True):
+    """x3_add_pos for an x3 linear: rows filling 256-row tiles come back as (y f32 or None, X3Rows)
+    (mmr_x3_add_pos_split), other row counts as (y, y)."""
+    c = x.shape[-1]
+    rows = x.numel() // c
+    kp = _L().mmr_x3_p8_kpad(c)
+    if not (rows > 0 and rows % 256 == 0 and kp > 0 and c % 4 == 0 and x.is_contiguous()):
+        y = x3_add_pos(x, pos, l)
+        return y, y
+    _lib.require_gpu(x)
+    y = torch.empty(x.shape, dtype=torch.float32, device=x.device) if keep_f32 else None
+    xs = torch.empty((rows, 2 * kp), dtype=torch.bfloat16, device=x.device)
+    _chk(_L().mmr_x3_add_pos_split(_lib.ptr(x), _lib.ptr(pos), _lib.ptr(y), _lib.ptr(xs), rows, l, c, _s(x)),
+         "mmr_x3_add_pos_split")
+    return y, X3Rows(xs, c, kp, tuple(x.shape[:-1]))
+
+
+def x3_assemble_seq_split(x1, pf, x2, pe, np_):
+    """x3_assemble_seq as X3Rows (the combiner QKV operand) when its rows fill 256-row tiles, else f32."""
+    B, c = x1.shape
+    rows = B * (np_ + 2)
+    kp = _L().mmr_x3_p8_kpad(c)
+    if not (rows % 256 == 0 and kp > 0 and c % 4 == 0):
+        return x3_assemble_seq(x1, pf, x2, pe, np_)
+    xs = torch.empty((rows, 2 * kp), dtype=torch.bfloat16, device=x1.device)
+    _chk(_L().mmr_x3_assemble_seq_split(_lib.ptr(x1), _lib.ptr(pf), _lib.ptr(x2), _lib.ptr(pe), _lib.ptr(xs), B, np_, c,
+                                        _s(x1)), "mmr_x3_assemble_seq_split")
+    return X3Rows(xs, c, kp, (rows,))
 
 
 def x3_assemble_seq(x1, pf, x2, pe, np_):

@@ -144,8 +144,8 @@ def test_ln_rows_split(rows, c, res):
     y = torch.empty(rows, c, device=DEV)
     xs = torch.full((rows, 2 * kp), 12345, dtype=torch.int16, device=DEV).view(torch.bfloat16)
     s = _lib.stream_ptr()
-    assert L.mmr_ln_rows_split(_lib.ptr(x), c, _lib.ptr(r), c if res else 0, _lib.ptr(g), _lib.ptr(b), _lib.ptr(y), c,
-                               _lib.ptr(xs), rows, c, 1e-5, s) == 0
+    assert L.mmr_ln_rows_split(_lib.ptr(x), c, None, _lib.ptr(r), c if res else 0, _lib.ptr(g), _lib.ptr(b),
+                               _lib.ptr(y), c, _lib.ptr(xs), rows, c, 1e-5, s) == 0
     torch.cuda.synchronize()
     ref = ops.ln_rows(x, g, b, 1e-5, residual=r)
     z = x.double() + (r.double() if res else 0)
@@ -159,7 +159,7 @@ def test_ln_rows_split(rows, c, res):
     assert (u[:, c:kp] == 0).all() and (u[:, kp + c:] == 0).all()
     # y optional: the split alone
     xs2 = torch.empty_like(xs)
-    assert L.mmr_ln_rows_split(_lib.ptr(x), c, _lib.ptr(r), c if res else 0, _lib.ptr(g), _lib.ptr(b), None, 0,
+    assert L.mmr_ln_rows_split(_lib.ptr(x), c, None, _lib.ptr(r), c if res else 0, _lib.ptr(g), _lib.ptr(b), None, 0,
                                _lib.ptr(xs2), rows, c, 1e-5, s) == 0
     torch.cuda.synchronize()
     assert torch.equal(xs2.view(torch.int16), u)
@@ -209,8 +209,8 @@ def test_x3_linear_p8_split_flags_rejected():
     assert L.mmr_x3_linear_p8(P(x), 1, P(w), None, None, P(y), 256, 384, 384, 0, 0, s) != 0
     assert L.mmr_x3_linear_p8(P(x), 1, P(w), P(b), None, P(y), 255, 384, 384, 0, 0, s) != 0
     f = torch.zeros(8, 100, device=DEV)
-    assert L.mmr_ln_rows_split(P(f), 100, None, 0, P(b), P(b), None, 0, P(y), 8, 98, 1e-5, s) != 0
-    assert L.mmr_ln_rows_split(P(f), 99, None, 0, P(b), P(b), None, 0, P(y), 8, 96, 1e-5, s) != 0
+    assert L.mmr_ln_rows_split(P(f), 100, None, None, 0, P(b), P(b), None, 0, P(y), 8, 98, 1e-5, s) != 0
+    assert L.mmr_ln_rows_split(P(f), 99, None, None, 0, P(b), P(b), None, 0, P(y), 8, 96, 1e-5, s) != 0
     torch.cuda.synchronize()
 
 
@@ -411,6 +411,77 @@ def test_x3_add_pos_exact(rows, l, c):
     y = ops.x3_add_pos(x, pos, l)
     torch.cuda.synchronize()
     assert torch.equal(y, x + pos.repeat(rows // l + 1, 1)[:rows])
+
+
+def _assert_split_of(xr, y):
+    """X3Rows xr = the split of f32 rows y bit for bit (padding columns zero)."""
+    assert isinstance(xr, ops.X3Rows)
+    assert torch.equal(xr.t.view(torch.int16), _split_bits(y.reshape(-1, y.shape[-1]), xr.kp))
+
+
+@pytest.mark.parametrize("rows,l,c", [(256 * 51, 51, 768), (512, 128, 96), (256, 1, 1000)])
+def test_x3_add_pos_split_bitwise(rows, l, c):
+    """add-pos writing the in_proj operand: f32 rows equal x3_add_pos, split rows = their split."""
+    g = torch.Generator().manual_seed(rows + c + 1)
+    x = torch.randn(rows, c, generator=g).to(DEV)
+    pos = torch.randn(l, c, generator=g).to(DEV)
+    y, xr = ops.x3_add_pos_split(x, pos, l)
+    ref = ops.x3_add_pos(x, pos, l)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+    _assert_split_of(xr, ref)
+    _, xr2 = ops.x3_add_pos_split(x, pos, l, keep_f32=False)
+    torch.cuda.synchronize()
+    assert torch.equal(xr2.t.view(torch.int16), xr.t.view(torch.int16))
+
+
+def test_x3_assemble_seq_split_bitwise():
+    b, np_, c = 256, 49, 768  # 256 * 51 rows
+    g = torch.Generator().manual_seed(11)
+    x1, x2 = torch.randn(b, c, generator=g).to(DEV), torch.randn(b, c, generator=g).to(DEV)
+    pf = torch.randn(b * np_, c, generator=g).to(DEV)
+    pe = torch.randn(np_ + 2, c, generator=g).to(DEV)
+    xr = ops.x3_assemble_seq_split(x1, pf, x2, pe, np_)
+    torch.cuda.synchronize()
+    _assert_split_of(xr, ops.x3_assemble_seq(x1, pf, x2, pe, np_))
+
+
+@pytest.mark.parametrize("rows,c", [(512, 768), (12544, 768), (256, 96)])
+def test_ln_rows_split_alpha(rows, c):
+    """LN(alpha x + residual) (the PreFusionEnhancer norm) in the split form: within f32 rounding of
+    ln_rows(alpha=...) and of f64; split rows = the split of its own f32 output."""
+    g_ = torch.Generator().manual_seed(rows + c + 7)
+    x = (torch.randn(rows, c, generator=g_) * 2).to(DEV)
+    r = torch.randn(rows, c, generator=g_).to(DEV)
+    g = (1 + 0.1 * torch.randn(c, generator=g_)).to(DEV)
+    b = (0.1 * torch.randn(c, generator=g_)).to(DEV)
+    alpha = torch.tensor([0.37], device=DEV)
+    y, xr = ops.x3_ln_split(x, g, b, 1e-5, residual=r, keep_f32=True, alpha=alpha)
+    ref = ops.ln_rows(x, g, b, 1e-5, alpha=alpha, residual=r)
+    torch.cuda.synchronize()
+    z = 0.37 * x.double() + r.double()
+    z64 = (z - z.mean(-1, keepdim=True)) / torch.sqrt(z.var(-1, unbiased=False, keepdim=True) + 1e-5) * g.double() + b.double()
+    assert (y - ref).abs().max().item() <= 2e-6 * ref.abs().max().item()
+    assert _rel(y, z64) < 2e-6
+    _assert_split_of(xr, y)
+
+
+def test_x3_attention_split_with_mean():
+    """The i2t cross attention's form: split-row output AND the query-row mean in one launch, equal to
+    the f32 form's output (split bit for bit) and mean."""
+    b, lq, lk, heads, dh = 256, 49, 128, 8, 96
+    g = torch.Generator().manual_seed(3)
+    C = heads * dh
+    q = (torch.randn(b * lq, C, generator=g) * 0.7).to(DEV)
+    kv = (torch.randn(b * lk, 2 * C, generator=g) * 0.7).to(DEV)
+    out = torch.empty(b * lq, C, device=DEV)
+    m_ref = torch.empty(b, C, device=DEV)
+    ops.x3_attention(q, kv[:, :C], kv[:, C:], b, lq, lk, heads, dh, dh ** -0.5, out=out, mean_out=m_ref)
+    m = torch.empty(b, C, device=DEV)
+    xr = ops.x3_attention_split(q, kv[:, :C], kv[:, C:], b, lq, lk, heads, dh, dh ** -0.5, mean_out=m)
+    torch.cuda.synchronize()
+    _assert_split_of(xr, out)
+    assert torch.equal(m, m_ref)
 
 
 @pytest.mark.parametrize("b,np_,c", [(256, 49, 768), (3, 5, 6)])
