@@ -200,8 +200,8 @@ int32_t mmr_linear_bf16_n_variants(void);
  *   MMR_PIN_GEMM_BF16: value = mmr_linear_bf16 variant index, or -1 = per-shape tuning (default);
  *   MMR_PIN_X3_WAVES:  value = 4 or 8 waves per mmr_linear_x3 tile (8 only where K % 256 == 0),
  *                      or -1 = automatic (default);
- *   MMR_PIN_X3_ATTN:   value = 1 runs the x3 attention entry points on the round-4 kernel (A/B only),
- *                      0 / -1 = the default x3_mha kernel.
+ *   MMR_PIN_X3_ATTN:   value = 1 runs the x3 attention entry points on the round-4 kernel, 2 the fused x3
+ *                      Swin MLP with ocml erff (A/B only); 0 / -1 = the defaults.
  * MMR_ERR_INVALID for an unknown pin or value. */
 enum { MMR_PIN_GEMM_BF16 = 0, MMR_PIN_X3_WAVES = 1, MMR_PIN_X3_ATTN = 2 };
 mmr_status mmr_pin_variant(int32_t which, int32_t value);
@@ -562,6 +562,14 @@ mmr_status mmr_x3_assemble_seq(const float* x1, const float* patches_fused, cons
 /* The same written only as the combiner QKV GEMM's x3 split operand rows (as mmr_x3_add_pos_split). */
 mmr_status mmr_x3_assemble_seq_split(const float* x1, const float* patches_fused, const float* x2, const float* pe,
                                      uint16_t* xs, int32_t b, int32_t np, int32_t c, void* stream);
+/* fp32-faithful fused Swin MLP (csrc/x3_mlp.hip): y = x + fc2(GELU_erf(fc1(LN(x)))) over tokens x (tokens, c)
+ * f32 (c in {96, 192}; y != x, 16-B aligned), both linears on bf16x3 MFMA, the hidden never leaving the CU.
+ * pack: mmr_x3_swin_mlp_pack_elems(c) bf16 elements, built once from the f32 fc1.weight [4c][c] and
+ * fc2.weight [c][4c] by mmr_x3_swin_mlp_pack (0 elements / MMR_ERR_UNSUPPORTED for other c). */
+int64_t mmr_x3_swin_mlp_pack_elems(int32_t c);
+mmr_status mmr_x3_swin_mlp_pack(const float* w1, const float* w2, uint16_t* pack, int32_t c, void* stream);
+mmr_status mmr_x3_swin_mlp(const float* x, const float* ln_g, const float* ln_b, const uint16_t* pack, const float* b1,
+                           const float* b2, float* y, int64_t tokens, int32_t c, float eps, void* stream);
 /* y (b, c) = (extra[b] + sum_t x[b][t]) / (l + 1) with extra (b, c), or sum_t x[b][t] / l when extra is
  * NULL; x (b, l, c) f32, summed in token order (unmasked token mean, model.py:370; the Swin global /
  * pooled means, fusion.py:263-265, model.py:463-468). */

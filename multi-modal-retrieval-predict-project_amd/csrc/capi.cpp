@@ -40,7 +40,7 @@ mmr_status mmr_pin_variant(int32_t which, int32_t value) {
     return MMR_OK;
   }
   if (which == MMR_PIN_X3_ATTN) {
-    MMR_REQUIRE(value == -1 || value == 0 || value == 1, "mmr_pin_variant: x3 attention %d (-1, 0, 1)", value);
+    MMR_REQUIRE(value >= -1 && value <= 2, "mmr_pin_variant: x3 attention %d (-1 .. 2)", value);
     mmr::pin_x3_attn.store(value);
     return MMR_OK;
   }

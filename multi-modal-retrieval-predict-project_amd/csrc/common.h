@@ -186,6 +186,24 @@ __device__ __forceinline__ void q8_chunk8(const float* vb, int64_t row, int ch, 
   }
 }
 
+// Fused-MLP weight images (swin_mlp.hip, x3_mlp.hip):
+// physical 16-B unit of logical unit q in row r (conflict-free for the b128 lane groups; checked
+// exhaustively for the 32x32x16 A-operand access pattern)
+template <int U>
+__host__ __device__ __forceinline__ int unit_swz(int r, int q) {
+  if constexpr (U == 12) return (q + ((r >> 2) & 3)) % 12;
+  else if constexpr (U == 4) return q ^ ((r >> 2) & 3);
+  else return q ^ ((r >> 1) & 7);  // U = 8, 24
+}
+
+// W2 column order inside each 16-wide group: stored position 8h + j holds hidden
+// 8(j>>2) + 4h + (j&3) — the order in which fc1's 32x32 C fragment leaves GELU'd values in lane
+// half h, so one ds_read_b128 fetches the A fragment that matches the packed B fragment.
+__host__ __device__ __forceinline__ int w2_hidden(int pos) {
+  const int h = (pos >> 3) & 1, j = pos & 7;
+  return (pos & ~15) + 8 * (j >> 2) + 4 * h + (j & 3);
+}
+
 }  // namespace mmr
 
 #define MMR_CHECK_HIP(expr)                                                                \

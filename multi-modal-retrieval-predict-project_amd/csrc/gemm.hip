@@ -699,6 +699,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
     }
     if (ll < TBN / 4) {
       if (HAS_BIAS) dma(bias + nof(tile) * TBN, lbias + par * NV * TBN, 0);
+      // KNN over a raw-row gallery (the native fp16 index): the tile's 256 per-row 1 / |g| in the bias slot
+      if (KNN && RS != nullptr) dma(RS + nof(tile) * TBN, lbias + par * NV * TBN, 0);
       if (LNM != 0) dma(LV1 + nof(tile) * TBN, lbias + (par * NV + 1) * TBN, 0);
       if (LNM == 2) dma(LV2 + nof(tile) * TBN, lbias + (par * NV + 2) * TBN, 0);
     }
@@ -1022,11 +1024,13 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
       // 4 efq) = the 2-row units rj / 2 and rj / 2 + 1 (one 8-B store); the wave column's 64 rows =
       // one block.  Every store issued (NSTORE exact for the next tile's counted wait)
       const int64_t r0 = n0 + wc * 64;
-      // RS (raw-row galleries, the native fp16 index): the per-row 1 / |g| turning q^ . g into the cosine
+      // RS (raw-row galleries, the native fp16 index): the per-row 1 / |g| turning q^ . g into the cosine,
+      // staged into LDS by LDS-DMA with the tile (bias_dma) — a global load here would retire behind the
+      // next tile's K-tile prefetch and drain it
       f32x4 rs[4];
       if (RS) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) rs[j] = *(const f32x4*)(RS + r0 + 16 * j + 4 * efq);
+        for (int j = 0; j < 4; ++j) rs[j] = *(const f32x4*)(lbias + par * NV * TBN + wc * 64 + 16 * j + 4 * efq);
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) rs[j] = (f32x4){1.f, 1.f, 1.f, 1.f};
@@ -1056,6 +1060,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
         if (efq == 0) BM[q * ldB + r0 / 64] = bmx;
       }
       if (!has_next) break;
+      par ^= 1;
+      bias_dma(tnext, par);
       t = tnext;
       first = false;
       continue;
@@ -1200,7 +1206,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
 #pragma unroll
       for (int ii = 0; ii < C::RM; ++ii) {
         const int i = rd * C::RM + ii;
-        float st1 = 0.f, st2 = 0.f;  // STO: this row's sum / sum of squares over the lane's columns
+        float st1 = 0.f;     // STO: this row's sum over the lane's columns
+        uint32_t sw[STO ? 2 * NT : 1];  // STO: the lane's stored (bf16-rounded) outputs, for the centred pass
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
           float v[4];
@@ -1237,7 +1244,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
             const float w0 = __uint_as_float(p0 << 16), w1 = __uint_as_float(p0 & 0xFFFF0000u);
             const float w2 = __uint_as_float(p1 << 16), w3 = __uint_as_float(p1 & 0xFFFF0000u);
             st1 += (w0 + w1) + (w2 + w3);
-            st2 = fmaf(w0, w0, fmaf(w1, w1, fmaf(w2, w2, fmaf(w3, w3, st2))));
+            sw[2 * j] = p0;
+            sw[2 * j + 1] = p1;
           }
           ds_write_b64_untracked(et + (ii * 16 + efr) * C::ELD + j * 16 + efq * 4, p0, p1);
         }
@@ -1249,7 +1257,17 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
             const auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(h), __float_as_uint(h), false, false);
             return __uint_as_float(q[0]) + __uint_as_float(q[1]);
           };
+          // the part's (sum, centred sum of squares M2) over its 16 NT columns — Chan's parallel form,
+          // merged in mmr_ln_row_coef (a raw sum of squares loses the variance of rows whose |mean| is
+          // large against their spread: ADVICE r04)
           st1 = sum4(st1);
+          const float pm = st1 * (1.0f / (16 * NT));
+          float st2 = 0.f;
+#pragma unroll
+          for (int q = 0; q < 2 * NT; ++q) {
+            const float d0 = __uint_as_float(sw[q] << 16) - pm, d1 = __uint_as_float(sw[q] & 0xFFFF0000u) - pm;
+            st2 = fmaf(d0, d0, fmaf(d1, d1, st2));
+          }
           st2 = sum4(st2);
           if (efq == 0)
             *(float2*)(SP + ((m0 + wr * 128 + i * 16 + efr) * (int64_t)(4 * tiles_n) + nof(t) * 4 + wc) * 2) =
@@ -1888,29 +1906,38 @@ void launch_x3p8(const uint16_t* xs, const uint16_t* w3, const float* b, const f
 }  // namespace
 
 namespace {
-// row statistics pairs -> LayerNorm coefficients (rstd, -mean rstd): 8 lanes per row, 2 pairs each per
-// step (np % 2 == 0), reduced by three xor swaps
+// row statistics -> LayerNorm coefficients (rstd, -mean rstd).  part[row][np] = (sum, M2) of np equal
+// parts of n / np columns each; merged with Chan's parallel formula: mean = sum / n, M2 = sum_p M2_p +
+// (n / np) sum_p (mean_p - mean)^2 — no E[y^2] - mean^2 cancellation.  8 lanes per row, 2 parts each
+// per step (np % 2 == 0), two passes over the (L2-resident) parts, reduced by xor swaps.
 __global__ __launch_bounds__(256) void ln_row_coef(const float* __restrict__ part, int64_t m, int np, float inv_n,
                                                    float eps, float* __restrict__ coef) {
   const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 3;
   const int sub = threadIdx.x & 7;
-  float s1 = 0.f, s2 = 0.f;
-  if (row < m) {
-    const float* p = part + row * np * 2;
-    for (int q = 2 * sub; q < np; q += 16) {
-      const float4 v = *(const float4*)(p + 2 * q);
-      s1 += v.x + v.z;
-      s2 += v.y + v.w;
-    }
+  const float* p = part + (row < m ? row : 0) * np * 2;
+  const float cnt = 1.0f / (inv_n * np), inv_cnt = inv_n * np;  // columns per part
+  float s1 = 0.f;
+  for (int q = 2 * sub; q < np; q += 16) {
+    const float4 v = *(const float4*)(p + 2 * q);
+    s1 += v.x + v.z;
+  }
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) s1 += __shfl_xor(s1, o, 64);
+  const float mean = s1 * inv_n;
+  float m2 = 0.f, dm = 0.f;
+  for (int q = 2 * sub; q < np; q += 16) {
+    const float4 v = *(const float4*)(p + 2 * q);
+    const float d0 = v.x * inv_cnt - mean, d1 = v.z * inv_cnt - mean;
+    m2 += v.y + v.w;
+    dm = fmaf(d0, d0, fmaf(d1, d1, dm));
   }
 #pragma unroll
   for (int o = 1; o < 8; o <<= 1) {
-    s1 += __shfl_xor(s1, o, 64);
-    s2 += __shfl_xor(s2, o, 64);
+    m2 += __shfl_xor(m2, o, 64);
+    dm += __shfl_xor(dm, o, 64);
   }
   if (row < m && sub == 0) {
-    const float mean = s1 * inv_n;
-    const float rstd = rsqrtf(fmaxf(s2 * inv_n - mean * mean, 0.f) + eps);
+    const float rstd = rsqrtf(fmaf(cnt, dm, m2) * inv_n + eps);
     *(float2*)(coef + 2 * row) = make_float2(rstd, -mean * rstd);
   }
 }

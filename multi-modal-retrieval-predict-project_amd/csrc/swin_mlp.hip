@@ -55,22 +55,8 @@ struct MlpGeo {
   static_assert(R == 2 || R == 3, "ring depth");
 };
 
-// physical 16-B unit of logical unit q in row r (conflict-free for the b128 lane groups; checked
-// exhaustively for the 32x32x16 A-operand access pattern)
-template <int U>
-__host__ __device__ __forceinline__ int unit_swz(int r, int q) {
-  if constexpr (U == 12) return (q + ((r >> 2) & 3)) % 12;
-  else if constexpr (U == 4) return q ^ ((r >> 2) & 3);
-  else return q ^ ((r >> 1) & 7);  // U = 8, 24
-}
-
-// W2 column order inside each 16-wide group: stored position 8h + j holds hidden
-// 8(j>>2) + 4h + (j&3) — the order in which fc1's 32x32 C fragment leaves GELU'd values in lane
-// half h, so one ds_read_b128 fetches the A fragment that matches the packed B fragment.
-__host__ __device__ __forceinline__ int w2_hidden(int pos) {
-  const int h = (pos >> 3) & 1, j = pos & 7;
-  return (pos & ~15) + 8 * (j >> 2) + 4 * h + (j & 3);
-}
+using mmr::unit_swz;
+using mmr::w2_hidden;
 
 // Output-row order for the resident kernel: MFMA C row 8i + 4h + rr of output tile u holds channel
 // 32u + 16(i>>1) + 8h + 4(i&1) + rr, so lane half h ends up with channels 32u + 8h + 0..7 and

@@ -1,0 +1,296 @@
+// fp32-faithful (x3) fused Swin MLP sub-block for the narrow, memory-bound stages (C = 96, 192):
+//   y = x + fc2(GELU(fc1(LN2(x))))            (timm SwinTransformerBlock, fusion.py:198-199)
+// in f32 with both linears on bf16x3 MFMA (a.b ~= a_hi.b_hi + a_hi.b_lo + a_lo.b_hi, f32 accumulate) and
+// torch's erf GELU (ocml erff), the 4C-wide hidden activation never leaving the CU.  The unfused x3
+// chain (LayerNorm split pass -> fc1 GEMM writing the hidden as split rows -> fc2 GEMM + residual) moves
+// 2 x 4 x 4C bytes of hidden per token through HBM and runs its short-K GEMMs at ~3.5 TB/s: at stage 1
+// 1.17 ms per block for 355 GF of bf16 MFMA work.
+// Structure (the bf16 streamed form of swin_mlp.hip on split operands): each wave owns 32 tokens,
+// LayerNorms them in f32 registers (row split over the lane pair sharing a token) straight into the
+// fc1 B operand as hi / lo fragments, and walks the hidden dimension 32 units at a time: fc1 in the
+// C^T orientation on v_mfma_f32_32x32x16_bf16 (3 products per k-step, bias in the accumulator), GELU,
+// the hidden split in registers into the hi / lo B operands of fc2 (C^T, A = W2 from LDS under the
+// k-permutation w2_hidden mirrors).  Weights are split and repacked once at load into per-HC-hidden-
+// unit chunks [W1_hi | W1_lo | W2_hi | W2_lo] — exact, bank-conflict-free LDS images — streamed through
+// an R-deep LDS ring by global_load_lds and shared by the workgroup's 32 NW tokens.  The residual x is
+// re-read (L2) in the epilogue; y is f32.
+#include <algorithm>
+#include <float.h>
+#include <math.h>
+
+#include "common.h"
+
+namespace {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+constexpr int vmcnt_n(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14); }
+
+template <int C, int NW, int HC, int R>
+struct X3MlpGeo {
+  static constexpr int U1 = C / 8;        // 16-B units per W1 row
+  static constexpr int U2 = HC / 8;       // 16-B units per W2 row (chunk columns)
+  static constexpr int KS1 = C / 16;      // fc1 k-steps
+  static constexpr int NU = C / 32;       // fc2 output tiles (32 channels)
+  static constexpr int NT = HC / 32;      // 32-wide hidden tiles per chunk
+  static constexpr int NCH = 4 * C / HC;  // chunks
+  static constexpr int W1B = HC * C * 2;  // bytes of one bf16 image (W1 rows or W2 columns of a chunk)
+  static constexpr int CHUNK_B = 4 * W1B;
+  static constexpr int PW = CHUNK_B / 1024 / NW;  // glds pieces per wave per chunk
+  static constexpr int TOK = 32 * NW;
+  static constexpr int LDS_B = R * CHUNK_B;
+  static_assert(CHUNK_B % (1024 * NW) == 0, "chunk must split evenly over the waves");
+  static_assert(R == 2 || R == 3, "ring depth");
+};
+
+// f32 w1 [4C][C], w2 [C][4C] -> chunk images [W1_hi | W1_lo | W2_hi | W2_lo] (hi = bf16(w), lo = bf16(w - hi))
+template <int C, int HC>
+__global__ __launch_bounds__(256) void x3_swin_mlp_pack(const float* __restrict__ w1, const float* __restrict__ w2,
+                                                        uint16_t* __restrict__ pack) {
+  constexpr int W1E = HC * C, CE = 4 * W1E;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // destination element
+  if (i >= (int64_t)16 * C * C) return;
+  const int ch = (int)(i / CE), e = (int)(i % CE), part = e / W1E, e2 = e % W1E;
+  float v;
+  int dst;
+  if (part < 2) {
+    const int rr = e2 / C, k = e2 % C;
+    dst = rr * C + 8 * mmr::unit_swz<C / 8>(rr, k >> 3) + (k & 7);
+    v = w1[(int64_t)(HC * ch + rr) * C + k];
+  } else {
+    const int c = e2 / HC, pos = e2 % HC;
+    dst = c * HC + 8 * mmr::unit_swz<HC / 8>(c, pos >> 3) + (pos & 7);
+    v = w2[(int64_t)c * 4 * C + HC * ch + mmr::w2_hidden(pos)];
+  }
+  const uint16_t hi = mmr::f2bf(v);
+  pack[(int64_t)ch * CE + part * W1E + dst] = (part & 1) ? mmr::f2bf(v - mmr::bf2f(hi)) : hi;
+}
+
+// GELU(erf).  ERF_AS: erf by Abramowitz-Stegun 7.1.26 (mmr::gelu_erf: |erf err| <= 1.5e-7, one v_exp + one
+// v_rcp, branch-free) — the GELU's absolute error <= 0.75e-7 |x|, 100x below the x3 products' 2^-17; ocml
+// erff otherwise (a branchy polynomial: the fused kernel's VALU bound)
+template <bool ERF_AS>
+__device__ __forceinline__ float gelu_exact(float v) {
+  if constexpr (ERF_AS) return mmr::gelu_erf(v);
+  else return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+}
+
+// two f32 -> (hi, lo) packed bf16 pairs
+__device__ __forceinline__ void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
+  hi = mmr::pack2bf(a, b);
+  lo = mmr::pack2bf(a - __uint_as_float(hi << 16), b - __uint_as_float(hi & 0xFFFF0000u));
+}
+
+template <int C, int NW, int HC, int R, bool ERF_AS>
+__global__ __launch_bounds__(64 * NW) void x3_swin_mlp(const float* __restrict__ x, const float* __restrict__ lng,
+                                                       const float* __restrict__ lnb, const uint16_t* __restrict__ pack,
+                                                       const float* __restrict__ b1, const float* __restrict__ b2,
+                                                       float* __restrict__ y, int64_t T, float eps) {
+  using G = X3MlpGeo<C, NW, HC, R>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // the weight ring only
+  __shared__ __attribute__((aligned(16))) float Pg[6 * C];               // gamma | beta | b1
+  const float* Pb = Pg + C;
+  const float* Pb1 = Pg + 2 * C;
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t tok = (int64_t)blockIdx.x * G::TOK + wave * 32 + r;
+  const bool ok = tok < T;
+  const float* xr = x + (ok ? tok : 0) * C;
+
+  for (int i = threadIdx.x; i < 6 * C; i += 64 * NW)
+    Pg[i] = i < C ? lng[i] : (i < 2 * C ? lnb[i - C] : b1[i - 2 * C]);
+  // lane half h: columns 16 ks + 8 h .. + 7 of its token (clamped row: unconditional loads)
+  f32x4 xv[2 * G::KS1];
+#pragma unroll
+  for (int ks = 0; ks < G::KS1; ++ks) {
+    xv[2 * ks] = *(const f32x4*)(xr + 16 * ks + 8 * h);
+    xv[2 * ks + 1] = *(const f32x4*)(xr + 16 * ks + 8 * h + 4);
+  }
+
+  auto stage = [&](int ch) {
+    const unsigned char* src = (const unsigned char*)pack + (size_t)ch * G::CHUNK_B;
+    unsigned char* dst = smem + (ch % R) * G::CHUNK_B;
+#pragma unroll
+    for (int p = 0; p < G::PW; ++p) {
+      const int piece = wave * G::PW + p;
+      __builtin_amdgcn_global_load_lds((const void*)(src + piece * 1024 + lane * 16), (lds_ptr_t)(dst + piece * 1024),
+                                       16, 0, 0);
+    }
+  };
+  stage(0);
+  if constexpr (R == 3) stage(1);
+  __builtin_amdgcn_s_waitcnt(vmcnt_n((R - 1) * G::PW));  // x and chunk 0 landed
+  __builtin_amdgcn_s_waitcnt(0xC07F);                    // lgkmcnt(0): parameter stores landed
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  // LayerNorm (f32, two-pass, row split over the lane pair) -> the fc1 B operand as hi / lo fragments
+  bf16x8 xh[G::KS1], xl[G::KS1];
+  {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 2 * G::KS1; ++q) s += (xv[q][0] + xv[q][1]) + (xv[q][2] + xv[q][3]);
+    s += __shfl_xor(s, 32, 64);
+    const float mean = s * (1.0f / C);
+    float ss = 0.f;
+#pragma unroll
+    for (int q = 0; q < 2 * G::KS1; ++q)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = xv[q][j] - mean;
+        ss += d * d;
+      }
+    ss += __shfl_xor(ss, 32, 64);
+    const float rstd = rsqrtf(ss * (1.0f / C) + eps);
+#pragma unroll
+    for (int ks = 0; ks < G::KS1; ++ks) {
+      const int k0 = 16 * ks + 8 * h;
+      uint32_t hh[4], ll[4];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const f32x4 g4 = *(const f32x4*)(Pg + k0 + 4 * p), c4 = *(const f32x4*)(Pb + k0 + 4 * p);
+        const f32x4 v = xv[2 * ks + p];
+        split2((v[0] - mean) * rstd * g4[0] + c4[0], (v[1] - mean) * rstd * g4[1] + c4[1], hh[2 * p], ll[2 * p]);
+        split2((v[2] - mean) * rstd * g4[2] + c4[2], (v[3] - mean) * rstd * g4[3] + c4[3], hh[2 * p + 1],
+               ll[2 * p + 1]);
+      }
+      xh[ks] = __builtin_bit_cast(bf16x8, make_uint4(hh[0], hh[1], hh[2], hh[3]));
+      xl[ks] = __builtin_bit_cast(bf16x8, make_uint4(ll[0], ll[1], ll[2], ll[3]));
+    }
+  }
+
+  f32x16 acc2[G::NU];
+#pragma unroll
+  for (int u = 0; u < G::NU; ++u) acc2[u] = (f32x16){0};
+
+  for (int ch = 0; ch < G::NCH; ++ch) {
+    if (R == 3 && ch + 1 < G::NCH) __builtin_amdgcn_s_waitcnt(vmcnt_n(G::PW));  // chunk ch landed
+    else __builtin_amdgcn_s_waitcnt(vmcnt_n(0));
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's pieces landed; the slot refilled next is free
+    asm volatile("" ::: "memory");
+    if (ch + R - 1 < G::NCH) stage(ch + R - 1);
+    const unsigned char* W1h = smem + (ch % R) * G::CHUNK_B;
+    const unsigned char* W1l = W1h + G::W1B;
+    const unsigned char* W2h = W1h + 2 * G::W1B;
+    const unsigned char* W2l = W1h + 3 * G::W1B;
+#pragma unroll
+    for (int t = 0; t < G::NT; ++t) {  // 32 hidden units per step
+      f32x16 a1;  // starts at fc1's bias (lane: hidden HC ch + 32 t + 8 i + 4 h + rr of token r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 bb = *(const f32x4*)(Pb1 + HC * ch + 32 * t + 8 * i + 4 * h);
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) a1[4 * i + rr] = bb[rr];
+      }
+      const int row = 32 * t + r;
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks) {
+        const int off = (row * G::U1 + mmr::unit_swz<G::U1>(row, 2 * ks + h)) * 16;
+        const bf16x8 wh = *(const bf16x8*)(W1h + off), wl = *(const bf16x8*)(W1l + off);
+        a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xh[ks], a1, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xl[ks], a1, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, xh[ks], a1, 0, 0, 0);
+      }
+      uint32_t hph[8], hpl[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        split2(gelu_exact<ERF_AS>(a1[4 * i]), gelu_exact<ERF_AS>(a1[4 * i + 1]), hph[2 * i], hpl[2 * i]);
+        split2(gelu_exact<ERF_AS>(a1[4 * i + 2]), gelu_exact<ERF_AS>(a1[4 * i + 3]), hph[2 * i + 1], hpl[2 * i + 1]);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {  // k-step over hidden 32 t + 16 s2 .. + 15
+        const bf16x8 hfh = __builtin_bit_cast(bf16x8, make_uint4(hph[4 * s2], hph[4 * s2 + 1], hph[4 * s2 + 2],
+                                                                 hph[4 * s2 + 3]));
+        const bf16x8 hfl = __builtin_bit_cast(bf16x8, make_uint4(hpl[4 * s2], hpl[4 * s2 + 1], hpl[4 * s2 + 2],
+                                                                 hpl[4 * s2 + 3]));
+        const int q = 2 * (2 * t + s2) + h;
+#pragma unroll
+        for (int u = 0; u < G::NU; ++u) {
+          const int c = 32 * u + r;
+          const int off = (c * G::U2 + mmr::unit_swz<G::U2>(c, q)) * 16;
+          const bf16x8 wh = *(const bf16x8*)(W2h + off), wl = *(const bf16x8*)(W2l + off);
+          acc2[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, hfh, acc2[u], 0, 0, 0);
+          acc2[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, hfl, acc2[u], 0, 0, 0);
+          acc2[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, hfh, acc2[u], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // y[tok][c] = x + (fc2 + b2), c = 32 u + 8 i + 4 h + rr (the residual re-read: no registers held)
+  if (ok) {
+#pragma unroll
+    for (int u = 0; u < G::NU; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = 32 * u + 8 * i + 4 * h;
+        const f32x4 bb = *(const f32x4*)(b2 + c), xq = *(const f32x4*)(x + tok * C + c);
+        f32x4 v;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) v[rr] = (acc2[u][4 * i + rr] + bb[rr]) + xq[rr];
+        *(f32x4*)(y + tok * C + c) = v;
+      }
+  }
+}
+
+template <int C, int HC>
+mmr_status launch_x3_pack(const float* w1, const float* w2, uint16_t* pack, hipStream_t st) {
+  const int64_t n = (int64_t)16 * C * C;
+  x3_swin_mlp_pack<C, HC><<<dim3((unsigned)mmr::ceil_div(n, 256)), 256, 0, st>>>(w1, w2, pack);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+template <int C, int NW, int HC, int R>
+mmr_status launch_x3_mlp(const float* x, const float* g, const float* b, const uint16_t* pack, const float* b1,
+                         const float* b2, float* y, int64_t T, float eps, hipStream_t st) {
+  using G = X3MlpGeo<C, NW, HC, R>;
+  const dim3 grid((unsigned)mmr::ceil_div(T, G::TOK));
+  if (mmr::pin_x3_attn.load(std::memory_order_relaxed) == 2)  // A/B: ocml erff
+    x3_swin_mlp<C, NW, HC, R, false><<<grid, 64 * NW, G::LDS_B, st>>>(x, g, b, pack, b1, b2, y, T, eps);
+  else
+    x3_swin_mlp<C, NW, HC, R, true><<<grid, 64 * NW, G::LDS_B, st>>>(x, g, b, pack, b1, b2, y, T, eps);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+constexpr int X3MLP_HC = 32;
+
+}  // namespace
+
+extern "C" {
+
+int64_t mmr_x3_swin_mlp_pack_elems(int32_t c) { return (c == 96 || c == 192) ? (int64_t)16 * c * c : 0; }
+
+mmr_status mmr_x3_swin_mlp_pack(const float* w1, const float* w2, uint16_t* pack, int32_t c, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(w1 && w2 && pack, "mmr_x3_swin_mlp_pack: NULL pointer");
+  hipStream_t st = mmr::as_stream(stream);
+  if (c == 96) return launch_x3_pack<96, X3MLP_HC>(w1, w2, pack, st);
+  if (c == 192) return launch_x3_pack<192, X3MLP_HC>(w1, w2, pack, st);
+  mmr::set_error("mmr_x3_swin_mlp_pack: C=%d not built (96, 192)", c);
+  return MMR_ERR_UNSUPPORTED;
+}
+
+mmr_status mmr_x3_swin_mlp(const float* x, const float* ln_g, const float* ln_b, const uint16_t* pack, const float* b1,
+                           const float* b2, float* y, int64_t tokens, int32_t c, float eps, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(x && ln_g && ln_b && pack && b1 && b2 && y, "mmr_x3_swin_mlp: NULL pointer");
+  MMR_REQUIRE(tokens >= 0 && x != y, "mmr_x3_swin_mlp: tokens < 0 or in place");
+  MMR_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 && ((uintptr_t)b2 & 15) == 0,
+              "mmr_x3_swin_mlp: x / y / b2 must be 16-B aligned");
+  if (tokens == 0) return MMR_OK;
+  hipStream_t st = mmr::as_stream(stream);
+  if (c == 96) return launch_x3_mlp<96, 8, X3MLP_HC, 3>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
+  if (c == 192) return launch_x3_mlp<192, 8, X3MLP_HC, 2>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
+  mmr::set_error("mmr_x3_swin_mlp: C=%d not built (96, 192)", c);
+  return MMR_ERR_UNSUPPORTED;
+}
+
+}  // extern "C"

@@ -761,6 +761,29 @@ def x3_ffn(x, w1, b1, w2, b2, residual=None):
     return y
 
 
+def x3_swin_mlp_pack(w1, w2):
+    """fc1.weight [4C][C], fc2.weight [C][4C] (f32, device) -> the split chunk images of x3_swin_mlp, or None
+    if C is not a fused width (96, 192)."""
+    C = w1.shape[1]
+    n = _L().mmr_x3_swin_mlp_pack_elems(C)
+    if n <= 0:
+        return None
+    pack = torch.empty((n,), dtype=torch.bfloat16, device=w1.device)
+    _chk(_L().mmr_x3_swin_mlp_pack(_lib.ptr(w1.contiguous()), _lib.ptr(w2.contiguous()), _lib.ptr(pack), C, _s(w1)),
+         "mmr_x3_swin_mlp_pack")
+    return pack
+
+
+def x3_swin_mlp(x, g, b, pack, b1, b2, eps):
+    """x + fc2(GELU(fc1(LN(x)))) in the x3 mode, fused (f32 tokens (..., C), C in {96, 192})."""
+    _lib.require_gpu(x)
+    C = x.shape[-1]
+    y = torch.empty_like(x)
+    _chk(_L().mmr_x3_swin_mlp(_lib.ptr(x), _lib.ptr(g), _lib.ptr(b), _lib.ptr(pack), _lib.ptr(b1), _lib.ptr(b2),
+                              _lib.ptr(y), x.numel() // C, C, float(eps), _s(x)), "mmr_x3_swin_mlp")
+    return y
+
+
 def x3_attention(q, k, v, b, lq, lk, heads, dh, scale, out=None, mean_out=None, mask=None):
     """f32 attention core over strided row views (mmr_x3_attention); mask (b, lk) int64 or None."""
     _lib.require_gpu(q)

@@ -22,7 +22,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from .retrieval import GalleryIndex, RetrievalEngine, check_status, merge_topk_packed, rerank_mix
+from .retrieval import GalleryIndex, RetrievalEngine, merge_topk_packed, rerank_mix
 
 
 def shard_bounds(n, world):
@@ -97,18 +97,30 @@ def rerank_mix_host(cand, comp, topk, alpha=0.6, beta=0.25, gamma=0.15):
     return tuple(out)
 
 
-def pack_lists(idx, s64, comp=None):
+def pack_lists(idx, s64, comp=None, status=None):
     """One rank's search result as the single all-gather payload: (Q, K) int64 + (Q, K) f64 (+ (Q, K, P)
-    f64 rerank components) -> (Q, K, 2 + P) f64 words {score, index bits, payload} (int64 bits carried
-    in an 8-byte slot: copies and all-gathers move bytes, nothing re-interprets them)."""
+    f64 rerank components) -> (Q + 1, K, 2 + P) f64 words {score, index bits, payload} (int64 bits
+    carried in an 8-byte slot: copies and all-gathers move bytes, nothing re-interprets them).  Row Q is
+    the rank's status row: word [Q, 0, 0] = its max per-query search status (a device scalar or None =
+    0), so every rank sees every rank's status after the one exchange and all raise together (a rank
+    raising alone before the exchange would leave the others blocked in the collective)."""
     parts = [s64.to(torch.float64).unsqueeze(-1), idx.to(torch.int64).contiguous().view(torch.float64).unsqueeze(-1)]
     if comp is not None:
         parts.append(comp.to(torch.float64))
-    return torch.cat(parts, -1).contiguous()
+    body = torch.cat(parts, -1)
+    srow = torch.zeros((1,) + tuple(body.shape[1:]), dtype=torch.float64, device=body.device)
+    if status is not None:
+        srow[0, 0, 0] = status.to(device=body.device, dtype=torch.float64)
+    return torch.cat([body, srow], 0).contiguous()
+
+
+def gathered_status(gathered):
+    """Max status over the ranks of an all-gathered pack_lists buffer [world][Q + 1][K][W] (host int)."""
+    return int(gathered[:, -1, 0, 0].max().item())
 
 
 def merge_gathered(gathered, q0, nq, k_out, payload_width=0):
-    """The post-gather merge: gathered [world][Q][K][2 + P] (all ranks' pack_lists, world = shards)
+    """The post-gather merge: gathered [world][Q + 1][K][2 + P] (all ranks' pack_lists, world = shards)
     -> this rank's queries [q0, q0 + nq): (idx, f32, f64) (+ payload (nq, k_out, P)).  Device tensors:
     mmr_merge_topk_packed reads the gathered buffer directly; host tensors (gloo): merge_topk_host."""
     if gathered.is_cuda:
@@ -127,7 +139,8 @@ class ShardedIndex:
     is the rank's GPU GalleryIndex in `mode` ("x3" | "f16" | "f32").  A non-zero per-query status
     would flag an inexact list; the selection kernel resolves candidate-buffer overflow in-kernel, so
     it never occurs — this is a guard: an injected `fallback_search` re-runs such queries, else the
-    search raises (no mode switch inside a collective: ADVICE r03)."""
+    status rides in the result exchange (pack_lists' status row) and EVERY rank raises after it (no
+    mode switch inside a collective: ADVICE r03; no rank raising alone before it: ADVICE r04)."""
 
     def __init__(self, gallery_rows, n_total, start, group=None, device=None, local_search=None, mode="x3",
                  fallback_search=None, local_components=None, index=None, status_out=None):
@@ -162,8 +175,10 @@ class ShardedIndex:
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
         s, e = shard_bounds(len(gallery), world)[rank]
-        if isinstance(gallery, torch.Tensor):
+        if isinstance(gallery, torch.Tensor):  # fp16 rows stay fp16 only for an f16 index (GalleryIndex)
             rows = gallery[s:e]
+            if rows.dtype == torch.float16 and mode != "f16":
+                rows = rows.float()
         else:  # an fp16 gallery in f16 mode stays fp16 (the native fp16 index: 2 B per element on device)
             keep16 = np.asarray(gallery[:0]).dtype == np.float16 and mode == "f16"
             rows = np.ascontiguousarray(gallery[s:e], dtype=np.float16 if keep16 else np.float32)
@@ -171,23 +186,34 @@ class ShardedIndex:
                    fallback_search=fallback_search)
 
     def _local(self, q, k):
+        """-> (idx, f64, status): status = the device max of the per-query statuses still flagged after
+        the fallback re-run (None when there is nothing to report: no status, or status_out took it)."""
         out = self.local_search(q, k)
         i, s64 = out[0], out[1]
         st = out[2] if len(out) > 2 else None
-        if st is not None and self.status_out is not None:
-            if st.numel():
-                torch.maximum(self.status_out, st.max().to(self.status_out.dtype), out=self.status_out)
-            return i, s64
-        if st is not None and st.numel() and int(st.max().item()) != 0:
-            if self.fallback_search is None:
-                check_status(st)
+        if st is None or not st.numel():
+            return i, s64, None
+        if self.status_out is not None:
+            torch.maximum(self.status_out, st.max().to(self.status_out.dtype), out=self.status_out)
+            return i, s64, None
+        if self.fallback_search is None:
+            return i, s64, st.max()  # raised on every rank after the exchange (_raise_status)
+        if int(st.max().item()) != 0:
             bad = torch.nonzero(st != 0).flatten()
             i2, s2 = self.fallback_search(q[bad.to(q.device)].contiguous(), k)
             i, s64 = i.clone(), s64.clone()
             i[bad.to(i.device)] = i2.to(i.device, i.dtype)
             s64[bad.to(s64.device)] = s2.to(s64.device, s64.dtype)
             self.reruns += int(bad.numel())
-        return i, s64
+        return i, s64, None
+
+    @staticmethod
+    def _raise_status(g, st):
+        """After the exchange: every rank holds every rank's status row, so all raise together."""
+        if st is not None:
+            worst = gathered_status(g)
+            if worst != 0:
+                raise RuntimeError(f"mmr_index_search returned status {worst} on a shard (collective search)")
 
     def search(self, q_local, k):
         """Collective: every rank passes its own (b, D) queries (same b on every rank); returns
@@ -195,8 +221,9 @@ class ShardedIndex:
         Two collectives: the queries' all-gather and ONE packed all-gather of the result lists."""
         b = q_local.shape[0]
         allq = self._gather_queries(q_local)
-        i, s64 = self._local(allq, k)
-        g = self._gather(pack_lists(i, s64))
+        i, s64, st = self._local(allq, k)
+        g = self._gather(pack_lists(i, s64, status=st))
+        self._raise_status(g, st)
         return merge_gathered(g, self.rank * b, b, k)
 
     def _gather_queries(self, q_local):
@@ -227,9 +254,10 @@ class ShardedIndex:
         b = q_local.shape[0]
         topk = k if topk is None else topk
         allq = self._gather_queries(q_local)
-        i, s64 = self._local(allq, k)
+        i, s64, st = self._local(allq, k)
         comp = self._components(allq, i, tables).to(s64.device)
-        g = self._gather(pack_lists(i, s64, comp))              # one collective: lists + components
+        g = self._gather(pack_lists(i, s64, comp, status=st))   # one collective: lists + components
+        self._raise_status(g, st)
         mi, _, _, mc = merge_gathered(g, self.rank * b, b, k, payload_width=comp.shape[-1])
         if mi.is_cuda:
             return rerank_mix(mi, mc, topk, alpha, beta, gamma)

@@ -71,7 +71,9 @@ class GalleryIndex:
 
     MODES = {"f32": 0, "x3": 1, "f16": 2}
 
-    def __init__(self, embs, device=None, idx_base: int = 0, mode: str = "x3"):
+    def __init__(self, embs, device=None, idx_base: int = 0, mode=None):
+        """mode None: "f16" for fp16 rows (a native fp16 index is f16-only), else "x3".  An fp16 gallery
+        with an explicit other mode raises ValueError (upcast the rows to f32 for an x3 / f32 index)."""
         _lib.require_gpu()
         L = _lib.lib()
         if device is None:
@@ -96,14 +98,17 @@ class GalleryIndex:
             torch.cuda.synchronize(self.device)  # the copy runs on the default stream
         h = ctypes.c_void_p()
         self.native_f16 = bool(half)
-        if half:
-            mode = "f16"  # a native fp16 index scans its own fp16 rows
+        if mode is None:
+            mode = "f16" if half else "x3"
+        if mode not in self.MODES:
+            raise ValueError(f"scan mode {mode!r} (x3 | f32 | f16)")
+        if half and mode != "f16":
+            raise ValueError(f"an fp16 gallery builds a native fp16 index, which scans only in mode 'f16' (asked "
+                             f"{mode!r}): pass f32 rows for an {mode} index")
         _lib.check(L.mmr_index_create(p, n, d, 1 if half else 0, is_host, idx_base, self.device, ctypes.byref(h)),
                    "mmr_index_create")
         del keep
         self._h = h
-        if mode not in self.MODES:
-            raise ValueError(f"scan mode {mode!r} (x3 | f32 | f16)")
         _lib.check(L.mmr_index_set_mode(h, self.MODES[mode]), "mmr_index_set_mode")
         self.mode = mode
         self.n, self.d, self.idx_base = int(n), int(d), int(idx_base)
@@ -114,6 +119,8 @@ class GalleryIndex:
     def set_mode(self, mode: str):
         if mode not in self.MODES:
             raise ValueError(f"scan mode {mode!r} (x3 | f32 | f16)")
+        if self.native_f16 and mode != "f16":
+            raise ValueError(f"a native fp16 index scans only in mode 'f16' (asked {mode!r})")
         with self._lock:
             _lib.check(_lib.lib().mmr_index_set_mode(self._h, self.MODES[mode]), "mmr_index_set_mode")
             self.mode = mode

@@ -10,7 +10,9 @@ same dataflow as the bf16 towers (towers.py, fusion.py), but:
   * linears: ops.x3_linear (X f32 split in registers, W pre-split once at load: ops.X3W), bias /
     GELU(erf, erff) / residual in the f32 epilogue;
   * attention: ops.x3_attention / ops.x3_swin_window_attention (q k^T and P V both bf16x3, expf softmax);
-  * LayerNorm: the f32 row kernel (ops.ln_rows), PatchMerging / BERT embeddings / means: f32 kernels.
+  * LayerNorm: the f32 row kernel (ops.ln_rows), PatchMerging / BERT embeddings / means: f32 kernels;
+  * Swin stages 1-2 (C = 96 / 192): LayerNorm + fc1 + GELU + fc2 + residual fused (ops.x3_swin_mlp,
+    csrc/x3_mlp.hip), the hidden never leaving the CU.
 """
 import math
 
@@ -76,9 +78,12 @@ class SwinTowerX3:
                     "fc1_w": _x3(sd[p + "mlp.fc1.weight"], dev), "fc1_b": _f(sd[p + "mlp.fc1.bias"], dev),
                     "fc2_w": _x3(sd[p + "mlp.fc2.weight"], dev), "fc2_b": _f(sd[p + "mlp.fc2.bias"], dev),
                 })
+                b_ = st["blocks"][-1]
+                b_["mlp_pack"] = ops.x3_swin_mlp_pack(b_["fc1_w"].w, b_["fc2_w"].w)  # C = 96 / 192: fused
             self.stages.append(st)
         self.norm_g, self.norm_b = _f(sd["norm.weight"], dev), _f(sd["norm.bias"], dev)
         self.num_features = E * 2 ** (len(self.cfg["depths"]) - 1)
+        self.fused_mlp = True  # the fused x3 MLP where built (A/B attribute)
 
     def tokens(self, image):
         """(B,3,H,W) f32 -> (B, h, w, C) f32 tokens BEFORE the final norm."""
@@ -100,8 +105,11 @@ class SwinTowerX3:
                 qkv = ops.x3_linear(h, bk["qkv_w"], bk["qkv_b"])
                 a = ops.x3_swin_window_attention_split(qkv, bk["bias"], H, heads, ws, bk["shift"])
                 x = ops.x3_linear(a, bk["proj_w"], bk["proj_b"], residual=x)
-                h = ops.x3_ln_split(x, bk["n2g"], bk["n2b"], 1e-5)
-                x = ops.x3_ffn(h, bk["fc1_w"], bk["fc1_b"], bk["fc2_w"], bk["fc2_b"], residual=x)
+                if self.fused_mlp and bk["mlp_pack"] is not None:
+                    x = ops.x3_swin_mlp(x, bk["n2g"], bk["n2b"], bk["mlp_pack"], bk["fc1_b"], bk["fc2_b"], 1e-5)
+                else:
+                    h = ops.x3_ln_split(x, bk["n2g"], bk["n2b"], 1e-5)
+                    x = ops.x3_ffn(h, bk["fc1_w"], bk["fc1_b"], bk["fc2_w"], bk["fc2_b"], residual=x)
         return x
 
     def forward_features(self, image):

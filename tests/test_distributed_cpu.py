@@ -141,6 +141,55 @@ def test_sharded_search_reruns_flagged_queries():
         np.testing.assert_allclose(m64, es[rank * b:(rank + 1) * b], rtol=0, atol=1e-14)
 
 
+def _worker_status_raise(rank, world, port, N, D, b, K, out_q):
+    """Rank 0's local search flags one query (status 1) and there is no fallback: the status rides in the
+    packed result exchange and EVERY rank raises after it — none is left blocked in the collective."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        G, _ = synthetic.labelled_gallery(N, D, 83)
+        Q, _ = synthetic.labelled_gallery(world * b, D, 84)
+        s, e = shard_bounds(N, world)[rank]
+
+        def local(q, k):
+            i, sc = oknn.exact_topk(q.numpy(), G[s:e], k)
+            st = torch.zeros(q.shape[0], dtype=torch.int32)
+            if rank == 0:
+                st[1] = 1
+            return torch.from_numpy(np.where(i >= 0, i + s, -1).astype(np.int64)), torch.from_numpy(sc), st
+
+        sh = ShardedIndex(G[s:e], N, s, local_search=local)
+        try:
+            sh.search(torch.from_numpy(Q[rank * b:(rank + 1) * b]), K)
+            out_q.put((rank, "no error"))
+        except RuntimeError as ex:
+            out_q.put((rank, str(ex)))
+        # the group is still usable afterwards (nobody was left inside a collective)
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        out_q.put((rank, float(t.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_search_status_raises_on_every_rank():
+    world, N, D, b, K = 2, 800, 32, 4, 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_status_raise, args=(r, world, port, N, D, b, K, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(2 * world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    msgs = [m for _, m in res if isinstance(m, str)]
+    assert len(msgs) == world and all("status 1" in m for m in msgs), msgs
+    assert [m for _, m in res if not isinstance(m, str)] == [float(world)] * world
+
+
 def test_dls_cache_path_naming(tmp_path, monkeypatch):
     """DLS link-graph cache file (retrieval.py:72-79): explicit path, name / default stem inside the
     feature-DB directory, always .npz (np.savez appends it to any other name)."""

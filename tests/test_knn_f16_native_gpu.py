@@ -10,7 +10,6 @@ import pytest
 import torch
 
 from mmr_amd import synthetic
-from mmr_amd._lib import MMRError
 from mmr_amd.retrieval import GalleryIndex, MI355XRetrievalEngine
 from oracle import knn as oknn
 
@@ -51,6 +50,20 @@ def test_native_f16_equals_f32_upcast_every_path(N, D, K):
         x.close()
 
 
+def test_native_f16_explicit_other_mode_is_refused():
+    """An fp16 gallery asked for an x3 / f32 index raises (it would otherwise become a silently f16-only
+    index: ADVICE r04); the default mode of fp16 rows (numpy or torch) is f16."""
+    G16 = _gallery16(3_000, 128, 7)
+    for bad in ("x3", "f32"):
+        with pytest.raises(ValueError, match="native fp16"):
+            GalleryIndex(G16, mode=bad)
+        with pytest.raises(ValueError, match="native fp16"):
+            GalleryIndex(torch.from_numpy(G16).cuda(), mode=bad)
+    ix = GalleryIndex(torch.from_numpy(G16).cuda())
+    assert ix.native_f16 and ix.mode == "f16"
+    ix.close()
+
+
 def test_native_f16_device_bytes_and_modes():
     """1M x 1024 fp16 gallery: 2 B per element + f32 / f64 norms on the device (the f32 index needs
     4 B rows + the 2-B scan copy); x3 / f32 modes (which need f32 rows) are refused."""
@@ -60,9 +73,9 @@ def test_native_f16_device_bytes_and_modes():
     g, _ = ix.device_bytes()
     Np = -(-N // 256) * 256
     assert g == Np * D * 2 + Np * 12
-    with pytest.raises(MMRError):
+    with pytest.raises(ValueError):
         ix.set_mode("x3")
-    with pytest.raises(MMRError):
+    with pytest.raises(ValueError):
         ix.set_mode("f32")
     q = torch.from_numpy(synthetic.gauss_gallery(2048, D, synthetic.SEED + 71)).cuda()
     i, _, s64 = ix.search(q, 10, want_f64=True)

@@ -456,7 +456,11 @@ def test_linear_ln_modes(M):
     assert st.shape == (M, ops.linear_ln_parts(M, C, 0), 2)
     s = st.double().sum(1)
     assert torch.allclose(s[:, 0], yd.sum(1), rtol=1e-5, atol=1e-3)
-    assert torch.allclose(s[:, 1], (yd * yd).sum(1), rtol=1e-5, atol=1e-3)
+    # second word: each part's centred sum of squares M2_p; Chan's merge gives the row's M2
+    npart = st.shape[1]
+    pm = st[..., 0].double() / (C // npart)
+    m2 = st[..., 1].double().sum(1) + (C // npart) * ((pm - yd.mean(1, keepdim=True)) ** 2).sum(1)
+    assert torch.allclose(m2, ((yd - yd.mean(1, keepdim=True)) ** 2).sum(1), rtol=1e-4, atol=1e-3)
     cf = ops.ln_row_coef(st, C, eps)
     yd64 = yd - yd.mean(1, keepdim=True)
     ref_cf = torch.stack([1 / torch.sqrt((yd64 ** 2).mean(1) + eps), -yd.mean(1) / torch.sqrt((yd64 ** 2).mean(1) + eps)], 1)
@@ -480,6 +484,24 @@ def test_linear_ln_modes(M):
     assert rel_err(y2, ref2) < 1e-2
     s2 = st2.double().sum(1)
     assert torch.allclose(s2[:, 0], y2.double().sum(1), rtol=1e-5, atol=1e-3)
+
+
+def test_ln_row_coef_large_row_offset():
+    """Rows whose |mean| is large against their spread (a residual stream offset by ~1e3): the producer's
+    per-part (sum, centred M2) merged by Chan's formula keep the variance that E[y^2] - mean^2 in f32 loses
+     — coefficients vs f64 on the stored bf16 rows."""
+    g = torch.Generator(device=DEV).manual_seed(9)
+    M, C, eps = 512, 768, 1e-12
+    ctx = bf(torch.randn(M, C, generator=g, device=DEV))
+    wo, bo = bf(torch.randn(C, C, generator=g, device=DEV) * C ** -0.5), torch.zeros(C, device=DEV)
+    h = bf(torch.randn(M, C, generator=g, device=DEV) * 4 + 1000.0)
+    y, st = ops.linear_ln(ctx, wo, bo, residual=h, want_stats=True)
+    cf = ops.ln_row_coef(st, C, eps).double()
+    yd = y.double()
+    var = ((yd - yd.mean(1, keepdim=True)) ** 2).mean(1)
+    rstd = 1 / torch.sqrt(var + eps)
+    assert torch.allclose(cf[:, 0], rstd, rtol=2e-4), (cf[:, 0] / rstd - 1).abs().max().item()
+    assert torch.allclose(cf[:, 1], -yd.mean(1) * rstd, rtol=2e-4)
 
 
 def test_linear_ln_rejects():

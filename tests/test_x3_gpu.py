@@ -129,6 +129,31 @@ def test_x3_ffn_split_handoff_bitwise(M, C, Fw, res):
     assert _rel(y, y64) < 1e-5
 
 
+@pytest.mark.parametrize("T,C", [(4096, 96), (1000, 96), (2048, 192), (77, 192)])
+def test_x3_swin_mlp_vs_f64(T, C):
+    """The fused x3 Swin MLP (LN -> fc1 -> erf GELU -> fc2 -> + x, hidden on chip) against f64, and against
+    the unfused x3 chain (x3_ln_split -> x3_ffn) within the x3 bound; ragged token counts."""
+    g_ = torch.Generator().manual_seed(T + C)
+    x = (torch.randn(T, C, generator=g_) * 1.5 + 0.3).to(DEV)
+    gm = (1 + 0.1 * torch.randn(C, generator=g_)).to(DEV)
+    bt = (0.1 * torch.randn(C, generator=g_)).to(DEV)
+    w1 = (torch.randn(4 * C, C, generator=g_) * C ** -0.5).to(DEV)
+    b1 = (0.1 * torch.randn(4 * C, generator=g_)).to(DEV)
+    w2 = (torch.randn(C, 4 * C, generator=g_) * (4 * C) ** -0.5).to(DEV)
+    b2 = (0.1 * torch.randn(C, generator=g_)).to(DEV)
+    pack = ops.x3_swin_mlp_pack(w1, w2)
+    y = ops.x3_swin_mlp(x, gm, bt, pack, b1, b2, 1e-5)
+    xd = x.double().cpu()
+    z = (xd - xd.mean(-1, keepdim=True)) / torch.sqrt(xd.var(-1, unbiased=False, keepdim=True) + 1e-5)
+    z = z * gm.double().cpu() + bt.double().cpu()
+    hid = F.gelu(z @ w1.double().cpu().T + b1.double().cpu())
+    y64 = xd + hid @ w2.double().cpu().T + b2.double().cpu()
+    assert _rel(y, y64) < 1e-5
+    h = ops.x3_ln_split(x, gm, bt, 1e-5)
+    y_chain = ops.x3_ffn(h, ops.X3W(w1), b1, ops.X3W(w2), b2, residual=x)
+    assert _rel(y, y_chain) < 1e-5
+
+
 @pytest.mark.parametrize("rows,c,res", [(1024, 96, True), (512, 192, False), (768, 384, True), (256, 768, True),
                                         (256, 100, False), (13, 768, True), (7, 96, False)])
 def test_ln_rows_split(rows, c, res):
