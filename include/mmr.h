@@ -567,6 +567,17 @@ mmr_status mmr_x3_assemble_seq_split(const float* x1, const float* patches_fused
  * pack: mmr_x3_swin_mlp_pack_elems(c) bf16 elements, built once from the f32 fc1.weight [4c][c] and
  * fc2.weight [c][4c] by mmr_x3_swin_mlp_pack (0 elements / MMR_ERR_UNSUPPORTED for other c). */
 int64_t mmr_x3_swin_mlp_pack_elems(int32_t c);
+/* fp32-faithful row-linear for the narrow Swin stages (csrc/x3_mlp.hip): y (tokens, n) f32 = LN(x) W^T + b
+ * (+ residual) with x f32 (tokens, c) and its LayerNorm (ln_g, ln_b), or = xs W^T + b (+ residual) with xs
+ * the x3 split-operand rows [hi | lo] (tokens, 2 kp), kp = mmr_x3_p8_kpad(c) (the window attention's _xs
+ * output) — exactly one of x / xs.  bf16x3 MFMA, W^T streamed through LDS.  c in {96, 192}, n % 32 == 0,
+ * n <= 4096 (c = 96: n > 64); pack = mmr_x3_rowlin_pack_elems(n, c) bf16 elements built once from the f32
+ * weight [n][c] by mmr_x3_rowlin_pack. */
+int64_t mmr_x3_rowlin_pack_elems(int32_t n, int32_t c);
+mmr_status mmr_x3_rowlin_pack(const float* w, uint16_t* pack, int32_t n, int32_t c, void* stream);
+mmr_status mmr_x3_rowlin(const float* x, const uint16_t* xs, const float* ln_g, const float* ln_b, const uint16_t* pack,
+                         const float* bias, const float* residual, float* y, int64_t tokens, int32_t n, int32_t c,
+                         float eps, void* stream);
 mmr_status mmr_x3_swin_mlp_pack(const float* w1, const float* w2, uint16_t* pack, int32_t c, void* stream);
 mmr_status mmr_x3_swin_mlp(const float* x, const float* ln_g, const float* ln_b, const uint16_t* pack, const float* b1,
                            const float* b2, float* y, int64_t tokens, int32_t c, float eps, void* stream);

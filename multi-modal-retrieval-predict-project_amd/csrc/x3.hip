@@ -451,6 +451,7 @@ __global__ __launch_bounds__(256, 2) void x3_mha(const AttnArgs a, int kbs) {
   const int kv_bytes = kbs * (KROW + VROW) * 4, epi_bytes = nwv * 32 * OROW * 4;
   float* msum = (float*)(smem + (kv_bytes > epi_bytes ? kv_bytes : epi_bytes));  // [nwv][DHP]
   float* madd = msum + nwv * DHP;                                                  // [kbs] (MODE 1)
+  int64_t* tokt = (int64_t*)(madd + kbs);  // [64] (MODE 2): the window's token rows (roll / partition map)
   const int unit = mmr::xcd_contiguous((int)blockIdx.x, (int)gridDim.x);
   const int head = unit % a.heads;
   const int64_t bb = unit / a.heads;
@@ -465,13 +466,18 @@ __global__ __launch_bounds__(256, 2) void x3_mha(const AttnArgs a, int kbs) {
     wx = win % nwin1;
     type = a.shift > 0 ? ((wy == nwin1 - 1) ? 2 : 0) + ((wx == nwin1 - 1) ? 1 : 0) : 0;
   }
-  auto qtok = [&](int i) -> int64_t {
-    if constexpr (MODE == 2) {
-      const int hr = wy * a.ws + i / a.ws, wr = wx * a.ws + i % a.ws;
-      return sw_base + (int64_t)((hr + a.shift) % a.hw) * a.hw + (wr + a.shift) % a.hw;
-    } else {
-      return bb * lq + i;
+  // MODE 2: the token map (runtime divisions by ws / hw: ~40 VALU each) computed once per block into LDS
+  if constexpr (MODE == 2) {
+    for (int i = tid; i < 64; i += nthr) {
+      const int ii = i < lq ? i : lq - 1;
+      const int hr = wy * a.ws + ii / a.ws, wr = wx * a.ws + ii % a.ws;
+      tokt[i] = sw_base + (int64_t)((hr + a.shift) % a.hw) * a.hw + (wr + a.shift) % a.hw;
     }
+    __syncthreads();
+  }
+  auto qtok = [&](int i) -> int64_t {
+    if constexpr (MODE == 2) return tokt[i];
+    else return bb * lq + i;
   };
   auto ktok = [&](int j) -> int64_t {
     if constexpr (MODE == 2) return qtok(j);
@@ -684,11 +690,12 @@ __global__ __launch_bounds__(256, 2) void x3_mha(const AttnArgs a, int kbs) {
               make_float4(o[dt][4 * g4] * inv, o[dt][4 * g4 + 1] * inv, o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes landed
       __builtin_amdgcn_wave_barrier();
-      const int nc4 = dh / 4;
-      if (a.out != nullptr || a.xs != nullptr)
-        for (int c = lane; c < 32 * nc4; c += 64) {
-          const int row = c / nc4, ch = c - row * nc4;
-          if (q0 + row >= lq) continue;
+      // lane -> (row lr + rpi j, 4-column chunk lc): the divisions once per lane, not per chunk
+      const int nc4 = dh / 4, rpi = 64 / nc4, lr = lane / nc4, lc = lane - lr * nc4;
+      if ((a.out != nullptr || a.xs != nullptr) && lr < rpi)
+        for (int row = lr; row < 32; row += rpi) {
+          const int ch = lc;
+          if (q0 + row >= lq) break;
           const float4 v = *(const float4*)(st + row * OROW + 4 * ch);
           const int64_t tk = qtok(q0 + row);
           if (a.xs != nullptr) {
@@ -1042,7 +1049,7 @@ mmr_status launch_attention(const char* who, AttnArgs a, int64_t nbh, bool swin,
     const int kbs = dt <= 2 ? std::min(128, lkp) : std::min(64, lkp);
     const int dhp = 32 * dt, krow = dhp + 8, vrow = dhp + ((dt & 1) ? 0 : 16), orow = dhp + 4;
     const size_t kv = (size_t)kbs * (krow + vrow) * 4, epi = (size_t)nwv * 32 * orow * 4;
-    const size_t lds = std::max(kv, epi) + (size_t)nwv * dhp * 4 + (size_t)kbs * 4;
+    const size_t lds = std::max(kv, epi) + (size_t)nwv * dhp * 4 + (size_t)kbs * 4 + (swin ? 64 * 8 : 0);
     const dim3 grid((unsigned)nbh), blk(64 * nwv);
     const int mode = swin ? 2 : (a.kmask ? 1 : 0);
 #define XM(D_, M_) x3_mha<D_, M_><<<grid, blk, lds, st>>>(a, kbs)

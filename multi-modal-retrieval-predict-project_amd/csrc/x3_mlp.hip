@@ -69,14 +69,11 @@ __global__ __launch_bounds__(256) void x3_swin_mlp_pack(const float* __restrict_
   pack[(int64_t)ch * CE + part * W1E + dst] = (part & 1) ? mmr::f2bf(v - mmr::bf2f(hi)) : hi;
 }
 
-// GELU(erf).  ERF_AS: erf by Abramowitz-Stegun 7.1.26 (mmr::gelu_erf: |erf err| <= 1.5e-7, one v_exp + one
-// v_rcp, branch-free) — the GELU's absolute error <= 0.75e-7 |x|, 100x below the x3 products' 2^-17; ocml
-// erff otherwise (a branchy polynomial: the fused kernel's VALU bound)
-template <bool ERF_AS>
-__device__ __forceinline__ float gelu_exact(float v) {
-  if constexpr (ERF_AS) return mmr::gelu_erf(v);
-  else return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
-}
+// GELU(erf) with erf by Abramowitz-Stegun 7.1.26 (mmr::gelu_erf: |erf err| <= 1.5e-7, one v_exp + one
+// v_rcp, branch-free): the GELU's absolute error <= 0.75e-7 |x|, 100x below the x3 products' 2^-17.  ocml
+// erff (a branchy polynomial) made the kernel VALU-bound: stage 1 615 vs 529 us, stage 2 587 vs 464 us at
+// B = 256, the same max deviation from the unfused chain (profiles/r05_x3_mlp_ab.txt)
+__device__ __forceinline__ float gelu_exact(float v) { return mmr::gelu_erf(v); }
 
 // two f32 -> (hi, lo) packed bf16 pairs
 __device__ __forceinline__ void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
@@ -84,7 +81,7 @@ __device__ __forceinline__ void split2(float a, float b, uint32_t& hi, uint32_t&
   lo = mmr::pack2bf(a - __uint_as_float(hi << 16), b - __uint_as_float(hi & 0xFFFF0000u));
 }
 
-template <int C, int NW, int HC, int R, bool ERF_AS>
+template <int C, int NW, int HC, int R>
 __global__ __launch_bounds__(64 * NW) void x3_swin_mlp(const float* __restrict__ x, const float* __restrict__ lng,
                                                        const float* __restrict__ lnb, const uint16_t* __restrict__ pack,
                                                        const float* __restrict__ b1, const float* __restrict__ b2,
@@ -200,8 +197,8 @@ __global__ __launch_bounds__(64 * NW) void x3_swin_mlp(const float* __restrict__
       uint32_t hph[8], hpl[8];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        split2(gelu_exact<ERF_AS>(a1[4 * i]), gelu_exact<ERF_AS>(a1[4 * i + 1]), hph[2 * i], hpl[2 * i]);
-        split2(gelu_exact<ERF_AS>(a1[4 * i + 2]), gelu_exact<ERF_AS>(a1[4 * i + 3]), hph[2 * i + 1], hpl[2 * i + 1]);
+        split2(gelu_exact(a1[4 * i]), gelu_exact(a1[4 * i + 1]), hph[2 * i], hpl[2 * i]);
+        split2(gelu_exact(a1[4 * i + 2]), gelu_exact(a1[4 * i + 3]), hph[2 * i + 1], hpl[2 * i + 1]);
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {  // k-step over hidden 32 t + 16 s2 .. + 15
@@ -239,6 +236,169 @@ __global__ __launch_bounds__(64 * NW) void x3_swin_mlp(const float* __restrict__
   }
 }
 
+// ------------------------------------------------------------------ x3 row-linear (narrow Swin stages)
+// y = LN?(x) W^T + b (+ r) for the short-K Swin linears of stages 1-2 (C = 96 / 192: qkv N = 3C with the
+// block's norm1 fused, proj N = C + residual reading the window attention's split-row output), whose
+// K' = 3 kp split GEMMs on the 8-phase kernel run HBM-bound at ~3.5 TB/s with padded tiles (stage-1 qkv
+// N 288 -> 384, proj N 96 -> 192).  The MLP kernel's structure without the hidden: each wave LayerNorms
+// (or loads as split rows) its 32 tokens into the hi / lo B operand in registers, and walks the output
+// features 32 at a time against W^T chunks [W_hi 64 x C | W_lo 64 x C] streamed through an R-deep LDS
+// ring (bias in the accumulator; f32 output rows, the residual added in the epilogue).
+template <int C, int NW, int R>
+struct X3RowGeo {
+  static constexpr int U1 = C / 8, KS1 = C / 16;
+  static constexpr int WB = 64 * C * 2;  // one bf16 image of a 64-row chunk
+  static constexpr int CHUNK_B = 2 * WB;
+  static constexpr int PW = CHUNK_B / 1024 / NW;
+  static constexpr int TOK = 32 * NW;
+  static constexpr int LDS_B = R * CHUNK_B;
+  static_assert(CHUNK_B % (1024 * NW) == 0, "chunk must split evenly over the waves");
+};
+
+// f32 W [n][C] -> 64-row chunks [W_hi | W_lo] (rows >= n zero), the fc1 image layout of the MLP pack
+template <int C>
+__global__ __launch_bounds__(256) void x3_rowlin_pack(const float* __restrict__ w, uint16_t* __restrict__ pack, int n,
+                                                      int64_t total) {
+  constexpr int WE = 64 * C;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int ch = (int)(i / (2 * WE)), e = (int)(i % (2 * WE)), part = e / WE, e2 = e % WE;
+  const int rr = e2 / C, k = e2 % C;
+  const int row = 64 * ch + rr;
+  const float v = row < n ? w[(int64_t)row * C + k] : 0.f;
+  const uint16_t hi = mmr::f2bf(v);
+  pack[(int64_t)ch * 2 * WE + part * WE + rr * C + 8 * mmr::unit_swz<C / 8>(rr, k >> 3) + (k & 7)] =
+      part ? mmr::f2bf(v - mmr::bf2f(hi)) : hi;
+}
+
+template <int C, int NW, int R, bool LN, bool RES>
+__global__ __launch_bounds__(64 * NW) void x3_rowlin(const float* __restrict__ x, const uint16_t* __restrict__ xs,
+                                                     int kp, const float* __restrict__ lng, const float* __restrict__ lnb,
+                                                     const uint16_t* __restrict__ pack, const float* __restrict__ bias,
+                                                     const float* __restrict__ res, float* __restrict__ y, int64_t T,
+                                                     int N, float eps) {
+  using G = X3RowGeo<C, NW, R>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // ring | bias [N] | gamma, beta
+  float* Pbias = (float*)(smem + G::LDS_B);
+  float* Pg = Pbias + N;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t tok = (int64_t)blockIdx.x * G::TOK + wave * 32 + r;
+  const bool ok = tok < T;
+  const int64_t tk = ok ? tok : 0;
+  const int nch = (N + 63) / 64;
+
+  for (int i = threadIdx.x; i < N; i += 64 * NW) Pbias[i] = bias[i];
+  if constexpr (LN)
+    for (int i = threadIdx.x; i < 2 * C; i += 64 * NW) Pg[i] = i < C ? lng[i] : lnb[i - C];
+  bf16x8 xh[G::KS1], xl[G::KS1];
+  f32x4 xv[LN ? 2 * G::KS1 : 1];
+  if constexpr (LN) {
+#pragma unroll
+    for (int ks = 0; ks < G::KS1; ++ks) {
+      xv[2 * ks] = *(const f32x4*)(x + tk * C + 16 * ks + 8 * h);
+      xv[2 * ks + 1] = *(const f32x4*)(x + tk * C + 16 * ks + 8 * h + 4);
+    }
+  } else {
+#pragma unroll
+    for (int ks = 0; ks < G::KS1; ++ks) {
+      xh[ks] = *(const bf16x8*)(xs + tk * 2 * kp + 16 * ks + 8 * h);
+      xl[ks] = *(const bf16x8*)(xs + tk * 2 * kp + kp + 16 * ks + 8 * h);
+    }
+  }
+  auto stage = [&](int ch) {
+    const unsigned char* src = (const unsigned char*)pack + (size_t)ch * G::CHUNK_B;
+    unsigned char* dst = smem + (ch % R) * G::CHUNK_B;
+#pragma unroll
+    for (int p = 0; p < G::PW; ++p) {
+      const int piece = wave * G::PW + p;
+      __builtin_amdgcn_global_load_lds((const void*)(src + piece * 1024 + lane * 16), (lds_ptr_t)(dst + piece * 1024),
+                                       16, 0, 0);
+    }
+  };
+  // (nch >= R - 1 is required by the launcher: every issued stage is waited for below)
+  stage(0);
+  if constexpr (R == 3) stage(1);
+  __builtin_amdgcn_s_waitcnt(vmcnt_n((R - 1) * G::PW));  // x and chunk 0 landed
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if constexpr (LN) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 2 * G::KS1; ++q) s += (xv[q][0] + xv[q][1]) + (xv[q][2] + xv[q][3]);
+    s += __shfl_xor(s, 32, 64);
+    const float mean = s * (1.0f / C);
+    float ss = 0.f;
+#pragma unroll
+    for (int q = 0; q < 2 * G::KS1; ++q)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = xv[q][j] - mean;
+        ss += d * d;
+      }
+    ss += __shfl_xor(ss, 32, 64);
+    const float rstd = rsqrtf(ss * (1.0f / C) + eps);
+#pragma unroll
+    for (int ks = 0; ks < G::KS1; ++ks) {
+      const int k0 = 16 * ks + 8 * h;
+      uint32_t hh[4], ll[4];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const f32x4 g4 = *(const f32x4*)(Pg + k0 + 4 * p), c4 = *(const f32x4*)(Pg + C + k0 + 4 * p);
+        const f32x4 v = xv[2 * ks + p];
+        split2((v[0] - mean) * rstd * g4[0] + c4[0], (v[1] - mean) * rstd * g4[1] + c4[1], hh[2 * p], ll[2 * p]);
+        split2((v[2] - mean) * rstd * g4[2] + c4[2], (v[3] - mean) * rstd * g4[3] + c4[3], hh[2 * p + 1],
+               ll[2 * p + 1]);
+      }
+      xh[ks] = __builtin_bit_cast(bf16x8, make_uint4(hh[0], hh[1], hh[2], hh[3]));
+      xl[ks] = __builtin_bit_cast(bf16x8, make_uint4(ll[0], ll[1], ll[2], ll[3]));
+    }
+  }
+  for (int ch = 0; ch < nch; ++ch) {
+    if (R == 3 && ch + 1 < nch) __builtin_amdgcn_s_waitcnt(vmcnt_n(G::PW));  // chunk ch landed
+    else __builtin_amdgcn_s_waitcnt(vmcnt_n(0));
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (ch + R - 1 < nch) stage(ch + R - 1);
+    const unsigned char* Wh = smem + (ch % R) * G::CHUNK_B;
+    const unsigned char* Wl = Wh + G::WB;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int u = 2 * ch + t;
+      if (32 * u >= N) break;  // wave-uniform (N % 32 == 0)
+      f32x16 acc;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 bb = *(const f32x4*)(Pbias + 32 * u + 8 * i + 4 * h);
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) acc[4 * i + rr] = bb[rr];
+      }
+      const int row = 32 * t + r;
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks) {
+        const int off = (row * G::U1 + mmr::unit_swz<G::U1>(row, 2 * ks + h)) * 16;
+        const bf16x8 wh = *(const bf16x8*)(Wh + off), wl = *(const bf16x8*)(Wl + off);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xh[ks], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xl[ks], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, xh[ks], acc, 0, 0, 0);
+      }
+      // lane: channels 32 u + 8 i + 4 h + rr of token r
+      if (ok) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = 32 * u + 8 * i + 4 * h;
+          f32x4 v = {acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]};
+          if constexpr (RES) v += *(const f32x4*)(res + tok * N + c);
+          *(f32x4*)(y + tok * N + c) = v;
+        }
+      }
+    }
+  }
+}
+
 template <int C, int HC>
 mmr_status launch_x3_pack(const float* w1, const float* w2, uint16_t* pack, hipStream_t st) {
   const int64_t n = (int64_t)16 * C * C;
@@ -252,15 +412,25 @@ mmr_status launch_x3_mlp(const float* x, const float* g, const float* b, const u
                          const float* b2, float* y, int64_t T, float eps, hipStream_t st) {
   using G = X3MlpGeo<C, NW, HC, R>;
   const dim3 grid((unsigned)mmr::ceil_div(T, G::TOK));
-  if (mmr::pin_x3_attn.load(std::memory_order_relaxed) == 2)  // A/B: ocml erff
-    x3_swin_mlp<C, NW, HC, R, false><<<grid, 64 * NW, G::LDS_B, st>>>(x, g, b, pack, b1, b2, y, T, eps);
-  else
-    x3_swin_mlp<C, NW, HC, R, true><<<grid, 64 * NW, G::LDS_B, st>>>(x, g, b, pack, b1, b2, y, T, eps);
+  x3_swin_mlp<C, NW, HC, R><<<grid, 64 * NW, G::LDS_B, st>>>(x, g, b, pack, b1, b2, y, T, eps);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }
 
 constexpr int X3MLP_HC = 32;
+
+template <int C, bool LN, bool RES>
+mmr_status launch_rowlin(const float* x, const uint16_t* xs, int kp, const float* g, const float* b,
+                         const uint16_t* pack, const float* bias, const float* res, float* y, int64_t T, int N,
+                         float eps, hipStream_t st) {
+  constexpr int R = C == 96 ? 3 : 2;
+  using G = X3RowGeo<C, 8, R>;
+  const size_t lds = G::LDS_B + (size_t)(N + 2 * C) * 4;
+  x3_rowlin<C, 8, R, LN, RES><<<dim3((unsigned)mmr::ceil_div(T, G::TOK)), 512, lds, st>>>(x, xs, kp, g, b, pack, bias,
+                                                                                         res, y, T, N, eps);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
 
 }  // namespace
 
@@ -291,6 +461,53 @@ mmr_status mmr_x3_swin_mlp(const float* x, const float* ln_g, const float* ln_b,
   if (c == 192) return launch_x3_mlp<192, 8, X3MLP_HC, 2>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
   mmr::set_error("mmr_x3_swin_mlp: C=%d not built (96, 192)", c);
   return MMR_ERR_UNSUPPORTED;
+}
+
+int64_t mmr_x3_rowlin_pack_elems(int32_t n, int32_t c) {
+  return (c == 96 || c == 192) && n > 0 && n % 32 == 0 && n <= 4096 ? (int64_t)(n + 63) / 64 * 128 * c : 0;
+}
+
+mmr_status mmr_x3_rowlin_pack(const float* w, uint16_t* pack, int32_t n, int32_t c, void* stream) {
+  mmr::clear_error();
+  const int64_t total = mmr_x3_rowlin_pack_elems(n, c);
+  MMR_REQUIRE(w && pack, "mmr_x3_rowlin_pack: NULL pointer");
+  if (total <= 0) {
+    mmr::set_error("mmr_x3_rowlin_pack: n=%d c=%d not built (c 96 / 192, n %% 32 == 0, n <= 4096)", n, c);
+    return MMR_ERR_UNSUPPORTED;
+  }
+  const dim3 grid((unsigned)mmr::ceil_div(total, 256));
+  hipStream_t st = mmr::as_stream(stream);
+  if (c == 96) x3_rowlin_pack<96><<<grid, 256, 0, st>>>(w, pack, n, total);
+  else x3_rowlin_pack<192><<<grid, 256, 0, st>>>(w, pack, n, total);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_x3_rowlin(const float* x, const uint16_t* xs, const float* ln_g, const float* ln_b, const uint16_t* pack,
+                         const float* bias, const float* residual, float* y, int64_t tokens, int32_t n, int32_t c,
+                         float eps, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(mmr_x3_rowlin_pack_elems(n, c) > 0, "mmr_x3_rowlin: n=%d c=%d not built", n, c);
+  MMR_REQUIRE((x != nullptr) != (xs != nullptr), "mmr_x3_rowlin: exactly one of x (f32 rows) / xs (split rows)");
+  MMR_REQUIRE(!x || (ln_g && ln_b), "mmr_x3_rowlin: f32 rows are taken with their LayerNorm");
+  MMR_REQUIRE(pack && bias && y && tokens >= 0 && y != residual && (const void*)y != (const void*)x,
+              "mmr_x3_rowlin: bad arguments");
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  MMR_REQUIRE(al(x) && al(xs) && al(y) && al(residual) && al(bias), "mmr_x3_rowlin: 16-B aligned pointers");
+  MMR_REQUIRE(c != 96 || n > 64, "mmr_x3_rowlin: c=96 takes n > 64 (its 3-deep weight ring)");
+  if (tokens == 0) return MMR_OK;
+  hipStream_t st = mmr::as_stream(stream);
+  const int kp = mmr_x3_p8_kpad(c);
+  if (c == 96) {
+    if (x) return residual ? launch_rowlin<96, true, true>(x, xs, kp, ln_g, ln_b, pack, bias, residual, y, tokens, n, eps, st)
+                           : launch_rowlin<96, true, false>(x, xs, kp, ln_g, ln_b, pack, bias, residual, y, tokens, n, eps, st);
+    return residual ? launch_rowlin<96, false, true>(x, xs, kp, ln_g, ln_b, pack, bias, residual, y, tokens, n, eps, st)
+                    : launch_rowlin<96, false, false>(x, xs, kp, ln_g, ln_b, pack, bias, residual, y, tokens, n, eps, st);
+  }
+  if (x) return residual ? launch_rowlin<192, true, true>(x, xs, kp, ln_g, ln_b, pack, bias, residual, y, tokens, n, eps, st)
+                         : launch_rowlin<192, true, false>(x, xs, kp, ln_g, ln_b, pack, bias, residual, y, tokens, n, eps, st);
+  return residual ? launch_rowlin<192, false, true>(x, xs, kp, ln_g, ln_b, pack, bias, residual, y, tokens, n, eps, st)
+                  : launch_rowlin<192, false, false>(x, xs, kp, ln_g, ln_b, pack, bias, residual, y, tokens, n, eps, st);
 }
 
 }  // extern "C"

@@ -784,6 +784,37 @@ def x3_swin_mlp(x, g, b, pack, b1, b2, eps):
     return y
 
 
+def x3_rowlin_pack(w):
+    """f32 weight [n][c] (device) -> the streamed W^T chunks of x3_rowlin, or None if (n, c) is not built."""
+    n, c = w.shape
+    e = _L().mmr_x3_rowlin_pack_elems(n, c)
+    if e <= 0 or (c == 96 and n <= 64):
+        return None
+    pack = torch.empty((e,), dtype=torch.bfloat16, device=w.device)
+    _chk(_L().mmr_x3_rowlin_pack(_lib.ptr(w.contiguous()), _lib.ptr(pack), n, c, _s(w)), "mmr_x3_rowlin_pack")
+    return pack
+
+
+def x3_rowlin(x, pack, bias, n, ln=None, residual=None):
+    """y = LN(x) W^T + b (+ residual) for f32 token rows x (..., c) with ln = (gamma, beta, eps), or
+    xs W^T + b (+ residual) for an X3Rows x (the window attention's split rows); y f32 (..., n)."""
+    if isinstance(x, X3Rows):
+        c, lead, xf, xs = x.k, x.lead, None, x.t
+    else:
+        c, lead, xf, xs = x.shape[-1], tuple(x.shape[:-1]), x.contiguous(), None
+        assert ln is not None, "f32 rows are taken with their LayerNorm"
+    _lib.require_gpu(x.t if xs is not None else xf)
+    rows = 1
+    for d in lead:
+        rows *= d
+    y = torch.empty(lead + (n,), dtype=torch.float32, device=(xs if xs is not None else xf).device)
+    r = residual.contiguous() if residual is not None else None
+    g, b, eps = ln if ln is not None else (None, None, 0.0)
+    _chk(_L().mmr_x3_rowlin(_lib.ptr(xf), _lib.ptr(xs), _lib.ptr(g), _lib.ptr(b), _lib.ptr(pack), _lib.ptr(bias),
+                            _lib.ptr(r), _lib.ptr(y), rows, n, c, float(eps), _s(y)), "mmr_x3_rowlin")
+    return y
+
+
 def x3_attention(q, k, v, b, lq, lk, heads, dh, scale, out=None, mean_out=None, mask=None):
     """f32 attention core over strided row views (mmr_x3_attention); mask (b, lk) int64 or None."""
     _lib.require_gpu(q)

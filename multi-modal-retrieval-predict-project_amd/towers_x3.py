@@ -12,7 +12,8 @@ same dataflow as the bf16 towers (towers.py, fusion.py), but:
   * attention: ops.x3_attention / ops.x3_swin_window_attention (q k^T and P V both bf16x3, expf softmax);
   * LayerNorm: the f32 row kernel (ops.ln_rows), PatchMerging / BERT embeddings / means: f32 kernels;
   * Swin stages 1-2 (C = 96 / 192): LayerNorm + fc1 + GELU + fc2 + residual fused (ops.x3_swin_mlp,
-    csrc/x3_mlp.hip), the hidden never leaving the CU.
+    csrc/x3_mlp.hip), the hidden never leaving the CU; norm1 + qkv and proj + residual as streamed
+    row-linears (ops.x3_rowlin: W^T through LDS, the x split in registers, no padded GEMM tiles).
 """
 import math
 
@@ -79,11 +80,15 @@ class SwinTowerX3:
                     "fc2_w": _x3(sd[p + "mlp.fc2.weight"], dev), "fc2_b": _f(sd[p + "mlp.fc2.bias"], dev),
                 })
                 b_ = st["blocks"][-1]
-                b_["mlp_pack"] = ops.x3_swin_mlp_pack(b_["fc1_w"].w, b_["fc2_w"].w)  # C = 96 / 192: fused
+                # C = 96 / 192: the fused MLP and the streamed row-linears (norm1 + qkv, proj + residual)
+                b_["mlp_pack"] = ops.x3_swin_mlp_pack(b_["fc1_w"].w, b_["fc2_w"].w)
+                b_["qkv_pack"] = ops.x3_rowlin_pack(b_["qkv_w"].w)
+                b_["proj_pack"] = ops.x3_rowlin_pack(b_["proj_w"].w)
             self.stages.append(st)
         self.norm_g, self.norm_b = _f(sd["norm.weight"], dev), _f(sd["norm.bias"], dev)
         self.num_features = E * 2 ** (len(self.cfg["depths"]) - 1)
-        self.fused_mlp = True  # the fused x3 MLP where built (A/B attribute)
+        self.fused_mlp = True      # the fused x3 MLP where built (A/B attribute)
+        self.fused_linears = True  # the streamed x3 row-linears (norm1 + qkv, proj) where built (A/B attribute)
 
     def tokens(self, image):
         """(B,3,H,W) f32 -> (B, h, w, C) f32 tokens BEFORE the final norm."""
@@ -101,10 +106,18 @@ class SwinTowerX3:
             heads = cfg["num_heads"][i]
             ws = min(cfg["window_size"], H)
             for bk in st["blocks"]:
-                h = ops.x3_ln_split(x, bk["n1g"], bk["n1b"], 1e-5)
-                qkv = ops.x3_linear(h, bk["qkv_w"], bk["qkv_b"])
+                C = x.shape[-1]
+                rowlin = self.fused_linears and bk["qkv_pack"] is not None
+                if rowlin:
+                    qkv = ops.x3_rowlin(x, bk["qkv_pack"], bk["qkv_b"], 3 * C, ln=(bk["n1g"], bk["n1b"], 1e-5))
+                else:
+                    h = ops.x3_ln_split(x, bk["n1g"], bk["n1b"], 1e-5)
+                    qkv = ops.x3_linear(h, bk["qkv_w"], bk["qkv_b"])
                 a = ops.x3_swin_window_attention_split(qkv, bk["bias"], H, heads, ws, bk["shift"])
-                x = ops.x3_linear(a, bk["proj_w"], bk["proj_b"], residual=x)
+                if rowlin and bk["proj_pack"] is not None and isinstance(a, ops.X3Rows):
+                    x = ops.x3_rowlin(a, bk["proj_pack"], bk["proj_b"], C, residual=x)
+                else:
+                    x = ops.x3_linear(a, bk["proj_w"], bk["proj_b"], residual=x)
                 if self.fused_mlp and bk["mlp_pack"] is not None:
                     x = ops.x3_swin_mlp(x, bk["n2g"], bk["n2b"], bk["mlp_pack"], bk["fc1_b"], bk["fc2_b"], 1e-5)
                 else:

@@ -154,6 +154,37 @@ def test_x3_swin_mlp_vs_f64(T, C):
     assert _rel(y, y_chain) < 1e-5
 
 
+@pytest.mark.parametrize("T,C,N,mode", [(4096, 96, 288, "ln"), (1000, 96, 96, "xs"), (2048, 192, 576, "ln"),
+                                         (300, 192, 192, "xs"), (512, 96, 96, "ln_res")])
+def test_x3_rowlin_vs_f64(T, C, N, mode):
+    """The streamed x3 row-linear: LN(x) W^T + b (the Swin norm1 + qkv) and xs W^T + b + r (proj over the
+    window attention's split rows) against f64, and against the x3 GEMM route within the x3 bound."""
+    g_ = torch.Generator().manual_seed(T + C + N)
+    x = (torch.randn(T, C, generator=g_) * 1.5 + 0.2).to(DEV)
+    gm = (1 + 0.1 * torch.randn(C, generator=g_)).to(DEV)
+    bt = (0.1 * torch.randn(C, generator=g_)).to(DEV)
+    w = (torch.randn(N, C, generator=g_) * C ** -0.5).to(DEV)
+    b = (0.1 * torch.randn(N, generator=g_)).to(DEV)
+    r = torch.randn(T, N, generator=g_).to(DEV) if mode != "ln" else None
+    pack = ops.x3_rowlin_pack(w)
+    xd = x.double().cpu()
+    if mode.startswith("ln"):
+        y = ops.x3_rowlin(x, pack, b, N, ln=(gm, bt, 1e-5), residual=r)
+        z = (xd - xd.mean(-1, keepdim=True)) / torch.sqrt(xd.var(-1, unbiased=False, keepdim=True) + 1e-5)
+        z = z * gm.double().cpu() + bt.double().cpu()
+        y_gemm = ops.x3_linear(ops.x3_ln_split(x, gm, bt, 1e-5), ops.X3W(w), b, residual=r)
+    else:
+        kp = _lib.lib().mmr_x3_p8_kpad(C)
+        xr = ops.X3Rows(_split_bits(x, kp).view(torch.bfloat16), C, kp, (T,))
+        y = ops.x3_rowlin(xr, pack, b, N, residual=r)
+        z = xr.t[:, :C].double().cpu() + xr.t[:, kp:kp + C].double().cpu()  # the split rows' exact value
+        y_gemm = ops.x3_linear(x, ops.X3W(w), b, residual=r)
+    y64 = z @ w.double().cpu().T + b.double().cpu() + (r.double().cpu() if r is not None else 0)
+    assert y.shape == (T, N)
+    assert _rel(y, y64) < 1e-5
+    assert _rel(y, y_gemm) < 1e-5
+
+
 @pytest.mark.parametrize("rows,c,res", [(1024, 96, True), (512, 192, False), (768, 384, True), (256, 768, True),
                                         (256, 100, False), (13, 768, True), (7, 96, False)])
 def test_ln_rows_split(rows, c, res):
