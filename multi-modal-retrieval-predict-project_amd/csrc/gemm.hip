@@ -1083,7 +1083,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
     }
     if constexpr (OF32) {
       // f32 output (the x3 towers' K' = 3K split GEMM): lane row 16 i + efr, columns 16 j + 4 efq .. + 3
-      // -> one 16-B store per (i, j), no LDS round; bias, exact-erf GELU (as torch), then the f32 residual
+      // -> one 16-B store per (i, j), no LDS round; bias, erf GELU (A-S erf, |err| <= 1.5e-7), then the f32 residual
       // (loaded per m-tile: they retire behind the next tile's prefetch, once per tile)
       // Y / R are [M][ldn] f32 with ldn <= N (N = the weight image's rows, padded to whole tiles): the
       // tile's 256 rows as one buffer (64-bit base in SGPRs, 32-bit offsets), columns >= ldn get an
@@ -1113,7 +1113,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
           f32x4 v = acc[i][j] + bq[j];
           if constexpr (ACT == 1) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = 0.5f * v[e] * (1.0f + erff(v[e] * 0.70710678118654752f));
+            for (int e = 0; e < 4; ++e) v[e] = mmr::gelu_erf(v[e]);  // A-S erf (1.5e-7): x3 mode, as linear_x3
           }
           if constexpr (HAS_RES) v += rr4[j];
           if constexpr (OSPL) {

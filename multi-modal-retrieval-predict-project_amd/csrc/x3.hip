@@ -58,8 +58,9 @@ __device__ __forceinline__ f32x4 mfma3(const bf16x8 ah, const bf16x8 al, const b
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc, 0, 0, 0);
 }
 
-// GELU exactly as torch's default (erf form), ocml erff
-__device__ __forceinline__ float gelu_exact(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// GELU (erf form, as torch) with erf by Abramowitz-Stegun 7.1.26 (|err| <= 1.5e-7, mmr::gelu_erf): 100x below
+// the bf16x3 products' 2^-17, branch-free (ocml erff made the GEMM epilogues VALU-heavy)
+__device__ __forceinline__ float gelu_exact(float x) { return mmr::gelu_erf(x); }
 
 // ------------------------------------------------------------------ GEMM
 constexpr int GX_BM = 128, GX_BN = 128, GX_BK = 32, GX_LD = 40;  // LDS row stride 80 B: conflict-free 16-B reads
