@@ -199,11 +199,9 @@ int32_t mmr_linear_bf16_n_variants(void);
 /* Test / A-B hook (the product path never calls it): pin a launch variant for the whole process.
  *   MMR_PIN_GEMM_BF16: value = mmr_linear_bf16 variant index, or -1 = per-shape tuning (default);
  *   MMR_PIN_X3_WAVES:  value = 4 or 8 waves per mmr_linear_x3 tile (8 only where K % 256 == 0),
- *                      or -1 = automatic (default);
- *   MMR_PIN_X3_ATTN:   value = 1 runs the x3 attention entry points on the round-4 kernel, 2 the fused x3
- *                      Swin MLP with ocml erff (A/B only); 0 / -1 = the defaults.
+ *                      or -1 = automatic (default).
  * MMR_ERR_INVALID for an unknown pin or value. */
-enum { MMR_PIN_GEMM_BF16 = 0, MMR_PIN_X3_WAVES = 1, MMR_PIN_X3_ATTN = 2 };
+enum { MMR_PIN_GEMM_BF16 = 0, MMR_PIN_X3_WAVES = 1 };
 mmr_status mmr_pin_variant(int32_t which, int32_t value);
 
 /* Resident-weight streaming linear for the short-K, narrow tower linears (Swin patch embed, stage-2

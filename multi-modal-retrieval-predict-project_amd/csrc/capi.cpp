@@ -19,7 +19,6 @@ void set_error(const char* fmt, ...) {
 void clear_error() { g_err[0] = 0; }
 std::atomic<int> pin_gemm_bf16{-1};
 std::atomic<int> pin_x3_waves{-1};
-std::atomic<int> pin_x3_attn{-1};
 }  // namespace mmr
 
 extern "C" {
@@ -37,11 +36,6 @@ mmr_status mmr_pin_variant(int32_t which, int32_t value) {
   if (which == MMR_PIN_X3_WAVES) {
     MMR_REQUIRE(value == -1 || value == 4 || value == 8, "mmr_pin_variant: x3 waves %d (-1, 4, 8)", value);
     mmr::pin_x3_waves.store(value);
-    return MMR_OK;
-  }
-  if (which == MMR_PIN_X3_ATTN) {
-    MMR_REQUIRE(value >= -1 && value <= 2, "mmr_pin_variant: x3 attention %d (-1 .. 2)", value);
-    mmr::pin_x3_attn.store(value);
     return MMR_OK;
   }
   mmr::set_error("mmr_pin_variant: unknown pin %d", which);

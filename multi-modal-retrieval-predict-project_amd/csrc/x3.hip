@@ -159,11 +159,6 @@ __global__ __launch_bounds__(256, 2) void x3_gemm(const float* __restrict__ X, i
 }
 
 // ------------------------------------------------------------------ attention
-// Workgroup = (sequence / window bb, head); 4 waves, wave w owns query tiles of 16 rows (w + 4 j);
-// keys in chunks of 64 staged in LDS as hi / lo K rows [key][DH + 8] and hi / lo V^T rows
-// [d][64 + 8]; head dims padded to DH = 32 DT with zeros (dh % 8 == 0).
-// S (16 x 64 per wave): lane (r, g) holds S[4 g + i][16 n + r]; P goes back through a wave-private
-// hi / lo LDS tile [16][64 + 8] as the A operand of O += P V (lane holds O[4 g + i][16 nd + r]).
 struct AttnArgs {
   const float* q;
   int64_t ldq;
@@ -183,248 +178,6 @@ struct AttnArgs {
   int kp;             //   instead of out; columns heads*dh .. kp written zero by the last head
 };
 
-template <int DT, bool SWIN, int QTW = 1>
-__global__ __launch_bounds__(256) void x3_attention(const AttnArgs a) {
-  // QTW query tiles of 64 rows per pass (wave w owns rows 64 u + 16 w ..): each staged key chunk serves
-  // QTW tiles (lq <= 128 with QTW = 2: K / V split and staged once instead of twice)
-  constexpr int DH = 32 * DT, KLD = DH + 8, VLD = 72;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint16_t* sKh = (uint16_t*)smem;
-  uint16_t* sKl = sKh + 64 * KLD;
-  uint16_t* sVh = sKl + 64 * KLD;
-  uint16_t* sVl = sVh + DH * VLD;
-  uint16_t* sPh = sVl + DH * VLD;    // [4 waves][16][VLD]
-  uint16_t* sPl = sPh + 4 * 16 * VLD;
-  float* sMean = (float*)(sPl + 4 * 16 * VLD);  // [4][DH]
-  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-  const int r = lane & 15, g = lane >> 4;
-  const int head = (int)(blockIdx.x % (unsigned)a.heads);
-  const int64_t bb = blockIdx.x / (unsigned)a.heads;
-  const int lq = a.lq, lk = a.lk, dh = a.dh;
-  // token maps
-  int64_t sw_base = 0;
-  int wy = 0, wx = 0, type = 0, nwin1 = 1;
-  if constexpr (SWIN) {
-    nwin1 = a.hw / a.ws;
-    const int nwin = nwin1 * nwin1;
-    const int win = (int)(bb % nwin);
-    sw_base = (bb / nwin) * (int64_t)a.hw * a.hw;
-    wy = win / nwin1;
-    wx = win % nwin1;
-    type = a.shift > 0 ? ((wy == nwin1 - 1) ? 2 : 0) + ((wx == nwin1 - 1) ? 1 : 0) : 0;
-  }
-  auto qtok = [&](int i) -> int64_t {
-    if constexpr (SWIN) {
-      const int hr = wy * a.ws + i / a.ws, wr = wx * a.ws + i % a.ws;
-      return sw_base + (int64_t)((hr + a.shift) % a.hw) * a.hw + (wr + a.shift) % a.hw;
-    } else {
-      return bb * lq + i;
-    }
-  };
-  auto ktok = [&](int j) -> int64_t {
-    if constexpr (SWIN) return qtok(j);
-    else return bb * lk + j;
-  };
-  const float* qb = a.q + head * dh;
-  const float* kb = a.k + head * dh;
-  const float* vb = a.v + head * dh;
-  float macc[2 * DT];
-#pragma unroll
-  for (int nd = 0; nd < 2 * DT; ++nd) macc[nd] = 0.f;
-  uint16_t* pH = sPh + wave * 16 * VLD;
-  uint16_t* pL = sPl + wave * 16 * VLD;
-  for (int q0 = 0; q0 < lq; q0 += 64 * QTW) {
-    int qbase[QTW];
-    bf16x8 qh[QTW][DT], ql[QTW][DT];
-#pragma unroll
-    for (int u = 0; u < QTW; ++u) {
-      qbase[u] = q0 + 64 * u + wave * 16;
-      const int qi = qbase[u] + r < lq ? qbase[u] + r : lq - 1;
-      const float* qp = qb + qtok(qi) * a.ldq;
-#pragma unroll
-      for (int ks = 0; ks < DT; ++ks) {
-        const int d = 32 * ks + 8 * g;
-        const int dc = d < dh ? d : 0;  // clamped, masked below
-        float4 x0 = *(const float4*)(qp + dc), x1 = *(const float4*)(qp + dc + 4);
-        if (d >= dh) x0 = x1 = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (SWIN) {  // timm scales q before q k^T
-          x0 = make_float4(x0.x * a.scale, x0.y * a.scale, x0.z * a.scale, x0.w * a.scale);
-          x1 = make_float4(x1.x * a.scale, x1.y * a.scale, x1.z * a.scale, x1.w * a.scale);
-        }
-        split8(x0, x1, qh[u][ks], ql[u][ks]);
-      }
-    }
-    float mrow[QTW][4], lrow[QTW][4];
-    f32x4 o[QTW][2 * DT];
-#pragma unroll
-    for (int u = 0; u < QTW; ++u) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        mrow[u][i] = -INFINITY;
-        lrow[u][i] = 0.f;
-      }
-#pragma unroll
-      for (int nd = 0; nd < 2 * DT; ++nd) o[u][nd] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-    for (int kc = 0; kc < lk; kc += 64) {
-      __syncthreads();  // every wave done with the previous chunk's K / V
-      for (int e = t; e < 64 * (DH / 4); e += 256) {
-        const int key = e / (DH / 4), d4 = e % (DH / 4), d = 4 * d4;
-        const int j = kc + key < lk ? kc + key : lk - 1;
-        const int64_t tk = ktok(j);
-        const int dc = d < dh ? d : 0;
-        float4 kv = *(const float4*)(kb + tk * a.ldk + dc);
-        float4 vv = *(const float4*)(vb + tk * a.ldv + dc);
-        if (d >= dh) kv = vv = make_float4(0.f, 0.f, 0.f, 0.f);
-        uint2 h, l;
-        split4(kv, h, l);
-        *(uint2*)(sKh + key * KLD + d) = h;
-        *(uint2*)(sKl + key * KLD + d) = l;
-        split4(vv, h, l);
-        sVh[(d + 0) * VLD + key] = (uint16_t)(h.x & 0xFFFF);
-        sVh[(d + 1) * VLD + key] = (uint16_t)(h.x >> 16);
-        sVh[(d + 2) * VLD + key] = (uint16_t)(h.y & 0xFFFF);
-        sVh[(d + 3) * VLD + key] = (uint16_t)(h.y >> 16);
-        sVl[(d + 0) * VLD + key] = (uint16_t)(l.x & 0xFFFF);
-        sVl[(d + 1) * VLD + key] = (uint16_t)(l.x >> 16);
-        sVl[(d + 2) * VLD + key] = (uint16_t)(l.y & 0xFFFF);
-        sVl[(d + 3) * VLD + key] = (uint16_t)(l.y >> 16);
-      }
-      __syncthreads();
-#pragma unroll
-      for (int u = 0; u < QTW; ++u) {
-        f32x4 s[4];
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-          s[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int ks = 0; ks < DT; ++ks) {
-            const bf16x8 khv = *(const bf16x8*)(sKh + (16 * n + r) * KLD + 32 * ks + 8 * g);
-            const bf16x8 klv = *(const bf16x8*)(sKl + (16 * n + r) * KLD + 32 * ks + 8 * g);
-            s[n] = mfma3(qh[u][ks], ql[u][ks], khv, klv, s[n]);
-          }
-        }
-        // scale / bias / mask, then the online softmax update per query row 4 g + i
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-          const int key = kc + 16 * n + r;
-          bool valid = key < lk;
-          if (!SWIN && a.kmask) valid = valid && a.kmask[bb * lk + (valid ? key : 0)] != 0;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float x = s[n][i];
-            if constexpr (SWIN) {
-              const int qi = qbase[u] + 4 * g + i;
-              x += a.bias[(((int64_t)type * a.heads + head) * 64 + (qi < 64 ? qi : 63)) * 64 + (key < 64 ? key : 63)];
-            } else {
-              x *= a.scale;
-            }
-            s[n][i] = valid ? x : -INFINITY;
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float cm = fmaxf(fmaxf(s[0][i], s[1][i]), fmaxf(s[2][i], s[3][i]));
-          cm = mmr::row16_max(cm);
-          const float mnew = fmaxf(mrow[u][i], cm);
-          float corr = 1.f, ps = 0.f;
-          if (mnew != -INFINITY) {
-            corr = mrow[u][i] == -INFINITY ? 0.f : expf(mrow[u][i] - mnew);
-#pragma unroll
-            for (int n = 0; n < 4; ++n) {
-              const float p = s[n][i] == -INFINITY ? 0.f : expf(s[n][i] - mnew);
-              s[n][i] = p;
-              ps += p;
-            }
-          } else {
-#pragma unroll
-            for (int n = 0; n < 4; ++n) s[n][i] = 0.f;
-          }
-          ps = mmr::row16_sum(ps);
-          lrow[u][i] = lrow[u][i] * corr + ps;
-          mrow[u][i] = mnew;
-#pragma unroll
-          for (int nd = 0; nd < 2 * DT; ++nd) o[u][nd][i] *= corr;
-        }
-        // P (f32) -> hi / lo through the wave's LDS tile
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float p = s[n][i];
-            const uint16_t h = mmr::f2bf(p);
-            const uint16_t l = mmr::f2bf(p - mmr::bf2f(h));
-            pH[(4 * g + i) * VLD + 16 * n + r] = h;
-            pL[(4 * g + i) * VLD + 16 * n + r] = l;
-          }
-        __syncthreads();
-#pragma unroll
-        for (int ks2 = 0; ks2 < 2; ++ks2) {
-          const bf16x8 pah = *(const bf16x8*)(pH + r * VLD + 32 * ks2 + 8 * g);
-          const bf16x8 pal = *(const bf16x8*)(pL + r * VLD + 32 * ks2 + 8 * g);
-#pragma unroll
-          for (int nd = 0; nd < 2 * DT; ++nd) {
-            const bf16x8 vbh = *(const bf16x8*)(sVh + (16 * nd + r) * VLD + 32 * ks2 + 8 * g);
-            const bf16x8 vbl = *(const bf16x8*)(sVl + (16 * nd + r) * VLD + 32 * ks2 + 8 * g);
-            o[u][nd] = mfma3(pah, pal, vbh, vbl, o[u][nd]);
-          }
-        }
-        if (QTW > 1) __syncthreads();  // the wave's P tile is rewritten by the next query tile
-      }
-    }
-    // finalise these query tiles: O / l (a row with every key masked -> 0)
-#pragma unroll
-    for (int u = 0; u < QTW; ++u)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int qi = qbase[u] + 4 * g + i;
-        const float inv = lrow[u][i] > 0.f ? 1.0f / lrow[u][i] : 0.f;
-        const bool ok = qi < lq;
-        float* orow = a.out ? a.out + qtok(ok ? qi : 0) * a.ldo + head * dh : nullptr;
-        uint16_t* xrow = a.xs ? a.xs + qtok(ok ? qi : 0) * 2 * a.kp : nullptr;
-#pragma unroll
-        for (int nd = 0; nd < 2 * DT; ++nd) {
-          const int d = 16 * nd + r;
-          const float val = o[u][nd][i] * inv;
-          if (xrow) {
-            // lane pair (r, r ^ 1) holds columns d0, d0 + 1: the even lane stores their hi pair, the odd
-            // lane their lo pair (one 4-B store per lane, as the f32 output's)
-            const float oth = mmr::dppf<0xB1>(val);  // quad_perm [1,0,3,2]: lane r ^ 1
-            const bool odd = r & 1;
-            const float v0 = odd ? oth : val, v1 = odd ? val : oth;
-            const uint32_t hp = mmr::pack2bf(v0, v1);
-            const uint32_t word =
-                odd ? mmr::pack2bf(v0 - __uint_as_float(hp << 16), v1 - __uint_as_float(hp & 0xFFFF0000u)) : hp;
-            if (ok && d < dh) *(uint32_t*)(xrow + (odd ? a.kp : 0) + head * dh + (d & ~1)) = word;
-          }
-          if (ok) {
-            if (xrow) {
-            } else if (orow && d < dh) {
-              orow[d] = val;
-            }
-            macc[nd] += val;
-          }
-        }
-        if (xrow && ok && head == a.heads - 1)
-          for (int z = a.heads * dh + r; z < a.kp; z += 16) xrow[z] = xrow[a.kp + z] = 0;
-      }
-  }
-  if (a.mean_out) {
-#pragma unroll
-    for (int nd = 0; nd < 2 * DT; ++nd) {
-      float v = macc[nd];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      if (g == 0) sMean[wave * DH + 16 * nd + r] = v;
-    }
-    __syncthreads();
-    if (t < dh) {
-      const float s4 = ((sMean[t] + sMean[DH + t]) + sMean[2 * DH + t]) + sMean[3 * DH + t];
-      a.mean_out[bb * (int64_t)a.heads * dh + head * dh + t] = s4 / lq;
-    }
-  }
-}
-
 // ------------------------------------------------------------------ attention, round 5 (x3_mha)
 // The bf16 core's structure (fusion.hip mha_small) on bf16x3 operands.  Block = (sequence or window,
 // head); nwv = min(4, ceil(lq / 32)) waves, one 32-query tile per wave, the block walking its query
@@ -434,8 +187,9 @@ __global__ __launch_bounds__(256) void x3_attention(const AttnArgs a) {
 // registers, and P^T is split in registers into the B operands of O^T += V^T . P^T (Vh.Ph + Vh.Pl +
 // Vl.Ph), V^T read from key-major hi / lo images by ds_read_b64_tr_b16 in P^T's key permutation.
 // K / V f32 rows are split ONCE per block while staged (16-B LDS writes), Q once per wave in registers.
-// (The round-4 kernel above ran 16-query tiles on 16x16x32 MFMAs with P re-split through LDS by
-// 2-byte stores and V^T written by 2-byte transposing stores: 0.06 of the bf16 MFMA peak.)
+// (The round-4 kernel ran 16-query tiles on 16x16x32 MFMAs with P re-split through LDS by 2-byte stores
+// and V^T written by 2-byte transposing stores: 0.06 of the bf16 MFMA peak; BERT 176 -> 119 us, Swin
+// stage 1 552 -> 444 us, profiles/r05_x3_attn_ab.txt.)
 // MODE 0: plain (nn.MultiheadAttention); 1: key-padding mask as HF's additive finfo.min (a row with
 // every key masked -> HF's uniform softmax, the mean of V over the lk keys); 2: Swin windows (roll /
 // partition folded into the token map, q pre-scaled as timm, rel-pos + shift-mask bias added).
@@ -1043,55 +797,33 @@ mmr_status launch_attention(const char* who, AttnArgs a, int64_t nbh, bool swin,
   if (nbh == 0) return MMR_OK;
   const int dt = (a.dh + 31) / 32;
   hipStream_t st = mmr::as_stream(stream);
-  if (mmr::pin_x3_attn.load(std::memory_order_relaxed) != 1) {
-    MMR_REQUIRE(!swin || dt == 1, "%s: Swin head_dim %d must be <= 32", who, a.dh);
-    const int nwv = std::min(4, (a.lq + 31) / 32);
-    const int lkp = (a.lk + 31) & ~31;
-    const int kbs = dt <= 2 ? std::min(128, lkp) : std::min(64, lkp);
-    const int dhp = 32 * dt, krow = dhp + 8, vrow = dhp + ((dt & 1) ? 0 : 16), orow = dhp + 4;
-    const size_t kv = (size_t)kbs * (krow + vrow) * 4, epi = (size_t)nwv * 32 * orow * 4;
-    const size_t lds = std::max(kv, epi) + (size_t)nwv * dhp * 4 + (size_t)kbs * 4 + (swin ? 64 * 8 : 0);
-    const dim3 grid((unsigned)nbh), blk(64 * nwv);
-    const int mode = swin ? 2 : (a.kmask ? 1 : 0);
+  MMR_REQUIRE(!swin || dt == 1, "%s: Swin head_dim %d must be <= 32", who, a.dh);
+  const int nwv = std::min(4, (a.lq + 31) / 32);
+  const int lkp = (a.lk + 31) & ~31;
+  const int kbs = dt <= 2 ? std::min(128, lkp) : std::min(64, lkp);
+  const int dhp = 32 * dt, krow = dhp + 8, vrow = dhp + ((dt & 1) ? 0 : 16), orow = dhp + 4;
+  const size_t kv = (size_t)kbs * (krow + vrow) * 4, epi = (size_t)nwv * 32 * orow * 4;
+  const size_t lds = std::max(kv, epi) + (size_t)nwv * dhp * 4 + (size_t)kbs * 4 + (swin ? 64 * 8 : 0);
+  const dim3 grid((unsigned)nbh), blk(64 * nwv);
+  const int mode = swin ? 2 : (a.kmask ? 1 : 0);
 #define XM(D_, M_) x3_mha<D_, M_><<<grid, blk, lds, st>>>(a, kbs)
-    if (mode == 2) XM(1, 2);
-    else if (mode == 1) {
-      switch (dt) {
-        case 1: XM(1, 1); break;
-        case 2: XM(2, 1); break;
-        case 3: XM(3, 1); break;
-        default: XM(4, 1); break;
-      }
-    } else {
-      switch (dt) {
-        case 1: XM(1, 0); break;
-        case 2: XM(2, 0); break;
-        case 3: XM(3, 0); break;
-        default: XM(4, 0); break;
-      }
-    }
-#undef XM
-    MMR_LAUNCH_CHECK();
-    return MMR_OK;
-  }
-  const int DH = 32 * dt;
-  const size_t lds = (size_t)2 * 64 * (DH + 8) * 2 + (size_t)2 * DH * 72 * 2 + (size_t)2 * 4 * 16 * 72 * 2 +
-                     (size_t)4 * DH * 4;
-  const dim3 grid((unsigned)nbh);
-  if (swin) {
-    MMR_REQUIRE(dt == 1, "%s: Swin head_dim %d must be <= 32", who, a.dh);
-    x3_attention<1, true><<<grid, 256, lds, st>>>(a);
-  } else {
-    // 65-128 query rows: both 64-row query tiles per key chunk (dh <= 64; at 96 / 128 the second tile's
-    // registers do not fit)
-    const bool two = a.lq > 64 && a.lq <= 128 && dt <= 2;
+  if (mode == 2) XM(1, 2);
+  else if (mode == 1) {
     switch (dt) {
-      case 1: if (two) x3_attention<1, false, 2><<<grid, 256, lds, st>>>(a); else x3_attention<1, false><<<grid, 256, lds, st>>>(a); break;
-      case 2: if (two) x3_attention<2, false, 2><<<grid, 256, lds, st>>>(a); else x3_attention<2, false><<<grid, 256, lds, st>>>(a); break;
-      case 3: if (two) x3_attention<3, false, 2><<<grid, 256, lds, st>>>(a); else x3_attention<3, false><<<grid, 256, lds, st>>>(a); break;
-      default: x3_attention<4, false><<<grid, 256, lds, st>>>(a); break;
+      case 1: XM(1, 1); break;
+      case 2: XM(2, 1); break;
+      case 3: XM(3, 1); break;
+      default: XM(4, 1); break;
+    }
+  } else {
+    switch (dt) {
+      case 1: XM(1, 0); break;
+      case 2: XM(2, 0); break;
+      case 3: XM(3, 0); break;
+      default: XM(4, 0); break;
     }
   }
+#undef XM
   MMR_LAUNCH_CHECK();
   return MMR_OK;
 }

@@ -1,4 +1,6 @@
-"""x3 attention A/B: the round-5 x3_mha kernel (default) vs the round-4 kernel (MMR_PIN_X3_ATTN = 1) on the
+"""(Round-5 record, profiles/r05_x3_attn_ab.txt: run at the commit that still held the round-4 kernel behind
+the pin mmr_pin_variant(2, 1); that kernel and pin are gone.)  x3 attention A/B: the round-5 x3_mha kernel vs
+the round-4 kernel on the
 cfg2 step's shapes (BERT B=256 x 128 with report-length masks, Swin stages 1-4 windows at B=256, the fusion
 stack's 8-head dh-96 calls), time per call (HIP events, min of 3 x 20 calls) and max |new - old| / max|old|.
 Diagnostic only."""

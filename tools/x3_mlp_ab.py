@@ -1,4 +1,5 @@
-"""x3 Swin MLP A/B at B = 256: the fused kernel (mmr_x3_swin_mlp) vs the unfused x3 chain (LayerNorm split
+"""(Round-5 record: the erff arm used a pin that is gone; the fused kernel now always uses the A-S erf.)
+x3 Swin MLP A/B at B = 256: the fused kernel (mmr_x3_swin_mlp) vs the unfused x3 chain (LayerNorm split
 -> fc1 GEMM writing split rows -> fc2 GEMM + residual) for stages 1-4 geometry, time per call (HIP events,
 min of 3 x 10) and max |fused - chain| / max|chain|.  Diagnostic only."""
 import os
