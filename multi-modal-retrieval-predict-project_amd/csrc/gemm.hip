@@ -1117,7 +1117,10 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
           }
           if constexpr (HAS_RES) v += rr4[j];
           if constexpr (OSPL) {
-            // [hi | lo] bf16 of the f32 value (the split mmr_x3_split_rows would make), row width 2 N
+            // [hi | lo] bf16 of the f32 value (the split mmr_x3_split_rows would make), row width 2 N; v pinned
+            // as the rounded f32 value: hipcc otherwise contracts the GELU's last multiply into v - hi (an fma),
+            // and lo would no longer be the split of the f32 output (bitwise tests against the f32 route)
+            mmr::pin(v);
             const uint32_t h0 = mmr::pack2bf(v[0], v[1]), h1 = mmr::pack2bf(v[2], v[3]);
             const uint32_t l0 = mmr::pack2bf(v[0] - __uint_as_float(h0 << 16), v[1] - __uint_as_float(h0 & 0xFFFF0000u));
             const uint32_t l1 = mmr::pack2bf(v[2] - __uint_as_float(h1 << 16), v[3] - __uint_as_float(h1 & 0xFFFF0000u));
