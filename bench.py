@@ -81,7 +81,7 @@ def parse(argv=None):
                         "8 heads), text / image (one tower + its head), both (both single-modality heads)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-queries", type=int, default=0)
-    p.add_argument("--parity-queries", type=int, default=64,
+    p.add_argument("--parity-queries", type=int, default=256,
                    help="queries re-embedded by the fp32 oracle for recall / P@10 vs the CPU path")
     a = p.parse_args(argv)
     pre = dict({"batch": 256, "gallery": 100_000, "k": 10, "model_type": "multimodal", "dim": 768,

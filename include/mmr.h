@@ -48,14 +48,18 @@ int mmr_max_k(void);
 /* Copy an (n, d) row-major gallery (host pointer if `gallery_is_host`, else device) into a
  * library-owned device layout on `device`, computing per-row inverse norms (f32) and norms (f64).
  * `idx_base` is added to every returned index (row-sharded galleries: global = local + base).
- * Only MMR_F32 is built in this round. */
+ * dtype MMR_F32: f32 rows (every scan mode).  MMR_F16: a native fp16 index — the raw fp16 rows are its only
+ * device copy (2 B per element + f32 inverse norms + f64 norms per row), scanned in mode 2 only (its exact
+ * f64 re-score reads the same rows: fp16 is exact in f64), results bit-identical to an MMR_F32 index of the
+ * f32-upcast rows; mmr_index_set_mode(0 / 1) returns MMR_ERR_UNSUPPORTED.  MMR_BF16: not built. */
 mmr_status mmr_index_create(const void* gallery, int64_t n, int32_t d, mmr_dtype dtype,
                             int gallery_is_host, int64_t idx_base, int device, mmr_index** out);
 mmr_status mmr_index_destroy(mmr_index* index);
 mmr_status mmr_index_info(const mmr_index* index, int64_t* n, int32_t* d, int64_t* idx_base);
-/* Device bytes the index holds: gallery_bytes = f32 rows + norms + the scan copies of the current
- * mode (x3: bf16 hi/lo split + tile16 f32, 8 B per element; f16: fp16 tile32h + row-major fp16,
- * 4 B per element; f32: none — copies of other modes are freed at a mode switch);
+/* Device bytes the index holds: gallery_bytes = the rows + norms + the scan copies of the current mode.
+ * MMR_F32 index: f32 rows (4 B per element) + the current mode's copies (x3: bf16 hi/lo split + tile16 f32,
+ * 8 B per element; f16: ONE fp16 unit-row copy in the tile32h layout, 2 B per element; f32: none — copies
+ * of other modes are freed at a mode switch).  MMR_F16 index: the fp16 rows only (2 B per element).
  * workspace_bytes = the query / per-unit-maxima workspace.  Either pointer may be NULL. */
 mmr_status mmr_index_device_bytes(const mmr_index* index, int64_t* gallery_bytes, int64_t* workspace_bytes);
 /* Pre-allocate the workspace for up to `max_q` queries in the CURRENT scan mode so that later

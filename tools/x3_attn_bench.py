@@ -1,9 +1,7 @@
-"""(Round-5 record, profiles/r05_x3_attn_ab.txt: run at the commit that still held the round-4 kernel behind
-the pin mmr_pin_variant(2, 1); that kernel and pin are gone.)  x3 attention A/B: the round-5 x3_mha kernel vs
-the round-4 kernel on the
-cfg2 step's shapes (BERT B=256 x 128 with report-length masks, Swin stages 1-4 windows at B=256, the fusion
-stack's 8-head dh-96 calls), time per call (HIP events, min of 3 x 20 calls) and max |new - old| / max|old|.
-Diagnostic only."""
+"""x3 attention (x3_mha) on the cfg2 step's shapes: BERT B=256 x 128 with report-length masks, Swin stages
+1-4 windows at B=256, the fusion stack's 8-head dh-96 calls; time per call (HIP events, min of 3 x 20).
+Also the driver of tools/gpu_pmc_swin.sh (PMC_PY) for the attention counters.  Diagnostic only.
+(The round-4 vs round-5 A/B it once ran is profiles/r05_x3_attn_ab.txt.)"""
 import math
 import os
 import sys
@@ -30,19 +28,9 @@ def timeit(fn, it=20):
 
 
 def ab(name, fn):
-    res = {}
-    for pin in (1, 0):
-        assert L.mmr_pin_variant(2, pin) == 0
-        t = min(timeit(fn) for _ in range(3))
-        out = fn()
-        torch.cuda.synchronize()
-        res[pin] = (t, [o.clone() for o in out])
-    L.mmr_pin_variant(2, -1)
-    err = max((n.double() - o.double()).abs().max().item() / max(o.double().abs().max().item(), 1e-30)
-              for n, o in zip(res[0][1], res[1][1]))
-    print(f"{name:34s} old {res[1][0]:8.1f} us  new {res[0][0]:8.1f} us  x{res[1][0] / res[0][0]:5.2f}  "
-          f"rel diff {err:.2e}", flush=True)
-    return res[1][0], res[0][0]
+    t = min(timeit(fn) for _ in range(3))
+    print(f"{name:34s} {t:8.1f} us", flush=True)
+    return t, t
 
 
 g = torch.Generator().manual_seed(5)
@@ -87,4 +75,4 @@ for name, b, lq, lk, want_out, per in (("fusion txt self 128x128", 256, 128, 128
     o, n = ab(name, run)
     tot_old += per * o
     tot_new += per * n
-print(f"per cfg2 x3 step (weighted by call counts): old {tot_old / 1e3:.2f} ms  new {tot_new / 1e3:.2f} ms", flush=True)
+print(f"per cfg2 x3 step (weighted by call counts): {tot_new / 1e3:.2f} ms", flush=True)

@@ -1,4 +1,4 @@
-"""(Round-5 record: the erff arm used a pin that is gone; the fused kernel now always uses the A-S erf.)
+"""(Round-5 record profiles/r05_x3_mlp_ab.txt; its erff arm used a pin that is gone.)
 x3 Swin MLP A/B at B = 256: the fused kernel (mmr_x3_swin_mlp) vs the unfused x3 chain (LayerNorm split
 -> fc1 GEMM writing split rows -> fc2 GEMM + residual) for stages 1-4 geometry, time per call (HIP events,
 min of 3 x 10) and max |fused - chain| / max|chain|.  Diagnostic only."""
@@ -39,13 +39,11 @@ for hw, C in ((56, 96), (28, 192)):
     tc = min(timeit(chain) for _ in range(3))
     yc = chain()
     gf = 48.0 * T * C * C / 1e9
-    for pin, name in ((2, "fused erff"), (-1, "fused A-S erf")):
-        L.mmr_pin_variant(2, pin)
+    for name in ("fused",):
         tf = min(timeit(fused) for _ in range(3))
         yf = fused()
         torch.cuda.synchronize()
         err = (yf - yc).abs().max().item() / yc.abs().max().item()
         print(f"C={C:4d} T={T:7d}: chain {tc:8.1f} us  {name} {tf:8.1f} us  x{tc / tf:5.2f}  ({gf / tf:.2f} PF bf16 "
               f"MFMA work)  rel diff vs chain {err:.2e}", flush=True)
-    L.mmr_pin_variant(2, -1)
     del x
