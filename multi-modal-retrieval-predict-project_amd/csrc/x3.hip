@@ -194,9 +194,12 @@ struct AttnArgs {
 // every key masked -> HF's uniform softmax, the mean of V over the lk keys); 2: Swin windows (roll /
 // partition folded into the token map, q pre-scaled as timm, rel-pos + shift-mask bias added).
 template <int DT, int MODE>
-__global__ __launch_bounds__(256, 2) void x3_mha(const AttnArgs a, int kbs) {
+__global__ __launch_bounds__(256, DT <= 2 ? 3 : 2) void x3_mha(const AttnArgs a, int kbs) {
   constexpr int DHP = DT * 32, KS = DHP / 16, KROW = DHP + 8, VROW = DHP + ((DT & 1) ? 0 : 16);
   constexpr int C8 = DHP / 8, OROW = DHP + 4;
+  // 32-key tiles per online-softmax step: 2 at DT = 1 (Swin); 1 at DT >= 2, so the S / P registers fit 3
+  // waves per SIMD at DT = 2 (an extra O rescale per 32 keys: one rounding, far below the products' 2^-17)
+  constexpr int TPS = DT >= 2 ? 1 : 2;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6, nwv = nthr >> 6;
   uint16_t* Kh = (uint16_t*)smem;  // [kbs][KROW]
@@ -257,7 +260,7 @@ __global__ __launch_bounds__(256, 2) void x3_mha(const AttnArgs a, int kbs) {
   // thread in flight (keys past lk / columns past dh read a clamped in-bounds chunk; columns past dh
   // are zeroed, keys past lk are -inf in the scores)
   auto stage = [&](int k0, int kn) {
-    constexpr int UB = DT >= 3 ? 2 : 4;  // chunks in flight per thread (register budget at DT 3 / 4)
+    constexpr int UB = DT >= 2 ? 2 : 4;  // chunks in flight per thread (register budget at DT >= 2)
     const int nch = kn * C8, tot = 2 * nch;
     for (int e0 = tid; e0 < tot; e0 += UB * nthr) {
       float4 xa[UB], xb[UB];
@@ -326,18 +329,18 @@ __global__ __launch_bounds__(256, 2) void x3_mha(const AttnArgs a, int kbs) {
       stage(k0, kn);
       __syncthreads();
       if (!active) continue;
-      for (int kb0 = 0; kb0 < kn; kb0 += 64) {
-        const int nt = min(64, kn - kb0) / 32;
-        bool live[2];
+      for (int kb0 = 0; kb0 < kn; kb0 += 32 * TPS) {
+        const int nt = min(32 * TPS, kn - kb0) / 32;
+        bool live[TPS];
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < TPS; ++t) {
           live[t] = t < nt;
           // fully masked 32-key tiles contribute exactly 0 once the row has an unmasked key
           if (MODE == 1 && live[t] && anyv) live[t] = __ballot(madd[kb0 + t * 32 + r] == 0.f) != 0;
         }
-        f32x16 s[2];
+        f32x16 s[TPS];
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < TPS; ++t) {
           s[t] = (f32x16){0};
           if (live[t]) {
             const int key = kb0 + t * 32 + r;
@@ -354,7 +357,7 @@ __global__ __launch_bounds__(256, 2) void x3_mha(const AttnArgs a, int kbs) {
         // scores (lane: query r; register rg: key kb0 + 32 t + (rg & 3) + 8 (rg >> 2) + 4 hf)
         float mloc = -INFINITY;
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < TPS; ++t) {
           if (!live[t]) continue;
 #pragma unroll
           for (int g4 = 0; g4 < 4; ++g4) {
@@ -383,7 +386,7 @@ __global__ __launch_bounds__(256, 2) void x3_mha(const AttnArgs a, int kbs) {
         m_run = m_new;
         float psum = 0.f;
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < TPS; ++t) {
           if (!live[t]) continue;
 #pragma unroll
           for (int rg = 0; rg < 16; ++rg) {
@@ -400,7 +403,7 @@ __global__ __launch_bounds__(256, 2) void x3_mha(const AttnArgs a, int kbs) {
         }
         // O^T[d][q] += V^T[d][key] . P^T[key][q] (three products), P^T split in registers
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < TPS; ++t) {
           if (!live[t]) continue;
 #pragma unroll
           for (int sidx = 0; sidx < 2; ++sidx) {
@@ -800,7 +803,7 @@ mmr_status launch_attention(const char* who, AttnArgs a, int64_t nbh, bool swin,
   MMR_REQUIRE(!swin || dt == 1, "%s: Swin head_dim %d must be <= 32", who, a.dh);
   const int nwv = std::min(4, (a.lq + 31) / 32);
   const int lkp = (a.lk + 31) & ~31;
-  const int kbs = dt <= 2 ? std::min(128, lkp) : std::min(64, lkp);
+  const int kbs = dt <= 1 ? std::min(128, lkp) : std::min(64, lkp);  // dt 2: 39 KB -> 3 blocks per CU (3 waves / SIMD)
   const int dhp = 32 * dt, krow = dhp + 8, vrow = dhp + ((dt & 1) ? 0 : 16), orow = dhp + 4;
   const size_t kv = (size_t)kbs * (krow + vrow) * 4, epi = (size_t)nwv * 32 * orow * 4;
   const size_t lds = std::max(kv, epi) + (size_t)nwv * dhp * 4 + (size_t)kbs * 4 + (swin ? 64 * 8 : 0);
