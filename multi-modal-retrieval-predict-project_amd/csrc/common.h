@@ -139,6 +139,37 @@ __device__ __forceinline__ T wave_sum(T v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// wave_sum of RB values at once (a[r] = lane's partial of row r): a reduce-scatter over the same xor
+// 32 / 16 / 8 ... tree, so every row total is bit-identical to wave_sum(a[r]) (each level adds the same
+// two partials; f64 / f32 addition is commutative).  The first log2(RB) levels halve the rows a lane
+// carries (upper lanes keep the upper half), the rest are wave_sum's levels on one value: the levels'
+// shuffles of all rows are independent, so a level costs one LDS round trip instead of RB.  Returns
+// the total of row `row` (padding rows past RB: 0); lanes with (lane & ((64 >> LOG) - 1)) == 0 hold
+// each row once.
+template <int RB, typename T>
+__device__ __forceinline__ T rows_wave_sum(const T (&a)[RB], int lane, int& row) {
+  constexpr int LOG = RB > 4 ? 3 : RB > 2 ? 2 : RB > 1 ? 1 : 0;
+  static_assert(RB <= 8, "rows_wave_sum: at most 8 rows");
+  constexpr int P = 1 << LOG;
+  T v[P];
+#pragma unroll
+  for (int r = 0; r < P; ++r) v[r] = r < RB ? a[r] : (T)0;
+  row = 0;
+#pragma unroll
+  for (int s = 0; s < LOG; ++s) {
+    const int m = 32 >> s, h = P >> (s + 1);
+    const bool up = (lane & m) != 0;
+    T sent[P / 2];
+#pragma unroll
+    for (int j = 0; j < h; ++j) sent[j] = __shfl_xor(up ? v[j] : v[h + j], m, 64);
+#pragma unroll
+    for (int j = 0; j < h; ++j) v[j] = (up ? v[h + j] : v[j]) + sent[j];
+    row += up ? h : 0;
+  }
+#pragma unroll
+  for (int m = 32 >> LOG; m > 0; m >>= 1) v[0] += __shfl_xor(v[0], m, 64);
+  return v[0];
+}
 template <typename T>
 __device__ __forceinline__ T wave_max(T v) {
 #pragma unroll

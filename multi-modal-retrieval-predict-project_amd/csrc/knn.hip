@@ -1241,7 +1241,7 @@ constexpr int kSlotCap = kMaxK + kCandCap;  // [0, kMaxK): carried top-K; [kMaxK
 
 // Phase clock of block 0 (tools/select_trace.hip builds this file with MMR_SELECT_TRACE; off in libmmr)
 #ifdef MMR_SELECT_TRACE
-__device__ long long g_sel_trace[16];
+__device__ long long g_sel_trace[24];
 #define SEL_MARK(i) \
   if (blockIdx.x == 0 && threadIdx.x == 0) g_sel_trace[i] = wall_clock64();
 #define SEL_VAL(i, v) \
@@ -1357,29 +1357,35 @@ __device__ uint32_t block_kth_lower_top4(uint32_t key, int kth, uint32_t* vals, 
   uint32_t v = key;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
+    // wave max: DPP within each 16-lane row, then the four rows' lanes 0 / 16 / 32 / 48 read into
+    // scalars (a 6-level shuffle butterfly paid 6 LDS round trips per round: 24 per call)
     uint32_t mx = v;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+    mx = max(mx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0xB1, 0xF, 0xF, false));
+    mx = max(mx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0x4E, 0xF, 0xF, false));
+    mx = max(mx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0x141, 0xF, 0xF, false));
+    mx = max(mx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mx, 0x140, 0xF, 0xF, false));
+    mx = max(max((uint32_t)__builtin_amdgcn_readlane((int)mx, 0), (uint32_t)__builtin_amdgcn_readlane((int)mx, 16)),
+             max((uint32_t)__builtin_amdgcn_readlane((int)mx, 32), (uint32_t)__builtin_amdgcn_readlane((int)mx, 48)));
     const uint64_t hit = __ballot(v == mx);
     if (lane == (int)__builtin_ctzll(hit)) v = 0u;  // key 0 sorts below every float key
     if (lane == 0) vals[wave * 4 + j] = mx;
   }
   __syncthreads();
-  if (tid < 64) {
-    const uint32_t mine = lane < NV ? vals[lane] : 0u;
-    int rank = 0;  // values ahead of mine (larger, or equal at a lower position); the others' values
-                   // by lane swaps (a loop of LDS reads paid the LDS latency per step, ~1.3 us)
+  // every wave ranks the NV candidates itself from LDS broadcast reads (one wave ranking them by lane
+  // swaps, then two more barriers to broadcast its pick, cost ~0.5 us of the phase)
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const uint32_t mine = lane < NV ? vals[lane] : 0u;
+  int rank = 0;  // values ahead of mine (larger, or equal at a lower position)
 #pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      const uint32_t o = (uint32_t)__shfl((int)mine, j, 64);
-      rank += (o > mine) || (o == mine && j < lane);
-    }
-    if (lane < NV && rank == kth - 1) bcast[0] = mine;
+  for (int j4 = 0; j4 < NV / 4; ++j4) {
+    const u32x4 o4 = *(const u32x4*)(vals + 4 * j4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) rank += (o4[e] > mine) || (o4[e] == mine && 4 * j4 + e < lane);
   }
-  __syncthreads();
-  const uint32_t r = bcast[0];
-  __syncthreads();
-  return r;
+  // ranks are a permutation of 0 .. NV-1 and kth <= NV: exactly one lane holds the kth largest
+  const uint64_t hit = __ballot(lane < NV && rank == kth - 1);
+  (void)bcast;
+  return (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)__builtin_ctzll(hit));
 }
 
 // COARSE (MODE 1 / 2: 16 units = one 64-row block; MODE 3: 32): the scan also wrote per-(query, block) maxima
@@ -1583,7 +1589,9 @@ __global__ __launch_bounds__(T) void knn_select_t(
       const int64_t g = unit_row<MODE>(L.cand_u[s / GS], s % GS);
       L.row_s[kMaxK + s] = (int)(g < n ? g : n);
     }
-    __syncthreads();
+    // the loads below compute their rows from cand_u themselves (row_s is for the rank, behind the
+    // caller's barrier); only a non-RAW selection waits here, for wave 0's |q|
+    if (!RAW) __syncthreads();
     qn = L.qn;
     SEL_MARK(8)
     if constexpr (NC > 0) {
@@ -1605,7 +1613,8 @@ __global__ __launch_bounds__(T) void knn_select_t(
 #pragma unroll
           for (int r = 0; r < RB; ++r) {
             const int s = s0 + r;
-            const int64_t gi = s < nslot ? L.row_s[kMaxK + s] : n;
+            const int64_t gu = s < nslot ? unit_row<MODE>(L.cand_u[s / GS], s % GS) : n;
+            const int64_t gi = gu < n ? gu : n;
             gir[r] = gi;
             const int64_t gl = gi < n ? gi : 0;
             gnr[r] = gnorm64[gl];
@@ -1619,7 +1628,8 @@ __global__ __launch_bounds__(T) void knn_select_t(
 #pragma unroll
           for (int r = 0; r < RB; ++r) {
             const int s = s0 + r;
-            const int64_t gi = s < nslot ? L.row_s[kMaxK + s] : n;
+            const int64_t gu = s < nslot ? unit_row<MODE>(L.cand_u[s / GS], s % GS) : n;
+            const int64_t gi = gu < n ? gu : n;
             gir[r] = gi;
             const int64_t gl = gi < n ? gi : 0;
             gnr[r] = gnorm64[gl];
@@ -1631,6 +1641,7 @@ __global__ __launch_bounds__(T) void knn_select_t(
             }
           }
         }
+        double part[RB];
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
           double acc = 0.0;
@@ -1640,17 +1651,29 @@ __global__ __launch_bounds__(T) void knn_select_t(
             acc += (double)qv.x * gv[r][c].x + (double)qv.y * gv[r][c].y + (double)qv.z * gv[r][c].z +
                    (double)qv.w * gv[r][c].w;
           }
-          acc = mmr::wave_sum(acc);
-          const int s = s0 + r;
-          if (lane == 0 && s < nslot) {
-            const double gn = gnr[r];
-            L.cand_d[kMaxK + s] = gir[r] >= n ? -INFINITY : ((qn > 0.0 && gn > 0.0) ? acc / (qn * gn) : 0.0);
-          }
+          part[r] = acc;
+        }
+        // the RB rows' wave sums together (bit-identical to one wave_sum per row, which paid RB x 6
+        // dependent LDS round trips after the fetch)
+        int rr;
+        const double acc = mmr::rows_wave_sum<RB>(part, lane, rr);
+        constexpr int LOG = RB > 4 ? 3 : RB > 2 ? 2 : RB > 1 ? 1 : 0;
+        if ((lane & ((64 >> LOG) - 1)) == 0 && rr < RB && s0 + rr < nslot) {
+          double gn = gnr[0];
+          int64_t gi = gir[0];
+#pragma unroll
+          for (int r = 1; r < RB; ++r)
+            if (rr == r) {
+              gn = gnr[r];
+              gi = gir[r];
+            }
+          L.cand_d[kMaxK + s0 + rr] = gi >= n ? -INFINITY : ((qn > 0.0 && gn > 0.0) ? acc / (qn * gn) : 0.0);
         }
       }
     } else {
       for (int s = wave; s < nslot; s += T / 64) {
-        const int64_t gi = L.row_s[kMaxK + s];
+        const int64_t gu = unit_row<MODE>(L.cand_u[s / GS], s % GS);
+        const int64_t gi = gu < n ? gu : n;
         double sc = -INFINITY;
         if (gi < n) {
           double acc = 0.0;
@@ -1676,38 +1699,46 @@ __global__ __launch_bounds__(T) void knn_select_t(
     auto slot = [&](int u) { return u < carry ? u : kMaxK + u - carry; };
     // G threads per slot (a power of two, G * mtot <= T, G <= 64: one wave's lanes), each counting a
     // contiguous share of the others, summed by lane swaps
-    int G = 1;
-    while (G < 64 && 2 * G * mtot <= T) G *= 2;
+    int G = 1, lgG = 0;
+    while (G < 64 && 2 * G * mtot <= T) {
+      G *= 2;
+      ++lgG;
+    }
     const int per = (mtot + G - 1) / G;
     const int rounds = (mtot * G + T - 1) / T;  // block-uniform
     for (int rd = 0; rd < rounds; ++rd) {
-      const int w = rd * T + tid, u = w / G, g = w % G;
+      const int w = rd * T + tid, u = w >> lgG, g = w & (G - 1);  // G a power of two: no divides
       const int a = slot(u < mtot ? u : 0);
       const double sa = L.cand_d[a];
       const int ra = L.row_s[a];
       const int v0 = g * per, v1 = v0 + per < mtot ? v0 + per : mtot;
-      int rk = 0, v = v0;
-      for (; v + 8 <= v1; v += 8) {  // 8 independent LDS reads in flight per step
+      int rk = 0;
+      for (int v = v0; v < v1; v += 8) {  // 8 independent LDS reads in flight per step (the tail
+                                          // predicated: a serial tail paid one LDS round trip per slot)
         double sb[8];
         int rb[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const int b = slot(v + e);
+          const int b = slot(v + e < v1 ? v + e : v1 - 1);
           sb[e] = L.cand_d[b];
           rb[e] = L.row_s[b];
         }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) rk += (sb[e] > sa) || (sb[e] == sa && rb[e] < ra);
+        for (int e = 0; e < 8; ++e)  // bitwise, not short-circuit: hipcc branched on each && / ||
+          rk += (int)((v + e < v1) & ((sb[e] > sa) | ((sb[e] == sa) & (rb[e] < ra))));
       }
-      for (; v < v1; ++v) {
-        const int b = slot(v);
-        const double sb = L.cand_d[b];
-        rk += (sb > sa) || (sb == sa && L.row_s[b] < ra);
-      }
-      for (int o = 1; o < G; o <<= 1) rk += __shfl_xor(rk, o, 64);
+      // group sum (G consecutive lanes, power of two): DPP xor 1 / 2, then row_half_mirror / row_mirror
+      // (pairing quads / halves whose lanes already agree), LDS swaps only across 16-lane rows
+      if (G > 1) rk += __builtin_amdgcn_update_dpp(0, rk, 0xB1, 0xF, 0xF, false);
+      if (G > 2) rk += __builtin_amdgcn_update_dpp(0, rk, 0x4E, 0xF, 0xF, false);
+      if (G > 4) rk += __builtin_amdgcn_update_dpp(0, rk, 0x141, 0xF, 0xF, false);
+      if (G > 8) rk += __builtin_amdgcn_update_dpp(0, rk, 0x140, 0xF, 0xF, false);
+      for (int o = 16; o < G; o <<= 1) rk += __shfl_xor(rk, o, 64);
       if (u < mtot && g == 0) L.rank_s[a] = rk;
     }
+    SEL_MARK(15)
     __syncthreads();
+    SEL_MARK(16)
     for (int u = tid; u < mtot; u += T) {
       const int sl = slot(u);
       const int rk = L.rank_s[sl];
@@ -1761,6 +1792,7 @@ __global__ __launch_bounds__(T) void knn_select_t(
     }
     __syncthreads();
     int nb = (int)L.bcast[3];
+    SEL_MARK(17)
     SEL_VAL(10, nb)
     __syncthreads();
     if (tid == 0) L.bcast[3] = 0;
@@ -1800,6 +1832,7 @@ __global__ __launch_bounds__(T) void knn_select_t(
       }
       __syncthreads();
       cnt = (int)L.bcast[2];
+      SEL_MARK(18)
       __syncthreads();
       if (tid == 0) L.bcast[2] = 0;
       __syncthreads();

@@ -37,13 +37,15 @@ int main(int argc, char** argv) {
       return 1;
     }
     hipDeviceSynchronize();
-    long long t[16];
+    long long t[24];
     hipMemset(0, 0, 0);
     hipMemcpyFromSymbol(t, HIP_SYMBOL(g_sel_trace), sizeof(t));
     if (it < 2) continue;
     printf("n=%lld Q=%d mode=%d run %d: groups collected %lld, total %.2f us |", (long long)n, Q, mode, it, t[6], (t[5] - t[0]) * 0.01);
     for (int p = 0; p < 5; ++p) printf(" %s %.2f |", names[p], (t[p + 1] - t[p]) * 0.01);
     printf(" [E: fill %.2f, loads+math (block 0, wave 0) %.2f]", (t[8] - t[3]) * 0.01, (t[9] - t[8]) * 0.01);
+    printf(" [C: blocks %.2f, units %.2f, tail %.2f]", (t[17] - t[2]) * 0.01, (t[18] - t[17]) * 0.01, (t[3] - t[18]) * 0.01);
+    printf(" [F: count %.2f, barrier %.2f, write %.2f]", (t[15] - t[4]) * 0.01, (t[16] - t[15]) * 0.01, (t[5] - t[16]) * 0.01);
     printf(" [coarse: blocks %lld, units %lld, final %lld, take_all %lld, thr %g]", t[10], t[11], t[12], t[13], __builtin_bit_cast(float, (int)t[14]));
     printf("\n");
   }
