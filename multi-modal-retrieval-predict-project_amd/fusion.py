@@ -335,7 +335,10 @@ class FusionStack:
 
     def _forward_x3(self, img_global, img_patches, txt_feats):
         """Phase 1 of forward in the fp32-faithful mode: f32 token rows, every GEMM and attention on
-        bf16x3 (ops.x3_linear / ops.x3_attention), one stream (a parity mode, not a throughput one)."""
+        bf16x3 (ops.x3_linear / ops.x3_attention).  As in the bf16 path, the patch-side work of every
+        layer (enhancer, folded k/v/q + patch projections) runs on a side stream ahead of the text
+        side, which waits per layer on an event before the cross attentions: the same kernels on the
+        same operands, so the results are those of one stream (side_streams = False)."""
         B, Np, Ci = img_patches.shape
         D, h, eps, dev = self.D, self.heads, self.eps, self.device
         nl = len(self.layers)
@@ -346,12 +349,31 @@ class FusionStack:
         m1 = torch.empty((nl, B, D), dtype=torch.float32, device=dev)
         m2 = torch.empty((nl, B, D), dtype=torch.float32, device=dev)
         PF = torch.empty((nl, B * Np, D), dtype=torch.float32, device=dev)
-        cls = None
+        two = getattr(self, "_warm", False) and self.side_streams
+        self._warm = True
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream(main) if two else main
+        pq, pp, ev = [], [], []
+        if two:
+            side.wait_stream(main)
+        with torch.cuda.stream(side):
+            for L in self.layers:
+                _, Pes = L["patch"].x3(P, B, Np, eps, keep_f32=False)        # (B*Np, Ci), split rows
+                PQPP = ops.x3_linear(Pes, L["ppp_x3"], L["ppp_b"])         # k_t2i | v_t2i | q_i2t | img_patch_proj
+                PQPP = PQPP.reshape(B * Np, -1)
+                pq.append(PQPP[:, :3 * D])
+                pp.append(PQPP[:, 3 * D:].contiguous())
+                if two:
+                    e = torch.cuda.Event()
+                    e.record(side)
+                    ev.append(e)
+        if two:
+            P.record_stream(side)
+            for t in pq + pp:
+                t.record_stream(main)
+        cls = torch.empty((nl, B, self.layers[0]["txt"].C), dtype=torch.float32, device=dev)
         for i, L in enumerate(self.layers):
-            _, Pes = L["patch"].x3(P, B, Np, eps, keep_f32=False)            # (B*Np, Ci), split rows
-            PQPP = ops.x3_linear(Pes, L["ppp_x3"], L["ppp_b"])             # k_t2i | v_t2i | q_i2t | img_patch_proj
-            PQPP = PQPP.reshape(B * Np, -1)
-            PQ, PP = PQPP[:, :3 * D], PQPP[:, 3 * D:].contiguous()
+            PQ, PP = pq[i], pp[i]
             if txt_feats is None:  # learnable default text token (fusion.py:404-407)
                 T, Lt = L["default_txt32"].expand(B, -1).contiguous(), 1
             else:
@@ -359,14 +381,15 @@ class FusionStack:
                 T = txt_feats.float().contiguous().view(B * Lt, -1)
             Te, Tes = L["txt"].x3(T, B, Lt, eps)                             # (B*Lt, Ct) f32 + split rows
             Ct = Te.shape[1]
-            if cls is None:
-                cls = torch.empty((nl, B, Ct), dtype=torch.float32, device=dev)
             ops.x3_gather_rows(Te, B, Ct, Lt * Ct, out=cls[i])              # CLS rows (fusion.py:447)
             TQ = ops.x3_linear(Tes, L["t_x3"], L["t_b"]).reshape(B * Lt, -1)  # q_t2i | k_i2t | v_i2t
+            if two:
+                main.wait_event(ev[i])
             ops.x3_attention(TQ[:, :D], PQ[:, :D], PQ[:, D:2 * D], B, Lt, Np, h, dh, sc, mean_out=m1[i])
             a2 = ops.x3_attention_split(PQ[:, 2 * D:], TQ[:, D:2 * D], TQ[:, 2 * D:], B, Np, Lt, h, dh, sc,
                                         mean_out=m2[i])
             ops.x3_linear(a2, L["o2_x3t"], L["o2_b"], residual=PP, out=PF[i])  # patches_fused (fusion.py:437)
+        del pq, pp
         return self._finish(G, m1, m2, cls, PF, B, Np, Ci)
 
     def _finish(self, G, m1, m2, cls, PF, B, Np, Ci):

@@ -206,6 +206,30 @@ def test_fusion_stack_vs_oracle_on_backbone_features(text):
     _check_emb(got, ref)
 
 
+@pytest.mark.parametrize("tower_dtype", ["bf16", "fp8", "x3"])
+def test_fusion_stack_side_stream_bitwise(tower_dtype):
+    """The patch-side layer work on a side stream (FusionStack.side_streams; bf16, MX-fp8 and x3
+    paths) runs the same kernels on the same operands as one stream: bitwise-equal joint embeddings
+    (first call in sequence, then with and without the side stream), at B = 256 where the patch
+    GEMMs take the 8-phase route."""
+    g = torch.Generator().manual_seed(17)
+    B, Lt, Np, C, D = 256, 128, 49, 768, 768
+    hs = init_head_state(C, C, D, 27)
+    hs.update(init_fusion_state(C, C, D, 8, 5, 28))
+    G = torch.randn(B, C, generator=g).to(DEV)
+    P = torch.randn(B, Np, C, generator=g).to(DEV)
+    T = bf(torch.randn(B, Lt, C, generator=g)).float().to(DEV)
+    from mmr_amd.fusion import FusionStack
+    fs = FusionStack(hs, 8, device=DEV, tower_dtype=tower_dtype)
+    first = fs.forward(G, P, T).clone()      # warm call: one stream
+    fs.side_streams = True
+    two = fs.forward(G, P, T).clone()
+    fs.side_streams = False
+    one = fs.forward(G, P, T).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(two, one) and torch.equal(first, one)
+
+
 def test_fusion_stack_exact_query_linears():
     """exact_query_linears=True routes the per-query linears (global enhancer, out-projections, the
     joint chain) to exact f32 (mmr_linear_f32*): both routes match the oracle; they differ from each
