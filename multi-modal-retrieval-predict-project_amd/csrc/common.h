@@ -133,10 +133,33 @@ __device__ __forceinline__ f32x2_t gelu_fast2(f32x2_t v) {
   return v * r;
 }
 
+// lane-permuted copy of a 32- or 64-bit value by DPP (64-bit: both halves)
+template <int CTRL, typename T>
+__device__ __forceinline__ T dpp_mov(T v) {
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+  } else {
+    static_assert(sizeof(T) == 8, "dpp_mov: 32- or 64-bit values");
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+    return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
+  }
+}
+// Sum over the wave as the xor butterfly 32, 16, 8, 4, 2, 1 (each lane adds its own and its partner's
+// value: the same tree, so the same bits, at every call site — the kNN norms and f64 re-scores rely on
+// the order).  Levels 32 / 16 are LDS swaps; the in-row levels are DPP: row_ror:8 reads lane i ^ 8;
+// row_ror:4 reads lane (i + 4) mod 16, which after the 8-level holds the same value as lane i ^ 4
+// (the values are symmetric under ^8); quad_perm [2,3,0,1] / [1,0,3,2] are xor 2 / 1.  (Six dependent
+// LDS round trips per call before; the f64 form cost the kNN selection's query norm ~0.3 us.)
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  v += __shfl_xor(v, 32, 64);
+  v += __shfl_xor(v, 16, 64);
+  v += dpp_mov<0x128>(v);
+  v += dpp_mov<0x124>(v);
+  v += dpp_mov<0x4E>(v);
+  v += dpp_mov<0xB1>(v);
   return v;
 }
 // wave_sum of RB values at once (a[r] = lane's partial of row r): a reduce-scatter over the same xor
@@ -166,15 +189,28 @@ __device__ __forceinline__ T rows_wave_sum(const T (&a)[RB], int lane, int& row)
     for (int j = 0; j < h; ++j) v[j] = (up ? v[h + j] : v[j]) + sent[j];
     row += up ? h : 0;
   }
-#pragma unroll
-  for (int m = 32 >> LOG; m > 0; m >>= 1) v[0] += __shfl_xor(v[0], m, 64);
+  // the remaining butterfly levels as in wave_sum (row_ror:4 only when the 8-level was a butterfly
+  // level: after a reduce-scatter 8-level, lanes i and i ^ 8 hold different rows)
+  if constexpr (LOG == 0) v[0] += __shfl_xor(v[0], 32, 64);
+  if constexpr (LOG <= 1) v[0] += __shfl_xor(v[0], 16, 64);
+  if constexpr (LOG <= 2) {
+    v[0] += dpp_mov<0x128>(v[0]);
+    v[0] += dpp_mov<0x124>(v[0]);
+  } else {
+    v[0] += __shfl_xor(v[0], 4, 64);
+  }
+  v[0] += dpp_mov<0x4E>(v[0]);
+  v[0] += dpp_mov<0xB1>(v[0]);
   return v[0];
 }
 template <typename T>
-__device__ __forceinline__ T wave_max(T v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+__device__ __forceinline__ T wave_max(T v) {  // max is order-free: the wave_sum lane pattern
+  v = fmaxf(v, __shfl_xor(v, 32, 64));
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  v = fmaxf(v, dpp_mov<0x128>(v));
+  v = fmaxf(v, dpp_mov<0x124>(v));
+  v = fmaxf(v, dpp_mov<0x4E>(v));
+  return fmaxf(v, dpp_mov<0xB1>(v));
 }
 
 // MX-fp8 activation operand of an 8-value chunk (channels 8*ch .. 8*ch+7 of a row), written by the

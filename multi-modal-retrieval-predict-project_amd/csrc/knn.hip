@@ -668,14 +668,25 @@ __global__ __launch_bounds__(64 * NWV) void knn_scan_f16_lq(const float* __restr
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int KP = Dp / 32;
-  if (blockIdx.x == 0) {
+  {
     // |q| (f64, the select's canonical order: lane sums elements lane + 64c, c < 16, then the xor
-    // tree — bit-identical to knn_select_t's own query_norm) and max |q_k| per query, for the select
-    for (int row = wave; row < nq; row += NWV) {
+    // tree — bit-identical to knn_select_t's own query_norm) and max |q_k| per query, for the select:
+    // row r by the LAST wave of workgroup r, which takes a gallery block only when its workgroup has
+    // more than NWV - 1 of them (100k rows: 6-7 per workgroup) — workgroup 0's waves computing every
+    // row first delayed its blocks, the scan's tail
+    for (int row = blockIdx.x; wave == NWV - 1 && row < nq; row += gridDim.x) {
       double ss = 0.0;
       float am = 0.f;
-      for (int e = lane; e < 1024; e += 64) {
-        const float x = e < d ? qraw[(int64_t)row * d + e] : 0.f;
+      float xv[16];  // every load issued before any use (clamped index, masked value: a "load if in
+                     // range" compiles into a branch and a wait per load)
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const int e = lane + 64 * c;
+        xv[c] = qraw[(int64_t)row * d + (e < d ? e : d - 1)];
+      }
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const float x = lane + 64 * c < d ? xv[c] : 0.f;
         ss += (double)x * (double)x;
         am = fmaxf(am, fabsf(x));
       }
