@@ -245,9 +245,67 @@ class FusionStack:
             self._side = collections.OrderedDict()
         return ops.side_stream(self._side, main, self.device)
 
-    def forward(self, img_global, img_patches, txt_feats):
+    def patch_work(self, img_patches):
+        """The patch-side token work of every layer (enhancer, folded k/v/q projection, patch
+        projection) on the CURRENT stream, an event recorded after each layer: it depends on the
+        image tower only, so a caller may start it as soon as that tower is done (the towers' side
+        stream: MultiModalRetrievalModel.query_embeddings) and hand it to forward(patch_work=...).
+        Returns {"pq": [...], "pp": [...], "ev": [...], "stream": the stream it ran on}."""
+        B, Np, Ci = img_patches.shape
+        D, eps = self.D, self.eps
+        pq, pp, ev = [], [], []
+        cur = torch.cuda.current_stream(self.device)
+        if self.x3:
+            P = img_patches.float().contiguous().view(B * Np, Ci)
+        else:
+            P = img_patches.contiguous().view(B * Np, Ci)
+        for L in self.layers:
+            if self.x3:
+                _, Pes = L["patch"].x3(P, B, Np, eps, keep_f32=False)        # (B*Np, Ci), split rows
+                PQPP = ops.x3_linear(Pes, L["ppp_x3"], L["ppp_b"])         # k_t2i | v_t2i | q_i2t | img_patch_proj
+                PQPP = PQPP.reshape(B * Np, -1)
+                pq.append(PQPP[:, :3 * D])
+                pp.append(PQPP[:, 3 * D:].contiguous())
+            elif L["patch"].fp8_ok(B * Np):  # MX-fp8 (config 5): the LayerNorm emits the operand
+                Pe, Pe8 = L["patch"](P, B, Np, eps, q8=True)
+                pq.append(ops.linear_mxfp8(Pe8, L["p_w8"], L["p_b"]))
+                pp.append(ops.linear_mxfp8(Pe8, L["pp_w8"], L["pp_b"]))
+            else:
+                Pe = L["patch"](P, B, Np, eps)                             # (B*Np, Ci) bf16
+                pq.append(ops.linear(Pe, L["p_w"], L["p_b"]))              # (B*Np, 3D): k_t2i | v_t2i | q_i2t
+                pp.append(ops.linear(Pe, L["pp_w"], L["pp_b"]))            # img_patch_proj
+            e = torch.cuda.Event()
+            e.record(cur)
+            ev.append(e)
+        return {"pq": pq, "pp": pp, "ev": ev, "stream": cur}
+
+    def _patch_side(self, img_patches, patch_work):
+        """(pq, pp, ev, two) for forward: the caller's early patch work, or the patch work run here on
+        a side stream (side_streams, after the first call) or in line."""
+        main = torch.cuda.current_stream(self.device)
+        if patch_work is not None:
+            if patch_work["stream"] != main:
+                for t in patch_work["pq"] + patch_work["pp"]:
+                    t.record_stream(main)
+            return patch_work["pq"], patch_work["pp"], patch_work["ev"], True
+        two = getattr(self, "_warm", False) and self.side_streams
+        self._warm = True
+        if not two:
+            w = self.patch_work(img_patches)
+            return w["pq"], w["pp"], w["ev"], False
+        side = self._side_stream(main)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            w = self.patch_work(img_patches)
+        img_patches.record_stream(side)
+        for t in w["pq"] + w["pp"]:
+            t.record_stream(main)
+        return w["pq"], w["pp"], w["ev"], True
+
+    def forward(self, img_global, img_patches, txt_feats, patch_work=None):
         """img_global (B, Ci) f32, img_patches (B, Np, Ci) f32, txt_feats (B, L, Ct) bf16/f32 or None
-        -> joint_emb (B, D) f32.
+        -> joint_emb (B, D) f32.  patch_work: this batch's patch_work(img_patches), started early by the
+        caller (else it runs here).
 
         Phase 1 (per layer, token level): enhancers, folded cross projections, the two cross
         attentions (means only where only means are used), patches_fused.
@@ -257,48 +315,23 @@ class FusionStack:
         nl*B*(Np+2) rows, its attention means and out-projection.
         Phase 4 (sequential): the joint chain (norm1 / alpha, norm2 -> FFN, adapter)."""
         if self.x3:
-            return self._forward_x3(img_global, img_patches, txt_feats)
+            return self._forward_x3(img_global, img_patches, txt_feats, patch_work)
         B, Np, Ci = img_patches.shape
         D, h, eps, dev = self.D, self.heads, self.eps, self.device
         nl = len(self.layers)
         dh = D // h
         sc = 1.0 / math.sqrt(dh)
         G = img_global.float().contiguous()
-        P = img_patches.contiguous().view(B * Np, Ci)
         m1 = torch.empty((nl, B, D), dtype=torch.float32, device=dev)
         m2 = torch.empty((nl, B, D), dtype=torch.float32, device=dev)
         PF = torch.empty((nl, B * Np, D), dtype=torch.bfloat16, device=dev)
         cls = None
-        # the patch-side token work of every layer (enhancer, folded k/v/q projection, patch
-        # projection) depends only on the image tower: it runs on a side stream, ahead of and
-        # concurrently with the text-side work, which waits per layer on an event before the
-        # cross attentions (side_streams = False: one stream)
-        # (first call in sequence: see MultiModalRetrievalModel._towers)
-        two = getattr(self, "_warm", False) and self.side_streams
-        self._warm = True
+        # the patch-side token work of every layer depends only on the image tower: it runs on a side
+        # stream (or the caller's early patch_work), ahead of and concurrently with the text-side work,
+        # which waits per layer on an event before the cross attentions (side_streams = False: one
+        # stream; first call in sequence: see MultiModalRetrievalModel._towers)
         main = torch.cuda.current_stream(dev)
-        side = self._side_stream(main) if two else main
-        pq, pp, ev = [], [], []
-        if two:
-            side.wait_stream(main)
-        with torch.cuda.stream(side):
-            for L in self.layers:
-                if L["patch"].fp8_ok(B * Np):  # MX-fp8 (config 5): the LayerNorm emits the operand
-                    Pe, Pe8 = L["patch"](P, B, Np, eps, q8=True)
-                    pq.append(ops.linear_mxfp8(Pe8, L["p_w8"], L["p_b"]))
-                    pp.append(ops.linear_mxfp8(Pe8, L["pp_w8"], L["pp_b"]))
-                else:
-                    Pe = L["patch"](P, B, Np, eps)                         # (B*Np, Ci) bf16
-                    pq.append(ops.linear(Pe, L["p_w"], L["p_b"]))          # (B*Np, 3D): k_t2i | v_t2i | q_i2t
-                    pp.append(ops.linear(Pe, L["pp_w"], L["pp_b"]))        # img_patch_proj
-                if two:
-                    e = torch.cuda.Event()
-                    e.record(side)
-                    ev.append(e)
-        if two:
-            P.record_stream(side)
-            for t in pq + pp:
-                t.record_stream(main)
+        pq, pp, ev, two = self._patch_side(img_patches, patch_work)
         for i, L in enumerate(self.layers):
             if txt_feats is None:  # learnable default text token (fusion.py:404-407)
                 T, Lt = L["default_txt"].expand(B, -1).contiguous(), 1
@@ -333,44 +366,23 @@ class FusionStack:
         del pq, pp
         return self._finish(G, m1, m2, cls, PF, B, Np, Ci)
 
-    def _forward_x3(self, img_global, img_patches, txt_feats):
+    def _forward_x3(self, img_global, img_patches, txt_feats, patch_work=None):
         """Phase 1 of forward in the fp32-faithful mode: f32 token rows, every GEMM and attention on
         bf16x3 (ops.x3_linear / ops.x3_attention).  As in the bf16 path, the patch-side work of every
-        layer (enhancer, folded k/v/q + patch projections) runs on a side stream ahead of the text
-        side, which waits per layer on an event before the cross attentions: the same kernels on the
-        same operands, so the results are those of one stream (side_streams = False)."""
+        layer (enhancer, folded k/v/q + patch projections) runs on a side stream (or early, by the
+        caller) ahead of the text side, which waits per layer on an event before the cross attentions:
+        the same kernels on the same operands, so the results are those of one stream."""
         B, Np, Ci = img_patches.shape
         D, h, eps, dev = self.D, self.heads, self.eps, self.device
         nl = len(self.layers)
         dh = D // h
         sc = 1.0 / math.sqrt(dh)
         G = img_global.float().contiguous()
-        P = img_patches.float().contiguous().view(B * Np, Ci)
         m1 = torch.empty((nl, B, D), dtype=torch.float32, device=dev)
         m2 = torch.empty((nl, B, D), dtype=torch.float32, device=dev)
         PF = torch.empty((nl, B * Np, D), dtype=torch.float32, device=dev)
-        two = getattr(self, "_warm", False) and self.side_streams
-        self._warm = True
         main = torch.cuda.current_stream(dev)
-        side = self._side_stream(main) if two else main
-        pq, pp, ev = [], [], []
-        if two:
-            side.wait_stream(main)
-        with torch.cuda.stream(side):
-            for L in self.layers:
-                _, Pes = L["patch"].x3(P, B, Np, eps, keep_f32=False)        # (B*Np, Ci), split rows
-                PQPP = ops.x3_linear(Pes, L["ppp_x3"], L["ppp_b"])         # k_t2i | v_t2i | q_i2t | img_patch_proj
-                PQPP = PQPP.reshape(B * Np, -1)
-                pq.append(PQPP[:, :3 * D])
-                pp.append(PQPP[:, 3 * D:].contiguous())
-                if two:
-                    e = torch.cuda.Event()
-                    e.record(side)
-                    ev.append(e)
-        if two:
-            P.record_stream(side)
-            for t in pq + pp:
-                t.record_stream(main)
+        pq, pp, ev, two = self._patch_side(img_patches, patch_work)
         cls = torch.empty((nl, B, self.layers[0]["txt"].C), dtype=torch.float32, device=dev)
         for i, L in enumerate(self.layers):
             PQ, PP = pq[i], pp[i]

@@ -363,22 +363,26 @@ class MultiModalRetrievalModel:
         if not mm and input_ids is None:
             _, _, pool = self.backbones.encode_image(image, want_patches=False)
             return self._head(pool, self.img_proj)
-        (g, p, pool), txt = self._towers(image, input_ids, attention_mask, mm)
+        # multimodal: the fusion stack's patch-side work (image tower only) starts on the towers'
+        # side stream as soon as the Swin tower is done, beside the BERT tower's tail
+        early = (lambda img: self.fusion.patch_work(img[1])) if mm and self.fusion.side_streams else None
+        (g, p, pool), txt, pw = self._towers(image, input_ids, attention_mask, mm, after_image=early)
         if mm:
-            return self.fusion.forward(g, p, txt)
+            return self.fusion.forward(g, p, txt, patch_work=pw)
         return torch.cat([self._head(pool, self.img_proj), self._head(self._txt_pool(txt), self.txt_proj)], 0)
 
-    def _towers(self, image, input_ids, attention_mask, want_patches):
+    def _towers(self, image, input_ids, attention_mask, want_patches, after_image=None):
         """Both towers, the Swin tower on a side stream so its kernels fill the CUs the BERT
         kernels leave idle (wave-quantisation tails, small LayerNorm / attention launches); the
         two towers share no data until the heads.  The first call runs them in sequence: the GEMM
         launcher times its variants per shape on first use, which concurrent kernels would skew.
-        concurrent_towers = False always runs them in sequence."""
+        concurrent_towers = False always runs them in sequence.  after_image(img) runs on the side
+        stream right after the image tower (its result is returned third; None in sequence)."""
         first = not self._warm
         self._warm = True
         if first or not self.concurrent_towers:
             return (self.backbones.encode_image(image, want_patches=want_patches),
-                    self.backbones.encode_text(input_ids, attention_mask))
+                    self.backbones.encode_text(input_ids, attention_mask), None)
         main = torch.cuda.current_stream(self.device)
         # one side stream per calling stream: callers that pipeline batches over several streams
         # (bench.py --pipeline) keep their batches independent
@@ -388,13 +392,16 @@ class MultiModalRetrievalModel:
         side.wait_stream(main)                        # the image batch is ready
         with torch.cuda.stream(side):
             img = self.backbones.encode_image(image, want_patches=want_patches)
+            img_done = torch.cuda.Event()
+            img_done.record(side)
+            extra = after_image(img) if after_image is not None else None  # carries its own events
         image.record_stream(side)                     # caching allocator: in use on the side stream
         txt = self.backbones.encode_text(input_ids, attention_mask)
-        main.wait_stream(side)
+        main.wait_event(img_done)                     # the image tower, not the early work after it
         for t in img:
             if t is not None:
                 t.record_stream(main)
-        return img, txt
+        return img, txt, extra
 
 
 def init_head_state(img_dim, txt_dim, joint_dim, seed=2711):

@@ -230,6 +230,25 @@ def test_fusion_stack_side_stream_bitwise(tower_dtype):
     assert torch.equal(two, one) and torch.equal(first, one)
 
 
+@pytest.mark.parametrize("tower_dtype", ["bf16", "x3"])
+def test_model_early_patch_work_bitwise(tower_dtype):
+    """MultiModalRetrievalModel.query_embeddings with the towers concurrent and the fusion stack's
+    patch-side work started on the towers' side stream right after the image tower (patch_work):
+    bitwise-equal joint embeddings to the first (in-sequence) call and to a call with the towers in
+    sequence (B = 64)."""
+    from mmr_amd.model import build_bench_model
+    B = 64
+    img = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(B, 81))).to(DEV)
+    ids, mask = (torch.from_numpy(a).to(DEV) for a in synthetic.reports(B, 128, 82))
+    m = build_bench_model(device=DEV, joint_dim=768, model_type="multimodal", tower_dtype=tower_dtype)
+    first = m.query_embeddings(img, ids, mask).clone()
+    early = m.query_embeddings(img, ids, mask).clone()
+    m.concurrent_towers = False
+    seq = m.query_embeddings(img, ids, mask).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(early, seq) and torch.equal(first, seq)
+
+
 def test_fusion_stack_exact_query_linears():
     """exact_query_linears=True routes the per-query linears (global enhancer, out-projections, the
     joint chain) to exact f32 (mmr_linear_f32*): both routes match the oracle; they differ from each
