@@ -583,6 +583,15 @@ mmr_status mmr_x3_rowlin(const float* x, const uint16_t* xs, const float* ln_g, 
 mmr_status mmr_x3_swin_mlp_pack(const float* w1, const float* w2, uint16_t* pack, int32_t c, void* stream);
 mmr_status mmr_x3_swin_mlp(const float* x, const float* ln_g, const float* ln_b, const uint16_t* pack, const float* b1,
                            const float* b2, float* y, int64_t tokens, int32_t c, float eps, void* stream);
+/* fp32-faithful Swin stem (csrc/x3_mlp.hip): y (b, hw/4, hw/4, 96) f32 = LayerNorm(Conv2d(3, 96, 4, stride 4)
+ * (img) + bias) (timm PatchEmbed with its norm) for img (b, 3, hw, hw) f32 NCHW, the conv on bf16x3 MFMA, one
+ * pass (no im2col rows).  hw % 4 == 0, (hw/4)^2 % 32 == 0, 16-B aligned pointers.  pack:
+ * mmr_x3_patch_embed_pack_elems() bf16 elements built once from the f32 conv weight [96][3*4*4] by
+ * mmr_x3_patch_embed_pack. */
+int64_t mmr_x3_patch_embed_pack_elems(void);
+mmr_status mmr_x3_patch_embed_pack(const float* w, uint16_t* pack, void* stream);
+mmr_status mmr_x3_patch_embed_ln(const float* img, int32_t b, int32_t hw, const uint16_t* pack, const float* bias,
+                                 const float* ln_g, const float* ln_b, float eps, float* y, void* stream);
 /* y (b, c) = (extra[b] + sum_t x[b][t]) / (l + 1) with extra (b, c), or sum_t x[b][t] / l when extra is
  * NULL; x (b, l, c) f32, summed in token order (unmasked token mean, model.py:370; the Swin global /
  * pooled means, fusion.py:263-265, model.py:463-468). */

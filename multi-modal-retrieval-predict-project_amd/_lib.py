@@ -120,13 +120,17 @@ SIGNATURES = {
     "mmr_x3_assemble_seq_split": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
     "mmr_x3_mean_rows": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
     "mmr_x3_gather_rows": [c_vp, c_i64, c_vp, c_i32, c_i32, c_vp],
+    "mmr_x3_patch_embed_pack_elems": [],
+    "mmr_x3_patch_embed_pack": [c_vp, c_vp, c_vp],
+    "mmr_x3_patch_embed_ln": [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp],
 }
 _RESTYPES = {"mmr_last_error": ctypes.c_char_p, "mmr_version": ctypes.c_int, "mmr_max_k": ctypes.c_int,
              "mmr_linear_bf16_variant": ctypes.c_int32, "mmr_linear_bf16_n_variants": ctypes.c_int32,
              "mmr_linear_bf16_ln_parts": ctypes.c_int32,
              "mmr_linear_rw_parts": ctypes.c_int32,
              "mmr_swin_mlp_pack_elems": ctypes.c_int64, "mmr_swin_attn_block_pack_bytes": ctypes.c_int64,
-             "mmr_x3_swin_mlp_pack_elems": ctypes.c_int64, "mmr_x3_rowlin_pack_elems": ctypes.c_int64}
+             "mmr_x3_swin_mlp_pack_elems": ctypes.c_int64, "mmr_x3_rowlin_pack_elems": ctypes.c_int64,
+             "mmr_x3_patch_embed_pack_elems": ctypes.c_int64}
 
 _lib = None
 

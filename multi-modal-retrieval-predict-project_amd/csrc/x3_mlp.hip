@@ -432,6 +432,118 @@ mmr_status launch_rowlin(const float* x, const uint16_t* xs, int kp, const float
   return MMR_OK;
 }
 
+// ------------------------------------------------------------------ x3 patch embed (the Swin stem)
+// y = LayerNorm(conv4x4/s4(img) + b) for timm's PatchEmbed (Conv2d(3, 96, 4, 4) + LayerNorm(96), reached
+// through fusion.py:198-199) in f32, the conv on bf16x3 MFMA, in one pass: the unfused x3 stem wrote the
+// im2col rows (4 B x 64 per token), re-read them in a 128 x 128-tile GEMM with N = 96 (25 % of each tile
+// idle, column stores) and ran the LayerNorm as a third pass (56 + 228 + 128 us at B = 256).  Each wave
+// owns 32 tokens (the N side of v_mfma_f32_32x32x16_bf16, C^T orientation): for k-step s (= input
+// channel s, k = 16 s + 4 ky + kx, PyTorch's flattened conv weight order) lane (token r, half h) loads
+// the two 16-B pixel rows ky = 2h, 2h + 1 of its patch — exactly its 8 B-operand k values — and splits
+// them into hi / lo fragments; A = the weight image in fragment order (LDS, 18 KB, [hi | lo]); bias in
+// the accumulators; the LayerNorm over the 96 outputs a lane pair holds (two-pass, f32), 16-B stores.
+constexpr int PE_E = 96, PE_K = 48;
+constexpr int PE_IMG_E = 3 * 3 * 64 * 8;  // bf16 per image: (3 output tiles x 3 k-steps) fragments
+
+__global__ __launch_bounds__(256) void x3_patch_embed_pack(const float* __restrict__ w, uint16_t* __restrict__ pack) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= PE_IMG_E) return;
+  const int j = i & 7, l = (i >> 3) & 63, f = i >> 9, u = f / 3, s = f % 3;
+  const float v = w[(32 * u + (l & 31)) * PE_K + 16 * s + 8 * (l >> 5) + j];
+  const uint16_t hi = mmr::f2bf(v);
+  pack[i] = hi;
+  pack[PE_IMG_E + i] = mmr::f2bf(v - mmr::bf2f(hi));
+}
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void x3_patch_embed_ln(const float* __restrict__ img,
+                                                             const uint16_t* __restrict__ pack,
+                                                             const float* __restrict__ bias,
+                                                             const float* __restrict__ lng,
+                                                             const float* __restrict__ lnb, float* __restrict__ y,
+                                                             int64_t ntile, int hw, float eps) {
+  __shared__ __attribute__((aligned(16))) uint16_t W[2 * PE_IMG_E];
+  __shared__ __attribute__((aligned(16))) float Pp[3 * PE_E];  // bias | gamma | beta
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  for (int i = threadIdx.x; i < 2 * PE_IMG_E / 8; i += 64 * NW) ((uint4*)W)[i] = ((const uint4*)pack)[i];
+  for (int i = threadIdx.x; i < 3 * PE_E; i += 64 * NW)
+    Pp[i] = i < PE_E ? bias[i] : (i < 2 * PE_E ? lng[i - PE_E] : lnb[i - 2 * PE_E]);
+  __syncthreads();
+  const int g = hw / 4, per_img = g * g;
+  for (int64_t tile = (int64_t)blockIdx.x * NW + wave; tile < ntile; tile += (int64_t)gridDim.x * NW) {
+    const int64_t tok = tile * 32 + r;
+    const int64_t b = tok / per_img;
+    const int p = (int)(tok - b * per_img), py = p / g, px = p - py * g;
+    const float* base = img + ((b * 3) * hw + 4 * py + 2 * h) * (int64_t)hw + 4 * px;
+    f32x4 xv[3][2];
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) xv[s][j] = *(const f32x4*)(base + ((int64_t)s * hw + j) * hw);
+    bf16x8 xh[3], xl[3];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      uint32_t hh[4], ll[4];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        split2(xv[s][j][0], xv[s][j][1], hh[2 * j], ll[2 * j]);
+        split2(xv[s][j][2], xv[s][j][3], hh[2 * j + 1], ll[2 * j + 1]);
+      }
+      xh[s] = __builtin_bit_cast(bf16x8, make_uint4(hh[0], hh[1], hh[2], hh[3]));
+      xl[s] = __builtin_bit_cast(bf16x8, make_uint4(ll[0], ll[1], ll[2], ll[3]));
+    }
+    f32x16 acc[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 bb = *(const f32x4*)(Pp + 32 * u + 8 * i + 4 * h);
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) acc[u][4 * i + rr] = bb[rr];
+      }
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const bf16x8 wh = *(const bf16x8*)(W + ((u * 3 + s) * 64 + lane) * 8);
+        const bf16x8 wl = *(const bf16x8*)(W + PE_IMG_E + ((u * 3 + s) * 64 + lane) * 8);
+        acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xh[s], acc[u], 0, 0, 0);
+        acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xl[s], acc[u], 0, 0, 0);
+        acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, xh[s], acc[u], 0, 0, 0);
+      }
+    }
+    // LayerNorm over the token's 96 outputs (lane half h holds 48 of them: channels 32 u + 8 i + 4 h + rr)
+    float sm = 0.f;
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) sm += acc[u][e];
+    sm += __shfl_xor(sm, 32, 64);
+    const float mean = sm * (1.0f / PE_E);
+    float ss = 0.f;
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const float d = acc[u][e] - mean;
+        ss += d * d;
+      }
+    ss += __shfl_xor(ss, 32, 64);
+    const float rstd = rsqrtf(ss * (1.0f / PE_E) + eps);
+    float* yr = y + tok * PE_E;
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = 32 * u + 8 * i + 4 * h;
+        const f32x4 g4 = *(const f32x4*)(Pp + PE_E + c), b4 = *(const f32x4*)(Pp + 2 * PE_E + c);
+        f32x4 v;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) v[rr] = (acc[u][4 * i + rr] - mean) * rstd * g4[rr] + b4[rr];
+        *(f32x4*)(yr + c) = v;
+      }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -508,6 +620,33 @@ mmr_status mmr_x3_rowlin(const float* x, const uint16_t* xs, const float* ln_g, 
                          : launch_rowlin<192, true, false>(x, xs, kp, ln_g, ln_b, pack, bias, residual, y, tokens, n, eps, st);
   return residual ? launch_rowlin<192, false, true>(x, xs, kp, ln_g, ln_b, pack, bias, residual, y, tokens, n, eps, st)
                   : launch_rowlin<192, false, false>(x, xs, kp, ln_g, ln_b, pack, bias, residual, y, tokens, n, eps, st);
+}
+
+int64_t mmr_x3_patch_embed_pack_elems(void) { return 2 * PE_IMG_E; }
+
+mmr_status mmr_x3_patch_embed_pack(const float* w, uint16_t* pack, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(w && pack, "mmr_x3_patch_embed_pack: NULL pointer");
+  x3_patch_embed_pack<<<dim3((unsigned)mmr::ceil_div(PE_IMG_E, 256)), 256, 0, mmr::as_stream(stream)>>>(w, pack);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
+}
+
+mmr_status mmr_x3_patch_embed_ln(const float* img, int32_t b, int32_t hw, const uint16_t* pack, const float* bias,
+                                 const float* ln_g, const float* ln_b, float eps, float* y, void* stream) {
+  mmr::clear_error();
+  MMR_REQUIRE(img && pack && bias && ln_g && ln_b && y, "mmr_x3_patch_embed_ln: NULL pointer");
+  MMR_REQUIRE(b >= 0 && hw > 0 && hw % 4 == 0 && ((hw / 4) * (hw / 4)) % 32 == 0,
+              "mmr_x3_patch_embed_ln: b=%d hw=%d (hw %% 4 == 0, (hw/4)^2 %% 32 == 0)", b, hw);
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  MMR_REQUIRE(al(img) && al(y) && al(bias) && al(ln_g) && al(ln_b) && al(pack), "mmr_x3_patch_embed_ln: 16-B aligned pointers");
+  if (b == 0) return MMR_OK;
+  const int64_t ntile = (int64_t)b * (hw / 4) * (hw / 4) / 32;
+  const int64_t grid = std::min<int64_t>(2048, mmr::ceil_div(ntile, 4));
+  x3_patch_embed_ln<4><<<dim3((unsigned)grid), 256, 0, mmr::as_stream(stream)>>>(img, pack, bias, ln_g, ln_b, y, ntile,
+                                                                              hw, eps);
+  MMR_LAUNCH_CHECK();
+  return MMR_OK;
 }
 
 }  // extern "C"

@@ -873,6 +873,28 @@ def x3_patch_im2col(img, patch=4, kp=64):
     return cols
 
 
+def x3_patch_embed_pack(w):
+    """f32 conv weight (96, 3, 4, 4) or (96, 48) (device) -> the fused x3 stem's weight image, or None when
+    the shape is not Swin-T's stem."""
+    w2 = w.reshape(w.shape[0], -1)
+    if tuple(w2.shape) != (96, 48):
+        return None
+    pack = torch.empty((_L().mmr_x3_patch_embed_pack_elems(),), dtype=torch.bfloat16, device=w.device)
+    _chk(_L().mmr_x3_patch_embed_pack(_lib.ptr(w2.float().contiguous()), _lib.ptr(pack), _s(w)), "mmr_x3_patch_embed_pack")
+    return pack
+
+
+def x3_patch_embed_ln(img, pack, bias, g, b, eps):
+    """(B, 3, H, W) f32 -> (B, H/4, W/4, 96) f32 = LayerNorm(conv4x4/s4(img) + bias) (timm PatchEmbed with its
+    norm), the conv on bf16x3 MFMA, one pass."""
+    _lib.require_gpu(img)
+    B, _, H, _ = img.shape
+    y = torch.empty((B, H // 4, H // 4, 96), dtype=torch.float32, device=img.device)
+    _chk(_L().mmr_x3_patch_embed_ln(_lib.ptr(img), B, H, _lib.ptr(pack), _lib.ptr(bias), _lib.ptr(g), _lib.ptr(b),
+                                    float(eps), _lib.ptr(y), _s(img)), "mmr_x3_patch_embed_ln")
+    return y
+
+
 def x3_patch_merge_ln_split(x, g, b, eps):
     """x3_patch_merge_ln as X3Rows (the reduction linear's split operand) when the merged token count
     fills 256-row tiles, else f32 rows."""

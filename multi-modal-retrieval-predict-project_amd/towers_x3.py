@@ -53,6 +53,9 @@ class SwinTowerX3:
         wp[:, :w.shape[1]] = w
         self.pe_w, self.pe_b = _x3(wp, dev), _f(sd["patch_embed.proj.bias"], dev)
         self.pe_g, self.pe_beta = _f(sd["patch_embed.norm.weight"], dev), _f(sd["patch_embed.norm.bias"], dev)
+        # Swin-T's stem (3 -> 96, 4 x 4 / 4): conv + its LayerNorm in one pass (None: im2col -> GEMM -> LN)
+        self.pe_pack = (ops.x3_patch_embed_pack(_f(w, dev)) if self.cfg["patch"] == 4 and w.shape == (96, 48)
+                        else None)
         self.stages = []
         res = self.cfg["img_size"] // self.cfg["patch"]
         ws0 = self.cfg["window_size"]
@@ -96,9 +99,13 @@ class SwinTowerX3:
         image = image.to(self.device, torch.float32).contiguous()
         B = image.shape[0]
         g = cfg["img_size"] // cfg["patch"]
-        cols = ops.x3_patch_im2col(image, cfg["patch"], self.kp)
-        x = ops.x3_linear(cols, self.pe_w, self.pe_b)                        # conv 4x4/s4 as a GEMM
-        x = _ln(x, self.pe_g, self.pe_beta, 1e-5).view(B, g, g, -1)
+        if self.pe_pack is not None and image.shape[1] == 3 and image.shape[2] == image.shape[3] \
+                and (g * g) % 32 == 0:
+            x = ops.x3_patch_embed_ln(image, self.pe_pack, self.pe_b, self.pe_g, self.pe_beta, 1e-5)
+        else:
+            cols = ops.x3_patch_im2col(image, cfg["patch"], self.kp)
+            x = ops.x3_linear(cols, self.pe_w, self.pe_b)                    # conv 4x4/s4 as a GEMM
+            x = _ln(x, self.pe_g, self.pe_beta, 1e-5).view(B, g, g, -1)
         for i, st in enumerate(self.stages):
             if i > 0:
                 x = ops.x3_linear(ops.x3_patch_merge_ln_split(x, st["ds_g"], st["ds_b"], 1e-5), st["ds_w"])

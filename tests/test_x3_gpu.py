@@ -459,6 +459,32 @@ def test_x3_patch_im2col_exact(B, cin, hw, kp):
     assert torch.equal(cols[..., :cin * 16], ref) and (cols[..., cin * 16:] == 0).all()
 
 
+@pytest.mark.parametrize("B,hw", [(3, 224), (2, 32), (1, 64)])
+def test_x3_patch_embed_ln_vs_f64(B, hw):
+    """The fused x3 Swin stem (conv 4x4/s4, 3 -> 96, + its LayerNorm) vs the f64 conv + LayerNorm, and vs the
+    unfused x3 route (im2col -> x3_linear -> ln_rows); timm-scale inputs (normalised pixels, fan-in init)."""
+    g_ = torch.Generator().manual_seed(hw + B)
+    img = (torch.randn(B, 3, hw, hw, generator=g_) * 1.5).to(DEV)
+    w = (torch.randn(96, 3, 4, 4, generator=g_) * 48 ** -0.5).to(DEV)
+    bias = (torch.randn(96, generator=g_) * 0.1).to(DEV)
+    gm = (1 + 0.2 * torch.randn(96, generator=g_)).to(DEV)
+    bt = (0.1 * torch.randn(96, generator=g_)).to(DEV)
+    pack = ops.x3_patch_embed_pack(w)
+    y = ops.x3_patch_embed_ln(img, pack, bias, gm, bt, 1e-5)
+    ref = torch.nn.functional.conv2d(img.double(), w.double(), bias.double(), stride=4).permute(0, 2, 3, 1)
+    ref = torch.nn.functional.layer_norm(ref, (96,), gm.double(), bt.double(), 1e-5)
+    assert y.shape == (B, hw // 4, hw // 4, 96)
+    assert _rel(y, ref) < 2e-5
+    kp = 64
+    wp = torch.zeros(96, kp, device=DEV)
+    wp[:, :48] = w.reshape(96, 48)
+    cols = ops.x3_patch_im2col(img, 4, kp)
+    un = ops.x3_linear(cols, ops.X3W(wp), bias)
+    un = ops.ln_rows(un.reshape(-1, 96), gm, bt, 1e-5).view(y.shape)
+    assert _rel(y, un) < 2e-5
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("rows,l,c", [(256 * 51, 51, 768), (1000, 7, 6), (4 * 130, 130, 1024)])
 def test_x3_add_pos_exact(rows, l, c):
     g = torch.Generator().manual_seed(rows + c)
