@@ -175,11 +175,14 @@ class BertTowerX3:
             })
         self.hidden = self.word.shape[1]
         self.gemm_events = None  # as BertTower.gemm_events (the bench's per-GEMM roofline pass)
+        # the residual adds in the O-proj / FFN2 epilogues ((acc + b) + h, the LayerNorm kernel's own order)
+        # instead of in the LayerNorm pass, which then reads one f32 row instead of two (A/B attribute)
+        self.res_in_gemm = True
 
-    def _gemm(self, name, x, w, b, act=0):
+    def _gemm(self, name, x, w, b, act=0, residual=None):
         ev = self.gemm_events
         if ev is None:
-            return ops.x3_linear(x, w, b, act=act)
+            return ops.x3_linear(x, w, b, act=act, residual=residual)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         y = ops.x3_linear(x, w, b, act=act)
@@ -208,15 +211,17 @@ class BertTowerX3:
             qkv = self._gemm("qkv", hs, ly["qkv_w"], ly["qkv_b"]).view(B * L, 3 * C)
             ctx = ops.x3_attention_split(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], B, L, L, heads, dh,
                                          1.0 / math.sqrt(dh), mask=mask)
-            a = self._gemm("o", ctx, ly["o_w"], ly["o_b"])
+            rg = self.res_in_gemm and self.gemm_events is None
+            a = self._gemm("o", ctx, ly["o_w"], ly["o_b"], residual=h if rg else None)
             if self.gemm_events is None:
                 # LN(dense(ctx) + h), kept f32 for the next residual and split for FFN1
-                h, hs = ops.x3_ln_split(a, ly["ln1_g"], ly["ln1_b"], 1e-12, residual=h, keep_f32=True)
-                f = ops.x3_ffn(hs, ly["i_w"], ly["i_b"], ly["f_w"], ly["f_b"])
+                h, hs = ops.x3_ln_split(a, ly["ln1_g"], ly["ln1_b"], 1e-12, residual=None if rg else h, keep_f32=True)
+                f = ops.x3_ffn(hs, ly["i_w"], ly["i_b"], ly["f_w"], ly["f_b"], residual=h if rg else None)
+                r2 = None if rg else h
                 if li + 1 < len(self.layers):
-                    h, hs = ops.x3_ln_split(f, ly["ln2_g"], ly["ln2_b"], 1e-12, residual=h, keep_f32=True)
+                    h, hs = ops.x3_ln_split(f, ly["ln2_g"], ly["ln2_b"], 1e-12, residual=r2, keep_f32=True)
                 else:
-                    h = _ln(f, ly["ln2_g"], ly["ln2_b"], 1e-12, residual=h)
+                    h = _ln(f, ly["ln2_g"], ly["ln2_b"], 1e-12, residual=r2)
             else:
                 h = _ln(a, ly["ln1_g"], ly["ln1_b"], 1e-12, residual=h)
                 f = self._gemm("ffn2", self._gemm("ffn1", h, ly["i_w"], ly["i_b"], act=1), ly["f_w"], ly["f_b"])
