@@ -757,9 +757,14 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   };
   auto gS = [&](int sb, int buf, int kt) {
     if constexpr (FP8) {
-      if (wave < 2)
+      if (wave < 2) {
+        // the lane offset from a freshly computed lane id: held across the K loop, the bias + residual
+        // instantiation spilled it, and its reload (a vmcnt op) drained the K-tile prefetch of waves 0 / 1
+        int ll;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ll));
         __builtin_amdgcn_raw_ptr_buffer_load_lds(wave == 0 ? xsr : wsr, (lds_ptr_t)(dsm + soff(buf) + wave * 512), 16,
-                                                 lane * 16, sb + kt * 1024, 0, 0);
+                                                 (uint32_t)ll * 16, sb + kt * 1024, 0, 0);
+      }
     }
   };
   auto gA = [&](__amdgpu_buffer_rsrc_t xb, int buf, int j, int kt) {

@@ -194,7 +194,7 @@ struct AttnArgs {
 // every key masked -> HF's uniform softmax, the mean of V over the lk keys); 2: Swin windows (roll /
 // partition folded into the token map, q pre-scaled as timm, rel-pos + shift-mask bias added).
 template <int DT, int MODE>
-__global__ __launch_bounds__(256, DT <= 2 ? 3 : 2) void x3_mha(const AttnArgs a, int kbs) {
+__global__ __launch_bounds__(256, DT == 1 ? 4 : (DT == 2 ? 3 : 2)) void x3_mha(const AttnArgs a, int kbs) {
   constexpr int DHP = DT * 32, KS = DHP / 16, KROW = DHP + 8, VROW = DHP + ((DT & 1) ? 0 : 16);
   constexpr int C8 = DHP / 8, OROW = DHP + 4;
   // 32-key tiles per online-softmax step: 2 at DT = 1 (Swin); 1 at DT >= 2, so the S / P registers fit 3
@@ -285,9 +285,13 @@ __global__ __launch_bounds__(256, DT <= 2 ? 3 : 2) void x3_mha(const AttnArgs a,
           if (d >= dh) xa[u] = xb[u] = make_float4(0.f, 0.f, 0.f, 0.f);
           bf16x8 h, l;
           split8(xa[u], xb[u], h, l);
-          const int off = isv ? key * VROW + d : key * KROW + d;
-          *(bf16x8*)((isv ? Vh : Kh) + off) = h;
-          *(bf16x8*)((isv ? Vl : Kl) + off) = l;
+          // integer offsets from the one LDS base, not a select between image pointers: at UB = 4 hipcc
+          // kept {Kh, Vh} / {Kl, Vl} as generic pointer tables in scratch, and every image access of
+          // the kernel became a flat op (the score loop's Kl reads then waited vmcnt(0))
+          const int hoff = isv ? 2 * kbs * KROW + key * VROW + d : key * KROW + d;
+          const int loff = hoff + (isv ? kbs * VROW : kbs * KROW);
+          *(bf16x8*)(Kh + hoff) = h;
+          *(bf16x8*)(Kh + loff) = l;
         }
       }
     }
