@@ -193,8 +193,8 @@ struct AttnArgs {
 // MODE 0: plain (nn.MultiheadAttention); 1: key-padding mask as HF's additive finfo.min (a row with
 // every key masked -> HF's uniform softmax, the mean of V over the lk keys); 2: Swin windows (roll /
 // partition folded into the token map, q pre-scaled as timm, rel-pos + shift-mask bias added).
-template <int DT, int MODE>
-__global__ __launch_bounds__(256, DT == 1 ? 4 : (DT == 2 ? 3 : 2)) void x3_mha(const AttnArgs a, int kbs) {
+template <int DT, int MODE, bool SINGLE>
+__global__ __launch_bounds__(256, DT <= 2 ? 3 : 2) void x3_mha(const AttnArgs a, int kbs) {
   constexpr int DHP = DT * 32, KS = DHP / 16, KROW = DHP + 8, VROW = DHP + ((DT & 1) ? 0 : 16);
   constexpr int C8 = DHP / 8, OROW = DHP + 4;
   // 32-key tiles per online-softmax step: 2 at DT = 1 (Swin); 1 at DT >= 2, so the S / P registers fit 3
@@ -307,31 +307,47 @@ __global__ __launch_bounds__(256, DT == 1 ? 4 : (DT == 2 ? 3 : 2)) void x3_mha(c
     const int q0 = qc + wave * 32;
     const bool active = q0 < lq;  // wave-uniform
     const int qi = q0 + r < lq ? q0 + r : lq - 1;
-    // Q^T fragments: lane (query r, half hf) holds d = 16 ks + 8 hf .. + 7, split in registers
+    // Q^T fragments: lane (query r, half hf) holds d = 16 ks + 8 hf .. + 7, split in registers.
+    // SINGLE (Swin windows: one key block, lk <= 64 <= kbs): the raw rows are held until the key block
+    // is staged, so the Q and K / V loads are in flight together (split first, the Q load's round trip
+    // preceded the stage's): Swin stage 1 371 -> 353 us, stage 2 204 -> 192, stage 3 110 -> 100 (at 3
+    // waves per SIMD; the same at the fusion stack's single-block dh-96 calls measured no gain, and at
+    // dh 64 the raw rows cost a wave per SIMD; profiles/r05_x3_attn_qlate_ab.txt)
+    constexpr bool QLATE = SINGLE;
     bf16x8 qh[KS], ql[KS];
+    float4 qx[KS][2];
     {
       const float* qrow = qb + qtok(qi) * a.ldq;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         const int d = 16 * ks + 8 * hf;
-        float4 x0 = *(const float4*)(qrow + (d < dh ? d : 0)), x1 = *(const float4*)(qrow + (d < dh ? d : 0) + 4);
-        if (d >= dh) x0 = x1 = make_float4(0.f, 0.f, 0.f, 0.f);
+        qx[ks][0] = *(const float4*)(qrow + (d < dh ? d : 0));
+        qx[ks][1] = *(const float4*)(qrow + (d < dh ? d : 0) + 4);
+      }
+    }
+    auto qsplit = [&] {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        float4 x0 = qx[ks][0], x1 = qx[ks][1];
+        if (16 * ks + 8 * hf >= dh) x0 = x1 = make_float4(0.f, 0.f, 0.f, 0.f);
         if constexpr (MODE == 2) {  // timm scales q before q k^T
           x0 = make_float4(x0.x * a.scale, x0.y * a.scale, x0.z * a.scale, x0.w * a.scale);
           x1 = make_float4(x1.x * a.scale, x1.y * a.scale, x1.z * a.scale, x1.w * a.scale);
         }
         split8(x0, x1, qh[ks], ql[ks]);
       }
-    }
+    };
+    if constexpr (!QLATE) qsplit();
     f32x16 o[DT];
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) o[dt] = (f32x16){0};
     float m_run = -INFINITY, l_run = 0.f;
-    for (int k0 = 0; k0 < lkp; k0 += kbs) {
+    for (int k0 = 0; k0 < (SINGLE ? 1 : lkp); k0 += kbs) {  // SINGLE: one block, a loop hipcc removes
       const int kn = min(kbs, lkp - k0);
       __syncthreads();  // previous key block / previous chunk's epilogue done with the LDS
       stage(k0, kn);
       __syncthreads();
+      if constexpr (QLATE) qsplit();
       if (!active) continue;
       for (int kb0 = 0; kb0 < kn; kb0 += 32 * TPS) {
         const int nt = min(32 * TPS, kn - kb0) / 32;
@@ -805,6 +821,7 @@ mmr_status launch_attention(const char* who, AttnArgs a, int64_t nbh, bool swin,
   const int dt = (a.dh + 31) / 32;
   hipStream_t st = mmr::as_stream(stream);
   MMR_REQUIRE(!swin || dt == 1, "%s: Swin head_dim %d must be <= 32", who, a.dh);
+  MMR_REQUIRE(!swin || (a.lq == a.lk && a.lk <= 64), "%s: Swin windows of <= 64 tokens (lq=%d lk=%d)", who, a.lq, a.lk);
   const int nwv = std::min(4, (a.lq + 31) / 32);
   const int lkp = (a.lk + 31) & ~31;
   const int kbs = dt <= 1 ? std::min(128, lkp) : std::min(64, lkp);  // dt 2: 39 KB -> 3 blocks per CU (3 waves / SIMD)
@@ -813,8 +830,8 @@ mmr_status launch_attention(const char* who, AttnArgs a, int64_t nbh, bool swin,
   const size_t lds = std::max(kv, epi) + (size_t)nwv * dhp * 4 + (size_t)kbs * 4 + (swin ? 64 * 8 : 0);
   const dim3 grid((unsigned)nbh), blk(64 * nwv);
   const int mode = swin ? 2 : (a.kmask ? 1 : 0);
-#define XM(D_, M_) x3_mha<D_, M_><<<grid, blk, lds, st>>>(a, kbs)
-  if (mode == 2) XM(1, 2);
+#define XM(D_, M_) x3_mha<D_, M_, false><<<grid, blk, lds, st>>>(a, kbs)
+  if (mode == 2) x3_mha<1, 2, true><<<grid, blk, lds, st>>>(a, kbs);  // lk <= 64 <= kbs (checked above)
   else if (mode == 1) {
     switch (dt) {
       case 1: XM(1, 1); break;
