@@ -456,7 +456,7 @@ __global__ __launch_bounds__(256) void x3_patch_embed_pack(const float* __restri
 }
 
 template <int NW>
-__global__ __launch_bounds__(64 * NW) void x3_patch_embed_ln(const float* __restrict__ img,
+__global__ __launch_bounds__(64 * NW, 4) void x3_patch_embed_ln(const float* __restrict__ img,
                                                              const uint16_t* __restrict__ pack,
                                                              const float* __restrict__ bias,
                                                              const float* __restrict__ lng,
@@ -494,6 +494,10 @@ __global__ __launch_bounds__(64 * NW) void x3_patch_embed_ln(const float* __rest
       xl[s] = __builtin_bit_cast(bf16x8, make_uint4(ll[0], ll[1], ll[2], ll[3]));
     }
     f32x16 acc[3];
+    // an opaque per-tile zero on the weight-image address: hipcc otherwise hoists the 18 loop-invariant
+    // fragment reads out of the tile loop (72 more VGPRs live: 1 wave per SIMD)
+    int wz = 0;
+    asm volatile("" : "+v"(wz));
 #pragma unroll
     for (int u = 0; u < 3; ++u) {
 #pragma unroll
@@ -504,8 +508,8 @@ __global__ __launch_bounds__(64 * NW) void x3_patch_embed_ln(const float* __rest
       }
 #pragma unroll
       for (int s = 0; s < 3; ++s) {
-        const bf16x8 wh = *(const bf16x8*)(W + ((u * 3 + s) * 64 + lane) * 8);
-        const bf16x8 wl = *(const bf16x8*)(W + PE_IMG_E + ((u * 3 + s) * 64 + lane) * 8);
+        const bf16x8 wh = *(const bf16x8*)(W + wz + ((u * 3 + s) * 64 + lane) * 8);
+        const bf16x8 wl = *(const bf16x8*)(W + wz + PE_IMG_E + ((u * 3 + s) * 64 + lane) * 8);
         acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xh[s], acc[u], 0, 0, 0);
         acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xl[s], acc[u], 0, 0, 0);
         acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, xh[s], acc[u], 0, 0, 0);
