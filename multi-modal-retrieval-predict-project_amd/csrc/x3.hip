@@ -260,7 +260,10 @@ __global__ __launch_bounds__(256, DT <= 2 ? 3 : 2) void x3_mha(const AttnArgs a,
   // thread in flight (keys past lk / columns past dh read a clamped in-bounds chunk; columns past dh
   // are zeroed, keys past lk are -inf in the scores)
   auto stage = [&](int k0, int kn) {
-    constexpr int UB = DT >= 2 ? 2 : 4;  // chunks in flight per thread (register budget at DT >= 2)
+    // chunks in flight per thread: a block's staging is UB-deep rounds of HBM round trips (dh 96 at 128
+    // threads: 12 chunks per thread, 6 rounds at UB = 2, 2 at 6); the registers come within each
+    // instantiation's occupancy (fusion combiner 236 -> 218 us, profiles/r05_x3_attn_ub_ab.txt)
+    constexpr int UB = DT == 1 ? 4 : (DT == 2 ? 4 : 6);
     const int nch = kn * C8, tot = 2 * nch;
     for (int e0 = tid; e0 < tot; e0 += UB * nthr) {
       float4 xa[UB], xb[UB];
