@@ -592,6 +592,12 @@ int64_t mmr_x3_patch_embed_pack_elems(void);
 mmr_status mmr_x3_patch_embed_pack(const float* w, uint16_t* pack, void* stream);
 mmr_status mmr_x3_patch_embed_ln(const float* img, int32_t b, int32_t hw, const uint16_t* pack, const float* bias,
                                  const float* ln_g, const float* ln_b, float eps, float* y, void* stream);
+/* The bf16 towers' stem on the same pack: y (b, hw/4, hw/4, 96) bf16 = LayerNorm(conv(img) + bias) with the
+ * pixels rounded to bf16 and one bf16 product with the pack's hi image (= the bf16 conv weight), the
+ * bias and LayerNorm on the f32 accumulators; replaces mmr_patch_im2col + the GEMM + mmr_layernorm_bf16
+ * (timm PatchEmbed, fusion.py:198-199). */
+mmr_status mmr_patch_embed_ln_bf16(const float* img, int32_t b, int32_t hw, const uint16_t* pack, const float* bias,
+                                   const float* ln_g, const float* ln_b, float eps, uint16_t* y, void* stream);
 /* y (b, c) = (extra[b] + sum_t x[b][t]) / (l + 1) with extra (b, c), or sum_t x[b][t] / l when extra is
  * NULL; x (b, l, c) f32, summed in token order (unmasked token mean, model.py:370; the Swin global /
  * pooled means, fusion.py:263-265, model.py:463-468). */

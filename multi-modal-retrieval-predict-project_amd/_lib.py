@@ -123,6 +123,7 @@ SIGNATURES = {
     "mmr_x3_patch_embed_pack_elems": [],
     "mmr_x3_patch_embed_pack": [c_vp, c_vp, c_vp],
     "mmr_x3_patch_embed_ln": [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp],
+    "mmr_patch_embed_ln_bf16": [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp],
 }
 _RESTYPES = {"mmr_last_error": ctypes.c_char_p, "mmr_version": ctypes.c_int, "mmr_max_k": ctypes.c_int,
              "mmr_linear_bf16_variant": ctypes.c_int32, "mmr_linear_bf16_n_variants": ctypes.c_int32,

@@ -455,12 +455,15 @@ __global__ __launch_bounds__(256) void x3_patch_embed_pack(const float* __restri
   pack[PE_IMG_E + i] = mmr::f2bf(v - mmr::bf2f(hi));
 }
 
-template <int NW>
+// X3 = false: the bf16 towers' stem — one product of the bf16-rounded pixels with the hi image (= the
+// bf16 weight), the bias and LayerNorm on the f32 accumulators (no bf16 rounding of the conv output in
+// between), bf16 tokens out; replaces im2col + GEMM + LayerNorm (39 + 49 + 43 us at B = 256).
+template <int NW, bool X3>
 __global__ __launch_bounds__(64 * NW, 4) void x3_patch_embed_ln(const float* __restrict__ img,
                                                              const uint16_t* __restrict__ pack,
                                                              const float* __restrict__ bias,
                                                              const float* __restrict__ lng,
-                                                             const float* __restrict__ lnb, float* __restrict__ y,
+                                                             const float* __restrict__ lnb, void* __restrict__ yv,
                                                              int64_t ntile, int hw, float eps) {
   __shared__ __attribute__((aligned(16))) uint16_t W[2 * PE_IMG_E];
   __shared__ __attribute__((aligned(16))) float Pp[3 * PE_E];  // bias | gamma | beta
@@ -511,8 +514,10 @@ __global__ __launch_bounds__(64 * NW, 4) void x3_patch_embed_ln(const float* __r
         const bf16x8 wh = *(const bf16x8*)(W + wz + ((u * 3 + s) * 64 + lane) * 8);
         const bf16x8 wl = *(const bf16x8*)(W + wz + PE_IMG_E + ((u * 3 + s) * 64 + lane) * 8);
         acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xh[s], acc[u], 0, 0, 0);
-        acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xl[s], acc[u], 0, 0, 0);
-        acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, xh[s], acc[u], 0, 0, 0);
+        if constexpr (X3) {
+          acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xl[s], acc[u], 0, 0, 0);
+          acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, xh[s], acc[u], 0, 0, 0);
+        }
       }
     }
     // LayerNorm over the token's 96 outputs (lane half h holds 48 of them: channels 32 u + 8 i + 4 h + rr)
@@ -533,7 +538,6 @@ __global__ __launch_bounds__(64 * NW, 4) void x3_patch_embed_ln(const float* __r
       }
     ss += __shfl_xor(ss, 32, 64);
     const float rstd = rsqrtf(ss * (1.0f / PE_E) + eps);
-    float* yr = y + tok * PE_E;
 #pragma unroll
     for (int u = 0; u < 3; ++u)
 #pragma unroll
@@ -543,7 +547,11 @@ __global__ __launch_bounds__(64 * NW, 4) void x3_patch_embed_ln(const float* __r
         f32x4 v;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) v[rr] = (acc[u][4 * i + rr] - mean) * rstd * g4[rr] + b4[rr];
-        *(f32x4*)(yr + c) = v;
+        if constexpr (X3) {
+          *(f32x4*)((float*)yv + tok * PE_E + c) = v;
+        } else {
+          *(uint2*)((uint16_t*)yv + tok * PE_E + c) = make_uint2(mmr::pack2bf(v[0], v[1]), mmr::pack2bf(v[2], v[3]));
+        }
       }
   }
 }
@@ -636,21 +644,36 @@ mmr_status mmr_x3_patch_embed_pack(const float* w, uint16_t* pack, void* stream)
   return MMR_OK;
 }
 
-mmr_status mmr_x3_patch_embed_ln(const float* img, int32_t b, int32_t hw, const uint16_t* pack, const float* bias,
-                                 const float* ln_g, const float* ln_b, float eps, float* y, void* stream) {
+static mmr_status patch_embed_ln(const char* who, bool x3, const float* img, int32_t b, int32_t hw,
+                                 const uint16_t* pack, const float* bias, const float* ln_g, const float* ln_b,
+                                 float eps, void* y, void* stream) {
   mmr::clear_error();
-  MMR_REQUIRE(img && pack && bias && ln_g && ln_b && y, "mmr_x3_patch_embed_ln: NULL pointer");
+  MMR_REQUIRE(img && pack && bias && ln_g && ln_b && y, "%s: NULL pointer", who);
   MMR_REQUIRE(b >= 0 && hw > 0 && hw % 4 == 0 && ((hw / 4) * (hw / 4)) % 32 == 0,
-              "mmr_x3_patch_embed_ln: b=%d hw=%d (hw %% 4 == 0, (hw/4)^2 %% 32 == 0)", b, hw);
+              "%s: b=%d hw=%d (hw %% 4 == 0, (hw/4)^2 %% 32 == 0)", who, b, hw);
   auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  MMR_REQUIRE(al(img) && al(y) && al(bias) && al(ln_g) && al(ln_b) && al(pack), "mmr_x3_patch_embed_ln: 16-B aligned pointers");
+  MMR_REQUIRE(al(img) && al(y) && al(bias) && al(ln_g) && al(ln_b) && al(pack), "%s: 16-B aligned pointers", who);
   if (b == 0) return MMR_OK;
   const int64_t ntile = (int64_t)b * (hw / 4) * (hw / 4) / 32;
   const int64_t grid = std::min<int64_t>(2048, mmr::ceil_div(ntile, 4));
-  x3_patch_embed_ln<4><<<dim3((unsigned)grid), 256, 0, mmr::as_stream(stream)>>>(img, pack, bias, ln_g, ln_b, y, ntile,
-                                                                              hw, eps);
+  if (x3)
+    x3_patch_embed_ln<4, true><<<dim3((unsigned)grid), 256, 0, mmr::as_stream(stream)>>>(img, pack, bias, ln_g, ln_b, y,
+                                                                                        ntile, hw, eps);
+  else
+    x3_patch_embed_ln<4, false><<<dim3((unsigned)grid), 256, 0, mmr::as_stream(stream)>>>(img, pack, bias, ln_g, ln_b, y,
+                                                                                         ntile, hw, eps);
   MMR_LAUNCH_CHECK();
   return MMR_OK;
+}
+
+mmr_status mmr_x3_patch_embed_ln(const float* img, int32_t b, int32_t hw, const uint16_t* pack, const float* bias,
+                                 const float* ln_g, const float* ln_b, float eps, float* y, void* stream) {
+  return patch_embed_ln("mmr_x3_patch_embed_ln", true, img, b, hw, pack, bias, ln_g, ln_b, eps, y, stream);
+}
+
+mmr_status mmr_patch_embed_ln_bf16(const float* img, int32_t b, int32_t hw, const uint16_t* pack, const float* bias,
+                                   const float* ln_g, const float* ln_b, float eps, uint16_t* y, void* stream) {
+  return patch_embed_ln("mmr_patch_embed_ln_bf16", false, img, b, hw, pack, bias, ln_g, ln_b, eps, y, stream);
 }
 
 }  // extern "C"

@@ -895,6 +895,17 @@ def x3_patch_embed_ln(img, pack, bias, g, b, eps):
     return y
 
 
+def patch_embed_ln_bf16(img, pack, bias, g, b, eps):
+    """(B, 3, H, W) f32 -> (B, H/4, W/4, 96) bf16 = LayerNorm(conv4x4/s4(img) + bias) for the bf16 towers: bf16
+    pixels x the bf16 weight (the x3 pack's hi image), bias + LayerNorm in f32, one pass."""
+    _lib.require_gpu(img)
+    B, _, H, _ = img.shape
+    y = torch.empty((B, H // 4, H // 4, 96), dtype=torch.bfloat16, device=img.device)
+    _chk(_L().mmr_patch_embed_ln_bf16(_lib.ptr(img), B, H, _lib.ptr(pack), _lib.ptr(bias), _lib.ptr(g), _lib.ptr(b),
+                                      float(eps), _lib.ptr(y), _s(img)), "mmr_patch_embed_ln_bf16")
+    return y
+
+
 def x3_patch_merge_ln_split(x, g, b, eps):
     """x3_patch_merge_ln as X3Rows (the reduction linear's split operand) when the merged token count
     fills 256-row tiles, else f32 rows."""

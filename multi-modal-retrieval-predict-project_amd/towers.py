@@ -143,6 +143,10 @@ class SwinTower:
         self.pe_w, self.pe_b = _bf(wp, dev), _f(sd["patch_embed.proj.bias"], dev)
         self.pe_rw = _rw(self.pe_w)
         self.pe_g, self.pe_beta = _f(sd["patch_embed.norm.weight"], dev), _f(sd["patch_embed.norm.bias"], dev)
+        # the fused stem (mmr_patch_embed_ln_bf16) for Swin-T's 4 x 4 / 3 -> 96 conv: its pack built from the
+        # bf16-rounded weight, so the hi image IS the bf16 conv weight
+        self.pe_pack = (ops.x3_patch_embed_pack(self.pe_w[:, :w.shape[1]].float().contiguous())
+                        if self.cfg["patch"] == 4 and tuple(w.shape) == (96, 48) else None)
         self.stages = []
         res = self.cfg["img_size"] // self.cfg["patch"]
         ws0 = self.cfg["window_size"]
@@ -191,10 +195,14 @@ class SwinTower:
         image = image.to(self.device, torch.float32).contiguous()
         B = image.shape[0]
         g = cfg["img_size"] // cfg["patch"]
-        cols = ops.patch_im2col(image, cfg["patch"])
-        x = (ops.linear_rw(cols, self.pe_rw, self.pe_b) if self.pe_rw is not None
-             else ops.linear(cols, self.pe_w, self.pe_b))                 # (B, g*g, E)
-        x = ops.layernorm(x, self.pe_g, self.pe_beta, 1e-5).view(B, g, g, -1)
+        if self.pe_pack is not None and image.shape[1] == 3 and image.shape[2] == image.shape[3] \
+                and (g * g) % 32 == 0:
+            x = ops.patch_embed_ln_bf16(image, self.pe_pack, self.pe_b, self.pe_g, self.pe_beta, 1e-5)
+        else:
+            cols = ops.patch_im2col(image, cfg["patch"])
+            x = (ops.linear_rw(cols, self.pe_rw, self.pe_b) if self.pe_rw is not None
+                 else ops.linear(cols, self.pe_w, self.pe_b))                 # (B, g*g, E)
+            x = ops.layernorm(x, self.pe_g, self.pe_beta, 1e-5).view(B, g, g, -1)
         ws0 = cfg["window_size"]
         for i, st in enumerate(self.stages):
             if i > 0:

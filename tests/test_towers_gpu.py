@@ -309,6 +309,34 @@ def test_patch_im2col_and_merge():
     assert rel_err(y, ref) < 1e-2
 
 
+
+@pytest.mark.parametrize("B,hw", [(3, 224), (2, 32), (1, 64)])
+def test_patch_embed_ln_bf16_fused(B, hw):
+    """The bf16 towers' fused stem (mmr_patch_embed_ln_bf16: bf16 pixels x bf16 conv weight, bias + LayerNorm
+    on the f32 accumulators, bf16 out) vs the f64 conv + LayerNorm of the same bf16-rounded operands: within
+    one bf16 rounding of the output (2^-8 relative + 2e-3 absolute per element); and vs the unfused route
+    (im2col -> GEMM -> LayerNorm, which also rounds the conv output to bf16) within 2 output ulps."""
+    g_ = torch.Generator().manual_seed(7 * hw + B)
+    img = (torch.randn(B, 3, hw, hw, generator=g_) * 1.5).to(DEV)
+    w = (torch.randn(96, 3, 4, 4, generator=g_) * 48 ** -0.5).to(DEV)
+    bias = (torch.randn(96, generator=g_) * 0.1).to(DEV)
+    gm = (1 + 0.2 * torch.randn(96, generator=g_)).to(DEV)
+    bt = (0.1 * torch.randn(96, generator=g_)).to(DEV)
+    wb = bf(w.reshape(96, 48))
+    pack = ops.x3_patch_embed_pack(wb.float().contiguous())
+    y = ops.patch_embed_ln_bf16(img, pack, bias, gm, bt, 1e-5)
+    assert y.shape == (B, hw // 4, hw // 4, 96) and y.dtype == torch.bfloat16
+    ref = F.conv2d(bf(img).double(), wb.double().reshape(96, 3, 4, 4), bias.double(), stride=4).permute(0, 2, 3, 1)
+    ref = F.layer_norm(ref, (96,), gm.double(), bt.double(), 1e-5)
+    err = (y.double() - ref).abs()
+    assert (err <= ref.abs() * 2.0 ** -8 + 2e-3).all(), err.max().item()
+    wp = torch.zeros(96, 64, device=DEV)
+    wp[:, :48] = wb.float()
+    cols = ops.patch_im2col(img, 4)
+    x = ops.layernorm(ops.linear(cols, bf(wp), bias), gm, bt, 1e-5).view(B, hw // 4, hw // 4, 96)
+    assert ((y.float() - x.float()).abs() <= x.float().abs() * 2.0 ** -7 + 4e-3).all()
+
+
 @pytest.mark.parametrize("B,H,C", [(2, 28, 96), (3, 14, 192), (1, 14, 384), (1, 2, 96), (5, 6, 192)])
 def test_patch_merge_ln_geometries(B, H, C):
     """PatchMerging gather + LN (timm: x0..x3 = x[0::2,0::2], x[1::2,0::2], x[0::2,1::2], x[1::2,1::2]

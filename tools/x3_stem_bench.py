@@ -31,3 +31,13 @@ pack = ops.x3_patch_embed_pack(w)
 t = min(timeit(lambda: ops.x3_patch_embed_ln(img, pack, bias, gam, bet, 1e-5)) for _ in range(3))
 nbytes = img.numel() * 4 + B * 56 * 56 * 96 * 4
 print(f"{os.path.basename(_lib.LIB_PATH)}: x3 stem B={B} {t:7.1f} us  {nbytes / t / 1e6:5.2f} TB/s algorithmic", flush=True)
+if hasattr(_lib.lib(), "mmr_patch_embed_ln_bf16"):
+    from mmr_amd.towers import SWIN_T, SwinTower, init_swin_state  # noqa: E402
+    wb = w.reshape(96, 48).to(torch.bfloat16)
+    pb = ops.x3_patch_embed_pack(wb.float().contiguous())
+    t1 = min(timeit(lambda: ops.patch_embed_ln_bf16(img, pb, bias, gam, bet, 1e-5)) for _ in range(3))
+    wp = torch.zeros(96, 64, device="cuda", dtype=torch.bfloat16)
+    wp[:, :48] = wb
+    t2 = min(timeit(lambda: ops.layernorm(ops.linear(ops.patch_im2col(img, 4), wp, bias), gam, bet, 1e-5))
+             for _ in range(3))
+    print(f"bf16 stem B={B}: fused {t1:7.1f} us | im2col + GEMM + LayerNorm {t2:7.1f} us", flush=True)
