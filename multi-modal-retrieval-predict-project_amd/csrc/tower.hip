@@ -1059,10 +1059,11 @@ static mmr_status swin_window_attention_launch(const uint16_t* qkv, const float*
   if (b == 0) return MMR_OK;
   MMR_REQUIRE((int64_t)b * hw * hw * 3 * c < ((int64_t)1 << 32), "mmr_swin_window_attention: %lld qkv elements (32-bit offsets)",
               (long long)b * hw * hw * 3 * c);
-  // head pairs per wave where single-head waves would be plentiful (stage 2: 24576 single units),
-  // one head per wave otherwise (stage 4, 6144 single units: 27 vs 31 us with pairs)
-  const int64_t single = (int64_t)b * (hw / ws) * (hw / ws) * heads;
-  const int hpw = single >= 16384 ? 2 : 1;
+  // one head per wave: the head pairs (hpw = 2, a wave reading whole 128-B lines) serialise two load
+  // round trips per wave, and the pair's halves of a line are read by adjacent waves of one workgroup
+  // anyway (6 / 12 / 24 heads, 4 waves per workgroup): in the cfg2 step stage 2 131 -> 116 us, at
+  // B = 2048 every stage 7 % faster with single heads (profiles/r05_swa_head_pairs_ab.txt)
+  const int hpw = 1;
   const int64_t units = (int64_t)b * (hw / ws) * (hw / ws) * ((heads + hpw - 1) / hpw);
   if (q8)
     swin_window_attention<true><<<dim3((unsigned)mmr::ceil_div(units, 4)), 256, 0, mmr::as_stream(stream)>>>(
