@@ -260,3 +260,58 @@ def test_set_mode_failure_keeps_index_usable():
     i, _, s64 = ix.search(Q, K, want_f64=True)
     assert torch.equal(i, ref_i) and torch.equal(s64, ref64)
     ix.close()
+
+
+def _worker_rccl1(port, out_q):
+    """One rank over RCCL (backend "nccl"): the product's device path exactly as the 8-GPU run takes it
+    — device queries all-gathered by all_gather_into_tensor, the per-shard search on the GPU, ONE packed
+    all-gather of the lists (+ rerank components), the device merge — at world 1 on this box's GPU."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        N, D, B, K, DK = 20_011, 256, 16, 12, 64
+        G, gb, qb, gk, qk = _rerank_data(N, D, B, DK)
+        Q = torch.from_numpy(synthetic.gauss_gallery(B, D, 512)).cuda()
+        dev = torch.device("cuda:0")
+        st = torch.zeros((), dtype=torch.int32, device=dev)
+        sh = ShardedIndex.from_full(G, device=0, mode="f16")
+        assert dist.get_backend() == "nccl" and sh.world == 1
+        mi, ms, m64 = sh.search(Q, K)
+        tables = (_t(qb, dev), _t(gb, dev), _t(qk, dev), _t(gk, dev))
+        rr = sh.search_rerank(Q, K, tables=tables)
+        torch.cuda.synchronize()
+        out_q.put((mi.cpu().numpy(), m64.cpu().numpy(), [t.cpu().numpy() for t in rr], int(st.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_index_over_rccl_world1_equals_single_index():
+    """The RCCL branch of ShardedIndex on hardware (world 1: the collectives run through RCCL on this
+    GPU; the 8-GPU scaling run takes the same calls): search and search_rerank equal the single index."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    p = ctx.Process(target=_worker_rccl1, args=(port, q))
+    p.start()
+    mi, m64, rr, _ = q.get(timeout=180)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    N, D, B, K, DK = 20_011, 256, 16, 12, 64
+    G, gb, qb, gk, qk = _rerank_data(N, D, B, DK)
+    dev = torch.device("cuda:0")
+    ix = GalleryIndex(G, mode="f16")
+    qd = torch.from_numpy(synthetic.gauss_gallery(B, D, 512)).cuda()
+    si, _, s64 = ix.search(qd, K, want_f64=True)
+    ref = [t.cpu().numpy() for t in ix.rerank(qd, si, _t(qb, dev), _t(gb, dev), _t(qk, dev), _t(gk, dev), K)]
+    si, s64 = si.cpu().numpy(), s64.cpu().numpy()
+    ix.close()
+    np.testing.assert_array_equal(mi, si)
+    np.testing.assert_array_equal(m64, s64)
+    np.testing.assert_array_equal(rr[0], ref[0])
+    for a, b in zip(rr[1:], ref[1:]):
+        np.testing.assert_allclose(a, b, rtol=0, atol=1e-12)
