@@ -80,6 +80,9 @@ def parse(argv=None):
                    help="joint-embedding head: multimodal (reference default, model.py:137; 5 fusion layers, "
                         "8 heads), text / image (one tower + its head), both (both single-modality heads)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--collective", action="store_true",
+                   help="take the sharded RCCL search path (ShardedIndex: query all-gather, packed result "
+                        "all-gather, device merge) even at one rank, to time it on one GPU")
     p.add_argument("--cpu-sample-queries", type=int, default=0)
     p.add_argument("--parity-queries", type=int, default=256,
                    help="queries re-embedded by the fp32 oracle for recall / P@10 vs the CPU path")
@@ -140,13 +143,28 @@ def main():
         sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}: refusing to report a mismatched run")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 or a.collective:
+        # the sharded path adds RCCL's stream to the towers' main / side streams and the fusion stack's
+        # patch-side stream: past HIP's default 4 hardware queues the command processor time-slices the
+        # queues and every kernel of the step ran ~4 % slower (one rank: 14.9 -> 15.6 ms per cfg2 step;
+        # with 8 queues 14.9 again, profiles/r05_rccl_hw_queues_ab.txt).  Set before HIP initialises (the
+        # pool's boxes export HIP's default 4 explicitly, so raise it rather than only default it).
+        if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+            os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
     import numpy as np
     import torch
     import torch.distributed as dist
 
     torch.cuda.set_device(local)
-    if world > 1:
+    coll = world > 1 or a.collective  # the sharded search path over RCCL
+    if coll:
+        if world == 1 and "MASTER_ADDR" not in os.environ:  # one rank without a launcher
+            import socket
+            with socket.socket() as so:
+                so.bind(("127.0.0.1", 0))
+                os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(so.getsockname()[1]), RANK="0",
+                                  WORLD_SIZE="1")
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     dev = torch.device(f"cuda:{local}")
 
@@ -202,7 +220,7 @@ def main():
 
     sh = None
     rec = {"on": False}
-    if world > 1:  # the product's sharded path (mmr_amd.parallel.ShardedIndex) over RCCL
+    if coll:  # the product's sharded path (mmr_amd.parallel.ShardedIndex) over RCCL
         from mmr_amd.parallel import ShardedIndex
 
         def local_search(qq, k):  # this rank's shard, events around the search call (kNN roofline)
@@ -224,7 +242,7 @@ def main():
             q = model.query_embeddings(imgs, ids, mask)            # (B or 2B, d) f32
         else:
             q = qbatch
-        if world > 1:
+        if coll:
             rec["on"] = record
             if rr is None:
                 i, s, _ = sh.search(q, K)
@@ -389,7 +407,8 @@ def main():
                 " + fused KG/label rerank of the %d candidates" % K if a.rerank else ""))
                        if a.mode == "full" else ("%s kNN only: Q=%d, top-%d over %dx%d f32 per GPU" % (a.preset, B, K, n, d)),
                        "global_batch": world * B, "gallery_rows": world * n, "dim": d, "k": K,
-                       "parallelism": f"gallery row-shard x{world} + tower DP x{world}" if world > 1 else "single"},
+                       "parallelism": (f"gallery row-shard x{world} + tower DP x{world}" if world > 1 else
+                                       "single rank, sharded RCCL search path (--collective)" if coll else "single")},
             "roofline": roof,
             "knn_status_ok": True,
             "recall_at_10_vs_cpu": recall["recall_at_k"] if recall else None,
@@ -400,7 +419,7 @@ def main():
             "x3_mode": x3_line,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if coll:
         dist.destroy_process_group()
 
 
