@@ -262,8 +262,9 @@ __global__ __launch_bounds__(256, DT <= 2 ? 3 : 2) void x3_mha(const AttnArgs a,
   auto stage = [&](int k0, int kn) {
     // chunks in flight per thread: a block's staging is UB-deep rounds of HBM round trips (dh 96 at 128
     // threads: 12 chunks per thread, 6 rounds at UB = 2, 2 at 6); the registers come within each
-    // instantiation's occupancy (fusion combiner 236 -> 218 us, profiles/r05_x3_attn_ub_ab.txt)
-    constexpr int UB = DT == 1 ? 4 : (DT == 2 ? 4 : 6);
+    // instantiation's occupancy (fusion combiner 236 -> 218 us, profiles/r05_x3_attn_ub_ab.txt; 4 at dh 128,
+    // whose 6 spilled once the first block's stage holds the raw Q rows)
+    constexpr int UB = DT == 3 ? 6 : 4;
     const int nch = kn * C8, tot = 2 * nch;
     for (int e0 = tid; e0 < tot; e0 += UB * nthr) {
       float4 xa[UB], xb[UB];
@@ -310,16 +311,14 @@ __global__ __launch_bounds__(256, DT <= 2 ? 3 : 2) void x3_mha(const AttnArgs a,
     const int q0 = qc + wave * 32;
     const bool active = q0 < lq;  // wave-uniform
     const int qi = q0 + r < lq ? q0 + r : lq - 1;
-    // Q^T fragments: lane (query r, half hf) holds d = 16 ks + 8 hf .. + 7, split in registers.
-    // SINGLE (Swin windows: one key block, lk <= 64 <= kbs): the raw rows are held until the key block
-    // is staged, so the Q and K / V loads are in flight together (split first, the Q load's round trip
-    // preceded the stage's): Swin stage 1 371 -> 353 us, stage 2 204 -> 192, stage 3 110 -> 100 (at 3
-    // waves per SIMD; the same at the fusion stack's single-block dh-96 calls measured no gain, and at
-    // dh 64 the raw rows cost a wave per SIMD; profiles/r05_x3_attn_qlate_ab.txt)
-    constexpr bool QLATE = SINGLE;
+    // Q^T fragments: lane (query r, half hf) holds d = 16 ks + 8 hf .. + 7, split in registers.  The
+    // raw rows are held until the first key block is staged, so the Q and K / V loads are in flight
+    // together (split first, the Q load's round trip preceded the stage's): Swin stage 1 371 -> 353 us,
+    // stage 2 204 -> 192, stage 3 110 -> 100 (profiles/r05_x3_attn_qlate_ab.txt); the first block's
+    // stage is peeled out of the key loop, so the raw rows are dead before any compute
     bf16x8 qh[KS], ql[KS];
-    float4 qx[KS][2];
     {
+      float4 qx[KS][2];
       const float* qrow = qb + qtok(qi) * a.ldq;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
@@ -327,8 +326,9 @@ __global__ __launch_bounds__(256, DT <= 2 ? 3 : 2) void x3_mha(const AttnArgs a,
         qx[ks][0] = *(const float4*)(qrow + (d < dh ? d : 0));
         qx[ks][1] = *(const float4*)(qrow + (d < dh ? d : 0) + 4);
       }
-    }
-    auto qsplit = [&] {
+      __syncthreads();  // the previous query chunk's epilogue done with the LDS
+      stage(0, min(kbs, lkp));
+      __syncthreads();
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         float4 x0 = qx[ks][0], x1 = qx[ks][1];
@@ -339,18 +339,18 @@ __global__ __launch_bounds__(256, DT <= 2 ? 3 : 2) void x3_mha(const AttnArgs a,
         }
         split8(x0, x1, qh[ks], ql[ks]);
       }
-    };
-    if constexpr (!QLATE) qsplit();
+    }
     f32x16 o[DT];
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) o[dt] = (f32x16){0};
     float m_run = -INFINITY, l_run = 0.f;
     for (int k0 = 0; k0 < (SINGLE ? 1 : lkp); k0 += kbs) {  // SINGLE: one block, a loop hipcc removes
       const int kn = min(kbs, lkp - k0);
-      __syncthreads();  // previous key block / previous chunk's epilogue done with the LDS
-      stage(k0, kn);
-      __syncthreads();
-      if constexpr (QLATE) qsplit();
+      if (k0 > 0) {
+        __syncthreads();  // previous key block done with the LDS
+        stage(k0, kn);
+        __syncthreads();
+      }
       if (!active) continue;
       for (int kb0 = 0; kb0 < kn; kb0 += 32 * TPS) {
         const int nt = min(32 * TPS, kn - kb0) / 32;
