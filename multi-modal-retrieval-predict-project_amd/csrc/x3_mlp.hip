@@ -467,6 +467,11 @@ __global__ __launch_bounds__(64 * NW, 4) void x3_patch_embed_ln(const float* __r
                                                              int64_t ntile, int hw, float eps) {
   __shared__ __attribute__((aligned(16))) uint16_t W[2 * PE_IMG_E];
   __shared__ __attribute__((aligned(16))) float Pp[3 * PE_E];  // bias | gamma | beta
+  // per wave: one 32-channel slice of its 32 tokens' outputs (row stride 36 f32: conflict-free 16-B
+  // writes), written back as whole 128-B (f32) / 64-B (bf16) row segments — the tile's rows are
+  // consecutive tokens, so each store instruction covers 8 / 16 complete segments instead of 32
+  // scattered 16-B (f32) / 8-B (bf16) pieces
+  __shared__ __attribute__((aligned(16))) float stg[NW][32 * 36];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
   for (int i = threadIdx.x; i < 2 * PE_IMG_E / 8; i += 64 * NW) ((uint4*)W)[i] = ((const uint4*)pack)[i];
@@ -538,8 +543,10 @@ __global__ __launch_bounds__(64 * NW, 4) void x3_patch_embed_ln(const float* __r
       }
     ss += __shfl_xor(ss, 32, 64);
     const float rstd = rsqrtf(ss * (1.0f / PE_E) + eps);
+    float* sw = stg[wave];
+    const int64_t tok0 = tile * 32;
 #pragma unroll
-    for (int u = 0; u < 3; ++u)
+    for (int u = 0; u < 3; ++u) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int c = 32 * u + 8 * i + 4 * h;
@@ -547,12 +554,29 @@ __global__ __launch_bounds__(64 * NW, 4) void x3_patch_embed_ln(const float* __r
         f32x4 v;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) v[rr] = (acc[u][4 * i + rr] - mean) * rstd * g4[rr] + b4[rr];
-        if constexpr (X3) {
-          *(f32x4*)((float*)yv + tok * PE_E + c) = v;
-        } else {
-          *(uint2*)((uint16_t*)yv + tok * PE_E + c) = make_uint2(mmr::pack2bf(v[0], v[1]), mmr::pack2bf(v[2], v[3]));
+        *(f32x4*)(sw + r * 36 + 8 * i + 4 * h) = v;
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slice is in LDS
+      __builtin_amdgcn_wave_barrier();
+      if constexpr (X3) {  // lane: token 8 k + lane / 8, channels 4 (lane % 8) .. + 3 of the slice
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int t = 8 * k + (lane >> 3), c4 = (lane & 7) * 4;
+          *(f32x4*)((float*)yv + (tok0 + t) * PE_E + 32 * u + c4) = *(const f32x4*)(sw + t * 36 + c4);
+        }
+      } else {  // lane: token 16 k + lane / 4, channels 8 (lane % 4) .. + 7
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int t = 16 * k + (lane >> 2), c8 = (lane & 3) * 8;
+          const f32x4 a = *(const f32x4*)(sw + t * 36 + c8), b2 = *(const f32x4*)(sw + t * 36 + c8 + 4);
+          *(uint4*)((uint16_t*)yv + (tok0 + t) * PE_E + 32 * u + c8) =
+              make_uint4(mmr::pack2bf(a[0], a[1]), mmr::pack2bf(a[2], a[3]), mmr::pack2bf(b2[0], b2[1]),
+                         mmr::pack2bf(b2[2], b2[3]));
         }
       }
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // this slice's reads done before the next slice's writes
+      __builtin_amdgcn_wave_barrier();
+    }
   }
 }
 
