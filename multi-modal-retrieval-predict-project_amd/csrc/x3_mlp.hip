@@ -220,19 +220,37 @@ __global__ __launch_bounds__(64 * NW) void x3_swin_mlp(const float* __restrict__
     }
   }
 
-  // y[tok][c] = x + (fc2 + b2), c = 32 u + 8 i + 4 h + rr (the residual re-read: no registers held)
-  if (ok) {
+  // y[tok][c] = x + (fc2 + b2), c = 32 u + 8 i + 4 h + rr: each 32-channel slice of the wave's 32
+  // (consecutive) tokens staged through the then idle weight ring, so the residual re-read and the
+  // store move whole 128-B row segments (8 per instruction) instead of 32 scattered 16-B pieces
+  __builtin_amdgcn_s_waitcnt(vmcnt_n(0));
+  __syncthreads();  // every wave done with the ring
+  float* sw = (float*)smem + wave * 32 * 36;
+  const int64_t tok0 = (int64_t)blockIdx.x * G::TOK + wave * 32;
 #pragma unroll
-    for (int u = 0; u < G::NU; ++u)
+  for (int u = 0; u < G::NU; ++u) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int c = 32 * u + 8 * i + 4 * h;
-        const f32x4 bb = *(const f32x4*)(b2 + c), xq = *(const f32x4*)(x + tok * C + c);
-        f32x4 v;
+    for (int i = 0; i < 4; ++i) {
+      const int c = 32 * u + 8 * i + 4 * h;
+      const f32x4 bb = *(const f32x4*)(b2 + c);
+      f32x4 v;
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) v[rr] = (acc2[u][4 * i + rr] + bb[rr]) + xq[rr];
-        *(f32x4*)(y + tok * C + c) = v;
+      for (int rr = 0; rr < 4; ++rr) v[rr] = acc2[u][4 * i + rr] + bb[rr];
+      *(f32x4*)(sw + r * 36 + 8 * i + 4 * h) = v;
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slice is in LDS
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // lane: token 8 k + lane / 8, channels 4 (lane % 8) .. + 3 of the slice
+      const int t = 8 * k + (lane >> 3), c4 = (lane & 7) * 4;
+      if (tok0 + t < T) {
+        const int64_t o = (tok0 + t) * C + 32 * u + c4;
+        const f32x4 xq = *(const f32x4*)(x + o);
+        *(f32x4*)(y + o) = *(const f32x4*)(sw + t * 36 + c4) + xq;
       }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
