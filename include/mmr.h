@@ -172,9 +172,11 @@ int32_t mmr_linear_bf16_variant(int64_t m, int32_t n, int32_t k, int32_t act, in
 /* The BERT linears with the residual LayerNorm folded in, so no LayerNorm pass runs between the
  * GEMMs of a layer (HF BertLayer: LN(dense(x) + residual), reference fusion.py:322-325 via BertModel).
  * Persistent 8-phase bf16 GEMM, 256-row tiles: m % 256 == 0, k % 128 == 0, n % 192 == 0 or n % 256 == 0.
- *   stats_out (optional, act == 0): per row, mmr_linear_bf16_ln_parts(m, n, ln_mode) f32 pairs
- *     (sum, sum of squares) of the bf16 outputs as stored — [m][parts][2], summed they give the row's
- *     LayerNorm statistics (deterministic: one pair per tile column and wave column, no atomics).
+ *   stats_out (optional, act == 0): per row, parts = mmr_linear_bf16_ln_parts(m, n, ln_mode) f32 pairs
+ *     (sum, M2) of the bf16 outputs as stored — [m][parts][2]: part p covers the n / parts columns
+ *     [p n / parts, (p + 1) n / parts) and M2 is its CENTRED sum of squares, sum (y - part mean)^2 (not
+ *     a raw sum of squares); mmr_ln_row_coef merges the parts with Chan's parallel formula into the
+ *     row's LayerNorm statistics (deterministic: one pair per tile column and wave column, no atomics).
  *   ln_mode 0: y = act(x W^T + bias) (+ residual).
  *   ln_mode 1: x is a raw residual-stream row y_in produced with stats, ln_coef = its mmr_ln_row_coef
  *     (f32 [m][2]); w = W diag(gamma) (bf16), ln_v1 = c = row sums of w (f32 [n]),
@@ -189,8 +191,10 @@ mmr_status mmr_linear_bf16_ln(const uint16_t* x, const uint16_t* w, const float*
                               int32_t act, int32_t ln_mode, const float* ln_coef, const float* ln_v1,
                               const float* ln_v2, float* stats_out, void* stream);
 
-/* The row statistics of a producer (stats [m][nparts][2], nparts even) -> LayerNorm coefficients
- * coef [m][2] = (rstd, -mean rstd) over a row width n, rstd = 1 / sqrt(var + eps). */
+/* The row statistics of a producer (stats [m][nparts][2] = per part (sum, centred M2) over n / nparts
+ * columns each, as mmr_linear_bf16_ln writes them; nparts even, n % nparts == 0 — checked) -> LayerNorm
+ * coefficients coef [m][2] = (rstd, -mean rstd) over the row width n, rstd = 1 / sqrt(var + eps):
+ * mean = sum_p sum_p / n, M2 = sum_p M2_p + (n / nparts) sum_p (mean_p - mean)^2 (Chan). */
 mmr_status mmr_ln_row_coef(const float* stats, int64_t m, int32_t nparts, int32_t n, float eps, float* coef,
                            void* stream);
 
@@ -465,7 +469,7 @@ mmr_status mmr_ln_rows(const void* x, int64_t ldx, const float* alpha, const voi
                        int32_t io_bf16, int32_t groups, int64_t group_div, void* stream);
 
 /* f32 y = LayerNorm(alpha * x + residual) (alpha: a DEVICE f32 scalar or NULL = 1; residual may be NULL,
- * y may be NULL) that also writes xs, the x3 split GEMM's x_hilo operand: [hi | lo] bf16 rows 2 kp wide
+ * y may be NULL) that also writes xs, the x3 split GEMM's X operand: [hi | lo] bf16 rows 2 kp wide
  * (kp = mmr_x3_p8_kpad(c), zero columns c..kp), the split mmr_x3_split_rows would make of y.
  * c % 4 == 0, c <= 1024; rows 16-B aligned. */
 mmr_status mmr_ln_rows_split(const float* x, int64_t ldx, const float* alpha, const float* residual, int64_t ldr,
@@ -499,25 +503,24 @@ mmr_status mmr_rows_to_f32(const uint16_t* x, int64_t ldx, float* y, int32_t b, 
 mmr_status mmr_x3_linear(const float* x, int64_t ldx, const uint16_t* w_hi, const uint16_t* w_lo, const float* bias,
                          const float* residual, int64_t ldr, float* y, int64_t ldy, int64_t m, int32_t n, int32_t k,
                          int32_t act, void* stream);
-/* The same linear at the 8-phase GEMM's rate, as ONE K' = 3 kp bf16 GEMM with f32 accumulation:
- * X' = [x_hi | x_hi | x_lo], W' = [w_hi | w_lo | w_hi], each segment kp = mmr_x3_p8_kpad(k) wide (k
- * rounded up to 128, zero padding; 0 = k not taken), so X'.W'^T = x_hi.w_hi + x_hi.w_lo + x_lo.w_hi.
- * mmr_x3_split_rows writes X' ([m][3 kp] bf16, caller-allocated) from x rows at stride ldx;
- * mmr_x3_linear_p8 takes X' and the weight image W' ([npad][3 kp] bf16, built once at load, npad =
+/* The same linear at the 8-phase GEMM's rate: the split operands X = [x_hi | x_lo] and W = [w_hi | w_lo]
+ * (bf16 rows, each segment kp = mmr_x3_p8_kpad(k) wide: k rounded up to 128, zero padding; 0 = k not
+ * taken) in ONE GEMM whose K-tiles hold 32 k of both segments and issue x_hi.w_hi + x_hi.w_lo + x_lo.w_hi
+ * into f32 accumulators (each operand staged once).
+ * mmr_x3_split_rows writes X ([m][2 kp] bf16, caller-allocated) from f32 x rows at stride ldx;
+ * mmr_ln_rows_split, the attention _xs forms below and a split output (out_hilo) write the same rows.
+ * mmr_x3_linear_p8 takes X and the weight image W ([npad][2 kp] bf16, built once at load, npad =
  * mmr_x3_p8_npad(n): n itself when it is a multiple of 192 or 256, else n rounded up to 192 with zero
  * rows; 0 = n not taken) and writes y (m, n) f32 contiguous: m % 256 == 0, act 0 / 1 (GELU, erf), bias
  * NULL or npad floats (zero-padded), residual (m, n) f32 contiguous or NULL (may be y).
- * x_hilo != 0: xs holds [x_hi | x_lo] rows (2 kp wide; the x_hi segment is read twice; mmr_ln_rows_split
- * or a split output below writes them); needs a bias.
- * out_hilo != 0: y is written as the NEXT x3 GEMM's x_hilo operand, [y_hi | y_lo] bf16 rows 2 n wide
+ * out_hilo != 0: y is written as the NEXT x3 GEMM's X operand, [y_hi | y_lo] bf16 rows 2 n wide
  * (the split of the f32 value mmr_x3_split_rows would make, bit for bit); needs n % 384 == 0 and no
  * residual — a FFN1 -> FFN2 pair then skips the f32 round trip and the split pass. */
 int32_t mmr_x3_p8_kpad(int32_t k);
 int32_t mmr_x3_p8_npad(int32_t n);
 mmr_status mmr_x3_split_rows(const float* x, int64_t ldx, int64_t m, int32_t k, uint16_t* xs, void* stream);
-mmr_status mmr_x3_linear_p8(const uint16_t* xs, int32_t x_hilo, const uint16_t* w3, const float* bias,
-                            const float* residual, void* y, int64_t m, int32_t n, int32_t k, int32_t act,
-                            int32_t out_hilo, void* stream);
+mmr_status mmr_x3_linear_p8(const uint16_t* xs, const uint16_t* w2, const float* bias, const float* residual, void* y,
+                            int64_t m, int32_t n, int32_t k, int32_t act, int32_t out_hilo, void* stream);
 /* Attention core (nn.MultiheadAttention / BERT self-attention, eval): per (batch, head)
  * softmax(q k^T * scale (+ key mask)) v; rows as mmr_mha (q row bi*lq + i at q + row*ldq + head*dh);
  * mask01 (b, lk) int64 or NULL (0 -> key excluded, HF's additive finfo.min); out (b*lq, ldo) and/or
@@ -529,7 +532,7 @@ mmr_status mmr_x3_attention(const float* q, int64_t ldq, const float* k, int64_t
  * (b*hw*hw, c), q scaled by dh^-0.5 before q k^T (timm), bias from mmr_swin_attn_bias.  head_dim <= 32. */
 mmr_status mmr_x3_swin_window_attention(const float* qkv, const float* bias, float* out, int32_t b, int32_t hw,
                                         int32_t c, int32_t heads, int32_t ws, int32_t shift, void* stream);
-/* The two above writing their output as the x3 split GEMM's x_hilo operand instead (the O-proj / proj
+/* The two above writing their output as the x3 split GEMM's X operand instead (the O-proj / proj
  * input): xs = [hi | lo] bf16 rows 2 kp wide, kp = mmr_x3_p8_kpad(heads*dh) (columns heads*dh..kp zero),
  * the split mmr_x3_split_rows would make of the f32 output. */
 mmr_status mmr_x3_attention_xs(const float* q, int64_t ldq, const float* k, int64_t ldk, const float* v, int64_t ldv,

@@ -97,7 +97,7 @@ SIGNATURES = {
     "mmr_x3_p8_kpad": [c_i32],
     "mmr_x3_p8_npad": [c_i32],
     "mmr_x3_split_rows": [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp],
-    "mmr_x3_linear_p8": [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp],
+    "mmr_x3_linear_p8": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp],
     "mmr_x3_attention": [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32,
                          c_i32, c_f32, c_vp],
     "mmr_x3_attention_xs": [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32,

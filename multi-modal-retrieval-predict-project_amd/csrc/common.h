@@ -45,6 +45,13 @@ template <class T>
 __device__ __forceinline__ void pin(T& v) {
   asm volatile("" : "+v"(v));
 }
+// a * b rounded to f32 on its own: HIP's __fmul_rn is a plain multiply (no OCML_BASIC_ROUNDED_OPERATIONS)
+// that hipcc may contract with a following add into one fma; the pinned product cannot be
+__device__ __forceinline__ float mul_rn(float a, float b) {
+  float p = a * b;
+  asm volatile("" : "+v"(p));
+  return p;
+}
 // max over each 16-lane row by DPP: quad_perm [1,0,3,2] / [2,3,0,1] (xor 1 / 2), then row_half_mirror /
 // row_mirror, which pair quads / halves whose lanes already agree — the xor-1/2/4/8 butterfly's result
 // without its 4 LDS permutes

@@ -431,7 +431,7 @@ __global__ __launch_bounds__(256) void ln_rows(const TI* __restrict__ x, int64_t
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
-    const float t = av * v[i] + rv[i];
+    const float t = mmr::mul_rn(av, v[i]) + rv[i];  // product rounded, then the sum (torch's alpha * x + r)
     v[i] = lane + 64 * i < c ? t : 0.f;
     s += v[i];
   }
@@ -505,7 +505,10 @@ __global__ __launch_bounds__(256) void ln_rows_v(const float* __restrict__ x, in
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
-    v[i] = i < ni ? av * v[i] + rv[i] : (fv_t)0.f;
+    fv_t t = v[i];
+#pragma unroll
+    for (int e = 0; e < VW; ++e) t[e] = mmr::mul_rn(av, t[e]);  // product rounded, then the sum
+    v[i] = i < ni ? t + rv[i] : (fv_t)0.f;
 #pragma unroll
     for (int e = 0; e < VW; ++e) s += v[i][e];
   }
@@ -568,7 +571,7 @@ __global__ __launch_bounds__(256) void ln_rows_s(const float* __restrict__ x, in
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    v[i] = j + LPR * i < c ? av * v[i] + rv[i] : 0.f;
+    v[i] = j + LPR * i < c ? mmr::mul_rn(av, v[i]) + rv[i] : 0.f;  // product rounded, then the sum
     s += v[i];
   }
   const float mean = gsum(s) / c;
@@ -610,7 +613,8 @@ __global__ __launch_bounds__(256) void ln_rows_split(const float* __restrict__ x
   if (alpha) {  // LN(alpha x + r) (PreFusionEnhancer, fusion.py:33): the product rounded, then the sum
     const float av = *alpha;
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) v[i] = make_float4(av * v[i].x, av * v[i].y, av * v[i].z, av * v[i].w);
+    for (int i = 0; i < NCH; ++i)  // mmr::mul_rn: never contracted into the residual add below
+      v[i] = make_float4(mmr::mul_rn(av, v[i].x), mmr::mul_rn(av, v[i].y), mmr::mul_rn(av, v[i].z), mmr::mul_rn(av, v[i].w));
   }
   if (r) {
 #pragma unroll

@@ -573,8 +573,9 @@ __device__ unsigned long long p8_stamps[1024 * 8 * 8 * 4];
 // rows >= nval as -inf, instead of the tile.
 // LNM / STO (bf16, 256-row tiles): the BERT residual + LayerNorm folded into the GEMMs around it, so
 // no LayerNorm pass runs between them (mmr_linear_bf16_ln).  A producer (STO) writes, besides its
-// bf16 output y, one (sum y, sum y^2) f32 pair per row, tile column and wave column — SP[row][4 n-tile
-// + wc], over the bf16-ROUNDED outputs (deterministic, no atomics).  A consumer reads the LP pairs of
+// bf16 output y, one (sum y, M2 = sum (y - part mean)^2) f32 pair per row, tile column and wave column
+// (a part of 16 NT columns) — SP[row][4 n-tile + wc], over the bf16-ROUNDED outputs (deterministic, no
+// atomics); mmr_ln_row_coef merges the parts by Chan's formula.  A consumer reads the LP pairs of
 // input rows, reduced by mmr_ln_row_coef to LC[row] = (rstd, -mean rstd) — staged per tile into LDS
 // by LDS-DMA beside the bias (a global load in the epilogue would retire behind the next tile's
 // prefetch and expose it) — and either
@@ -582,8 +583,11 @@ __device__ unsigned long long p8_stamps[1024 * 8 * 8 * 4];
 //            epilogue (W' = W diag(gamma) pre-folded, LV1 = c = row sums of W', bias = d = W beta + b);
 //   LNM = 2: takes the raw y as the residual R and adds LN(y) = gamma (rstd y - rstd mean) + beta
 //            (LV1 = gamma, LV2 = beta over the output columns).
+#ifndef MMR_X3_PRODUCTS
+#define MMR_X3_PRODUCTS 3
+#endif
 template <int NT, int ACT, bool HAS_BIAS, bool HAS_RES, bool FP8 = false, bool OUT8 = false, int KNN = 0,
-          int LNM = 0, bool STO = false, bool OF32 = false, bool OSPL = false, bool XHL = false>
+          int LNM = 0, bool STO = false, bool OF32 = false, bool OSPL = false, bool X3P = false>
 __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restrict__ X,
                                                        const uint16_t* __restrict__ W,
                                                        const float* __restrict__ bias,
@@ -599,7 +603,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
                                                        const float* __restrict__ LC = nullptr,
                                                        const float* __restrict__ LV1 = nullptr,
                                                        const float* __restrict__ LV2 = nullptr,
-                                                       float* __restrict__ SP = nullptr, int ldn = 0, int xseg = 0) {
+                                                       float* __restrict__ SP = nullptr, int ldn = 0) {
   static_assert(!OUT8 || (FP8 && NT == 4 && !HAS_RES), "OUT8: MX-fp8 256x256 tiles without residual");
   static_assert((LNM == 0 && !STO) || (!FP8 && !KNN), "LayerNorm fold: bf16 GEMMs");
   static_assert(LNM != 2 || HAS_RES, "LNM = 2 normalises the residual");
@@ -608,7 +612,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   // OSPL (with OF32): the output written as the next x3 GEMM's split operand rows [hi | lo] (bf16, row
   // width 2 N) instead of f32 — one 8-B store of each per (m-tile, n-tile)
   static_assert(!OSPL || (OF32 && NT == 3 && !HAS_RES), "split output: OF32 256 x 192 tiles without residual");
-  static_assert(!XHL || OF32, "split input: the x3 split GEMM");
+  static_assert(!X3P || OF32, "three-product split operands: the x3 split GEMM (f32 output)");
   static_assert(KNN == 0 || ((KNN == 2 || KNN == 4) && NT == 4 && !FP8 && !HAS_BIAS && !HAS_RES && ACT == 0),
                 "KNN (rows per unit 2 / 4): plain 256x256 fp16 tiles");
 #if defined(__HIP_DEVICE_COMPILE__)  // buffer-descriptor builtins exist in the device pass only
@@ -713,16 +717,16 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   // one per-lane offset serves every piece of an operand: 64 j rows go into the uniform soffset
   const int prow = lane >> 3, pch = lane & 7;
   const int row0 = 8 * wave + prow;
-  const uint32_t off0 = (uint32_t)(row0 * K * ESZ + swz(row0, pch) * 16);
+  // X3P (the x3 split GEMM): X and W rows are [hi | lo] bf16, each segment kp = K / 2 wide, and one K-tile
+  // is 32 k of BOTH: LDS row = [hi 32 k | lo 32 k] (logical chunks 0-3 hi, 4-7 lo), so k-step 0 reads the
+  // hi fragment and k-step 1 the lo fragment of the same 32 k, and the MFMA segment issues hi.hi, lo.hi and
+  // hi.lo from those four fragments — each operand staged once (no [w_hi | w_lo | w_hi] image, no x_hi
+  // re-read) and 3 MFMAs per (m-tile, n-tile) per fragment set instead of 2.  A logical chunk c >= 4 sits
+  // kp elements (K bytes) further along the row; a K-tile advances 64 bytes.
+  auto chb = [&](int c) { return X3P ? (c < 4 ? c * 16 : K + (c - 4) * 16) : c * 16; };
+  const uint32_t off0 = (uint32_t)(row0 * K * ESZ + chb(swz(row0, pch)));
   const uint32_t pstride = (uint32_t)(64 * K * ESZ);  // bytes between consecutive pieces of an operand
-  // OF32, xseg > 0 (the x3 split GEMM fed [x_hi | x_lo] rows, 2 kp wide, against W' = [w_hi | w_lo |
-  // w_hi], 3 kp): X K-tile kt is read from kt - xseg once kt >= xseg (segment 1 re-reads x_hi, segment
-  // 2 reads x_lo), X rows are Kx = K - 64 xseg wide
-  // (XHL instantiations only: a per-lane offset more costs the others a spill)
-  const int Kx = XHL ? K - 64 * xseg : K;
-  const uint32_t off0x = XHL ? (uint32_t)(row0 * Kx * ESZ + swz(row0, pch) * 16) : off0;
-  const uint32_t pstridex = XHL ? (uint32_t)(64 * Kx * ESZ) : pstride;
-  auto kxt = [&](int kt) { return XHL && kt >= xseg ? kt - xseg : kt; };
+  constexpr int KTX = X3P ? 64 : KB * 2;              // X bytes per K-tile
   // KNN: the gallery W is in the index's tile32h layout (16-row x 32-half 1-KB pieces, knn.hip
   // tile32h_index) — the same image every other fp16 scan reads, so the index keeps ONE fp16 copy.
   // Logical chunk c of row r in K-tile kt = piece (r/16, 2 kt + c/4), lane slot (c%4) 16 + r%16: the
@@ -730,8 +734,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   const int wch = swz(row0, pch);
   const uint32_t off0w = KNN ? (uint32_t)(((row0 >> 4) * (K / 32) + (wch >> 2)) * 1024 + (((wch & 3) << 4) + (row0 & 15)) * 16)
                              : off0;
-  constexpr int KTW = KNN ? 2048 : KB * 2;  // W bytes per K-tile
-  const int nk = K * ESZ / 128;  // 128-byte K-tiles; even (launcher)
+  constexpr int KTW = KNN ? 2048 : KTX;  // W bytes per K-tile
+  const int nk = K * ESZ / 128;  // 128-byte K-tiles (X3P: 2 x 64 bytes); even (launcher)
   // operand panels as buffer descriptors (uniform, SGPRs): a piece is buffer_load ... lds with the
   // per-lane offset in voffset and the K-tile offset in soffset — no per-piece address registers
 #ifdef MMR_P8_SAMEPANEL
@@ -741,7 +745,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   auto pan = [](int v) { return v; };
 #endif
   auto xbase = [&](int tile) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)X + (int64_t)pan(mof(tile)) * 256 * Kx * ESZ), 0, 0x7FFFFFFF, 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)X + (int64_t)pan(mof(tile)) * 256 * K * ESZ), 0, 0x7FFFFFFF, 0x00020000);
   };
   auto wbase = [&](int tile) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)W + (int64_t)pan(nof(tile)) * TBN * K * ESZ), 0, 0x7FFFFFFF, 0x00020000);
@@ -768,8 +772,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
     }
   };
   auto gA = [&](__amdgpu_buffer_rsrc_t xb, int buf, int j, int kt) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(xb, (lds_ptr_t)(dsm + aoff(buf) + (64 * j + 8 * wave) * KB), 16, off0x,
-                                             kxt(kt) * (KB * 2) + j * pstridex, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(xb, (lds_ptr_t)(dsm + aoff(buf) + (64 * j + 8 * wave) * KB), 16, off0,
+                                             kt * KTX + j * pstride, 0, 0);
   };
   auto gB = [&](__amdgpu_buffer_rsrc_t wb, int buf, int j, int kt) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(wb, (lds_ptr_t)(dsm + boff(buf) + (64 * j + 8 * wave) * KB), 16, off0w,
@@ -978,6 +982,32 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
               for (int j = 0; j < NT - NH0; ++j)
                 acc[mi][NH0 + j] = mx_mfma(fb18[j], fa8[i], acc[mi][NH0 + j], scb, NH0 + j, sca[mi >> 2], mi & 3);
             }
+          }
+        } else if constexpr (X3P) {
+          // hi.hi, then lo.hi (w_lo . x_hi), then hi.lo (w_hi . x_lo): product-outermost, so 4 NH MFMAs
+          // separate two into the same accumulator
+          // (MMR_X3_PRODUCTS: diagnostic builds only — 1 = hi.hi alone, 6 = every product twice; results wrong)
+          constexpr int wk[6] = {0, 1, 0, 0, 1, 0}, xk[6] = {0, 0, 1, 0, 0, 1};  // k-step (0 hi, 1 lo) of W / X
+          constexpr int NPR = MMR_X3_PRODUCTS;
+          if (q == 0 || q == 3) {
+#pragma unroll
+            for (int pr = 0; pr < NPR; ++pr)
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                if (pr == 0 && i == 1) issue(2 * p + 1);
+#pragma unroll
+                for (int j = 0; j < NH0; ++j) acc[mb + i][j] = mfma16(fb0[j][wk[pr]], fa[i][xk[pr]], acc[mb + i][j]);
+              }
+          } else {
+#pragma unroll
+            for (int pr = 0; pr < NPR; ++pr)
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                if (pr == 0 && i == 1) issue(2 * p + 1);
+#pragma unroll
+                for (int j = 0; j < NT - NH0; ++j)
+                  acc[mb + i][NH0 + j] = mfma16(fb1[j][wk[pr]], fa[i][xk[pr]], acc[mb + i][NH0 + j]);
+              }
           }
         } else if (q == 0 || q == 3) {
 #pragma unroll
@@ -1867,10 +1897,11 @@ void launch_ln(const uint16_t* x, const uint16_t* w, const float* b, const uint1
                                             nullptr, 0, 0, 0, p8_nt(m, n, 2), nullptr, lc, v1, v2, sp);
 }
 
-// ---- fp32-faithful (x3) linears on the 8-phase GEMM: Y = X W^T + b as ONE K' = 3 kp bf16 GEMM with f32
-// accumulation, X' = [x_hi | x_hi | x_lo] and W' = [w_hi | w_lo | w_hi] (kp = K padded to 128 with zeros):
-// X'.W'^T = x_hi.w_hi + x_hi.w_lo + x_lo.w_hi, the three-term split of csrc/x3.hip at the 8-phase GEMM's
-// rate instead of the 128 x 128 x3_gemm's.  x3_split_rows writes X' (6 bytes per element of x).
+// ---- fp32-faithful (x3) linears on the 8-phase GEMM: Y = X W^T + b with f32 accumulation over the split
+// operands X = [x_hi | x_lo] and W = [w_hi | w_lo] (bf16 rows, each segment kp = K padded to 128 with
+// zeros): x_hi.w_hi + x_hi.w_lo + x_lo.w_hi, the three-term split of csrc/x3.hip, as ONE 8-phase GEMM
+// whose K-tiles hold 32 k of both segments and whose MFMA segments issue the three products (X3P).
+// x3_split_rows writes X (4 bytes per element of x).
 template <bool VEC>
 __global__ __launch_bounds__(256) void x3_split_rows(const float* __restrict__ x, int64_t ldx, int64_t m, int k, int kp,
                                                      uint16_t* __restrict__ xs) {
@@ -1894,22 +1925,20 @@ __global__ __launch_bounds__(256) void x3_split_rows(const float* __restrict__ x
     hi[e] = mmr::pack2bf(v[2 * e], v[2 * e + 1]);
     lo[e] = mmr::pack2bf(v[2 * e] - __uint_as_float(hi[e] << 16), v[2 * e + 1] - __uint_as_float(hi[e] & 0xFFFF0000u));
   }
-  uint16_t* o = xs + row * 3 * kp + c0;
-  const uint4 h4 = make_uint4(hi[0], hi[1], hi[2], hi[3]);
-  *(uint4*)o = h4;
-  *(uint4*)(o + kp) = h4;
-  *(uint4*)(o + 2 * kp) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+  uint16_t* o = xs + row * 2 * kp + c0;
+  *(uint4*)o = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+  *(uint4*)(o + kp) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
 }
 
-template <int NT, int ACT, bool HB, bool HR, bool OSPL = false, bool XHL = false>
-void launch_x3p8(const uint16_t* xs, const uint16_t* w3, const float* b, const float* r, void* y, int64_t m, int npad,
-                 int n, int k3, int xseg, hipStream_t st) {
+template <int NT, int ACT, bool HB, bool HR, bool OSPL = false>
+void launch_x3p8(const uint16_t* xs, const uint16_t* w2, const float* b, const float* r, void* y, int64_t m, int npad,
+                 int n, int kp, hipStream_t st) {
   const int grid = std::max(8, cu_count() / 8 * 8);
   const int tm = (int)(m / 256), tn = npad / (64 * NT);
-  gemm_bf16_tn_p8<NT, ACT, HB, HR, false, false, 0, 0, false, true, OSPL, XHL>
+  gemm_bf16_tn_p8<NT, ACT, HB, HR, false, false, 0, 0, false, true, OSPL, true>
       <<<dim3(std::max<int64_t>(8, std::min<int64_t>(grid, (int64_t)tm * tn) / 8 * 8)), dim3(512), P8<NT>::LDS_B, st>>>(
-          xs, w3, b, (const uint16_t*)r, (uint16_t*)y, m, npad, k3, tm, tn, nullptr, nullptr, nullptr, nullptr, nullptr,
-          0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, n, xseg);
+          xs, w2, b, (const uint16_t*)r, (uint16_t*)y, m, npad, 2 * kp, tm, tn, nullptr, nullptr, nullptr, nullptr,
+          nullptr, 0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, n);
 }
 }  // namespace
 
@@ -1955,7 +1984,8 @@ extern "C" mmr_status mmr_ln_row_coef(const float* stats, int64_t m, int32_t npa
                                       void* stream) {
   mmr::clear_error();
   MMR_REQUIRE(stats && coef, "mmr_ln_row_coef: NULL pointer");
-  MMR_REQUIRE(m >= 0 && nparts > 0 && nparts % 2 == 0 && n > 0, "mmr_ln_row_coef: m=%lld nparts=%d n=%d", (long long)m,
+  MMR_REQUIRE(m >= 0 && nparts > 0 && nparts % 2 == 0 && n > 0 && n % nparts == 0,
+              "mmr_ln_row_coef: m=%lld nparts=%d n=%d (nparts even, equal parts of n / nparts columns)", (long long)m,
               nparts, n);
   MMR_REQUIRE(((uintptr_t)stats & 15u) == 0 && ((uintptr_t)coef & 7u) == 0, "mmr_ln_row_coef: alignment");
   if (m == 0) return MMR_OK;
@@ -1994,11 +2024,11 @@ extern "C" mmr_status mmr_x3_split_rows(const float* x, int64_t ldx, int64_t m, 
   return MMR_OK;
 }
 
-extern "C" mmr_status mmr_x3_linear_p8(const uint16_t* xs, int32_t x_hilo, const uint16_t* w3, const float* bias,
-                                       const float* residual, void* y, int64_t m, int32_t n, int32_t k, int32_t act,
-                                       int32_t out_hilo, void* stream) {
+extern "C" mmr_status mmr_x3_linear_p8(const uint16_t* xs, const uint16_t* w2, const float* bias, const float* residual,
+                                       void* y, int64_t m, int32_t n, int32_t k, int32_t act, int32_t out_hilo,
+                                       void* stream) {
   mmr::clear_error();
-  MMR_REQUIRE(xs && w3 && y, "mmr_x3_linear_p8: NULL pointer");
+  MMR_REQUIRE(xs && w2 && y, "mmr_x3_linear_p8: NULL pointer");
   const int kp = mmr_x3_p8_kpad(k);
   MMR_REQUIRE(kp > 0 && m > 0 && m % 256 == 0, "mmr_x3_linear_p8: m=%lld (multiple of 256), k=%d", (long long)m, k);
   const int npad = mmr_x3_p8_npad(n);
@@ -2008,55 +2038,33 @@ extern "C" mmr_status mmr_x3_linear_p8(const uint16_t* xs, int32_t x_hilo, const
               "mmr_x3_linear_p8: split output needs n %% 384 == 0 and no residual (n=%d)", n);
   // (residual == y is fine: every output element is read, then written, by the one lane that owns it)
   hipStream_t st = mmr::as_stream(stream);
-  const int xseg = x_hilo ? kp / 64 : 0;  // [x_hi | x_lo] rows: segment 1 re-reads x_hi
   const int nt = out_hilo ? 3 : (npad % 192 == 0 && npad % 256 == 0 ? ln_nt(m, npad) : (npad % 256 == 0 ? 4 : 3));
   const bool hb = bias != nullptr, hr = residual != nullptr;
-  MMR_REQUIRE(!x_hilo || bias, "mmr_x3_linear_p8: split input is taken with a bias");
   if (out_hilo) {
-    if (x_hilo) {
-      if (act) launch_x3p8<3, 1, true, false, true, true>(xs, w3, bias, nullptr, y, m, npad, n, 3 * kp, xseg, st);
-      else launch_x3p8<3, 0, true, false, true, true>(xs, w3, bias, nullptr, y, m, npad, n, 3 * kp, xseg, st);
-    } else if (act) {
-      if (hb) launch_x3p8<3, 1, true, false, true>(xs, w3, bias, nullptr, y, m, npad, n, 3 * kp, 0, st);
-      else launch_x3p8<3, 1, false, false, true>(xs, w3, bias, nullptr, y, m, npad, n, 3 * kp, 0, st);
+    if (act) {
+      if (hb) launch_x3p8<3, 1, true, false, true>(xs, w2, bias, nullptr, y, m, npad, n, kp, st);
+      else launch_x3p8<3, 1, false, false, true>(xs, w2, bias, nullptr, y, m, npad, n, kp, st);
     } else {
-      if (hb) launch_x3p8<3, 0, true, false, true>(xs, w3, bias, nullptr, y, m, npad, n, 3 * kp, 0, st);
-      else launch_x3p8<3, 0, false, false, true>(xs, w3, bias, nullptr, y, m, npad, n, 3 * kp, 0, st);
+      if (hb) launch_x3p8<3, 0, true, false, true>(xs, w2, bias, nullptr, y, m, npad, n, kp, st);
+      else launch_x3p8<3, 0, false, false, true>(xs, w2, bias, nullptr, y, m, npad, n, kp, st);
     }
     MMR_LAUNCH_CHECK();
     return MMR_OK;
   }
   void* yf = y;
-  if (x_hilo) {
-#define X3P8H(NT_, A_)                                                                                               \
-  do {                                                                                                                \
-    if (hr) launch_x3p8<NT_, A_, true, true, false, true>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, xseg, st); \
-    else launch_x3p8<NT_, A_, true, false, false, true>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, xseg, st);   \
-  } while (0)
-    if (nt == 4) {
-      if (act) X3P8H(4, 1);
-      else X3P8H(4, 0);
-    } else {
-      if (act) X3P8H(3, 1);
-      else X3P8H(3, 0);
-    }
-#undef X3P8H
-    MMR_LAUNCH_CHECK();
-    return MMR_OK;
-  }
-#define X3P8(NT_)                                                                                             \
-  do {                                                                                                         \
-    if (act) {                                                                                                 \
-      if (hb && hr) launch_x3p8<NT_, 1, true, true>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, 0, st); \
-      else if (hb) launch_x3p8<NT_, 1, true, false>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, 0, st); \
-      else if (hr) launch_x3p8<NT_, 1, false, true>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, 0, st); \
-      else launch_x3p8<NT_, 1, false, false>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, 0, st);        \
-    } else {                                                                                                   \
-      if (hb && hr) launch_x3p8<NT_, 0, true, true>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, 0, st); \
-      else if (hb) launch_x3p8<NT_, 0, true, false>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, 0, st); \
-      else if (hr) launch_x3p8<NT_, 0, false, true>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, 0, st); \
-      else launch_x3p8<NT_, 0, false, false>(xs, w3, bias, residual, yf, m, npad, n, 3 * kp, 0, st);        \
-    }                                                                                                          \
+#define X3P8(NT_)                                                                                       \
+  do {                                                                                                   \
+    if (act) {                                                                                           \
+      if (hb && hr) launch_x3p8<NT_, 1, true, true>(xs, w2, bias, residual, yf, m, npad, n, kp, st);   \
+      else if (hb) launch_x3p8<NT_, 1, true, false>(xs, w2, bias, residual, yf, m, npad, n, kp, st);   \
+      else if (hr) launch_x3p8<NT_, 1, false, true>(xs, w2, bias, residual, yf, m, npad, n, kp, st);   \
+      else launch_x3p8<NT_, 1, false, false>(xs, w2, bias, residual, yf, m, npad, n, kp, st);          \
+    } else {                                                                                             \
+      if (hb && hr) launch_x3p8<NT_, 0, true, true>(xs, w2, bias, residual, yf, m, npad, n, kp, st);   \
+      else if (hb) launch_x3p8<NT_, 0, true, false>(xs, w2, bias, residual, yf, m, npad, n, kp, st);   \
+      else if (hr) launch_x3p8<NT_, 0, false, true>(xs, w2, bias, residual, yf, m, npad, n, kp, st);   \
+      else launch_x3p8<NT_, 0, false, false>(xs, w2, bias, residual, yf, m, npad, n, kp, st);          \
+    }                                                                                                    \
   } while (0)
   if (nt == 4) X3P8(4);
   else X3P8(3);

@@ -93,8 +93,8 @@ def linear_ln(x, w, bias, residual=None, act=0, ln_mode=0, coef=None, v1=None, v
     """mmr_linear_bf16_ln: the BERT linears with the residual LayerNorm folded in (no LayerNorm pass).
     coef = ln_row_coef of the producer of x (ln_mode 1: x raw, w = W diag(gamma), v1 = row sums of w,
     bias = W beta + b) or of the residual (ln_mode 2: residual raw, v1 / v2 = gamma / beta).
-    Returns (y, stats) — stats [rows, parts, 2] f32 (sum, sum of squares of the bf16 outputs) when
-    want_stats, else None."""
+    Returns (y, stats) — stats [rows, parts, 2] f32 when want_stats, else None: per part of N / parts
+    columns, (sum, M2 = centred sum of squares) of the bf16 outputs, merged by ln_row_coef (Chan)."""
     lead = x.shape[:-1]
     x2 = x.reshape(-1, x.shape[-1])
     M, K = x2.shape
@@ -403,28 +403,27 @@ def linear_f32(x, w, bias=None, residual=None, act=0, out=None):
 
 class X3W:
     """A per-query linear weight for linear_x3: the f32 weight (kept for the exact-f32 fallback) and its
-    bf16 split hi = bf16(w), lo = bf16(w - hi); (..., cout, cin).  `w3()`: the 8-phase GEMM image
-    [hi | lo | hi] (each segment kp = mmr_x3_p8_kpad(cin) wide, zero-padded) of a 2-D weight, built on
-    first use (x3_linear)."""
-    __slots__ = ("w", "hi", "lo", "_w3", "_bpad")
+    bf16 split hi = bf16(w), lo = bf16(w - hi); (..., cout, cin).  `w2()`: the split GEMM's weight image
+    [hi | lo] (each segment kp = mmr_x3_p8_kpad(cin) wide, zero-padded) of a 2-D weight, built on first use
+    (x3_linear)."""
+    __slots__ = ("w", "hi", "lo", "_w2", "_bpad")
 
     def __init__(self, w):
         self.w = w.contiguous()
         self.hi = self.w.to(torch.bfloat16)
         self.lo = (self.w - self.hi.float()).to(torch.bfloat16)
-        self._w3 = None
+        self._w2 = None
         self._bpad = None
 
-    def w3(self, kp, npad):
-        """[npad][3 kp] bf16: rows n.. npad - 1 and each segment's columns k.. kp - 1 zero."""
-        if self._w3 is None:
+    def w2(self, kp, npad):
+        """[npad][2 kp] bf16: rows n.. npad - 1 and each segment's columns k.. kp - 1 zero."""
+        if self._w2 is None:
             n, k = self.w.shape
-            img = torch.zeros((npad, 3 * kp), dtype=torch.bfloat16, device=self.w.device)
+            img = torch.zeros((npad, 2 * kp), dtype=torch.bfloat16, device=self.w.device)
             img[:n, :k] = self.hi
             img[:n, kp:kp + k] = self.lo
-            img[:n, 2 * kp:2 * kp + k] = self.hi
-            self._w3 = img
-        return self._w3
+            self._w2 = img
+        return self._w2
 
     def bias_padded(self, bias, npad):
         """bias zero-padded to npad entries (cached for the last bias seen)."""
@@ -659,7 +658,7 @@ def x3_ln_split(x, g, b, eps, residual=None, keep_f32=False, alpha=None):
 
 
 def _x3_linear_split_in(xr, wx, bias, residual, act, out):
-    """x3_linear of an X3Rows operand (mmr_x3_linear_p8 x_hilo)."""
+    """x3_linear of an X3Rows operand (mmr_x3_linear_p8 on the rows as they are)."""
     N, Kw = wx.w.shape
     assert xr.k == Kw, f"x3_linear: K {xr.k} != weight K {Kw}"
     M = xr.rows
@@ -669,8 +668,6 @@ def _x3_linear_split_in(xr, wx, bias, residual, act, out):
         # its re-split can differ from (hi, lo) where lo rounded to half an ulp of hi (same value)
         x = (xr.t[:, :xr.k].float() + xr.t[:, xr.kp:xr.kp + xr.k].float()).view(xr.lead + (xr.k,))
         return x3_linear(x, wx, bias, residual=residual, act=act, out=out)
-    if bias is None:  # the split-input kernels take a bias: zeros add exactly (v + 0 = v)
-        bias = torch.zeros(npad, dtype=torch.float32, device=xr.t.device)
     if out is not None and not out.is_contiguous():
         out.copy_(_x3_linear_split_in(xr, wx, bias, residual, act, None))
         return out
@@ -678,7 +675,7 @@ def _x3_linear_split_in(xr, wx, bias, residual, act, out):
         residual = residual.contiguous()
     r2 = residual.reshape(-1, N) if residual is not None else None
     y = out if out is not None else torch.empty(xr.lead + (N,), dtype=torch.float32, device=xr.t.device)
-    _chk(_L().mmr_x3_linear_p8(_lib.ptr(xr.t), 1, _lib.ptr(wx.w3(xr.kp, npad)), _lib.ptr(wx.bias_padded(bias, npad)),
+    _chk(_L().mmr_x3_linear_p8(_lib.ptr(xr.t), _lib.ptr(wx.w2(xr.kp, npad)), _lib.ptr(wx.bias_padded(bias, npad)),
                                _lib.ptr(r2), _lib.ptr(y), M, N, xr.k, act, 0, _s(xr.t)), "mmr_x3_linear_p8")
     return y
 
@@ -686,7 +683,7 @@ def _x3_linear_split_in(xr, wx, bias, residual, act, out):
 def x3_linear(x, wx, bias=None, residual=None, act=0, out=None):
     """act(x @ w.T + bias) (+ residual) for any number of rows: x (..., K) f32 (last-dim contiguous rows),
     wx an X3W of w (N, K), K % 32 == 0; residual may be `out`.  Row counts that fill 256-row tiles with
-    N >= 192 run as one K' = 3 kp split GEMM on the 8-phase kernel (mmr_x3_split_rows +
+    N >= 192 run as one three-product split GEMM on the 8-phase kernel (mmr_x3_split_rows +
     mmr_x3_linear_p8, N padded to whole tiles); the rest on mmr_x3_linear (128 x 128 tiles).  x may be
     an X3Rows (x3_ln_split), read as is."""
     if isinstance(x, X3Rows):
@@ -701,13 +698,13 @@ def x3_linear(x, wx, bias=None, residual=None, act=0, out=None):
     y = out if out is not None else torch.empty(x.shape[:-1] + (N,), dtype=torch.float32, device=x.device)
     r2 = residual.reshape(-1, N) if residual is not None else None
     kp, npad = _L().mmr_x3_p8_kpad(K), _L().mmr_x3_p8_npad(N)
-    # (N < 192: the split pass, 6 bytes written per element of x, costs more than the GEMM saves —
-    # Swin stage-1 fc2, N = 96 K = 384: 0.96 -> 1.11 ms per call)
+    # (N < 192: the split pass costs more than the GEMM saves — Swin stage-1 fc2, N = 96 K = 384: 0.96 ->
+    # 1.11 ms per call with the earlier 6-byte split)
     if (M > 0 and M % 256 == 0 and N >= 192 and kp > 0 and npad > 0 and y.is_contiguous()
             and (r2 is None or r2.is_contiguous())):
-        xs = torch.empty((M, 3 * kp), dtype=torch.bfloat16, device=x.device)
+        xs = torch.empty((M, 2 * kp), dtype=torch.bfloat16, device=x.device)
         _chk(_L().mmr_x3_split_rows(_lib.ptr(x2), x2.stride(0), M, K, _lib.ptr(xs), _s(x)), "mmr_x3_split_rows")
-        _chk(_L().mmr_x3_linear_p8(_lib.ptr(xs), 0, _lib.ptr(wx.w3(kp, npad)), _lib.ptr(wx.bias_padded(bias, npad)),
+        _chk(_L().mmr_x3_linear_p8(_lib.ptr(xs), _lib.ptr(wx.w2(kp, npad)), _lib.ptr(wx.bias_padded(bias, npad)),
                                    _lib.ptr(r2), _lib.ptr(y), M, N, K, act, 0, _s(x)), "mmr_x3_linear_p8")
         return y
     _chk(_L().mmr_x3_linear(_lib.ptr(x2), x2.stride(0), _lib.ptr(wx.hi), _lib.ptr(wx.lo), _lib.ptr(bias), _lib.ptr(r2),
@@ -719,7 +716,7 @@ def x3_linear(x, wx, bias=None, residual=None, act=0, out=None):
 def x3_ffn(x, w1, b1, w2, b2, residual=None):
     """fc2(GELU(fc1(x))) (+ residual), f32 in and out (the BERT / Swin MLP in the x3 mode).  When both
     rows fill 256-row tiles and fc1's width is a multiple of 384, fc1 writes its output straight as
-    fc2's [hi | lo] bf16 operand rows (mmr_x3_linear_p8 out_hilo / x_hilo): the f32 round trip and the
+    fc2's [hi | lo] bf16 operand rows (mmr_x3_linear_p8 out_hilo): the f32 round trip and the
     split pass drop out; bit-identical to the two x3_linear calls where those take the 8-phase route
     (fc2 N >= 192), within the split's rounding of them otherwise.  x may be an X3Rows."""
     L = _L()
@@ -733,10 +730,10 @@ def x3_ffn(x, w1, b1, w2, b2, residual=None):
             return x3_linear(x3_linear(x, w1, b1, act=1), w2, b2, residual=residual)
         assert x.k == w1.w.shape[1]
         hl = torch.empty((M, 2 * N1), dtype=torch.bfloat16, device=x.t.device)
-        _chk(L.mmr_x3_linear_p8(_lib.ptr(x.t), 1, _lib.ptr(w1.w3(x.kp, N1)), _lib.ptr(b1), None, _lib.ptr(hl), M, N1,
+        _chk(L.mmr_x3_linear_p8(_lib.ptr(x.t), _lib.ptr(w1.w2(x.kp, N1)), _lib.ptr(b1), None, _lib.ptr(hl), M, N1,
                                 x.k, 1, 1, _s(x.t)), "mmr_x3_linear_p8")
         y = torch.empty(x.lead + (N2,), dtype=torch.float32, device=x.t.device)
-        _chk(L.mmr_x3_linear_p8(_lib.ptr(hl), 1, _lib.ptr(w2.w3(kp2, np2)), _lib.ptr(w2.bias_padded(b2, np2)),
+        _chk(L.mmr_x3_linear_p8(_lib.ptr(hl), _lib.ptr(w2.w2(kp2, np2)), _lib.ptr(w2.bias_padded(b2, np2)),
                                 _lib.ptr(r2), _lib.ptr(y), M, N2, N1, 0, 0, _s(x.t)), "mmr_x3_linear_p8")
         return y
     _lib.require_gpu(x)
@@ -750,13 +747,13 @@ def x3_ffn(x, w1, b1, w2, b2, residual=None):
             and np2 > 0 and b1 is not None and b2 is not None and x2.stride(1) == 1
             and (r2 is None or r2.is_contiguous())):
         return x3_linear(x3_linear(x, w1, b1, act=1), w2, b2, residual=residual)
-    xs = torch.empty((M, 3 * kp1), dtype=torch.bfloat16, device=x.device)
+    xs = torch.empty((M, 2 * kp1), dtype=torch.bfloat16, device=x.device)
     _chk(L.mmr_x3_split_rows(_lib.ptr(x2), x2.stride(0), M, K, _lib.ptr(xs), _s(x)), "mmr_x3_split_rows")
     hl = torch.empty((M, 2 * N1), dtype=torch.bfloat16, device=x.device)  # [h_hi | h_lo] rows
-    _chk(L.mmr_x3_linear_p8(_lib.ptr(xs), 0, _lib.ptr(w1.w3(kp1, N1)), _lib.ptr(w1.bias_padded(b1, N1)), None,
+    _chk(L.mmr_x3_linear_p8(_lib.ptr(xs), _lib.ptr(w1.w2(kp1, N1)), _lib.ptr(w1.bias_padded(b1, N1)), None,
                             _lib.ptr(hl), M, N1, K, 1, 1, _s(x)), "mmr_x3_linear_p8")
     y = torch.empty(x.shape[:-1] + (N2,), dtype=torch.float32, device=x.device)
-    _chk(L.mmr_x3_linear_p8(_lib.ptr(hl), 1, _lib.ptr(w2.w3(kp2, np2)), _lib.ptr(w2.bias_padded(b2, np2)),
+    _chk(L.mmr_x3_linear_p8(_lib.ptr(hl), _lib.ptr(w2.w2(kp2, np2)), _lib.ptr(w2.bias_padded(b2, np2)),
                             _lib.ptr(r2), _lib.ptr(y), M, N2, N1, 0, 0, _s(x)), "mmr_x3_linear_p8")
     return y
 

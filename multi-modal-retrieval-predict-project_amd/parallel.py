@@ -158,6 +158,13 @@ class ShardedIndex:
         if local_search is None and index is not None:
             local_search = self._index_search
         if local_search is None:
+            # fp16 rows build the native fp16 index in f16 mode only; any other mode takes them upcast
+            # (as from_full does: GalleryIndex rejects fp16 rows with a non-f16 mode — ADVICE r05)
+            if mode != "f16":
+                if isinstance(gallery_rows, torch.Tensor) and gallery_rows.dtype == torch.float16:
+                    gallery_rows = gallery_rows.float()
+                elif isinstance(gallery_rows, np.ndarray) and gallery_rows.dtype == np.float16:
+                    gallery_rows = gallery_rows.astype(np.float32)
             self.index = GalleryIndex(gallery_rows, device=device, idx_base=start, mode=mode)
             local_search = self._index_search
         self.local_search = local_search

@@ -70,8 +70,9 @@ def _kernels(elf):
 
 @pytest.fixture(scope="module")
 def kernels():
-    if not os.path.exists(LIB):
-        subprocess.run(["make", "-j8"], cwd=os.path.join(ge.PKG, "csrc"), check=True)
+    # always the incremental build (a no-op when nothing changed): a stale libmmr.so left by an earlier
+    # build would pass the guard after a kernel change started spilling
+    subprocess.run(["make", "-j8"], cwd=os.path.join(ge.PKG, "csrc"), check=True, capture_output=True)
     data = open(LIB, "rb").read()
     ks = [kd for co in _code_objects(data) for kd in _kernels(co)]
     assert len(ks) > 100, "no gfx950 kernel metadata found in libmmr.so"

@@ -275,14 +275,35 @@ def _worker_rccl1(port, out_q):
         G, gb, qb, gk, qk = _rerank_data(N, D, B, DK)
         Q = torch.from_numpy(synthetic.gauss_gallery(B, D, 512)).cuda()
         dev = torch.device("cuda:0")
-        st = torch.zeros((), dtype=torch.int32, device=dev)
         sh = ShardedIndex.from_full(G, device=0, mode="f16")
         assert dist.get_backend() == "nccl" and sh.world == 1
         mi, ms, m64 = sh.search(Q, K)
         tables = (_t(qb, dev), _t(gb, dev), _t(qk, dev), _t(gk, dev))
         rr = sh.search_rerank(Q, K, tables=tables)
         torch.cuda.synchronize()
-        out_q.put((mi.cpu().numpy(), m64.cpu().numpy(), [t.cpu().numpy() for t in rr], int(st.item())))
+
+        # the device status row through RCCL: a local search that flags one query with a
+        # DEVICE status tensor — written into the packed all_gather_into_tensor buffer, read back by
+        # gathered_status — makes search raise 'status 1' after the exchange; the group still works
+        def flagged(q, k):
+            i, s64, st = sh._index_search(q, k)
+            st = st.clone()
+            st[1] = 1
+            return i, s64, st
+
+        msg = "no error"
+        try:
+            ShardedIndex(None, sh.n_total, sh.start, local_search=flagged).search(Q, K)
+        except RuntimeError as ex:
+            msg = str(ex)
+        t = torch.ones(1, device=dev)
+        dist.all_reduce(t)
+        # with status_out the flag accumulates on the device instead (no host sync, no raise)
+        so = torch.zeros((), dtype=torch.int32, device=dev)
+        fi, _, _ = ShardedIndex(None, sh.n_total, sh.start, local_search=flagged, status_out=so).search(Q, K)
+        torch.cuda.synchronize()
+        out_q.put((mi.cpu().numpy(), m64.cpu().numpy(), [t_.cpu().numpy() for t_ in rr],
+                   (msg, float(t.item()), int(so.item()), bool(torch.equal(fi, mi)))))
     finally:
         dist.destroy_process_group()
 
@@ -298,9 +319,11 @@ def test_sharded_index_over_rccl_world1_equals_single_index():
     s.close()
     p = ctx.Process(target=_worker_rccl1, args=(port, q))
     p.start()
-    mi, m64, rr, _ = q.get(timeout=180)
+    mi, m64, rr, (msg, red, so, same) = q.get(timeout=180)
     p.join(timeout=60)
     assert p.exitcode == 0
+    assert "status 1" in msg, msg
+    assert red == 1.0 and so == 1 and same
     N, D, B, K, DK = 20_011, 256, 16, 12, 64
     G, gb, qb, gk, qk = _rerank_data(N, D, B, DK)
     dev = torch.device("cuda:0")

@@ -530,6 +530,9 @@ def test_ln_row_coef_large_row_offset():
     rstd = 1 / torch.sqrt(var + eps)
     assert torch.allclose(cf[:, 0], rstd, rtol=2e-4), (cf[:, 0] / rstd - 1).abs().max().item()
     assert torch.allclose(cf[:, 1], -yd.mean(1) * rstd, rtol=2e-4)
+    # the parts are n / nparts columns each: a row width they do not divide fails loudly
+    with pytest.raises(Exception, match="equal parts"):
+        ops.ln_row_coef(st, C + 2, eps)
 
 
 def test_linear_ln_rejects():

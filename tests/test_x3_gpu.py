@@ -106,7 +106,7 @@ def test_x3_linear_p8_inplace_residual_and_route():
                                        (512, 768, 3072, True), (768, 384, 1536, True),
                                        (1000, 768, 3072, False)])  # rows not a multiple of 256: unfused
 def test_x3_ffn_split_handoff_bitwise(M, C, Fw, res):
-    """x3_ffn (fc1 writes fc2's [hi | lo] operand rows, fc2 reads them with the hi segment twice)
+    """x3_ffn (fc1 writes fc2's [hi | lo] operand rows, fc2 reads them as they are)
     equals x3_linear(GELU) -> x3_linear bit for bit where fc2 alone takes the 8-phase route (N >= 192;
     N = 96 runs the 128 x 128 x3 kernel alone: same products, another summation order -> 1e-5 of max),
     and stays within the x3 bound of f64."""
@@ -221,6 +221,28 @@ def test_ln_rows_split(rows, c, res):
     assert torch.equal(xs2.view(torch.int16), u)
 
 
+@pytest.mark.parametrize("rows,c", [(512, 768), (256, 96), (300, 96), (256, 100), (64, 1024)])
+def test_ln_alpha_product_rounded(rows, c):
+    """LN(alpha * x + r) (PreFusionEnhancer, reference src/Model/fusion.py:33): the kernels round the
+    product, then add — bit for bit the same as feeding torch's own rounded alpha * x with no alpha, for
+    ln_rows and for the split LayerNorm (f32 output and split rows); hipcc may not contract the product
+    into the residual add."""
+    g_ = torch.Generator().manual_seed(rows * 7 + c)
+    x = (torch.randn(rows, c, generator=g_) * 3 + 0.5).to(DEV)
+    r = torch.randn(rows, c, generator=g_).to(DEV)
+    gm = (1 + 0.1 * torch.randn(c, generator=g_)).to(DEV)
+    bt = (0.1 * torch.randn(c, generator=g_)).to(DEV)
+    alpha = torch.tensor([0.7377123], device=DEV)
+    xa = alpha * x
+    assert torch.equal(ops.ln_rows(x, gm, bt, 1e-5, alpha=alpha, residual=r), ops.ln_rows(xa, gm, bt, 1e-5, residual=r))
+    y1, s1 = ops.x3_ln_split(x, gm, bt, 1e-5, residual=r, keep_f32=True, alpha=alpha)
+    y0, s0 = ops.x3_ln_split(xa, gm, bt, 1e-5, residual=r, keep_f32=True)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y0)
+    if isinstance(s1, ops.X3Rows):
+        assert torch.equal(s1.t.view(torch.int16), s0.t.view(torch.int16))
+
+
 @pytest.mark.parametrize("M,C,Fw", [(1024, 96, 384), (512, 768, 3072), (768, 384, 1536)])
 def test_x3_split_rows_operand_bitwise(M, C, Fw):
     """A LayerNorm's split rows (x3_ln_split -> X3Rows) feed x3_linear / x3_ffn with the same bits as
@@ -250,20 +272,21 @@ def test_x3_split_rows_operand_bitwise(M, C, Fw):
 
 
 def test_x3_linear_p8_split_flags_rejected():
-    """The split operand flags' preconditions fail loudly at the C-ABI."""
+    """The split GEMM's preconditions fail loudly at the C-ABI."""
     L = _lib.lib()
-    x = torch.zeros(256, 3 * 384, dtype=torch.bfloat16, device=DEV)
-    w = torch.zeros(384, 3 * 384, dtype=torch.bfloat16, device=DEV)
+    x = torch.zeros(256, 2 * 384, dtype=torch.bfloat16, device=DEV)
+    w = torch.zeros(384, 2 * 384, dtype=torch.bfloat16, device=DEV)
     b = torch.zeros(384, dtype=torch.float32, device=DEV)
     y = torch.zeros(256, 2 * 384, dtype=torch.bfloat16, device=DEV)
     s = _lib.stream_ptr()
     P = _lib.ptr
-    # split output with a residual / n not a multiple of 384; split input without a bias; m not a
-    # multiple of 256; the split LayerNorm with c % 4 != 0 / misaligned rows
-    assert L.mmr_x3_linear_p8(P(x), 0, P(w), P(b), P(b), P(y), 256, 384, 384, 0, 1, s) != 0
-    assert L.mmr_x3_linear_p8(P(x), 0, P(w), P(b), None, P(y), 256, 192, 384, 0, 1, s) != 0
-    assert L.mmr_x3_linear_p8(P(x), 1, P(w), None, None, P(y), 256, 384, 384, 0, 0, s) != 0
-    assert L.mmr_x3_linear_p8(P(x), 1, P(w), P(b), None, P(y), 255, 384, 384, 0, 0, s) != 0
+    # split output with a residual / n not a multiple of 384; a NULL weight image; m not a multiple of
+    # 256; k past 4096; the split LayerNorm with c % 4 != 0 / misaligned rows
+    assert L.mmr_x3_linear_p8(P(x), P(w), P(b), P(b), P(y), 256, 384, 384, 0, 1, s) != 0
+    assert L.mmr_x3_linear_p8(P(x), P(w), P(b), None, P(y), 256, 192, 384, 0, 1, s) != 0
+    assert L.mmr_x3_linear_p8(P(x), None, P(b), None, P(y), 256, 384, 384, 0, 0, s) != 0
+    assert L.mmr_x3_linear_p8(P(x), P(w), P(b), None, P(y), 255, 384, 384, 0, 0, s) != 0
+    assert L.mmr_x3_linear_p8(P(x), P(w), P(b), None, P(y), 256, 384, 4097, 0, 0, s) != 0
     f = torch.zeros(8, 100, device=DEV)
     assert L.mmr_ln_rows_split(P(f), 100, None, None, 0, P(b), P(b), None, 0, P(y), 8, 98, 1e-5, s) != 0
     assert L.mmr_ln_rows_split(P(f), 99, None, None, 0, P(b), P(b), None, 0, P(y), 8, 96, 1e-5, s) != 0

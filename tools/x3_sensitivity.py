@@ -45,17 +45,16 @@ def p10(idx):
 
 
 class Wrap:
-    """An X3W stand-in whose split-GEMM image has segments zeroed."""
+    """An X3W stand-in whose split-GEMM weight image [w_hi | w_lo] has its lo segment zeroed (the weight
+    rounded to bf16; x keeps its split — the round-5 record in profiles/r05_x3_sensitivity.txt was taken on
+    the earlier [w_hi | w_lo | w_hi] image, where one bf16 product could be isolated)."""
     def __init__(self, wx, how):
         self.__dict__.update(w=wx.w, hi=wx.hi, lo=wx.lo, _inner=wx, _how=how, _img=None)
 
-    def w3(self, kp, npad):
+    def w2(self, kp, npad):
         if self._img is None:
-            img = self._inner.w3(kp, npad).clone()
-            if self._how == "bf16":
-                img[:, kp:] = 0
-            else:
-                img[:, kp:2 * kp] = 0
+            img = self._inner.w2(kp, npad).clone()
+            img[:, kp:] = 0
             self._img = img
         return self._img
 
