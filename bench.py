@@ -701,12 +701,54 @@ def x3_block(a, index, G, imgs, ids, mask, emb_par, nq_par, K, dev, steps=5):
     el = (time.perf_counter() - t0) / steps
     p10 = precision_vs_cpu(q[:nq_par], emb_par, a.dim, a.knn_mode)
     rec = recall_vs_cpu(index, q[:nq_par], emb_par, G, K)
+    gemms = x3_bert_gemms(m3.backbones.bert, ids.numel(), dev) if a.model_type != "image" else None
     del m3
     torch.cuda.empty_cache()
     return {"tower_dtype": "x3", "query_embeddings_per_s": a.batch / el, "ms_per_step": el * 1e3, "steps": steps,
+            "bert_gemms_x3": gemms,
             "note": "same step as the headline (B=%d, top-%d over the same index) with f32 towers: every linear and "
                     "attention contraction as hi*hi + hi*lo + lo*hi bf16 MFMA (csrc/x3.hip)" % (a.batch, K),
             "p_at_10": p10, "recall_vs_cpu": rec}
+
+
+def x3_bert_gemms(bert, rows, dev, reps=10):
+    """The four BERT split GEMMs of the x3 step at its shapes (rows = B x L tokens), each launched as the step
+    launches it (split-row operands; FFN1 writing FFN2's split rows; O-proj / FFN2 with the f32 residual),
+    on layer 0's weights and N(0,1) activations: HIP events around `reps` back-to-back launches on the
+    current stream.  frac = bf16 MFMA work (3 products per f32 product) / time / 2.5 PF."""
+    import torch
+    from mmr_amd import ops
+    if not hasattr(bert, "layers") or rows % 256:
+        return None
+    ly = bert.layers[0]
+    C, F = bert.hidden, ly["i_w"].w.shape[0]
+    g = torch.Generator(device=dev).manual_seed(11)
+    x = torch.randn(rows, C, device=dev, generator=g)
+    r = torch.randn(rows, C, device=dev, generator=g)
+    xr = ops.x3_ln_split(x, ly["ln1_g"], ly["ln1_b"], 1e-12)
+    if not isinstance(xr, ops.X3Rows) or F % 384:
+        return None
+    hr = ops.x3_linear_split_out(xr, ly["i_w"], ly["i_b"], act=1)
+    fns = {"qkv": (lambda: ops.x3_linear(xr, ly["qkv_w"], ly["qkv_b"]), 3 * C * C),
+           "o": (lambda: ops.x3_linear(xr, ly["o_w"], ly["o_b"], residual=r), C * C),
+           "ffn1": (lambda: ops.x3_linear_split_out(xr, ly["i_w"], ly["i_b"], act=1), F * C),
+           "ffn2": (lambda: ops.x3_linear(hr, ly["f_w"], ly["f_b"], residual=r), C * F)}
+    out = {}
+    stream = torch.cuda.current_stream(dev)
+    for name, (fn, nk) in fns.items():
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / reps
+        work = 3 * 2.0 * rows * nk
+        out[name] = {"ms_per_launch": ms, "bf16_mfma_flops": work, "frac_of_2p5pf": work / (ms * 1e-3) / 2.5e15}
+    out["note"] = ("x3 split GEMMs at the step's shapes, M = %d: HIP events over %d launches each; the bf16 line's "
+                   "bert_gemms are in roofline" % (rows, reps))
+    return out
 
 
 def recall_vs_cpu(index, q_gpu, emb_cpu, G, K):

@@ -938,8 +938,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
           for (int i = 0; i < 4; ++i) ldA(buf, i, 4 + i);
         }
         auto issue = [&](int sg) {
-#ifdef MMR_X3_NOLOAD
-          if (X3P && !last_it) return;  // diagnostic build only: the K loop on stale LDS (results wrong)
+#ifdef MMR_P8_NOLOAD
+          if (!KNN && !last_it) return;  // diagnostic build only: the K loop on stale LDS (results wrong)
 #endif
           if (loads) {
             if (sg == 2) gA(xl, 0, 0, ke);

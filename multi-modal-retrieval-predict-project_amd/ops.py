@@ -713,6 +713,18 @@ def x3_linear(x, wx, bias=None, residual=None, act=0, out=None):
     return y
 
 
+def x3_linear_split_out(xr, wx, bias, act=0):
+    """x3_linear of an X3Rows operand with its output written as the NEXT x3 GEMM's operand: X3Rows of
+    [hi | lo] bf16 rows 2 N wide (mmr_x3_linear_p8 out_hilo; the split of the f32 output, bit for bit).
+    N % 384 == 0, rows % 256 == 0, no residual."""
+    N, K = wx.w.shape
+    assert isinstance(xr, X3Rows) and xr.k == K and N % 384 == 0 and xr.rows % 256 == 0
+    hl = torch.empty((xr.rows, 2 * N), dtype=torch.bfloat16, device=xr.t.device)
+    _chk(_L().mmr_x3_linear_p8(_lib.ptr(xr.t), _lib.ptr(wx.w2(xr.kp, N)), _lib.ptr(wx.bias_padded(bias, N)), None,
+                               _lib.ptr(hl), xr.rows, N, K, act, 1, _s(xr.t)), "mmr_x3_linear_p8")
+    return X3Rows(hl, N, N, xr.lead)
+
+
 def x3_ffn(x, w1, b1, w2, b2, residual=None):
     """fc2(GELU(fc1(x))) (+ residual), f32 in and out (the BERT / Swin MLP in the x3 mode).  When both
     rows fill 256-row tiles and fc1's width is a multiple of 384, fc1 writes its output straight as
@@ -728,10 +740,7 @@ def x3_ffn(x, w1, b1, w2, b2, residual=None):
         if not (N1 % 384 == 0 and kp2 == N1 and np1 == N1 and np2 > 0 and b1 is not None and b2 is not None
                 and (r2 is None or r2.is_contiguous())):
             return x3_linear(x3_linear(x, w1, b1, act=1), w2, b2, residual=residual)
-        assert x.k == w1.w.shape[1]
-        hl = torch.empty((M, 2 * N1), dtype=torch.bfloat16, device=x.t.device)
-        _chk(L.mmr_x3_linear_p8(_lib.ptr(x.t), _lib.ptr(w1.w2(x.kp, N1)), _lib.ptr(b1), None, _lib.ptr(hl), M, N1,
-                                x.k, 1, 1, _s(x.t)), "mmr_x3_linear_p8")
+        hl = x3_linear_split_out(x, w1, b1, act=1).t
         y = torch.empty(x.lead + (N2,), dtype=torch.float32, device=x.t.device)
         _chk(L.mmr_x3_linear_p8(_lib.ptr(hl), _lib.ptr(w2.w2(kp2, np2)), _lib.ptr(w2.bias_padded(b2, np2)),
                                 _lib.ptr(r2), _lib.ptr(y), M, N2, N1, 0, 0, _s(x.t)), "mmr_x3_linear_p8")
