@@ -1262,7 +1262,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
                                  fmaf(ra[i], acc[i][j][rg + 1], fmaf(rb[i], cq[rg + 1], bq[j][rg + 1]))};
             else
               u = (mmr::f32x2_t){acc[i][j][rg] + bq[j][rg], acc[i][j][rg + 1] + bq[j][rg + 1]};
-            if (ACT == 1) u = mmr::gelu_fast2(u);
+            if (ACT == 1) u = OUT8 ? mmr::gelu_q8x2(u) : mmr::gelu_fast2(u);  // e4m3 output: the cheap form
             v[rg] = u.x;
             v[rg + 1] = u.y;
           }

@@ -1,7 +1,7 @@
 """The BERT FFN1 kernel the timed cfg2 / cfg5 steps run, launched N times for rocprofv3 --pmc passes:
   fold: mmr_linear_bf16_ln ln_mode 1 + GELU (bf16, LayerNorm folded; gemm_bf16_tn_p8<4, 1, LNM=1>)
   mx8:  mmr_linear_mxfp8_q8 + GELU (MX-fp8 in, fp8 operand of FFN2 out; gemm_bf16_tn_p8<4, 1, FP8, OUT8>)
-usage: python tools/pmc_ffn1.py fold|mx8 [M] [launches]"""
+usage: python tools/pmc_ffn1.py fold|mx8 [M] [launches] [tag: also time the launches with HIP events]"""
 import os
 import sys
 
@@ -33,7 +33,15 @@ elif mode == "mx8":
 else:
     raise SystemExit(f"unknown mode {mode}")
 torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+run()
+e0.record()
 for _ in range(n_launch):
     run()
+e1.record()
 torch.cuda.synchronize()
-print(f"{mode} M={M} N={N} K={C}: {n_launch} launches")
+us = e0.elapsed_time(e1) / n_launch * 1e3
+fl = 2.0 * M * N * C
+tag = sys.argv[4] if len(sys.argv) > 4 else ""
+print(f"{tag} {mode} M={M} N={N} K={C}: {n_launch} launches, {us:.1f} us each = {fl / us / 1e6:.0f} TF "
+      f"({fl / us / 1e6 / (5000 if mode == 'mx8' else 2500):.3f} of the dtype's dense peak)")
