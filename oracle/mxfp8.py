@@ -73,3 +73,15 @@ def e4m3_decode(b):
     v = np.where(E == 0, m / 8.0 * 2.0 ** -6, (1 + m / 8.0) * np.ldexp(1.0, E - 7))
     v = np.where((b & 0x7F) == 0x7F, np.nan, v)
     return (s * v).astype(np.float32)
+
+
+GELU_Q8_A, GELU_Q8_B = np.float32(1.60031416), np.float32(0.06940179)
+
+
+def gelu_q8(x):
+    """The GELU the MX-fp8 output epilogue computes (csrc/common.h gelu_q8x2: x sigmoid(x (a + b x^2)), (a, b)
+    minimax-fitted to the erf form), restated in f32 numpy (the device's v_exp / v_rcp differ by ~1 ulp)."""
+    x = np.asarray(x, np.float32)
+    p = (GELU_Q8_B * (x * x) + GELU_Q8_A).astype(np.float32)
+    return (x / (np.float32(1) + np.exp(-(x * p)).astype(np.float32))).astype(np.float32)
+

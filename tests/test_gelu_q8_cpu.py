@@ -7,13 +7,7 @@ amax, and under 2.8e-4 absolute everywhere."""
 import numpy as np
 from scipy.special import erf
 
-A, B = np.float32(1.60031416), np.float32(0.06940179)  # gelu_q8x2's coefficients (csrc/common.h)
-
-
-def gelu_q8(x):
-    x = np.asarray(x, np.float32)
-    p = (B * (x * x) + A).astype(np.float32)
-    return (x / (np.float32(1) + np.exp(-(x * p)).astype(np.float32))).astype(np.float32)
+from oracle.mxfp8 import gelu_q8
 
 
 def test_gelu_q8_under_half_e4m3_ulp():

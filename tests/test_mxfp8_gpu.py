@@ -108,26 +108,37 @@ def test_linear_mxfp8_q8_equals_quantised_bf16_output(M, N, K, act):
         assert torch.equal(y8.q, ref8.q)
         assert torch.equal(y8.s, ref8.s)
         return
-    # GELU: the e4m3 epilogue runs the cheap sigmoid form (common.h gelu_q8x2, bounded in
+    # GELU: the e4m3 epilogue runs the cheap sigmoid form (common.h gelu_q8x2 = oracle.mxfp8.gelu_q8, bounded in
     # tests/test_gelu_q8_cpu.py) — against the oracle's MX-fp8 of the f64 GEMM + erf GELU, rounded to bf16 as
-    # the epilogue rounds: the scale bytes equal (but for blocks whose amax sits on a binade edge), the
-    # elements bit-equal but where the erf value lies within the approximation's error of an e4m3 rounding
-    # boundary (< 2 %), and never further apart than one e4m3 step plus the approximation's own absolute
-    # bound (2.75e-4: tiny values in a block's subnormal range, far below its amax 2^-4 rounding of the rest)
-    ref = _ref(x8, w8, M, N, bias, None, act)
+    # the epilogue rounds: bit-exact wherever the bound allows, i.e. a code differs only where the erf value
+    # lies within |gelu_q8 - gelu_erf| (+ one bf16 ulp — both sides round to bf16 before e4m3 — and the f32
+    # accumulation) of an e4m3 rounding boundary, and then by one step plus that bound; the scale bytes equal
+    # but for blocks whose amax moved across a binade
+    z = _ref(x8, w8, M, N, bias, None, 0)                                  # f64 pre-activation
+    ref = _ref(x8, w8, M, N, bias, None, act)                              # erf GELU
     refb = torch.from_numpy(ref).float().to(torch.bfloat16).float().numpy()
     qo, eo = mx.quantize(refb, N)
     torch.cuda.synchronize()
     q, e = _decode(y8, M, 0)
     assert np.mean(e != eo) < 2e-3, np.mean(e != eo)
     same = np.repeat(e == eo, 32, axis=1)
-    bad = (q != qo) & same
-    assert bad.mean() < 0.02, bad.mean()
+    er = np.ldexp(1.0, -np.repeat(e, 32, axis=1))                          # 2^-e: real -> scaled units
+    qx, ex_ = _decode(x8, M, 0)
+    qw, ew = _decode(w8, N, w8.layout)
+    absdot = np.abs(mx.dequantize(qx, ex_)) @ np.abs(mx.dequantize(qw, ew)).T
+    acc = K * 2.0 ** -24 * absdot + 2.0 ** -24 * np.abs(z)                 # f32 accumulation (+ the bias add)
+    ulp16 = np.ldexp(1.0, np.floor(np.log2(np.maximum(np.abs(ref), 1e-30))).astype(int) - 7)  # bf16 ulp of ref
+    slack = (np.abs(mx.gelu_q8(z).astype(np.float64) - ref) + ulp16 + 1.13 * acc) * er
+    diff = (q != qo) & same
+    mid = (q.astype(np.float64) + qo) / 2                                  # the boundary between the two codes
+    near = np.abs(refb * er - mid) <= slack * 1.0001
+    assert np.all(near[diff]), f"{np.count_nonzero(diff & ~near)} codes differ away from a rounding boundary"
     a = np.maximum(np.abs(q), np.abs(qo))
     ex = np.floor(np.log2(np.maximum(a, 2.0 ** -30)))
-    step = np.where(ex >= -6, 2.0 ** (ex - 3), 2.0 ** -9) * np.ldexp(1.0, np.repeat(e, 32, axis=1))
-    diff = np.abs(mx.dequantize(q, e) - mx.dequantize(qo, eo))
-    assert np.all(diff[same] <= step[same] * 1.0001 + 2.75e-4), (diff - step)[same].max()
+    step = np.where(ex >= -6, 2.0 ** (ex - 3), 2.0 ** -9)
+    assert np.all(np.abs(q - qo)[diff] <= (step + 2 * slack)[diff] * 1.0001)  # one step (more only in a block's
+    #                                                  subnormal range, where the GELU's 2.7e-4 spans several)
+    print(f"codes differing at a rounding boundary: {diff.mean():.4%}")
 
 
 @pytest.mark.parametrize("rows,c,add", [(512, 768, True), (256, 768, False), (256, 1536, True)])
