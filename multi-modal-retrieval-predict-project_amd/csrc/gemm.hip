@@ -586,6 +586,9 @@ __device__ unsigned long long p8_stamps[1024 * 8 * 8 * 4];
 #ifndef MMR_X3_PRODUCTS
 #define MMR_X3_PRODUCTS 3
 #endif
+#ifndef X3ST_AUX
+#define X3ST_AUX 0
+#endif
 template <int NT, int ACT, bool HAS_BIAS, bool HAS_RES, bool FP8 = false, bool OUT8 = false, int KNN = 0,
           int LNM = 0, bool STO = false, bool OF32 = false, bool OSPL = false, bool X3P = false>
 __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restrict__ X,
@@ -654,11 +657,12 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
   constexpr bool skip_gm = false;
 #endif
   // STO: 8 more (one row-statistics store per m-tile, lanes fq = 0 — the instruction always issues)
-  // OF32: one 16-B store per (m-tile, n-tile) straight from the accumulators
+  // OF32: one 16-B store per (m-tile, n-tile) straight from the accumulators; OSPL: two (hi, lo) per (m-tile,
+  // n-tile pair)
   constexpr int nstore = skip_st ? 0
-                                 : (OF32 ? (OSPL ? 16 : 8) * NT
+                                 : (OF32 ? (NT == 3 ? 24 : (OSPL ? 16 * ((NT + 1) / 2) : 8 * NT))
                                          : (skip_gm ? 8 : (epi_pl ? C::NSTORE_PL : C::NSTORE_LDS) + (STO ? 8 : 0)));
-  static_assert(!OF32 || (OSPL ? 16 : 8) * NT + 5 <= 63, "vmcnt range");
+  static_assert(!OF32 || (OSPL ? 16 * ((NT + 1) / 2) : 8 * NT) + 5 <= 63, "vmcnt range");
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
 
   const int ntiles = tiles_m * tiles_n;
@@ -1119,7 +1123,92 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
         rb[i] = cf.y;
       }
     }
-    if constexpr (OF32) {
+    if constexpr (OF32 && NT == 3) {
+      // f32 output of the x3 split GEMM (NT = 3, every BERT / Swin / fusion x3 shape): staged per m-tile round
+      // through the m-group's LDS epilogue area so the stores are row-major — the group's 4 waves (one per
+      // n-column block of 48) write their 16 x 48 fragment values, one barrier, then wave wc stores rows
+      // 4 wc .. 4 wc + 3 of the round's 16 rows across the tile's 192 columns: an instruction covers ~1.3
+      // rows x 768 B of whole 128-B lines, where the fragment-layout stores (16 rows x 64 B per instruction)
+      // ran the store phase at a quarter of the write path and held up the next tile's first waits (vmcnt is
+      // in order): QKV 310 -> 159 us with no stores at all (profiles/r06_x3_epilogue_ab.txt).
+      // OSPL stages the hi and lo bf16 images the same way and stores 16-B chunks of either.  Two barriers per
+      // round (every wave runs the same 16); values and rounding exactly as the fragment-layout path.
+      constexpr int RS = 16 * NT * 4 + 4;       // f32 row stride of the group's staging image (196)
+      constexpr int RSH = 16 * NT * 4 + 8;      // bf16 row stride of an OSPL image (200)
+      static_assert(!OSPL ? 16 * RS * 4 <= 4 * 16 * C::RM * C::ELD * 2 : 2 * 16 * RSH * 2 <= 4 * 16 * C::RM * C::ELD * 2,
+                    "group staging image fits the group's epilogue areas");
+      float* grp = (float*)(dsm + 2 * BUF + (wr * 4) * 16 * C::RM * C::ELD);
+      uint16_t* grh = (uint16_t*)grp;          // OSPL: hi image [16][RSH], lo image behind it
+      uint16_t* grl = grh + 16 * RSH;
+      const int64_t tb = m0 * ldn * 4;
+      const uint32_t nrec = (uint32_t)(256 * ldn * 4);
+      const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)((char*)Y + tb), 0, (int)nrec, 0x00020000);
+      const auto rr = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)R + (HAS_RES ? tb : 0)), 0, (int)nrec,
+                                                        0x00020000);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {  // (unrolled: acc[i] must be a register, not an indexed array)
+        // (1) fragment layout -> the group image: bias, erf GELU (A-S erf, |err| <= 1.5e-7), OSPL's split
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          f32x4 v = acc[i][j] + bq[j];
+          if constexpr (ACT == 1) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = mmr::gelu_erf(v[e]);
+          }
+          const int cc = wc * 16 * NT + j * 16 + efq * 4;  // column in the tile
+          if constexpr (OSPL) {
+            // v pinned as the rounded f32 value: hipcc otherwise contracts the GELU's last multiply into
+            // v - hi (an fma), and lo would no longer be the split of the f32 output
+            mmr::pin(v);
+            const uint32_t h0 = mmr::pack2bf(v[0], v[1]), h1 = mmr::pack2bf(v[2], v[3]);
+            const uint32_t l0 = mmr::pack2bf(v[0] - __uint_as_float(h0 << 16), v[1] - __uint_as_float(h0 & 0xFFFF0000u));
+            const uint32_t l1 = mmr::pack2bf(v[2] - __uint_as_float(h1 << 16), v[3] - __uint_as_float(h1 & 0xFFFF0000u));
+            ds_write_b64_untracked(grh + efr * RSH + cc, h0, h1);
+            ds_write_b64_untracked(grl + efr * RSH + cc, l0, l1);
+          } else {
+            ds_write_b128_untracked(grp + efr * RS + cc, __builtin_bit_cast(uint4, v));
+          }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        barrier();
+        // (2) rows 4 wc .. 4 wc + 3 of the round, row-major 16-B chunks (3 per lane)
+        if constexpr (OSPL) {
+          // 4 rows x (24 hi + 24 lo) chunks of 8 bf16
+          uint4 ch[3];
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const int idx = c * 64 + le, part = idx / 96, k = idx % 96, r = k / 24, q = k % 24;
+            ch[c] = *(const uint4*)((part ? grl : grh) + (4 * wc + r) * RSH + 8 * q);
+          }
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const int idx = c * 64 + le, part = idx / 96, k = idx % 96, r = k / 24, q = k % 24;
+            uint16_t* ys = Y + (m0 + wr * 128 + i * 16 + 4 * wc + r) * 2 * (int64_t)N + (part ? N : 0) + n0 + 8 * q;
+            if (!skip_st) st16(ys, ch[c], false);
+            else asm volatile("" ::"v"(ch[c]));
+          }
+        } else {
+          f32x4 ov[3], rv[3];
+          uint32_t off[3];
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const int idx = c * 64 + le, r = idx / (16 * NT), q = idx % (16 * NT);  // 48 f32x4 chunks per row
+            const int rl = wr * 128 + i * 16 + 4 * wc + r, col = n0 + 4 * q;
+            off[c] = col < ldn ? (uint32_t)((rl * ldn + col) * 4) : 0x7FFFFFF0u;
+            if constexpr (HAS_RES) rv[c] = __builtin_amdgcn_raw_buffer_load_b128(rr, off[c], 0, 0);
+            ov[c] = *(const f32x4*)(grp + (4 * wc + r) * RS + 4 * q);
+          }
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            if constexpr (HAS_RES) ov[c] += rv[c];
+            if (!skip_st) __builtin_amdgcn_raw_buffer_store_b128(ov[c], ry, off[c], 0, 0);
+            else asm volatile("" ::"v"(ov[c]));
+          }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // the image is read before the next round overwrites it
+        barrier();
+      }
+    } else if constexpr (OF32) {
       // f32 output (the x3 towers' K' = 3K split GEMM): lane row 16 i + efr, columns 16 j + 4 efq .. + 3
       // -> one 16-B store per (i, j), no LDS round; bias, erf GELU (A-S erf, |err| <= 1.5e-7), then the f32 residual
       // (loaded per m-tile: they retire behind the next tile's prefetch, once per tile)
@@ -1146,6 +1235,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
 #pragma unroll
           for (int j = 0; j < NT; ++j) rr4[j] = __builtin_amdgcn_raw_buffer_load_b128(rr, off[j], 0, 0);
         }
+        uint2 ph[OSPL ? NT : 1], pl[OSPL ? NT : 1];  // OSPL: the hi / lo bf16 quads of each n-tile
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
           f32x4 v = acc[i][j] + bq[j];
@@ -1160,15 +1250,33 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
             // and lo would no longer be the split of the f32 output (bitwise tests against the f32 route)
             mmr::pin(v);
             const uint32_t h0 = mmr::pack2bf(v[0], v[1]), h1 = mmr::pack2bf(v[2], v[3]);
-            const uint32_t l0 = mmr::pack2bf(v[0] - __uint_as_float(h0 << 16), v[1] - __uint_as_float(h0 & 0xFFFF0000u));
-            const uint32_t l1 = mmr::pack2bf(v[2] - __uint_as_float(h1 << 16), v[3] - __uint_as_float(h1 & 0xFFFF0000u));
-            uint16_t* ys = Y + (m0 + rl) * 2 * (int64_t)N + n0 + wc * 16 * NT + j * 16 + efq * 4;
-            if (!skip_st) {
-              *(uint2*)ys = make_uint2(h0, h1);
-              *(uint2*)(ys + N) = make_uint2(l0, l1);
-            }
+            ph[j] = make_uint2(h0, h1);
+            pl[j] = make_uint2(mmr::pack2bf(v[0] - __uint_as_float(h0 << 16), v[1] - __uint_as_float(h0 & 0xFFFF0000u)),
+                               mmr::pack2bf(v[2] - __uint_as_float(h1 << 16), v[3] - __uint_as_float(h1 & 0xFFFF0000u)));
           } else if (!skip_st) {
-            __builtin_amdgcn_raw_buffer_store_b128(v, ry, off[j], 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(v, ry, off[j], 0, X3ST_AUX);
+          }
+        }
+        if constexpr (OSPL) {
+          // n-tile pairs (j, j + 1) through v_permlane16_swap as the GELU epilogue does (epi_pl): every lane
+          // then holds 8 consecutive columns, so hi and lo go out as one 16-B store each per pair — a row's
+          // 4 lanes write the pair's 64 contiguous bytes (8-B stores per tile wrote 32-B segments, twice the
+          // instructions); an odd last tile pairs with itself (lanes fq 0 / 1 and 2 / 3 write the same bytes)
+#pragma unroll
+          for (int j = 0; j < NT; j += 2) {
+            const int j2 = j + 1 < NT ? j + 1 : j;
+            const auto hx = __builtin_amdgcn_permlane16_swap(ph[j].x, ph[j2].x, false, false);
+            const auto hy = __builtin_amdgcn_permlane16_swap(ph[j].y, ph[j2].y, false, false);
+            const auto lx = __builtin_amdgcn_permlane16_swap(pl[j].x, pl[j2].x, false, false);
+            const auto ly = __builtin_amdgcn_permlane16_swap(pl[j].y, pl[j2].y, false, false);
+            const int col = n0 + wc * 16 * NT + 16 * j + (j2 != j && (efq & 1) ? 16 : 0) + (efq >> 1) * 8;
+            uint16_t* ys = Y + (m0 + rl) * 2 * (int64_t)N + col;
+            if (!skip_st) {
+              st16(ys, make_uint4(hx[0], hy[0], hx[1], hy[1]), X3ST_AUX != 0);
+              st16(ys + N, make_uint4(lx[0], ly[0], lx[1], ly[1]), X3ST_AUX != 0);
+            } else {
+              asm volatile("" ::"v"(hx[0]), "v"(hy[0]), "v"(lx[0]), "v"(ly[0]));
+            }
           }
         }
       }

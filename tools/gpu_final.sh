@@ -1,6 +1,7 @@
 #!/bin/bash
 # Session-end GPU pass: GPU tests, smoke, bench lines (cfg2 full + kNN, cfg3, cfg5), rocprofv3 kernel
-# stats of cfg2 (towers in sequence) and of the kNN leg, kNN PMC traffic.  Each GPU step has its own
+# stats of cfg2 (towers in sequence) and of the kNN leg, kNN PMC traffic; x3 counters / step table (pmcx3,
+# x3prof) and the roofline kernels' traffic (pmct).  Each GPU step has its own
 # time limit; the first failing step ends the script.
 # usage (via gpurun): bash tools/gpu_final.sh <tag> [steps...]
 set -e -o pipefail
@@ -46,6 +47,15 @@ for s in $STEPS; do
       timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc -o kwrite \
         -- python3 bench.py --sequential-towers --mode knn --steps 5 --warmup 1 --no-cpu-baseline > $OUT/pmc_kwrite.log 2>&1
       echo pmc ok ;;
+    pmcx3)  # x3 kernels' counters (tools/pmc_x3.py) -> gpurun_out/pmc_<tag>/pmc_x3.json
+      bash tools/gpu_pmc_x3.sh $TAG > $OUT/pmc_x3.log 2>&1 || { tail -5 $OUT/pmc_x3.log; exit 1; }
+      echo pmcx3 ok ;;
+    pmct)   # HBM traffic of the roofline kernels -> gpurun_out/pmc_r06/r06_pmc_traffic.json
+      bash tools/gpu_pmc_traffic.sh r06 > $OUT/pmc_traffic.log 2>&1 || { tail -5 $OUT/pmc_traffic.log; exit 1; }
+      echo pmct ok ;;
+    x3prof) # one sequential x3 cfg2 step, per-kernel table
+      bash tools/gpu_x3_prof.sh $TAG > $OUT/x3prof.log 2>&1 || { tail -5 $OUT/x3prof.log; exit 1; }
+      echo x3prof ok ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -1,7 +1,7 @@
 """x3 split GEMMs for whichever libmmr MMR_LIBMMR selects: the BERT FFN (fc1 + GELU writing split rows ->
 fc2, M = 32768, 768 -> 3072 -> 768), BERT QKV (N = 2304) and the Swin stage-3 fc1 + GELU (M = 50176,
 384 -> 1536), time per call (HIP events, min of 3 x 10) and a checksum.  Run once per library,
-interleaved, for a same-box A/B.  Diagnostic only."""
+interleaved, for a same-box A/B.  Diagnostic only.  usage: python tools/x3_gemm_ab.py <tag> [M]"""
 import os
 import sys
 
@@ -25,7 +25,7 @@ def timeit(fn, it=10):
 
 tag = sys.argv[1] if len(sys.argv) > 1 else os.path.basename(os.environ.get("MMR_LIBMMR", "libmmr.so"))
 g = torch.Generator().manual_seed(4)
-M, C, F4 = 32768, 768, 3072
+M, C, F4 = (int(sys.argv[2]) if len(sys.argv) > 2 else 32768), 768, 3072
 x = torch.randn(M, C, generator=g).cuda()
 gm, bt = torch.ones(C).cuda(), torch.zeros(C).cuda()
 w1, b1 = ops.X3W((torch.randn(F4, C, generator=g) * C ** -0.5).cuda()), (0.1 * torch.randn(F4, generator=g)).cuda()
