@@ -1185,7 +1185,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tn_p8(const uint16_t* __restric
             const int idx = c * 64 + le, part = idx / 96, k = idx % 96, r = k / 24, q = k % 24;
             uint16_t* ys = Y + (m0 + wr * 128 + i * 16 + 4 * wc + r) * 2 * (int64_t)N + (part ? N : 0) + n0 + 8 * q;
             if (!skip_st) st16(ys, ch[c], false);
-            else asm volatile("" ::"v"(ch[c]));
+            else asm volatile("" ::"v"(ch[c].x), "v"(ch[c].y), "v"(ch[c].z), "v"(ch[c].w));
           }
         } else {
           f32x4 ov[3], rv[3];
