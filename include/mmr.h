@@ -208,8 +208,10 @@ int32_t mmr_linear_bf16_n_variants(void);
  *   MMR_PIN_GEMM_BF16: value = mmr_linear_bf16 variant index, or -1 = per-shape tuning (default);
  *   MMR_PIN_X3_WAVES:  value = 4 or 8 waves per mmr_linear_x3 tile (8 only where K % 256 == 0),
  *                      or -1 = automatic (default).
+ *   MMR_PIN_X3_MLP:    value = 0 (8-wave workgroups) or 1 (4-wave workgroups, two per CU) for
+ *                      mmr_x3_swin_mlp at C = 96, or -1 = automatic (1).  Both give bit-identical outputs.
  * MMR_ERR_INVALID for an unknown pin or value. */
-enum { MMR_PIN_GEMM_BF16 = 0, MMR_PIN_X3_WAVES = 1 };
+enum { MMR_PIN_GEMM_BF16 = 0, MMR_PIN_X3_WAVES = 1, MMR_PIN_X3_MLP = 2 };
 mmr_status mmr_pin_variant(int32_t which, int32_t value);
 
 /* Resident-weight streaming linear for the short-K, narrow tower linears (Swin patch embed, stage-2

@@ -19,6 +19,7 @@ void set_error(const char* fmt, ...) {
 void clear_error() { g_err[0] = 0; }
 std::atomic<int> pin_gemm_bf16{-1};
 std::atomic<int> pin_x3_waves{-1};
+std::atomic<int> pin_x3_mlp{-1};
 }  // namespace mmr
 
 extern "C" {
@@ -38,6 +39,12 @@ mmr_status mmr_pin_variant(int32_t which, int32_t value) {
     mmr::pin_x3_waves.store(value);
     return MMR_OK;
   }
+  if (which == MMR_PIN_X3_MLP) {
+    MMR_REQUIRE(value >= -1 && value <= 1, "mmr_pin_variant: x3 mlp form %d (-1, 0, 1)", value);
+    mmr::pin_x3_mlp.store(value);
+    return MMR_OK;
+  }
+
   mmr::set_error("mmr_pin_variant: unknown pin %d", which);
   return MMR_ERR_INVALID;
 }

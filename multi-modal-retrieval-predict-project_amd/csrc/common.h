@@ -15,6 +15,7 @@ void clear_error();
 // process-wide launch-variant pins (mmr_pin_variant; -1 = the launcher's own choice)
 extern std::atomic<int> pin_gemm_bf16;
 extern std::atomic<int> pin_x3_waves;
+extern std::atomic<int> pin_x3_mlp;
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -623,7 +623,14 @@ mmr_status mmr_x3_swin_mlp(const float* x, const float* ln_g, const float* ln_b,
               "mmr_x3_swin_mlp: x / y / b2 must be 16-B aligned");
   if (tokens == 0) return MMR_OK;
   hipStream_t st = mmr::as_stream(stream);
-  if (c == 96) return launch_x3_mlp<96, 8, X3MLP_HC, 3>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
+  if (c == 96) {
+    // 4-wave workgroups, two per CU (their chunk barriers and prologue / epilogue latencies independent):
+    // 491 vs 516 us for the 8-wave one at stage 1, B = 256 (profiles/r06_x3_mlp_walk_ab.txt); a test / A-B
+    // pins the 8-wave form through mmr_pin_variant
+    if (mmr::pin_x3_mlp.load(std::memory_order_relaxed) == 0)
+      return launch_x3_mlp<96, 8, X3MLP_HC, 3>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
+    return launch_x3_mlp<96, 4, X3MLP_HC, 3>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
+  }
   if (c == 192) return launch_x3_mlp<192, 8, X3MLP_HC, 2>(x, ln_g, ln_b, pack, b1, b2, y, tokens, eps, st);
   mmr::set_error("mmr_x3_swin_mlp: C=%d not built (96, 192)", c);
   return MMR_ERR_UNSUPPORTED;

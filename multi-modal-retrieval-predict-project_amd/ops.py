@@ -38,13 +38,14 @@ def _chk(status, what):
     _lib.check(status, what)
 
 
-PIN_GEMM_BF16, PIN_X3_WAVES = 0, 1  # mmr.h MMR_PIN_*
+PIN_GEMM_BF16, PIN_X3_WAVES, PIN_X3_MLP = 0, 1, 2  # mmr.h MMR_PIN_*
 
 
 @contextlib.contextmanager
 def pinned(which, value):
     """Pin a launch variant for the duration (mmr_pin_variant: tests and A/B tools only; the product
-    path never pins).  PIN_GEMM_BF16: mmr_linear_bf16 variant index; PIN_X3_WAVES: 4 / 8."""
+    path never pins).  PIN_GEMM_BF16: mmr_linear_bf16 variant index; PIN_X3_WAVES: 4 / 8; PIN_X3_MLP: 0 / 1
+    (8-wave / 4-wave workgroups of the x3 Swin MLP at C = 96)."""
     _chk(_L().mmr_pin_variant(which, value), "mmr_pin_variant")
     try:
         yield

@@ -154,6 +154,29 @@ def test_x3_swin_mlp_vs_f64(T, C):
     assert _rel(y, y_chain) < 1e-5
 
 
+@pytest.mark.parametrize("T", [4096, 1000, 33])
+def test_x3_swin_mlp_workgroup_forms_bit_identical(T):
+    """The C = 96 MLP's 4-wave workgroups (the default) and 8-wave ones run the same per-token products in the
+    same order: bit-identical outputs, ragged token counts (partial last workgroup)."""
+    C = 96
+    g_ = torch.Generator().manual_seed(T + 7)
+    x = (torch.randn(T, C, generator=g_) * 1.5 + 0.3).to(DEV)
+    gm = (1 + 0.1 * torch.randn(C, generator=g_)).to(DEV)
+    bt = (0.1 * torch.randn(C, generator=g_)).to(DEV)
+    w1 = (torch.randn(4 * C, C, generator=g_) * C ** -0.5).to(DEV)
+    b1 = (0.1 * torch.randn(4 * C, generator=g_)).to(DEV)
+    w2 = (torch.randn(C, 4 * C, generator=g_) * (4 * C) ** -0.5).to(DEV)
+    b2 = (0.1 * torch.randn(C, generator=g_)).to(DEV)
+    pack = ops.x3_swin_mlp_pack(w1, w2)
+    with ops.pinned(ops.PIN_X3_MLP, 0):
+        y0 = ops.x3_swin_mlp(x, gm, bt, pack, b1, b2, 1e-5)
+    with ops.pinned(ops.PIN_X3_MLP, 1):
+        y1 = ops.x3_swin_mlp(x, gm, bt, pack, b1, b2, 1e-5)
+    y = ops.x3_swin_mlp(x, gm, bt, pack, b1, b2, 1e-5)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1) and torch.equal(y, y1)
+
+
 @pytest.mark.parametrize("T,C,N,mode", [(4096, 96, 288, "ln"), (1000, 96, 96, "xs"), (2048, 192, 576, "ln"),
                                          (300, 192, 192, "xs"), (512, 96, 96, "ln_res")])
 def test_x3_rowlin_vs_f64(T, C, N, mode):
