@@ -79,6 +79,21 @@ __device__ __forceinline__ uint32_t pack2bf(float a, float b) {
   return __builtin_bit_cast(uint32_t, v);
 }
 
+// e^x for the x3 softmax (x = s - max <= 0; -inf is the caller's case): 2^t with t = RN(x log2 e) and t's
+// rounding error carried to first order, 2^t (1 + ln 2 (fma(x, L2E, -t) + x L2E_lo)) — one v_exp_f32
+// (1 ulp) and four FMA-class ops, <= ~2 ulp, against ocml expf's ~14 VALU (range reduction by rndne /
+// ldexp and overflow / underflow selects the softmax never needs); results below 2^-126 may flush to 0.
+// x is clamped at -104 (e^-104 is below the smallest f32 denormal): a masked score (HF's -FLT_MAX) would
+// otherwise overflow x log2 e to -inf and turn the correction into inf * 0
+__device__ __forceinline__ float exp_acc(float x) {
+  constexpr float L2E = 1.44269504088896341f, L2E_LO = 1.925962991e-08f;  // log2 e = L2E + L2E_LO
+  x = fmaxf(x, -104.0f);
+  const float t = x * L2E;
+  const float c = fmaf(x, L2E_LO, fmaf(x, L2E, -t));
+  const float e = __builtin_amdgcn_exp2f(t);
+  return fmaf(e, c * 0.69314718055994531f, e);
+}
+
 // GELU(erf) with erf from Abramowitz-Stegun 7.1.26 (|err| <= 1.5e-7): branch-free, one exp + one
 // rcp instead of ocml's erff.
 __device__ __forceinline__ float erf_as(float x) {

@@ -3,7 +3,8 @@
 // attention products) on bf16 MFMA with three-term splits: a = a_hi + a_lo (a_hi = bf16(a),
 // a_lo = bf16(a - a_hi), |a - a_hi - a_lo| <= 2^-18 |a|), a.b ~= a_hi.b_hi + a_hi.b_lo + a_lo.b_hi
 // summed in f32 (~2^-17 relative per product, f32 accumulation).  Everything else — LayerNorm,
-// softmax (expf), GELU (erff), means — runs in f32 as torch does.  The reference runs these towers
+// softmax, GELU, means — runs in f32 as torch does (the softmax's exp by mmr::exp_acc and the GELU's erf
+// by Abramowitz-Stegun 7.1.26: a few f32 ulp, far below the products' 2^-17).  The reference runs these towers
 // in fp32 (src/Model/fusion.py:198-199 timm forward_features, :322-325 BertModel, model.py:365-479
 // heads); this mode exists so the end-to-end lists can be held to BASELINE.md §3's bar (identical
 // top-K up to 1e-6 ties, scores within 1e-4, identical P@10) — the bf16 / MX-fp8 tower modes move
@@ -16,7 +17,7 @@
 //                  register-prefetched next K-step, XCD-contiguous tile order.
 //   x3_attention   per (sequence or window, head): softmax(q k^T * scale + bias / mask) v, keys in
 //                  LDS chunks of 64 (hi / lo K rows, hi / lo V^T), online softmax (running max and
-//                  sum per query row, expf), P re-split through a wave-private LDS tile; optional
+//                  sum per query row, f32 exp), P re-split through a wave-private LDS tile; optional
 //                  mean over the query rows (fixed-order reduction, deterministic).  Modes: strided
 //                  rows (nn.MultiheadAttention, BERT with a key-padding mask) and Swin windows (the
 //                  roll + window partition / reverse folded into the token index map, the dense
@@ -183,7 +184,7 @@ struct AttnArgs {
 // head); nwv = min(4, ceil(lq / 32)) waves, one 32-query tile per wave, the block walking its query
 // chunks of 32 nwv rows (one chunk up to lq = 128; the mean then reduces in a fixed order inside the
 // block).  S^T = K . Q^T on v_mfma_f32_32x32x16_bf16 as Kh.Qh + Kh.Ql + Kl.Qh puts the query on the
-// lane: the softmax (f32, expf, online over 64-key sub-blocks of kbs-key staged blocks) stays in
+// lane: the softmax (f32, mmr::exp_acc, online over 64-key sub-blocks of kbs-key staged blocks) stays in
 // registers, and P^T is split in registers into the B operands of O^T += V^T . P^T (Vh.Ph + Vh.Pl +
 // Vl.Ph), V^T read from key-major hi / lo images by ds_read_b64_tr_b16 in P^T's key permutation.
 // K / V f32 rows are split ONCE per block while staged (16-B LDS writes), Q once per wave in registers.
@@ -405,7 +406,7 @@ __global__ __launch_bounds__(256, DT <= 2 ? 3 : 2) void x3_mha(const AttnArgs a,
         }
         mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
         const float m_new = fmaxf(m_run, mloc);
-        const float alpha = m_run == -INFINITY ? 0.f : expf(m_run - m_new);
+        const float alpha = m_run == -INFINITY ? 0.f : mmr::exp_acc(m_run - m_new);
         m_run = m_new;
         float psum = 0.f;
 #pragma unroll
@@ -414,7 +415,7 @@ __global__ __launch_bounds__(256, DT <= 2 ? 3 : 2) void x3_mha(const AttnArgs a,
 #pragma unroll
           for (int rg = 0; rg < 16; ++rg) {
             const float x = s[t][rg];
-            const float p = (x == -INFINITY || m_new == -INFINITY) ? 0.f : expf(x - m_new);
+            const float p = (x == -INFINITY || m_new == -INFINITY) ? 0.f : mmr::exp_acc(x - m_new);
             s[t][rg] = p;
             psum += p;
           }
