@@ -586,6 +586,19 @@ mmr_status mmr_x3_rowlin(const float* x, const uint16_t* xs, const float* ln_g, 
                          const float* bias, const float* residual, float* y, int64_t tokens, int32_t n, int32_t c,
                          float eps, void* stream);
 mmr_status mmr_x3_swin_mlp_pack(const float* w1, const float* w2, uint16_t* pack, int32_t c, void* stream);
+/* fp32-faithful fused Swin attention sub-block for C = 96 (3 heads of 32, window 7; Swin-T stage 1,
+ * csrc/x3_sab.hip): y = x + proj(W-MSA(LayerNorm1(x))) with torch.roll shift, window partition / reverse,
+ * relative-position bias and shift mask (timm SwinTransformerBlock, fusion.py:198-199) in f32, every
+ * contraction on bf16x3 MFMA — the x3_rowlin (norm1 + qkv) -> x3 window attention -> x3_rowlin (proj +
+ * residual) chain in one pass.  x, y f32 (b, hw, hw, 96) (x != y, 16-B aligned); `bias` = the block's dense
+ * table from mmr_swin_attn_bias; `pack` = mmr_x3_swin_attn_block_pack_bytes(96) bytes built once from the
+ * f32 attn.qkv.weight [288][96] / .bias, attn.proj.weight [96][96] / .bias and norm1.weight / .bias
+ * (0 bytes / MMR_ERR_UNSUPPORTED for other c). */
+int64_t mmr_x3_swin_attn_block_pack_bytes(int32_t c);
+mmr_status mmr_x3_swin_attn_block_pack(const float* qkv_w, const float* qkv_b, const float* proj_w, const float* proj_b,
+                                       const float* ln_g, const float* ln_b, void* pack, int32_t c, void* stream);
+mmr_status mmr_x3_swin_attn_block(const float* x, const void* pack, const float* bias, float* y, int32_t b, int32_t hw,
+                                  int32_t c, int32_t ws, int32_t shift, float eps, void* stream);
 mmr_status mmr_x3_swin_mlp(const float* x, const float* ln_g, const float* ln_b, const uint16_t* pack, const float* b1,
                            const float* b2, float* y, int64_t tokens, int32_t c, float eps, void* stream);
 /* fp32-faithful Swin stem (csrc/x3_mlp.hip): y (b, hw/4, hw/4, 96) f32 = LayerNorm(Conv2d(3, 96, 4, stride 4)

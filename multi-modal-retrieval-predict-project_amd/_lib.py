@@ -115,6 +115,9 @@ SIGNATURES = {
     "mmr_x3_rowlin_pack": [c_vp, c_vp, c_i32, c_i32, c_vp],
     "mmr_x3_rowlin": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_f32, c_vp],
     "mmr_x3_swin_mlp_pack": [c_vp, c_vp, c_vp, c_i32, c_vp],
+    "mmr_x3_swin_attn_block_pack_bytes": [c_i32],
+    "mmr_x3_swin_attn_block_pack": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp],
+    "mmr_x3_swin_attn_block": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_f32, c_vp],
     "mmr_x3_swin_mlp": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp],
     "mmr_x3_assemble_seq": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
     "mmr_x3_assemble_seq_split": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
@@ -131,7 +134,8 @@ _RESTYPES = {"mmr_last_error": ctypes.c_char_p, "mmr_version": ctypes.c_int, "mm
              "mmr_linear_rw_parts": ctypes.c_int32,
              "mmr_swin_mlp_pack_elems": ctypes.c_int64, "mmr_swin_attn_block_pack_bytes": ctypes.c_int64,
              "mmr_x3_swin_mlp_pack_elems": ctypes.c_int64, "mmr_x3_rowlin_pack_elems": ctypes.c_int64,
-             "mmr_x3_patch_embed_pack_elems": ctypes.c_int64}
+             "mmr_x3_patch_embed_pack_elems": ctypes.c_int64,
+             "mmr_x3_swin_attn_block_pack_bytes": ctypes.c_int64}
 
 _lib = None
 

@@ -822,6 +822,32 @@ def x3_rowlin(x, pack, bias, n, ln=None, residual=None):
     return y
 
 
+def x3_swin_attn_block_pack(qkv_w, qkv_b, proj_w, proj_b, ln_g, ln_b):
+    """f32 weights of one Swin block's attention half (attn.qkv [3C][C] / .bias, attn.proj [C][C] / .bias,
+    norm1) -> the LDS image of mmr_x3_swin_attn_block, or None if C is not a fused width (96)."""
+    C = qkv_w.shape[1]
+    n = _L().mmr_x3_swin_attn_block_pack_bytes(C)
+    if n <= 0:
+        return None
+    pack = torch.empty((n,), dtype=torch.uint8, device=qkv_w.device)
+    args = [t.contiguous().float() for t in (qkv_w, qkv_b, proj_w, proj_b, ln_g, ln_b)]
+    _chk(_L().mmr_x3_swin_attn_block_pack(*(_lib.ptr(t) for t in args), _lib.ptr(pack), C, _s(qkv_w)),
+         "mmr_x3_swin_attn_block_pack")
+    return pack
+
+
+def x3_swin_attn_block(x, pack, bias, ws, shift, eps):
+    """x + proj(W-MSA(LN1(x))) for f32 x (B, H, H, C), fused in one pass (C = 96): the x3_rowlin (norm1 +
+    qkv) -> x3 window attention -> x3_rowlin (proj + residual) chain."""
+    _lib.require_gpu(x)
+    B, H, _, C = x.shape
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    _chk(_L().mmr_x3_swin_attn_block(_lib.ptr(x), _lib.ptr(pack), _lib.ptr(bias), _lib.ptr(y), B, H, C, ws, shift,
+                                     float(eps), _s(x)), "mmr_x3_swin_attn_block")
+    return y
+
+
 def x3_attention(q, k, v, b, lq, lk, heads, dh, scale, out=None, mean_out=None, mask=None):
     """f32 attention core over strided row views (mmr_x3_attention); mask (b, lk) int64 or None."""
     _lib.require_gpu(q)

@@ -87,11 +87,16 @@ class SwinTowerX3:
                 b_["mlp_pack"] = ops.x3_swin_mlp_pack(b_["fc1_w"].w, b_["fc2_w"].w)
                 b_["qkv_pack"] = ops.x3_rowlin_pack(b_["qkv_w"].w)
                 b_["proj_pack"] = ops.x3_rowlin_pack(b_["proj_w"].w)
+                # C = 96 (stage 1): norm1 + qkv + window attention + proj + residual in one pass
+                b_["sab_pack"] = (ops.x3_swin_attn_block_pack(b_["qkv_w"].w, b_["qkv_b"], b_["proj_w"].w,
+                                                              b_["proj_b"], b_["n1g"], b_["n1b"])
+                                  if ws == 7 and res % 7 == 0 else None)
             self.stages.append(st)
         self.norm_g, self.norm_b = _f(sd["norm.weight"], dev), _f(sd["norm.bias"], dev)
         self.num_features = E * 2 ** (len(self.cfg["depths"]) - 1)
         self.fused_mlp = True      # the fused x3 MLP where built (A/B attribute)
         self.fused_linears = True  # the streamed x3 row-linears (norm1 + qkv, proj) where built (A/B attribute)
+        self.fused_attn = True     # the fused x3 attention half (C = 96) where built (A/B attribute)
 
     def tokens(self, image):
         """(B,3,H,W) f32 -> (B, h, w, C) f32 tokens BEFORE the final norm."""
@@ -113,24 +118,30 @@ class SwinTowerX3:
             heads = cfg["num_heads"][i]
             ws = min(cfg["window_size"], H)
             for bk in st["blocks"]:
-                C = x.shape[-1]
-                rowlin = self.fused_linears and bk["qkv_pack"] is not None
-                if rowlin:
-                    qkv = ops.x3_rowlin(x, bk["qkv_pack"], bk["qkv_b"], 3 * C, ln=(bk["n1g"], bk["n1b"], 1e-5))
-                else:
-                    h = ops.x3_ln_split(x, bk["n1g"], bk["n1b"], 1e-5)
-                    qkv = ops.x3_linear(h, bk["qkv_w"], bk["qkv_b"])
-                a = ops.x3_swin_window_attention_split(qkv, bk["bias"], H, heads, ws, bk["shift"])
-                if rowlin and bk["proj_pack"] is not None and isinstance(a, ops.X3Rows):
-                    x = ops.x3_rowlin(a, bk["proj_pack"], bk["proj_b"], C, residual=x)
-                else:
-                    x = ops.x3_linear(a, bk["proj_w"], bk["proj_b"], residual=x)
+                x = self._attn_half(x, bk, H, heads, ws)
                 if self.fused_mlp and bk["mlp_pack"] is not None:
                     x = ops.x3_swin_mlp(x, bk["n2g"], bk["n2b"], bk["mlp_pack"], bk["fc1_b"], bk["fc2_b"], 1e-5)
                 else:
                     h = ops.x3_ln_split(x, bk["n2g"], bk["n2b"], 1e-5)
                     x = ops.x3_ffn(h, bk["fc1_w"], bk["fc1_b"], bk["fc2_w"], bk["fc2_b"], residual=x)
         return x
+
+    def _attn_half(self, x, bk, H, heads, ws):
+        """x + proj(W-MSA(norm1(x))) of one block: fused in one pass at C = 96 (x3_swin_attn_block), else
+        the streamed row-linears around the window attention (split rows in between), else split GEMMs."""
+        C = x.shape[-1]
+        if self.fused_attn and bk["sab_pack"] is not None and ws == 7:
+            return ops.x3_swin_attn_block(x, bk["sab_pack"], bk["bias"], ws, bk["shift"], 1e-5)
+        rowlin = self.fused_linears and bk["qkv_pack"] is not None
+        if rowlin:
+            qkv = ops.x3_rowlin(x, bk["qkv_pack"], bk["qkv_b"], 3 * C, ln=(bk["n1g"], bk["n1b"], 1e-5))
+        else:
+            h = ops.x3_ln_split(x, bk["n1g"], bk["n1b"], 1e-5)
+            qkv = ops.x3_linear(h, bk["qkv_w"], bk["qkv_b"])
+        a = ops.x3_swin_window_attention_split(qkv, bk["bias"], H, heads, ws, bk["shift"])
+        if rowlin and bk["proj_pack"] is not None and isinstance(a, ops.X3Rows):
+            return ops.x3_rowlin(a, bk["proj_pack"], bk["proj_b"], C, residual=x)
+        return ops.x3_linear(a, bk["proj_w"], bk["proj_b"], residual=x)
 
     def forward_features(self, image):
         return _ln(self.tokens(image), self.norm_g, self.norm_b, 1e-5)

@@ -413,6 +413,68 @@ def test_x3_swin_window_attention_vs_f64(hw, c, heads, shift):
     assert _rel(out, o) <= 5e-5
 
 
+def _swin_attn_half_f64(x, g, b, wqkv, bqkv, wp, bp, table, heads, ws, shift, eps=1e-5):
+    """x + proj(W-MSA(LN1(x))) (timm SwinTransformerBlock's attention half) in f64, oracle helpers."""
+    x = x.double()
+    B, hw, _, c = x.shape
+    dh, N = c // heads, ws * ws
+    h = F.layer_norm(x, (c,), g.double(), b.double(), eps)
+    qkv = h @ wqkv.double().T + bqkv.double()
+    if shift:
+        qkv = torch.roll(qkv, shifts=(-shift, -shift), dims=(1, 2))
+    win = otw.window_partition(qkv, ws).view(-1, N, 3, heads, dh).permute(2, 0, 3, 1, 4)
+    q, k, v = win[0] * dh ** -0.5, win[1], win[2]
+    a = q @ k.transpose(-2, -1)
+    a = a + table.double()[otw.relative_position_index(ws).view(-1)].view(N, N, heads).permute(2, 0, 1)[None]
+    if shift:
+        msk = otw.shift_mask(hw, hw, ws, shift).double()
+        nW = msk.shape[0]
+        a = (a.view(-1, nW, heads, N, N) + msk[None, :, None]).view(-1, heads, N, N)
+    o = (a.softmax(-1) @ v).transpose(1, 2).reshape(-1, ws, ws, c)
+    o = otw.window_reverse(o, ws, hw, hw)
+    if shift:
+        o = torch.roll(o, shifts=(shift, shift), dims=(1, 2))
+    return x + o @ wp.double().T + bp.double()
+
+
+@pytest.mark.parametrize("B,shift", [(4, 0), (4, 3), (1, 3), (3, 0)])
+def test_x3_swin_attn_block_vs_chain_and_f64(B, shift):
+    """The fused stage-1 attention half (mmr_x3_swin_attn_block, C = 96) against the unfused x3 chain it
+    replaces (x3_rowlin norm1 + qkv -> window attention -> x3_rowlin proj + residual: same products,
+    another kernel's summation order) and against f64 (timm's attention half restated)."""
+    c, heads, ws, hw = 96, 3, 7, 56
+    gen = torch.Generator().manual_seed(100 + B + shift)
+    x = torch.randn(B, hw, hw, c, generator=gen)
+    lg, lb = 1 + 0.1 * torch.randn(c, generator=gen), 0.1 * torch.randn(c, generator=gen)
+    wqkv, bqkv = torch.randn(3 * c, c, generator=gen) * c ** -0.5, 0.1 * torch.randn(3 * c, generator=gen)
+    wp, bp = torch.randn(c, c, generator=gen) * c ** -0.5, 0.1 * torch.randn(c, generator=gen)
+    table = torch.randn((2 * ws - 1) ** 2, heads, generator=gen) * 0.5
+    d = [t.to(DEV) for t in (x, lg, lb, wqkv, bqkv, wp, bp)]
+    xd, lgd, lbd, wqd, bqd, wpd, bpd = d
+    bias = ops.swin_attn_bias(table.to(DEV), heads, ws, hw, shift)
+    pack = ops.x3_swin_attn_block_pack(wqd, bqd, wpd, bpd, lgd, lbd)
+    assert pack is not None
+    y = ops.x3_swin_attn_block(xd, pack, bias, ws, shift, 1e-5)
+    assert y.shape == x.shape and torch.isfinite(y).all()
+    ref = _swin_attn_half_f64(x, lg, lb, wqkv, bqkv, wp, bp, table, heads, ws, shift)
+    err = _rel(y, ref)
+    if B * hw * hw % 256 == 0:
+        qkv = ops.x3_rowlin(xd, ops.x3_rowlin_pack(wqd), bqd, 3 * c, ln=(lgd, lbd, 1e-5))
+        a = ops.x3_swin_window_attention_split(qkv, bias, hw, heads, ws, shift)
+        chain = ops.x3_rowlin(a, ops.x3_rowlin_pack(wpd), bpd, c, residual=xd)
+        dc = _rel(y, chain)
+        print(json.dumps({"B": B, "shift": shift, "vs_f64": err, "vs_chain": dc, "chain_vs_f64": _rel(chain, ref)}))
+        assert dc <= 1e-5  # both ~4e-6 from f64 (the products' 2^-17 bound), in different orders
+    assert err <= 1e-5
+
+
+def test_x3_swin_attn_block_rejects():
+    """Unbuilt widths / windows are refused with MMR_ERR_UNSUPPORTED (pack: 0 bytes, None from ops)."""
+    assert _lib.lib().mmr_x3_swin_attn_block_pack_bytes(192) == 0
+    w = torch.zeros(3 * 192, 192, device=DEV)
+    assert ops.x3_swin_attn_block_pack(w, w[0], w[:192], w[0, :192], w[0, :192], w[0, :192]) is None
+
+
 def _split_bits(y, kp):
     """[hi | lo] rows (int16 view) of f32 rows y (rows, c), zero columns c..kp: mmr_x3_split_rows' split."""
     c = y.shape[-1]

@@ -7,7 +7,7 @@ import sys
 src = sys.argv[1]
 flt = sys.argv[2] if len(sys.argv) > 2 else ""
 out = subprocess.run(["/opt/rocm/bin/hipcc", "-x", "hip", "--offload-arch=gfx950", "-O3", "-std=c++17",
-                      "-I/root/repo/include", "-c", src, "-o", "/dev/null",
+                      "-I/root/repo/include", "-I/root/repo/multi-modal-retrieval-predict-project_amd/csrc", "-c", src, "-o", "/dev/null",
                       "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True).stderr
 cur = None
 rows = {}
