@@ -232,6 +232,16 @@ __global__ __launch_bounds__(S_NWV * 64, 1) void x3_swin_attn_block(const float*
       // token tiles, and Q^T (scaled) of both query tiles, as hi / lo fragments; biases start the
       // accumulators
       bf16x8 kfh[2][2], kfl[2][2], vfh[2][2], vfl[2][2], qfh[2][2], qfl[2][2];
+      // the score accumulators start at the bias rows (L2): query tile 0's loaded before the QKV products,
+      // tile 1's before tile 0's scores, so neither round trip is waited for at the scores
+      f32x4 bq[2][2][4];
+      auto load_bias = [&](int qt) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) bq[qt][kt][i] = *(const f32x4*)(bt + (32 * qt + r) * 64 + 32 * kt + 8 * i + 4 * h);
+      };
+      load_bias(0);
 #pragma unroll
       for (int t2 = 0; t2 < 2; ++t2) {
         f32x16 ak, aq;
@@ -268,15 +278,14 @@ __global__ __launch_bounds__(S_NWV * 64, 1) void x3_swin_attn_block(const float*
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
         // S^T[key][query] = K (scale Q)^T + bias (the rel-pos / mask rows start the accumulator)
+        if (qt == 0) load_bias(1);
         f32x16 s[2];
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const f32x4 b4 = *(const f32x4*)(bt + (32 * qt + r) * 64 + 32 * kt + 8 * i + 4 * h);
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) s[kt][4 * i + rr] = b4[rr];
-          }
+            for (int rr = 0; rr < 4; ++rr) s[kt][4 * i + rr] = bq[qt][kt][i][rr];
 #pragma unroll
           for (int k2 = 0; k2 < 2; ++k2) s[kt] = mfma3(kfh[kt][k2], kfl[kt][k2], qfh[qt][k2], qfl[qt][k2], s[kt]);
         }
@@ -318,7 +327,6 @@ __global__ __launch_bounds__(S_NWV * 64, 1) void x3_swin_attn_block(const float*
 #pragma unroll
           for (int u = 0; u < SC / 32; ++u) {
             acc[qt][u] = mfma3(wfrag(Wph, u, 2 * hd + k2), wfrag(Wpl, u, 2 * hd + k2), oh, ol, acc[qt][u]);
-            __builtin_amdgcn_sched_barrier(0);
           }
         }
       }

@@ -23,6 +23,8 @@ PLAN = [
     ("bert_mha", "x3_mha<2, 1", 1, ("mfma", 3 * 2 * 2 * 256 * H * 128 * 128 * 64)),
     ("swin1_attn", "x3_mha<1, 2", 1, ("mfma", 3 * 2 * 2 * 256 * 64 * 3 * 49 * 49 * 32)),
     ("swin1_mlp", "x3_swin_mlp<96", 1, ("mfma", 3 * 2 * 2 * 256 * 3136 * 96 * 384)),
+    # the fused stage-1 attention half: 576 v_mfma_f32_32x32x16_bf16 per 64-token (padded) window
+    ("swin1_attn_block", "x3_swin_attn_block", 1, ("mfma", 576 * 32768 * 256 * 64)),
 ]
 
 
@@ -58,6 +60,9 @@ def main():
     sw2 = (torch.randn(c1, 4 * c1, generator=g) * 0.02).to(dev)
     sb1, sb2 = (0.02 * torch.randn(4 * c1, generator=g)).to(dev), (0.02 * torch.randn(c1, generator=g)).to(dev)
     pack = ops.x3_swin_mlp_pack(sw1, sw2)
+    swq, sbq = (torch.randn(3 * c1, c1, generator=g) * c1 ** -0.5).to(dev), (0.1 * torch.randn(3 * c1, generator=g)).to(dev)
+    swp, sbp = (torch.randn(c1, c1, generator=g) * c1 ** -0.5).to(dev), (0.1 * torch.randn(c1, generator=g)).to(dev)
+    sab = ops.x3_swin_attn_block_pack(swq, sbq, swp, sbp, sg, sb)
     torch.cuda.synchronize()
 
     def ffn1():
@@ -74,6 +79,7 @@ def main():
                                                    0.125, mask=mask),
         "swin1_attn": lambda: ops.x3_swin_window_attention_split(sqkv, sbias, hw, h1, 7, 3),
         "swin1_mlp": lambda: ops.x3_swin_mlp(st, sg, sb, pack, sb1, sb2, 1e-5),
+        "swin1_attn_block": lambda: ops.x3_swin_attn_block(st, sab, sbias, 7, 3, 1e-5),
     }
     for name, _, _, _ in PLAN:  # warm (variant tuners, weight images) outside the labelled dispatches
         ops_[name]()

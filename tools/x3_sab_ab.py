@@ -2,7 +2,7 @@
 x3 chain it replaces (x3_rowlin norm1 + qkv -> x3 window attention, split rows -> x3_rowlin proj + residual) at
 the Swin-T stage-1 shape (B = 256, 56 x 56 x 96), shift 0 and 3, HIP events over several launches, alternated
 over rounds on one box; prints the max relative difference of the two outputs.  Diagnostic only.
-usage: python tools/x3_sab_ab.py [B] [rounds]"""
+usage: python tools/x3_sab_ab.py [B] [rounds] [fused]  (fused: time the fused block only)"""
 import json
 import os
 import sys
@@ -29,6 +29,7 @@ def timeit(fn, iters=10):
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    fused_only = len(sys.argv) > 3 and sys.argv[3] == "fused"
     c, heads, ws, hw = 96, 3, 7, 56
     g = torch.Generator().manual_seed(7)
     dev = "cuda"
@@ -54,7 +55,8 @@ def main():
         diff = ((yc - yf).abs().max() / yc.abs().max()).item()
         tc, tf = [], []
         for _ in range(rounds):
-            tc.append(timeit(chain))
+            if not fused_only:
+                tc.append(timeit(chain))
             tf.append(timeit(fused))
         print(json.dumps({"B": B, "shift": shift, "chain_us": [round(t, 1) for t in tc],
                           "fused_us": [round(t, 1) for t in tf], "max_rel_diff": diff}), flush=True)
