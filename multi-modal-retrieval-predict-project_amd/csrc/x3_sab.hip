@@ -331,8 +331,12 @@ __global__ __launch_bounds__(S_NWV * 64, 1) void x3_swin_attn_block(const float*
         }
       }
     };
-#pragma unroll 1
-    for (int hd = 0; hd < SNH; ++hd) head(hd);
+    // the heads unrolled: rolled, the loop-carried proj accumulators and the AGPR-resident MFMA results cost
+    // ~1.7k accvgpr moves / reads per window against ~0.8k unrolled, 453-481 -> 404-433 us per block
+    // (profiles/r06_x3_sab_variants_ab.txt; SLP vectorisation off on top of it: slower)
+    head(0);
+    head(1);
+    head(2);
 
     // ---- y = x + proj (f32 rows; the residual re-read is L2-hot)
 #pragma unroll
