@@ -468,6 +468,21 @@ def test_x3_swin_attn_block_vs_chain_and_f64(B, shift):
     assert err <= 1e-5
 
 
+def test_x3_swin_tower_fused_attn_half_matches_chain():
+    """Swin-T x3 forward_features (random init, B = 2) with the fused stage-1 attention half against the same
+    tower on the unfused chain (fused_attn = False): same f32 features within the products' error."""
+    ssd = init_swin_state(SWIN_T, 11)
+    img = torch.from_numpy(synthetic.image_from_u8(synthetic.image_u8(2, 12))).to(DEV)
+    sw = SwinTowerX3(ssd, SWIN_T, DEV)
+    assert sw.stages[0]["blocks"][0]["sab_pack"] is not None and sw.stages[1]["blocks"][0]["sab_pack"] is None
+    f_fused = sw.forward_features(img)
+    sw.fused_attn = False
+    f_chain = sw.forward_features(img)
+    d = _rel(f_fused, f_chain)
+    print(json.dumps({"fused_vs_chain": d}))
+    assert d <= 1e-5
+
+
 def test_x3_swin_attn_block_rejects():
     """Unbuilt widths / windows are refused with MMR_ERR_UNSUPPORTED (pack: 0 bytes, None from ops)."""
     assert _lib.lib().mmr_x3_swin_attn_block_pack_bytes(192) == 0
